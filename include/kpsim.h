@@ -1,0 +1,250 @@
+/*
+ * kpsim.h — C-ABI of the MI355X-native Karpenter scheduling-simulation library (libkpsim.so).
+ *
+ * This is the drop-in boundary for the ONE hot path of jonathan-innis/karpenter-provider-aws that is
+ * accelerated here: the provisioning scheduling simulation (core `scheduling.Scheduler.Solve`) and
+ * its consolidation re-simulation, fed by the AWS provider's instance-type catalog.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the reference root; `[core]` =
+ * sigs.k8s.io/karpenter v1.6.1-0.20250908174930-91341612ebc6, go.mod:49, not vendored):
+ *
+ *   kp_ctx_create / kp_ctx_destroy
+ *       — process-wide provider wiring: cmd/controller/main.go:30-85 (CloudProvider construction),
+ *         solver options from pkg/operator/options/options.go:36-58 and core settings
+ *         (MIN_VALUES_POLICY, website/content/en/preview/reference/settings.md:39).
+ *   kp_catalog_upload
+ *       — the `[]*cloudprovider.InstanceType` snapshot returned by
+ *         CloudProvider.GetInstanceTypes (pkg/cloudprovider/cloudprovider.go:181-197) →
+ *         instancetype.DefaultProvider.List (pkg/providers/instancetype/instancetype.go:123-165),
+ *         including Offerings injected by offering.InjectOfferings
+ *         (pkg/providers/instancetype/offering/offering.go:70-196).  `epoch` mirrors the List cache
+ *         key (instancetype.go:219-229) plus ICE seqnums (pkg/cache/unavailableofferings.go:76-83).
+ *   kp_catalog_patch_avail / kp_catalog_patch_price
+ *       — ICE marks (pkg/cache/unavailableofferings.go:93-120) and price refreshes
+ *         (pkg/providers/pricing/pricing.go:379-423) as table deltas.
+ *   kp_solve
+ *       — [core] provisioning.Scheduler.Solve (pkg/controllers/provisioning/scheduling/scheduler.go),
+ *         reached today from the provisioner batch loop registered at cmd/controller/main.go:50-58,
+ *         followed by [core] Results.TruncateInstanceTypes (InstanceTypes.Truncate, called at
+ *         pkg/providers/instance/instance.go:293 with maxInstanceTypes = 60, instance.go:62).
+ *   kp_result_nodeclaim_requirements
+ *       — read-back of NodeClaim.Requirements for instanceToNodeClaim-style write-back
+ *         (pkg/cloudprovider/cloudprovider.go:381-444).
+ *
+ * Conventions
+ *   - Every function is extern "C", noexcept, and returns kp_status.
+ *   - Inputs are borrowed for the duration of the call; outputs go into caller-allocated buffers
+ *     (KP_E_BUFFER + required sizes when they are too small).  No pointer to library memory escapes.
+ *   - Quantities are int64 MILLI-units of the Kubernetes resource.Quantity (Quantity.MilliValue()):
+ *     cpu in millicores, memory/ephemeral-storage in milli-bytes, counts ×1000.
+ *   - Strings are NUL-terminated UTF-8; they are interned at catalog upload / solve time.
+ *   - A kp_ctx is single-threaded: concurrent callers use one ctx each (the reference calls List()
+ *     from many goroutines, pkg/providers/instancetype/suite_test.go:2857-2891; each ctx owns its
+ *     own device stream and buffers).  The catalog is immutable per epoch.
+ */
+#ifndef KPSIM_H_
+#define KPSIM_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t kp_status;
+enum {
+    KP_OK = 0,
+    KP_E_INVALID = 1,                /* malformed input view */
+    KP_E_BUFFER = 2,                 /* output buffer too small; required sizes written back */
+    KP_E_DEVICE = 3,                 /* HIP runtime error or no gfx950 device */
+    KP_E_INSUFFICIENT_CAPACITY = 4,  /* cloudprovider.NewInsufficientCapacityError (cloudprovider.go:96, instance.go:283) */
+    KP_E_NODECLASS_NOT_READY = 5,    /* cloudprovider.go:104 */
+    KP_E_CREATE = 6,                 /* cloudprovider.go:118, instance.go:295 */
+    KP_E_UNSUPPORTED = 7,            /* input uses a feature this build does not implement (never silently ignored) */
+    KP_E_STATE = 8                   /* call order violated (e.g. solve before catalog upload) */
+};
+
+/* corev1.NodeSelectorOperator */
+enum { KP_OP_IN = 0, KP_OP_NOT_IN = 1, KP_OP_EXISTS = 2, KP_OP_DOES_NOT_EXIST = 3, KP_OP_GT = 4, KP_OP_LT = 5 };
+
+/* core MIN_VALUES_POLICY */
+enum { KP_MIN_VALUES_STRICT = 0, KP_MIN_VALUES_BEST_EFFORT = 1 };
+
+/* scheduling.Requirement as built by NewRequirementWithFlexibility / NewNodeSelectorRequirementsWithMinValues. */
+typedef struct kp_requirement {
+    const char* key;
+    int32_t op;                      /* KP_OP_* */
+    int32_t n_values;
+    const char* const* values;       /* In/NotIn: the set; Gt/Lt: values[0] is the integer bound */
+    int32_t min_values;              /* < 0 : nil */
+} kp_requirement;
+
+typedef struct kp_taint {
+    const char* key;
+    const char* value;
+    const char* effect;              /* "NoSchedule" | "PreferNoSchedule" | "NoExecute" */
+} kp_taint;
+
+enum { KP_TOL_EQUAL = 0, KP_TOL_EXISTS = 1 };
+typedef struct kp_toleration {
+    const char* key;                 /* "" matches every key (only with Exists) */
+    int32_t op;                      /* KP_TOL_* */
+    const char* value;
+    const char* effect;              /* "" matches every effect */
+} kp_toleration;
+
+/* Per (type, label key) and (offering, label key) state of InstanceType.Requirements. */
+enum { KP_LABEL_ABSENT = 0, KP_LABEL_DOES_NOT_EXIST = 1, KP_LABEL_IN = 2 };
+
+/*
+ * The cloudprovider.InstanceType catalog as SoA (one row per instance type as returned by
+ * GetInstanceTypes; rows from different EC2NodeClasses may share a name).
+ */
+typedef struct kp_catalog_view {
+    int32_t n_types;                         /* T */
+    int32_t n_resources;                     /* R */
+    const char* const* resource_names;       /* [R] corev1.ResourceName */
+    const char* const* type_names;           /* [T] */
+    const int64_t* capacity;                 /* [T*R] InstanceType.Capacity (milli) */
+    const int64_t* allocatable;              /* [T*R] InstanceType.Allocatable() = Capacity − Overhead.Total() */
+
+    int32_t n_label_keys;                    /* K */
+    const char* const* label_keys;           /* [K] */
+    const int8_t* label_state;               /* [T*K] KP_LABEL_* */
+    const int32_t* label_offsets;            /* [T*K+1] CSR offsets into label_values (used when KP_LABEL_IN) */
+    const char* const* label_values;
+
+    int32_t n_offerings;                     /* O, rows grouped by type (offering_type non-decreasing) */
+    const int32_t* offering_type;            /* [O] */
+    const double* offering_price;            /* [O] Offering.Price */
+    const uint8_t* offering_available;       /* [O] Offering.Available */
+    const int32_t* offering_reservation_capacity; /* [O] Offering.ReservationCapacity (0 for od/spot) */
+    int32_t n_offering_keys;                 /* KO: keys of Offering.Requirements */
+    const char* const* offering_keys;        /* [KO] */
+    const int8_t* offering_label_state;      /* [O*KO] KP_LABEL_* (single value when IN) */
+    const char* const* offering_label_values;/* [O*KO] value when KP_LABEL_IN, else ignored */
+} kp_catalog_view;
+
+/* A NodePool as the scheduler sees it: NodeClaimTemplate (core scheduling/nodeclaimtemplate.go). */
+typedef struct kp_nodepool {
+    const char* name;
+    int32_t weight;                          /* .spec.weight (templates ordered weight desc, name asc) */
+    int32_t n_requirements;                  /* template Requirements: spec requirements + template labels */
+    const kp_requirement* requirements;      /*   + karpenter.sh/nodepool In [name] */
+    int32_t n_taints;
+    const kp_taint* taints;
+    const int64_t* daemon_overhead;          /* [R] or NULL: daemonset overhead added to every new NodeClaim */
+    const uint8_t* limit_set;                /* [R] or NULL: resources that carry a NodePool limit */
+    const int64_t* limit_remaining;          /* [R] remaining = limits − capacity of this pool's existing nodes */
+    int32_t n_types;                         /* GetInstanceTypes(nodepool) rows; < 0 means all catalog rows */
+    const int32_t* type_index;
+} kp_nodepool;
+
+/* A pod class: pods that share scheduling constraints (podData.Requirements, tolerations). */
+typedef struct kp_pod_class {
+    int32_t n_requirements;                  /* nodeSelector ∪ requiredDuringScheduling term[0] */
+    const kp_requirement* requirements;
+    int32_t n_tolerations;
+    const kp_toleration* tolerations;
+} kp_pod_class;
+
+typedef struct kp_pods_view {
+    int32_t n_pods;                          /* P */
+    const int32_t* class_id;                 /* [P] */
+    const int64_t* requests;                 /* [P*R] resources.RequestsForPods (incl. pods = 1000 milli) */
+    const int64_t* creation_ns;              /* [P] CreationTimestamp (queue tie-break) */
+    const char* const* uids;                 /* [P] UID (final queue tie-break) */
+} kp_pods_view;
+
+/* An existing (or in-flight real) node: ExistingNode in core scheduling/existingnode.go. */
+typedef struct kp_existing_node {
+    const char* name;
+    int32_t n_labels;                        /* node labels (each becomes `key In [value]`) */
+    const char* const* label_keys;
+    const char* const* label_values;
+    int32_t n_taints;
+    const kp_taint* taints;
+    const int64_t* available;                /* [R] StateNode.Available() */
+    const int64_t* requests;                 /* [R] remaining daemonset requests (initial n.requests) */
+} kp_existing_node;
+
+typedef struct kp_solve_input {
+    int32_t n_nodepools;
+    const kp_nodepool* nodepools;
+    int32_t n_classes;
+    const kp_pod_class* classes;
+    kp_pods_view pods;
+    int32_t n_existing;
+    const kp_existing_node* existing;        /* in scheduling order (initialized first, core sorts stably) */
+    int32_t max_instance_types;              /* 60 (instance.go:62); <= 0 disables truncation */
+    int32_t min_values_policy;               /* KP_MIN_VALUES_* */
+} kp_solve_input;
+
+/* Per-solve counters: evaluation counts feed the algorithmic-bytes roofline. */
+typedef struct kp_solve_stats {
+    int64_t pods_popped;                     /* queue pops incl. retries */
+    int64_t nodeclaim_evals;                 /* NodeClaim.Add attempts */
+    int64_t nodeclaim_candidates_scanned;    /* Σ_steps N_t (rows in the sorted in-flight list per step) */
+    int64_t template_evals;                  /* new-NodeClaim attempts */
+    int64_t existing_evals;
+    int64_t sorts_fast;                      /* sort.Slice emulations resolved on the fast path */
+    int64_t sorts_full;                      /* ... needing the full pdqsort emulation */
+    double  ns_host_prep;
+    double  ns_device_solve;
+    double  ns_device_finalize;
+    double  ns_total;
+} kp_solve_stats;
+
+/* pod_result encoding */
+#define KP_POD_UNSCHEDULABLE (-1)            /* pod has an entry in Results.PodErrors */
+#define KP_POD_EXISTING(j) (-2 - (j))        /* scheduled onto existing node j */
+
+typedef struct kp_solve_output {
+    /* capacities, set by the caller */
+    int32_t cap_nodeclaims;
+    int32_t cap_type_ids;
+    /* results */
+    int32_t n_nodeclaims;                    /* Results.NewNodeClaims (creation order) */
+    int32_t n_type_ids;                      /* entries written to type_ids */
+    int32_t* nodeclaim_nodepool;             /* [cap_nodeclaims] index into input nodepools */
+    int32_t* nodeclaim_n_pods;               /* [cap_nodeclaims] */
+    int32_t* nodeclaim_slice_pos;            /* [cap_nodeclaims] position in s.newNodeClaims at the end of Solve */
+    int32_t* nodeclaim_n_options;            /* [cap_nodeclaims] InstanceTypeOptions before truncation */
+    int32_t* nodeclaim_type_offset;          /* [cap_nodeclaims+1] into type_ids */
+    int32_t* type_ids;                       /* [cap_type_ids] truncated, price-ordered catalog rows */
+    int32_t* pod_result;                     /* [P] >= 0 nodeclaim index, KP_POD_EXISTING(j), KP_POD_UNSCHEDULABLE */
+    int32_t* pod_order;                      /* [P] queue position of the pod's final placement (-1 if none) */
+    kp_solve_stats stats;
+} kp_solve_output;
+
+typedef struct kp_device_opts {
+    int32_t device;                          /* HIP device ordinal */
+    int32_t reserved0;
+} kp_device_opts;
+
+typedef struct kp_ctx kp_ctx;
+
+kp_status kp_ctx_create(const kp_device_opts* opts, kp_ctx** out);
+kp_status kp_ctx_destroy(kp_ctx* ctx);
+const char* kp_last_error(const kp_ctx* ctx);
+const char* kp_version(void);
+
+kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* catalog, uint64_t epoch);
+/* ICE / availability delta: available[o] for every offering row, same order as the upload. */
+kp_status kp_catalog_patch_avail(kp_ctx* ctx, const uint8_t* available, int32_t n_offerings, uint64_t epoch);
+/* price delta: price of offering rows idx[i] becomes price[i]. */
+kp_status kp_catalog_patch_price(kp_ctx* ctx, const int32_t* idx, const double* price, int32_t n, uint64_t epoch);
+
+kp_status kp_solve(kp_ctx* ctx, const kp_solve_input* in, kp_solve_output* out);
+
+/*
+ * Requirements of NodeClaim `nc` from the last kp_solve on this ctx, serialized as lines
+ * "key\top\tminValues\tv1\x1fv2..." (op = KP_OP_*; hostname removed as in FinalizeScheduling).
+ * Writes at most cap bytes (incl. NUL); *needed receives the full size.
+ */
+kp_status kp_result_nodeclaim_requirements(kp_ctx* ctx, int32_t nc, char* buf, int64_t cap, int64_t* needed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KPSIM_H_ */

@@ -1,0 +1,169 @@
+"""ctypes mirror of include/kpsim.h plus marshaling of the Python model into the C views.
+
+The same views are handed to libkpsim.so (the product) and, in tests only, to the CPU oracle, so both
+sides see byte-identical inputs.
+"""
+import ctypes as C
+
+import numpy as np
+
+c_int8_p = C.POINTER(C.c_int8)
+c_uint8_p = C.POINTER(C.c_uint8)
+c_int32_p = C.POINTER(C.c_int32)
+c_int64_p = C.POINTER(C.c_int64)
+c_double_p = C.POINTER(C.c_double)
+c_char_pp = C.POINTER(C.c_char_p)
+
+KP_OK, KP_E_INVALID, KP_E_BUFFER, KP_E_DEVICE, KP_E_INSUFFICIENT_CAPACITY, KP_E_NODECLASS_NOT_READY, \
+    KP_E_CREATE, KP_E_UNSUPPORTED, KP_E_STATE = range(9)
+STATUS_NAMES = {0: "KP_OK", 1: "KP_E_INVALID", 2: "KP_E_BUFFER", 3: "KP_E_DEVICE", 4: "KP_E_INSUFFICIENT_CAPACITY",
+                5: "KP_E_NODECLASS_NOT_READY", 6: "KP_E_CREATE", 7: "KP_E_UNSUPPORTED", 8: "KP_E_STATE"}
+
+OPS = {"In": 0, "NotIn": 1, "Exists": 2, "DoesNotExist": 3, "Gt": 4, "Lt": 5}
+KP_TOL_EQUAL, KP_TOL_EXISTS = 0, 1
+KP_LABEL_ABSENT, KP_LABEL_DOES_NOT_EXIST, KP_LABEL_IN = 0, 1, 2
+KP_POD_UNSCHEDULABLE = -1
+
+
+def KP_POD_EXISTING(j):
+    return -2 - j
+
+
+class kp_requirement(C.Structure):
+    _fields_ = [("key", C.c_char_p), ("op", C.c_int32), ("n_values", C.c_int32), ("values", c_char_pp),
+                ("min_values", C.c_int32)]
+
+
+class kp_taint(C.Structure):
+    _fields_ = [("key", C.c_char_p), ("value", C.c_char_p), ("effect", C.c_char_p)]
+
+
+class kp_toleration(C.Structure):
+    _fields_ = [("key", C.c_char_p), ("op", C.c_int32), ("value", C.c_char_p), ("effect", C.c_char_p)]
+
+
+class kp_catalog_view(C.Structure):
+    _fields_ = [
+        ("n_types", C.c_int32), ("n_resources", C.c_int32), ("resource_names", c_char_pp), ("type_names", c_char_pp),
+        ("capacity", c_int64_p), ("allocatable", c_int64_p),
+        ("n_label_keys", C.c_int32), ("label_keys", c_char_pp), ("label_state", c_int8_p),
+        ("label_offsets", c_int32_p), ("label_values", c_char_pp),
+        ("n_offerings", C.c_int32), ("offering_type", c_int32_p), ("offering_price", c_double_p),
+        ("offering_available", c_uint8_p), ("offering_reservation_capacity", c_int32_p),
+        ("n_offering_keys", C.c_int32), ("offering_keys", c_char_pp), ("offering_label_state", c_int8_p),
+        ("offering_label_values", c_char_pp),
+    ]
+
+
+class kp_nodepool(C.Structure):
+    _fields_ = [
+        ("name", C.c_char_p), ("weight", C.c_int32), ("n_requirements", C.c_int32),
+        ("requirements", C.POINTER(kp_requirement)), ("n_taints", C.c_int32), ("taints", C.POINTER(kp_taint)),
+        ("daemon_overhead", c_int64_p), ("limit_set", c_uint8_p), ("limit_remaining", c_int64_p),
+        ("n_types", C.c_int32), ("type_index", c_int32_p),
+    ]
+
+
+class kp_pod_class(C.Structure):
+    _fields_ = [("n_requirements", C.c_int32), ("requirements", C.POINTER(kp_requirement)),
+                ("n_tolerations", C.c_int32), ("tolerations", C.POINTER(kp_toleration))]
+
+
+class kp_pods_view(C.Structure):
+    _fields_ = [("n_pods", C.c_int32), ("class_id", c_int32_p), ("requests", c_int64_p), ("creation_ns", c_int64_p),
+                ("uids", c_char_pp)]
+
+
+class kp_existing_node(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("n_labels", C.c_int32), ("label_keys", c_char_pp), ("label_values", c_char_pp),
+                ("n_taints", C.c_int32), ("taints", C.POINTER(kp_taint)), ("available", c_int64_p),
+                ("requests", c_int64_p)]
+
+
+class kp_solve_input(C.Structure):
+    _fields_ = [("n_nodepools", C.c_int32), ("nodepools", C.POINTER(kp_nodepool)),
+                ("n_classes", C.c_int32), ("classes", C.POINTER(kp_pod_class)),
+                ("pods", kp_pods_view),
+                ("n_existing", C.c_int32), ("existing", C.POINTER(kp_existing_node)),
+                ("max_instance_types", C.c_int32), ("min_values_policy", C.c_int32)]
+
+
+class kp_solve_stats(C.Structure):
+    _fields_ = [("pods_popped", C.c_int64), ("nodeclaim_evals", C.c_int64), ("nodeclaim_candidates_scanned", C.c_int64),
+                ("template_evals", C.c_int64), ("existing_evals", C.c_int64), ("sorts_fast", C.c_int64),
+                ("sorts_full", C.c_int64), ("ns_host_prep", C.c_double), ("ns_device_solve", C.c_double),
+                ("ns_device_finalize", C.c_double), ("ns_total", C.c_double)]
+
+
+class kp_solve_output(C.Structure):
+    _fields_ = [("cap_nodeclaims", C.c_int32), ("cap_type_ids", C.c_int32), ("n_nodeclaims", C.c_int32),
+                ("n_type_ids", C.c_int32), ("nodeclaim_nodepool", c_int32_p), ("nodeclaim_n_pods", c_int32_p),
+                ("nodeclaim_slice_pos", c_int32_p), ("nodeclaim_n_options", c_int32_p),
+                ("nodeclaim_type_offset", c_int32_p), ("type_ids", c_int32_p), ("pod_result", c_int32_p),
+                ("pod_order", c_int32_p), ("stats", kp_solve_stats)]
+
+
+class kp_device_opts(C.Structure):
+    _fields_ = [("device", C.c_int32), ("reserved0", C.c_int32)]
+
+
+# ------------------------------------------------------------------------------------------------
+# marshaling helpers — a Keep object owns every buffer a view points into
+# ------------------------------------------------------------------------------------------------
+class Keep:
+    def __init__(self):
+        self.refs = []
+
+    def hold(self, x):
+        self.refs.append(x)
+        return x
+
+    def cstrs(self, strs):
+        arr = (C.c_char_p * max(1, len(strs)))(*[s.encode() if isinstance(s, str) else s for s in strs])
+        return self.hold(arr)
+
+    def np(self, a, dtype):
+        a = np.ascontiguousarray(a, dtype=dtype)
+        self.hold(a)
+        return a
+
+    def ptr(self, a, dtype, ctype):
+        a = self.np(a, dtype)
+        return a.ctypes.data_as(C.POINTER(ctype))
+
+
+def requirement_array(keep, reqs):
+    """reqs: iterable of model.Requirement -> (n, POINTER(kp_requirement))"""
+    reqs = list(reqs)
+    arr = (kp_requirement * max(1, len(reqs)))()
+    for i, r in enumerate(reqs):
+        arr[i].key = r.key.encode()
+        arr[i].op = OPS[r.op]
+        arr[i].n_values = len(r.values)
+        arr[i].values = keep.cstrs(list(r.values))
+        arr[i].min_values = -1 if r.min_values is None else int(r.min_values)
+    keep.hold(arr)
+    return len(reqs), arr
+
+
+def taint_array(keep, taints):
+    taints = list(taints)
+    arr = (kp_taint * max(1, len(taints)))()
+    for i, t in enumerate(taints):
+        arr[i].key = t.key.encode()
+        arr[i].value = (t.value or "").encode()
+        arr[i].effect = t.effect.encode()
+    keep.hold(arr)
+    return len(taints), arr
+
+
+def toleration_array(keep, tols):
+    tols = list(tols)
+    arr = (kp_toleration * max(1, len(tols)))()
+    for i, t in enumerate(tols):
+        arr[i].key = (t.key or "").encode()
+        arr[i].op = KP_TOL_EXISTS if t.operator == "Exists" else KP_TOL_EQUAL
+        arr[i].value = (t.value or "").encode()
+        arr[i].effect = (t.effect or "").encode()
+    keep.hold(arr)
+    return len(tols), arr
