@@ -1,0 +1,167 @@
+#!/usr/bin/env python3
+"""Benchmark: pods scheduled/sec for Solve on BASELINE.json configs[1] (50k heterogeneous pods × the 918-type
+EC2 catalog × 3 AZ × {spot, on-demand}) on the gfx950 library.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+One step = one kp_solve_execute (queue sort, class×type masks, template filter, the FFD Solve kernel and
+Truncate(60)) with every input already resident in HBM.  Provisioning Solve is a serial chain, so N GPUs run
+N independent replicas ("replicas only"); value = pods of all ranks ÷ max-over-ranks time.
+Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(ROOT, "karpenter-provider-aws_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+    sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+
+
+def algorithmic_bytes(stats, n_nodeclaims, T, R=12, K_bytes=64):
+    """B_solve = Σ_steps [N_t × S_nc + S_pod] + P_new × T × S_type,
+    S_nc = ceil(T/8) + 8R + 64, S_pod = 8R + 64, S_type = 8R + 2·32 + 16·6."""
+    s_nc = (T + 7) // 8 + 8 * R + K_bytes
+    s_pod = 8 * R + K_bytes
+    s_type = 8 * R + 64 + 96
+    return stats["nodeclaim_candidates_scanned"] * s_nc + stats["pods_popped"] * s_pod + n_nodeclaims * T * s_type
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pods", type=int, default=50_000)
+    ap.add_argument("--cpu-sample", type=int, default=8000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    from kpsim import catalog, model, native, synth
+
+    fx = catalog.load_fixtures()
+    cat = catalog.golden_catalog(fx=fx)
+    prob = synth.config2(n_pods=a.pods, catalog=cat)
+    ctx = native.Context(local)
+    cv = model.CatalogView(cat)
+    ctx.upload_catalog(cv)
+    iv = model.SolveInputView(prob)
+    cap_nc = max(16, prob.pods.n + 1)
+    out = model.OutputBuffers(prob.pods.n, cap_nc, cap_nc * 60)
+
+    # end-to-end (PCIe-inclusive) call once, for the record
+    t = time.perf_counter()
+    ctx.solve(iv, out)
+    e2e_ms = (time.perf_counter() - t) * 1e3
+    res = out.results()
+    ctx.prepare(iv)  # inputs resident in HBM from here on
+
+    for _ in range(a.warmup):
+        ctx.execute()
+
+    def barrier():
+        if dist is not None:
+            import torch
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    barrier()
+    ffd_ms = []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ctx.execute()  # synchronous on the library's stream
+        ffd_ms.append(ctx.kernel_times_ms())
+    elapsed = time.perf_counter() - t0
+    barrier()
+    if dist is not None:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    kt = np.array(ffd_ms).mean(axis=0)
+    P = prob.pods.n
+    value = P * a.steps * world / elapsed
+    T = len(cat)
+    B = algorithmic_bytes(res.stats, res.n_nodeclaims, T)
+    ffd_s = kt[3] / 1e3
+    achieved = B / ffd_s / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_ffd.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    cpu = None
+    parity_ok = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        import parity
+        import pyoracle
+        sample = synth.subsample(prob, a.cpu_sample)
+        t = time.perf_counter()
+        orc = pyoracle.solve(sample)
+        cpu_s = time.perf_counter() - t
+        cpu = {"value": sample.pods.n / cpu_s, "unit": "pods/s", "cores": 1, "kind": "port",
+               "sample": "oracle (C++ restatement, 1 thread) on a seeded %d-pod subsample of the same config2 "
+                         "workload (same catalog, NodePools, classes): %.1f s" % (sample.pods.n, cpu_s)}
+        dev = parity.run_device(ctx, sample)
+        try:
+            parity.assert_same(dev, (orc.results, [model.parse_requirements_blob(orc.requirements(i))
+                                                    for i in range(orc.results.n_nodeclaims)]))
+            parity_ok = True
+        except AssertionError:
+            parity_ok = False
+
+    if rank == 0:
+        line = {
+            "metric": "pods scheduled/sec (Solve, 50k pods × EC2 catalog)",
+            "value": value,
+            "unit": "pods/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic (seeded config2 over the reference's golden 918-type catalog)",
+            "config": {"workload": "config2: %d heterogeneous pods (250 classes) x %d types x 3 AZ x {spot,on-demand},"
+                                   " 2 NodePools" % (P, T), "pods": P, "types": T,
+                       "parallelism": "replicas" if world > 1 else "single"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "ffd_kernel", "kernel_ms": float(kt[3]), "algorithmic_bytes": int(B)},
+            "cpu_baseline": cpu,
+            "parity_sample": parity_ok,
+            "kernel_ms": {"queue_sort": float(kt[0]), "class_mask": float(kt[1]), "template_init": float(kt[2]),
+                          "ffd": float(kt[3]), "finalize": float(kt[4])},
+            "end_to_end_ms": e2e_ms,
+            "nodeclaims": res.n_nodeclaims,
+            "unschedulable": int((res.pod_result == -1).sum()),
+            "solve_stats": {k: v for k, v in res.stats.items() if not k.startswith("ns_")},
+        }
+        print(json.dumps(line))
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -237,9 +237,23 @@ kp_status kp_catalog_patch_price(kp_ctx* ctx, const int32_t* idx, const double* 
 
 kp_status kp_solve(kp_ctx* ctx, const kp_solve_input* in, kp_solve_output* out);
 
+/* kp_solve split into its phases (kp_solve == prepare + execute + fetch):
+ *   prepare — intern strings into the catalog dictionaries, encode digests, upload inputs to HBM;
+ *   execute — all scheduling work on the device (queue sort, class masks, template filter, FFD, Truncate),
+ *             synchronous; inputs are HBM-resident when it starts;
+ *   fetch   — download and decode results into the caller's buffers. */
+kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in);
+kp_status kp_solve_execute(kp_ctx* ctx);
+kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out);
+
+/* Device time (ms, HIP events on the ctx stream) of the last kp_solve_execute, per phase:
+ * [0] queue sort, [1] class masks, [2] template filter, [3] FFD solve kernel, [4] finalize/Truncate. */
+kp_status kp_last_kernel_times(kp_ctx* ctx, double* ms, int32_t n);
+
 /*
- * Requirements of NodeClaim `nc` from the last kp_solve on this ctx, serialized as lines
- * "key\top\tminValues\tv1\x1fv2..." (op = KP_OP_*; hostname removed as in FinalizeScheduling).
+ * Requirements of NodeClaim `nc` from the last kp_solve on this ctx (hostname removed as in
+ * FinalizeScheduling), one line per key, lines sorted:
+ *   "key \t complement(0|1) \t gt|- \t lt|- \t minValues|- \t v1 \x1f v2 ..."   (values sorted)
  * Writes at most cap bytes (incl. NUL); *needed receives the full size.
  */
 kp_status kp_result_nodeclaim_requirements(kp_ctx* ctx, int32_t nc, char* buf, int64_t cap, int64_t* needed);

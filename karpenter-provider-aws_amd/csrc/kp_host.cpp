@@ -1,0 +1,1178 @@
+// kp_host.cpp — C-ABI implementation of libkpsim.so (include/kpsim.h): dictionary encoding of the catalog
+// and of a solve's requirements into device digests, device buffer management, kernel orchestration and
+// result decoding.  All scheduling decisions are made by the gfx950 kernels in kp_kernels.hip; this file
+// only encodes inputs and decodes outputs (there is no host fallback: without a device every call fails
+// with KP_E_DEVICE).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/kpsim.h"
+#include "kp_layout.h"
+
+size_t kp_ffd_shared_bytes();
+hipError_t kp_launch_class_mask(const KpDev& d, hipStream_t s);
+hipError_t kp_launch_template_init(const KpDev& d, hipStream_t s);
+hipError_t kp_launch_ffd(const KpDev& d, hipStream_t s);
+hipError_t kp_launch_finalize(const KpDev& d, int n_nodeclaims, hipStream_t s);
+hipError_t kp_queue_sort(const int64_t* fields, int n, int32_t* perm_a, int32_t* perm_b, uint64_t* keys_a,
+                         uint64_t* keys_b, void* temp, size_t* temp_bytes, hipStream_t s, int32_t** result);
+
+namespace {
+
+using clk = std::chrono::steady_clock;
+double ns_since(clk::time_point t0) { return std::chrono::duration<double, std::nano>(clk::now() - t0).count(); }
+
+// ---------------------------------------------------------------------------------------------
+// label dictionaries
+// ---------------------------------------------------------------------------------------------
+bool go_atoi(const char* s, int64_t& out) {  // strconv.Atoi (64-bit)
+    size_t n = strlen(s), i = 0;
+    bool neg = false;
+    if (n == 0) return false;
+    if (s[0] == '+' || s[0] == '-') {
+        neg = s[0] == '-';
+        i = 1;
+    }
+    if (i >= n) return false;
+    unsigned __int128 v = 0;
+    for (; i < n; i++) {
+        if (s[i] < '0' || s[i] > '9') return false;
+        v = v * 10 + (unsigned)(s[i] - '0');
+        if (v > (unsigned __int128)1 << 63) return false;
+    }
+    if (!neg && v > (unsigned __int128)INT64_MAX) return false;
+    out = neg ? (int64_t)(0 - (uint64_t)v) : (int64_t)v;
+    return true;
+}
+
+const char* const kWellKnown[] = {
+    // karpv1.WellKnownLabels ([core] pkg/apis/v1/labels.go)
+    "karpenter.sh/nodepool", "topology.kubernetes.io/zone", "topology.kubernetes.io/region",
+    "node.kubernetes.io/instance-type", "kubernetes.io/arch", "kubernetes.io/os", "karpenter.sh/capacity-type",
+    "node.kubernetes.io/windows-build",
+    // AWS additions, pkg/apis/v1/labels.go:31-57
+    "karpenter.k8s.aws/capacity-reservation-id", "karpenter.k8s.aws/capacity-reservation-type",
+    "karpenter.k8s.aws/instance-hypervisor", "karpenter.k8s.aws/instance-encryption-in-transit-supported",
+    "karpenter.k8s.aws/instance-category", "karpenter.k8s.aws/instance-capacity-flex", "karpenter.k8s.aws/instance-family",
+    "karpenter.k8s.aws/instance-generation", "karpenter.k8s.aws/instance-size", "karpenter.k8s.aws/instance-local-nvme",
+    "karpenter.k8s.aws/instance-cpu", "karpenter.k8s.aws/instance-cpu-manufacturer",
+    "karpenter.k8s.aws/instance-cpu-sustained-clock-speed-mhz", "karpenter.k8s.aws/instance-memory",
+    "karpenter.k8s.aws/instance-ebs-bandwidth", "karpenter.k8s.aws/instance-network-bandwidth",
+    "karpenter.k8s.aws/instance-gpu-name", "karpenter.k8s.aws/instance-gpu-manufacturer",
+    "karpenter.k8s.aws/instance-gpu-count", "karpenter.k8s.aws/instance-gpu-memory",
+    "karpenter.k8s.aws/instance-accelerator-name", "karpenter.k8s.aws/instance-accelerator-manufacturer",
+    "karpenter.k8s.aws/instance-accelerator-count", "topology.k8s.aws/zone-id",
+};
+bool well_known(const std::string& k) {
+    for (auto* w : kWellKnown)
+        if (k == w) return true;
+    return false;
+}
+// karpv1.NormalizedLabels + topology.ebs.csi.aws.com/zone (pkg/operator/operator.go:71)
+std::string normalize(const char* k) {
+    static const std::pair<const char*, const char*> m[] = {
+        {"failure-domain.beta.kubernetes.io/zone", "topology.kubernetes.io/zone"},
+        {"failure-domain.beta.kubernetes.io/region", "topology.kubernetes.io/region"},
+        {"beta.kubernetes.io/arch", "kubernetes.io/arch"},
+        {"beta.kubernetes.io/os", "kubernetes.io/os"},
+        {"beta.kubernetes.io/instance-type", "node.kubernetes.io/instance-type"},
+        {"topology.ebs.csi.aws.com/zone", "topology.kubernetes.io/zone"},
+    };
+    for (auto& p : m)
+        if (!strcmp(k, p.first)) return p.second;
+    return k;
+}
+
+struct KeyDict {
+    std::string name;
+    std::unordered_map<std::string, int> ids;
+    std::vector<std::string> vals;
+    int id(const std::string& v) {
+        auto it = ids.find(v);
+        if (it != ids.end()) return it->second;
+        int i = (int)vals.size();
+        ids.emplace(v, i);
+        vals.push_back(v);
+        return i;
+    }
+    int find(const std::string& v) const {
+        auto it = ids.find(v);
+        return it == ids.end() ? -1 : it->second;
+    }
+};
+
+struct Dicts {
+    std::vector<KeyDict> keys;
+    std::unordered_map<std::string, int> kid;
+    int key(const std::string& k) {
+        auto it = kid.find(k);
+        if (it != kid.end()) return it->second;
+        int i = (int)keys.size();
+        kid.emplace(k, i);
+        keys.emplace_back();
+        keys.back().name = k;
+        return i;
+    }
+    int find_key(const std::string& k) const {
+        auto it = kid.find(k);
+        return it == kid.end() ? -1 : it->second;
+    }
+};
+
+// host requirement (value ids) used while encoding digests
+struct HReq {
+    int key = -1;
+    bool complement = false;
+    std::vector<int> vals;  // sorted unique
+    bool has_gt = false, has_lt = false;
+    int64_t gt = 0, lt = 0;
+    bool has_min = false;
+    int minv = 0;
+};
+
+template <class T>
+struct DBuf {  // device buffer, grow-only
+    T* p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t count) {
+        if (count <= n && p) return hipSuccess;
+        if (p) hipFree(p);
+        p = nullptr;
+        n = 0;
+        size_t c = count ? count : 1;
+        hipError_t e = hipMalloc((void**)&p, c * sizeof(T));
+        if (e == hipSuccess) n = c;
+        return e;
+    }
+    hipError_t upload(const std::vector<T>& v, hipStream_t s) {
+        hipError_t e = ensure(v.size());
+        if (e != hipSuccess || v.empty()) return e;
+        return hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------------------------
+struct kp_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // catalog (host copies)
+    bool have_catalog = false;
+    uint64_t epoch = 0;
+    int T = 0, TW = 0, R = 0, Kcat = 0, n_multi = 0, n_slots = 0;
+    std::vector<std::string> resource_names, type_names;
+    Dicts cat;                               // catalog dictionaries (keys 0..Kcat-1 are catalog label keys)
+    std::vector<uint32_t> cat_kflags;        // per catalog key: KF_CAT_SINGLE / KF_CAT_MULTI
+    std::vector<int> cat_multi;              // per catalog key: multi index or -1
+    std::vector<int64_t> cap_rt, alloc_rt;   // [R][T]
+    std::vector<uint64_t> avail_zc;          // [T]
+    std::vector<int> off_type, off_slot;     // per offering row
+    std::vector<double> slot_price;          // [T][KP_MAX_SLOTS]
+    std::vector<int32_t> slot_zone, slot_ct, slot_zoneid;
+    int key_zone = -1, key_ct = -1, key_zoneid = -1, key_resvid = -1, key_resvtype = -1;
+    // catalog device tables
+    DBuf<uint16_t> d_type_val;
+    DBuf<uint64_t> d_multi_mask, d_dne_mask, d_avail_zc, d_nonneg;
+    DBuf<int64_t> d_alloc, d_cap;
+    DBuf<double> d_slot_price;
+    DBuf<int32_t> d_slot_zone, d_slot_ct, d_slot_zoneid;
+    DBuf<uint32_t> d_name_rank;
+    // solve
+    bool prepared = false, executed = false;
+    Dicts sol;                               // per-solve dictionaries = catalog ∪ requirement strings
+    KpDev dev{};
+    int P = 0, C = 0, NT = 0, K = 0, DW = 0;
+    std::vector<int> tmpl_np;                // template → input nodepool index
+    std::vector<int64_t> h_remaining;        // NodePool limits at solve start (re-applied by every execute)
+    DBuf<uint32_t> d_kflags, d_cls_flags, d_tol;
+    DBuf<int32_t> d_kcat, d_kmulti, d_woff, d_nw, d_nval, d_vbase, d_cls_koff, d_cls_keys, d_cls_wsoff, d_min_keys;
+    DBuf<uint8_t> d_val_isint, d_limit_set;
+    DBuf<int64_t> d_val_int, d_daemon, d_remaining, d_pod_req, d_sort_fields, d_nc_req, d_stats;
+    DBuf<ReqHdr> d_cls_hdr, d_nc_hdr, d_empty_hdr;
+    DBuf<uint64_t> d_cls_words, d_V, d_tmpl_rows, d_tmpl_opts, d_nc_words, d_nc_opts, d_empty_words, d_keys_a, d_keys_b;
+    DBuf<int32_t> d_tmpl_ok, d_pod_cls, d_pod_shape, d_perm_a, d_perm_b, d_nc_tmpl, d_qbuf, d_last_len, d_pod_result,
+        d_pod_order, d_nc_count, d_nc_npods, d_nc_slice_pos, d_nc_nopts, d_nc_valid, d_nc_types, d_nc_ntypes, d_err;
+    DBuf<char> d_sort_temp;
+    size_t sort_temp_bytes = 0;
+    double ns_prep = 0, ns_exec = 0, ns_fin = 0;
+    hipEvent_t ev[6] = {};
+    double kernel_ms[5] = {};
+    // last results (host)
+    int last_N = 0, M = 0;
+    std::vector<int32_t> h_nc_tmpl;
+};
+
+static kp_status fail(kp_ctx* c, kp_status st, const std::string& msg) {
+    if (c) c->err = msg;
+    return st;
+}
+#define HIPCHK(expr)                                                                        \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess) return fail(ctx, KP_E_DEVICE, std::string(#expr ": ") + hipGetErrorString(_e)); \
+    } while (0)
+
+extern "C" const char* kp_version(void) { return "kpsim 0.1 (gfx950)"; }
+
+extern "C" const char* kp_last_error(const kp_ctx* ctx) { return ctx ? ctx->err.c_str() : "null ctx"; }
+
+extern "C" kp_status kp_ctx_create(const kp_device_opts* opts, kp_ctx** out) try {
+    if (!out) return KP_E_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return KP_E_DEVICE;
+    auto ctx = std::make_unique<kp_ctx>();
+    ctx->device = opts ? opts->device : 0;
+    if (ctx->device < 0 || ctx->device >= n) return KP_E_DEVICE;
+    if (hipSetDevice(ctx->device) != hipSuccess) return KP_E_DEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, ctx->device) != hipSuccess) return KP_E_DEVICE;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return KP_E_DEVICE;
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) return KP_E_DEVICE;
+    for (auto& e : ctx->ev)
+        if (hipEventCreate(&e) != hipSuccess) return KP_E_DEVICE;
+    *out = ctx.release();
+    return KP_OK;
+} catch (...) {
+    return KP_E_DEVICE;
+}
+
+extern "C" kp_status kp_ctx_destroy(kp_ctx* ctx) {
+    if (!ctx) return KP_OK;
+    hipSetDevice(ctx->device);
+    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    // buffers are released with the process / device reset; explicit frees for long-lived processes
+    ctx->d_type_val.release();
+    ctx->d_multi_mask.release();
+    ctx->d_dne_mask.release();
+    ctx->d_avail_zc.release();
+    ctx->d_nonneg.release();
+    ctx->d_alloc.release();
+    ctx->d_cap.release();
+    ctx->d_slot_price.release();
+    ctx->d_slot_zone.release();
+    ctx->d_slot_ct.release();
+    ctx->d_slot_zoneid.release();
+    ctx->d_name_rank.release();
+    ctx->d_kflags.release(); ctx->d_cls_flags.release(); ctx->d_tol.release();
+    ctx->d_kcat.release(); ctx->d_kmulti.release(); ctx->d_woff.release(); ctx->d_nw.release(); ctx->d_nval.release();
+    ctx->d_vbase.release(); ctx->d_cls_koff.release(); ctx->d_cls_keys.release(); ctx->d_cls_wsoff.release();
+    ctx->d_min_keys.release(); ctx->d_val_isint.release(); ctx->d_limit_set.release(); ctx->d_val_int.release();
+    ctx->d_daemon.release(); ctx->d_remaining.release(); ctx->d_pod_req.release(); ctx->d_sort_fields.release();
+    ctx->d_nc_req.release(); ctx->d_stats.release(); ctx->d_cls_hdr.release(); ctx->d_nc_hdr.release();
+    ctx->d_empty_hdr.release(); ctx->d_cls_words.release(); ctx->d_V.release(); ctx->d_tmpl_rows.release();
+    ctx->d_tmpl_opts.release(); ctx->d_nc_words.release(); ctx->d_nc_opts.release(); ctx->d_empty_words.release();
+    ctx->d_keys_a.release(); ctx->d_keys_b.release(); ctx->d_tmpl_ok.release(); ctx->d_pod_cls.release();
+    ctx->d_pod_shape.release(); ctx->d_perm_a.release(); ctx->d_perm_b.release(); ctx->d_nc_tmpl.release();
+    ctx->d_qbuf.release(); ctx->d_last_len.release(); ctx->d_pod_result.release(); ctx->d_pod_order.release();
+    ctx->d_nc_count.release(); ctx->d_nc_npods.release(); ctx->d_nc_slice_pos.release(); ctx->d_nc_nopts.release();
+    ctx->d_nc_valid.release(); ctx->d_nc_types.release(); ctx->d_nc_ntypes.release(); ctx->d_err.release();
+    ctx->d_sort_temp.release();
+    for (auto& e : ctx->ev)
+        if (e) hipEventDestroy(e);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return KP_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// catalog upload
+// ---------------------------------------------------------------------------------------------
+static void rebuild_avail(kp_ctx* c, const std::vector<uint8_t>& avail) {
+    std::fill(c->avail_zc.begin(), c->avail_zc.end(), 0ull);
+    for (size_t o = 0; o < c->off_type.size(); o++)
+        if (c->off_slot[o] >= 0 && avail[o]) c->avail_zc[c->off_type[o]] |= 1ull << c->off_slot[o];
+}
+
+extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, uint64_t epoch) try {
+    if (!ctx || !v) return KP_E_INVALID;
+    HIPCHK(hipSetDevice(ctx->device));
+    const int T = v->n_types, R = v->n_resources, KL = v->n_label_keys;
+    if (T <= 0 || R <= 0 || R > KP_MAX_R) return fail(ctx, KP_E_INVALID, "bad n_types / n_resources");
+    if (T > KP_MAX_TYPES) return fail(ctx, KP_E_UNSUPPORTED, "more than KP_MAX_TYPES instance types");
+    kp_ctx* c = ctx;
+    c->have_catalog = false;
+    c->T = T;
+    c->TW = (T + 63) / 64;
+    c->R = R;
+    c->resource_names.assign(v->resource_names, v->resource_names + R);
+    c->type_names.assign(v->type_names, v->type_names + T);
+    c->cat = Dicts();
+    // label keys (type requirements) then offering keys
+    std::vector<int> lk(KL), ok(v->n_offering_keys);
+    for (int k = 0; k < KL; k++) lk[k] = c->cat.key(normalize(v->label_keys[k]));
+    for (int k = 0; k < v->n_offering_keys; k++) ok[k] = c->cat.key(normalize(v->offering_keys[k]));
+    const int Kc = (int)c->cat.keys.size();
+    c->Kcat = Kc;
+    // type values: state per (t, catalog key)
+    std::vector<int8_t> st((size_t)T * Kc, KP_LABEL_ABSENT);
+    std::vector<std::vector<int>> tv((size_t)T * Kc);
+    std::vector<uint8_t> multi(Kc, 0);
+    for (int t = 0; t < T; t++) {
+        for (int k = 0; k < KL; k++) {
+            const int s = v->label_state[(size_t)t * KL + k];
+            const int key = lk[k];
+            auto& cell = tv[(size_t)t * Kc + key];
+            if (s == KP_LABEL_ABSENT) continue;
+            int8_t& stt = st[(size_t)t * Kc + key];
+            if (s == KP_LABEL_DOES_NOT_EXIST) {
+                if (stt == KP_LABEL_ABSENT) stt = KP_LABEL_DOES_NOT_EXIST;
+                continue;
+            }
+            const int o0 = v->label_offsets[(size_t)t * KL + k], o1 = v->label_offsets[(size_t)t * KL + k + 1];
+            std::vector<int> ids;
+            for (int i = o0; i < o1; i++) ids.push_back(c->cat.keys[key].id(v->label_values[i]));
+            std::sort(ids.begin(), ids.end());
+            ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+            cell = ids;
+            stt = ids.empty() ? KP_LABEL_DOES_NOT_EXIST : KP_LABEL_IN;
+            if (ids.size() > 1) multi[key] = 1;
+        }
+    }
+    // offering-role keys are multi-valued on the type side in AWS (zone, capacity-type, ...): treat every key
+    // that appears in offerings as multi so their value masks exist
+    for (int k = 0; k < v->n_offering_keys; k++) multi[ok[k]] = 1;
+    // offering values
+    const int O = v->n_offerings, KO = v->n_offering_keys;
+    auto role = [&](const char* n) { return c->cat.find_key(n); };
+    c->key_zone = role("topology.kubernetes.io/zone");
+    c->key_ct = role("karpenter.sh/capacity-type");
+    c->key_zoneid = role("topology.k8s.aws/zone-id");
+    c->key_resvid = role("karpenter.k8s.aws/capacity-reservation-id");
+    c->key_resvtype = role("karpenter.k8s.aws/capacity-reservation-type");
+    for (int k = 0; k < KO; k++) {
+        const int key = ok[k];
+        if (key != c->key_zone && key != c->key_ct && key != c->key_zoneid && key != c->key_resvid &&
+            key != c->key_resvtype)
+            return fail(ctx, KP_E_UNSUPPORTED, "offering requirement key outside {zone, capacity-type, zone-id, reservation}");
+    }
+    if (c->key_zone < 0 || c->key_ct < 0) return fail(ctx, KP_E_INVALID, "offerings need zone and capacity-type keys");
+    int kz = -1, kc = -1, kzi = -1, kri = -1, krt = -1;
+    for (int k = 0; k < KO; k++) {
+        if (ok[k] == c->key_zone) kz = k;
+        if (ok[k] == c->key_ct) kc = k;
+        if (ok[k] == c->key_zoneid) kzi = k;
+        if (ok[k] == c->key_resvid) kri = k;
+        if (ok[k] == c->key_resvtype) krt = k;
+    }
+    std::vector<int> zslots, cslots;  // value ids
+    std::map<int, int> zone_to_zid;   // zone value id → zone-id value id or -1
+    c->off_type.assign(O, 0);
+    c->off_slot.assign(O, -1);
+    std::vector<int> off_zone(O), off_ct(O);
+    std::vector<uint8_t> avail(O);
+    for (int o = 0; o < O; o++) {
+        const int t = v->offering_type[o];
+        if (t < 0 || t >= T) return fail(ctx, KP_E_INVALID, "offering_type out of range");
+        c->off_type[o] = t;
+        avail[o] = v->offering_available[o] ? 1 : 0;
+        auto lab = [&](int k, int& state) -> const char* {
+            if (k < 0) {
+                state = KP_LABEL_ABSENT;
+                return nullptr;
+            }
+            state = v->offering_label_state[(size_t)o * KO + k];
+            return v->offering_label_values[(size_t)o * KO + k];
+        };
+        int sz, sc, szi, sri, srt;
+        const char* z = lab(kz, sz);
+        const char* ct = lab(kc, sc);
+        const char* zi = lab(kzi, szi);
+        lab(kri, sri);
+        lab(krt, srt);
+        if (sz != KP_LABEL_IN || sc != KP_LABEL_IN) return fail(ctx, KP_E_UNSUPPORTED, "offering without zone / capacity-type");
+        if (sri == KP_LABEL_IN || srt == KP_LABEL_IN)
+            return fail(ctx, KP_E_UNSUPPORTED, "reserved (capacity-reservation) offerings are not supported by this build");
+        if (sri == KP_LABEL_ABSENT || srt == KP_LABEL_ABSENT)
+            return fail(ctx, KP_E_UNSUPPORTED, "od/spot offerings must carry reservation keys as DoesNotExist (offering.go:144-145)");
+        const int zv = c->cat.keys[c->key_zone].id(z), cv = c->cat.keys[c->key_ct].id(ct);
+        int ziv = -1;
+        if (szi == KP_LABEL_IN) ziv = c->cat.keys[c->key_zoneid].id(zi);
+        else if (szi == KP_LABEL_DOES_NOT_EXIST) return fail(ctx, KP_E_UNSUPPORTED, "zone-id DoesNotExist on an offering");
+        auto itz = zone_to_zid.find(zv);
+        if (itz == zone_to_zid.end()) zone_to_zid[zv] = ziv;
+        else if (itz->second != ziv) return fail(ctx, KP_E_UNSUPPORTED, "zone-id is not a function of zone");
+        int zi_ = (int)(std::find(zslots.begin(), zslots.end(), zv) - zslots.begin());
+        if (zi_ == (int)zslots.size()) zslots.push_back(zv);
+        int ci_ = (int)(std::find(cslots.begin(), cslots.end(), cv) - cslots.begin());
+        if (ci_ == (int)cslots.size()) cslots.push_back(cv);
+        off_zone[o] = zi_;
+        off_ct[o] = ci_;
+    }
+    const int NZ = (int)zslots.size(), NC = (int)cslots.size();
+    if (NZ * NC > KP_MAX_SLOTS) return fail(ctx, KP_E_UNSUPPORTED, "more than 64 zone x capacity-type pools");
+    c->n_slots = NZ * NC;
+    c->slot_zone.assign(c->n_slots, 0);
+    c->slot_ct.assign(c->n_slots, 0);
+    c->slot_zoneid.assign(c->n_slots, -1);
+    for (int zi_ = 0; zi_ < NZ; zi_++)
+        for (int ci_ = 0; ci_ < NC; ci_++) {
+            const int s = zi_ * NC + ci_;
+            c->slot_zone[s] = zslots[zi_];
+            c->slot_ct[s] = cslots[ci_];
+            c->slot_zoneid[s] = zone_to_zid[zslots[zi_]];
+        }
+    c->slot_price.assign((size_t)T * KP_MAX_SLOTS, 1.7976931348623157e308);
+    for (int o = 0; o < O; o++) {
+        const int s = off_zone[o] * NC + off_ct[o];
+        c->off_slot[o] = s;
+        c->slot_price[(size_t)c->off_type[o] * KP_MAX_SLOTS + s] = v->offering_price[o];
+    }
+    c->avail_zc.assign(T, 0);
+    rebuild_avail(c, avail);
+    // multi-valued keys: value masks (<= 64 values)
+    c->cat_kflags.assign(Kc, 0);
+    c->cat_multi.assign(Kc, -1);
+    c->n_multi = 0;
+    for (int k = 0; k < Kc; k++) {
+        bool present = false;
+        for (int t = 0; t < T && !present; t++) present = st[(size_t)t * Kc + k] != KP_LABEL_ABSENT;
+        if (!present && !multi[k]) continue;  // offering-only key absent from every type
+        if (multi[k]) {
+            if (c->cat.keys[k].vals.size() > 64) return fail(ctx, KP_E_UNSUPPORTED, "multi-valued label with > 64 values");
+            c->cat_kflags[k] = KF_CAT_MULTI;
+            c->cat_multi[k] = c->n_multi++;
+        } else {
+            c->cat_kflags[k] = KF_CAT_SINGLE;
+        }
+    }
+    const int TW = c->TW;
+    std::vector<uint16_t> tval((size_t)Kc * T, VAL_ABSENT);
+    std::vector<uint64_t> mmask((size_t)std::max(1, c->n_multi) * T, 0), dne((size_t)Kc * TW, 0);
+    for (int k = 0; k < Kc; k++) {
+        for (int t = 0; t < T; t++) {
+            const int8_t s = st[(size_t)t * Kc + k];
+            if (s == KP_LABEL_DOES_NOT_EXIST) dne[(size_t)k * TW + t / 64] |= 1ull << (t % 64);
+            if (c->cat_kflags[k] & KF_CAT_SINGLE) {
+                if (s == KP_LABEL_DOES_NOT_EXIST) tval[(size_t)k * T + t] = VAL_DNE;
+                else if (s == KP_LABEL_IN) tval[(size_t)k * T + t] = (uint16_t)tv[(size_t)t * Kc + k][0];
+                if (c->cat.keys[k].vals.size() >= VAL_ABSENT) return fail(ctx, KP_E_UNSUPPORTED, "label dictionary too large");
+            } else if (c->cat_kflags[k] & KF_CAT_MULTI) {
+                uint64_t m = 0;
+                if (s == KP_LABEL_IN)
+                    for (int id : tv[(size_t)t * Kc + k]) m |= 1ull << id;
+                mmask[(size_t)c->cat_multi[k] * T + t] = m;
+            }
+        }
+    }
+    c->alloc_rt.assign((size_t)R * T, 0);
+    c->cap_rt.assign((size_t)R * T, 0);
+    std::vector<uint64_t> nonneg(TW, 0);
+    for (int t = 0; t < T; t++) {
+        bool nn = true;
+        for (int r = 0; r < R; r++) {
+            c->alloc_rt[(size_t)r * T + t] = v->allocatable[(size_t)t * R + r];
+            c->cap_rt[(size_t)r * T + t] = v->capacity[(size_t)t * R + r];
+            nn = nn && v->allocatable[(size_t)t * R + r] >= 0;
+        }
+        if (nn) nonneg[t / 64] |= 1ull << (t % 64);
+    }
+    std::vector<int> idx(T);
+    for (int t = 0; t < T; t++) idx[t] = t;
+    std::sort(idx.begin(), idx.end(), [&](int a, int b) { return c->type_names[a] < c->type_names[b]; });
+    std::vector<uint32_t> rank(T);
+    for (int i = 0; i < T; i++) {
+        rank[idx[i]] = (i > 0 && c->type_names[idx[i]] == c->type_names[idx[i - 1]]) ? rank[idx[i - 1]] : (uint32_t)i;
+    }
+    hipStream_t s = c->stream;
+    HIPCHK(c->d_type_val.upload(tval, s));
+    HIPCHK(c->d_multi_mask.upload(mmask, s));
+    HIPCHK(c->d_dne_mask.upload(dne, s));
+    HIPCHK(c->d_alloc.upload(c->alloc_rt, s));
+    HIPCHK(c->d_cap.upload(c->cap_rt, s));
+    HIPCHK(c->d_avail_zc.upload(c->avail_zc, s));
+    HIPCHK(c->d_slot_price.upload(c->slot_price, s));
+    HIPCHK(c->d_slot_zone.upload(c->slot_zone, s));
+    HIPCHK(c->d_slot_ct.upload(c->slot_ct, s));
+    HIPCHK(c->d_slot_zoneid.upload(c->slot_zoneid, s));
+    HIPCHK(c->d_name_rank.upload(rank, s));
+    HIPCHK(c->d_nonneg.upload(nonneg, s));
+    HIPCHK(hipStreamSynchronize(s));
+    c->epoch = epoch;
+    c->have_catalog = true;
+    c->prepared = c->executed = false;
+    return KP_OK;
+} catch (const std::exception& e) {
+    return fail(ctx, KP_E_INVALID, e.what());
+}
+
+extern "C" kp_status kp_catalog_patch_avail(kp_ctx* ctx, const uint8_t* available, int32_t n, uint64_t epoch) {
+    if (!ctx || !available) return KP_E_INVALID;
+    if (!ctx->have_catalog) return fail(ctx, KP_E_STATE, "no catalog");
+    if (n != (int)ctx->off_type.size()) return fail(ctx, KP_E_INVALID, "offering count mismatch");
+    HIPCHK(hipSetDevice(ctx->device));
+    rebuild_avail(ctx, std::vector<uint8_t>(available, available + n));
+    HIPCHK(ctx->d_avail_zc.upload(ctx->avail_zc, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->epoch = epoch;
+    return KP_OK;
+}
+
+extern "C" kp_status kp_catalog_patch_price(kp_ctx* ctx, const int32_t* idx, const double* price, int32_t n,
+                                            uint64_t epoch) {
+    if (!ctx || (n > 0 && (!idx || !price))) return KP_E_INVALID;
+    if (!ctx->have_catalog) return fail(ctx, KP_E_STATE, "no catalog");
+    HIPCHK(hipSetDevice(ctx->device));
+    for (int i = 0; i < n; i++) {
+        if (idx[i] < 0 || idx[i] >= (int)ctx->off_type.size()) return fail(ctx, KP_E_INVALID, "offering index");
+        ctx->slot_price[(size_t)ctx->off_type[idx[i]] * KP_MAX_SLOTS + ctx->off_slot[idx[i]]] = price[i];
+    }
+    HIPCHK(ctx->d_slot_price.upload(ctx->slot_price, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->epoch = epoch;
+    return KP_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// solve: prepare (encode + upload)
+// ---------------------------------------------------------------------------------------------
+static bool build_hreqs(kp_ctx* c, const kp_requirement* rs, int n, std::map<int, HReq>& out, std::string& err) {
+    for (int i = 0; i < n; i++) {
+        const kp_requirement& r = rs[i];
+        if (!r.key || r.op < 0 || r.op > 5) {
+            err = "bad requirement";
+            return false;
+        }
+        HReq q;
+        q.key = c->sol.key(normalize(r.key));
+        q.complement = !(r.op == KP_OP_IN || r.op == KP_OP_DOES_NOT_EXIST);
+        if (r.op == KP_OP_IN || r.op == KP_OP_NOT_IN) {
+            for (int j = 0; j < r.n_values; j++) q.vals.push_back(c->sol.keys[q.key].id(r.values[j] ? r.values[j] : ""));
+            std::sort(q.vals.begin(), q.vals.end());
+            q.vals.erase(std::unique(q.vals.begin(), q.vals.end()), q.vals.end());
+        }
+        if (r.op == KP_OP_GT || r.op == KP_OP_LT) {
+            int64_t x = 0;
+            go_atoi(r.n_values > 0 && r.values[0] ? r.values[0] : "", x);
+            if (r.op == KP_OP_GT) {
+                q.has_gt = true;
+                q.gt = x;
+            } else {
+                q.has_lt = true;
+                q.lt = x;
+            }
+        }
+        q.has_min = r.min_values >= 0;
+        q.minv = r.min_values;
+        auto it = out.find(q.key);
+        if (it == out.end()) {
+            out.emplace(q.key, q);
+            continue;
+        }
+        // Requirements.Add: requirement.Intersection(existing); values filtered after all keys are interned
+        HReq& e = it->second;
+        HReq o;
+        o.key = q.key;
+        o.complement = q.complement && e.complement;
+        o.has_gt = q.has_gt || e.has_gt;
+        o.gt = (q.has_gt && e.has_gt) ? std::max(q.gt, e.gt) : (q.has_gt ? q.gt : e.gt);
+        o.has_lt = q.has_lt || e.has_lt;
+        o.lt = (q.has_lt && e.has_lt) ? std::min(q.lt, e.lt) : (q.has_lt ? q.lt : e.lt);
+        o.has_min = q.has_min || e.has_min;
+        o.minv = (q.has_min && e.has_min) ? std::max(q.minv, e.minv) : (q.has_min ? q.minv : e.minv);
+        if (o.has_gt && o.has_lt && o.gt >= o.lt) {
+            HReq dne;
+            dne.key = q.key;
+            dne.has_min = o.has_min;
+            dne.minv = o.minv;
+            it->second = dne;
+            continue;
+        }
+        std::vector<int> vals;
+        if (q.complement && e.complement)
+            std::set_union(q.vals.begin(), q.vals.end(), e.vals.begin(), e.vals.end(), std::back_inserter(vals));
+        else if (q.complement)
+            std::set_difference(e.vals.begin(), e.vals.end(), q.vals.begin(), q.vals.end(), std::back_inserter(vals));
+        else if (e.complement)
+            std::set_difference(q.vals.begin(), q.vals.end(), e.vals.begin(), e.vals.end(), std::back_inserter(vals));
+        else
+            std::set_intersection(q.vals.begin(), q.vals.end(), e.vals.begin(), e.vals.end(), std::back_inserter(vals));
+        o.vals.clear();
+        for (int vv : vals) {
+            bool ok = true;
+            if (o.has_gt || o.has_lt) {
+                int64_t x = 0;
+                if (!go_atoi(c->sol.keys[q.key].vals[vv].c_str(), x)) ok = false;
+                else if ((o.has_gt && o.gt >= x) || (o.has_lt && o.lt <= x)) ok = false;
+            }
+            if (ok) o.vals.push_back(vv);
+        }
+        if (!o.complement) o.has_gt = o.has_lt = false;
+        it->second = o;
+    }
+    return true;
+}
+
+static bool tolerates(const kp_taint& taint, const kp_toleration* tols, int n) {
+    for (int i = 0; i < n; i++) {
+        const kp_toleration& t = tols[i];
+        const char* te = t.effect ? t.effect : "";
+        const char* tk = t.key ? t.key : "";
+        if (*te && strcmp(te, taint.effect ? taint.effect : "")) continue;
+        if (*tk && strcmp(tk, taint.key ? taint.key : "")) continue;
+        if (t.op == KP_TOL_EXISTS) return true;
+        if (!strcmp(t.value ? t.value : "", taint.value ? taint.value : "")) return true;
+    }
+    return false;
+}
+
+extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try {
+    if (!ctx || !in) return KP_E_INVALID;
+    if (!ctx->have_catalog) return fail(ctx, KP_E_STATE, "kp_solve before kp_catalog_upload");
+    const auto t0 = clk::now();
+    HIPCHK(hipSetDevice(ctx->device));
+    kp_ctx* c = ctx;
+    c->prepared = c->executed = false;
+    if (in->min_values_policy != KP_MIN_VALUES_STRICT)
+        return fail(ctx, KP_E_UNSUPPORTED, "MIN_VALUES_POLICY=BestEffort is not supported by this build");
+    if (in->n_existing > 0) return fail(ctx, KP_E_UNSUPPORTED, "existing nodes are not supported by this build");
+    const int T = c->T, TW = c->TW, R = c->R, P = in->pods.n_pods, C = in->n_classes;
+    // ---- dictionaries: catalog ∪ solve strings ----
+    c->sol = c->cat;
+    std::vector<std::map<int, HReq>> creq(C);
+    std::string err;
+    for (int i = 0; i < C; i++)
+        if (!build_hreqs(c, in->classes[i].requirements, in->classes[i].n_requirements, creq[i], err)) return fail(ctx, KP_E_INVALID, err);
+    // templates: NodePools ordered by weight desc, name asc ([core] NodePoolList.OrderByWeight)
+    std::vector<int> npo(in->n_nodepools);
+    for (int i = 0; i < in->n_nodepools; i++) npo[i] = i;
+    std::sort(npo.begin(), npo.end(), [&](int a, int b) {
+        if (in->nodepools[a].weight != in->nodepools[b].weight) return in->nodepools[a].weight > in->nodepools[b].weight;
+        return strcmp(in->nodepools[a].name, in->nodepools[b].name) < 0;
+    });
+    const int NT = (int)npo.size();
+    if (NT > 32) return fail(ctx, KP_E_UNSUPPORTED, "more than 32 NodePools");
+    std::vector<std::map<int, HReq>> treq(NT);
+    for (int j = 0; j < NT; j++) {
+        const kp_nodepool& np = in->nodepools[npo[j]];
+        if (!build_hreqs(c, np.requirements, np.n_requirements, treq[j], err)) return fail(ctx, KP_E_INVALID, err);
+    }
+    for (int i = 0; i < C; i++)
+        for (auto& kv : creq[i])
+            if (kv.second.has_min) return fail(ctx, KP_E_INVALID, "pod requirements cannot carry minValues");
+    const int K = (int)c->sol.keys.size();
+    if (K > KP_MAX_KEYS) return fail(ctx, KP_E_UNSUPPORTED, "too many label keys");
+    // ---- key layout ----
+    std::vector<uint32_t> kflags(K, 0);
+    std::vector<int32_t> kcat(K, -1), kmulti(K, -1), woff(K), nw(K), nval(K), vbase(K);
+    std::vector<uint8_t> isint;
+    std::vector<int64_t> ival;
+    int DW = 0;
+    for (int k = 0; k < K; k++) {
+        const KeyDict& kd = c->sol.keys[k];
+        if (well_known(kd.name)) kflags[k] |= KF_WELL_KNOWN;
+        if (k < c->Kcat && c->cat_kflags[k]) {
+            kflags[k] |= c->cat_kflags[k];
+            kcat[k] = k;
+            kmulti[k] = c->cat_multi[k];
+        }
+        nval[k] = (int)kd.vals.size();
+        nw[k] = std::max(1, (nval[k] + 63) / 64);
+        woff[k] = DW;
+        DW += nw[k];
+        vbase[k] = (int)isint.size();
+        for (auto& s : kd.vals) {
+            int64_t x = 0;
+            isint.push_back(go_atoi(s.c_str(), x) ? 1 : 0);
+            ival.push_back(x);
+        }
+        if ((kflags[k] & KF_CAT_MULTI) && nval[k] > 64)
+            return fail(ctx, KP_E_UNSUPPORTED, "multi-valued label with > 64 values after adding pod values");
+    }
+    // ---- class digests: pod classes then templates ----
+    const int CT = C + NT;
+    std::vector<ReqHdr> chdr((size_t)CT * K);
+    std::vector<uint64_t> cwords((size_t)CT * DW, 0);
+    std::vector<int32_t> koff(CT + 1, 0), ckeys, cwsoff;
+    std::vector<uint32_t> cflags(CT, 0);
+    std::vector<int32_t> min_keys((size_t)NT * KP_MAX_CLASS_KEYS, -1);
+    auto encode = [&](int row, const std::map<int, HReq>& rq) -> bool {
+        int so = 0;
+        for (auto& kv : rq) {
+            const HReq& q = kv.second;
+            ReqHdr h{};
+            h.flags = RF_DEF | (q.complement ? RF_CMP : 0u) | (q.has_gt ? RF_GT : 0u) | (q.has_lt ? RF_LT : 0u) |
+                      (q.has_min ? RF_MIN : 0u);
+            h.minv = q.minv;
+            h.gt = q.gt;
+            h.lt = q.lt;
+            chdr[(size_t)row * K + q.key] = h;
+            for (int vv : q.vals) cwords[(size_t)row * DW + woff[q.key] + vv / 64] |= 1ull << (vv % 64);
+            ckeys.push_back(q.key);
+            cwsoff.push_back(so);
+            so += nw[q.key];
+            if (q.key == c->key_zone || q.key == c->key_ct || q.key == c->key_zoneid || q.key == c->key_resvid ||
+                q.key == c->key_resvtype)
+                cflags[row] |= 1u;
+        }
+        if ((int)rq.size() > KP_MAX_CLASS_KEYS || so > KP_MAX_SCR_WORDS) return false;
+        koff[row + 1] = (int)ckeys.size();
+        return true;
+    };
+    for (int i = 0; i < C; i++)
+        if (!encode(i, creq[i])) return fail(ctx, KP_E_UNSUPPORTED, "pod class constrains too many labels");
+    for (int j = 0; j < NT; j++) {
+        if (!encode(C + j, treq[j])) return fail(ctx, KP_E_UNSUPPORTED, "NodePool constrains too many labels");
+        int q = 0;
+        for (auto& kv : treq[j])
+            if (kv.second.has_min) min_keys[(size_t)j * KP_MAX_CLASS_KEYS + q++] = kv.first;
+    }
+    // ---- templates: taints, daemon overhead, limits, instance-type rows ----
+    std::vector<uint32_t> tol(std::max(C, 1), 0);
+    std::vector<int64_t> daemon((size_t)NT * R, 0), remaining((size_t)NT * R, 0);
+    std::vector<uint8_t> limit_set((size_t)NT * R, 0);
+    std::vector<uint64_t> rows((size_t)NT * TW, 0);
+    c->tmpl_np.assign(npo.begin(), npo.end());
+    for (int j = 0; j < NT; j++) {
+        const kp_nodepool& np = in->nodepools[npo[j]];
+        for (int i = 0; i < C; i++) {
+            bool all = true;
+            for (int q = 0; q < np.n_taints && all; q++)
+                all = tolerates(np.taints[q], in->classes[i].tolerations, in->classes[i].n_tolerations);
+            if (all) tol[i] |= 1u << j;
+        }
+        for (int r = 0; r < R; r++) {
+            if (np.daemon_overhead) daemon[(size_t)j * R + r] = np.daemon_overhead[r];
+            if (np.limit_set && np.limit_set[r]) {
+                limit_set[(size_t)j * R + r] = 1;
+                remaining[(size_t)j * R + r] = np.limit_remaining[r];
+            }
+        }
+        if (np.n_types < 0) {
+            for (int t = 0; t < T; t++) rows[(size_t)j * TW + t / 64] |= 1ull << (t % 64);
+        } else {
+            for (int q = 0; q < np.n_types; q++) {
+                const int t = np.type_index[q];
+                if (t < 0 || t >= T) return fail(ctx, KP_E_INVALID, "nodepool type_index out of range");
+                rows[(size_t)j * TW + t / 64] |= 1ull << (t % 64);
+            }
+        }
+    }
+    // ---- pods ----
+    std::vector<int32_t> pcls(P), pshape(P);
+    std::vector<int64_t> preq((size_t)P * R), fields((size_t)P * 4);
+    int cpu_axis = -1, mem_axis = -1;
+    for (int r = 0; r < R; r++) {
+        if (c->resource_names[r] == "cpu") cpu_axis = r;
+        if (c->resource_names[r] == "memory") mem_axis = r;
+    }
+    if (cpu_axis < 0 || mem_axis < 0) return fail(ctx, KP_E_INVALID, "catalog lacks cpu/memory axes");
+    std::vector<uint8_t> active(R, 0);
+    for (int j = 0; j < NT; j++)
+        for (int r = 0; r < R; r++)
+            if (daemon[(size_t)j * R + r] != 0) active[r] = 1;
+    struct ShapeKey {
+        int cls;
+        std::vector<int64_t> req;
+        bool operator<(const ShapeKey& o) const { return cls != o.cls ? cls < o.cls : req < o.req; }
+    };
+    std::map<ShapeKey, int> shapes;
+    std::unordered_map<uint64_t, int> uidseen;
+    uidseen.reserve((size_t)P * 2);
+    bool uid_collision = false;
+    const kp_pods_view& pv = in->pods;
+    for (int p = 0; p < P; p++) {
+        const int cl = pv.class_id[p];
+        if (cl < 0 || cl >= C) return fail(ctx, KP_E_INVALID, "pod class out of range");
+        pcls[p] = cl;
+        ShapeKey sk{cl, std::vector<int64_t>(pv.requests + (size_t)p * R, pv.requests + (size_t)(p + 1) * R)};
+        for (int r = 0; r < R; r++) {
+            preq[(size_t)p * R + r] = sk.req[r];
+            if (sk.req[r] != 0) active[r] = 1;
+            if (sk.req[r] < 0) return fail(ctx, KP_E_INVALID, "negative request");
+        }
+        auto it = shapes.find(sk);
+        if (it == shapes.end()) it = shapes.emplace(std::move(sk), (int)shapes.size()).first;
+        pshape[p] = it->second;
+        // NewQueue key: cpu desc, memory desc, creation asc, UID asc.  The UID enters as its first 8 bytes
+        // (big-endian, order-preserving); if two distinct UIDs share that prefix, exact string ranks are used.
+        const char* u = pv.uids && pv.uids[p] ? pv.uids[p] : "";
+        uint64_t uk = 0;
+        const char* q = u;
+        for (int i = 0; i < 8; i++) {
+            uk <<= 8;
+            if (*q) uk |= (uint8_t)*q++;
+        }
+        fields[(size_t)p * 4 + 0] = preq[(size_t)p * R + cpu_axis];
+        fields[(size_t)p * 4 + 1] = preq[(size_t)p * R + mem_axis];
+        fields[(size_t)p * 4 + 2] = pv.creation_ns ? pv.creation_ns[p] : 0;
+        fields[(size_t)p * 4 + 3] = (int64_t)(uk ^ 0x8000000000000000ull);
+        auto ins = uidseen.emplace(uk, p);
+        if (!ins.second && strcmp(pv.uids[ins.first->second] ? pv.uids[ins.first->second] : "", u) != 0) uid_collision = true;
+    }
+    if (uid_collision) {
+        std::vector<int> idx(P);
+        for (int p = 0; p < P; p++) idx[p] = p;
+        std::sort(idx.begin(), idx.end(), [&](int a, int b) { return strcmp(pv.uids[a], pv.uids[b]) < 0; });
+        int rank = 0;
+        for (int i = 0; i < P; i++) {
+            if (i > 0 && strcmp(pv.uids[idx[i]], pv.uids[idx[i - 1]]) != 0) rank = i;
+            fields[(size_t)idx[i] * 4 + 3] = (int64_t)((uint64_t)rank ^ 0x8000000000000000ull);
+        }
+    }
+    KpDev& d = c->dev;
+    d = KpDev{};
+    d.n_active = 0;
+    for (int r = 0; r < R; r++)
+        if (active[r]) d.active_axes[d.n_active++] = r;
+    // ---- device buffers ----
+    hipStream_t s = c->stream;
+    std::vector<ReqHdr> empty_hdr(K);
+    memset(empty_hdr.data(), 0, empty_hdr.size() * sizeof(ReqHdr));
+    std::vector<uint64_t> empty_words(DW, 0);
+    HIPCHK(c->d_kflags.upload(kflags, s));
+    HIPCHK(c->d_kcat.upload(kcat, s));
+    HIPCHK(c->d_kmulti.upload(kmulti, s));
+    HIPCHK(c->d_woff.upload(woff, s));
+    HIPCHK(c->d_nw.upload(nw, s));
+    HIPCHK(c->d_nval.upload(nval, s));
+    HIPCHK(c->d_vbase.upload(vbase, s));
+    if (isint.empty()) {
+        isint.push_back(0);
+        ival.push_back(0);
+    }
+    HIPCHK(c->d_val_isint.upload(isint, s));
+    HIPCHK(c->d_val_int.upload(ival, s));
+    HIPCHK(c->d_cls_koff.upload(koff, s));
+    if (ckeys.empty()) {
+        ckeys.push_back(0);
+        cwsoff.push_back(0);
+    }
+    HIPCHK(c->d_cls_keys.upload(ckeys, s));
+    HIPCHK(c->d_cls_wsoff.upload(cwsoff, s));
+    HIPCHK(c->d_cls_hdr.upload(chdr, s));
+    HIPCHK(c->d_cls_words.upload(cwords, s));
+    HIPCHK(c->d_cls_flags.upload(cflags, s));
+    HIPCHK(c->d_V.ensure((size_t)CT * TW));
+    HIPCHK(c->d_tmpl_rows.upload(rows, s));
+    HIPCHK(c->d_tmpl_opts.ensure((size_t)std::max(NT, 1) * TW));
+    HIPCHK(c->d_tmpl_ok.ensure(std::max(NT, 1)));
+    HIPCHK(c->d_tol.upload(tol, s));
+    HIPCHK(c->d_daemon.upload(daemon, s));
+    HIPCHK(c->d_limit_set.upload(limit_set, s));
+    HIPCHK(c->d_remaining.upload(remaining, s));
+    c->h_remaining = remaining;
+    HIPCHK(c->d_min_keys.upload(min_keys, s));
+    HIPCHK(c->d_pod_cls.upload(pcls, s));
+    HIPCHK(c->d_pod_shape.upload(pshape, s));
+    HIPCHK(c->d_pod_req.upload(preq, s));
+    HIPCHK(c->d_sort_fields.upload(fields, s));
+    HIPCHK(c->d_empty_hdr.upload(empty_hdr, s));
+    HIPCHK(c->d_empty_words.upload(empty_words, s));
+    const int NCcap = std::min(KP_MAX_NC, std::max(P, 1));
+    HIPCHK(c->d_nc_hdr.ensure((size_t)NCcap * K));
+    HIPCHK(c->d_nc_words.ensure((size_t)NCcap * DW));
+    HIPCHK(c->d_nc_opts.ensure((size_t)NCcap * TW));
+    HIPCHK(c->d_nc_req.ensure((size_t)NCcap * R));
+    HIPCHK(c->d_nc_tmpl.ensure(NCcap));
+    HIPCHK(c->d_qbuf.ensure(std::max(P, 1)));
+    HIPCHK(c->d_last_len.ensure(std::max(P, 1)));
+    HIPCHK(c->d_pod_result.ensure(std::max(P, 1)));
+    HIPCHK(c->d_pod_order.ensure(std::max(P, 1)));
+    HIPCHK(c->d_perm_a.ensure(std::max(P, 1)));
+    HIPCHK(c->d_perm_b.ensure(std::max(P, 1)));
+    HIPCHK(c->d_keys_a.ensure(std::max(P, 1)));
+    HIPCHK(c->d_keys_b.ensure(std::max(P, 1)));
+    HIPCHK(c->d_nc_count.ensure(1));
+    HIPCHK(c->d_err.ensure(1));
+    HIPCHK(c->d_nc_npods.ensure(NCcap));
+    HIPCHK(c->d_nc_slice_pos.ensure(NCcap));
+    HIPCHK(c->d_nc_nopts.ensure(NCcap));
+    HIPCHK(c->d_nc_valid.ensure(NCcap));
+    HIPCHK(c->d_nc_ntypes.ensure(NCcap));
+    const int M = in->max_instance_types > 0 ? std::min(in->max_instance_types, T) : T;
+    HIPCHK(c->d_nc_types.ensure((size_t)NCcap * M));
+    HIPCHK(c->d_stats.ensure(ST_COUNT));
+    if (P > 0) {
+        size_t tb = 0;
+        HIPCHK(kp_queue_sort(nullptr, P, c->d_perm_a.p, c->d_perm_b.p, c->d_keys_a.p, c->d_keys_b.p, nullptr, &tb, s, nullptr));
+        HIPCHK(c->d_sort_temp.ensure(tb));
+        c->sort_temp_bytes = tb;
+    }
+    // ---- KpDev ----
+    d.T = T;
+    d.TW = TW;
+    d.R = R;
+    d.K = K;
+    d.n_slots = c->n_slots;
+    d.n_multi = c->n_multi;
+    d.type_val = c->d_type_val.p;
+    d.multi_mask = c->d_multi_mask.p;
+    d.dne_mask = c->d_dne_mask.p;
+    d.alloc = c->d_alloc.p;
+    d.cap = c->d_cap.p;
+    d.avail_zc = c->d_avail_zc.p;
+    d.slot_price = c->d_slot_price.p;
+    d.slot_zone = c->d_slot_zone.p;
+    d.slot_ct = c->d_slot_ct.p;
+    d.slot_zoneid = c->d_slot_zoneid.p;
+    d.name_rank = c->d_name_rank.p;
+    d.nonneg = c->d_nonneg.p;
+    d.kflags = c->d_kflags.p;
+    d.kcat = c->d_kcat.p;
+    d.kmulti = c->d_kmulti.p;
+    d.woff = c->d_woff.p;
+    d.nw = c->d_nw.p;
+    d.nval = c->d_nval.p;
+    d.vbase = c->d_vbase.p;
+    d.val_isint = c->d_val_isint.p;
+    d.val_int = c->d_val_int.p;
+    d.DW = DW;
+    d.key_zone = c->key_zone;
+    d.key_ct = c->key_ct;
+    d.key_zoneid = c->key_zoneid;
+    d.key_resvid = c->key_resvid;
+    d.key_resvtype = c->key_resvtype;
+    d.C = C;
+    d.NT = NT;
+    d.cls_koff = c->d_cls_koff.p;
+    d.cls_keys = c->d_cls_keys.p;
+    d.cls_wsoff = c->d_cls_wsoff.p;
+    d.cls_hdr = c->d_cls_hdr.p;
+    d.cls_words = c->d_cls_words.p;
+    d.cls_flags = c->d_cls_flags.p;
+    d.V = c->d_V.p;
+    d.tmpl_rows = c->d_tmpl_rows.p;
+    d.tmpl_opts = c->d_tmpl_opts.p;
+    d.tmpl_ok = c->d_tmpl_ok.p;
+    d.tol = c->d_tol.p;
+    d.daemon = c->d_daemon.p;
+    d.limit_set = c->d_limit_set.p;
+    d.remaining = c->d_remaining.p;
+    d.min_keys = c->d_min_keys.p;
+    d.P = P;
+    d.pod_cls = c->d_pod_cls.p;
+    d.pod_shape = c->d_pod_shape.p;
+    d.pod_req = c->d_pod_req.p;
+    d.queue0 = nullptr;  // set by execute (sort output)
+    d.NCcap = NCcap;
+    d.nc_hdr = c->d_nc_hdr.p;
+    d.nc_words = c->d_nc_words.p;
+    d.nc_opts = c->d_nc_opts.p;
+    d.nc_req = c->d_nc_req.p;
+    d.nc_tmpl = c->d_nc_tmpl.p;
+    d.empty_hdr = c->d_empty_hdr.p;
+    d.empty_words = c->d_empty_words.p;
+    d.qbuf = c->d_qbuf.p;
+    d.last_len = c->d_last_len.p;
+    d.pod_result = c->d_pod_result.p;
+    d.pod_order = c->d_pod_order.p;
+    d.nc_count = c->d_nc_count.p;
+    d.nc_npods = c->d_nc_npods.p;
+    d.nc_slice_pos = c->d_nc_slice_pos.p;
+    d.nc_nopts = c->d_nc_nopts.p;
+    d.nc_valid = c->d_nc_valid.p;
+    d.M = M;
+    d.nc_types = c->d_nc_types.p;
+    d.nc_ntypes = c->d_nc_ntypes.p;
+    d.stats = c->d_stats.p;
+    d.err = c->d_err.p;
+    c->P = P;
+    c->C = C;
+    c->NT = NT;
+    c->K = K;
+    c->DW = DW;
+    c->M = M;
+    HIPCHK(hipStreamSynchronize(s));
+    c->ns_prep = ns_since(t0);
+    c->prepared = true;
+    return KP_OK;
+} catch (const std::exception& e) {
+    return fail(ctx, KP_E_INVALID, e.what());
+}
+
+// ---------------------------------------------------------------------------------------------
+// solve: execute (device only)
+// ---------------------------------------------------------------------------------------------
+extern "C" kp_status kp_solve_execute(kp_ctx* ctx) {
+    if (!ctx) return KP_E_INVALID;
+    if (!ctx->prepared) return fail(ctx, KP_E_STATE, "kp_solve_execute before kp_solve_prepare");
+    HIPCHK(hipSetDevice(ctx->device));
+    kp_ctx* c = ctx;
+    KpDev& d = c->dev;
+    hipStream_t s = c->stream;
+    const auto t0 = clk::now();
+    // per-call state (remaining limits are mutated by the FFD kernel)
+    HIPCHK(hipMemsetAsync(c->d_nc_count.p, 0, sizeof(int32_t), s));
+    HIPCHK(hipMemsetAsync(c->d_err.p, 0, sizeof(int32_t), s));
+    if (!c->h_remaining.empty())
+        HIPCHK(hipMemcpyAsync(c->d_remaining.p, c->h_remaining.data(), c->h_remaining.size() * sizeof(int64_t),
+                              hipMemcpyHostToDevice, s));
+    int32_t* q0 = nullptr;
+    HIPCHK(hipEventRecord(c->ev[0], s));
+    if (d.P > 0) {
+        size_t tb = c->sort_temp_bytes;
+        HIPCHK(kp_queue_sort(c->d_sort_fields.p, d.P, c->d_perm_a.p, c->d_perm_b.p, c->d_keys_a.p, c->d_keys_b.p,
+                             c->d_sort_temp.p, &tb, s, &q0));
+    }
+    d.queue0 = q0;
+    HIPCHK(hipEventRecord(c->ev[1], s));
+    HIPCHK(kp_launch_class_mask(d, s));
+    HIPCHK(hipEventRecord(c->ev[2], s));
+    HIPCHK(kp_launch_template_init(d, s));
+    HIPCHK(hipEventRecord(c->ev[3], s));
+    HIPCHK(kp_launch_ffd(d, s));
+    HIPCHK(hipEventRecord(c->ev[4], s));
+    HIPCHK(kp_launch_finalize(d, d.NCcap, s));
+    HIPCHK(hipEventRecord(c->ev[5], s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (int i = 0; i < 5; i++) {
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]));
+        c->kernel_ms[i] = ms;
+    }
+    c->ns_exec = ns_since(t0);
+    c->executed = true;
+    return KP_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// solve: fetch (D2H + decode)
+// ---------------------------------------------------------------------------------------------
+extern "C" kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out) {
+    if (!ctx || !out) return KP_E_INVALID;
+    if (!ctx->executed) return fail(ctx, KP_E_STATE, "kp_solve_fetch before kp_solve_execute");
+    HIPCHK(hipSetDevice(ctx->device));
+    kp_ctx* c = ctx;
+    hipStream_t s = c->stream;
+    const auto t0 = clk::now();
+    int32_t N = 0, err = 0;
+    int64_t st[ST_COUNT];
+    HIPCHK(hipMemcpyAsync(&N, c->d_nc_count.p, sizeof N, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&err, c->d_err.p, sizeof err, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(st, c->d_stats.p, sizeof st, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (err) return fail(ctx, KP_E_UNSUPPORTED, "in-flight NodeClaim capacity (KP_MAX_NC) exceeded");
+    const int P = c->P, M = c->M;
+    std::vector<int32_t> npods(N), spos(N), nopts(N), valid(N), ntypes(N), tmpl(N), types((size_t)N * M), pres(P), pord(P);
+    if (N > 0) {
+        HIPCHK(hipMemcpyAsync(npods.data(), c->d_nc_npods.p, N * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(spos.data(), c->d_nc_slice_pos.p, N * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(nopts.data(), c->d_nc_nopts.p, N * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(valid.data(), c->d_nc_valid.p, N * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(ntypes.data(), c->d_nc_ntypes.p, N * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(tmpl.data(), c->d_nc_tmpl.p, N * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(types.data(), c->d_nc_types.p, (size_t)N * M * 4, hipMemcpyDeviceToHost, s));
+    }
+    if (P > 0) {
+        HIPCHK(hipMemcpyAsync(pres.data(), c->d_pod_result.p, P * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(pord.data(), c->d_pod_order.p, P * 4, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    c->last_N = N;
+    c->h_nc_tmpl = tmpl;
+    int n_ids = 0;
+    for (int i = 0; i < N; i++) n_ids += ntypes[i];
+    out->n_nodeclaims = N;
+    out->n_type_ids = n_ids;
+    kp_solve_stats& so = out->stats;
+    so = kp_solve_stats{};
+    so.pods_popped = st[ST_POPPED];
+    so.nodeclaim_evals = st[ST_NC_EVALS];
+    so.nodeclaim_candidates_scanned = st[ST_NC_SCANNED];
+    so.template_evals = st[ST_TMPL_EVALS];
+    so.existing_evals = st[ST_EXIST_EVALS];
+    so.sorts_fast = st[ST_SORT_FAST];
+    so.sorts_full = st[ST_SORT_FULL];
+    so.ns_host_prep = c->ns_prep;
+    so.ns_device_solve = c->ns_exec;
+    if (N > out->cap_nodeclaims || n_ids > out->cap_type_ids) return fail(ctx, KP_E_BUFFER, "output buffers too small");
+    int off = 0;
+    for (int i = 0; i < N; i++) {
+        out->nodeclaim_nodepool[i] = valid[i] ? c->tmpl_np[tmpl[i]] : -1;
+        out->nodeclaim_n_pods[i] = npods[i];
+        if (out->nodeclaim_slice_pos) out->nodeclaim_slice_pos[i] = spos[i];
+        if (out->nodeclaim_n_options) out->nodeclaim_n_options[i] = nopts[i];
+        out->nodeclaim_type_offset[i] = off;
+        for (int q = 0; q < ntypes[i]; q++) out->type_ids[off++] = types[(size_t)i * M + q];
+    }
+    out->nodeclaim_type_offset[N] = off;
+    for (int p = 0; p < P; p++) {
+        int r = pres[p];
+        int o = pord[p];
+        if (r >= 0 && !valid[r]) {
+            r = KP_POD_UNSCHEDULABLE;
+            o = -1;
+        }
+        out->pod_result[p] = r;
+        if (out->pod_order) out->pod_order[p] = o;
+    }
+    so.ns_device_finalize = ns_since(t0);
+    so.ns_total = c->ns_prep + c->ns_exec + so.ns_device_finalize;
+    return KP_OK;
+}
+
+extern "C" kp_status kp_last_kernel_times(kp_ctx* ctx, double* ms, int32_t n) {
+    if (!ctx || !ms) return KP_E_INVALID;
+    if (!ctx->executed) return fail(ctx, KP_E_STATE, "no execute yet");
+    for (int i = 0; i < n && i < 5; i++) ms[i] = ctx->kernel_ms[i];
+    return KP_OK;
+}
+
+extern "C" kp_status kp_solve(kp_ctx* ctx, const kp_solve_input* in, kp_solve_output* out) {
+    kp_status st = kp_solve_prepare(ctx, in);
+    if (st != KP_OK) return st;
+    st = kp_solve_execute(ctx);
+    if (st != KP_OK) return st;
+    return kp_solve_fetch(ctx, out);
+}
+
+extern "C" kp_status kp_result_nodeclaim_requirements(kp_ctx* ctx, int32_t nc, char* buf, int64_t cap, int64_t* needed) {
+    if (!ctx) return KP_E_INVALID;
+    if (!ctx->executed) return fail(ctx, KP_E_STATE, "no solve result");
+    if (nc < 0 || nc >= ctx->last_N) return fail(ctx, KP_E_INVALID, "nodeclaim index");
+    HIPCHK(hipSetDevice(ctx->device));
+    const int K = ctx->K, DW = ctx->DW;
+    std::vector<ReqHdr> h(K);
+    std::vector<uint64_t> w(DW);
+    HIPCHK(hipMemcpy(h.data(), ctx->d_nc_hdr.p + (size_t)nc * K, K * sizeof(ReqHdr), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(w.data(), ctx->d_nc_words.p + (size_t)nc * DW, DW * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    std::vector<std::string> lines;
+    int off = 0;
+    for (int k = 0; k < K; k++) {
+        const KeyDict& kd = ctx->sol.keys[k];
+        const int nwk = std::max(1, ((int)kd.vals.size() + 63) / 64);
+        const int wo = off;
+        off += nwk;
+        if (!(h[k].flags & RF_DEF)) continue;
+        std::string l = kd.name + "\t" + ((h[k].flags & RF_CMP) ? "1" : "0") + "\t" +
+                        ((h[k].flags & RF_GT) ? std::to_string(h[k].gt) : "-") + "\t" +
+                        ((h[k].flags & RF_LT) ? std::to_string(h[k].lt) : "-") + "\t" +
+                        ((h[k].flags & RF_MIN) ? std::to_string(h[k].minv) : "-") + "\t";
+        std::vector<std::string> vs;
+        for (int v = 0; v < (int)kd.vals.size(); v++)
+            if ((w[wo + v / 64] >> (v % 64)) & 1ull) vs.push_back(kd.vals[v]);
+        std::sort(vs.begin(), vs.end());
+        for (size_t i = 0; i < vs.size(); i++) {
+            if (i) l += '\x1f';
+            l += vs[i];
+        }
+        lines.push_back(l);
+    }
+    std::sort(lines.begin(), lines.end());
+    std::string s;
+    for (auto& l : lines) s += l + "\n";
+    if (needed) *needed = (int64_t)s.size() + 1;
+    if ((int64_t)s.size() + 1 > cap || !buf) return KP_E_BUFFER;
+    memcpy(buf, s.c_str(), s.size() + 1);
+    return KP_OK;
+}

@@ -1,0 +1,145 @@
+// kp_layout.h — device-resident table layout shared by the host encoder (kp_host.cpp) and the gfx950
+// kernels (kp_kernels.hip).  Everything here is plain data: the host fills a KpDev of device pointers
+// and passes it by value to every kernel.
+//
+// Encoding:
+//   * label requirement sets (scheduling.Requirements) become DIGESTS: per solve key k a header
+//     {flags, minValues, gt, lt} plus a value bitset of nw[k] u64 words over that key's value dictionary
+//     (catalog values first, then values that only appear in pod/NodePool requirements);
+//   * the catalog's single-valued labels become u16 value ids per (key, type); multi-valued labels
+//     (zone, capacity-type, zone-id, reservation-*) become a u64 value mask per (key, type);
+//   * offerings become one u64 per type: bit (zone slot × capacity-type slot) set when an on-demand/spot
+//     offering in that pool is Available (offering.go:148);
+//   * instance-type option sets are bitsets of TW = ceil(T/64) words.
+#pragma once
+#include <stdint.h>
+
+#define KP_MAX_TYPES 1024            // TW <= 16
+#define KP_TW_MAX (KP_MAX_TYPES / 64)
+#define KP_MAX_NC 4096               // in-flight NodeClaims per solve (LDS order/key arrays)
+#define KP_MAX_KEYS 96               // label keys per solve
+#define KP_MAX_CLASS_KEYS 32         // label keys constrained by one pod class / template
+#define KP_MAX_SLOTS 64              // zone slots × capacity-type slots
+#define KP_MAX_R 16                  // resource axes
+#define KP_NWAVES 8                  // waves in the single-workgroup FFD kernel
+#define KP_LDS_AXES 6                // allocatable axes staged in LDS
+#define KP_MAX_SCR_WORDS 64          // value-bitset words of one class's keys (per-wave LDS scratch)
+#define KP_MAX_MIN_WORDS 64          // value bitset for a minValues distinct count (4096 values)
+
+// ReqHdr.flags
+#define RF_DEF 1u                    // key present in the Requirements map
+#define RF_CMP 2u                    // complement
+#define RF_GT 4u
+#define RF_LT 8u
+#define RF_MIN 16u
+
+// per solve key flags (KpDev.kflags)
+#define KF_WELL_KNOWN 1u             // AllowUndefinedWellKnownLabels
+#define KF_CAT_SINGLE 2u             // catalog label key, every type has <= 1 value
+#define KF_CAT_MULTI 4u              // catalog label key with a multi-valued type (zone, capacity-type, ...)
+
+// type value ids for single-valued keys
+#define VAL_DNE 0xFFFFu              // label DoesNotExist on the type
+#define VAL_ABSENT 0xFFFEu           // key absent from the type's Requirements map (never checked)
+
+struct ReqHdr {
+    uint32_t flags;
+    int32_t minv;
+    int64_t gt;
+    int64_t lt;
+};
+
+// Device pointers and sizes for one solve (catalog tables + solve tables + state + outputs).
+struct KpDev {
+    // ---------------- catalog (uploaded once per epoch) ----------------
+    int32_t T, TW, R, K;             // types, option words, resource axes, solve keys
+    int32_t n_slots;                 // zone × capacity-type slots
+    int32_t n_multi;                 // multi-valued catalog keys
+    const uint16_t* type_val;        // [K_cat][T] (indexed by kcat[k])
+    const uint64_t* multi_mask;      // [n_multi][T]
+    const uint64_t* dne_mask;        // [K_cat][TW] types whose label is DoesNotExist (or an empty In)
+    const int64_t* alloc;            // [R][T]
+    const int64_t* cap;              // [R][T]
+    const uint64_t* avail_zc;        // [T] available od/spot offerings by slot
+    const double* slot_price;        // [T][KP_MAX_SLOTS] price of the (type, slot) offering
+    const int32_t* slot_zone;        // [n_slots] zone value id
+    const int32_t* slot_ct;          // [n_slots] capacity-type value id
+    const int32_t* slot_zoneid;      // [n_slots] zone-id value id or -1 (offering has no zone-id)
+    const uint32_t* name_rank;       // [T] rank of the type name (OrderByPrice tie-break)
+    const uint64_t* nonneg;          // [TW] types whose allocatable is non-negative everywhere
+
+    // ---------------- solve keys ----------------
+    const uint32_t* kflags;          // [K]
+    const int32_t* kcat;             // [K] catalog key index or -1
+    const int32_t* kmulti;           // [K] multi index or -1
+    const int32_t* woff;             // [K] word offset in a digest
+    const int32_t* nw;               // [K] words
+    const int32_t* nval;             // [K] dictionary size
+    const int32_t* vbase;            // [K] offset into val_isint/val_int
+    const uint8_t* val_isint;        // strconv.Atoi succeeded
+    const int64_t* val_int;
+    int32_t DW;                      // digest words
+    int32_t key_zone, key_ct, key_zoneid, key_resvid, key_resvtype;  // offering-key roles (-1 absent)
+
+    // ---------------- classes (pod classes, then one pseudo-class per template) ----------------
+    int32_t C;                       // pod classes
+    int32_t NT;                      // templates (NodePools in weight order)
+    const int32_t* cls_koff;         // [C+NT+1] CSR into cls_keys
+    const int32_t* cls_keys;         // solve key ids constrained by the class
+    const int32_t* cls_wsoff;        // parallel to cls_keys: word offset of the key in the wave scratch
+    const ReqHdr* cls_hdr;           // [C+NT][K]
+    const uint64_t* cls_words;       // [C+NT][DW]
+    const uint32_t* cls_flags;       // [C+NT] bit0: defines an offering key, bit1: has minValues
+    uint64_t* V;                     // [C+NT][TW] per-class single-valued label compatibility (class_mask kernel)
+
+    // ---------------- templates ----------------
+    const uint64_t* tmpl_rows;       // [NT][TW] GetInstanceTypes(nodepool) rows
+    uint64_t* tmpl_opts;             // [NT][TW] NodeClaimTemplate.InstanceTypeOptions (template_init kernel)
+    int32_t* tmpl_ok;                // [NT]
+    const uint32_t* tol;             // [C] bit j: class tolerates template j's taints
+    const int64_t* daemon;           // [NT][R]
+    const uint8_t* limit_set;        // [NT][R]
+    int64_t* remaining;              // [NT][R] (mutated by the FFD kernel)
+    const int32_t* min_keys;         // [NT][KP_MAX_CLASS_KEYS] keys carrying minValues (-1 terminated)
+
+    // ---------------- pods ----------------
+    int32_t P;
+    const int32_t* pod_cls;          // [P]
+    const int32_t* pod_shape;        // [P] id of (class, requests)
+    const int64_t* pod_req;          // [P][R]
+    const int32_t* queue0;           // [P] queue order (NewQueue sort), device-sorted
+    int32_t active_axes[KP_MAX_R];   // axes any pod/daemon requests, LDS-staged first
+    int32_t n_active;
+
+    // ---------------- state ----------------
+    int32_t NCcap;
+    ReqHdr* nc_hdr;                  // [NCcap][K]
+    uint64_t* nc_words;              // [NCcap][DW]
+    uint64_t* nc_opts;               // [NCcap][TW]
+    int64_t* nc_req;                 // [NCcap][R]
+    int32_t* nc_tmpl;                // [NCcap]
+    const ReqHdr* empty_hdr;         // [K] all-undefined digest (template init)
+    const uint64_t* empty_words;     // [DW]
+    int32_t* qbuf;                   // [P] queue ring
+    int32_t* last_len;               // [P]
+
+    // ---------------- outputs ----------------
+    int32_t* pod_result;             // [P]
+    int32_t* pod_order;              // [P]
+    int32_t* nc_count;               // [1]
+    int32_t* nc_npods;               // [NCcap]
+    int32_t* nc_slice_pos;           // [NCcap]
+    int32_t* nc_nopts;               // [NCcap]
+    int32_t* nc_valid;               // [NCcap]
+    int32_t M;                       // max instance types (Truncate)
+    int32_t* nc_types;               // [NCcap][M]
+    int32_t* nc_ntypes;              // [NCcap]
+    int64_t* stats;                  // [16]
+    int32_t* err;                    // [1] device-side error code (capacity overflow etc.)
+};
+
+// stats slots
+enum {
+    ST_POPPED = 0, ST_NC_EVALS, ST_NC_SCANNED, ST_TMPL_EVALS, ST_EXIST_EVALS, ST_SORT_FAST, ST_SORT_FULL,
+    ST_MEMO_SKIPS, ST_COUNT = 16
+};

@@ -1,0 +1,128 @@
+"""Loader for libkpsim.so (the gfx950 library).  Fails loudly if it is missing: there is no CPU fallback."""
+import ctypes as C
+import os
+
+from . import abi
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "..", "lib", "libkpsim.so")
+
+EXPORTS = [
+    "kp_ctx_create", "kp_ctx_destroy", "kp_last_error", "kp_version", "kp_catalog_upload", "kp_catalog_patch_avail",
+    "kp_catalog_patch_price", "kp_solve", "kp_solve_prepare", "kp_solve_execute", "kp_solve_fetch",
+    "kp_result_nodeclaim_requirements", "kp_last_kernel_times",
+]
+
+_lib = None
+
+
+class KpError(RuntimeError):
+    def __init__(self, status, msg=""):
+        super().__init__("%s: %s" % (abi.STATUS_NAMES.get(status, status), msg))
+        self.status = status
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = os.path.normpath(LIB_PATH)
+    if not os.path.exists(path):
+        raise ImportError("libkpsim.so not built at %s (run __graft_entry__.build() or make -C karpenter-provider-aws_amd)"
+                          % path)
+    L = C.CDLL(path)
+    L.kp_ctx_create.argtypes = [C.POINTER(abi.kp_device_opts), C.POINTER(C.c_void_p)]
+    L.kp_ctx_destroy.argtypes = [C.c_void_p]
+    L.kp_last_error.argtypes = [C.c_void_p]
+    L.kp_last_error.restype = C.c_char_p
+    L.kp_version.restype = C.c_char_p
+    L.kp_catalog_upload.argtypes = [C.c_void_p, C.POINTER(abi.kp_catalog_view), C.c_uint64]
+    L.kp_catalog_patch_avail.argtypes = [C.c_void_p, C.POINTER(C.c_uint8), C.c_int32, C.c_uint64]
+    L.kp_catalog_patch_price.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_double), C.c_int32, C.c_uint64]
+    L.kp_solve.argtypes = [C.c_void_p, C.POINTER(abi.kp_solve_input), C.POINTER(abi.kp_solve_output)]
+    L.kp_solve_prepare.argtypes = [C.c_void_p, C.POINTER(abi.kp_solve_input)]
+    L.kp_solve_execute.argtypes = [C.c_void_p]
+    L.kp_solve_fetch.argtypes = [C.c_void_p, C.POINTER(abi.kp_solve_output)]
+    L.kp_result_nodeclaim_requirements.argtypes = [C.c_void_p, C.c_int32, C.c_char_p, C.c_int64, C.POINTER(C.c_int64)]
+    L.kp_last_kernel_times.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_int32]
+    for f in EXPORTS:
+        if f not in ("kp_last_error", "kp_version"):
+            getattr(L, f).restype = C.c_int32
+    _lib = L
+    return L
+
+
+class Context:
+    """One kp_ctx (device stream + buffers).  Not thread-safe; use one per thread."""
+
+    def __init__(self, device=0):
+        L = load()
+        self.L = L
+        h = C.c_void_p()
+        opts = abi.kp_device_opts(device=device)
+        st = L.kp_ctx_create(C.byref(opts), C.byref(h))
+        if st != 0:
+            raise KpError(st, "kp_ctx_create(device=%d) — a gfx950 device is required" % device)
+        self.h = h
+        self._catalog = None
+
+    def check(self, st, what):
+        if st != 0:
+            raise KpError(st, "%s: %s" % (what, self.L.kp_last_error(self.h).decode()))
+
+    def upload_catalog(self, catalog_view, epoch=1):
+        self.check(self.L.kp_catalog_upload(self.h, C.byref(catalog_view.view), epoch), "kp_catalog_upload")
+        self._catalog = catalog_view
+
+    def patch_avail(self, available, epoch):
+        import numpy as np
+        a = np.ascontiguousarray(available, np.uint8)
+        self.check(self.L.kp_catalog_patch_avail(self.h, a.ctypes.data_as(C.POINTER(C.c_uint8)), len(a), epoch),
+                   "kp_catalog_patch_avail")
+
+    def patch_price(self, idx, price, epoch):
+        import numpy as np
+        i = np.ascontiguousarray(idx, np.int32)
+        p = np.ascontiguousarray(price, np.float64)
+        self.check(self.L.kp_catalog_patch_price(self.h, i.ctypes.data_as(C.POINTER(C.c_int32)),
+                                                 p.ctypes.data_as(C.POINTER(C.c_double)), len(i), epoch),
+                   "kp_catalog_patch_price")
+
+    def prepare(self, input_view):
+        self.check(self.L.kp_solve_prepare(self.h, C.byref(input_view.view)), "kp_solve_prepare")
+
+    def execute(self):
+        self.check(self.L.kp_solve_execute(self.h), "kp_solve_execute")
+
+    def fetch(self, out_buffers):
+        self.check(self.L.kp_solve_fetch(self.h, C.byref(out_buffers.view)), "kp_solve_fetch")
+
+    def solve(self, input_view, out_buffers):
+        self.check(self.L.kp_solve(self.h, C.byref(input_view.view), C.byref(out_buffers.view)), "kp_solve")
+
+    def nodeclaim_requirements(self, nc):
+        need = C.c_int64(0)
+        buf = C.create_string_buffer(1 << 16)
+        st = self.L.kp_result_nodeclaim_requirements(self.h, nc, buf, len(buf), C.byref(need))
+        if st == abi.KP_E_BUFFER:
+            buf = C.create_string_buffer(need.value)
+            st = self.L.kp_result_nodeclaim_requirements(self.h, nc, buf, len(buf), C.byref(need))
+        self.check(st, "kp_result_nodeclaim_requirements")
+        return buf.value.decode()
+
+    def kernel_times_ms(self):
+        """[queue sort, class masks, template filter, FFD, finalize] of the last execute (HIP events)."""
+        a = (C.c_double * 5)()
+        self.check(self.L.kp_last_kernel_times(self.h, a, 5), "kp_last_kernel_times")
+        return list(a)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.kp_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,101 @@
+"""Seeded random scheduling problems that exercise the requirement algebra end to end.
+
+Operators In / NotIn / Exists / DoesNotExist / Gt / Lt over catalog labels (single- and multi-valued), values
+absent from the catalog, non-well-known custom keys, taints/tolerations, NodePool weights, limits, daemon
+overhead and minValues.  Used by the GPU parity tests (device vs. CPU oracle on identical inputs).
+"""
+import numpy as np
+
+from kpsim import model
+from kpsim.model import (ARCH, CAPACITY_TYPE, INSTANCE_TYPE, NodePool, PodClass, Problem, Requirement, Taint,
+                         Toleration, ZONE)
+from kpsim.synth import _pods_from_milli
+
+AWS = "karpenter.k8s.aws/"
+ZONES = ["test-zone-1a", "test-zone-1b", "test-zone-1c"]
+
+
+def _rand_req(rng, catalog):
+    it = catalog[int(rng.integers(0, len(catalog)))]
+    kind = int(rng.integers(0, 14))
+    if kind == 0:
+        return Requirement(ARCH, str(rng.choice(["In", "NotIn"])), [str(rng.choice(["amd64", "arm64"]))])
+    if kind == 1:
+        return Requirement(ZONE, str(rng.choice(["In", "NotIn"])),
+                           sorted(set(rng.choice(ZONES + ["us-west-2z"], size=int(rng.integers(1, 3))).tolist())))
+    if kind == 2:
+        return Requirement(CAPACITY_TYPE, "In", [str(rng.choice(["spot", "on-demand"]))])
+    if kind == 3:
+        return Requirement(AWS + "instance-category", str(rng.choice(["In", "NotIn"])),
+                           sorted(set(rng.choice(["c", "m", "r", "t", "g", "x"], size=int(rng.integers(1, 4))).tolist())))
+    if kind == 4:
+        return Requirement(AWS + "instance-generation", str(rng.choice(["Gt", "Lt"])), [str(int(rng.integers(2, 8)))])
+    if kind == 5:
+        return Requirement(AWS + "instance-cpu", str(rng.choice(["Gt", "Lt"])), [str(int(rng.choice([2, 4, 8, 16, 48])))])
+    if kind == 6:
+        return Requirement(AWS + "instance-gpu-name", str(rng.choice(["Exists", "DoesNotExist"])))
+    if kind == 7:
+        return Requirement(AWS + "instance-local-nvme", str(rng.choice(["Exists", "DoesNotExist", "NotIn"])),
+                           ["1900"] if rng.random() < 0.5 else [])
+    if kind == 8:
+        return Requirement(INSTANCE_TYPE, "In", sorted(set([it.name] + [catalog[int(i)].name for i in
+                                                                         rng.integers(0, len(catalog), size=20)])))
+    if kind == 9:
+        return Requirement("example.com/team", str(rng.choice(["In", "NotIn", "Exists", "DoesNotExist"])), ["a"])
+    if kind == 10:
+        return Requirement(AWS + "instance-family", "NotIn", [str(v) for v in (it.labels.get(AWS + "instance-family") or ["m5"])])
+    if kind == 11:
+        return Requirement(AWS + "instance-memory", str(rng.choice(["Gt", "Lt"])), [str(int(rng.choice([4096, 16384, 65536])))])
+    if kind == 12:
+        return Requirement(AWS + "instance-hypervisor", "In", [str(rng.choice(["nitro", "xen", ""]))])
+    return Requirement(AWS + "instance-size", str(rng.choice(["In", "NotIn"])),
+                       sorted(set(rng.choice(["large", "xlarge", "2xlarge", "metal", "medium"], size=2).tolist())))
+
+
+def fuzz_problem(catalog, seed, n_pods=300, n_classes=12, n_pools=3, with_min=True, with_limits=True):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    T = len(catalog)
+    pools = []
+    for j in range(n_pools):
+        reqs = [Requirement(CAPACITY_TYPE, "In", sorted(set(rng.choice(["spot", "on-demand"], size=2).tolist())))]
+        for _ in range(int(rng.integers(0, 3))):
+            reqs.append(_rand_req(rng, catalog))
+        if with_min and rng.random() < 0.3:
+            reqs.append(Requirement(AWS + "instance-family", "Exists", [], int(rng.integers(2, 6))))
+        labels = {"example.com/team": "a"} if rng.random() < 0.4 else {}
+        taints = [Taint("example.com/gpu", "true", "NoSchedule")] if rng.random() < 0.3 else []
+        daemon = np.zeros(model.R, np.int64)
+        if rng.random() < 0.5:
+            daemon[model.RIDX["cpu"]] = int(rng.choice([100, 250]))
+            daemon[model.RIDX["memory"]] = int(rng.choice([128, 512])) * 2 ** 20 * 1000
+            daemon[model.RIDX["pods"]] = 2000
+        limits = None
+        if with_limits and rng.random() < 0.4:
+            limits = {"cpu": int(rng.choice([16, 64, 256])) * 1000}
+        rows = None
+        if rng.random() < 0.3:
+            rows = sorted(rng.choice(T, size=max(1, T // 2), replace=False).tolist())
+        pools.append(NodePool(name="pool-%d" % j, weight=int(rng.choice([0, 10, 10, 50])), requirements=reqs,
+                              labels=labels, taints=taints, daemon_overhead=daemon, limits_remaining=limits,
+                              instance_types=rows))
+    classes, creqs = [], []
+    for c in range(n_classes):
+        reqs = [_rand_req(rng, catalog) for _ in range(int(rng.integers(0, 3)))]
+        tols = [Toleration("example.com/gpu", "Exists", "", "NoSchedule")] if rng.random() < 0.3 else []
+        classes.append(PodClass(reqs, tols))
+        cpu = int(rng.choice([100, 500, 1000, 2000, 4000]))
+        r = {"cpu": cpu, "memory": cpu * int(rng.choice([1, 2, 4])) * (2 ** 30) // 1000 * 1000}
+        if rng.random() < 0.1:
+            r["nvidia.com/gpu"] = 1000
+        creqs.append(r)
+    specs = []
+    for _ in range(n_pods):
+        c = int(rng.integers(0, n_classes))
+        specs.append((c, creqs[c]))
+    # runs of identical pods (deployments) and some shuffling
+    if rng.random() < 0.5:
+        specs.sort(key=lambda s: s[0])
+    pods = _pods_from_milli(specs)
+    if rng.random() < 0.5:  # equal creation times: UID order decides ties
+        pods.creation_ns[:] = pods.creation_ns[0]
+    return Problem(catalog, pools, classes, pods)

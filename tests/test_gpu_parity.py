@@ -1,0 +1,125 @@
+"""GPU: the gfx950 path (libkpsim.so) against the CPU oracle on identical inputs — bit-exact.
+
+Compared per solve: pod → NodeClaim assignment, placement order, NodeClaim NodePool / pod count / slice
+position / option count, the truncated price-ordered instance-type list, and the NodeClaim requirements.
+"""
+import numpy as np
+import pytest
+
+import fuzzgen
+import parity
+from kpsim import catalog as cat
+from kpsim import model, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from kpsim import native
+    c = native.Context(0)
+    yield c
+    c.close()
+
+
+def test_native_library_is_loaded(ctx):
+    from kpsim import native
+    assert native.load() is not None and ctx.h
+
+
+@pytest.mark.parametrize("i", range(7))
+def test_kat_gpu_packing_device(ctx, fx, fake, i):
+    """suite_test.go:753-972 on the device: expected type and node count, identical to the oracle."""
+    case = fx["kats"]["gpu_packing"]["cases"][i]
+    np_ = synth.default_nodepool()
+    if "nodepool_instance_type" in case:
+        np_.requirements = [model.Requirement(model.INSTANCE_TYPE, "In", [case["nodepool_instance_type"]])]
+    pods = synth.pods_from_specs([(0, {case["resource"]: str(q)}) for q in case["requests"]])
+    prob = model.Problem(fake, [np_], [model.PodClass()], pods)
+    dev = parity.run_device(ctx, prob)
+    assert dev[0].n_nodeclaims == case["nodes"]
+    assert all(fake[ts[0]].name == case["type"] for ts in dev[0].nodeclaim_types)
+    parity.assert_same(dev, parity.run_oracle(prob))
+
+
+def test_kat_ephemeral_and_pod_eni_device(ctx, fx):
+    pods = synth.pods_from_specs([(0, {"ephemeral-storage": "5000Gi"})])
+    for raid0 in (False, True):
+        fc = cat.fake_catalog(opts=cat.TypeOptions(raid0=raid0), fx=fx)
+        prob = model.Problem(fc, [synth.default_nodepool()], [model.PodClass()], pods)
+        dev = parity.run_device(ctx, prob)
+        parity.assert_same(dev, parity.run_oracle(prob))
+        assert (dev[0].pod_result >= 0).all() == raid0
+    fc = cat.fake_catalog(fx=fx)
+    prob = model.Problem(fc, [synth.default_nodepool()],
+                         [model.PodClass([model.Requirement(model.INSTANCE_TYPE, "In", ["t3.large"])])],
+                         synth.pods_from_specs([(0, {"vpc.amazonaws.com/pod-eni": "1"})]))
+    dev = parity.run_device(ctx, prob)
+    assert (dev[0].pod_result == -1).all()
+
+
+def test_config1_plumbing(ctx, golden):
+    """BASELINE configs[0]: 2,000 homogeneous pods, one on-demand NodePool."""
+    prob = synth.config1(catalog=golden)
+    parity.assert_same(parity.run_device(ctx, prob), parity.run_oracle(prob))
+
+
+@pytest.mark.parametrize("n", [500, 3000])
+def test_config2_sample(ctx, golden, n):
+    """BASELINE configs[1] workload shape on a pod sample the oracle finishes in seconds."""
+    prob = synth.subsample(synth.config2(catalog=golden), n)
+    parity.assert_same(parity.run_device(ctx, prob), parity.run_oracle(prob))
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_fuzz_requirements(ctx, golden, seed):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=160, replace=False))]
+    prob = fuzzgen.fuzz_problem(sub, seed, n_pods=int(rng.integers(50, 400)))
+    parity.assert_same(parity.run_device(ctx, prob), parity.run_oracle(prob))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_fuzz_fake_catalog(ctx, fake, seed):
+    prob = fuzzgen.fuzz_problem(fake, 1000 + seed, n_pods=120)
+    parity.assert_same(parity.run_device(ctx, prob), parity.run_oracle(prob))
+
+
+def test_sort_emulation_many_equal_counts(ctx, golden):
+    """Hundreds of identical small pods across many narrow NodeClaims: exercises sort.Slice ties (13 ≤ n < 50
+    full emulation and n ≥ 50 fast path), compared through slice positions and assignments."""
+    sub = golden[:200]
+    classes = [model.PodClass([model.Requirement(model.INSTANCE_TYPE, "In", [it.name])]) for it in sub[:120]]
+    specs = []
+    for rep in range(6):
+        for c in range(len(classes)):
+            specs.append((c, {"cpu": 100, "memory": 100 * 2 ** 20 * 1000}))
+    pods = synth._pods_from_milli(specs)
+    prob = model.Problem(sub, [synth.default_nodepool(capacity_types=("spot", "on-demand"))], classes, pods)
+    dev = parity.run_device(ctx, prob)
+    parity.assert_same(dev, parity.run_oracle(prob))
+    assert dev[0].stats["sorts_full"] > 0 and dev[0].stats["sorts_fast"] >= 0
+
+
+def test_config2_full_properties(ctx, golden):
+    """Full 50k-pod config 2: size-independent properties (the oracle is too slow at this size)."""
+    prob = synth.config2(catalog=golden)
+    r, _ = parity.run_device(ctx, prob)
+    P = prob.pods.n
+    assert r.pod_result.shape == (P,)
+    sched = r.pod_result >= 0
+    assert sched.sum() > 0.9 * P
+    # every placement has a unique order number
+    orders = r.pod_order[sched]
+    assert len(np.unique(orders)) == len(orders)
+    # per NodeClaim: total requests + daemon fit every truncated type; pod counts agree
+    counts = np.bincount(r.pod_result[sched], minlength=r.n_nodeclaims)
+    np.testing.assert_array_equal(counts, r.nodeclaim_n_pods)
+    tot = np.zeros((r.n_nodeclaims, model.R), np.int64)
+    np.add.at(tot, r.pod_result[sched], prob.pods.requests[sched])
+    for i, ts in enumerate(r.nodeclaim_types):
+        assert 0 < len(ts) <= 60
+        pool = prob.nodepools[r.nodeclaim_nodepool[i]]
+        need = tot[i] + (pool.daemon_overhead if pool.daemon_overhead is not None else 0)
+        for t in ts:
+            assert (need <= prob.catalog[t].allocatable).all()
