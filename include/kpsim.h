@@ -247,7 +247,9 @@ kp_status kp_solve_execute(kp_ctx* ctx);
 kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out);
 
 /* Device time (ms, HIP events on the ctx stream) of the last kp_solve_execute, per phase:
- * [0] queue sort, [1] class masks, [2] template filter, [3] FFD solve kernel, [4] finalize/Truncate. */
+ * [0] queue sort, [1] class masks, [2] template filter, [3] FFD solve kernel, [4] finalize/Truncate;
+ * then (after kp_solve_fetch) FFD-kernel shader-clock counters [5..10]: pop, sort.Slice, scan+NodeClaim.Add,
+ * new-NodeClaim templates, commit, full-pdqsort share of sort.Slice. */
 kp_status kp_last_kernel_times(kp_ctx* ctx, double* ms, int32_t n);
 
 /*

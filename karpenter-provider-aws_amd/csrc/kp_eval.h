@@ -1,0 +1,342 @@
+// kp_eval.h — NodeClaim.Add evaluated by ONE wave (64 lanes), LDS-resident operands.
+//
+// Reference semantics ([core] sigs.k8s.io/karpenter pkg/controllers/provisioning/scheduling/nodeclaim.go):
+//   NodeClaim.Add(pod):
+//     Taints(template).ToleratesPod(pod)
+//     nodeClaimRequirements.Compatible(podRequirements, AllowUndefinedWellKnownLabels); Add(podRequirements)
+//     requests = Merge(nodeClaim.requests, pod.requests)
+//     remaining = filterInstanceTypesByRequirements(options, reqs, requests):
+//         it.Requirements.Intersects(reqs) ∧ resources.Fits(requests, it.Allocatable()) ∧
+//         ∃ offering: Available ∧ reqs.IsCompatible(offering.Requirements, AllowUndefinedWellKnownLabels)
+//         then SatisfiesMinValues (MIN_VALUES_POLICY=Strict)
+//
+// Encoding that makes this a bitset sweep:
+//   * options ⊆ compatible(nodeClaim requirements) is an invariant, and for a single-valued label
+//     Has(merged, v) = Has(nc, v) ∧ Has(class, v); so label compatibility of a type reduces to the class's
+//     precomputed V bitset, except for types whose label is DoesNotExist, which survive only when the merged
+//     operator is NotIn/DoesNotExist (dne masks), and multi-valued labels (zone, capacity-type, ...), tested per
+//     type as (type value mask ∧ merged admissible mask) ≠ 0;
+//   * offerings reduce to one u64 per type over (zone × capacity-type) slots; the merged requirements give the
+//     admissible slot mask;
+//   * Fits compares the request totals with LDS-staged allocatable columns of the active resource axes.
+#pragma once
+#include "kp_device.h"
+
+// Per-wave LDS scratch: merged requirements of the class's keys, resulting options, minValues bitset.
+struct WaveScratch {
+    ReqHdr hdr[KP_MAX_CLASS_KEYS];
+    uint64_t words[KP_MAX_SCR_WORDS];
+    uint64_t opts[KP_TW_MAX];
+    uint64_t minbits[KP_MAX_MIN_WORDS];
+};
+
+// Class-side operands of the evaluation, cached in LDS while consecutive pods share a class.
+struct ClassCache {
+    int cls;
+    int nck;
+    uint32_t tol;
+    uint32_t flags;
+    int role[5];  // class-key index of zone, capacity-type, zone-id, reservation-id, reservation-type (or -1)
+    int key[KP_MAX_CLASS_KEYS];
+    int wsoff[KP_MAX_CLASS_KEYS];
+    int nw[KP_MAX_CLASS_KEYS];
+    int woff[KP_MAX_CLASS_KEYS];
+    uint32_t kflags[KP_MAX_CLASS_KEYS];
+    int kcat[KP_MAX_CLASS_KEYS];
+    int kmulti[KP_MAX_CLASS_KEYS];
+    int nval[KP_MAX_CLASS_KEYS];
+    int nbB[KP_MAX_CLASS_KEYS];
+    ReqHdr hdr[KP_MAX_CLASS_KEYS];
+    uint64_t words[KP_MAX_SCR_WORDS];
+    uint64_t V[KP_TW_MAX];
+    uint64_t dne[KP_MAX_CLASS_KEYS][KP_TW_MAX];
+};
+
+// Offering-role keys (zone, capacity-type, zone-id, reservation-id, reservation-type) of the solve.
+struct Roles {
+    int key[5];
+    int woff[5];
+    int nw[5];
+};
+
+// Tables shared by every evaluation of a kernel (LDS in ffd_kernel).
+struct EvalEnv {
+    const int64_t* alloc;      // [KP_LDS_AXES][KP_MAX_TYPES] staged allocatable of the first active axes
+    const uint64_t* avail;     // [T] available od/spot slot mask per type
+    const uint16_t* multi16;   // [n_multi][KP_MAX_TYPES] multi-valued label masks, or null → global multi_mask
+    const int* slot_zone;
+    const int* slot_ct;
+    const int* slot_zoneid;
+    const Roles* roles;
+};
+
+// Cooperative fill by all threads of the block; contains two __syncthreads().
+__device__ inline void fill_class_cache(const KpDev& d, int c, ClassCache& CC, int tid, int nthr) {
+    const int k0 = d.cls_koff[c], nck = d.cls_koff[c + 1] - k0;
+    for (int i = tid; i < nck; i += nthr) {
+        const int k = d.cls_keys[k0 + i];
+        CC.key[i] = k;
+        CC.wsoff[i] = d.cls_wsoff[k0 + i];
+        CC.nw[i] = d.nw[k];
+        CC.woff[i] = d.woff[k];
+        CC.kflags[i] = d.kflags[k];
+        CC.kcat[i] = d.kcat[k];
+        CC.kmulti[i] = d.kmulti[k];
+        CC.nval[i] = d.nval[k];
+        CC.hdr[i] = d.cls_hdr[(size_t)c * d.K + k];
+        int nb = 0;
+        for (int w = 0; w < d.nw[k]; w++) {
+            const uint64_t x = d.cls_words[(size_t)c * d.DW + d.woff[k] + w];
+            CC.words[d.cls_wsoff[k0 + i] + w] = x;
+            nb += __popcll(x);
+        }
+        CC.nbB[i] = nb;
+        const int kc = d.kcat[k];
+        for (int w = 0; w < d.TW; w++) CC.dne[i][w] = kc >= 0 ? d.dne_mask[(size_t)kc * d.TW + w] : 0ull;
+    }
+    for (int w = tid; w < d.TW; w += nthr) CC.V[w] = d.V[(size_t)c * d.TW + w];
+    if (tid == 0) {
+        CC.cls = c;
+        CC.nck = nck;
+        CC.tol = c < d.C ? d.tol[c] : 0xFFFFFFFFu;
+        CC.flags = d.cls_flags[c];
+    }
+    __syncthreads();
+    if (tid < 5) {
+        const int rk = tid == 0 ? d.key_zone : tid == 1 ? d.key_ct : tid == 2 ? d.key_zoneid : tid == 3 ? d.key_resvid : d.key_resvtype;
+        int idx = -1;
+        for (int i = 0; i < nck; i++)
+            if (CC.key[i] == rk && rk >= 0) idx = i;
+        CC.role[tid] = idx;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
+    for (int o = 32; o >= 1; o >>= 1) x |= __shfl_xor(x, o);
+    return x;
+}
+__device__ __forceinline__ int64_t wave_max64(int64_t x) {
+    for (int o = 32; o >= 1; o >>= 1) {
+        const int64_t y = __shfl_xor(x, o);
+        x = y > x ? y : x;
+    }
+    return x;
+}
+
+// Has(merged, v) for an offering-role key r: merged = scratch (class constrains the key) or the base digest.
+__device__ __forceinline__ bool role_adm(const KpDev& d, const EvalEnv& E, const ClassCache& CC, const WaveScratch& ws,
+                                         const ReqHdr* Ahdr, const uint64_t* Aw, int r, int v) {
+    const int k = E.roles->key[r];
+    if (k < 0) return true;
+    const int i = CC.role[r];
+    if (i >= 0) return req_has(d, k, v, ws.hdr[i], ws.words + CC.wsoff[i]);
+    const ReqHdr h = Ahdr[k];
+    if (!(h.flags & RF_DEF)) return true;  // undefined well-known offering key → AllowUndefined
+    return req_has(d, k, v, h, Aw + E.roles->woff[r]);
+}
+// Offering carries the key as DoesNotExist: passes iff the merged operator is NotIn / DoesNotExist.
+__device__ __forceinline__ bool role_dneok(const KpDev& d, const EvalEnv& E, const ClassCache& CC,
+                                           const WaveScratch& ws, const ReqHdr* Ahdr, const uint64_t* Aw, int r) {
+    const int k = E.roles->key[r];
+    if (k < 0) return true;
+    const int i = CC.role[r];
+    ReqHdr h;
+    const uint64_t* w;
+    int n = E.roles->nw[r];
+    if (i >= 0) {
+        h = ws.hdr[i];
+        w = ws.words + CC.wsoff[i];
+    } else {
+        h = Ahdr[k];
+        if (!(h.flags & RF_DEF)) return true;
+        w = Aw + E.roles->woff[r];
+    }
+    return op_notin_or_dne(req_op(h.flags, popc_words(w, n)));
+}
+
+struct EvalIn {
+    const ReqHdr* Ahdr;       // base requirements digest (NodeClaim, template or empty)
+    const uint64_t* Aw;
+    uint64_t opts;            // lane l < TW: option word l
+    const int64_t* base_req;  // [R] (global) or null
+    const int64_t* pod_req;   // [R] (LDS or global) or null
+    int tmpl;                 // template of the NodeClaim (taints bit, minValues keys)
+    bool compat;              // taints + Requirements.Compatible
+    bool force_off;           // always apply the offering test (template filter)
+};
+
+// Wave-uniform result: does NodeClaim.Add(pod) succeed?  On success ws.opts / ws.hdr / ws.words hold the new state.
+__device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, const ClassCache& CC, const EvalIn& a,
+                                          WaveScratch& ws, int lane) {
+    const int TW = d.TW, T = d.T;
+    if (a.compat && !((CC.tol >> a.tmpl) & 1u)) return false;
+    const int nck = CC.nck;
+
+    // ---- requirements: Compatible + Add (lane = class key) ----
+    bool fail = false, kill = false;
+    uint64_t adm = ~0ull;
+    int kmul = -1;
+    if (lane < nck) {
+        const int k = CC.key[lane];
+        const int n = CC.nw[lane];
+        const ReqHdr A = a.Ahdr[k];
+        const uint64_t* aw = a.Aw + CC.woff[lane];
+        const ReqHdr B = CC.hdr[lane];
+        const uint64_t* bw = CC.words + CC.wsoff[lane];
+        uint64_t* ow = ws.words + CC.wsoff[lane];
+        ReqHdr O;
+        int cnt;
+        const int nb = CC.nbB[lane];
+        if (!(A.flags & RF_DEF)) {
+            if (a.compat && !op_notin_or_dne(req_op(B.flags, nb)) && !(CC.kflags[lane] & KF_WELL_KNOWN)) fail = true;
+            O = B;
+            for (int i = 0; i < n; i++) ow[i] = bw[i];
+            cnt = nb;
+        } else {
+            cnt = req_intersect(d, k, A, aw, B, bw, O, ow);
+            if (a.compat && !(O.flags & RF_CMP) && cnt == 0) {
+                const int na = popc_words(aw, n);
+                if (!(op_notin_or_dne(req_op(B.flags, nb)) && op_notin_or_dne(req_op(A.flags, na)))) fail = true;
+            }
+        }
+        ws.hdr[lane] = O;
+        const uint32_t kf = CC.kflags[lane];
+        if (kf & (KF_CAT_SINGLE | KF_CAT_MULTI)) kill = !op_notin_or_dne(req_op(O.flags, cnt));
+        if (kf & KF_CAT_MULTI) {
+            kmul = CC.kmulti[lane];
+            adm = 0;
+            const int nv = CC.nval[lane] < 64 ? CC.nval[lane] : 64;
+            for (int v = 0; v < nv; v++)
+                if (req_has(d, k, v, O, ow)) adm |= 1ull << v;
+        }
+    }
+    if (ballot(fail)) return false;
+
+    // ---- options ∧ V[class] ∧ ¬DoesNotExist-types of keys whose merged operator is In/Exists ----
+    uint64_t myopt = 0;
+    if (lane < TW) myopt = a.opts & CC.V[lane];
+    uint64_t km = ballot(kill);
+    while (km) {
+        const int i = __ffsll((unsigned long long)km) - 1;
+        km &= km - 1;
+        if (lane < TW) myopt &= ~CC.dne[i][lane];
+    }
+    const uint64_t mm = ballot(kmul >= 0);
+
+    // ---- offerings over zone × capacity-type slots ----
+    const bool need_off = a.force_off || (CC.flags & 1u);
+    uint64_t mzc = ~0ull;
+    if (need_off) {
+        bool ok = false;
+        if (lane < d.n_slots) {
+            const int zid = E.slot_zoneid[lane];
+            ok = role_adm(d, E, CC, ws, a.Ahdr, a.Aw, 0, E.slot_zone[lane]) &&
+                 role_adm(d, E, CC, ws, a.Ahdr, a.Aw, 1, E.slot_ct[lane]) &&
+                 (zid < 0 || role_adm(d, E, CC, ws, a.Ahdr, a.Aw, 2, zid)) &&
+                 role_dneok(d, E, CC, ws, a.Ahdr, a.Aw, 3) && role_dneok(d, E, CC, ws, a.Ahdr, a.Aw, 4);
+        }
+        mzc = ballot(ok);
+    }
+
+    // ---- request totals over the active axes (the first KP_LDS_AXES live in registers) ----
+    int64_t tot[KP_LDS_AXES];
+#pragma unroll
+    for (int ai = 0; ai < KP_LDS_AXES; ai++) {
+        tot[ai] = 0;
+        if (ai < d.n_active) {
+            const int r = d.active_axes[ai];
+            tot[ai] = (a.base_req ? a.base_req[r] : 0) + (a.pod_req ? a.pod_req[r] : 0);
+        }
+    }
+    const int n_extra = d.n_active > KP_LDS_AXES ? d.n_active - KP_LDS_AXES : 0;
+
+    // ---- per type: Fits ∧ multi-valued labels ∧ offerings (64 types per ballot) ----
+    uint64_t anyw = 0, newword = 0;
+    for (int w = 0; w < TW; w++) {
+        const uint64_t cw = rl64(myopt, w);
+        if (cw == 0) continue;
+        const int t = w * 64 + lane;
+        bool keep = (cw >> lane) & 1ull;
+#pragma unroll
+        for (int ai = 0; ai < KP_LDS_AXES; ai++) {
+            if (tot[ai] > 0) keep = keep && tot[ai] <= E.alloc[ai * KP_MAX_TYPES + t];
+        }
+        for (int x = 0; x < n_extra; x++) {
+            const int r = d.active_axes[KP_LDS_AXES + x];
+            const int64_t tr = (a.base_req ? a.base_req[r] : 0) + (a.pod_req ? a.pod_req[r] : 0);
+            if (tr > 0) keep = keep && tr <= d.alloc[(size_t)r * T + (t < T ? t : 0)];
+        }
+        uint64_t mmm = mm;
+        while (mmm) {
+            const int i = __ffsll((unsigned long long)mmm) - 1;
+            mmm &= mmm - 1;
+            const int m = rl32(kmul, i);
+            const uint64_t am = rl64(adm, i);
+            const uint64_t tm = E.multi16 ? (uint64_t)E.multi16[m * KP_MAX_TYPES + t]
+                                          : d.multi_mask[(size_t)m * T + (t < T ? t : 0)];
+            keep = keep && (tm == 0 || (tm & am) != 0);
+        }
+        if (need_off) keep = keep && (E.avail[t] & mzc) != 0;
+        const uint64_t nb = ballot(keep);
+        if (lane == w) newword = nb;
+        anyw |= nb;
+    }
+    if (anyw == 0) return false;
+
+    // ---- minValues (Strict): distinct values per key over the remaining options ----
+    if (a.tmpl >= 0) {
+        const int* mk = d.min_keys + (size_t)a.tmpl * KP_MAX_CLASS_KEYS;
+        for (int q = 0; q < KP_MAX_CLASS_KEYS; q++) {
+            const int k = mk[q];
+            if (k < 0) break;
+            int ci = -1;
+            for (int i = 0; i < nck; i++)
+                if (CC.key[i] == k) ci = i;
+            const ReqHdr h = ci >= 0 ? ws.hdr[ci] : a.Ahdr[k];
+            if (!(h.flags & RF_MIN)) continue;
+            int count = 0;
+            const int kc = d.kcat[k];
+            if (kc >= 0 && (d.kflags[k] & KF_CAT_MULTI)) {
+                uint64_t acc = 0;
+                for (int w = 0; w < TW; w++) {
+                    const uint64_t nwd = rl64(newword, w);
+                    const int t = w * 64 + lane;
+                    if ((nwd >> lane) & 1ull) acc |= d.multi_mask[(size_t)d.kmulti[k] * T + t];
+                }
+                count = __popcll(wave_or64(acc));
+            } else if (kc >= 0) {
+                const int nwk = (d.nval[k] + 63) / 64;
+                for (int i = lane; i < KP_MAX_MIN_WORDS; i += 64) ws.minbits[i] = 0;
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                for (int w = 0; w < TW; w++) {
+                    const uint64_t nwd = rl64(newword, w);
+                    const int t = w * 64 + lane;
+                    if ((nwd >> lane) & 1ull) {
+                        const uint16_t v = d.type_val[(size_t)kc * T + t];
+                        if (v < VAL_ABSENT && v < KP_MAX_MIN_WORDS * 64)
+                            atomicOr((unsigned long long*)&ws.minbits[v >> 6], 1ull << (v & 63));
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                int c = 0;
+                for (int i = lane; i < nwk && i < KP_MAX_MIN_WORDS; i += 64) c += __popcll(ws.minbits[i]);
+                for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
+                count = c;
+            }
+            if (count < h.minv) return false;
+        }
+    }
+    if (lane < TW) ws.opts[lane] = newword;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    return true;
+}
+
+// Write the merged class keys of a successful evaluation into NodeClaim slot n.
+__device__ __forceinline__ void commit_reqs(const KpDev& d, const ClassCache& CC, const WaveScratch& ws, int n, int lane) {
+    if (lane < CC.nck) {
+        const int k = CC.key[lane];
+        d.nc_hdr[(size_t)n * d.K + k] = ws.hdr[lane];
+        for (int i = 0; i < CC.nw[lane]; i++) d.nc_words[(size_t)n * d.DW + CC.woff[lane] + i] = ws.words[CC.wsoff[lane] + i];
+    }
+}

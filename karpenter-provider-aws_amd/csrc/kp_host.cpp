@@ -190,7 +190,8 @@ struct kp_ctx {
     std::vector<int32_t> slot_zone, slot_ct, slot_zoneid;
     int key_zone = -1, key_ct = -1, key_zoneid = -1, key_resvid = -1, key_resvtype = -1;
     // catalog device tables
-    DBuf<uint16_t> d_type_val;
+    DBuf<uint16_t> d_type_val, d_multi16;
+    bool multi16_ok = false;
     DBuf<uint64_t> d_multi_mask, d_dne_mask, d_avail_zc, d_nonneg;
     DBuf<int64_t> d_alloc, d_cap;
     DBuf<double> d_slot_price;
@@ -216,6 +217,7 @@ struct kp_ctx {
     double ns_prep = 0, ns_exec = 0, ns_fin = 0;
     hipEvent_t ev[6] = {};
     double kernel_ms[5] = {};
+    int64_t cycles[6] = {};  // FFD phases (s_memtime): pop, sort, scan+eval, templates, commit, full pdqsort
     // last results (host)
     int last_N = 0, M = 0;
     std::vector<int32_t> h_nc_tmpl;
@@ -262,6 +264,7 @@ extern "C" kp_status kp_ctx_destroy(kp_ctx* ctx) {
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
     // buffers are released with the process / device reset; explicit frees for long-lived processes
     ctx->d_type_val.release();
+    ctx->d_multi16.release();
     ctx->d_multi_mask.release();
     ctx->d_dne_mask.release();
     ctx->d_avail_zc.release();
@@ -496,6 +499,14 @@ extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, ui
     hipStream_t s = c->stream;
     HIPCHK(c->d_type_val.upload(tval, s));
     HIPCHK(c->d_multi_mask.upload(mmask, s));
+    c->multi16_ok = c->n_multi <= 5;
+    for (int k = 0; k < Kc; k++)
+        if ((c->cat_kflags[k] & KF_CAT_MULTI) && c->cat.keys[k].vals.size() > 16) c->multi16_ok = false;
+    if (c->multi16_ok) {
+        std::vector<uint16_t> m16(mmask.size());
+        for (size_t i = 0; i < mmask.size(); i++) m16[i] = (uint16_t)mmask[i];
+        HIPCHK(c->d_multi16.upload(m16, s));
+    }
     HIPCHK(c->d_dne_mask.upload(dne, s));
     HIPCHK(c->d_alloc.upload(c->alloc_rt, s));
     HIPCHK(c->d_cap.upload(c->cap_rt, s));
@@ -917,6 +928,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.n_multi = c->n_multi;
     d.type_val = c->d_type_val.p;
     d.multi_mask = c->d_multi_mask.p;
+    d.multi16 = c->multi16_ok ? c->d_multi16.p : nullptr;
     d.dne_mask = c->d_dne_mask.p;
     d.alloc = c->d_alloc.p;
     d.cap = c->d_cap.p;
@@ -1093,6 +1105,7 @@ extern "C" kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out) {
     so.existing_evals = st[ST_EXIST_EVALS];
     so.sorts_fast = st[ST_SORT_FAST];
     so.sorts_full = st[ST_SORT_FULL];
+    for (int i = 0; i < 6; i++) c->cycles[i] = st[ST_CYC_POP + i];
     so.ns_host_prep = c->ns_prep;
     so.ns_device_solve = c->ns_exec;
     if (N > out->cap_nodeclaims || n_ids > out->cap_type_ids) return fail(ctx, KP_E_BUFFER, "output buffers too small");
@@ -1125,6 +1138,7 @@ extern "C" kp_status kp_last_kernel_times(kp_ctx* ctx, double* ms, int32_t n) {
     if (!ctx || !ms) return KP_E_INVALID;
     if (!ctx->executed) return fail(ctx, KP_E_STATE, "no execute yet");
     for (int i = 0; i < n && i < 5; i++) ms[i] = ctx->kernel_ms[i];
+    for (int i = 5; i < n && i < 11; i++) ms[i] = (double)ctx->cycles[i - 5];
     return KP_OK;
 }
 

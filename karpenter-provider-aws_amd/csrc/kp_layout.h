@@ -57,6 +57,7 @@ struct KpDev {
     int32_t n_multi;                 // multi-valued catalog keys
     const uint16_t* type_val;        // [K_cat][T] (indexed by kcat[k])
     const uint64_t* multi_mask;      // [n_multi][T]
+    const uint16_t* multi16;         // [n_multi][T] same masks as u16 when every multi key has <= 16 catalog values, else null
     const uint64_t* dne_mask;        // [K_cat][TW] types whose label is DoesNotExist (or an empty In)
     const int64_t* alloc;            // [R][T]
     const int64_t* cap;              // [R][T]
@@ -141,5 +142,5 @@ struct KpDev {
 // stats slots
 enum {
     ST_POPPED = 0, ST_NC_EVALS, ST_NC_SCANNED, ST_TMPL_EVALS, ST_EXIST_EVALS, ST_SORT_FAST, ST_SORT_FULL,
-    ST_MEMO_SKIPS, ST_COUNT = 16
+    ST_MEMO_SKIPS, ST_CYC_POP, ST_CYC_SORT, ST_CYC_SCAN, ST_CYC_TMPL, ST_CYC_COMMIT, ST_CYC_SORT_FULL, ST_COUNT = 16
 };

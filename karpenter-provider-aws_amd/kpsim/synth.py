@@ -51,7 +51,7 @@ def config1(n_pods=2000, catalog=None, seed=SEED) -> Problem:
 
 
 def _classes_config2(rng, n_classes, taint_key):
-    """250 pod classes: cpu ∈ {100m..8} weighted small, memory = cpu × {1,2,4,8} GiB, 10% ephemeral-storage (1–15Gi: every type has 17Gi allocatable),
+    """250 pod classes: cpu ∈ {100m..8} weighted small, memory = cpu × {1,2,4,8} GiB, 10% ephemeral-storage (256Mi–4Gi; every type has 17Gi allocatable with the default 20Gi root volume),
     2% nvidia.com/gpu, 30% nodeSelectors over {arch, capacity-type, zone, instance-category, generation Gt 4},
     20% tolerate the tainted template."""
     cpus = np.array([100, 250, 500, 1000, 2000, 4000, 8000])
@@ -63,7 +63,7 @@ def _classes_config2(rng, n_classes, taint_key):
         mem = cpu_m * ratio * (1 << 30) // 1000  # bytes
         r = {"cpu": cpu_m, "memory": mem * 1000}
         if rng.random() < 0.10:
-            r["ephemeral-storage"] = int(rng.integers(1, 16)) * (1 << 30) * 1000
+            r["ephemeral-storage"] = int(rng.choice([256, 512, 1024, 2048, 4096])) * (1 << 20) * 1000
         if rng.random() < 0.02:
             r["nvidia.com/gpu"] = int(rng.choice([1, 2, 4, 8])) * 1000
         sel = []
