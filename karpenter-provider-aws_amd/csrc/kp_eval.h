@@ -68,6 +68,7 @@ struct EvalEnv {
     const int* slot_ct;
     const int* slot_zoneid;
     const Roles* roles;
+    uint32_t min_tmpl_mask;    // templates whose requirements carry minValues
 };
 
 // Cooperative fill by all threads of the block; contains two __syncthreads().
@@ -164,12 +165,23 @@ struct EvalIn {
     int tmpl;                 // template of the NodeClaim (taints bit, minValues keys)
     bool compat;              // taints + Requirements.Compatible
     bool force_off;           // always apply the offering test (template filter)
+    long long* prof;          // LDS stage-cycle counters (diagnostics) or null
 };
+#define EV_STAMP(slot)                                                           \
+    do {                                                                         \
+        if (a.prof) {                                                            \
+            const long long _t = __builtin_amdgcn_s_memtime();                   \
+            if (lane == 0) atomicAdd((unsigned long long*)&a.prof[slot], (unsigned long long)(_t - _t0)); \
+            _t0 = _t;                                                            \
+        }                                                                        \
+    } while (0)
 
 // Wave-uniform result: does NodeClaim.Add(pod) succeed?  On success ws.opts / ws.hdr / ws.words hold the new state.
 __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, const ClassCache& CC, const EvalIn& a,
                                           WaveScratch& ws, int lane) {
     const int TW = d.TW, T = d.T;
+    long long _t0 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
+    if (a.prof && lane == 0) atomicAdd((unsigned long long*)&a.prof[ST_EV_CALLS - ST_EV_REQ], 1ull);
     if (a.compat && !((CC.tol >> a.tmpl) & 1u)) return false;
     const int nck = CC.nck;
 
@@ -212,6 +224,7 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         }
     }
     if (ballot(fail)) return false;
+    EV_STAMP(0);
 
     // ---- options ∧ V[class] ∧ ¬DoesNotExist-types of keys whose merged operator is In/Exists ----
     uint64_t myopt = 0;
@@ -223,6 +236,7 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         if (lane < TW) myopt &= ~CC.dne[i][lane];
     }
     const uint64_t mm = ballot(kmul >= 0);
+    EV_STAMP(1);
 
     // ---- offerings over zone × capacity-type slots ----
     const bool need_off = a.force_off || (CC.flags & 1u);
@@ -238,6 +252,7 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         }
         mzc = ballot(ok);
     }
+    EV_STAMP(2);
 
     // ---- request totals over the active axes (the first KP_LDS_AXES live in registers) ----
     int64_t tot[KP_LDS_AXES];
@@ -258,15 +273,18 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         if (cw == 0) continue;
         const int t = w * 64 + lane;
         bool keep = (cw >> lane) & 1ull;
+        bool fit = true;
 #pragma unroll
         for (int ai = 0; ai < KP_LDS_AXES; ai++) {
-            if (tot[ai] > 0) keep = keep && tot[ai] <= E.alloc[ai * KP_MAX_TYPES + t];
+            const int64_t av = E.alloc[ai * KP_MAX_TYPES + t];
+            fit &= !(tot[ai] > 0) | (tot[ai] <= av);
         }
         for (int x = 0; x < n_extra; x++) {
             const int r = d.active_axes[KP_LDS_AXES + x];
             const int64_t tr = (a.base_req ? a.base_req[r] : 0) + (a.pod_req ? a.pod_req[r] : 0);
-            if (tr > 0) keep = keep && tr <= d.alloc[(size_t)r * T + (t < T ? t : 0)];
+            if (tr > 0) fit &= tr <= d.alloc[(size_t)r * T + (t < T ? t : 0)];
         }
+        keep &= fit;
         uint64_t mmm = mm;
         while (mmm) {
             const int i = __ffsll((unsigned long long)mmm) - 1;
@@ -275,17 +293,18 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
             const uint64_t am = rl64(adm, i);
             const uint64_t tm = E.multi16 ? (uint64_t)E.multi16[m * KP_MAX_TYPES + t]
                                           : d.multi_mask[(size_t)m * T + (t < T ? t : 0)];
-            keep = keep && (tm == 0 || (tm & am) != 0);
+            keep &= (tm == 0) | ((tm & am) != 0);
         }
-        if (need_off) keep = keep && (E.avail[t] & mzc) != 0;
+        if (need_off) keep &= (E.avail[t] & mzc) != 0;
         const uint64_t nb = ballot(keep);
         if (lane == w) newword = nb;
         anyw |= nb;
     }
+    EV_STAMP(3);
     if (anyw == 0) return false;
 
     // ---- minValues (Strict): distinct values per key over the remaining options ----
-    if (a.tmpl >= 0) {
+    if (a.tmpl >= 0 && ((E.min_tmpl_mask >> a.tmpl) & 1u)) {
         const int* mk = d.min_keys + (size_t)a.tmpl * KP_MAX_CLASS_KEYS;
         for (int q = 0; q < KP_MAX_CLASS_KEYS; q++) {
             const int k = mk[q];
@@ -329,6 +348,7 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
     }
     if (lane < TW) ws.opts[lane] = newword;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    EV_STAMP(4);
     return true;
 }
 
@@ -339,4 +359,84 @@ __device__ __forceinline__ void commit_reqs(const KpDev& d, const ClassCache& CC
         d.nc_hdr[(size_t)n * d.K + k] = ws.hdr[lane];
         for (int i = 0; i < CC.nw[lane]; i++) d.nc_words[(size_t)n * d.DW + CC.woff[lane] + i] = ws.words[CC.wsoff[lane] + i];
     }
+}
+
+// NodeClaim.Add for a NodeClaim that has already absorbed this pod class: Compatible/Add of the class requirements
+// is idempotent (Intersection is idempotent and associative), and its label, DoesNotExist, multi-valued and
+// offering filters are already applied to the options, which only shrink.  What remains is
+// resources.Fits(requests + pod, Allocatable) over the options, then minValues.
+__device__ __forceinline__ bool eval_fits_only(const KpDev& d, const EvalEnv& E, const EvalIn& a, WaveScratch& ws,
+                                               int lane) {
+    const int TW = d.TW, T = d.T;
+    int64_t tot[KP_LDS_AXES];
+#pragma unroll
+    for (int ai = 0; ai < KP_LDS_AXES; ai++) {
+        tot[ai] = 0;
+        if (ai < d.n_active) {
+            const int r = d.active_axes[ai];
+            tot[ai] = a.base_req[r] + a.pod_req[r];
+        }
+    }
+    const int n_extra = d.n_active > KP_LDS_AXES ? d.n_active - KP_LDS_AXES : 0;
+    uint64_t anyw = 0, newword = 0;
+    for (int w = 0; w < TW; w++) {
+        const uint64_t cw = rl64(a.opts, w);
+        if (cw == 0) continue;
+        const int t = w * 64 + lane;
+        bool keep = (cw >> lane) & 1ull;
+#pragma unroll
+        for (int ai = 0; ai < KP_LDS_AXES; ai++) {
+            const int64_t av = E.alloc[ai * KP_MAX_TYPES + t];
+            keep &= !(tot[ai] > 0) | (tot[ai] <= av);
+        }
+        for (int x = 0; x < n_extra; x++) {
+            const int r = d.active_axes[KP_LDS_AXES + x];
+            const int64_t tr = a.base_req[r] + a.pod_req[r];
+            if (tr > 0) keep &= tr <= d.alloc[(size_t)r * T + (t < T ? t : 0)];
+        }
+        const uint64_t nb = ballot(keep);
+        if (lane == w) newword = nb;
+        anyw |= nb;
+    }
+    if (anyw == 0) return false;
+    if ((E.min_tmpl_mask >> a.tmpl) & 1u) {
+        const int* mk = d.min_keys + (size_t)a.tmpl * KP_MAX_CLASS_KEYS;
+        for (int q = 0; q < KP_MAX_CLASS_KEYS; q++) {
+            const int k = mk[q];
+            if (k < 0) break;
+            const ReqHdr h = a.Ahdr[k];
+            if (!(h.flags & RF_MIN)) continue;
+            int count = 0;
+            const int kc = d.kcat[k];
+            if (kc >= 0 && (d.kflags[k] & KF_CAT_MULTI)) {
+                uint64_t acc = 0;
+                for (int w = 0; w < TW; w++) {
+                    const uint64_t nwd = rl64(newword, w);
+                    if ((nwd >> lane) & 1ull) acc |= d.multi_mask[(size_t)d.kmulti[k] * T + w * 64 + lane];
+                }
+                count = __popcll(wave_or64(acc));
+            } else if (kc >= 0) {
+                const int nwk = (d.nval[k] + 63) / 64;
+                for (int i = lane; i < KP_MAX_MIN_WORDS; i += 64) ws.minbits[i] = 0;
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                for (int w = 0; w < TW; w++) {
+                    const uint64_t nwd = rl64(newword, w);
+                    if ((nwd >> lane) & 1ull) {
+                        const uint16_t v = d.type_val[(size_t)kc * T + w * 64 + lane];
+                        if (v < VAL_ABSENT && v < KP_MAX_MIN_WORDS * 64)
+                            atomicOr((unsigned long long*)&ws.minbits[v >> 6], 1ull << (v & 63));
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                int c = 0;
+                for (int i = lane; i < nwk && i < KP_MAX_MIN_WORDS; i += 64) c += __popcll(ws.minbits[i]);
+                for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
+                count = c;
+            }
+            if (count < h.minv) return false;
+        }
+    }
+    if (lane < TW) ws.opts[lane] = newword;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    return true;
 }

@@ -305,12 +305,12 @@ __device__ inline void wave_rotate_left(SortSlice& d, int a, int e, int lane) {
             o = d.ord[i + 1];
             k = d.key[i + 1];
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        asm volatile("" ::: "memory");
         if (i < e - 1) {
             d.ord[i] = o;
             d.key[i] = k;
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        asm volatile("" ::: "memory");
     }
     if (lane == 0) {
         d.ord[e - 1] = fo;
@@ -330,12 +330,12 @@ __device__ inline void wave_rotate_right(SortSlice& d, int q, int n, int lane) {
             o = d.ord[i - 1];
             k = d.key[i - 1];
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        asm volatile("" ::: "memory");
         if (i > q) {
             d.ord[i] = o;
             d.key[i] = k;
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        asm volatile("" ::: "memory");
     }
     if (lane == 0) {
         d.ord[q] = lo;

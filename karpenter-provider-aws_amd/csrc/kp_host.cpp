@@ -217,7 +217,7 @@ struct kp_ctx {
     double ns_prep = 0, ns_exec = 0, ns_fin = 0;
     hipEvent_t ev[6] = {};
     double kernel_ms[5] = {};
-    int64_t cycles[6] = {};  // FFD phases (s_memtime): pop, sort, scan+eval, templates, commit, full pdqsort
+    int64_t cycles[12] = {};  // FFD phases (s_memtime): pop, sort, scan+eval, templates, commit, full pdqsort
     // last results (host)
     int last_N = 0, M = 0;
     std::vector<int32_t> h_nc_tmpl;
@@ -672,6 +672,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     });
     const int NT = (int)npo.size();
     if (NT > 32) return fail(ctx, KP_E_UNSUPPORTED, "more than 32 NodePools");
+    if (C + NT >= 65535) return fail(ctx, KP_E_UNSUPPORTED, "too many pod classes");
     std::vector<std::map<int, HReq>> treq(NT);
     for (int j = 0; j < NT; j++) {
         const kp_nodepool& np = in->nodepools[npo[j]];
@@ -998,6 +999,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.nc_ntypes = c->d_nc_ntypes.p;
     d.stats = c->d_stats.p;
     d.err = c->d_err.p;
+    d.profile = getenv("KPSIM_PROFILE") ? 1 : 0;
     c->P = P;
     c->C = C;
     c->NT = NT;
@@ -1106,6 +1108,7 @@ extern "C" kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out) {
     so.sorts_fast = st[ST_SORT_FAST];
     so.sorts_full = st[ST_SORT_FULL];
     for (int i = 0; i < 6; i++) c->cycles[i] = st[ST_CYC_POP + i];
+    for (int i = 0; i < 6; i++) c->cycles[6 + i] = st[ST_EV_REQ + i];
     so.ns_host_prep = c->ns_prep;
     so.ns_device_solve = c->ns_exec;
     if (N > out->cap_nodeclaims || n_ids > out->cap_type_ids) return fail(ctx, KP_E_BUFFER, "output buffers too small");
@@ -1138,7 +1141,7 @@ extern "C" kp_status kp_last_kernel_times(kp_ctx* ctx, double* ms, int32_t n) {
     if (!ctx || !ms) return KP_E_INVALID;
     if (!ctx->executed) return fail(ctx, KP_E_STATE, "no execute yet");
     for (int i = 0; i < n && i < 5; i++) ms[i] = ctx->kernel_ms[i];
-    for (int i = 5; i < n && i < 11; i++) ms[i] = (double)ctx->cycles[i - 5];
+    for (int i = 5; i < n && i < 17; i++) ms[i] = (double)ctx->cycles[i - 5];
     return KP_OK;
 }
 

@@ -63,6 +63,7 @@ __global__ __launch_bounds__(64) void template_init_kernel(KpDev d) {
     E.slot_ct = d.slot_ct;
     E.slot_zoneid = d.slot_zoneid;
     E.roles = &roles;
+    E.min_tmpl_mask = d.min_keys[(size_t)j * KP_MAX_CLASS_KEYS] >= 0 ? (1u << j) : 0u;
     EvalIn a;
     a.Ahdr = d.empty_hdr;
     a.Aw = d.empty_words;
@@ -72,6 +73,7 @@ __global__ __launch_bounds__(64) void template_init_kernel(KpDev d) {
     a.tmpl = j;
     a.compat = false;
     a.force_off = true;
+    a.prof = nullptr;
     const bool ok = eval_wave(d, E, CC, a, ws, lane);
     if (lane < d.TW) d.tmpl_opts[(size_t)j * d.TW + lane] = ok ? ws.opts[lane] : 0;
     if (lane == 0) d.tmpl_ok[j] = ok ? 1 : 0;
@@ -88,6 +90,11 @@ struct FfdShared {
     uint32_t ncnt[KP_MAX_NC];  // len(Pods) by NodeClaim id
     uint16_t ord[KP_MAX_NC];   // s.newNodeClaims: NodeClaim id by slice position
     uint32_t rej[KP_MAX_NC / 32];  // NodeClaims that rejected the current pod shape (valid until they change)
+    uint16_t last_cls[KP_MAX_NC];  // last pod class each NodeClaim absorbed (repeat fast path)
+    int qw_pod[64], qw_cls[64], qw_shape[64], qw_last[64];  // queue prefetch window
+    int64_t qw_req[64][KP_MAX_R];
+    int qw_base, qw_n;
+    int fastp[2][KP_NWAVES];
     WaveScratch ws[KP_NWAVES];
     ClassCache CC;
     Roles roles;
@@ -202,6 +209,8 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
         S.err = 0;
         S.CC.cls = -1;
         S.cur_cls = -1;
+        S.qw_base = 0;
+        S.qw_n = 0;
         for (int i = 0; i < ST_COUNT; i++) S.st[i] = 0;
     }
     __syncthreads();
@@ -213,36 +222,66 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
     E.slot_ct = S.slot_ct;
     E.slot_zoneid = S.slot_zoneid;
     E.roles = &S.roles;
+    {
+        uint32_t mmask = 0;
+        for (int j = 0; j < d.NT; j++)
+            if (d.min_keys[(size_t)j * KP_MAX_CLASS_KEYS] >= 0) mmask |= 1u << j;
+        E.min_tmpl_mask = mmask;
+    }
     SortSlice sl{S.key, S.ord};
 
     long long tclk = 0;
     for (;;) {
         // ================= wave 0: Queue.Pop, sort.Slice, first candidates =================
         if (wave == 0) {
-            if (lane == 0) {
-                tclk = __builtin_amdgcn_s_memtime();
-                if (S.qcount == 0 || S.err) {
-                    S.done = 1;
-                } else {
-                    const int p = d.qbuf[S.qhead];
-                    if (d.last_len[p] == S.qcount) {
-                        S.done = 1;
-                    } else {
-                        S.qhead = (S.qhead + 1 == P) ? 0 : S.qhead + 1;
-                        S.qcount--;
-                        S.cur_pod = p;
-                        const int c = d.pod_cls[p];
-                        S.cls_changed = c != S.cur_cls || S.CC.cls != c;
-                        S.cur_cls = c;
-                        S.cur_shape = d.pod_shape[p];
-                        S.st[ST_POPPED]++;
+            if (lane == 0) tclk = __builtin_amdgcn_s_memtime();
+            // Queue.Pop through an LDS window over the next <= 64 queue slots (pushes never land inside it)
+            const int qcount = S.qcount;
+            int done = (qcount == 0 || S.err) ? 1 : 0;
+            if (!done) {
+                const int head = S.qhead;
+                int off = head - S.qw_base;
+                if (off < 0) off += P;
+                if (off >= S.qw_n) {
+                    const int wn = qcount < 64 ? qcount : 64;
+                    int p = -1;
+                    if (lane < wn) {
+                        int pos = head + lane;
+                        if (pos >= P) pos -= P;
+                        p = d.qbuf[pos];
+                        S.qw_pod[lane] = p;
+                        S.qw_cls[lane] = d.pod_cls[p];
+                        S.qw_shape[lane] = d.pod_shape[p];
+                        S.qw_last[lane] = d.last_len[p];
+                        for (int r = 0; r < R; r++) S.qw_req[lane][r] = d.pod_req[(size_t)p * R + r];
                     }
+                    if (lane == 0) {
+                        S.qw_base = head;
+                        S.qw_n = wn;
+                    }
+                    asm volatile("" ::: "memory");
+                    off = 0;
                 }
+                if (S.qw_last[off] == qcount) {
+                    done = 1;
+                } else if (lane == 0) {
+                    const int p = S.qw_pod[off];
+                    const int c = S.qw_cls[off];
+                    S.qhead = (head + 1 == P) ? 0 : head + 1;
+                    S.qcount = qcount - 1;
+                    S.cur_pod = p;
+                    S.cls_changed = c != S.cur_cls || S.CC.cls != c;
+                    S.cur_cls = c;
+                    S.cur_shape = S.qw_shape[off];
+                    S.st[ST_POPPED]++;
+                }
+                if (!done && lane < R) S.pod_req[lane] = S.qw_req[off][lane];
             }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            if (!S.done) {
+            if (lane == 0) S.done = done;
+            asm volatile("" ::: "memory");
+            if (!done) {
                 const int pod = S.cur_pod;
-                if (lane < R) S.pod_req[lane] = d.pod_req[(size_t)pod * R + lane];
+                (void)pod;
                 if (S.cur_shape != S.prev_shape) {
                     for (int i = lane; i < KP_MAX_NC / 32; i += 64) S.rej[i] = 0;
                 }
@@ -290,8 +329,11 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                 a.tmpl = d.nc_tmpl[nc];
                 a.compat = true;
                 a.force_off = false;
-                const bool ok = eval_wave(d, E, S.CC, a, S.ws[wave], lane);
+                a.prof = d.profile ? &S.st[ST_EV_REQ] : nullptr;
+                const bool fast = S.last_cls[nc] == (uint16_t)S.cur_cls;
+                const bool ok = fast ? eval_fits_only(d, E, a, S.ws[wave], lane) : eval_wave(d, E, S.CC, a, S.ws[wave], lane);
                 if (lane == 0) {
+                    S.fastp[b][wave] = fast;
                     S.acc[b][wave] = ok;
                     if (!ok) atomicOr(&S.rej[nc >> 5], 1u << (nc & 31));
                 }
@@ -318,10 +360,11 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
             if (wave == win) {
                 const int pos = S.cand_pos[round & 1][win];
                 const int nc = S.ord[pos];
-                commit_reqs(d, S.CC, S.ws[win], nc, lane);
+                if (!S.fastp[round & 1][win]) commit_reqs(d, S.CC, S.ws[win], nc, lane);
                 if (lane < TW) d.nc_opts[(size_t)nc * TW + lane] = S.ws[win].opts[lane];
                 for (int r = lane; r < R; r += 64) d.nc_req[(size_t)nc * R + r] += S.pod_req[r];
                 if (lane == 0) {
+                    S.last_cls[nc] = (uint16_t)S.cur_cls;
                     S.ncnt[nc]++;
                     S.key[pos]++;
                     S.dirty_kind = 1;
@@ -349,6 +392,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                         a.tmpl = j;
                         a.compat = true;
                         a.force_off = false;
+                        a.prof = nullptr;
                         ok = eval_wave(d, E, S.CC, a, S.ws[wave], lane);
                     }
                     if (lane == 0) S.tacc[wave] = ok;
@@ -392,6 +436,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                             if (lane == 0) d.remaining[(size_t)jj * R + r] -= mx;
                         }
                         if (lane == 0) {
+                            S.last_cls[n] = (uint16_t)S.cur_cls;
                             d.nc_tmpl[n] = jj;
                             S.ord[n] = (uint16_t)n;
                             S.key[n] = 1;

@@ -137,10 +137,12 @@ struct KpDev {
     int32_t* nc_ntypes;              // [NCcap]
     int64_t* stats;                  // [16]
     int32_t* err;                    // [1] device-side error code (capacity overflow etc.)
+    int32_t profile;                 // accumulate per-stage evaluation cycles (diagnostics)
 };
 
 // stats slots
 enum {
     ST_POPPED = 0, ST_NC_EVALS, ST_NC_SCANNED, ST_TMPL_EVALS, ST_EXIST_EVALS, ST_SORT_FAST, ST_SORT_FULL,
-    ST_MEMO_SKIPS, ST_CYC_POP, ST_CYC_SORT, ST_CYC_SCAN, ST_CYC_TMPL, ST_CYC_COMMIT, ST_CYC_SORT_FULL, ST_COUNT = 16
+    ST_MEMO_SKIPS, ST_CYC_POP, ST_CYC_SORT, ST_CYC_SCAN, ST_CYC_TMPL, ST_CYC_COMMIT, ST_CYC_SORT_FULL,
+    ST_EV_REQ = 16, ST_EV_MASK, ST_EV_OFF, ST_EV_TYPES, ST_EV_MIN, ST_EV_CALLS, ST_COUNT = 32
 };

@@ -118,8 +118,8 @@ class Context:
 
     def ffd_cycles(self):
         """FFD-kernel s_memtime counters of the last fetched solve: pop, sort, scan+eval, templates, commit, full-sort."""
-        a = (C.c_double * 11)()
-        self.check(self.L.kp_last_kernel_times(self.h, a, 11), "kp_last_kernel_times")
+        a = (C.c_double * 17)()
+        self.check(self.L.kp_last_kernel_times(self.h, a, 17), "kp_last_kernel_times")
         return list(a)[5:]
 
     def close(self):
