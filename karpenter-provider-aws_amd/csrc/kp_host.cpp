@@ -1075,7 +1075,8 @@ extern "C" kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out) {
     HIPCHK(hipMemcpyAsync(&err, c->d_err.p, sizeof err, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(st, c->d_stats.p, sizeof st, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    if (err) return fail(ctx, KP_E_UNSUPPORTED, "in-flight NodeClaim capacity (KP_MAX_NC) exceeded");
+    if (err == 1) return fail(ctx, KP_E_UNSUPPORTED, "in-flight NodeClaim capacity (KP_MAX_NC) exceeded");
+    if (err) return fail(ctx, KP_E_STATE, "device solve loop exceeded its pop bound (internal error)");
     const int P = c->P, M = c->M;
     std::vector<int32_t> npods(N), spos(N), nopts(N), valid(N), ntypes(N), tmpl(N), types((size_t)N * M), pres(P), pord(P);
     if (N > 0) {

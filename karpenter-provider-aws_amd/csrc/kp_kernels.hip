@@ -93,7 +93,7 @@ struct FfdShared {
     uint16_t last_cls[KP_MAX_NC];  // last pod class each NodeClaim absorbed (repeat fast path)
     int qw_pod[64], qw_cls[64], qw_shape[64], qw_last[64];  // queue prefetch window
     int64_t qw_req[64][KP_MAX_R];
-    int qw_base, qw_n;
+    int qw_base, qw_n, qw_used;
     int fastp[2][KP_NWAVES];
     WaveScratch ws[KP_NWAVES];
     ClassCache CC;
@@ -211,6 +211,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
         S.cur_cls = -1;
         S.qw_base = 0;
         S.qw_n = 0;
+        S.qw_used = 0;
         for (int i = 0; i < ST_COUNT; i++) S.st[i] = 0;
     }
     __syncthreads();
@@ -237,11 +238,13 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
             if (lane == 0) tclk = __builtin_amdgcn_s_memtime();
             // Queue.Pop through an LDS window over the next <= 64 queue slots (pushes never land inside it)
             const int qcount = S.qcount;
+            // termination guard: Go's loop ends within P·(retries+1) pops; a runaway loop is reported, not hung
+            if (lane == 0 && S.st[ST_POPPED] > (long long)P * 64 + 4096) S.err = 2;
+            asm volatile("" ::: "memory");
             int done = (qcount == 0 || S.err) ? 1 : 0;
             if (!done) {
                 const int head = S.qhead;
-                int off = head - S.qw_base;
-                if (off < 0) off += P;
+                int off = S.qw_used;  // window slot of `head` (slots are consumed strictly in order)
                 if (off >= S.qw_n) {
                     const int wn = qcount < 64 ? qcount : 64;
                     int p = -1;
@@ -258,6 +261,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                     if (lane == 0) {
                         S.qw_base = head;
                         S.qw_n = wn;
+                        S.qw_used = 0;
                     }
                     asm volatile("" ::: "memory");
                     off = 0;
@@ -267,6 +271,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                 } else if (lane == 0) {
                     const int p = S.qw_pod[off];
                     const int c = S.qw_cls[off];
+                    S.qw_used = off + 1;
                     S.qhead = (head + 1 == P) ? 0 : head + 1;
                     S.qcount = qcount - 1;
                     S.cur_pod = p;
