@@ -274,10 +274,12 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         const int t = w * 64 + lane;
         bool keep = (cw >> lane) & 1ull;
         bool fit = true;
+        if (E.alloc) {
 #pragma unroll
-        for (int ai = 0; ai < KP_LDS_AXES; ai++) {
-            const int64_t av = E.alloc[ai * KP_MAX_TYPES + t];
-            fit &= !(tot[ai] > 0) | (tot[ai] <= av);
+            for (int ai = 0; ai < KP_LDS_AXES; ai++) {
+                const int64_t av = E.alloc[ai * KP_MAX_TYPES + t];
+                fit &= !(tot[ai] > 0) | (tot[ai] <= av);
+            }
         }
         for (int x = 0; x < n_extra; x++) {
             const int r = d.active_axes[KP_LDS_AXES + x];

@@ -26,7 +26,7 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
-    path = os.path.normpath(LIB_PATH)
+    path = os.path.normpath(os.environ.get("KPSIM_LIB", LIB_PATH))  # A/B diagnostics override
     if not os.path.exists(path):
         raise ImportError("libkpsim.so not built at %s (run __graft_entry__.build() or make -C karpenter-provider-aws_amd)"
                           % path)
