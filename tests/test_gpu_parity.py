@@ -107,8 +107,14 @@ def test_sort_emulation_many_equal_counts(ctx, golden, n_classes, reps):
         assert st["sorts_fast"] > 0
 
 
+def test_config2_full_parity(ctx, golden):
+    """BASELINE configs[1] at full size (50k pods, 918 types): bit-exact against the oracle (about 6 s on one core)."""
+    prob = synth.config2(catalog=golden)
+    parity.assert_same(parity.run_device(ctx, prob), parity.run_oracle(prob))
+
+
 def test_config2_full_properties(ctx, golden):
-    """Full 50k-pod config 2: size-independent properties (the oracle is too slow at this size)."""
+    """Full 50k-pod config 2: size-independent properties of the device result on its own."""
     prob = synth.config2(catalog=golden)
     r, _ = parity.run_device(ctx, prob)
     P = prob.pods.n
