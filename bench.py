@@ -156,8 +156,9 @@ def main():
             "kernel_ms": {"queue_sort": float(kt[0]), "class_mask": float(kt[1]), "template_init": float(kt[2]),
                           "ffd": float(kt[3]), "finalize": float(kt[4])},
             "end_to_end_ms": e2e_ms,
-            "ffd_phase_cycles": dict(zip(["pop", "sort", "scan_eval", "templates", "commit", "sort_full", "ev_req",
-                                          "ev_mask", "ev_off", "ev_types", "ev_min", "ev_calls"], cyc)),
+            "ffd_counters": dict(zip(["cyc_fast_loop", "cyc_sort", "cyc_slow_eval", "cyc_templates", "-",
+                                      "cyc_sort_full", "ev_req", "ev_mask", "ev_off", "ev_types", "ev_min", "ev_calls",
+                                      "quick_accepts", "slow_pods", "witness_misses"], cyc)),
             "nodeclaims": res.n_nodeclaims,
             "unschedulable": int((res.pod_result == -1).sum()),
             "solve_stats": {k: v for k, v in res.stats.items() if not k.startswith("ns_")},

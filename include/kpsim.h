@@ -248,8 +248,10 @@ kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out);
 
 /* Device time (ms, HIP events on the ctx stream) of the last kp_solve_execute, per phase:
  * [0] queue sort, [1] class masks, [2] template filter, [3] FFD solve kernel, [4] finalize/Truncate;
- * then (after kp_solve_fetch) FFD-kernel shader-clock counters [5..10]: pop, sort.Slice, scan+NodeClaim.Add,
- * new-NodeClaim templates, commit, full-pdqsort share of sort.Slice. */
+ * then (after kp_solve_fetch, KPSIM_PROFILE=1 in the environment at prepare) FFD-kernel shader-clock counters
+ * [5..10]: wave-0 fast loop, its sort.Slice share, slow-path NodeClaim.Add rounds, new-NodeClaim templates, -,
+ * full-pdqsort share; [11..16] per-stage evaluation cycles; then event counts [17] quick accepts, [18] slow-path
+ * pods, [19] witness misses (slow-path evaluations of a NodeClaim whose class repeats). */
 kp_status kp_last_kernel_times(kp_ctx* ctx, double* ms, int32_t n);
 
 /*

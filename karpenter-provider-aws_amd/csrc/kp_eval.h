@@ -28,6 +28,7 @@ struct WaveScratch {
     uint64_t words[KP_MAX_SCR_WORDS];
     uint64_t opts[KP_TW_MAX];
     uint64_t minbits[KP_MAX_MIN_WORDS];
+    int32_t hr[KP_LDS_AXES];   // quick-accept headroom of the chosen witness type (scaled, lower bound)
 };
 
 // Class-side operands of the evaluation, cached in LDS while consecutive pods share a class.
@@ -61,9 +62,10 @@ struct Roles {
 
 // Tables shared by every evaluation of a kernel (LDS in ffd_kernel).
 struct EvalEnv {
-    const int64_t* alloc;      // [KP_LDS_AXES][KP_MAX_TYPES] staged allocatable of the first active axes
+    const int64_t* alloc;      // [lds_nstage][astride] staged allocatable of the first active axes
     const uint64_t* avail;     // [T] available od/spot slot mask per type
-    const uint16_t* multi16;   // [n_multi][KP_MAX_TYPES] multi-valued label masks, or null → global multi_mask
+    const uint16_t* multi16;   // [n_multi][astride] multi-valued label masks, or null → global multi_mask
+    int astride;               // row stride of alloc / multi16
     const int* slot_zone;
     const int* slot_ct;
     const int* slot_zoneid;
@@ -113,6 +115,11 @@ __device__ inline void fill_class_cache(const KpDev& d, int c, ClassCache& CC, i
     __syncthreads();
 }
 
+// NodeClaim request totals are updated with device-scope atomics by the quick-accept path; read them past L1.
+__device__ __forceinline__ int64_t ld_req(const int64_t* p) {
+    return __hip_atomic_load(const_cast<int64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
     for (int o = 32; o >= 1; o >>= 1) x |= __shfl_xor(x, o);
     return x;
@@ -155,6 +162,9 @@ __device__ __forceinline__ bool role_dneok(const KpDev& d, const EvalEnv& E, con
     }
     return op_notin_or_dne(req_op(h.flags, popc_words(w, n)));
 }
+
+__device__ __forceinline__ void pick_witness(const KpDev& d, const EvalEnv& E, uint64_t newword, const int64_t* tot,
+                                             const int64_t* pod_req, bool minv, WaveScratch& ws, int lane);
 
 struct EvalIn {
     const ReqHdr* Ahdr;       // base requirements digest (NodeClaim, template or empty)
@@ -261,7 +271,7 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         tot[ai] = 0;
         if (ai < d.n_active) {
             const int r = d.active_axes[ai];
-            tot[ai] = (a.base_req ? a.base_req[r] : 0) + (a.pod_req ? a.pod_req[r] : 0);
+            tot[ai] = (a.base_req ? ld_req(a.base_req + r) : 0) + (a.pod_req ? a.pod_req[r] : 0);
         }
     }
     const int n_extra = d.n_active > KP_LDS_AXES ? d.n_active - KP_LDS_AXES : 0;
@@ -277,13 +287,13 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         if (E.alloc) {
 #pragma unroll
             for (int ai = 0; ai < KP_LDS_AXES; ai++) {
-                const int64_t av = E.alloc[ai * KP_MAX_TYPES + t];
+                const int64_t av = E.alloc[ai * E.astride + t];
                 fit &= !(tot[ai] > 0) | (tot[ai] <= av);
             }
         }
         for (int x = 0; x < n_extra; x++) {
             const int r = d.active_axes[KP_LDS_AXES + x];
-            const int64_t tr = (a.base_req ? a.base_req[r] : 0) + (a.pod_req ? a.pod_req[r] : 0);
+            const int64_t tr = (a.base_req ? ld_req(a.base_req + r) : 0) + (a.pod_req ? a.pod_req[r] : 0);
             if (tr > 0) fit &= tr <= d.alloc[(size_t)r * T + (t < T ? t : 0)];
         }
         keep &= fit;
@@ -293,7 +303,7 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
             mmm &= mmm - 1;
             const int m = rl32(kmul, i);
             const uint64_t am = rl64(adm, i);
-            const uint64_t tm = E.multi16 ? (uint64_t)E.multi16[m * KP_MAX_TYPES + t]
+            const uint64_t tm = E.multi16 ? (uint64_t)E.multi16[m * E.astride + t]
                                           : d.multi_mask[(size_t)m * T + (t < T ? t : 0)];
             keep &= (tm == 0) | ((tm & am) != 0);
         }
@@ -349,9 +359,64 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         }
     }
     if (lane < TW) ws.opts[lane] = newword;
+    pick_witness(d, E, newword, tot, a.pod_req, a.tmpl >= 0 && ((E.min_tmpl_mask >> a.tmpl) & 1u), ws, lane);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     EV_STAMP(4);
     return true;
+}
+
+// Quick-accept witness for the NodeClaim state an evaluation just produced (options `newword`, totals `tot`).
+// Lazy Fits: request totals only grow, so filterInstanceTypesByRequirements' Fits term applied at every Add equals
+// Fits against the final totals; a NodeClaim whose absorbed class repeats accepts the pod iff SOME option still fits.
+// One fitting option (the witness) proves acceptance.  The witness maximises the number of further copies of the
+// current pod that fit; ws.hr[a] = floor((alloc[a][w] - tot[a]) >> qshift[a]) is a lower bound of its headroom that
+// the quick path decrements by ceil(pod[a] >> qshift[a]) per accepted pod.  minValues templates
+// need the full option set, so they get hr = -1 (never quick).
+__device__ __forceinline__ void pick_witness(const KpDev& d, const EvalEnv& E, uint64_t newword, const int64_t* tot,
+                                             const int64_t* pod_req, bool minv, WaveScratch& ws, int lane) {
+    const int A = d.lds_A;
+    if (A == 0) return;
+    if (minv || !E.alloc || !pod_req) {
+        if (lane < A) ws.hr[lane] = -1;
+        return;
+    }
+    float inv[KP_LDS_AXES];
+#pragma unroll
+    for (int ai = 0; ai < KP_LDS_AXES; ai++) {
+        const int64_t p = ai < A ? pod_req[d.active_axes[ai]] : 0;
+        inv[ai] = p > 0 ? 1.0f / (float)p : 0.0f;
+    }
+    float best = -1.0f;
+    int bt = 0x7fffffff;
+    for (int w = 0; w < d.TW; w++) {
+        const uint64_t nwd = rl64(newword, w);
+        if (!((nwd >> lane) & 1ull)) continue;
+        const int t = w * 64 + lane;
+        float sc = 3.0e38f;
+#pragma unroll
+        for (int ai = 0; ai < KP_LDS_AXES; ai++)
+            if (inv[ai] > 0.0f) sc = fminf(sc, (float)(E.alloc[ai * E.astride + t] - tot[ai]) * inv[ai]);
+        if (sc > best) {
+            best = sc;
+            bt = t;
+        }
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        const float ob = __shfl_xor(best, o);
+        const int ot = __shfl_xor(bt, o);
+        if (ob > best || (ob == best && ot < bt)) {
+            best = ob;
+            bt = ot;
+        }
+    }
+    int64_t my = 0;
+#pragma unroll
+    for (int ai = 0; ai < KP_LDS_AXES; ai++)
+        if (lane == ai) my = tot[ai];
+    if (lane < A) {
+        const int64_t h = E.alloc[lane * E.astride + bt] - my;
+        ws.hr[lane] = h < 0 ? -1 : (int32_t)(h >> d.qshift[lane]);
+    }
 }
 
 // Write the merged class keys of a successful evaluation into NodeClaim slot n.
@@ -376,7 +441,7 @@ __device__ __forceinline__ bool eval_fits_only(const KpDev& d, const EvalEnv& E,
         tot[ai] = 0;
         if (ai < d.n_active) {
             const int r = d.active_axes[ai];
-            tot[ai] = a.base_req[r] + a.pod_req[r];
+            tot[ai] = ld_req(a.base_req + r) + a.pod_req[r];
         }
     }
     const int n_extra = d.n_active > KP_LDS_AXES ? d.n_active - KP_LDS_AXES : 0;
@@ -388,12 +453,12 @@ __device__ __forceinline__ bool eval_fits_only(const KpDev& d, const EvalEnv& E,
         bool keep = (cw >> lane) & 1ull;
 #pragma unroll
         for (int ai = 0; ai < KP_LDS_AXES; ai++) {
-            const int64_t av = E.alloc[ai * KP_MAX_TYPES + t];
+            const int64_t av = E.alloc[ai * E.astride + t];
             keep &= !(tot[ai] > 0) | (tot[ai] <= av);
         }
         for (int x = 0; x < n_extra; x++) {
             const int r = d.active_axes[KP_LDS_AXES + x];
-            const int64_t tr = a.base_req[r] + a.pod_req[r];
+            const int64_t tr = ld_req(a.base_req + r) + a.pod_req[r];
             if (tr > 0) keep &= tr <= d.alloc[(size_t)r * T + (t < T ? t : 0)];
         }
         const uint64_t nb = ballot(keep);
@@ -439,6 +504,7 @@ __device__ __forceinline__ bool eval_fits_only(const KpDev& d, const EvalEnv& E,
         }
     }
     if (lane < TW) ws.opts[lane] = newword;
+    pick_witness(d, E, newword, tot, a.pod_req, (E.min_tmpl_mask >> a.tmpl) & 1u, ws, lane);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     return true;
 }

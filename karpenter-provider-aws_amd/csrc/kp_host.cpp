@@ -20,6 +20,7 @@
 #include "kp_layout.h"
 
 size_t kp_ffd_shared_bytes();
+bool kp_ffd_plan_lds(KpDev& d, int max_bytes);
 hipError_t kp_launch_class_mask(const KpDev& d, hipStream_t s);
 hipError_t kp_launch_template_init(const KpDev& d, hipStream_t s);
 hipError_t kp_launch_ffd(const KpDev& d, hipStream_t s);
@@ -217,7 +218,7 @@ struct kp_ctx {
     double ns_prep = 0, ns_exec = 0, ns_fin = 0;
     hipEvent_t ev[6] = {};
     double kernel_ms[5] = {};
-    int64_t cycles[12] = {};  // FFD phases (s_memtime): pop, sort, scan+eval, templates, commit, full pdqsort
+    int64_t cycles[15] = {};  // FFD phases (s_memtime): pop, sort, scan+eval, templates, commit, full pdqsort
     // last results (host)
     int last_N = 0, M = 0;
     std::vector<int32_t> h_nc_tmpl;
@@ -1000,6 +1001,17 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.stats = c->d_stats.p;
     d.err = c->d_err.p;
     d.profile = getenv("KPSIM_PROFILE") ? 1 : 0;
+    // quick-accept headroom scale per active axis: every allocatable value >> qshift fits in 30 bits
+    for (int ai = 0; ai < KP_LDS_AXES; ai++) {
+        int sh = 0;
+        if (ai < d.n_active) {
+            int64_t mx = 0;
+            for (int t = 0; t < T; t++) mx = std::max(mx, c->alloc_rt[(size_t)d.active_axes[ai] * T + t]);
+            while ((mx >> sh) > 0x3FFFFFFF) sh++;
+        }
+        d.qshift[ai] = sh;
+    }
+    if (!kp_ffd_plan_lds(d, KP_LDS_BYTES)) return fail(ctx, KP_E_UNSUPPORTED, "FFD kernel LDS plan exceeds 160 KB");
     c->P = P;
     c->C = C;
     c->NT = NT;
@@ -1110,6 +1122,7 @@ extern "C" kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out) {
     so.sorts_full = st[ST_SORT_FULL];
     for (int i = 0; i < 6; i++) c->cycles[i] = st[ST_CYC_POP + i];
     for (int i = 0; i < 6; i++) c->cycles[6 + i] = st[ST_EV_REQ + i];
+    for (int i = 0; i < 3; i++) c->cycles[12 + i] = st[ST_QUICK + i];
     so.ns_host_prep = c->ns_prep;
     so.ns_device_solve = c->ns_exec;
     if (N > out->cap_nodeclaims || n_ids > out->cap_type_ids) return fail(ctx, KP_E_BUFFER, "output buffers too small");
@@ -1142,7 +1155,7 @@ extern "C" kp_status kp_last_kernel_times(kp_ctx* ctx, double* ms, int32_t n) {
     if (!ctx || !ms) return KP_E_INVALID;
     if (!ctx->executed) return fail(ctx, KP_E_STATE, "no execute yet");
     for (int i = 0; i < n && i < 5; i++) ms[i] = ctx->kernel_ms[i];
-    for (int i = 5; i < n && i < 17; i++) ms[i] = (double)ctx->cycles[i - 5];
+    for (int i = 5; i < n && i < 20; i++) ms[i] = (double)ctx->cycles[i - 5];
     return KP_OK;
 }
 

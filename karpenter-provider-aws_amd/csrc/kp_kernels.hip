@@ -57,6 +57,7 @@ __global__ __launch_bounds__(64) void template_init_kernel(KpDev d) {
     __syncthreads();
     EvalEnv E;
     E.alloc = nullptr;  // no requests: Fits({}, alloc) only needs non-negative allocatable (tmpl rows ∧ nonneg)
+    E.astride = 0;
     E.avail = d.avail_zc;
     E.multi16 = nullptr;
     E.slot_zone = d.slot_zone;
@@ -82,18 +83,13 @@ __global__ __launch_bounds__(64) void template_init_kernel(KpDev d) {
 // ------------------------------------------------------------------------------------------------
 // Solve: single-workgroup first-fit-decreasing
 // ------------------------------------------------------------------------------------------------
+// Fixed part of the FFD kernel's LDS.  The variable-size tables follow it at the offsets of the LDS plan
+// (kp_ffd_plan_lds): slice keys/order and last absorbed class per NodeClaim, the staged allocatable / offering /
+// multi-valued label tables, and the quick-accept headroom table hr[lds_A][lds_nq].
 struct FfdShared {
-    int64_t sAlloc[KP_LDS_AXES * KP_MAX_TYPES];
-    uint64_t sAvail[KP_MAX_TYPES];
-    uint16_t sMulti[5 * KP_MAX_TYPES];
-    uint32_t key[KP_MAX_NC];   // len(Pods) by slice position
-    uint32_t ncnt[KP_MAX_NC];  // len(Pods) by NodeClaim id
-    uint16_t ord[KP_MAX_NC];   // s.newNodeClaims: NodeClaim id by slice position
     uint32_t rej[KP_MAX_NC / 32];  // NodeClaims that rejected the current pod shape (valid until they change)
-    uint16_t last_cls[KP_MAX_NC];  // last pod class each NodeClaim absorbed (repeat fast path)
     int qw_pod[64], qw_cls[64], qw_shape[64], qw_last[64];  // queue prefetch window
     int64_t qw_req[64][KP_MAX_R];
-    int qw_base, qw_n, qw_used;
     int fastp[2][KP_NWAVES];
     WaveScratch ws[KP_NWAVES];
     ClassCache CC;
@@ -105,20 +101,20 @@ struct FfdShared {
     int tacc[KP_NWAVES];
     int n_cand[2], scan_done[2], scan_next[2];
     int sstack[64 * 5];
-    int N, qhead, qcount, done, cur_pod, cur_cls, cur_shape, prev_shape, cls_changed;
-    int dirty_kind, dirty_pos, seq, tw_winner, err;
+    // control state: owned by wave 0 inside its fast loop, by the block between the slow-path barriers
+    int N, qhead, qcount, qw_base, qw_n, qw_used, done, cur_pod, cur_cls, cur_shape, prev_shape;
+    int dirty_kind, dirty_pos, seq, err, cls_fill;
     long long st[ST_COUNT];
 };
 
 // wave 0: collect up to KP_NWAVES slice positions >= start whose NodeClaim has not rejected the current shape
-__device__ inline void collect_candidates(FfdShared& S, int start, int buf, int lane) {
-    const int N = S.N;
+__device__ inline void collect_candidates(FfdShared& S, const uint16_t* ord, int N, int start, int buf, int lane) {
     int cnt = 0, pos = start, next = N;
     while (pos < N) {
         const int p = pos + lane;
         bool c = false;
         if (p < N) {
-            const int nc = S.ord[p];
+            const int nc = ord[p];
             c = !((S.rej[nc >> 5] >> (nc & 31)) & 1u);
         }
         const uint64_t m = __ballot(c);
@@ -163,22 +159,35 @@ __device__ inline uint64_t limit_filter(const KpDev& d, int j, uint64_t o, int l
     return out;
 }
 
+__device__ __forceinline__ long long prof_clock(const KpDev& d) { return d.profile ? __builtin_amdgcn_s_memtime() : 0; }
+
+// Scheduler.Solve.  Wave 0 runs the queue, the sort.Slice emulation and the first-fit scan for as many pods as it
+// can resolve alone: a pod whose first non-rejected NodeClaim (slice order) has already absorbed the pod's class
+// and whose witness type still fits is placed without an evaluation (exact: see pick_witness).  Any other pod is
+// handed to all 8 waves (the slow path: NodeClaim.Add of up to 8 candidates at once, or the templates).
 __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     FfdShared& S = *reinterpret_cast<FfdShared*>(smem);
+    uint32_t* const skey = reinterpret_cast<uint32_t*>(smem + d.off_key);   // len(Pods) by slice position
+    uint16_t* const sord = reinterpret_cast<uint16_t*>(smem + d.off_ord);   // NodeClaim id by slice position
+    uint16_t* const slast = reinterpret_cast<uint16_t*>(smem + d.off_last); // last absorbed class by NodeClaim id
+    int64_t* const sAlloc = reinterpret_cast<int64_t*>(smem + d.off_alloc);
+    uint64_t* const sAvail = reinterpret_cast<uint64_t*>(smem + d.off_avail);
+    uint16_t* const sMulti = reinterpret_cast<uint16_t*>(smem + d.off_multi);
+    int32_t* const shr = reinterpret_cast<int32_t*>(smem + d.off_hr);       // [A][NQ] witness headroom
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nthr = blockDim.x;
     const int T = d.T, TW = d.TW, K = d.K, R = d.R, P = d.P;
+    const int TP = d.lds_tpad, NQ = d.lds_nq, A = d.lds_A, NCMAX = d.lds_ncmax;
     // ---- stage the type tables in LDS ----
-    const int nstage = d.n_active < KP_LDS_AXES ? d.n_active : KP_LDS_AXES;
-    for (int i = tid; i < nstage * KP_MAX_TYPES; i += nthr) {
-        const int ai = i / KP_MAX_TYPES, t = i % KP_MAX_TYPES;
-        S.sAlloc[i] = t < T ? d.alloc[(size_t)d.active_axes[ai] * T + t] : 0;
+    for (int i = tid; i < d.lds_nstage * TP; i += nthr) {
+        const int ai = i / TP, t = i % TP;
+        sAlloc[i] = t < T ? d.alloc[(size_t)d.active_axes[ai] * T + t] : 0;
     }
-    for (int t = tid; t < KP_MAX_TYPES; t += nthr) S.sAvail[t] = t < T ? d.avail_zc[t] : 0;
+    for (int t = tid; t < TP; t += nthr) sAvail[t] = t < T ? d.avail_zc[t] : 0;
     if (d.multi16)
-        for (int i = tid; i < d.n_multi * KP_MAX_TYPES; i += nthr) {
-            const int m = i / KP_MAX_TYPES, t = i % KP_MAX_TYPES;
-            S.sMulti[i] = t < T ? d.multi16[(size_t)m * T + t] : 0;
+        for (int i = tid; i < d.n_multi * TP; i += nthr) {
+            const int m = i / TP, t = i % TP;
+            sMulti[i] = t < T ? d.multi16[(size_t)m * T + t] : 0;
         }
     for (int s = tid; s < KP_MAX_SLOTS; s += nthr) {
         S.slot_zone[s] = s < d.n_slots ? d.slot_zone[s] : 0;
@@ -202,23 +211,25 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
         S.N = 0;
         S.qhead = 0;
         S.qcount = P;
+        S.qw_base = 0;
+        S.qw_n = 0;
+        S.qw_used = 0;
         S.done = 0;
         S.prev_shape = -1;
         S.dirty_kind = 0;
+        S.dirty_pos = 0;
         S.seq = 0;
         S.err = 0;
         S.CC.cls = -1;
         S.cur_cls = -1;
-        S.qw_base = 0;
-        S.qw_n = 0;
-        S.qw_used = 0;
         for (int i = 0; i < ST_COUNT; i++) S.st[i] = 0;
     }
     __syncthreads();
     EvalEnv E;
-    E.alloc = S.sAlloc;
-    E.avail = S.sAvail;
-    E.multi16 = d.multi16 ? S.sMulti : nullptr;
+    E.alloc = sAlloc;
+    E.astride = TP;
+    E.avail = sAvail;
+    E.multi16 = d.multi16 ? sMulti : nullptr;
     E.slot_zone = S.slot_zone;
     E.slot_ct = S.slot_ct;
     E.slot_zoneid = S.slot_zoneid;
@@ -229,102 +240,166 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
             if (d.min_keys[(size_t)j * KP_MAX_CLASS_KEYS] >= 0) mmask |= 1u << j;
         E.min_tmpl_mask = mmask;
     }
-    SortSlice sl{S.key, S.ord};
+    SortSlice sl{skey, sord};
+    // per-lane quick-accept axis (lane a < A) and its scale
+    int my_axis = 0, my_shift = 0;
+#pragma unroll
+    for (int ai = 0; ai < KP_LDS_AXES; ai++)
+        if (lane == ai) {
+            my_axis = d.active_axes[ai];
+            my_shift = d.qshift[ai];
+        }
+    const long long pop_bound = (long long)P * 64 + 4096;  // Go's loop ends within P·(retries+1) pops
 
-    long long tclk = 0;
     for (;;) {
-        // ================= wave 0: Queue.Pop, sort.Slice, first candidates =================
+        // ================= wave 0: the fast loop =================
         if (wave == 0) {
-            if (lane == 0) tclk = __builtin_amdgcn_s_memtime();
-            // Queue.Pop through an LDS window over the next <= 64 queue slots (pushes never land inside it)
-            const int qcount = S.qcount;
-            // termination guard: Go's loop ends within P·(retries+1) pops; a runaway loop is reported, not hung
-            if (lane == 0 && S.st[ST_POPPED] > (long long)P * 64 + 4096) S.err = 2;
-            asm volatile("" ::: "memory");
-            int done = (qcount == 0 || S.err) ? 1 : 0;
-            if (!done) {
-                const int head = S.qhead;
-                int off = S.qw_used;  // window slot of `head` (slots are consumed strictly in order)
-                if (off >= S.qw_n) {
+            const long long c_in = prof_clock(d);
+            const int N = S.N;
+            int qhead = S.qhead, qcount = S.qcount, qw_n = S.qw_n, qw_used = S.qw_used;
+            int seq = S.seq, prev_shape = S.prev_shape, dkind = S.dirty_kind, dpos = S.dirty_pos;
+            int done = 0, err = S.err;
+            long long popped = S.st[ST_POPPED], scanned = 0, nquick = 0, sfast = 0, sfull = 0, csort = 0;
+            for (;;) {
+                if (qcount == 0 || err) {
+                    done = 1;
+                    break;
+                }
+                if (popped > pop_bound) {  // a runaway loop is reported, not hung
+                    err = 2;
+                    done = 1;
+                    break;
+                }
+                // Queue.Pop through an LDS window over the next <= 64 queue slots (pushes never land inside it)
+                if (qw_used >= qw_n) {
                     const int wn = qcount < 64 ? qcount : 64;
-                    int p = -1;
                     if (lane < wn) {
-                        int pos = head + lane;
+                        int pos = qhead + lane;
                         if (pos >= P) pos -= P;
-                        p = d.qbuf[pos];
+                        const int p = d.qbuf[pos];
                         S.qw_pod[lane] = p;
                         S.qw_cls[lane] = d.pod_cls[p];
                         S.qw_shape[lane] = d.pod_shape[p];
                         S.qw_last[lane] = d.last_len[p];
                         for (int r = 0; r < R; r++) S.qw_req[lane][r] = d.pod_req[(size_t)p * R + r];
                     }
-                    if (lane == 0) {
-                        S.qw_base = head;
-                        S.qw_n = wn;
-                        S.qw_used = 0;
-                    }
-                    asm volatile("" ::: "memory");
-                    off = 0;
+                    qw_n = wn;
+                    qw_used = 0;
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 }
+                const int off = qw_used;
                 if (S.qw_last[off] == qcount) {
                     done = 1;
-                } else if (lane == 0) {
-                    const int p = S.qw_pod[off];
-                    const int c = S.qw_cls[off];
-                    S.qw_used = off + 1;
-                    S.qhead = (head + 1 == P) ? 0 : head + 1;
-                    S.qcount = qcount - 1;
-                    S.cur_pod = p;
-                    S.cls_changed = c != S.cur_cls || S.CC.cls != c;
-                    S.cur_cls = c;
-                    S.cur_shape = S.qw_shape[off];
-                    S.st[ST_POPPED]++;
+                    break;
                 }
-                if (!done && lane < R) S.pod_req[lane] = S.qw_req[off][lane];
-            }
-            if (lane == 0) S.done = done;
-            asm volatile("" ::: "memory");
-            if (!done) {
-                const int pod = S.cur_pod;
-                (void)pod;
-                if (S.cur_shape != S.prev_shape) {
-                    for (int i = lane; i < KP_MAX_NC / 32; i += 64) S.rej[i] = 0;
-                }
-                if (lane == 0) {
-                    const long long t1 = __builtin_amdgcn_s_memtime();
-                    S.st[ST_CYC_POP] += t1 - tclk;
-                    tclk = t1;
-                }
-                const long long c0 = __builtin_amdgcn_s_memtime();
-                const int how = sort_slice_after_change(sl, S.N, S.dirty_kind, S.dirty_pos, S.sstack, lane);
-                if (lane == 0) {
-                    if (how == 1) S.st[ST_SORT_FAST]++;
-                    if (how == 2) {
-                        S.st[ST_SORT_FULL]++;
-                        S.st[ST_CYC_SORT_FULL] += __builtin_amdgcn_s_memtime() - c0;
-                    }
-                    S.dirty_kind = 0;
-                    S.prev_shape = S.cur_shape;
-                    S.st[ST_NC_SCANNED] += S.N;
-                    const long long t1 = __builtin_amdgcn_s_memtime();
-                    S.st[ST_CYC_SORT] += t1 - tclk;
-                    tclk = t1;
-                }
+                const int p = S.qw_pod[off], c = S.qw_cls[off], shape = S.qw_shape[off];
+                qw_used++;
+                qhead = qhead + 1 == P ? 0 : qhead + 1;
+                qcount--;
+                popped++;
+                if (shape != prev_shape)
+                    for (int i = lane; i < (NCMAX + 31) / 32; i += 64) S.rej[i] = 0;
+                // sort.Slice(s.newNodeClaims, by len(Pods))
+                const long long c0 = prof_clock(d);
+                const int how = sort_slice_after_change(sl, N, dkind, dpos, S.sstack, lane);
+                sfast += how == 1;
+                sfull += how == 2;
+                csort += prof_clock(d) - c0;
+                dkind = 0;
+                prev_shape = shape;
+                scanned += N;
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                collect_candidates(S, 0, 0, lane);
+                // first NodeClaim in slice order that has not rejected this shape
+                int f = N;
+                for (int base = 0; base < N; base += 64) {
+                    const int q = base + lane;
+                    bool cand = false;
+                    if (q < N) {
+                        const int nc = sord[q];
+                        cand = !((S.rej[nc >> 5] >> (nc & 31)) & 1u);
+                    }
+                    const uint64_t m = ballot(cand);
+                    if (m) {
+                        f = base + __ffsll((unsigned long long)m) - 1;
+                        break;
+                    }
+                }
+                if (f < N) {
+                    const int nc = sord[f];
+                    if (nc < NQ && slast[nc] == (uint16_t)c) {
+                        bool ok = true;
+                        int64_t pq = 0;
+                        if (lane < A) {
+                            const int64_t pr = S.qw_req[off][my_axis];
+                            pq = (pr + ((1ll << my_shift) - 1)) >> my_shift;
+                            ok = pq <= (int64_t)shr[lane * NQ + nc];
+                        }
+                        if (ballot(!ok) == 0) {
+                            // quick accept: NodeClaim.Add(pod) succeeds with state (requirements, options) unchanged
+                            if (lane < A) shr[lane * NQ + nc] -= (int32_t)pq;
+                            if (lane < R) {
+                                const int64_t pr = S.qw_req[off][lane];
+                                if (pr) atomicAdd((unsigned long long*)&d.nc_req[(size_t)nc * R + lane], (unsigned long long)pr);
+                            }
+                            if (lane == 0) {
+                                skey[f]++;
+                                d.pod_result[p] = nc;
+                                d.pod_order[p] = seq;
+                            }
+                            seq++;
+                            dkind = 1;
+                            dpos = f;
+                            nquick++;
+                            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                            continue;
+                        }
+                    }
+                }
+                // slow path: the whole block evaluates this pod
+                if (lane < R) S.pod_req[lane] = S.qw_req[off][lane];
+                if (lane == 0) {
+                    S.cur_pod = p;
+                    S.cur_cls = c;
+                    S.cur_shape = shape;
+                    S.cls_fill = S.CC.cls != c;  // decided before the barrier: fill_class_cache rewrites CC.cls
+                }
+                collect_candidates(S, sord, N, f, 0, lane);
+                break;
             }
+            if (lane == 0) {
+                S.qhead = qhead;
+                S.qcount = qcount;
+                S.qw_n = qw_n;
+                S.qw_used = qw_used;
+                S.seq = seq;
+                S.prev_shape = prev_shape;
+                S.dirty_kind = dkind;
+                S.dirty_pos = dpos;
+                S.done = done;
+                S.err = err;
+                S.st[ST_POPPED] = popped;
+                S.st[ST_NC_SCANNED] += scanned;
+                S.st[ST_QUICK] += nquick;
+                S.st[ST_SLOW] += done ? 0 : 1;
+                S.st[ST_SORT_FAST] += sfast;
+                S.st[ST_SORT_FULL] += sfull;
+                S.st[ST_CYC_SORT] += csort;
+                S.st[ST_CYC_POP] += prof_clock(d) - c_in;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // quick-path atomics have reached L2
         }
         __syncthreads();
         if (S.done) break;
+        const long long c_slow = prof_clock(d);
         const int pod = S.cur_pod;
-        if (S.cls_changed) fill_class_cache(d, S.cur_cls, S.CC, tid, nthr);
+        if (S.cls_fill) fill_class_cache(d, S.cur_cls, S.CC, tid, nthr);
 
         // ================= in-flight NodeClaims in slice order: first whose Add succeeds =================
         int round = 0, win = -1;
         for (;;) {
             const int b = round & 1;
             if (wave < S.n_cand[b]) {
-                const int nc = S.ord[S.cand_pos[b][wave]];
+                const int nc = sord[S.cand_pos[b][wave]];
                 EvalIn a;
                 a.Ahdr = d.nc_hdr + (size_t)nc * K;
                 a.Aw = d.nc_words + (size_t)nc * d.DW;
@@ -335,12 +410,13 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                 a.compat = true;
                 a.force_off = false;
                 a.prof = d.profile ? &S.st[ST_EV_REQ] : nullptr;
-                const bool fast = S.last_cls[nc] == (uint16_t)S.cur_cls;
+                const bool fast = slast[nc] == (uint16_t)S.cur_cls;
                 const bool ok = fast ? eval_fits_only(d, E, a, S.ws[wave], lane) : eval_wave(d, E, S.CC, a, S.ws[wave], lane);
                 if (lane == 0) {
                     S.fastp[b][wave] = fast;
                     S.acc[b][wave] = ok;
                     if (!ok) atomicOr(&S.rej[nc >> 5], 1u << (nc & 31));
+                    if (fast) S.st[ST_WITNESS_MISS]++;
                 }
             }
             __syncthreads();
@@ -352,34 +428,36 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                 }
             if (tid == 0) S.st[ST_NC_EVALS] += nc_;
             if (win >= 0 || S.scan_done[b]) break;
-            if (wave == 0) collect_candidates(S, S.scan_next[b], b ^ 1, lane);
+            if (wave == 0) collect_candidates(S, sord, S.N, S.scan_next[b], b ^ 1, lane);
             __syncthreads();
             round++;
         }
-        if (tid == 0) {
+        if (tid == 0 && d.profile) {
             const long long t1 = __builtin_amdgcn_s_memtime();
-            S.st[ST_CYC_SCAN] += t1 - tclk;
-            tclk = t1;
+            S.st[ST_CYC_SCAN] += t1 - c_slow;
         }
         if (win >= 0) {
             if (wave == win) {
                 const int pos = S.cand_pos[round & 1][win];
-                const int nc = S.ord[pos];
+                const int nc = sord[pos];
                 if (!S.fastp[round & 1][win]) commit_reqs(d, S.CC, S.ws[win], nc, lane);
                 if (lane < TW) d.nc_opts[(size_t)nc * TW + lane] = S.ws[win].opts[lane];
-                for (int r = lane; r < R; r += 64) d.nc_req[(size_t)nc * R + r] += S.pod_req[r];
+                if (lane < R && S.pod_req[lane])
+                    atomicAdd((unsigned long long*)&d.nc_req[(size_t)nc * R + lane], (unsigned long long)S.pod_req[lane]);
+                if (lane < A && nc < NQ) shr[lane * NQ + nc] = S.ws[win].hr[lane];
                 if (lane == 0) {
-                    S.last_cls[nc] = (uint16_t)S.cur_cls;
-                    S.ncnt[nc]++;
-                    S.key[pos]++;
+                    slast[nc] = (uint16_t)S.cur_cls;
+                    skey[pos]++;
                     S.dirty_kind = 1;
                     S.dirty_pos = pos;
                     d.pod_result[pod] = nc;
                     d.pod_order[pod] = S.seq++;
                 }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
         } else {
             // ================= new NodeClaim from the templates (NodePool weight order) =================
+            const long long c_t = prof_clock(d);
             int twin = -1;
             for (int tb = 0; tb < d.NT; tb += KP_NWAVES) {
                 const int j = tb + wave;
@@ -409,7 +487,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                         break;
                     }
                 if (tid == 0) S.st[ST_TMPL_EVALS] += (d.NT - tb < KP_NWAVES ? d.NT - tb : KP_NWAVES);
-                if (twin >= 0 && (S.N >= KP_MAX_NC || S.N >= d.NCcap)) {
+                if (twin >= 0 && (S.N >= NCMAX || S.N >= d.NCcap)) {
                     if (tid == 0) S.err = 1;
                     twin = -1;
                     break;
@@ -425,7 +503,10 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         commit_reqs(d, S.CC, S.ws[wave], n, lane);
                         if (lane < TW) d.nc_opts[(size_t)n * TW + lane] = S.ws[wave].opts[lane];
-                        for (int r = lane; r < R; r += 64) d.nc_req[(size_t)n * R + r] = d.daemon[(size_t)jj * R + r] + S.pod_req[r];
+                        for (int r = lane; r < R; r += 64)
+                            __hip_atomic_store(&d.nc_req[(size_t)n * R + r], d.daemon[(size_t)jj * R + r] + S.pod_req[r],
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (lane < A && n < NQ) shr[lane * NQ + n] = S.ws[wave].hr[lane];
                         // subtractMax(remaining, nodeClaim.InstanceTypeOptions)
                         for (int r = 0; r < R; r++) {
                             if (!d.limit_set[(size_t)jj * R + r]) continue;
@@ -433,34 +514,32 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                             for (int w2 = 0; w2 < TW; w2++) {
                                 const uint64_t ow = S.ws[wave].opts[w2];
                                 if ((ow >> lane) & 1ull) {
-                                    const int64_t c = d.cap[(size_t)r * T + w2 * 64 + lane];
-                                    mx = c > mx ? c : mx;
+                                    const int64_t cp = d.cap[(size_t)r * T + w2 * 64 + lane];
+                                    mx = cp > mx ? cp : mx;
                                 }
                             }
                             mx = wave_max64(mx);
                             if (lane == 0) d.remaining[(size_t)jj * R + r] -= mx;
                         }
                         if (lane == 0) {
-                            S.last_cls[n] = (uint16_t)S.cur_cls;
+                            slast[n] = (uint16_t)S.cur_cls;
                             d.nc_tmpl[n] = jj;
-                            S.ord[n] = (uint16_t)n;
-                            S.key[n] = 1;
-                            S.ncnt[n] = 1;
+                            sord[n] = (uint16_t)n;
+                            skey[n] = 1;
                             S.N = n + 1;
                             S.dirty_kind = 2;
                             S.dirty_pos = n;
                             d.pod_result[pod] = n;
                             d.pod_order[pod] = S.seq++;
                         }
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     }
                     break;
                 }
                 __syncthreads();  // tacc is rewritten by the next template batch
             }
             if (tid == 0) {
-                const long long t1 = __builtin_amdgcn_s_memtime();
-                S.st[ST_CYC_TMPL] += t1 - tclk;
-                tclk = t1;
+                if (d.profile) S.st[ST_CYC_TMPL] += __builtin_amdgcn_s_memtime() - c_t;
                 if (twin < 0) {  // Queue.Push(pod, relaxed=false)
                     const int tail = (S.qhead + S.qcount) % P;
                     d.qbuf[tail] = pod;
@@ -475,8 +554,8 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
     // ---- outputs ----
     const int N = S.N;
     for (int i = tid; i < N; i += nthr) {
-        d.nc_npods[i] = S.ncnt[i];
-        d.nc_slice_pos[S.ord[i]] = i;
+        d.nc_npods[sord[i]] = (int32_t)skey[i];
+        d.nc_slice_pos[sord[i]] = i;
     }
     if (tid == 0) {
         d.nc_count[0] = N;
@@ -496,6 +575,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(KpDev d) {
     __shared__ int s_n;
     __shared__ uint64_t s_bits[KP_MAX_MIN_WORDS];
     __shared__ int s_ok;
+    __shared__ int64_t s_tot[KP_MAX_R];
     const int nc = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (nc >= d.nc_count[0]) return;
     const int T = d.T, TW = d.TW, M = d.M;
@@ -528,11 +608,20 @@ __global__ __launch_bounds__(256) void finalize_kernel(KpDev d) {
         const uint64_t m = ballot(ok);
         if (lane == 0) s_mzc = m;
     }
+    if (tid < d.R) s_tot[tid] = d.nc_req[(size_t)nc * d.R + tid];
     __syncthreads();
     const uint64_t mzc = s_mzc;
     for (int t = tid; t < TW * 64; t += blockDim.x) {
         if (t >= T) continue;
         if (!((d.nc_opts[(size_t)nc * TW + (t >> 6)] >> (t & 63)) & 1ull)) continue;
+        // Fits(final requests, Allocatable): the quick-accept path applies Fits lazily (pick_witness)
+        bool fit = true;
+        for (int ai = 0; ai < d.n_active; ai++) {
+            const int r = d.active_axes[ai];
+            const int64_t tr = s_tot[r];
+            if (tr > 0 && tr > d.alloc[(size_t)r * T + t]) fit = false;
+        }
+        if (!fit) continue;
         uint64_t m = d.avail_zc[t] & mzc;
         double price = 1.7976931348623157e308;  // math.MaxFloat64
         while (m) {
@@ -622,6 +711,43 @@ __global__ void iota_kernel(int32_t* out, int n) {
 
 size_t kp_ffd_shared_bytes() { return sizeof(FfdShared); }
 
+// Lay out the FFD kernel's dynamic LDS for this solve (fills d.off_*, d.lds_*).  Returns false if even the
+// quick-accept-free layout exceeds max_bytes.
+bool kp_ffd_plan_lds(KpDev& d, int max_bytes) {
+    auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    size_t off = al(sizeof(FfdShared));
+    const int ncmax = d.NCcap < KP_MAX_NC ? d.NCcap : KP_MAX_NC;
+    d.lds_ncmax = ncmax;
+    d.off_key = (int)off;
+    off = al(off + 4 * (size_t)ncmax);
+    d.off_ord = (int)off;
+    off = al(off + 2 * (size_t)ncmax);
+    d.off_last = (int)off;
+    off = al(off + 2 * (size_t)ncmax);
+    const int tp = (d.T + 63) / 64 * 64;
+    d.lds_tpad = tp;
+    d.lds_nstage = d.n_active < KP_LDS_AXES ? d.n_active : KP_LDS_AXES;
+    d.off_alloc = (int)off;
+    off = al(off + 8 * (size_t)d.lds_nstage * tp);
+    d.off_avail = (int)off;
+    off = al(off + 8 * (size_t)tp);
+    d.off_multi = (int)off;
+    if (d.multi16) off = al(off + 2 * (size_t)d.n_multi * tp);
+    d.off_hr = (int)off;
+    if ((int)off > max_bytes) return false;
+    d.lds_A = d.n_active <= KP_LDS_AXES ? d.n_active : 0;
+    int nq = 0;
+    if (d.lds_A > 0) {
+        nq = (int)((max_bytes - (int)off) / (4 * d.lds_A));
+        nq = nq < ncmax ? nq : ncmax;
+    }
+    d.lds_nq = nq;
+    if (nq == 0) d.lds_A = 0;
+    off += 4 * (size_t)d.lds_A * nq;
+    d.lds_bytes = (int)off;
+    return true;
+}
+
 hipError_t kp_launch_class_mask(const KpDev& d, hipStream_t s) {
     dim3 g(d.TW, d.C + d.NT);
     hipLaunchKernelGGL(class_mask_kernel, g, dim3(64), 0, s, d);
@@ -634,9 +760,9 @@ hipError_t kp_launch_template_init(const KpDev& d, hipStream_t s) {
 }
 hipError_t kp_launch_ffd(const KpDev& d, hipStream_t s) {
     static bool attr = false;
-    const size_t bytes = sizeof(FfdShared);
+    const size_t bytes = (size_t)d.lds_bytes;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)ffd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        hipError_t e = hipFuncSetAttribute((const void*)ffd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, KP_LDS_BYTES);
         if (e != hipSuccess) return e;
         attr = true;
     }

@@ -25,6 +25,7 @@
 #define KP_LDS_AXES 6                // allocatable axes staged in LDS
 #define KP_MAX_SCR_WORDS 64          // value-bitset words of one class's keys (per-wave LDS scratch)
 #define KP_MAX_MIN_WORDS 64          // value bitset for a minValues distinct count (4096 values)
+#define KP_LDS_BYTES (160 * 1024)    // LDS per workgroup on gfx950
 
 // ReqHdr.flags
 #define RF_DEF 1u                    // key present in the Requirements map
@@ -138,11 +139,24 @@ struct KpDev {
     int64_t* stats;                  // [16]
     int32_t* err;                    // [1] device-side error code (capacity overflow etc.)
     int32_t profile;                 // accumulate per-stage evaluation cycles (diagnostics)
+
+    // ---------------- FFD kernel LDS plan (kp_ffd_plan_lds) ----------------
+    // Dynamic LDS after the fixed FfdShared block: slice arrays sized by lds_ncmax, the staged type tables
+    // sized by lds_tpad, and the quick-accept headroom table hr[lds_A][lds_nq].
+    int32_t lds_ncmax;               // in-flight NodeClaim capacity of the kernel (<= KP_MAX_NC, <= NCcap)
+    int32_t lds_tpad;                // staged-table row stride (T rounded up to 64)
+    int32_t lds_nstage;              // allocatable axes staged in LDS
+    int32_t lds_A;                   // quick-accept axes (= n_active when n_active <= KP_LDS_AXES, else 0)
+    int32_t lds_nq;                  // NodeClaims with a quick-accept headroom row (ids < lds_nq)
+    int32_t off_key, off_ord, off_last, off_alloc, off_avail, off_multi, off_hr;
+    int32_t lds_bytes;
+    int32_t qshift[KP_LDS_AXES];     // headroom scale per quick axis: value >> qshift fits 30 bits
 };
 
 // stats slots
 enum {
     ST_POPPED = 0, ST_NC_EVALS, ST_NC_SCANNED, ST_TMPL_EVALS, ST_EXIST_EVALS, ST_SORT_FAST, ST_SORT_FULL,
     ST_MEMO_SKIPS, ST_CYC_POP, ST_CYC_SORT, ST_CYC_SCAN, ST_CYC_TMPL, ST_CYC_COMMIT, ST_CYC_SORT_FULL,
-    ST_EV_REQ = 16, ST_EV_MASK, ST_EV_OFF, ST_EV_TYPES, ST_EV_MIN, ST_EV_CALLS, ST_COUNT = 32
+    ST_EV_REQ = 16, ST_EV_MASK, ST_EV_OFF, ST_EV_TYPES, ST_EV_MIN, ST_EV_CALLS,
+    ST_QUICK = 24, ST_SLOW, ST_WITNESS_MISS, ST_COUNT = 32
 };

@@ -117,9 +117,11 @@ class Context:
         return list(a)
 
     def ffd_cycles(self):
-        """FFD-kernel s_memtime counters of the last fetched solve: pop, sort, scan+eval, templates, commit, full-sort."""
-        a = (C.c_double * 17)()
-        self.check(self.L.kp_last_kernel_times(self.h, a, 17), "kp_last_kernel_times")
+        """FFD-kernel counters of the last fetched solve (kpsim.h kp_last_kernel_times [5..19]): s_memtime cycles
+        (with KPSIM_PROFILE=1) of the fast loop, sort, slow-path rounds, templates, -, full sort, six evaluation
+        stages; then quick accepts, slow-path pods, witness misses."""
+        a = (C.c_double * 20)()
+        self.check(self.L.kp_last_kernel_times(self.h, a, 20), "kp_last_kernel_times")
         return list(a)[5:]
 
     def close(self):
