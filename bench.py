@@ -158,7 +158,9 @@ def main():
             "end_to_end_ms": e2e_ms,
             "ffd_counters": dict(zip(["cyc_fast_loop", "cyc_sort", "cyc_slow_eval", "cyc_templates", "-",
                                       "cyc_sort_full", "ev_req", "ev_mask", "ev_off", "ev_types", "ev_min", "ev_calls",
-                                      "quick_accepts", "slow_pods", "witness_misses"], cyc)),
+                                      "quick_accepts", "slow_pods", "witness_misses", "cyc_q_pop", "cyc_q_scan",
+                                      "cyc_q_check", "cyc_q_commit", "n_noinv", "n_winmove", "n_ldssort", "n_pivot",
+                                      "n_winload", "n_flush", "n_shape", "n_lds_append", "n_lds_nowin", "n_lds_outside", "n_batches"], cyc)),
             "nodeclaims": res.n_nodeclaims,
             "unschedulable": int((res.pod_result == -1).sum()),
             "solve_stats": {k: v for k, v in res.stats.items() if not k.startswith("ns_")},

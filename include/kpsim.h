@@ -251,7 +251,8 @@ kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out);
  * then (after kp_solve_fetch, KPSIM_PROFILE=1 in the environment at prepare) FFD-kernel shader-clock counters
  * [5..10]: wave-0 fast loop, its sort.Slice share, slow-path NodeClaim.Add rounds, new-NodeClaim templates, -,
  * full-pdqsort share; [11..16] per-stage evaluation cycles; then event counts [17] quick accepts, [18] slow-path
- * pods, [19] witness misses (slow-path evaluations of a NodeClaim whose class repeats). */
+ * pods, [19] witness misses (slow-path evaluations of a NodeClaim whose class repeats), [20..23] fast-loop
+ * cycles: pop, scan, quick check, quick commit. */
 kp_status kp_last_kernel_times(kp_ctx* ctx, double* ms, int32_t n);
 
 /*

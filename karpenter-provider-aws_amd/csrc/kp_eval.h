@@ -163,8 +163,66 @@ __device__ __forceinline__ bool role_dneok(const KpDev& d, const EvalEnv& E, con
     return op_notin_or_dne(req_op(h.flags, popc_words(w, n)));
 }
 
-__device__ __forceinline__ void pick_witness(const KpDev& d, const EvalEnv& E, uint64_t newword, const int64_t* tot,
-                                             const int64_t* pod_req, bool minv, WaveScratch& ws, int lane);
+// Quick-accept witness for the NodeClaim state an evaluation produces (options `newword`, totals `tot`).
+// Lazy Fits: request totals only grow, so filterInstanceTypesByRequirements' Fits term applied at every Add equals
+// Fits against the final totals; a NodeClaim whose absorbed class repeats accepts the pod iff SOME option still fits.
+// One fitting option (the witness) proves acceptance.  The witness maximises the number of further copies of the
+// current pod that fit (scored inside the type sweep, from the allocatable values it already loaded);
+// ws.hr[a] = floor((alloc[a][w] - tot[a]) >> qshift[a]) is a lower bound of its headroom that the quick path
+// decrements by ceil(pod[a] >> qshift[a]) per accepted pod.  minValues templates need the full
+// option set, so they get hr = -1 (never quick).
+struct WitnessAcc {
+    float inv[KP_LDS_AXES];
+    float best;
+    int bt;
+    bool on;
+    __device__ __forceinline__ void init(const KpDev& d, const EvalEnv& E, const int64_t* pod_req) {
+        on = d.lds_A > 0 && E.alloc && pod_req;
+        best = -1.0f;
+        bt = 0x7fffffff;
+#pragma unroll
+        for (int ai = 0; ai < KP_LDS_AXES; ai++) {
+            const int64_t p = (on && ai < d.lds_A) ? pod_req[d.active_axes[ai]] : 0;
+            inv[ai] = p > 0 ? 1.0f / (float)p : 0.0f;
+        }
+    }
+    // lane's type t survived with staged allocatable av[] against totals tot[]
+    __device__ __forceinline__ void add(const int64_t* av, const int64_t* tot, int t) {
+        float sc = 3.0e38f;
+#pragma unroll
+        for (int ai = 0; ai < KP_LDS_AXES; ai++)
+            if (inv[ai] > 0.0f) sc = fminf(sc, (float)(av[ai] - tot[ai]) * inv[ai]);
+        if (sc > best) {
+            best = sc;
+            bt = t;
+        }
+    }
+    __device__ __forceinline__ void finish(const KpDev& d, const EvalEnv& E, const int64_t* tot, bool minv,
+                                           WaveScratch& ws, int lane) {
+        const int A = d.lds_A;
+        if (A == 0) return;
+        if (!on || minv) {
+            if (lane < A) ws.hr[lane] = -1;
+            return;
+        }
+        for (int o = 32; o >= 1; o >>= 1) {
+            const float ob = __shfl_xor(best, o);
+            const int ot = __shfl_xor(bt, o);
+            if (ob > best || (ob == best && ot < bt)) {
+                best = ob;
+                bt = ot;
+            }
+        }
+        int64_t my = 0;
+#pragma unroll
+        for (int ai = 0; ai < KP_LDS_AXES; ai++)
+            if (lane == ai) my = tot[ai];
+        if (lane < A) {
+            const int64_t h = E.alloc[lane * E.astride + bt] - my;
+            ws.hr[lane] = h < 0 ? -1 : (int32_t)(h >> d.qshift[lane]);
+        }
+    }
+};
 
 struct EvalIn {
     const ReqHdr* Ahdr;       // base requirements digest (NodeClaim, template or empty)
@@ -277,6 +335,8 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
     const int n_extra = d.n_active > KP_LDS_AXES ? d.n_active - KP_LDS_AXES : 0;
 
     // ---- per type: Fits ∧ multi-valued labels ∧ offerings (64 types per ballot) ----
+    WitnessAcc wit;
+    wit.init(d, E, a.pod_req);
     uint64_t anyw = 0, newword = 0;
     for (int w = 0; w < TW; w++) {
         const uint64_t cw = rl64(myopt, w);
@@ -284,11 +344,12 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         const int t = w * 64 + lane;
         bool keep = (cw >> lane) & 1ull;
         bool fit = true;
+        int64_t av[KP_LDS_AXES];
         if (E.alloc) {
 #pragma unroll
             for (int ai = 0; ai < KP_LDS_AXES; ai++) {
-                const int64_t av = E.alloc[ai * E.astride + t];
-                fit &= !(tot[ai] > 0) | (tot[ai] <= av);
+                av[ai] = ai < d.lds_nstage ? E.alloc[ai * E.astride + t] : 0;
+                fit &= !(tot[ai] > 0) | (tot[ai] <= av[ai]);
             }
         }
         for (int x = 0; x < n_extra; x++) {
@@ -308,6 +369,7 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
             keep &= (tm == 0) | ((tm & am) != 0);
         }
         if (need_off) keep &= (E.avail[t] & mzc) != 0;
+        if (keep && wit.on) wit.add(av, tot, t);
         const uint64_t nb = ballot(keep);
         if (lane == w) newword = nb;
         anyw |= nb;
@@ -359,64 +421,10 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         }
     }
     if (lane < TW) ws.opts[lane] = newword;
-    pick_witness(d, E, newword, tot, a.pod_req, a.tmpl >= 0 && ((E.min_tmpl_mask >> a.tmpl) & 1u), ws, lane);
+    wit.finish(d, E, tot, a.tmpl >= 0 && ((E.min_tmpl_mask >> a.tmpl) & 1u), ws, lane);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     EV_STAMP(4);
     return true;
-}
-
-// Quick-accept witness for the NodeClaim state an evaluation just produced (options `newword`, totals `tot`).
-// Lazy Fits: request totals only grow, so filterInstanceTypesByRequirements' Fits term applied at every Add equals
-// Fits against the final totals; a NodeClaim whose absorbed class repeats accepts the pod iff SOME option still fits.
-// One fitting option (the witness) proves acceptance.  The witness maximises the number of further copies of the
-// current pod that fit; ws.hr[a] = floor((alloc[a][w] - tot[a]) >> qshift[a]) is a lower bound of its headroom that
-// the quick path decrements by ceil(pod[a] >> qshift[a]) per accepted pod.  minValues templates
-// need the full option set, so they get hr = -1 (never quick).
-__device__ __forceinline__ void pick_witness(const KpDev& d, const EvalEnv& E, uint64_t newword, const int64_t* tot,
-                                             const int64_t* pod_req, bool minv, WaveScratch& ws, int lane) {
-    const int A = d.lds_A;
-    if (A == 0) return;
-    if (minv || !E.alloc || !pod_req) {
-        if (lane < A) ws.hr[lane] = -1;
-        return;
-    }
-    float inv[KP_LDS_AXES];
-#pragma unroll
-    for (int ai = 0; ai < KP_LDS_AXES; ai++) {
-        const int64_t p = ai < A ? pod_req[d.active_axes[ai]] : 0;
-        inv[ai] = p > 0 ? 1.0f / (float)p : 0.0f;
-    }
-    float best = -1.0f;
-    int bt = 0x7fffffff;
-    for (int w = 0; w < d.TW; w++) {
-        const uint64_t nwd = rl64(newword, w);
-        if (!((nwd >> lane) & 1ull)) continue;
-        const int t = w * 64 + lane;
-        float sc = 3.0e38f;
-#pragma unroll
-        for (int ai = 0; ai < KP_LDS_AXES; ai++)
-            if (inv[ai] > 0.0f) sc = fminf(sc, (float)(E.alloc[ai * E.astride + t] - tot[ai]) * inv[ai]);
-        if (sc > best) {
-            best = sc;
-            bt = t;
-        }
-    }
-    for (int o = 32; o >= 1; o >>= 1) {
-        const float ob = __shfl_xor(best, o);
-        const int ot = __shfl_xor(bt, o);
-        if (ob > best || (ob == best && ot < bt)) {
-            best = ob;
-            bt = ot;
-        }
-    }
-    int64_t my = 0;
-#pragma unroll
-    for (int ai = 0; ai < KP_LDS_AXES; ai++)
-        if (lane == ai) my = tot[ai];
-    if (lane < A) {
-        const int64_t h = E.alloc[lane * E.astride + bt] - my;
-        ws.hr[lane] = h < 0 ? -1 : (int32_t)(h >> d.qshift[lane]);
-    }
 }
 
 // Write the merged class keys of a successful evaluation into NodeClaim slot n.
@@ -445,22 +453,26 @@ __device__ __forceinline__ bool eval_fits_only(const KpDev& d, const EvalEnv& E,
         }
     }
     const int n_extra = d.n_active > KP_LDS_AXES ? d.n_active - KP_LDS_AXES : 0;
+    WitnessAcc wit;
+    wit.init(d, E, a.pod_req);
     uint64_t anyw = 0, newword = 0;
     for (int w = 0; w < TW; w++) {
         const uint64_t cw = rl64(a.opts, w);
         if (cw == 0) continue;
         const int t = w * 64 + lane;
         bool keep = (cw >> lane) & 1ull;
+        int64_t av[KP_LDS_AXES];
 #pragma unroll
         for (int ai = 0; ai < KP_LDS_AXES; ai++) {
-            const int64_t av = E.alloc[ai * E.astride + t];
-            keep &= !(tot[ai] > 0) | (tot[ai] <= av);
+            av[ai] = ai < d.lds_nstage ? E.alloc[ai * E.astride + t] : 0;
+            keep &= !(tot[ai] > 0) | (tot[ai] <= av[ai]);
         }
         for (int x = 0; x < n_extra; x++) {
             const int r = d.active_axes[KP_LDS_AXES + x];
             const int64_t tr = ld_req(a.base_req + r) + a.pod_req[r];
             if (tr > 0) keep &= tr <= d.alloc[(size_t)r * T + (t < T ? t : 0)];
         }
+        if (keep && wit.on) wit.add(av, tot, t);
         const uint64_t nb = ballot(keep);
         if (lane == w) newword = nb;
         anyw |= nb;
@@ -504,7 +516,7 @@ __device__ __forceinline__ bool eval_fits_only(const KpDev& d, const EvalEnv& E,
         }
     }
     if (lane < TW) ws.opts[lane] = newword;
-    pick_witness(d, E, newword, tot, a.pod_req, (E.min_tmpl_mask >> a.tmpl) & 1u, ws, lane);
+    wit.finish(d, E, tot, (E.min_tmpl_mask >> a.tmpl) & 1u, ws, lane);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     return true;
 }

@@ -13,10 +13,14 @@
 #pragma once
 #include "kp_device.h"
 
+// Slice keys carry the FFD rejection memo in bit 31 (the NodeClaim rejected the current pod shape); comparisons
+// use the low 31 bits = len(Pods).
+#define KEYMASK 0x7FFFFFFFu
+
 struct SortSlice {
-    uint32_t* key;  // len(Pods) by slice position
+    uint32_t* key;  // len(Pods) by slice position (| KEY_REJ)
     uint16_t* ord;  // NodeClaim id by slice position
-    __device__ bool less(int i, int j) const { return key[i] < key[j]; }
+    __device__ bool less(int i, int j) const { return (key[i] & KEYMASK) < (key[j] & KEYMASK); }
     __device__ void swap(int i, int j) {
         const uint32_t k = key[i];
         key[i] = key[j];
@@ -29,8 +33,32 @@ struct SortSlice {
 
 __device__ __forceinline__ int go_bits_len(unsigned x) { return x ? 32 - __clz(x) : 0; }
 
+// The same slice held one element per lane (n <= 64): compares and swaps are readlanes on wave-uniform indices,
+// so the pdqsort emulation runs as scalar control flow without LDS round trips.
+struct RegSlice {
+    uint32_t k;
+    uint32_t o;
+    int lane;
+    __device__ __forceinline__ bool less(int i, int j) const {
+        return ((uint32_t)__builtin_amdgcn_readlane((int)k, i) & KEYMASK) <
+               ((uint32_t)__builtin_amdgcn_readlane((int)k, j) & KEYMASK);
+    }
+    __device__ __forceinline__ void swap(int i, int j) {
+        const uint32_t ki = __builtin_amdgcn_readlane((int)k, i), kj = __builtin_amdgcn_readlane((int)k, j);
+        const uint32_t oi = __builtin_amdgcn_readlane((int)o, i), oj = __builtin_amdgcn_readlane((int)o, j);
+        if (lane == i) {
+            k = kj;
+            o = oj;
+        } else if (lane == j) {
+            k = ki;
+            o = oi;
+        }
+    }
+};
+
 // order2_func / median_func / medianAdjacent_func / choosePivot_func (one lane)
-__device__ inline void go_order2(const SortSlice& d, int a, int b, int& swaps, int& x, int& y) {
+template <class D>
+__device__ inline void go_order2(const D& d, int a, int b, int& swaps, int& x, int& y) {
     if (d.less(b, a)) {
         swaps++;
         x = b;
@@ -40,7 +68,8 @@ __device__ inline void go_order2(const SortSlice& d, int a, int b, int& swaps, i
         y = b;
     }
 }
-__device__ inline int go_median(const SortSlice& d, int a, int b, int c, int& swaps) {
+template <class D>
+__device__ inline int go_median(const D& d, int a, int b, int c, int& swaps) {
     int x, y;
     go_order2(d, a, b, swaps, x, y);
     a = x;
@@ -52,7 +81,8 @@ __device__ inline int go_median(const SortSlice& d, int a, int b, int c, int& sw
     return y;
 }
 // hint: 0 unknown, 1 increasing, 2 decreasing
-__device__ inline void go_choose_pivot(const SortSlice& d, int a, int b, int& pivot, int& hint) {
+template <class D>
+__device__ inline void go_choose_pivot(const D& d, int a, int b, int& pivot, int& hint) {
     const int l = b - a;
     int swaps = 0;
     int i = a + l / 4 * 1, j = a + l / 4 * 2, k = a + l / 4 * 3;
@@ -79,7 +109,7 @@ __device__ inline int choose_pivot_hint_wave(const SortSlice& d, int n, int lane
         p = lane == 0 ? i : lane == 1 ? j : k;
     }
     const int nl = l >= 50 ? 9 : 3;
-    const uint32_t kv = (lane < nl) ? d.key[p] : 0u;
+    const uint32_t kv = (lane < nl) ? (d.key[p] & KEYMASK) : 0u;
     uint32_t v[9];
 #pragma unroll
     for (int q = 0; q < 9; q++) v[q] = __builtin_amdgcn_readlane(kv, q);
@@ -105,11 +135,13 @@ __device__ inline int choose_pivot_hint_wave(const SortSlice& d, int n, int lane
     return swaps == 0 ? 1 : (swaps == 12 ? 2 : 0);
 }
 
-__device__ inline void go_insertion_sort(SortSlice& d, int a, int b) {
+template <class D>
+__device__ inline void go_insertion_sort(D& d, int a, int b) {
     for (int i = a + 1; i < b; i++)
         for (int j = i; j > a && d.less(j, j - 1); j--) d.swap(j, j - 1);
 }
-__device__ inline void go_sift_down(SortSlice& d, int lo, int hi, int first) {
+template <class D>
+__device__ inline void go_sift_down(D& d, int lo, int hi, int first) {
     int root = lo;
     for (;;) {
         int child = 2 * root + 1;
@@ -120,7 +152,8 @@ __device__ inline void go_sift_down(SortSlice& d, int lo, int hi, int first) {
         root = child;
     }
 }
-__device__ inline void go_heap_sort(SortSlice& d, int a, int b) {
+template <class D>
+__device__ inline void go_heap_sort(D& d, int a, int b) {
     const int first = a, lo = 0, hi = b - a;
     for (int i = (hi - 1) / 2; i >= 0; i--) go_sift_down(d, i, hi, first);
     for (int i = hi - 1; i >= 0; i--) {
@@ -128,7 +161,8 @@ __device__ inline void go_heap_sort(SortSlice& d, int a, int b) {
         go_sift_down(d, lo, i, first);
     }
 }
-__device__ inline int go_partition(SortSlice& d, int a, int b, int pivot, bool& already) {
+template <class D>
+__device__ inline int go_partition(D& d, int a, int b, int pivot, bool& already) {
     d.swap(a, pivot);
     int i = a + 1, j = b - 1;
     while (i <= j && d.less(i, a)) i++;
@@ -153,7 +187,8 @@ __device__ inline int go_partition(SortSlice& d, int a, int b, int pivot, bool& 
     already = false;
     return j;
 }
-__device__ inline int go_partition_equal(SortSlice& d, int a, int b, int pivot) {
+template <class D>
+__device__ inline int go_partition_equal(D& d, int a, int b, int pivot) {
     d.swap(a, pivot);
     int i = a + 1, j = b - 1;
     for (;;) {
@@ -166,7 +201,8 @@ __device__ inline int go_partition_equal(SortSlice& d, int a, int b, int pivot) 
     }
     return i;
 }
-__device__ inline bool go_partial_insertion_sort(SortSlice& d, int a, int b) {
+template <class D>
+__device__ inline bool go_partial_insertion_sort(D& d, int a, int b) {
     int i = a + 1;
     for (int j = 0; j < 5; j++) {
         while (i < b && !d.less(i, i - 1)) i++;
@@ -188,7 +224,8 @@ __device__ inline bool go_partial_insertion_sort(SortSlice& d, int a, int b) {
     }
     return false;
 }
-__device__ inline void go_break_patterns(SortSlice& d, int a, int b) {
+template <class D>
+__device__ inline void go_break_patterns(D& d, int a, int b) {
     const int length = b - a;
     if (length >= 8) {
         uint64_t random = (uint64_t)length;  // xorshift(length)
@@ -204,7 +241,8 @@ __device__ inline void go_break_patterns(SortSlice& d, int a, int b) {
         }
     }
 }
-__device__ inline void go_reverse_range(SortSlice& d, int a, int b) {
+template <class D>
+__device__ inline void go_reverse_range(D& d, int a, int b) {
     int i = a, j = b - 1;
     while (i < j) {
         d.swap(i, j);
@@ -213,7 +251,8 @@ __device__ inline void go_reverse_range(SortSlice& d, int a, int b) {
     }
 }
 // pdqsort_func(data, 0, n, bits.Len(n)) with Go's recursion order (smaller side first) on an explicit stack.
-__device__ inline void pdqsort_full(SortSlice d, int n, int* stk) {
+template <class D>
+__device__ inline void pdqsort_full(D& d, int n, int* stk) {
     int sp = 0;
     auto push = [&](int a, int b, int limit, int wb, int wp) {
         stk[sp * 5 + 0] = a;
@@ -279,7 +318,7 @@ __device__ inline void pdqsort_full(SortSlice d, int n, int* stk) {
 __device__ inline int wave_find_first_ge(const SortSlice& d, int s, int n, uint32_t v, int lane) {
     for (int base = s; base < n; base += 64) {
         const int p = base + lane;
-        const uint64_t m = __ballot(p < n && d.key[p] >= v);
+        const uint64_t m = __ballot(p < n && (d.key[p] & KEYMASK) >= v);
         if (m) return base + __ffsll((unsigned long long)m) - 1;
     }
     return n;
@@ -287,7 +326,7 @@ __device__ inline int wave_find_first_ge(const SortSlice& d, int s, int n, uint3
 __device__ inline int wave_find_first_gt(const SortSlice& d, int s, int n, uint32_t v, int lane) {
     for (int base = s; base < n; base += 64) {
         const int p = base + lane;
-        const uint64_t m = __ballot(p < n && d.key[p] > v);
+        const uint64_t m = __ballot(p < n && (d.key[p] & KEYMASK) > v);
         if (m) return base + __ffsll((unsigned long long)m) - 1;
     }
     return n;
@@ -343,26 +382,83 @@ __device__ inline void wave_rotate_right(SortSlice& d, int q, int n, int lane) {
     }
 }
 
-// sort.Slice after one change (kind 1: element at pos gained a pod; kind 2: element appended at n-1).
-// Returns 0 nothing to do, 1 fast stable move, 2 full emulation (done by lane 0).  One wave, all lanes.
-__device__ inline int sort_slice_after_change(SortSlice d, int n, int kind, int pos, int* stk, int lane) {
-    if (kind == 0 || n <= 1) return 0;
-    bool inv;
-    if (kind == 1) inv = (pos + 1 < n) && (d.key[pos + 1] < d.key[pos]);
-    else inv = d.key[n - 2] > d.key[n - 1];
-    if (!inv) return 0;
-    bool fast = n <= 12;
-    if (!fast) fast = n >= 50 && choose_pivot_hint_wave(d, n, lane) == 1;
-    if (fast) {
-        if (kind == 1) {
-            const int e = wave_find_first_ge(d, pos + 1, n, d.key[pos], lane);
-            wave_rotate_left(d, pos, e, lane);
-        } else {
-            const int q = wave_find_first_gt(d, 0, n - 1, d.key[n - 1], lane);
-            wave_rotate_right(d, q, n, lane);
+// Full pdqsort_func emulation: in registers for n <= 64, else on lane 0 over LDS.
+__device__ inline void pdqsort_any(SortSlice d, int n, int* stk, int lane) {
+    if (n <= 64) {
+        RegSlice r;
+        r.lane = lane;
+        r.k = lane < n ? d.key[lane] : 0u;
+        r.o = lane < n ? d.ord[lane] : 0u;
+        pdqsort_full(r, n, stk);
+        if (lane < n) {
+            d.key[lane] = r.k;
+            d.ord[lane] = (uint16_t)r.o;
         }
-        return 1;
+        return;
     }
     if (lane == 0) pdqsort_full(d, n, stk);
+}
+
+// Is `pos` one of the positions choosePivot samples for a slice of length n >= 50 (l/4·{1,2,3} ± 1)?
+__device__ __forceinline__ bool is_pivot_sample(int n, int pos) {
+    const int q = n / 4;
+    const int d1 = pos - q, d2 = pos - 2 * q, d3 = pos - 3 * q;
+    return (d1 >= -1 && d1 <= 1) || (d2 >= -1 && d2 <= 1) || (d3 >= -1 && d3 <= 1);
+}
+
+// sort.Slice after one change (kind 1: element at pos gained a pod; kind 2: element appended at n-1).
+// Returns 0 nothing to do, 1 fast stable move, 2 full emulation (done by lane 0).  One wave, all lanes.
+//
+// The slice was sorted before the change and only position pos moved, so choosePivot's 9 samples can show a
+// swap only if pos is one of them: elsewhere the hint is "increasing" without loading them.  The stable move of
+// kind 1 is one LDS round trip when the run it crosses is shorter than 64: every lane loads one (key, ord) after
+// pos, the ballot gives the run end e, and lanes shift [pos+1, e) left by one.
+__device__ inline int sort_slice_after_change(SortSlice d, int n, int kind, int pos, int* stk, int lane) {
+    if (kind == 0 || n <= 1) return 0;
+    if (kind == 1) {
+        if (pos + 1 >= n) return 0;
+        const uint32_t kr = d.key[pos], kv = kr & KEYMASK;
+        const int q = pos + 1 + lane;
+        uint32_t k = 0xFFFFFFFFu;
+        uint16_t o = 0;
+        if (q < n) {
+            k = d.key[q];
+            o = d.ord[q];
+        }
+        const uint64_t ge = __ballot((k & KEYMASK) >= kv || q >= n);  // lanes past n count as >=
+        if (ge & 1ull) return 0;                // key[pos+1] >= key[pos]: no inversion
+        bool fast = n <= 12;
+        if (!fast) fast = n >= 50 && (!is_pivot_sample(n, pos) || choose_pivot_hint_wave(d, n, lane) == 1);
+        if (!fast) {
+            pdqsort_any(d, n, stk, lane);
+            return 2;
+        }
+        if (ge) {
+            const int first = __ffsll((unsigned long long)ge) - 1;  // run end e = pos + 1 + first
+            const uint16_t mo = d.ord[pos];
+            if (lane < first) {
+                d.key[pos + lane] = k;
+                d.ord[pos + lane] = o;
+            }
+            if (lane == 0) {
+                d.key[pos + first] = kr;
+                d.ord[pos + first] = mo;
+            }
+            return 1;
+        }
+        const int e = wave_find_first_ge(d, pos + 1, n, kv, lane);
+        wave_rotate_left(d, pos, e, lane);
+        return 1;
+    }
+    const bool inv = (d.key[n - 2] & KEYMASK) > (d.key[n - 1] & KEYMASK);
+    if (!inv) return 0;
+    bool fast = n <= 12;
+    if (!fast) fast = n >= 50 && (!is_pivot_sample(n, n - 1) || choose_pivot_hint_wave(d, n, lane) == 1);
+    if (fast) {
+        const int q = wave_find_first_gt(d, 0, n - 1, d.key[n - 1] & KEYMASK, lane);
+        wave_rotate_right(d, q, n, lane);
+        return 1;
+    }
+    pdqsort_any(d, n, stk, lane);
     return 2;
 }

@@ -218,7 +218,7 @@ struct kp_ctx {
     double ns_prep = 0, ns_exec = 0, ns_fin = 0;
     hipEvent_t ev[6] = {};
     double kernel_ms[5] = {};
-    int64_t cycles[15] = {};  // FFD phases (s_memtime): pop, sort, scan+eval, templates, commit, full pdqsort
+    int64_t cycles[30] = {};  // FFD phases (s_memtime): pop, sort, scan+eval, templates, commit, full pdqsort
     // last results (host)
     int last_N = 0, M = 0;
     std::vector<int32_t> h_nc_tmpl;
@@ -672,7 +672,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         return strcmp(in->nodepools[a].name, in->nodepools[b].name) < 0;
     });
     const int NT = (int)npo.size();
-    if (NT > 32) return fail(ctx, KP_E_UNSUPPORTED, "more than 32 NodePools");
+    if (NT > 31) return fail(ctx, KP_E_UNSUPPORTED, "more than 31 NodePools");
     if (C + NT >= 65535) return fail(ctx, KP_E_UNSUPPORTED, "too many pod classes");
     std::vector<std::map<int, HReq>> treq(NT);
     for (int j = 0; j < NT; j++) {
@@ -737,6 +737,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
                 q.key == c->key_resvtype)
                 cflags[row] |= 1u;
         }
+        if (rq.empty()) cflags[row] |= 4u;  // no requirement keys: NodeClaim.Add = tolerations + Fits (+ minValues)
         if ((int)rq.size() > KP_MAX_CLASS_KEYS || so > KP_MAX_SCR_WORDS) return false;
         koff[row + 1] = (int)ckeys.size();
         return true;
@@ -1122,7 +1123,8 @@ extern "C" kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out) {
     so.sorts_full = st[ST_SORT_FULL];
     for (int i = 0; i < 6; i++) c->cycles[i] = st[ST_CYC_POP + i];
     for (int i = 0; i < 6; i++) c->cycles[6 + i] = st[ST_EV_REQ + i];
-    for (int i = 0; i < 3; i++) c->cycles[12 + i] = st[ST_QUICK + i];
+    for (int i = 0; i < 7; i++) c->cycles[12 + i] = st[ST_QUICK + i];
+    for (int i = 0; i < 11; i++) c->cycles[19 + i] = st[ST_N_NOINV + i];
     so.ns_host_prep = c->ns_prep;
     so.ns_device_solve = c->ns_exec;
     if (N > out->cap_nodeclaims || n_ids > out->cap_type_ids) return fail(ctx, KP_E_BUFFER, "output buffers too small");
@@ -1155,7 +1157,7 @@ extern "C" kp_status kp_last_kernel_times(kp_ctx* ctx, double* ms, int32_t n) {
     if (!ctx || !ms) return KP_E_INVALID;
     if (!ctx->executed) return fail(ctx, KP_E_STATE, "no execute yet");
     for (int i = 0; i < n && i < 5; i++) ms[i] = ctx->kernel_ms[i];
-    for (int i = 5; i < n && i < 20; i++) ms[i] = (double)ctx->cycles[i - 5];
+    for (int i = 5; i < n && i < 35; i++) ms[i] = (double)ctx->cycles[i - 5];
     return KP_OK;
 }
 

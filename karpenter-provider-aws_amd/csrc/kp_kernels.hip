@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "kp_device.h"
 #include "kp_eval.h"
 #include "kp_gosort.h"
@@ -87,9 +89,7 @@ __global__ __launch_bounds__(64) void template_init_kernel(KpDev d) {
 // (kp_ffd_plan_lds): slice keys/order and last absorbed class per NodeClaim, the staged allocatable / offering /
 // multi-valued label tables, and the quick-accept headroom table hr[lds_A][lds_nq].
 struct FfdShared {
-    uint32_t rej[KP_MAX_NC / 32];  // NodeClaims that rejected the current pod shape (valid until they change)
-    int qw_pod[64], qw_cls[64], qw_shape[64], qw_last[64];  // queue prefetch window
-    int64_t qw_req[64][KP_MAX_R];
+    int64_t qw_req[64][KP_MAX_R];  // requests of the queue window's pods
     int fastp[2][KP_NWAVES];
     WaveScratch ws[KP_NWAVES];
     ClassCache CC;
@@ -102,21 +102,22 @@ struct FfdShared {
     int n_cand[2], scan_done[2], scan_next[2];
     int sstack[64 * 5];
     // control state: owned by wave 0 inside its fast loop, by the block between the slow-path barriers
-    int N, qhead, qcount, qw_base, qw_n, qw_used, done, cur_pod, cur_cls, cur_shape, prev_shape;
-    int dirty_kind, dirty_pos, seq, err, cls_fill;
+    int N, qhead, qcount, done, cur_pod, cur_cls, cur_shape, prev_shape;
+    int dirty_kind, dirty_pos, seq, err, cls_fill, scan_start, any_rej;
+    uint32_t cur_tol;              // tolerations word of the current shape's class (bit 31: no requirement keys)
+    int32_t cur_pq[KP_LDS_AXES];   // scaled quick-accept requests of the current shape
+    int64_t shape_req[KP_MAX_R];   // requests of the current shape (pending-total flush)
     long long st[ST_COUNT];
 };
 
 // wave 0: collect up to KP_NWAVES slice positions >= start whose NodeClaim has not rejected the current shape
-__device__ inline void collect_candidates(FfdShared& S, const uint16_t* ord, int N, int start, int buf, int lane) {
+__device__ inline void collect_candidates(FfdShared& S, const uint32_t* key, const uint16_t* ord, int N, int start,
+                                          int buf, int lane) {
+    (void)ord;
     int cnt = 0, pos = start, next = N;
     while (pos < N) {
         const int p = pos + lane;
-        bool c = false;
-        if (p < N) {
-            const int nc = ord[p];
-            c = !((S.rej[nc >> 5] >> (nc & 31)) & 1u);
-        }
+        const bool c = p < N && !(key[p] >> 31);
         const uint64_t m = __ballot(c);
         const int rank = cnt + __popcll(m & ((1ull << lane) - 1ull));
         if (c && rank < KP_NWAVES) S.cand_pos[buf][rank] = p;
@@ -171,6 +172,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
     uint32_t* const skey = reinterpret_cast<uint32_t*>(smem + d.off_key);   // len(Pods) by slice position
     uint16_t* const sord = reinterpret_cast<uint16_t*>(smem + d.off_ord);   // NodeClaim id by slice position
     uint16_t* const slast = reinterpret_cast<uint16_t*>(smem + d.off_last); // last absorbed class by NodeClaim id
+    uint8_t* const stmpl = reinterpret_cast<uint8_t*>(smem + d.off_tmpl);   // template by NodeClaim id
     int64_t* const sAlloc = reinterpret_cast<int64_t*>(smem + d.off_alloc);
     uint64_t* const sAvail = reinterpret_cast<uint64_t*>(smem + d.off_avail);
     uint16_t* const sMulti = reinterpret_cast<uint16_t*>(smem + d.off_multi);
@@ -200,7 +202,6 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
         S.roles.woff[tid] = rk >= 0 ? d.woff[rk] : 0;
         S.roles.nw[tid] = rk >= 0 ? d.nw[rk] : 0;
     }
-    for (int i = tid; i < KP_MAX_NC / 32; i += nthr) S.rej[i] = 0;
     for (int p = tid; p < P; p += nthr) {
         d.qbuf[p] = d.queue0[p];
         d.last_len[p] = 0;
@@ -211,17 +212,19 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
         S.N = 0;
         S.qhead = 0;
         S.qcount = P;
-        S.qw_base = 0;
-        S.qw_n = 0;
-        S.qw_used = 0;
         S.done = 0;
         S.prev_shape = -1;
         S.dirty_kind = 0;
         S.dirty_pos = 0;
+        S.scan_start = 0;
+        S.any_rej = 0;
         S.seq = 0;
         S.err = 0;
         S.CC.cls = -1;
         S.cur_cls = -1;
+        S.cur_tol = 0;
+        for (int i = 0; i < KP_LDS_AXES; i++) S.cur_pq[i] = 0;
+        for (int i = 0; i < KP_MAX_R; i++) S.shape_req[i] = 0;
         for (int i = 0; i < ST_COUNT; i++) S.st[i] = 0;
     }
     __syncthreads();
@@ -250,16 +253,86 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
             my_shift = d.qshift[ai];
         }
     const long long pop_bound = (long long)P * 64 + 4096;  // Go's loop ends within P·(retries+1) pops
+    // wave 0 state that lives across slow-path episodes:
+    //   queue window — lane i holds the i-th next queued pod (refilled every 64 pops; pushes land after it):
+    //     pod, class, shape, lastLen, tolerations word (bit 31: class has no requirement keys), and
+    //     vq[a] = ceil(request[axis a] >> qshift[a]) for the quick-accept axes (clamped to int32).
+    int qw_n = 0, qw_used = 0;
+    int vp = 0, vc = 0, vshape = 0, vlast = 0;
+    uint32_t vtol = 0;
+    int32_t vq[KP_LDS_AXES];
+#pragma unroll
+    for (int ai = 0; ai < KP_LDS_AXES; ai++) vq[ai] = 0;
 
     for (;;) {
         // ================= wave 0: the fast loop =================
         if (wave == 0) {
             const long long c_in = prof_clock(d);
             const int N = S.N;
-            int qhead = S.qhead, qcount = S.qcount, qw_n = S.qw_n, qw_used = S.qw_used;
+            int qhead = S.qhead, qcount = S.qcount;
             int seq = S.seq, prev_shape = S.prev_shape, dkind = S.dirty_kind, dpos = S.dirty_pos;
+            int sstart = S.scan_start;  // every slice position < sstart has rejected the current shape
+            int any_rej = S.any_rej;
             int done = 0, err = S.err;
-            long long popped = S.st[ST_POPPED], scanned = 0, nquick = 0, sfast = 0, sfull = 0, csort = 0;
+            int c = S.cur_cls;
+            uint32_t tl = S.cur_tol;
+            int pq[KP_LDS_AXES];
+#pragma unroll
+            for (int ai = 0; ai < KP_LDS_AXES; ai++) pq[ai] = S.cur_pq[ai];
+            long long popped = S.st[ST_POPPED], scanned = 0, nquick = 0, sfast = 0, sfull = 0, csort = 0, csfull = 0;
+            long long cqpop = 0, cqscan = 0, cqcheck = 0, cqcommit = 0;
+            long long n_noinv = 0, n_winmove = 0, n_ldssort = 0, n_pivot = 0, n_winload = 0, n_flush = 0, n_shape = 0;
+            long long n_r2 = 0, n_rwb = 0, n_rout = 0, n_batch = 0;
+            // ---- slice window: lane i mirrors slice position wb + i and its NodeClaim (authoritative while valid) ----
+            int wb = -1;
+            uint32_t wk = 0xFFFFFFFFu, wo = 0, wm = 0xFFFFu;  // key|rejected, NodeClaim id, lastClass | template << 16
+            int32_t wh[KP_LDS_AXES];                            // witness headroom (scaled), -1: never quick
+            bool wa = false;                                    // the NodeClaim has absorbed the current class
+            int wcnt = 0;                                       // current-shape pods placed since the last flush
+#pragma unroll
+            for (int ai = 0; ai < KP_LDS_AXES; ai++) wh[ai] = -1;
+            auto absorbed = [&](uint32_t m) -> bool {
+                return (int)(m & 0xFFFFu) == c || ((tl >> 31) && ((tl >> (m >> 16)) & 1u));
+            };
+            // write the window back to LDS and the pending request totals to HBM (same-shape requests are identical)
+            auto win_flush = [&]() {
+                if (wb < 0) return;
+                n_flush++;
+                const int q = wb + lane;
+                if (q < N) {
+                    skey[q] = wk;
+                    sord[q] = (uint16_t)wo;
+                    if ((int)wo < NQ)
+                        for (int ai = 0; ai < A; ai++) shr[ai * NQ + wo] = wh[ai];
+                    if (wcnt)
+                        for (int r = 0; r < R; r++) {
+                            const int64_t x = S.shape_req[r];
+                            if (x) atomicAdd((unsigned long long*)&d.nc_req[(size_t)wo * R + r], (unsigned long long)(x * wcnt));
+                        }
+                }
+                wcnt = 0;
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            };
+            auto win_load = [&](int base) {
+                n_winload++;
+                wb = base;
+                const int q = wb + lane;
+                if (q < N) {
+                    wk = skey[q];
+                    wo = sord[q];
+                    wm = (uint32_t)slast[wo] | ((uint32_t)stmpl[wo] << 16);
+#pragma unroll
+                    for (int ai = 0; ai < KP_LDS_AXES; ai++) wh[ai] = (ai < A && (int)wo < NQ) ? shr[ai * NQ + wo] : -1;
+                } else {
+                    wk = 0xFFFFFFFFu;
+                    wo = 0;
+                    wm = 0xFFFFu;
+#pragma unroll
+                    for (int ai = 0; ai < KP_LDS_AXES; ai++) wh[ai] = -1;
+                }
+                wa = q < N && absorbed(wm);
+                wcnt = 0;
+            };
             for (;;) {
                 if (qcount == 0 || err) {
                     done = 1;
@@ -270,113 +343,323 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                     done = 1;
                     break;
                 }
-                // Queue.Pop through an LDS window over the next <= 64 queue slots (pushes never land inside it)
+                // Queue.Pop through a register window over the next <= 64 queue slots (pushes never land inside)
                 if (qw_used >= qw_n) {
                     const int wn = qcount < 64 ? qcount : 64;
                     if (lane < wn) {
                         int pos = qhead + lane;
                         if (pos >= P) pos -= P;
-                        const int p = d.qbuf[pos];
-                        S.qw_pod[lane] = p;
-                        S.qw_cls[lane] = d.pod_cls[p];
-                        S.qw_shape[lane] = d.pod_shape[p];
-                        S.qw_last[lane] = d.last_len[p];
-                        for (int r = 0; r < R; r++) S.qw_req[lane][r] = d.pod_req[(size_t)p * R + r];
+                        vp = d.qbuf[pos];
+                        vc = d.pod_cls[vp];
+                        vshape = d.pod_shape[vp];
+                        vlast = d.last_len[vp];
+                        vtol = (d.tol[vc] & 0x7FFFFFFFu) | ((d.cls_flags[vc] & 4u) ? 0x80000000u : 0u);
+                        for (int r = 0; r < R; r++) S.qw_req[lane][r] = d.pod_req[(size_t)vp * R + r];
+#pragma unroll
+                        for (int ai = 0; ai < KP_LDS_AXES; ai++) {
+                            const int64_t pr = ai < A ? d.pod_req[(size_t)vp * R + d.active_axes[ai]] : 0;
+                            const int64_t x = (pr + ((1ll << d.qshift[ai]) - 1)) >> d.qshift[ai];
+                            vq[ai] = x > 0x7FFFFFFF ? 0x7FFFFFFF : (int32_t)x;
+                        }
                     }
                     qw_n = wn;
                     qw_used = 0;
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 }
+                const long long t_a = prof_clock(d);
                 const int off = qw_used;
-                if (S.qw_last[off] == qcount) {
+                if (rl32(vlast, off) == qcount) {
                     done = 1;
                     break;
                 }
-                const int p = S.qw_pod[off], c = S.qw_cls[off], shape = S.qw_shape[off];
+                const int p = rl32(vp, off), shape = rl32(vshape, off);
                 qw_used++;
                 qhead = qhead + 1 == P ? 0 : qhead + 1;
                 qcount--;
                 popped++;
-                if (shape != prev_shape)
-                    for (int i = lane; i < (NCMAX + 31) / 32; i += 64) S.rej[i] = 0;
-                // sort.Slice(s.newNodeClaims, by len(Pods))
-                const long long c0 = prof_clock(d);
-                const int how = sort_slice_after_change(sl, N, dkind, dpos, S.sstack, lane);
-                sfast += how == 1;
-                sfull += how == 2;
-                csort += prof_clock(d) - c0;
-                dkind = 0;
-                prev_shape = shape;
-                scanned += N;
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                // first NodeClaim in slice order that has not rejected this shape
-                int f = N;
-                for (int base = 0; base < N; base += 64) {
-                    const int q = base + lane;
-                    bool cand = false;
-                    if (q < N) {
-                        const int nc = sord[q];
-                        cand = !((S.rej[nc >> 5] >> (nc & 31)) & 1u);
+                if (shape != prev_shape) {
+                    n_shape++;
+                    win_flush();  // pending totals belong to the previous shape
+                    if (any_rej) {
+                        for (int i = lane; i < N; i += 64) skey[i] &= KEYMASK;
+                        wk = wk == 0xFFFFFFFFu ? wk : (wk & KEYMASK);
+                        any_rej = 0;
                     }
-                    const uint64_t m = ballot(cand);
+                    c = rl32(vc, off);
+                    tl = (uint32_t)rl32((int)vtol, off);
+#pragma unroll
+                    for (int ai = 0; ai < KP_LDS_AXES; ai++) pq[ai] = rl32(vq[ai], off);
+                    if (lane < R) S.shape_req[lane] = S.qw_req[off][lane];
+                    wa = wb >= 0 && wb + lane < N && absorbed(wm);
+                    sstart = 0;
+                    prev_shape = shape;
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                }
+                scanned += N;
+                const long long t_b = prof_clock(d);
+                cqpop += t_b - t_a;
+                // sort.Slice(s.newNodeClaims, by len(Pods)) at the start of add(): at most one element changed since
+                // the last sort (dkind 1: position dpos gained a pod; dkind 2: a NodeClaim was appended)
+                if (dkind) {
+                    int how = 0;
+                    bool done_here = false;
+                    if (dkind == 1 && wb >= 0 && dpos >= wb && dpos < wb + 64) {
+                        // in the window: key[f] (already incremented) moves to the end of its old run
+                        const int f = dpos;
+                        uint32_t kv = (uint32_t)rl32((int)wk, f - wb) & KEYMASK;
+                        uint64_t ge = ballot(wb + lane > f && (wb + lane >= N || (wk & KEYMASK) >= kv));
+                        if (ge == 0 && wb + 64 < N && wb != f) {  // the run leaves the window: re-base it at f
+                            win_flush();
+                            win_load(f);
+                            ge = ballot(wb + lane > f && (wb + lane >= N || (wk & KEYMASK) >= kv));
+                        }
+                        const int fl = f - wb, q = wb + lane;
+                        const bool in_window = ge != 0 || wb + 64 >= N;
+                        const int el = ge ? __ffsll((unsigned long long)ge) - 1 : N - wb;  // run end e - wb
+                        if (el == fl + 1) {
+                            n_noinv++;
+                            done_here = true;  // key[f+1] >= key[f]: no inversion
+                        } else if (in_window) {
+                            bool fast = N <= 12;
+                            if (!fast && N >= 50) {
+                                fast = !is_pivot_sample(N, f);
+                                if (!fast) {
+                                    n_pivot++;
+                                    win_flush();
+                                    fast = choose_pivot_hint_wave(sl, N, lane) == 1;
+                                }
+                            }
+                            if (fast) {
+                                // stable move: [f, e-1) <- [f+1, e), e-1 <- the changed element (registers move along)
+                                const bool sh = lane >= fl && lane < el - 1, last = lane == el - 1;
+                                auto mv = [&](auto& x) {
+                                    using X = std::remove_reference_t<decltype(x)>;
+                                    const int xf = rl32((int)x, fl);
+                                    const int nx = __shfl_down((int)x, 1);
+                                    x = sh ? (X)nx : (last ? (X)xf : x);
+                                };
+                                mv(wk);
+                                mv(wo);
+                                mv(wm);
+                                mv(wcnt);
+#pragma unroll
+                                for (int ai = 0; ai < KP_LDS_AXES; ai++) mv(wh[ai]);
+                                {
+                                    int wai = wa ? 1 : 0;
+                                    mv(wai);
+                                    wa = wai != 0;
+                                }
+                                how = 1;
+                                n_winmove++;
+                                done_here = true;
+                            }
+                        }
+                    }
+                    if (!done_here) {
+                        n_ldssort++;
+                        if (dkind == 2) n_r2++;
+                        else if (wb < 0) n_rwb++;
+                        else if (!(dpos >= wb && dpos < wb + 64)) n_rout++;
+                        win_flush();
+                        how = sort_slice_after_change(sl, N, dkind, dpos, S.sstack, lane);
+                        wb = -1;
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    sfast += how == 1;
+                    sfull += how == 2;
+                    const long long c1 = prof_clock(d);
+                    csort += c1 - t_b;
+                    if (how == 2) csfull += c1 - t_b;
+                    // positions < dpos are untouched by a stable move of dpos and rejected this shape (when the
+                    // shape repeats); an append or a full pdqsort permutes everything
+                    if (dkind == 2 || how == 2 || sstart > dpos) sstart = 0;
+                    dkind = 0;
+                }
+                // first NodeClaim in slice order (from sstart) that has not rejected this shape
+                const long long t_c = prof_clock(d);
+                int f = N;
+                for (int pos = sstart; pos < N;) {
+                    if (wb < 0 || pos < wb || pos >= wb + 64) {
+                        win_flush();
+                        win_load(pos);
+                    }
+                    const int q = wb + lane;
+                    const uint64_t m = ballot(q >= pos && !(wk >> 31));  // positions >= N carry bit 31
                     if (m) {
-                        f = base + __ffsll((unsigned long long)m) - 1;
+                        f = wb + __ffsll((unsigned long long)m) - 1;
                         break;
                     }
+                    pos = wb + 64;
                 }
+                const long long t_d = prof_clock(d);
+                cqscan += t_d - t_c;
                 if (f < N) {
-                    const int nc = sord[f];
-                    if (nc < NQ && slast[nc] == (uint16_t)c) {
-                        bool ok = true;
-                        int64_t pq = 0;
-                        if (lane < A) {
-                            const int64_t pr = S.qw_req[off][my_axis];
-                            pq = (pr + ((1ll << my_shift) - 1)) >> my_shift;
-                            ok = pq <= (int64_t)shr[lane * NQ + nc];
+                    const int fl = f - wb;
+                    bool ok = wa;
+#pragma unroll
+                    for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                        if (ai < A) ok &= pq[ai] <= wh[ai];
+                    const uint64_t okm = ballot(ok);
+                    if ((okm >> fl) & 1ull) {
+                        // quick accept: NodeClaim.Add(pod) succeeds with state (requirements, options) unchanged.
+                        // Batch: the next pods of the same shape go one each to the following NodeClaims of the run of
+                        // equal len(Pods) starting at f (each placement moves the NodeClaim at f to the end of the run,
+                        // so pod i meets the run's i-th element at f), as long as each of them quick-accepts, each move
+                        // is pdqsort's stable move (no choosePivot sample at f), and the run ends inside the window.
+                        const uint32_t kk = (uint32_t)rl32((int)wk, fl);  // len(Pods) at f, rejected bit clear
+                        int m = 1;
+                        const bool movable = N <= 12 || (N >= 50 && !is_pivot_sample(N, f));
+                        uint64_t ge = ballot(wb + lane > f && (wb + lane >= N || (wk & KEYMASK) > kk));
+                        uint64_t okm2 = okm;
+                        int fl2 = fl;
+                        if (movable && ge == 0 && fl > 0 && qw_used < qw_n) {
+                            // the run leaves the window: re-base the window at f to batch over up to 64 of its elements
+                            win_flush();
+                            win_load(f);
+                            bool ok2 = wa;
+#pragma unroll
+                            for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                                if (ai < A) ok2 &= pq[ai] <= wh[ai];
+                            okm2 = ballot(ok2);
+                            fl2 = 0;
+                            ge = ballot(wb + lane > f && (wb + lane >= N || (wk & KEYMASK) > kk));
                         }
-                        if (ballot(!ok) == 0) {
-                            // quick accept: NodeClaim.Add(pod) succeeds with state (requirements, options) unchanged
-                            if (lane < A) shr[lane * NQ + nc] -= (int32_t)pq;
-                            if (lane < R) {
-                                const int64_t pr = S.qw_req[off][lane];
-                                if (pr) atomicAdd((unsigned long long*)&d.nc_req[(size_t)nc * R + lane], (unsigned long long)pr);
+                        const int fl = fl2;
+                        const uint64_t okm = okm2;
+                        const int el = ge ? __ffsll((unsigned long long)ge) - 1 : 64;  // run end (lane), 64: beyond window
+                        if (movable && qw_used < qw_n && (el < 64 || fl == 0)) {
+                            // same-shape pods queued right after this one (lastLen termination checked per pod)
+                            const int q0 = qcount + 1;  // len(queue) when this pod was popped
+                            const uint64_t sm = ballot(lane >= off && lane < qw_n && vshape == shape &&
+                                                       vlast != q0 - (lane - off));
+                            const int np = __builtin_ctzll(~(sm >> off));
+                            // run elements from f on that are not rejected and quick-accept
+                            const uint64_t tm = okm & ~ballot((wk >> 31) != 0) & (ge ? (ge - 1) : ~0ull);
+                            const int nt = __builtin_ctzll(~(tm >> fl));
+                            m = np < nt ? np : nt;
+                            if (m > 64) m = 64;
+                        }
+                        // lanes fl .. fl+m-1 take pods off .. off+m-1
+                        const int pi = lane - fl;
+                        const bool tgt = pi >= 0 && pi < m;
+                        const int podl = __shfl(vp, (off + (pi < 0 ? 0 : pi)) & 63);
+                        if (tgt) {
+#pragma unroll
+                            for (int ai = 0; ai < KP_LDS_AXES; ai++) wh[ai] -= pq[ai];
+                            wk += 1;
+                            wcnt += 1;
+                            d.pod_result[podl] = (int)wo;
+                            d.pod_order[podl] = seq + pi;
+                        }
+                        if (m > 1 && el == 64) {
+                            // the run [f, e) continues past the window: write the window back, then permute in LDS:
+                            // [f, e) becomes elem_{m-1}, elem_m .. elem_{L-1}, elem_{m-2} .. elem_0
+                            const uint32_t mk = wk, mo = wo;  // lanes < m: the placed elements (keys incremented)
+                            win_flush();
+                            int e = N;
+                            for (int base = f + 64; base < N; base += 64) {
+                                const int qq = base + lane;
+                                const uint64_t gm = ballot(qq >= N || (skey[qq < N ? qq : 0] & KEYMASK) > kk);
+                                if (gm) {
+                                    e = base + __ffsll((unsigned long long)gm) - 1;
+                                    break;
+                                }
                             }
-                            if (lane == 0) {
-                                skey[f]++;
-                                d.pod_result[p] = nc;
-                                d.pod_order[p] = seq;
+                            if (e > N) e = N;
+                            // [f+m, e) -> [f+1, e-m+1), ascending chunks (each chunk is read before it is overwritten)
+                            for (int base = f + m; base < e; base += 64) {
+                                const int qq = base + lane;
+                                uint32_t kx = 0;
+                                uint16_t ox = 0;
+                                if (qq < e) {
+                                    kx = skey[qq];
+                                    ox = sord[qq];
+                                }
+                                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                                if (qq < e) {
+                                    skey[qq - (m - 1)] = kx;
+                                    sord[qq - (m - 1)] = ox;
+                                }
+                                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                             }
-                            seq++;
-                            dkind = 1;
-                            dpos = f;
-                            nquick++;
+                            if (lane == m - 1) {
+                                skey[f] = mk;
+                                sord[f] = (uint16_t)mo;
+                            } else if (lane < m - 1) {
+                                skey[e - 1 - lane] = mk;
+                                sord[e - 1 - lane] = (uint16_t)mo;
+                            }
                             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                            continue;
+                            wb = -1;
+                            sfast += m - 1;
+                            n_winmove += m - 1;
+                            qw_used += m - 1;
+                            qhead += m - 1;
+                            if (qhead >= P) qhead -= P;
+                            qcount -= m - 1;
+                            popped += m - 1;
+                            scanned += (long long)N * (m - 1);
+                        } else if (m > 1) {
+                            // apply the m-1 completed stable moves: [f, e) becomes
+                            // elem_{m-1}, elem_m .. elem_{L-1}, elem_{m-2} .. elem_0   (elem_{m-1}'s move is pending)
+                            int src = lane;
+                            if (lane >= fl && lane < el) {
+                                if (lane == fl) src = fl + m - 1;
+                                else if (lane <= el - m) src = lane + m - 1;
+                                else src = fl + el - 1 - lane;
+                            }
+                            wk = (uint32_t)__shfl((int)wk, src);
+                            wo = (uint32_t)__shfl((int)wo, src);
+                            wm = (uint32_t)__shfl((int)wm, src);
+                            wcnt = __shfl(wcnt, src);
+#pragma unroll
+                            for (int ai = 0; ai < KP_LDS_AXES; ai++) wh[ai] = __shfl(wh[ai], src);
+                            wa = __shfl(wa ? 1 : 0, src) != 0;
+                            sfast += m - 1;
+                            n_winmove += m - 1;
+                            qw_used += m - 1;
+                            qhead += m - 1;
+                            if (qhead >= P) qhead -= P;
+                            qcount -= m - 1;
+                            popped += m - 1;
+                            scanned += (long long)N * (m - 1);
                         }
+                        seq += m;
+                        dkind = 1;
+                        dpos = f;
+                        sstart = f;
+                        nquick += m;
+                        n_batch++;
+                        const long long t_e = prof_clock(d);
+                        cqcheck += t_e - t_d;
+                        continue;
                     }
                 }
                 // slow path: the whole block evaluates this pod
+                win_flush();
+                wb = -1;
                 if (lane < R) S.pod_req[lane] = S.qw_req[off][lane];
                 if (lane == 0) {
                     S.cur_pod = p;
-                    S.cur_cls = c;
-                    S.cur_shape = shape;
                     S.cls_fill = S.CC.cls != c;  // decided before the barrier: fill_class_cache rewrites CC.cls
                 }
-                collect_candidates(S, sord, N, f, 0, lane);
+                collect_candidates(S, skey, sord, N, f, 0, lane);
                 break;
             }
+            win_flush();
             if (lane == 0) {
                 S.qhead = qhead;
                 S.qcount = qcount;
-                S.qw_n = qw_n;
-                S.qw_used = qw_used;
                 S.seq = seq;
                 S.prev_shape = prev_shape;
                 S.dirty_kind = dkind;
                 S.dirty_pos = dpos;
+                S.scan_start = sstart;
+                S.any_rej = any_rej;
                 S.done = done;
                 S.err = err;
+                S.cur_cls = c;
+                S.cur_tol = tl;
                 S.st[ST_POPPED] = popped;
                 S.st[ST_NC_SCANNED] += scanned;
                 S.st[ST_QUICK] += nquick;
@@ -384,9 +667,30 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                 S.st[ST_SORT_FAST] += sfast;
                 S.st[ST_SORT_FULL] += sfull;
                 S.st[ST_CYC_SORT] += csort;
+                S.st[ST_CYC_SORT_FULL] += csfull;
+                S.st[ST_CYC_QPOP] += cqpop;
+                S.st[ST_CYC_QSCAN] += cqscan;
+                S.st[ST_CYC_QCHECK] += cqcheck;
+                S.st[ST_CYC_QCOMMIT] += cqcommit;
+                S.st[ST_N_NOINV] += n_noinv;
+                S.st[ST_N_WINMOVE] += n_winmove;
+                S.st[ST_N_LDSSORT] += n_ldssort;
+                S.st[ST_N_PIVOT] += n_pivot;
+                S.st[ST_N_WINLOAD] += n_winload;
+                S.st[ST_N_FLUSH] += n_flush;
+                S.st[ST_N_SHAPE] += n_shape;
+                S.st[ST_N_SHAPE + 1] += n_r2;
+                S.st[ST_N_SHAPE + 2] += n_rwb;
+                S.st[ST_N_SHAPE + 3] += n_rout;
+                S.st[ST_N_SHAPE + 4] += n_batch;
                 S.st[ST_CYC_POP] += prof_clock(d) - c_in;
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // quick-path atomics have reached L2
+            if (lane < KP_LDS_AXES) {
+#pragma unroll
+                for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                    if (lane == ai) S.cur_pq[ai] = pq[ai];
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // flushed request totals have reached L2
         }
         __syncthreads();
         if (S.done) break;
@@ -410,13 +714,17 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                 a.compat = true;
                 a.force_off = false;
                 a.prof = d.profile ? &S.st[ST_EV_REQ] : nullptr;
-                const bool fast = slast[nc] == (uint16_t)S.cur_cls;
+                const bool fast = slast[nc] == (uint16_t)S.cur_cls ||
+                                  ((S.CC.flags & 4u) && ((S.CC.tol >> a.tmpl) & 1u));
                 const bool ok = fast ? eval_fits_only(d, E, a, S.ws[wave], lane) : eval_wave(d, E, S.CC, a, S.ws[wave], lane);
                 if (lane == 0) {
                     S.fastp[b][wave] = fast;
                     S.acc[b][wave] = ok;
-                    if (!ok) atomicOr(&S.rej[nc >> 5], 1u << (nc & 31));
-                    if (fast) S.st[ST_WITNESS_MISS]++;
+                    if (!ok) {
+                        skey[S.cand_pos[b][wave]] |= 0x80000000u;  // rejected this shape (positions are stable here)
+                        S.any_rej = 1;
+                    }
+                    if (fast) atomicAdd((unsigned long long*)&S.st[ST_WITNESS_MISS], 1ull);
                 }
             }
             __syncthreads();
@@ -428,7 +736,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                 }
             if (tid == 0) S.st[ST_NC_EVALS] += nc_;
             if (win >= 0 || S.scan_done[b]) break;
-            if (wave == 0) collect_candidates(S, sord, S.N, S.scan_next[b], b ^ 1, lane);
+            if (wave == 0) collect_candidates(S, skey, sord, S.N, S.scan_next[b], b ^ 1, lane);
             __syncthreads();
             round++;
         }
@@ -450,6 +758,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                     skey[pos]++;
                     S.dirty_kind = 1;
                     S.dirty_pos = pos;
+                    S.scan_start = pos;  // every position before the winner rejected this shape
                     d.pod_result[pod] = nc;
                     d.pod_order[pod] = S.seq++;
                 }
@@ -523,6 +832,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                         }
                         if (lane == 0) {
                             slast[n] = (uint16_t)S.cur_cls;
+                            stmpl[n] = (uint8_t)jj;
                             d.nc_tmpl[n] = jj;
                             sord[n] = (uint16_t)n;
                             skey[n] = 1;
@@ -554,7 +864,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
     // ---- outputs ----
     const int N = S.N;
     for (int i = tid; i < N; i += nthr) {
-        d.nc_npods[sord[i]] = (int32_t)skey[i];
+        d.nc_npods[sord[i]] = (int32_t)(skey[i] & KEYMASK);
         d.nc_slice_pos[sord[i]] = i;
     }
     if (tid == 0) {
@@ -724,6 +1034,8 @@ bool kp_ffd_plan_lds(KpDev& d, int max_bytes) {
     off = al(off + 2 * (size_t)ncmax);
     d.off_last = (int)off;
     off = al(off + 2 * (size_t)ncmax);
+    d.off_tmpl = (int)off;
+    off = al(off + (size_t)ncmax);
     const int tp = (d.T + 63) / 64 * 64;
     d.lds_tpad = tp;
     d.lds_nstage = d.n_active < KP_LDS_AXES ? d.n_active : KP_LDS_AXES;

@@ -91,7 +91,7 @@ struct KpDev {
     const int32_t* cls_wsoff;        // parallel to cls_keys: word offset of the key in the wave scratch
     const ReqHdr* cls_hdr;           // [C+NT][K]
     const uint64_t* cls_words;       // [C+NT][DW]
-    const uint32_t* cls_flags;       // [C+NT] bit0: defines an offering key, bit1: has minValues
+    const uint32_t* cls_flags;       // [C+NT] bit0: defines an offering key, bit1: has minValues, bit2: no keys
     uint64_t* V;                     // [C+NT][TW] per-class single-valued label compatibility (class_mask kernel)
 
     // ---------------- templates ----------------
@@ -148,7 +148,7 @@ struct KpDev {
     int32_t lds_nstage;              // allocatable axes staged in LDS
     int32_t lds_A;                   // quick-accept axes (= n_active when n_active <= KP_LDS_AXES, else 0)
     int32_t lds_nq;                  // NodeClaims with a quick-accept headroom row (ids < lds_nq)
-    int32_t off_key, off_ord, off_last, off_alloc, off_avail, off_multi, off_hr;
+    int32_t off_key, off_ord, off_last, off_tmpl, off_alloc, off_avail, off_multi, off_hr;
     int32_t lds_bytes;
     int32_t qshift[KP_LDS_AXES];     // headroom scale per quick axis: value >> qshift fits 30 bits
 };
@@ -158,5 +158,6 @@ enum {
     ST_POPPED = 0, ST_NC_EVALS, ST_NC_SCANNED, ST_TMPL_EVALS, ST_EXIST_EVALS, ST_SORT_FAST, ST_SORT_FULL,
     ST_MEMO_SKIPS, ST_CYC_POP, ST_CYC_SORT, ST_CYC_SCAN, ST_CYC_TMPL, ST_CYC_COMMIT, ST_CYC_SORT_FULL,
     ST_EV_REQ = 16, ST_EV_MASK, ST_EV_OFF, ST_EV_TYPES, ST_EV_MIN, ST_EV_CALLS,
-    ST_QUICK = 24, ST_SLOW, ST_WITNESS_MISS, ST_COUNT = 32
+    ST_QUICK = 24, ST_SLOW, ST_WITNESS_MISS, ST_CYC_QPOP, ST_CYC_QSCAN, ST_CYC_QCHECK, ST_CYC_QCOMMIT,
+    ST_N_NOINV = 32, ST_N_WINMOVE, ST_N_LDSSORT, ST_N_PIVOT, ST_N_WINLOAD, ST_N_FLUSH, ST_N_SHAPE, ST_COUNT = 48
 };
