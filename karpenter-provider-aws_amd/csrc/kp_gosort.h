@@ -265,8 +265,10 @@ __device__ inline void pdqsort_full(D& d, int n, int* stk) {
     push(0, n, go_bits_len((unsigned)n), 1, 1);
     while (sp > 0) {
         sp--;
-        int a = stk[sp * 5 + 0], b = stk[sp * 5 + 1], limit = stk[sp * 5 + 2];
-        bool wasBalanced = stk[sp * 5 + 3], wasPartitioned = stk[sp * 5 + 4];
+        int a = __builtin_amdgcn_readfirstlane(stk[sp * 5 + 0]), b = __builtin_amdgcn_readfirstlane(stk[sp * 5 + 1]);
+        int limit = __builtin_amdgcn_readfirstlane(stk[sp * 5 + 2]);
+        bool wasBalanced = __builtin_amdgcn_readfirstlane(stk[sp * 5 + 3]) != 0;
+        bool wasPartitioned = __builtin_amdgcn_readfirstlane(stk[sp * 5 + 4]) != 0;
         for (;;) {
             const int length = b - a;
             if (length <= 12) {
@@ -382,6 +384,204 @@ __device__ inline void wave_rotate_right(SortSlice& d, int q, int n, int lane) {
     }
 }
 
+// The slice in LDS driven by the whole wave: control flow is wave-uniform (keys are read with readfirstlane), the
+// O(n) scans of partition / partitionEqual / partialInsertionSort become 64-wide ballot searches, and swaps are
+// written by lane 0.  Same comparison outcomes and swap sequence as Go, hence the same permutation.
+struct WaveLds {
+    uint32_t* key;
+    uint16_t* ord;
+    int lane;
+    __device__ __forceinline__ uint32_t k(int i) const { return (uint32_t)__builtin_amdgcn_readfirstlane((int)key[i]) & KEYMASK; }
+    __device__ __forceinline__ bool less(int i, int j) const { return k(i) < k(j); }
+    __device__ __forceinline__ void swap(int i, int j) {
+        const uint32_t ki = key[i], kj = key[j];
+        const uint16_t oi = ord[i], oj = ord[j];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (lane == 0) {
+            key[i] = kj;
+            key[j] = ki;
+            ord[i] = oj;
+            ord[j] = oi;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    // first q in [lo, hi] with pred(masked key[q]) (hi + 1 if none)
+    template <class F>
+    __device__ __forceinline__ int find_first(int lo, int hi, F pred) const {
+        for (int base = lo; base <= hi; base += 64) {
+            const int q = base + lane;
+            const uint64_t m = __ballot(q <= hi && pred(key[q] & KEYMASK));
+            if (m) return base + __ffsll((unsigned long long)m) - 1;
+        }
+        return hi + 1;
+    }
+    // last q in [lo, hi] with pred(masked key[q]) (lo - 1 if none)
+    template <class F>
+    __device__ __forceinline__ int find_last(int lo, int hi, F pred) const {
+        for (int top = hi; top >= lo; top -= 64) {
+            const int q = top - lane;
+            const uint64_t m = __ballot(q >= lo && pred(key[q] & KEYMASK));
+            if (m) return top - (__ffsll((unsigned long long)m) - 1);
+        }
+        return lo - 1;
+    }
+    // [a, e): element a moves to e-1, the rest shift left by one
+    __device__ __forceinline__ void rotl(int a, int e) {
+        if (e - a < 2) return;
+        const uint32_t fk = key[a];
+        const uint16_t fo = ord[a];
+        for (int base = a; base < e - 1; base += 64) {
+            const int i = base + lane;
+            uint32_t kx = 0;
+            uint16_t ox = 0;
+            if (i < e - 1) {
+                kx = key[i + 1];
+                ox = ord[i + 1];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (i < e - 1) {
+                key[i] = kx;
+                ord[i] = ox;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
+        if (lane == 0) {
+            key[e - 1] = fk;
+            ord[e - 1] = fo;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    // [q, n): element n-1 moves to q, the rest shift right by one
+    __device__ __forceinline__ void rotr(int q, int n) {
+        if (n - q < 2) return;
+        const uint32_t lk = key[n - 1];
+        const uint16_t lo = ord[n - 1];
+        for (int top = n - 1; top > q; top -= 64) {
+            const int i = top - lane;
+            uint32_t kx = 0;
+            uint16_t ox = 0;
+            if (i > q) {
+                kx = key[i - 1];
+                ox = ord[i - 1];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (i > q) {
+                key[i] = kx;
+                ord[i] = ox;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
+        if (lane == 0) {
+            key[q] = lk;
+            ord[q] = lo;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+};
+
+// partition_func with wave scans
+__device__ inline int go_partition(WaveLds& d, int a, int b, int pivot, bool& already) {
+    d.swap(a, pivot);
+    const uint32_t pk = d.k(a);
+    int i = a + 1, j = b - 1;
+    i = d.find_first(i, j, [&](uint32_t x) { return !(x < pk); });  // while i <= j && less(data[i], data[a]) i++
+    j = d.find_last(i, j, [&](uint32_t x) { return x < pk; });      // while i <= j && !less(data[j], data[a]) j--
+    if (i > j) {
+        d.swap(j, a);
+        already = true;
+        return j;
+    }
+    d.swap(i, j);
+    i++;
+    j--;
+    for (;;) {
+        i = d.find_first(i, j, [&](uint32_t x) { return !(x < pk); });
+        j = d.find_last(i, j, [&](uint32_t x) { return x < pk; });
+        if (i > j) break;
+        d.swap(i, j);
+        i++;
+        j--;
+    }
+    d.swap(j, a);
+    already = false;
+    return j;
+}
+// partitionEqual_func with wave scans
+__device__ inline int go_partition_equal(WaveLds& d, int a, int b, int pivot) {
+    d.swap(a, pivot);
+    const uint32_t pk = d.k(a);
+    int i = a + 1, j = b - 1;
+    for (;;) {
+        i = d.find_first(i, j, [&](uint32_t x) { return pk < x; });   // while i <= j && !less(data[a], data[i]) i++
+        j = d.find_last(i, j, [&](uint32_t x) { return !(pk < x); }); // while i <= j && less(data[a], data[j]) j--
+        if (i > j) break;
+        d.swap(i, j);
+        i++;
+        j--;
+    }
+    return i;
+}
+// partialInsertionSort_func with wave scans; the two shift loops are single-element moves (rotations)
+__device__ inline bool go_partial_insertion_sort(WaveLds& d, int a, int b) {
+    int i = a + 1;
+    for (int j = 0; j < 5; j++) {
+        // while i < b && !less(data[i], data[i-1]) i++
+        {
+            int r = b;
+            for (int base = i; base < b; base += 64) {
+                const int q = base + d.lane;
+                const uint64_t m = __ballot(q < b && (d.key[q] & KEYMASK) < (d.key[q - 1] & KEYMASK));
+                if (m) {
+                    r = base + __ffsll((unsigned long long)m) - 1;
+                    break;
+                }
+            }
+            i = r;
+        }
+        if (i == b) return true;
+        if (b - a < 50) return false;
+        d.swap(i, i - 1);
+        if (i - a >= 2) {
+            // for k := i-1; k >= 1 && less(data[k], data[k-1]); k-- { swap(k, k-1) }: x = data[i-1] moves left past
+            // the larger keys before it (Go bounds this loop by 1, not a)
+            const uint32_t x = d.k(i - 1);
+            const int t = d.find_last(0, i - 2, [&](uint32_t y) { return !(x < y); });  // last position not > x
+            int dst = t + 1;
+            d.rotr(dst, i);
+        }
+        if (b - i >= 2) {
+            // for k := i+1; k < b && less(data[k], data[k-1]); k++ { swap(k, k-1) }: x = data[i] moves right past
+            // the smaller keys after it
+            const uint32_t x = d.k(i);
+            const int t = d.find_first(i + 1, b - 1, [&](uint32_t y) { return !(y < x); });
+            d.rotl(i, t);
+        }
+    }
+    return false;
+}
+__device__ inline void go_reverse_range(WaveLds& d, int a, int b) {
+    const int n = b - a, h = n / 2;
+    for (int base = 0; base < h; base += 64) {
+        const int i = base + d.lane;
+        uint32_t ki = 0, kj = 0;
+        uint16_t oi = 0, oj = 0;
+        if (i < h) {
+            ki = d.key[a + i];
+            kj = d.key[b - 1 - i];
+            oi = d.ord[a + i];
+            oj = d.ord[b - 1 - i];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (i < h) {
+            d.key[a + i] = kj;
+            d.key[b - 1 - i] = ki;
+            d.ord[a + i] = oj;
+            d.ord[b - 1 - i] = oi;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+}
+
 // Full pdqsort_func emulation: in registers for n <= 64, else on lane 0 over LDS.
 __device__ inline void pdqsort_any(SortSlice d, int n, int* stk, int lane) {
     if (n <= 64) {
@@ -396,7 +596,8 @@ __device__ inline void pdqsort_any(SortSlice d, int n, int* stk, int lane) {
         }
         return;
     }
-    if (lane == 0) pdqsort_full(d, n, stk);
+    WaveLds w{d.key, d.ord, lane};
+    pdqsort_full(w, n, stk);
 }
 
 // Is `pos` one of the positions choosePivot samples for a slice of length n >= 50 (l/4·{1,2,3} ± 1)?
