@@ -54,6 +54,60 @@ __device__ __forceinline__ int popc_words(const uint64_t* w, int n) {
     return c;
 }
 
+// Is Requirement.Intersection(A, B) empty (Len() == 0)?  Count-free form of req_intersect, single lane.
+__device__ inline bool req_intersect_empty(const KpDev& d, int k, const ReqHdr& A, const uint64_t* aw, const ReqHdr& B,
+                                           const uint64_t* bw) {
+    const bool ac = A.flags & RF_CMP, bc = B.flags & RF_CMP;
+    const bool hg = (A.flags | B.flags) & RF_GT, hl = (A.flags | B.flags) & RF_LT;
+    ReqHdr o;
+    o.flags = (hg ? RF_GT : 0u) | (hl ? RF_LT : 0u);
+    o.gt = 0;
+    o.lt = 0;
+    o.minv = 0;
+    if (hg) o.gt = ((A.flags & RF_GT) && (B.flags & RF_GT)) ? (A.gt > B.gt ? A.gt : B.gt) : ((A.flags & RF_GT) ? A.gt : B.gt);
+    if (hl) o.lt = ((A.flags & RF_LT) && (B.flags & RF_LT)) ? (A.lt < B.lt ? A.lt : B.lt) : ((A.flags & RF_LT) ? A.lt : B.lt);
+    if (hg && hl && o.gt >= o.lt) return true;  // DoesNotExist
+    if (ac && bc) return false;                 // complement: Len = MaxInt64 - |values|
+    const int n = d.nw[k];
+    for (int i = 0; i < n; i++) {
+        uint64_t x;
+        if (ac) x = bw[i] & ~aw[i];
+        else if (bc) x = aw[i] & ~bw[i];
+        else x = aw[i] & bw[i];
+        if (hg || hl) {
+            uint64_t y = x;
+            while (y) {
+                const int jb = __ffsll((unsigned long long)y) - 1;
+                y &= y - 1;
+                if (!within(d, k, i * 64 + jb, o)) x &= ~(1ull << jb);
+            }
+        }
+        if (x) return false;
+    }
+    return true;
+}
+
+// Requirements.Compatible(node, podRequirements) with no undefined-label allowance (ExistingNode.Add), single lane:
+// every key of pod class c must be defined on the node unless its operator is NotIn/DoesNotExist, and the
+// intersection must be non-empty unless both operators are NotIn/DoesNotExist.
+__device__ inline bool node_compatible(const KpDev& d, const ReqHdr* nh, const uint64_t* nwords, int c) {
+    for (int i = d.cls_xkoff[c]; i < d.cls_xkoff[c + 1]; i++) {
+        const int k = d.cls_xkeys[i];
+        const ReqHdr B = d.cls_hdr[(size_t)c * d.K + k];
+        const uint64_t* bw = d.cls_words + (size_t)c * d.DW + d.woff[k];
+        const bool bno = op_notin_or_dne(req_op(B.flags, popc_words(bw, d.nw[k])));
+        const ReqHdr A = nh[k];
+        if (!(A.flags & RF_DEF)) {
+            if (!bno) return false;
+            continue;
+        }
+        const uint64_t* aw = nwords + d.woff[k];
+        if (req_intersect_empty(d, k, A, aw, B, bw) && !(bno && op_notin_or_dne(req_op(A.flags, popc_words(aw, d.nw[k])))))
+            return false;
+    }
+    return true;
+}
+
 // O = A ∩ B (Requirement.Intersection), single lane.  Returns |O.values|.
 __device__ inline int req_intersect(const KpDev& d, int k, const ReqHdr& A, const uint64_t* aw, const ReqHdr& B,
                                     const uint64_t* bw, ReqHdr& O, uint64_t* ow) {
@@ -112,4 +166,26 @@ __device__ inline int req_intersect(const KpDev& d, int k, const ReqHdr& A, cons
     }
     O = o;
     return cnt;
+}
+
+// Node requirement A = B ∩ A in place (Requirements.Add of one pod requirement), single lane.  Returns whether A changed.
+__device__ inline bool req_merge_inplace(const KpDev& d, int k, ReqHdr& A, uint64_t* aw, const ReqHdr& B,
+                                         const uint64_t* bw) {
+    const int n = d.nw[k];
+    if (!(A.flags & RF_DEF)) {
+        A = B;
+        for (int i = 0; i < n; i++) aw[i] = bw[i];
+        return true;
+    }
+    ReqHdr O;
+    uint64_t tmp[KP_MAX_SCR_WORDS];
+    const int nn = n < KP_MAX_SCR_WORDS ? n : KP_MAX_SCR_WORDS;
+    req_intersect(d, k, B, bw, A, aw, O, tmp);
+    bool ch = O.flags != A.flags || O.minv != A.minv || O.gt != A.gt || O.lt != A.lt;
+    for (int i = 0; i < nn; i++) {
+        ch |= tmp[i] != aw[i];
+        aw[i] = tmp[i];
+    }
+    A = O;
+    return ch;
 }

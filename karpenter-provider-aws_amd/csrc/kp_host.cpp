@@ -23,6 +23,7 @@ size_t kp_ffd_shared_bytes();
 bool kp_ffd_plan_lds(KpDev& d, int max_bytes);
 hipError_t kp_launch_class_mask(const KpDev& d, hipStream_t s);
 hipError_t kp_launch_template_init(const KpDev& d, hipStream_t s);
+hipError_t kp_launch_existing(const KpDev& d, hipStream_t s);
 hipError_t kp_launch_ffd(const KpDev& d, hipStream_t s);
 hipError_t kp_launch_finalize(const KpDev& d, int n_nodeclaims, hipStream_t s);
 hipError_t kp_queue_sort(const int64_t* fields, int n, int32_t* perm_a, int32_t* perm_b, uint64_t* keys_a,
@@ -206,6 +207,11 @@ struct kp_ctx {
     std::vector<int> tmpl_np;                // template → input nodepool index
     std::vector<int64_t> h_remaining;        // NodePool limits at solve start (re-applied by every execute)
     DBuf<uint32_t> d_kflags, d_cls_flags, d_tol;
+    DBuf<ReqHdr> d_ex_hdr0, d_ex_hdr;
+    DBuf<uint64_t> d_ex_words0, d_ex_words, d_ex_tol, d_XT;
+    DBuf<int64_t> d_ex_avail, d_ex_req, d_ex_head;
+    DBuf<uint8_t> d_ex_static;
+    DBuf<int32_t> d_cls_xkoff, d_cls_xkeys;
     DBuf<int32_t> d_kcat, d_kmulti, d_woff, d_nw, d_nval, d_vbase, d_cls_koff, d_cls_keys, d_cls_wsoff, d_min_keys;
     DBuf<uint8_t> d_val_isint, d_limit_set;
     DBuf<int64_t> d_val_int, d_daemon, d_remaining, d_pod_req, d_sort_fields, d_nc_req, d_stats;
@@ -656,7 +662,6 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     c->prepared = c->executed = false;
     if (in->min_values_policy != KP_MIN_VALUES_STRICT)
         return fail(ctx, KP_E_UNSUPPORTED, "MIN_VALUES_POLICY=BestEffort is not supported by this build");
-    if (in->n_existing > 0) return fail(ctx, KP_E_UNSUPPORTED, "existing nodes are not supported by this build");
     const int T = c->T, TW = c->TW, R = c->R, P = in->pods.n_pods, C = in->n_classes;
     // ---- dictionaries: catalog ∪ solve strings ----
     c->sol = c->cat;
@@ -682,6 +687,22 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     for (int i = 0; i < C; i++)
         for (auto& kv : creq[i])
             if (kv.second.has_min) return fail(ctx, KP_E_INVALID, "pod requirements cannot carry minValues");
+    // existing nodes (ExistingNode, [core] scheduling/existingnode.go NewExistingNode): requirements =
+    // NewLabelRequirements(node labels) + hostname In [name].  Only label keys some pod class constrains can
+    // influence Compatible (it iterates the pod's keys), so only those are interned.
+    const int E = in->n_existing;
+    const int hostname_key = c->sol.find_key("kubernetes.io/hostname");
+    std::vector<std::vector<std::pair<int, int>>> exlab(E);  // (key, value id) per node
+    for (int j = 0; j < E; j++) {
+        const kp_existing_node& en = in->existing[j];
+        if (!en.available) return fail(ctx, KP_E_INVALID, "existing node without available resources");
+        for (int l = 0; l < en.n_labels; l++) {
+            const int k = c->sol.find_key(normalize(en.label_keys[l]));
+            if (k < 0 || k == hostname_key) continue;
+            exlab[j].push_back({k, c->sol.keys[k].id(en.label_values[l] ? en.label_values[l] : "")});
+        }
+        if (hostname_key >= 0) exlab[j].push_back({hostname_key, c->sol.keys[hostname_key].id(en.name ? en.name : "")});
+    }
     const int K = (int)c->sol.keys.size();
     if (K > KP_MAX_KEYS) return fail(ctx, KP_E_UNSUPPORTED, "too many label keys");
     // ---- key layout ----
@@ -718,8 +739,11 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     std::vector<int32_t> koff(CT + 1, 0), ckeys, cwsoff;
     std::vector<uint32_t> cflags(CT, 0);
     std::vector<int32_t> min_keys((size_t)NT * KP_MAX_CLASS_KEYS, -1);
+    std::vector<int32_t> xkoff(C + 1, 0), xkeys;
+    std::vector<uint8_t> hblock(std::max(C, 1), 0);
+    bool mayfix = false;
     auto encode = [&](int row, const std::map<int, HReq>& rq) -> bool {
-        int so = 0;
+        int so = 0, nk = 0;
         for (auto& kv : rq) {
             const HReq& q = kv.second;
             ReqHdr h{};
@@ -730,6 +754,17 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
             h.lt = q.lt;
             chdr[(size_t)row * K + q.key] = h;
             for (int vv : q.vals) cwords[(size_t)row * DW + woff[q.key] + vv / 64] |= 1ull << (vv % 64);
+            if (row < C) {
+                xkeys.push_back(q.key);
+                if ((q.complement && !q.vals.empty()) || (!q.complement && q.vals.empty())) mayfix = true;  // NotIn / DNE
+                if (q.key == hostname_key) {
+                    // every new NodeClaim carries hostname In [a fresh placeholder]: only NotIn / Exists (no bounds)
+                    // intersect it; the merged value stays the placeholder and is dropped at FinalizeScheduling
+                    if (!(q.complement && !q.has_gt && !q.has_lt)) hblock[row] = 1;
+                    continue;
+                }
+            }
+            nk++;
             ckeys.push_back(q.key);
             cwsoff.push_back(so);
             so += nw[q.key];
@@ -737,9 +772,10 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
                 q.key == c->key_resvtype)
                 cflags[row] |= 1u;
         }
-        if (rq.empty()) cflags[row] |= 4u;  // no requirement keys: NodeClaim.Add = tolerations + Fits (+ minValues)
-        if ((int)rq.size() > KP_MAX_CLASS_KEYS || so > KP_MAX_SCR_WORDS) return false;
+        if (nk == 0) cflags[row] |= 4u;  // no requirement keys: NodeClaim.Add = tolerations + Fits (+ minValues)
+        if (nk > KP_MAX_CLASS_KEYS || so > KP_MAX_SCR_WORDS) return false;
         koff[row + 1] = (int)ckeys.size();
+        if (row < C) xkoff[row + 1] = (int)xkeys.size();
         return true;
     };
     for (int i = 0; i < C; i++)
@@ -779,6 +815,32 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
                 if (t < 0 || t >= T) return fail(ctx, KP_E_INVALID, "nodepool type_index out of range");
                 rows[(size_t)j * TW + t / 64] |= 1ull << (t % 64);
             }
+        }
+    }
+    for (int i = 0; i < C; i++)
+        if (hblock[i]) tol[i] = 0;  // hostname requirement no new or in-flight NodeClaim can satisfy
+    // ---- existing nodes: digests, tolerations ----
+    const int EW = (E + 63) / 64;
+    std::vector<ReqHdr> exhdr((size_t)std::max(E, 1) * K);
+    memset(exhdr.data(), 0, exhdr.size() * sizeof(ReqHdr));
+    std::vector<uint64_t> exw((size_t)std::max(E, 1) * DW, 0), extol((size_t)std::max(C, 1) * std::max(EW, 1), 0);
+    std::vector<int64_t> exav((size_t)std::max(E, 1) * R, 0), exrq((size_t)std::max(E, 1) * R, 0);
+    for (int j = 0; j < E; j++) {
+        const kp_existing_node& en = in->existing[j];
+        for (auto& kv : exlab[j]) {
+            ReqHdr& h = exhdr[(size_t)j * K + kv.first];
+            h.flags = RF_DEF;
+            exw[(size_t)j * DW + woff[kv.first] + kv.second / 64] |= 1ull << (kv.second % 64);
+        }
+        for (int r = 0; r < R; r++) {
+            exav[(size_t)j * R + r] = en.available[r];
+            exrq[(size_t)j * R + r] = en.requests ? en.requests[r] : 0;
+        }
+        for (int i = 0; i < C; i++) {
+            bool all = true;
+            for (int q = 0; q < en.n_taints && all; q++)
+                all = tolerates(en.taints[q], in->classes[i].tolerations, in->classes[i].n_tolerations);
+            if (all) extol[(size_t)i * EW + j / 64] |= 1ull << (j % 64);
         }
     }
     // ---- pods ----
@@ -886,6 +948,19 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     HIPCHK(c->d_remaining.upload(remaining, s));
     c->h_remaining = remaining;
     HIPCHK(c->d_min_keys.upload(min_keys, s));
+    if (xkeys.empty()) xkeys.push_back(0);
+    HIPCHK(c->d_cls_xkoff.upload(xkoff, s));
+    HIPCHK(c->d_cls_xkeys.upload(xkeys, s));
+    HIPCHK(c->d_ex_hdr0.upload(exhdr, s));
+    HIPCHK(c->d_ex_words0.upload(exw, s));
+    HIPCHK(c->d_ex_hdr.ensure(exhdr.size()));
+    HIPCHK(c->d_ex_words.ensure(exw.size()));
+    HIPCHK(c->d_ex_avail.upload(exav, s));
+    HIPCHK(c->d_ex_req.upload(exrq, s));
+    HIPCHK(c->d_ex_head.ensure((size_t)KP_MAX_R * std::max(E, 1)));
+    HIPCHK(c->d_ex_static.ensure(std::max(E, 1)));
+    HIPCHK(c->d_ex_tol.upload(extol, s));
+    HIPCHK(c->d_XT.ensure(extol.size()));
     HIPCHK(c->d_pod_cls.upload(pcls, s));
     HIPCHK(c->d_pod_shape.upload(pshape, s));
     HIPCHK(c->d_pod_req.upload(preq, s));
@@ -974,6 +1049,21 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.limit_set = c->d_limit_set.p;
     d.remaining = c->d_remaining.p;
     d.min_keys = c->d_min_keys.p;
+    d.E = E;
+    d.EW = EW;
+    d.ex_hdr0 = c->d_ex_hdr0.p;
+    d.ex_words0 = c->d_ex_words0.p;
+    d.ex_hdr = c->d_ex_hdr.p;
+    d.ex_words = c->d_ex_words.p;
+    d.ex_avail = c->d_ex_avail.p;
+    d.ex_req = c->d_ex_req.p;
+    d.ex_head = c->d_ex_head.p;
+    d.ex_static = c->d_ex_static.p;
+    d.XT = c->d_XT.p;
+    d.ex_tol = c->d_ex_tol.p;
+    d.cls_xkoff = c->d_cls_xkoff.p;
+    d.cls_xkeys = c->d_cls_xkeys.p;
+    d.ex_mayfix = mayfix ? 1 : 0;
     d.P = P;
     d.pod_cls = c->d_pod_cls.p;
     d.pod_shape = c->d_pod_shape.p;
@@ -1056,6 +1146,7 @@ extern "C" kp_status kp_solve_execute(kp_ctx* ctx) {
     HIPCHK(kp_launch_class_mask(d, s));
     HIPCHK(hipEventRecord(c->ev[2], s));
     HIPCHK(kp_launch_template_init(d, s));
+    HIPCHK(kp_launch_existing(d, s));
     HIPCHK(hipEventRecord(c->ev[3], s));
     HIPCHK(kp_launch_ffd(d, s));
     HIPCHK(hipEventRecord(c->ev[4], s));
@@ -1118,7 +1209,7 @@ extern "C" kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out) {
     so.nodeclaim_evals = st[ST_NC_EVALS];
     so.nodeclaim_candidates_scanned = st[ST_NC_SCANNED];
     so.template_evals = st[ST_TMPL_EVALS];
-    so.existing_evals = st[ST_EXIST_EVALS];
+    so.existing_evals = st[ST_EXIST_PLACED];
     so.sorts_fast = st[ST_SORT_FAST];
     so.sorts_full = st[ST_SORT_FULL];
     for (int i = 0; i < 6; i++) c->cycles[i] = st[ST_CYC_POP + i];

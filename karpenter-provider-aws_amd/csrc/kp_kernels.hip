@@ -42,6 +42,64 @@ __global__ __launch_bounds__(64) void class_mask_kernel(KpDev d) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// existing nodes: working copies, headroom, static fit; then class × node Compatible ∧ tolerations (XT)
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void existing_init_kernel(KpDev d) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= d.E) return;
+    for (int k = 0; k < d.K; k++) d.ex_hdr[(size_t)j * d.K + k] = d.ex_hdr0[(size_t)j * d.K + k];
+    for (int i = 0; i < d.DW; i++) d.ex_words[(size_t)j * d.DW + i] = d.ex_words0[(size_t)j * d.DW + i];
+    // resources.Fits(requests + pod, available): any negative available fails; axes no pod requests are static
+    bool ok = true;
+    for (int r = 0; r < d.R; r++) {
+        const int64_t av = d.ex_avail[(size_t)j * d.R + r], rq = d.ex_req[(size_t)j * d.R + r];
+        bool act = false;
+        for (int ai = 0; ai < d.n_active; ai++) act |= d.active_axes[ai] == r;
+        if (av < 0 || (!act && rq > av)) ok = false;
+    }
+    d.ex_static[j] = ok ? 1 : 0;
+    for (int ai = 0; ai < d.n_active; ai++) {
+        const int r = d.active_axes[ai];
+        d.ex_head[(size_t)ai * d.E + j] = d.ex_avail[(size_t)j * d.R + r] - d.ex_req[(size_t)j * d.R + r];
+    }
+}
+
+// ExistingNode.Add's requirement merge of class c into node j (wave 0; only solves whose classes carry
+// NotIn/DoesNotExist keys).  When node j's requirements change, its XT column is recomputed for every class.
+__device__ inline void existing_merge(const KpDev& d, int j, int c, int lane) {
+    const int k0 = d.cls_xkoff[c], nk = d.cls_xkoff[c + 1] - k0;
+    ReqHdr* nh = d.ex_hdr + (size_t)j * d.K;
+    uint64_t* nwp = d.ex_words + (size_t)j * d.DW;
+    bool ch = false;
+    for (int i = lane; i < nk; i += 64) {
+        const int k = d.cls_xkeys[k0 + i];
+        ReqHdr A = nh[k];
+        ch |= req_merge_inplace(d, k, A, nwp + d.woff[k], d.cls_hdr[(size_t)c * d.K + k],
+                                d.cls_words + (size_t)c * d.DW + d.woff[k]);
+        nh[k] = A;
+    }
+    if (!ballot(ch)) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");  // the merged requirements are visible to every lane
+    const int w = j >> 6;
+    const uint64_t bm = 1ull << (j & 63);
+    for (int cc = lane; cc < d.C; cc += 64) {
+        const bool ok = d.ex_static[j] && (d.ex_tol[(size_t)cc * d.EW + w] & bm) && node_compatible(d, nh, nwp, cc);
+        if (ok) atomicOr((unsigned long long*)&d.XT[(size_t)cc * d.EW + w], (unsigned long long)bm);
+        else atomicAnd((unsigned long long*)&d.XT[(size_t)cc * d.EW + w], (unsigned long long)~bm);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__global__ __launch_bounds__(64) void existing_mask_kernel(KpDev d) {
+    const int w = blockIdx.x, c = blockIdx.y, lane = threadIdx.x, j = w * 64 + lane;
+    bool bit = j < d.E && d.ex_static[j] && ((d.ex_tol[(size_t)c * d.EW + w] >> lane) & 1ull);
+    if (bit) bit = node_compatible(d, d.ex_hdr0 + (size_t)j * d.K, d.ex_words0 + (size_t)j * d.DW, c);
+    const uint64_t m = ballot(bit);
+    if (lane == 0) d.XT[(size_t)c * d.EW + w] = m;
+}
+
+// ------------------------------------------------------------------------------------------------
 // NodeClaimTemplate.InstanceTypeOptions (NewScheduler): one wave per template
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void template_init_kernel(KpDev d) {
@@ -104,6 +162,7 @@ struct FfdShared {
     // control state: owned by wave 0 inside its fast loop, by the block between the slow-path barriers
     int N, qhead, qcount, done, cur_pod, cur_cls, cur_shape, prev_shape;
     int dirty_kind, dirty_pos, seq, err, cls_fill, scan_start, any_rej;
+    int xstart;                    // every existing node < xstart has rejected the current shape
     uint32_t cur_tol;              // tolerations word of the current shape's class (bit 31: no requirement keys)
     int32_t cur_pq[KP_LDS_AXES];   // scaled quick-accept requests of the current shape
     int64_t shape_req[KP_MAX_R];   // requests of the current shape (pending-total flush)
@@ -218,6 +277,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
         S.dirty_pos = 0;
         S.scan_start = 0;
         S.any_rej = 0;
+        S.xstart = 0;
         S.seq = 0;
         S.err = 0;
         S.CC.cls = -1;
@@ -273,6 +333,23 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
             int seq = S.seq, prev_shape = S.prev_shape, dkind = S.dirty_kind, dpos = S.dirty_pos;
             int sstart = S.scan_start;  // every slice position < sstart has rejected the current shape
             int any_rej = S.any_rej;
+            int xstart = S.xstart;
+            long long nexist = 0;
+            // pods of the current shape placed on existing node xj whose headroom update is still pending (flushed
+            // when xj changes; xj is never scanned again within the shape: positions < xstart are skipped)
+            int xj = -1, xcnt = 0;
+            auto ex_flush = [&]() {
+                if (xj >= 0 && xcnt && lane < d.n_active) {
+                    int r = 0;
+#pragma unroll
+                    for (int ai = 0; ai < KP_MAX_R; ai++)
+                        if (ai == lane) r = d.active_axes[ai];
+                    const int64_t x = S.shape_req[r];
+                    if (x) atomicAdd((unsigned long long*)&d.ex_head[(size_t)lane * d.E + xj], (unsigned long long)(-x * xcnt));
+                }
+                xj = -1;
+                xcnt = 0;
+            };
             int done = 0, err = S.err;
             int c = S.cur_cls;
             uint32_t tl = S.cur_tol;
@@ -379,6 +456,9 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                 popped++;
                 if (shape != prev_shape) {
                     n_shape++;
+                    ex_flush();
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nodes are scanned again from 0
+                    xstart = 0;
                     win_flush();  // pending totals belong to the previous shape
                     if (any_rej) {
                         for (int i = lane; i < N; i += 64) skey[i] &= KEYMASK;
@@ -394,6 +474,48 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                     sstart = 0;
                     prev_shape = shape;
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                }
+                // ExistingNode.Add on the existing nodes in order, before sort.Slice (no re-sort when one accepts)
+                if (d.E > 0 && xstart < d.E) {
+                    int jf = -1;
+                    for (int base = xstart; base < d.E; base += 64) {
+                        const int j = base + lane;
+                        bool cand = false;
+                        if (j < d.E) {
+                            const uint64_t xw = __hip_atomic_load(&d.XT[(size_t)c * d.EW + (j >> 6)], __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT);
+                            cand = (xw >> (j & 63)) & 1ull;
+                            for (int ai = 0; ai < d.n_active; ai++) {
+                                const int64_t pr = S.shape_req[d.active_axes[ai]];
+                                const int64_t h = ld_req(&d.ex_head[(size_t)ai * d.E + j]) - (j == xj ? pr * xcnt : 0);
+                                cand &= pr <= h;
+                            }
+                        }
+                        const uint64_t m = ballot(cand);
+                        if (m) {
+                            jf = base + __ffsll((unsigned long long)m) - 1;
+                            break;
+                        }
+                    }
+                    if (jf >= 0) {
+                        if (jf != xj) ex_flush();
+                        xj = jf;
+                        xcnt++;
+                        if (d.ex_mayfix) {
+                            ex_flush();
+                            existing_merge(d, jf, c, lane);
+                        }
+                        if (lane == 0) {
+                            d.pod_result[p] = -2 - jf;
+                            d.pod_order[p] = seq;
+                        }
+                        seq++;
+                        xstart = jf;
+                        nexist++;
+                        continue;
+                    }
+                    ex_flush();
+                    xstart = d.E;
                 }
                 scanned += N;
                 const long long t_b = prof_clock(d);
@@ -512,7 +634,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                         uint64_t ge = ballot(wb + lane > f && (wb + lane >= N || (wk & KEYMASK) > kk));
                         uint64_t okm2 = okm;
                         int fl2 = fl;
-                        if (movable && ge == 0 && fl > 0 && qw_used < qw_n) {
+                        if (movable && ge == 0 && fl > 0 && qw_used < qw_n && xstart >= d.E) {
                             // the run leaves the window: re-base the window at f to batch over up to 64 of its elements
                             win_flush();
                             win_load(f);
@@ -527,7 +649,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                         const int fl = fl2;
                         const uint64_t okm = okm2;
                         const int el = ge ? __ffsll((unsigned long long)ge) - 1 : 64;  // run end (lane), 64: beyond window
-                        if (movable && qw_used < qw_n && (el < 64 || fl == 0)) {
+                        if (movable && qw_used < qw_n && (el < 64 || fl == 0) && xstart >= d.E) {
                             // same-shape pods queued right after this one (lastLen termination checked per pod)
                             const int q0 = qcount + 1;  // len(queue) when this pod was popped
                             const uint64_t sm = ballot(lane >= off && lane < qw_n && vshape == shape &&
@@ -647,7 +769,10 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                 break;
             }
             win_flush();
+            ex_flush();
             if (lane == 0) {
+                S.xstart = xstart;
+                S.st[ST_EXIST_PLACED] += nexist;
                 S.qhead = qhead;
                 S.qcount = qcount;
                 S.seq = seq;
@@ -1063,6 +1188,12 @@ bool kp_ffd_plan_lds(KpDev& d, int max_bytes) {
 hipError_t kp_launch_class_mask(const KpDev& d, hipStream_t s) {
     dim3 g(d.TW, d.C + d.NT);
     hipLaunchKernelGGL(class_mask_kernel, g, dim3(64), 0, s, d);
+    return hipGetLastError();
+}
+hipError_t kp_launch_existing(const KpDev& d, hipStream_t s) {
+    if (d.E == 0) return hipSuccess;
+    hipLaunchKernelGGL(existing_init_kernel, dim3((d.E + 255) / 256), dim3(256), 0, s, d);
+    if (d.C > 0) hipLaunchKernelGGL(existing_mask_kernel, dim3(d.EW, d.C), dim3(64), 0, s, d);
     return hipGetLastError();
 }
 hipError_t kp_launch_template_init(const KpDev& d, hipStream_t s) {

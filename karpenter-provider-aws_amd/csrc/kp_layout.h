@@ -140,6 +140,22 @@ struct KpDev {
     int32_t* err;                    // [1] device-side error code (capacity overflow etc.)
     int32_t profile;                 // accumulate per-stage evaluation cycles (diagnostics)
 
+    // ---------------- existing nodes (ExistingNode, [core] scheduling/existingnode.go) ----------------
+    int32_t E, EW;                   // existing nodes in scheduling order; words of an E-bit row
+    const ReqHdr* ex_hdr0;           // [E][K] NewLabelRequirements(node labels) + hostname In [name]
+    const uint64_t* ex_words0;       // [E][DW]
+    ReqHdr* ex_hdr;                  // [E][K] working copy (ExistingNode.Add narrows requirements)
+    uint64_t* ex_words;              // [E][DW]
+    const int64_t* ex_avail;         // [E][R] StateNode.Available()
+    const int64_t* ex_req;           // [E][R] remaining daemonset requests (initial ExistingNode.requests)
+    int64_t* ex_head;                // [n_active][E] available - requests on the active axes (working)
+    uint8_t* ex_static;              // [E] Fits holds on every inactive axis and no available quantity is negative
+    uint64_t* XT;                    // [C][EW] taints tolerated ∧ static fit ∧ Requirements.Compatible(node, class)
+    const uint64_t* ex_tol;          // [C][EW] the class tolerates the node's taints
+    const int32_t* cls_xkoff;        // [C+1] CSR of every key a pod class constrains (incl. hostname)
+    const int32_t* cls_xkeys;
+    int32_t ex_mayfix;               // some class has a NotIn/DoesNotExist key: Add may change node requirements
+
     // ---------------- FFD kernel LDS plan (kp_ffd_plan_lds) ----------------
     // Dynamic LDS after the fixed FfdShared block: slice arrays sized by lds_ncmax, the staged type tables
     // sized by lds_tpad, and the quick-accept headroom table hr[lds_A][lds_nq].
@@ -159,5 +175,5 @@ enum {
     ST_MEMO_SKIPS, ST_CYC_POP, ST_CYC_SORT, ST_CYC_SCAN, ST_CYC_TMPL, ST_CYC_COMMIT, ST_CYC_SORT_FULL,
     ST_EV_REQ = 16, ST_EV_MASK, ST_EV_OFF, ST_EV_TYPES, ST_EV_MIN, ST_EV_CALLS,
     ST_QUICK = 24, ST_SLOW, ST_WITNESS_MISS, ST_CYC_QPOP, ST_CYC_QSCAN, ST_CYC_QCHECK, ST_CYC_QCOMMIT,
-    ST_N_NOINV = 32, ST_N_WINMOVE, ST_N_LDSSORT, ST_N_PIVOT, ST_N_WINLOAD, ST_N_FLUSH, ST_N_SHAPE, ST_COUNT = 48
+    ST_N_NOINV = 32, ST_N_WINMOVE, ST_N_LDSSORT, ST_N_PIVOT, ST_N_WINLOAD, ST_N_FLUSH, ST_N_SHAPE, ST_EXIST_PLACED = 44, ST_COUNT = 48
 };

@@ -9,6 +9,8 @@ import numpy as np
 from kpsim import model
 from kpsim.model import (ARCH, CAPACITY_TYPE, INSTANCE_TYPE, NodePool, PodClass, Problem, Requirement, Taint,
                          Toleration, ZONE)
+
+HOSTNAME = "kubernetes.io/hostname"
 from kpsim.synth import _pods_from_milli
 
 AWS = "karpenter.k8s.aws/"
@@ -52,7 +54,50 @@ def _rand_req(rng, catalog):
                        sorted(set(rng.choice(["large", "xlarge", "2xlarge", "metal", "medium"], size=2).tolist())))
 
 
-def fuzz_problem(catalog, seed, n_pods=300, n_classes=12, n_pools=3, with_min=True, with_limits=True):
+def existing_nodes(rng, catalog, n_nodes):
+    """Existing (in-flight / running) nodes: labels of a catalog type (+ zone, capacity-type, a custom team label),
+    available = a fraction of the type's allocatable, daemonset requests, sometimes a taint."""
+    nodes = []
+    for j in range(n_nodes):
+        it = catalog[int(rng.integers(0, len(catalog)))]
+        labels = {}
+        for k, v in it.labels.items():
+            if isinstance(v, (list, tuple)):
+                if v:
+                    labels[k] = str(v[int(rng.integers(0, len(v)))])
+            elif v is not None:
+                labels[k] = str(v)
+        labels[ZONE] = str(rng.choice(ZONES))
+        labels[CAPACITY_TYPE] = str(rng.choice(["spot", "on-demand"]))
+        if rng.random() < 0.5:
+            labels["example.com/team"] = str(rng.choice(["a", "b"]))
+        avail = np.array(it.allocatable, np.int64).copy()
+        frac = float(rng.choice([0.0, 0.3, 0.6, 0.9, 1.0]))
+        for ax in ("cpu", "memory", "pods"):
+            avail[model.RIDX[ax]] = int(avail[model.RIDX[ax]] * (1.0 - frac))
+        req = np.zeros(model.R, np.int64)
+        if rng.random() < 0.5:
+            req[model.RIDX["cpu"]] = 100
+            req[model.RIDX["pods"]] = 1000
+        taints = [Taint("example.com/gpu", "true", "NoSchedule")] if rng.random() < 0.2 else []
+        nodes.append(model.ExistingNode(name="node-%d" % j, labels=labels, available=avail, requests=req, taints=taints))
+    return nodes
+
+
+def _existing_req(rng, n_nodes):
+    kind = int(rng.integers(0, 5))
+    if kind == 0:
+        return Requirement(HOSTNAME, "In", ["node-%d" % int(rng.integers(0, n_nodes))])
+    if kind == 1:
+        return Requirement(HOSTNAME, "NotIn", ["node-%d" % int(rng.integers(0, n_nodes))])
+    if kind == 2:
+        return Requirement("example.com/team", str(rng.choice(["NotIn", "DoesNotExist"])), ["a"])
+    if kind == 3:
+        return Requirement("example.com/team", "In", [str(rng.choice(["a", "b"]))])
+    return Requirement(HOSTNAME, "Exists")
+
+
+def fuzz_problem(catalog, seed, n_pods=300, n_classes=12, n_pools=3, with_min=True, with_limits=True, n_existing=0):
     rng = np.random.Generator(np.random.PCG64(seed))
     T = len(catalog)
     pools = []
@@ -81,6 +126,8 @@ def fuzz_problem(catalog, seed, n_pods=300, n_classes=12, n_pools=3, with_min=Tr
     classes, creqs = [], []
     for c in range(n_classes):
         reqs = [_rand_req(rng, catalog) for _ in range(int(rng.integers(0, 3)))]
+        if n_existing and rng.random() < 0.4:
+            reqs.append(_existing_req(rng, n_existing))
         tols = [Toleration("example.com/gpu", "Exists", "", "NoSchedule")] if rng.random() < 0.3 else []
         classes.append(PodClass(reqs, tols))
         cpu = int(rng.choice([100, 500, 1000, 2000, 4000]))
@@ -98,4 +145,5 @@ def fuzz_problem(catalog, seed, n_pods=300, n_classes=12, n_pools=3, with_min=Tr
     pods = _pods_from_milli(specs)
     if rng.random() < 0.5:  # equal creation times: UID order decides ties
         pods.creation_ns[:] = pods.creation_ns[0]
-    return Problem(catalog, pools, classes, pods)
+    existing = existing_nodes(rng, catalog, n_existing) if n_existing else []
+    return Problem(catalog, pools, classes, pods, existing)

@@ -135,3 +135,21 @@ def test_config2_full_properties(ctx, golden):
         need = tot[i] + (pool.daemon_overhead if pool.daemon_overhead is not None else 0)
         for t in ts:
             assert (need <= prob.catalog[t].allocatable).all()
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_fuzz_existing_nodes(ctx, golden, seed):
+    """ExistingNode.Add before in-flight NodeClaims: labels, taints, hostname selectors, NotIn/DoesNotExist merges."""
+    rng = np.random.Generator(np.random.PCG64(1000 + seed))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=160, replace=False))]
+    prob = fuzzgen.fuzz_problem(sub, 1000 + seed, n_pods=int(rng.integers(50, 400)),
+                                n_existing=int(rng.integers(3, 120)))
+    parity.assert_same(parity.run_device(ctx, prob), parity.run_oracle(prob))
+
+
+def test_config2_with_existing_nodes(ctx, golden):
+    """config2 classes against 400 partially used existing nodes, then new NodeClaims."""
+    rng = np.random.Generator(np.random.PCG64(77))
+    prob = synth.subsample(synth.config2(catalog=golden), 3000)
+    prob.existing = fuzzgen.existing_nodes(rng, golden, 400)
+    parity.assert_same(parity.run_device(ctx, prob), parity.run_oracle(prob))
