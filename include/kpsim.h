@@ -256,6 +256,76 @@ kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out);
 kp_status kp_last_kernel_times(kp_ctx* ctx, double* ms, int32_t n);
 
 /*
+ * Consolidation re-simulation — replaces the scheduling simulation of [core] pkg/controllers/disruption:
+ * SimulateScheduling (helpers.go) + consolidation.computeConsolidation (consolidation.go), driven by
+ * SingleNodeConsolidation (singlenodeconsolidation.go: first valid candidate in disruption-cost order) and
+ * MultiNodeConsolidation.firstNConsolidationOption (multinodeconsolidation.go: binary search over the prefix
+ * length).  Reached today from the disruption controller registered at cmd/controller/main.go:50-58; the decision
+ * semantics are restated from the un-vendored core module and are marked "recalled" in DESIGN.md.
+ *
+ * A probe is one SimulateScheduling call: the pods of its candidates (plus pending pods) are rescheduled onto every
+ * other existing node, the in-flight NodeClaims it creates and the NodePools.
+ *   single mode: probe i = { candidates[i] }                       (i = 0 .. n_candidates-1)
+ *   multi mode:  probe i = { candidates[0 .. i+2) }                (firstNConsolidationOption's mid = i+1: prefix
+ *                sizes 2 .. n when n <= max_candidates, else 2 .. max_candidates+1)
+ * Probes are independent, so [probe_begin, probe_end) may be any shard of them (one shard per GPU); the caller replays
+ * the single-node scan (first valid probe) or the multi-node binary search over the results, which is exact because
+ * every probe the sequential search would visit has been evaluated.
+ * cluster.existing must be in NewScheduler's order (initialized nodes first, then by name); probes keep that order
+ * with the candidates removed.  Candidate prices must be >= 0 (getCandidatePrices fails otherwise).
+ */
+enum { KP_CONSOLIDATE_SINGLE = 0, KP_CONSOLIDATE_MULTI = 1 };
+enum { KP_DECISION_NONE = 0, KP_DECISION_DELETE = 1, KP_DECISION_REPLACE = 2 };
+enum { KP_CT_ON_DEMAND = 0, KP_CT_SPOT = 1, KP_CT_RESERVED = 2 };
+
+typedef struct kp_candidate {
+    int32_t node;                    /* index into cluster.existing */
+    int32_t n_pods;                  /* Candidate.ReschedulablePods, indices into cluster.pods */
+    const int32_t* pods;
+    double price;                    /* getCandidatePrices term: cheapest offering compatible with the node's labels */
+    int32_t capacity_type;           /* KP_CT_* of the node */
+    int32_t instance_type;           /* catalog row of the node's instance type (filterOutSameInstanceType), -1 */
+    int32_t nodepool;                /* index into cluster.nodepools, -1 */
+    const int64_t* capacity;         /* [R] node capacity, added back to its NodePool's remaining limits, or NULL */
+} kp_candidate;
+
+typedef struct kp_consolidate_input {
+    kp_solve_input cluster;          /* nodepools, classes, pods (pending + reschedulable), existing = all state nodes */
+    const uint8_t* initialized;      /* [n_existing] StateNode.Initialized(); NULL: all initialized */
+    int32_t n_pending;               /* provisioner.GetPendingPods, indices into cluster.pods */
+    const int32_t* pending;
+    int32_t n_candidates;            /* in disruption-cost order */
+    const kp_candidate* candidates;
+    int32_t mode;                    /* KP_CONSOLIDATE_* */
+    int32_t max_candidates;          /* multi: 100 */
+    int32_t probe_begin, probe_end;  /* shard of the probe list; probe_end <= 0: to the end */
+    int32_t spot_to_spot;            /* feature gate SpotToSpotConsolidation */
+} kp_consolidate_input;
+
+typedef struct kp_probe_result {
+    int32_t decision;                /* KP_DECISION_* of computeConsolidation */
+    int32_t valid;                   /* single: decision != NONE; multi: DELETE, or REPLACE with options left by
+                                        filterOutSameInstanceType (the binary search's test) */
+    int32_t all_scheduled;           /* Results.AllNonPendingPodsScheduled; uninitialized-node placements are errors */
+    int32_t n_new_nodeclaims;        /* valid new NodeClaims, capped at 2 (the device stops a probe at its second
+                                        NodeClaim, after which the decision is NONE and all_scheduled is undefined) */
+    int32_t n_replacement_types;     /* replacement options of the command (REPLACE; spot-to-spot single: at most 15;
+                                        multi: after filterOutSameInstanceType) */
+    int32_t n_pods;                  /* pods the probe rescheduled */
+    double candidate_price;          /* Σ candidate prices */
+    double replacement_price;        /* cheapest WorstLaunchPrice among the replacement options (REPLACE), else 0 */
+} kp_probe_result;
+
+/* Number of probes of an input (mode, n_candidates, max_candidates). */
+int32_t kp_consolidate_probe_count(const kp_consolidate_input* in);
+/* Evaluates probes [probe_begin, probe_end) on the ctx's device; results[i] is probe probe_begin + i. */
+kp_status kp_consolidate(kp_ctx* ctx, const kp_consolidate_input* in, kp_probe_result* results, int32_t cap_results);
+/* Diagnostics of the last kp_consolidate: ms[3] = {device prep (queue sort, masks), probe kernel, whole call};
+ * counters[8] = {pods popped, existing-node slots examined, NodeClaim evaluations, template evaluations, probes,
+ * queue-bitmap words scanned, existing-node placements, new NodeClaims}. */
+kp_status kp_consolidate_stats(kp_ctx* ctx, double* ms, int64_t* counters, int32_t n_counters);
+
+/*
  * Requirements of NodeClaim `nc` from the last kp_solve on this ctx (hostname removed as in
  * FinalizeScheduling), one line per key, lines sorted:
  *   "key \t complement(0|1) \t gt|- \t lt|- \t minValues|- \t v1 \x1f v2 ..."   (values sorted)

@@ -1,0 +1,47 @@
+// kp_cons.h — device tables of a consolidation pass (kp_consolidate), shared by kp_host.cpp and kp_consolidate.hip.
+//
+// A probe is one SimulateScheduling + computeConsolidation ([core] pkg/controllers/disruption/helpers.go,
+// consolidation.go): the probe's pods (pending + its candidates' reschedulable pods) are rescheduled onto every
+// state node except its candidates, then onto at most one new NodeClaim (a second one makes the decision NONE, so
+// the probe stops there).  One wave runs one probe; a persistent grid of waves pulls probes from a counter.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/kpsim.h"
+#include "kp_layout.h"
+
+enum { CS_POPS = 0, CS_EX_NODES, CS_NC_EVALS, CS_TMPL_EVALS, CS_PROBES, CS_BITMAP_WORDS, CS_PLACED_EXISTING,
+       CS_NEW_NC, CS_COUNT = 8 };
+
+struct KpCons {
+    int32_t n_probes;           // probes of this call: global probe ids probe0 .. probe0 + n_probes - 1
+    int32_t probe0;
+    int32_t mode;               // KP_CONSOLIDATE_*
+    int32_t n_cand;
+    int32_t spot_to_spot;
+    int32_t v_spot, v_od;       // capacity-type value ids in the solve dictionary, -1 when absent
+    uint64_t spot_slots;        // offering slots whose capacity type is spot / on-demand
+    uint64_t od_slots;
+    const int32_t* cand_i;      // [n_cand][4]: node, capacity type (KP_CT_*), catalog row, template (-1)
+    const int32_t* cand_off;    // [n_cand + 1] CSR into cand_pods
+    const int32_t* cand_pods;   // reschedulable pods of each candidate
+    const double* cand_price;   // [n_cand]
+    const int64_t* cand_cap;    // [n_cand][R] capacity returned to the candidate's NodePool limits
+    const int32_t* rank;        // [P] queue position of each pod (NewQueue order)
+    const uint64_t* pend_bits;  // [PW] pending pods by queue position
+    int32_t PW;
+    const uint8_t* initialized; // [E] StateNode.Initialized()
+    const int64_t* alloc_act;   // [n_active][astride] allocatable of the active axes (EvalEnv.alloc)
+    int32_t astride;
+    // per-worker scratch
+    int32_t ring_cap;           // >= pods of any probe
+    int32_t* ring;              // [workers][ring_cap] queue entries: pod | pending << 31
+    int32_t* ring_last;         // [workers][ring_cap] Queue.lastLen of the entry (-1: never pushed)
+    int64_t* delta;             // [workers][n_active][E] requests added to node j by this probe (valid: mod bit)
+    uint64_t* pbits;            // [workers][PW] probe pods by queue position (all zero between probes)
+    int32_t* next_probe;        // [1] work counter
+    kp_probe_result* out;       // [n_probes]
+    int64_t* stats;             // [CS_COUNT]
+    // dynamic LDS plan (kp_cons_plan_lds)
+    int32_t off_hdr, off_words, off_rem, off_excl, off_mod, lds_bytes;
+};

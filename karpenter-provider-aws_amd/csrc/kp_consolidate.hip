@@ -1,0 +1,617 @@
+// kp_consolidate.hip — consolidation probes on gfx950: one wave per SimulateScheduling + computeConsolidation.
+//
+// Reference semantics ([core] sigs.k8s.io/karpenter pkg/controllers/disruption, recalled):
+//   SimulateScheduling (helpers.go): state nodes minus the candidates, pods = pending + candidates' reschedulable
+//     pods, NewScheduler (NodePool limits recomputed without the candidates), Solve, TruncateInstanceTypes(60); a pod
+//     placed on an uninitialized node is an error.
+//   computeConsolidation (consolidation.go): not all non-pending pods scheduled → NONE; no new NodeClaim → DELETE;
+//     more than one → NONE; else the NodeClaim's options OrderByPrice'd, spot-to-spot gate (computeSpotToSpotConsolidation:
+//     feature gate, ≥ 15 cheaper types for one candidate, the 15 cheapest kept), otherwise
+//     RemoveInstanceTypeOptionsByPriceAndMinValues(WorstLaunchPrice < Σ candidate prices) and capacity-type
+//     narrowed to spot when both spot and on-demand remain.
+//   multinodeconsolidation.go: filterOutSameInstanceType on a REPLACE (the search's validity test).
+//
+// Per probe the wave keeps: an exclusion bitmap of its candidates and a modified-node bitmap (LDS), the requests it
+// added to existing nodes (global delta slab, read past L1), the queue as a ring in global memory with a 64-entry
+// register window, and at most one in-flight NodeClaim (requirements digest, options, requests) in LDS.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cfloat>
+
+#include "kp_cons.h"
+#include "kp_device.h"
+#include "kp_eval.h"
+#include "kp_layout.h"
+
+namespace {
+
+struct ConsShared {
+    ClassCache CC;
+    WaveScratch ws;
+    Roles roles;
+    int64_t nc_req[KP_MAX_R];
+};
+
+__device__ __forceinline__ int32_t ld32(const int32_t* p) {
+    return __hip_atomic_load(const_cast<int32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld64u(const uint64_t* p) {
+    return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double wave_min_f64(double x) {
+    for (int o = 32; o >= 1; o >>= 1) {
+        const double y = __shfl_xor(x, o);
+        x = y < x ? y : x;
+    }
+    return x;
+}
+
+// types whose Capacity exceeds the probe's remaining NodePool limits (filterByRemainingResources)
+__device__ inline uint64_t limit_filter_rem(const KpDev& d, int j, uint64_t o, const int64_t* rem, int lane) {
+    bool any_limit = false;
+    for (int r = 0; r < d.R; r++) any_limit |= d.limit_set[(size_t)j * d.R + r] != 0;
+    if (!any_limit) return o;
+    uint64_t out = 0;
+    for (int w = 0; w < d.TW; w++) {
+        const uint64_t cw = rl64(o, w);
+        if (!cw) continue;
+        const int t = w * 64 + lane;
+        bool keep = (cw >> lane) & 1ull;
+        if (keep) {
+            for (int r = 0; r < d.R; r++)
+                if (d.limit_set[(size_t)j * d.R + r] && d.cap[(size_t)r * d.T + t] > rem[j * d.R + r]) keep = false;
+        }
+        const uint64_t nb = ballot(keep);
+        if (lane == w) out = nb;
+    }
+    return out;
+}
+
+// Offerings.Available().WorstLaunchPrice(reqs) over the admissible slots m of type t: reserved (none in this build's
+// catalogs), then spot, then on-demand; the most expensive offering of the first capacity type present.
+__device__ inline double worst_launch_price(const KpDev& d, const KpCons& k, int t, uint64_t m) {
+    const uint64_t ms = m & k.spot_slots;
+    uint64_t mm = ms ? ms : (m & k.od_slots);
+    if (!mm) return DBL_MAX;
+    double mx = 0.0;
+    bool first = true;
+    while (mm) {
+        const int s = __ffsll((unsigned long long)mm) - 1;
+        mm &= mm - 1;
+        const double p = d.slot_price[(size_t)t * KP_MAX_SLOTS + s];
+        if (first || p > mx) mx = p;
+        first = false;
+    }
+    return mx;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    ConsShared& S = *reinterpret_cast<ConsShared*>(smem);
+    ReqHdr* nch = reinterpret_cast<ReqHdr*>(smem + k.off_hdr);
+    uint64_t* ncw = reinterpret_cast<uint64_t*>(smem + k.off_words);
+    int64_t* rem = reinterpret_cast<int64_t*>(smem + k.off_rem);
+    uint64_t* excl = reinterpret_cast<uint64_t*>(smem + k.off_excl);
+    uint64_t* modb = reinterpret_cast<uint64_t*>(smem + k.off_mod);
+    const int lane = threadIdx.x;
+    const int wid = blockIdx.x;
+    const int E = d.E, EW = d.EW, A = d.n_active, R = d.R, K = d.K, TW = d.TW, T = d.T, NT = d.NT;
+    const int cap = k.ring_cap;
+    int32_t* ring = k.ring + (size_t)wid * cap;
+    int32_t* rlast = k.ring_last + (size_t)wid * cap;
+    int64_t* delta = k.delta + (size_t)wid * A * (E > 0 ? E : 1);
+    uint64_t* pbits = k.pbits + (size_t)wid * k.PW;
+
+    if (lane < 5) {
+        const int rk = lane == 0 ? d.key_zone : lane == 1 ? d.key_ct : lane == 2 ? d.key_zoneid : lane == 3 ? d.key_resvid : d.key_resvtype;
+        S.roles.key[lane] = rk;
+        S.roles.woff[lane] = rk >= 0 ? d.woff[rk] : 0;
+        S.roles.nw[lane] = rk >= 0 ? d.nw[rk] : 0;
+    }
+    if (lane == 0) S.CC.cls = -1;
+    __syncthreads();
+    EvalEnv Ev;
+    Ev.alloc = k.alloc_act;
+    Ev.astride = k.astride;
+    Ev.avail = d.avail_zc;
+    Ev.multi16 = nullptr;
+    Ev.slot_zone = d.slot_zone;
+    Ev.slot_ct = d.slot_ct;
+    Ev.slot_zoneid = d.slot_zoneid;
+    Ev.roles = &S.roles;
+    Ev.min_tmpl_mask = 0;  // minValues templates are rejected by kp_consolidate
+
+    for (;;) {
+        int probe = 0;
+        if (lane == 0) probe = atomicAdd(k.next_probe, 1);
+        probe = __builtin_amdgcn_readfirstlane(__shfl(probe, 0));
+        if (probe >= k.n_probes) break;
+        const int gp = k.probe0 + probe;
+        const bool single = k.mode == KP_CONSOLIDATE_SINGLE;
+        const int c0 = single ? gp : 0, c1 = single ? gp + 1 : gp + 2;
+        int64_t st_pops = 0, st_nodes = 0, st_nc = 0, st_tmpl = 0, st_words = 0, st_placed = 0;
+
+        // ---- probe state: excluded candidates, modified nodes, NodePool limits + candidate capacity ----
+        for (int w = lane; w < EW; w += 64) {
+            excl[w] = 0;
+            modb[w] = 0;
+        }
+        for (int i = lane; i < NT * R; i += 64) rem[i] = d.remaining[i];
+        __syncthreads();
+        for (int c = c0 + lane; c < c1; c += 64) {
+            const int node = k.cand_i[c * 4 + 0];
+            atomicOr((unsigned long long*)&excl[node >> 6], 1ull << (node & 63));
+        }
+        double cprice = 0.0;
+        bool all_spot = true;
+        int n_np = 0;
+        for (int c = c0; c < c1; c++) {  // getCandidatePrices: Σ in candidate order
+            cprice += k.cand_price[c];
+            all_spot &= k.cand_i[c * 4 + 1] == KP_CT_SPOT;
+            n_np += k.cand_off[c + 1] - k.cand_off[c];
+            const int j = k.cand_i[c * 4 + 3];
+            if (j >= 0 && lane < R && d.limit_set[(size_t)j * R + lane])
+                rem[j * R + lane] += k.cand_cap[(size_t)c * R + lane];
+        }
+        // ---- the probe's pods in queue order: mark queue positions, then scan the bitmap with the pending pods ----
+        for (int c = c0; c < c1; c++) {
+            const int o0 = k.cand_off[c], o1 = k.cand_off[c + 1];
+            for (int i = o0 + lane; i < o1; i += 64) {
+                const int r = k.rank[k.cand_pods[i]];
+                __hip_atomic_fetch_or(&pbits[r >> 6], 1ull << (r & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int n = 0;
+        for (int wb = 0; wb < k.PW; wb += 64) {
+            const int w = wb + lane;
+            uint64_t mine = 0, pend = 0;
+            if (w < k.PW) {
+                mine = ld64u(&pbits[w]);
+                pend = k.pend_bits[w];
+            }
+            uint64_t x = mine | pend;
+            const int cnt = __popcll(x);
+            int v = cnt;
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(v, o);
+                if (lane >= o) v += y;
+            }
+            const int total = __shfl(v, 63);
+            int pos = n + v - cnt;
+            while (x) {
+                const int b = __ffsll((unsigned long long)x) - 1;
+                x &= x - 1;
+                const int r = w * 64 + b;
+                ring[pos] = d.queue0[r] | (int32_t)(((pend >> b) & 1ull) << 31);
+                rlast[pos] = -1;
+                pos++;
+            }
+            if (mine) __hip_atomic_store(&pbits[w], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            n += total;
+        }
+        st_words += k.PW;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+
+        // ---- Solve: queue with lastLen termination; existing nodes, the in-flight NodeClaim, the templates ----
+        int head = 0, count = n, wbase = -64;
+        int vpod = -1, vlast = -1, vc = 0, vshape = -1;
+        int64_t vq[KP_LDS_AXES];
+#pragma unroll
+        for (int ai = 0; ai < KP_LDS_AXES; ai++) vq[ai] = 0;
+        auto win_load = [&](int base) {
+            wbase = base;
+            const int pos = base + lane;
+            vpod = -1;
+            vlast = -1;
+            vc = 0;
+            vshape = -1;
+            if (pos < head + count) {
+                const int slot = pos % cap;
+                vpod = ld32(&ring[slot]);
+                vlast = ld32(&rlast[slot]);
+                const int p = vpod & 0x7fffffff;
+                vc = d.pod_cls[p];
+                vshape = d.pod_shape[p];
+#pragma unroll
+                for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                    vq[ai] = ai < A ? d.pod_req[(size_t)p * R + d.active_axes[ai]] : 0;
+            }
+        };
+        int n_nc = 0, nc_tmpl = -1, prev_shape = -1, xstart = 0, ok_np = 0;
+        bool bad = false, stop = false;
+        uint64_t nc_opts = 0;
+        while (count > 0) {
+            if (head - wbase >= 64) win_load(head);
+            const int off = head - wbase;
+            const int ent = rl32(vpod, off);
+            if (rl32(vlast, off) == count) break;  // Queue.Pop: cycled through the queue without progress
+            head++;
+            count--;
+            st_pops++;
+            const bool pend = ent < 0;
+            const int p = ent & 0x7fffffff;
+            const int c = rl32(vc, off);
+            const int shape = rl32(vshape, off);
+            int64_t q[KP_LDS_AXES];
+#pragma unroll
+            for (int ai = 0; ai < KP_LDS_AXES; ai++) {
+                const uint32_t lo = (uint32_t)rl32((int)(uint32_t)vq[ai], off);
+                const uint32_t hi = (uint32_t)rl32((int)(uint32_t)((uint64_t)vq[ai] >> 32), off);
+                q[ai] = (int64_t)(((uint64_t)hi << 32) | lo);
+            }
+            if (shape != prev_shape) {  // nodes before xstart rejected this shape and only lose headroom
+                prev_shape = shape;
+                xstart = 0;
+            }
+            // ExistingNode.Add in scheduling order (candidates excluded)
+            int jf = -1;
+            for (int base = xstart; base < E; base += 64) {
+                const int j = base + lane;
+                bool cand = false;
+                if (j < E) {
+                    const uint64_t xw = d.XT[(size_t)c * EW + (j >> 6)] & ~excl[j >> 6];
+                    cand = (xw >> (j & 63)) & 1ull;
+                    if (cand) {
+                        const bool md = (modb[j >> 6] >> (j & 63)) & 1ull;
+#pragma unroll
+                        for (int ai = 0; ai < KP_LDS_AXES; ai++) {
+                            if (ai < A) {
+                                int64_t h = d.ex_head[(size_t)ai * E + j];
+                                if (md) h -= ld_req(&delta[(size_t)ai * E + j]);
+                                cand &= q[ai] <= h;
+                            }
+                        }
+                    }
+                }
+                st_nodes += 64;
+                const uint64_t m = ballot(cand);
+                if (m) {
+                    jf = base + __ffsll((unsigned long long)m) - 1;
+                    break;
+                }
+            }
+            if (jf >= 0) {
+                const bool md = (modb[jf >> 6] >> (jf & 63)) & 1ull;
+                if (lane < A) {
+                    int64_t qq = 0;
+#pragma unroll
+                    for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                        if (lane == ai) qq = q[ai];
+                    int64_t* dp = &delta[(size_t)lane * E + jf];
+                    __hip_atomic_store(dp, md ? ld_req(dp) + qq : qq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0 && !md) modb[jf >> 6] |= 1ull << (jf & 63);
+                __syncthreads();
+                xstart = jf;
+                st_placed++;
+                if (!pend) {
+                    if (k.initialized[jf]) ok_np++;
+                    else bad = true;  // SimulateScheduling: uninitialized-node placement is an error
+                }
+                continue;
+            }
+            xstart = E;
+            bool placed = false;
+            const int64_t* preq = d.pod_req + (size_t)p * R;
+            if (n_nc == 1) {  // NodeClaim.Add on the in-flight NodeClaim
+                if (S.CC.cls != c) fill_class_cache(d, c, S.CC, lane, 64);
+                EvalIn a;
+                a.Ahdr = nch;
+                a.Aw = ncw;
+                a.opts = nc_opts;
+                a.base_req = S.nc_req;
+                a.pod_req = preq;
+                a.tmpl = nc_tmpl;
+                a.compat = true;
+                a.force_off = false;
+                a.prof = nullptr;
+                st_nc++;
+                if (eval_wave(d, Ev, S.CC, a, S.ws, lane)) {
+                    if (lane < S.CC.nck) {
+                        const int kk = S.CC.key[lane];
+                        nch[kk] = S.ws.hdr[lane];
+                        for (int i = 0; i < S.CC.nw[lane]; i++) ncw[S.CC.woff[lane] + i] = S.ws.words[S.CC.wsoff[lane] + i];
+                    }
+                    if (lane < TW) nc_opts = S.ws.opts[lane];
+                    if (lane < R) S.nc_req[lane] += preq[lane];
+                    __syncthreads();
+                    placed = true;
+                }
+            }
+            if (!placed) {  // new NodeClaim from the templates in weight order
+                for (int j = 0; j < NT; j++) {
+                    uint64_t o = (lane < TW && d.tmpl_ok[j]) ? d.tmpl_opts[(size_t)j * TW + lane] : 0;
+                    o = limit_filter_rem(d, j, o, rem, lane);
+                    if (!ballot(o != 0)) continue;
+                    if (S.CC.cls != c) fill_class_cache(d, c, S.CC, lane, 64);
+                    EvalIn a;
+                    a.Ahdr = d.cls_hdr + (size_t)(d.C + j) * K;
+                    a.Aw = d.cls_words + (size_t)(d.C + j) * d.DW;
+                    a.opts = o;
+                    a.base_req = d.daemon + (size_t)j * R;
+                    a.pod_req = preq;
+                    a.tmpl = j;
+                    a.compat = true;
+                    a.force_off = false;
+                    a.prof = nullptr;
+                    st_tmpl++;
+                    if (!eval_wave(d, Ev, S.CC, a, S.ws, lane)) continue;
+                    if (n_nc == 1) {  // a second NodeClaim: computeConsolidation returns NONE
+                        stop = true;
+                        break;
+                    }
+                    for (int kk = lane; kk < K; kk += 64) nch[kk] = d.cls_hdr[(size_t)(d.C + j) * K + kk];
+                    for (int i = lane; i < d.DW; i += 64) ncw[i] = d.cls_words[(size_t)(d.C + j) * d.DW + i];
+                    __syncthreads();
+                    if (lane < S.CC.nck) {
+                        const int kk = S.CC.key[lane];
+                        nch[kk] = S.ws.hdr[lane];
+                        for (int i = 0; i < S.CC.nw[lane]; i++) ncw[S.CC.woff[lane] + i] = S.ws.words[S.CC.wsoff[lane] + i];
+                    }
+                    nc_opts = lane < TW ? S.ws.opts[lane] : 0;
+                    if (lane < R) S.nc_req[lane] = d.daemon[(size_t)j * R + lane] + preq[lane];
+                    // subtractMax(remaining, nodeClaim.InstanceTypeOptions)
+                    for (int r = 0; r < R; r++) {
+                        if (!d.limit_set[(size_t)j * R + r]) continue;
+                        int64_t mx = INT64_MIN;
+                        for (int w = 0; w < TW; w++) {
+                            const uint64_t ow = rl64(nc_opts, w);
+                            if ((ow >> lane) & 1ull) {
+                                const int64_t cp = d.cap[(size_t)r * T + w * 64 + lane];
+                                mx = cp > mx ? cp : mx;
+                            }
+                        }
+                        mx = wave_max64(mx);
+                        if (lane == 0) rem[j * R + r] -= mx;
+                    }
+                    nc_tmpl = j;
+                    n_nc = 1;
+                    placed = true;
+                    __syncthreads();
+                    break;
+                }
+            }
+            if (stop) break;
+            if (placed) {
+                if (!pend) ok_np++;
+                continue;
+            }
+            // Queue.Push(pod, relaxed=false): lastLen = len after the append
+            const int tail = head + count;
+            if (lane == 0) {
+                ring[tail % cap] = ent;
+                rlast[tail % cap] = count + 1;
+            }
+            if (tail - wbase < 64 && lane == tail - wbase) {
+                vpod = ent;
+                vlast = count + 1;
+                vc = c;
+                vshape = shape;
+#pragma unroll
+                for (int ai = 0; ai < KP_LDS_AXES; ai++) vq[ai] = q[ai];
+            }
+            count++;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+
+        // ---- computeConsolidation ----
+        int decision = KP_DECISION_NONE, valid = 0, nrep = 0;
+        double rprice = 0.0;
+        const bool all = !stop && !bad && ok_np == n_np;
+        if (all && n_nc == 0) {
+            decision = KP_DECISION_DELETE;
+            valid = 1;
+        } else if (all) {
+            // Offerings.Available().Compatible(NodeClaim requirements) over zone × capacity-type slots
+            bool okslot = false;
+            if (lane < d.n_slots) {
+                auto adm = [&](int kk, int v) -> bool {
+                    if (kk < 0) return true;
+                    const ReqHdr h = nch[kk];
+                    if (!(h.flags & RF_DEF)) return true;
+                    return req_has(d, kk, v, h, ncw + d.woff[kk]);
+                };
+                auto dneok = [&](int kk) -> bool {
+                    if (kk < 0) return true;
+                    const ReqHdr h = nch[kk];
+                    if (!(h.flags & RF_DEF)) return true;
+                    return op_notin_or_dne(req_op(h.flags, popc_words(ncw + d.woff[kk], d.nw[kk])));
+                };
+                okslot = adm(d.key_zone, d.slot_zone[lane]) && adm(d.key_ct, d.slot_ct[lane]) &&
+                         (d.slot_zoneid[lane] < 0 || adm(d.key_zoneid, d.slot_zoneid[lane])) && dneok(d.key_resvid) &&
+                         dneok(d.key_resvtype);
+            }
+            const uint64_t mzc = ballot(okslot);
+            // OrderByPrice(reqs) + Truncate(M): select the M cheapest options by (price, name)
+            double pr[KP_TW_MAX];
+            uint32_t rk[KP_TW_MAX];
+            uint32_t present = 0;
+            int n_opt = 0;
+#pragma unroll
+            for (int w = 0; w < KP_TW_MAX; w++) {
+                pr[w] = DBL_MAX;
+                rk[w] = 0xFFFFFFFFu;
+                if (w < TW) {
+                    const uint64_t word = rl64(nc_opts, w);
+                    n_opt += __popcll(word);
+                    if ((word >> lane) & 1ull) {
+                        const int t = w * 64 + lane;
+                        uint64_t m = d.avail_zc[t] & mzc;
+                        double price = DBL_MAX;
+                        while (m) {
+                            const int s = __ffsll((unsigned long long)m) - 1;
+                            m &= m - 1;
+                            const double sp = d.slot_price[(size_t)t * KP_MAX_SLOTS + s];
+                            price = sp < price ? sp : price;
+                        }
+                        pr[w] = price;
+                        rk[w] = d.name_rank[t];
+                        present |= 1u << w;
+                    }
+                }
+            }
+            const int nsel = n_opt < d.M ? n_opt : d.M;
+            int my_t = -1;
+            for (int i = 0; i < nsel; i++) {
+                double bp = DBL_MAX;
+                uint32_t br = 0xFFFFFFFFu;
+                int bw = -1;
+#pragma unroll
+                for (int w = 0; w < KP_TW_MAX; w++) {
+                    if (((present >> w) & 1u) && (bw < 0 || pr[w] < bp || (pr[w] == bp && rk[w] < br))) {
+                        bp = pr[w];
+                        br = rk[w];
+                        bw = w;
+                    }
+                }
+                int gl = bw >= 0 ? lane : -1, gw = bw;
+                for (int o = 32; o >= 1; o >>= 1) {
+                    const double op = __shfl_xor(bp, o);
+                    const uint32_t orr = (uint32_t)__shfl_xor((int)br, o);
+                    const int ol = __shfl_xor(gl, o), ow = __shfl_xor(gw, o);
+                    if (ol >= 0 && (gl < 0 || op < bp || (op == bp && orr < br))) {
+                        bp = op;
+                        br = orr;
+                        gl = ol;
+                        gw = ow;
+                    }
+                }
+                gl = __builtin_amdgcn_readfirstlane(gl);
+                gw = __builtin_amdgcn_readfirstlane(gw);
+                if (lane == i) my_t = gw * 64 + gl;
+                if (lane == gl) present &= ~(1u << gw);
+            }
+            // capacity-type requirement of the NodeClaim: Has(spot) / Has(on-demand)
+            auto ct_has = [&](int vid) -> bool {
+                const int kk = d.key_ct;
+                if (kk < 0) return true;
+                const ReqHdr h = nch[kk];
+                if (!(h.flags & RF_DEF)) return true;  // undefined: Get() is Exists
+                if (vid < 0) return (h.flags & RF_CMP) && !(h.flags & (RF_GT | RF_LT));
+                return req_has(d, kk, vid, h, ncw + d.woff[kk]);
+            };
+            const bool has_spot = ct_has(k.v_spot), has_od = ct_has(k.v_od);
+            const uint64_t mt = my_t >= 0 ? d.avail_zc[my_t] & mzc : 0;
+            bool keep = false, none = false, spot_only = false;
+            if (all_spot && has_spot) {  // computeSpotToSpotConsolidation
+                if (!k.spot_to_spot) {
+                    none = true;
+                } else {
+                    spot_only = true;  // Requirements.Add(capacity-type In [spot])
+                    keep = my_t >= 0 && worst_launch_price(d, k, my_t, mt & k.spot_slots) < cprice;
+                    const uint64_t km = ballot(keep);
+                    if (!km) {
+                        none = true;
+                    } else if (c1 - c0 == 1) {
+                        if (__popcll(km) < 15) none = true;  // MinInstanceTypesForSpotToSpotConsolidation
+                        else keep = keep && __popcll(km & ((1ull << lane) - 1)) < 15;
+                    }
+                }
+            } else {  // RemoveInstanceTypeOptionsByPriceAndMinValues
+                keep = my_t >= 0 && worst_launch_price(d, k, my_t, mt) < cprice;
+                if (!ballot(keep)) none = true;
+                spot_only = has_spot && has_od;  // spot/on-demand flexible replacement narrowed to spot
+            }
+            if (!none) {
+                decision = KP_DECISION_REPLACE;
+                const uint64_t mr = spot_only ? (mt & k.spot_slots) : mt;
+                const double wl = keep ? worst_launch_price(d, k, my_t, mr) : DBL_MAX;
+                if (!single) {  // filterOutSameInstanceType
+                    double mp = DBL_MAX;
+                    if (keep)
+                        for (int c = c0; c < c1; c++)
+                            if (k.cand_i[c * 4 + 2] == my_t && k.cand_price[c] < mp) mp = k.cand_price[c];
+                    const double maxp = wave_min_f64(mp);
+                    keep = keep && wl < maxp;
+                }
+                const uint64_t km = ballot(keep);
+                valid = km != 0;
+                nrep = __popcll(km);
+                rprice = nrep ? wave_min_f64(keep ? wl : DBL_MAX) : 0.0;
+            }
+        }
+        if (lane == 0) {
+            kp_probe_result o;
+            o.decision = decision;
+            o.valid = valid;
+            o.all_scheduled = all ? 1 : 0;
+            o.n_new_nodeclaims = stop ? 2 : n_nc;
+            o.n_replacement_types = nrep;
+            o.n_pods = n;
+            o.candidate_price = cprice;
+            o.replacement_price = rprice;
+            k.out[probe] = o;
+            atomicAdd((unsigned long long*)&k.stats[CS_POPS], (unsigned long long)st_pops);
+            atomicAdd((unsigned long long*)&k.stats[CS_EX_NODES], (unsigned long long)st_nodes);
+            atomicAdd((unsigned long long*)&k.stats[CS_NC_EVALS], (unsigned long long)st_nc);
+            atomicAdd((unsigned long long*)&k.stats[CS_TMPL_EVALS], (unsigned long long)st_tmpl);
+            atomicAdd((unsigned long long*)&k.stats[CS_PROBES], 1ull);
+            atomicAdd((unsigned long long*)&k.stats[CS_BITMAP_WORDS], (unsigned long long)st_words);
+            atomicAdd((unsigned long long*)&k.stats[CS_PLACED_EXISTING], (unsigned long long)st_placed);
+            atomicAdd((unsigned long long*)&k.stats[CS_NEW_NC], (unsigned long long)(stop ? 2 : n_nc));
+        }
+        if (lane == 0) S.CC.cls = -1;  // the class cache is refilled lazily per probe
+        __syncthreads();
+    }
+}
+
+// queue position of each pod: rank[queue0[i]] = i
+__global__ void rank_kernel(const int32_t* __restrict__ queue0, int32_t* __restrict__ rank, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) rank[queue0[i]] = i;
+}
+__global__ void pending_bits_kernel(const int32_t* __restrict__ pending, int n, const int32_t* __restrict__ rank,
+                                    uint64_t* __restrict__ bits) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const int r = rank[pending[i]];
+        atomicOr((unsigned long long*)&bits[r >> 6], 1ull << (r & 63));
+    }
+}
+
+// Dynamic LDS of consolidate_kernel: fixed block, NodeClaim digest, limits, candidate / modified-node bitmaps.
+bool kp_cons_plan_lds(const KpDev& d, KpCons& k, int max_bytes) {
+    auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    size_t off = al(sizeof(ConsShared));
+    k.off_hdr = (int)off;
+    off = al(off + sizeof(ReqHdr) * (size_t)(d.K > 0 ? d.K : 1));
+    k.off_words = (int)off;
+    off = al(off + 8 * (size_t)(d.DW > 0 ? d.DW : 1));
+    k.off_rem = (int)off;
+    off = al(off + 8 * (size_t)(d.NT * d.R > 0 ? d.NT * d.R : 1));
+    k.off_excl = (int)off;
+    off = al(off + 8 * (size_t)(d.EW > 0 ? d.EW : 1));
+    k.off_mod = (int)off;
+    off = al(off + 8 * (size_t)(d.EW > 0 ? d.EW : 1));
+    k.lds_bytes = (int)off;
+    return (int)off <= max_bytes;
+}
+
+hipError_t kp_launch_consolidate(const KpDev& d, const KpCons& k, int n_workers, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)consolidate_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           KP_LDS_BYTES);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    if (n_workers <= 0 || k.n_probes <= 0) return hipSuccess;
+    hipLaunchKernelGGL(consolidate_kernel, dim3(n_workers), dim3(64), (size_t)k.lds_bytes, s, d, k);
+    return hipGetLastError();
+}
+
+hipError_t kp_launch_cons_prep(const int32_t* queue0, int P, int32_t* rank, const int32_t* pending, int n_pending,
+                               uint64_t* pend_bits, hipStream_t s) {
+    if (P > 0) hipLaunchKernelGGL(rank_kernel, dim3((P + 255) / 256), dim3(256), 0, s, queue0, rank, P);
+    if (n_pending > 0)
+        hipLaunchKernelGGL(pending_bits_kernel, dim3((n_pending + 255) / 256), dim3(256), 0, s, pending, n_pending,
+                           rank, pend_bits);
+    return hipGetLastError();
+}

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -17,6 +18,7 @@
 #include <vector>
 
 #include "../../include/kpsim.h"
+#include "kp_cons.h"
 #include "kp_layout.h"
 
 size_t kp_ffd_shared_bytes();
@@ -26,6 +28,11 @@ hipError_t kp_launch_template_init(const KpDev& d, hipStream_t s);
 hipError_t kp_launch_existing(const KpDev& d, hipStream_t s);
 hipError_t kp_launch_ffd(const KpDev& d, hipStream_t s);
 hipError_t kp_launch_finalize(const KpDev& d, int n_nodeclaims, hipStream_t s);
+struct KpCons;
+bool kp_cons_plan_lds(const KpDev& d, KpCons& k, int max_bytes);
+hipError_t kp_launch_consolidate(const KpDev& d, const KpCons& k, int n_workers, hipStream_t s);
+hipError_t kp_launch_cons_prep(const int32_t* queue0, int P, int32_t* rank, const int32_t* pending, int n_pending,
+                               uint64_t* pend_bits, hipStream_t s);
 hipError_t kp_queue_sort(const int64_t* fields, int n, int32_t* perm_a, int32_t* perm_b, uint64_t* keys_a,
                          uint64_t* keys_b, void* temp, size_t* temp_bytes, hipStream_t s, int32_t** result);
 
@@ -225,6 +232,17 @@ struct kp_ctx {
     hipEvent_t ev[6] = {};
     double kernel_ms[5] = {};
     int64_t cycles[30] = {};  // FFD phases (s_memtime): pop, sort, scan+eval, templates, commit, full pdqsort
+    bool any_min_values = false;             // some template requirement carries minValues
+    bool cons_mayfix = false;                // a pod's NotIn/DoesNotExist merge can change a later Compatible
+    // consolidation probes
+    DBuf<int32_t> d_rank, d_cand_i, d_cand_off, d_cand_pods, d_pending, d_ring, d_ring_last, d_next;
+    DBuf<double> d_cand_price;
+    DBuf<int64_t> d_cand_cap, d_delta, d_alloc_act, d_cons_stats;
+    DBuf<uint64_t> d_pend_bits, d_pbits;
+    DBuf<uint8_t> d_init;
+    DBuf<kp_probe_result> d_probe_out;
+    double cons_ms[3] = {};                  // device prep (sort, masks), probe kernel, whole call
+    int64_t cons_stats[CS_COUNT] = {};
     // last results (host)
     int last_N = 0, M = 0;
     std::vector<int32_t> h_nc_tmpl;
@@ -297,6 +315,10 @@ extern "C" kp_status kp_ctx_destroy(kp_ctx* ctx) {
     ctx->d_nc_count.release(); ctx->d_nc_npods.release(); ctx->d_nc_slice_pos.release(); ctx->d_nc_nopts.release();
     ctx->d_nc_valid.release(); ctx->d_nc_types.release(); ctx->d_nc_ntypes.release(); ctx->d_err.release();
     ctx->d_sort_temp.release();
+    ctx->d_rank.release(); ctx->d_cand_i.release(); ctx->d_cand_off.release(); ctx->d_pending.release(); ctx->d_cand_pods.release(); ctx->d_ring.release();
+    ctx->d_ring_last.release(); ctx->d_next.release(); ctx->d_cand_price.release(); ctx->d_cand_cap.release();
+    ctx->d_delta.release(); ctx->d_alloc_act.release(); ctx->d_cons_stats.release(); ctx->d_pend_bits.release();
+    ctx->d_pbits.release(); ctx->d_init.release(); ctx->d_probe_out.release();
     for (auto& e : ctx->ev)
         if (e) hipEventDestroy(e);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
@@ -660,6 +682,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     HIPCHK(hipSetDevice(ctx->device));
     kp_ctx* c = ctx;
     c->prepared = c->executed = false;
+    c->any_min_values = false;
     if (in->min_values_policy != KP_MIN_VALUES_STRICT)
         return fail(ctx, KP_E_UNSUPPORTED, "MIN_VALUES_POLICY=BestEffort is not supported by this build");
     const int T = c->T, TW = c->TW, R = c->R, P = in->pods.n_pods, C = in->n_classes;
@@ -705,6 +728,29 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     }
     const int K = (int)c->sol.keys.size();
     if (K > KP_MAX_KEYS) return fail(ctx, KP_E_UNSUPPORTED, "too many label keys");
+    // ExistingNode.Add's requirement merge only changes a node when a NotIn / DoesNotExist pod requirement meets a key
+    // the node lacks, and that change only alters a later Compatible for a class constraining the key positively
+    // (In / Exists / Gt / Lt).  Consolidation probes treat node requirements as immutable, which needs this to be false.
+    {
+        std::vector<uint8_t> neg(K, 0), pos(K, 0), undef(K, 0);
+        for (int i = 0; i < C; i++)
+            for (auto& kv : creq[i]) {
+                const HReq& q = kv.second;
+                const bool ng = (q.complement && !q.vals.empty()) || (!q.complement && q.vals.empty());
+                (ng ? neg : pos)[kv.first] = 1;
+            }
+        std::vector<uint8_t> has(K, 0);
+        for (int j = 0; j < E; j++) {
+            for (auto& kv : exlab[j]) has[kv.first] = 1;
+            for (int k = 0; k < K; k++) {
+                if (!has[k]) undef[k] = 1;
+            }
+            for (auto& kv : exlab[j]) has[kv.first] = 0;
+        }
+        c->cons_mayfix = false;
+        for (int k = 0; k < K; k++)
+            if (neg[k] && pos[k] && undef[k]) c->cons_mayfix = true;
+    }
     // ---- key layout ----
     std::vector<uint32_t> kflags(K, 0);
     std::vector<int32_t> kcat(K, -1), kmulti(K, -1), woff(K), nw(K), nval(K), vbase(K);
@@ -784,7 +830,10 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         if (!encode(C + j, treq[j])) return fail(ctx, KP_E_UNSUPPORTED, "NodePool constrains too many labels");
         int q = 0;
         for (auto& kv : treq[j])
-            if (kv.second.has_min) min_keys[(size_t)j * KP_MAX_CLASS_KEYS + q++] = kv.first;
+            if (kv.second.has_min) {
+                min_keys[(size_t)j * KP_MAX_CLASS_KEYS + q++] = kv.first;
+                c->any_min_values = true;
+            }
     }
     // ---- templates: taints, daemon overhead, limits, instance-type rows ----
     std::vector<uint32_t> tol(std::max(C, 1), 0);
@@ -1298,5 +1347,201 @@ extern "C" kp_status kp_result_nodeclaim_requirements(kp_ctx* ctx, int32_t nc, c
     if (needed) *needed = (int64_t)s.size() + 1;
     if ((int64_t)s.size() + 1 > cap || !buf) return KP_E_BUFFER;
     memcpy(buf, s.c_str(), s.size() + 1);
+    return KP_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// consolidation probes (kp_consolidate): encode the cluster with kp_solve_prepare, then one wave per probe
+// ---------------------------------------------------------------------------------------------
+extern "C" int32_t kp_consolidate_probe_count(const kp_consolidate_input* in) {
+    if (!in) return 0;
+    const int n = in->n_candidates;
+    if (in->mode == KP_CONSOLIDATE_SINGLE) return n > 0 ? n : 0;
+    if (n < 2) return 0;
+    const int mx = in->max_candidates > 0 ? in->max_candidates : 100;
+    return n <= mx ? n - 1 : mx;  // firstNConsolidationOption: mid in [1, max], prefix candidates[0 : mid+1]
+}
+
+extern "C" kp_status kp_consolidate(kp_ctx* ctx, const kp_consolidate_input* in, kp_probe_result* results,
+                                    int32_t cap_results) try {
+    if (!ctx || !in) return KP_E_INVALID;
+    if (in->mode != KP_CONSOLIDATE_SINGLE && in->mode != KP_CONSOLIDATE_MULTI)
+        return fail(ctx, KP_E_INVALID, "unknown consolidation mode");
+    const int np = kp_consolidate_probe_count(in);
+    const int b0 = in->probe_begin > 0 ? in->probe_begin : 0;
+    const int b1 = in->probe_end > 0 && in->probe_end < np ? in->probe_end : np;
+    if (b0 > b1) return fail(ctx, KP_E_INVALID, "probe range outside the probe list");
+    const int nprobe = b1 - b0;
+    if (nprobe > cap_results || (nprobe > 0 && !results)) return fail(ctx, KP_E_BUFFER, "probe results buffer too small");
+    const kp_solve_input& cl = in->cluster;
+    const int P = cl.pods.n_pods, E = cl.n_existing, NC = in->n_candidates;
+    // inputs: candidates on distinct nodes, each pod pending or owned by one candidate, prices >= 0
+    {
+        std::vector<uint8_t> seen_pod(std::max(P, 1), 0), seen_node(std::max(E, 1), 0);
+        for (int i = 0; i < in->n_pending; i++) {
+            const int p = in->pending[i];
+            if (p < 0 || p >= P || seen_pod[p]++) return fail(ctx, KP_E_INVALID, "pending pod out of range or repeated");
+        }
+        for (int ci = 0; ci < NC; ci++) {
+            const kp_candidate& cd = in->candidates[ci];
+            if (cd.node < 0 || cd.node >= E || seen_node[cd.node]++) return fail(ctx, KP_E_INVALID, "candidate node out of range or repeated");
+            if (!(cd.price >= 0) || cd.price > DBL_MAX) return fail(ctx, KP_E_INVALID, "candidate price must be finite and >= 0");
+            if (cd.n_pods < 0 || (cd.n_pods > 0 && !cd.pods)) return fail(ctx, KP_E_INVALID, "candidate pods");
+            for (int i = 0; i < cd.n_pods; i++) {
+                const int p = cd.pods[i];
+                if (p < 0 || p >= P || seen_pod[p]++) return fail(ctx, KP_E_INVALID, "candidate pod out of range or repeated");
+            }
+        }
+    }
+    if (nprobe == 0) return KP_OK;
+    kp_status st = kp_solve_prepare(ctx, &cl);
+    if (st != KP_OK) return st;
+    HIPCHK(hipSetDevice(ctx->device));
+    kp_ctx* c = ctx;
+    KpDev d = c->dev;
+    if (c->any_min_values) return fail(ctx, KP_E_UNSUPPORTED, "consolidation with minValues NodePools is not supported by this build");
+    if (c->cons_mayfix)
+        return fail(ctx, KP_E_UNSUPPORTED, "consolidation with NotIn/DoesNotExist pod requirements on keys some node lacks "
+                                           "and other pods select positively is not supported by this build");
+    if (d.n_active > KP_LDS_AXES) return fail(ctx, KP_E_UNSUPPORTED, "more than 6 requested resource axes");
+    if (d.M <= 0 || d.M > 64) return fail(ctx, KP_E_UNSUPPORTED, "consolidation needs max_instance_types in 1..64");
+    const int T = c->T, TW = c->TW, R = c->R, A = d.n_active;
+    d.lds_A = 0;  // no quick-accept witness in probes
+    d.lds_nstage = A;
+    d.profile = 0;
+    hipStream_t s = c->stream;
+    KpCons k{};
+    k.n_probes = nprobe;
+    k.probe0 = b0;
+    k.mode = in->mode;
+    k.n_cand = NC;
+    k.spot_to_spot = in->spot_to_spot ? 1 : 0;
+    k.v_spot = k.v_od = -1;
+    if (c->key_ct >= 0) {
+        k.v_spot = c->sol.keys[c->key_ct].find("spot");
+        k.v_od = c->sol.keys[c->key_ct].find("on-demand");
+    }
+    for (int sl = 0; sl < c->n_slots; sl++) {
+        if (c->slot_ct[sl] == k.v_spot && k.v_spot >= 0) k.spot_slots |= 1ull << sl;
+        if (c->slot_ct[sl] == k.v_od && k.v_od >= 0) k.od_slots |= 1ull << sl;
+    }
+    std::vector<int> np_tmpl(cl.n_nodepools, -1);
+    for (int j = 0; j < (int)c->tmpl_np.size(); j++) np_tmpl[c->tmpl_np[j]] = j;
+    std::vector<int32_t> ci((size_t)std::max(NC, 1) * 4, 0), coff(NC + 1, 0), cpods;
+    std::vector<double> cprice(std::max(NC, 1), 0.0);
+    std::vector<int64_t> ccap((size_t)std::max(NC, 1) * R, 0);
+    for (int i = 0; i < NC; i++) {
+        const kp_candidate& cd = in->candidates[i];
+        ci[i * 4 + 0] = cd.node;
+        ci[i * 4 + 1] = cd.capacity_type;
+        ci[i * 4 + 2] = cd.instance_type >= 0 && cd.instance_type < T ? cd.instance_type : -1;
+        ci[i * 4 + 3] = cd.nodepool >= 0 && cd.nodepool < cl.n_nodepools && cd.capacity ? np_tmpl[cd.nodepool] : -1;
+        cprice[i] = cd.price;
+        if (cd.capacity)
+            for (int r = 0; r < R; r++) ccap[(size_t)i * R + r] = cd.capacity[r];
+        coff[i + 1] = coff[i] + cd.n_pods;
+        for (int q = 0; q < cd.n_pods; q++) cpods.push_back(cd.pods[q]);
+    }
+    if (cpods.empty()) cpods.push_back(0);
+    // ring capacity: pods of the largest probe
+    int maxp = 0;
+    if (in->mode == KP_CONSOLIDATE_SINGLE) {
+        for (int i = b0; i < b1; i++) maxp = std::max(maxp, coff[i + 1] - coff[i]);
+    } else {
+        maxp = coff[std::min(NC, b1 + 1)];
+    }
+    k.ring_cap = std::max(1, in->n_pending + maxp);
+    std::vector<int32_t> pend(in->pending, in->pending + in->n_pending);
+    if (pend.empty()) pend.push_back(0);
+    std::vector<uint8_t> init(std::max(E, 1), 1);
+    if (in->initialized)
+        for (int j = 0; j < E; j++) init[j] = in->initialized[j] ? 1 : 0;
+    const int astride = TW * 64;
+    std::vector<int64_t> act((size_t)std::max(A, 1) * astride, 0);
+    for (int ai = 0; ai < A; ai++)
+        for (int t = 0; t < T; t++) act[(size_t)ai * astride + t] = c->alloc_rt[(size_t)d.active_axes[ai] * T + t];
+    k.PW = std::max(1, (P + 63) / 64);
+    if (!kp_cons_plan_lds(d, k, KP_LDS_BYTES)) return fail(ctx, KP_E_UNSUPPORTED, "consolidation LDS plan exceeds 160 KB");
+    int occ = std::max(1, std::min(8, KP_LDS_BYTES / std::max(k.lds_bytes, 1)));
+    int workers = std::min(nprobe, 256 * occ);
+    const auto t0 = clk::now();
+    HIPCHK(c->d_cand_i.upload(ci, s));
+    HIPCHK(c->d_cand_pods.upload(cpods, s));
+    HIPCHK(c->d_cand_price.upload(cprice, s));
+    HIPCHK(c->d_cand_cap.upload(ccap, s));
+    HIPCHK(c->d_init.upload(init, s));
+    HIPCHK(c->d_alloc_act.upload(act, s));
+    HIPCHK(c->d_cand_off.upload(coff, s));
+    HIPCHK(c->d_pending.upload(pend, s));
+    HIPCHK(c->d_next.ensure(1));
+    HIPCHK(c->d_rank.ensure(std::max(P, 1)));
+    HIPCHK(c->d_pend_bits.ensure(k.PW));
+    HIPCHK(hipMemsetAsync(c->d_pend_bits.p, 0, (size_t)k.PW * 8, s));
+    HIPCHK(c->d_ring.ensure((size_t)workers * k.ring_cap));
+    HIPCHK(c->d_ring_last.ensure((size_t)workers * k.ring_cap));
+    HIPCHK(c->d_delta.ensure((size_t)workers * std::max(A, 1) * std::max(E, 1)));
+    HIPCHK(c->d_pbits.ensure((size_t)workers * k.PW));
+    HIPCHK(hipMemsetAsync(c->d_pbits.p, 0, (size_t)workers * k.PW * 8, s));
+    HIPCHK(c->d_probe_out.ensure(nprobe));
+    HIPCHK(c->d_cons_stats.ensure(CS_COUNT));
+    HIPCHK(hipMemsetAsync(c->d_cons_stats.p, 0, CS_COUNT * sizeof(int64_t), s));
+    HIPCHK(hipMemsetAsync(c->d_next.p, 0, sizeof(int32_t), s));
+    if (!c->h_remaining.empty())
+        HIPCHK(hipMemcpyAsync(c->d_remaining.p, c->h_remaining.data(), c->h_remaining.size() * sizeof(int64_t),
+                              hipMemcpyHostToDevice, s));
+    HIPCHK(hipEventRecord(c->ev[0], s));
+    int32_t* q0 = nullptr;
+    if (P > 0) {
+        size_t tb = c->sort_temp_bytes;
+        HIPCHK(kp_queue_sort(c->d_sort_fields.p, P, c->d_perm_a.p, c->d_perm_b.p, c->d_keys_a.p, c->d_keys_b.p,
+                             c->d_sort_temp.p, &tb, s, &q0));
+    }
+    d.queue0 = q0;
+    HIPCHK(kp_launch_cons_prep(q0, P, c->d_rank.p, c->d_pending.p, in->n_pending, c->d_pend_bits.p, s));
+    HIPCHK(kp_launch_class_mask(d, s));
+    HIPCHK(kp_launch_template_init(d, s));
+    HIPCHK(kp_launch_existing(d, s));
+    HIPCHK(hipEventRecord(c->ev[1], s));
+    k.cand_i = c->d_cand_i.p;
+    k.cand_off = c->d_cand_off.p;
+    k.cand_pods = c->d_cand_pods.p;
+    k.cand_price = c->d_cand_price.p;
+    k.cand_cap = c->d_cand_cap.p;
+    k.rank = c->d_rank.p;
+    k.pend_bits = c->d_pend_bits.p;
+    k.initialized = c->d_init.p;
+    k.alloc_act = c->d_alloc_act.p;
+    k.astride = astride;
+    k.ring = c->d_ring.p;
+    k.ring_last = c->d_ring_last.p;
+    k.delta = c->d_delta.p;
+    k.pbits = c->d_pbits.p;
+    k.next_probe = c->d_next.p;
+    k.out = c->d_probe_out.p;
+    k.stats = c->d_cons_stats.p;
+    HIPCHK(kp_launch_consolidate(d, k, workers, s));
+    HIPCHK(hipEventRecord(c->ev[2], s));
+    HIPCHK(hipMemcpyAsync(results, c->d_probe_out.p, (size_t)nprobe * sizeof(kp_probe_result), hipMemcpyDeviceToHost, s));
+    int64_t cst[CS_COUNT];
+    HIPCHK(hipMemcpyAsync(cst, c->d_cons_stats.p, sizeof cst, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+    c->cons_ms[0] = ms;
+    HIPCHK(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
+    c->cons_ms[1] = ms;
+    c->cons_ms[2] = ns_since(t0) * 1e-6;
+    for (int i = 0; i < CS_COUNT; i++) c->cons_stats[i] = cst[i];
+    return KP_OK;
+} catch (const std::exception& e) {
+    return fail(ctx, KP_E_INVALID, e.what());
+}
+
+extern "C" kp_status kp_consolidate_stats(kp_ctx* ctx, double* ms, int64_t* counters, int32_t n_counters) {
+    if (!ctx) return KP_E_INVALID;
+    if (ms)
+        for (int i = 0; i < 3; i++) ms[i] = ctx->cons_ms[i];
+    if (counters)
+        for (int i = 0; i < n_counters && i < CS_COUNT; i++) counters[i] = ctx->cons_stats[i];
     return KP_OK;
 }

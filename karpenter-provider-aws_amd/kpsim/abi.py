@@ -103,6 +103,36 @@ class kp_solve_output(C.Structure):
                 ("pod_order", c_int32_p), ("stats", kp_solve_stats)]
 
 
+KP_CONSOLIDATE_SINGLE, KP_CONSOLIDATE_MULTI = 0, 1
+KP_DECISION_NONE, KP_DECISION_DELETE, KP_DECISION_REPLACE = 0, 1, 2
+KP_CT_ON_DEMAND, KP_CT_SPOT, KP_CT_RESERVED = 0, 1, 2
+
+
+class kp_candidate(C.Structure):
+    _fields_ = [("node", C.c_int32), ("n_pods", C.c_int32), ("pods", c_int32_p), ("price", C.c_double),
+                ("capacity_type", C.c_int32), ("instance_type", C.c_int32), ("nodepool", C.c_int32),
+                ("capacity", c_int64_p)]
+
+
+class kp_consolidate_input(C.Structure):
+    _fields_ = [("cluster", kp_solve_input), ("initialized", c_uint8_p), ("n_pending", C.c_int32),
+                ("pending", c_int32_p), ("n_candidates", C.c_int32), ("candidates", C.POINTER(kp_candidate)),
+                ("mode", C.c_int32), ("max_candidates", C.c_int32), ("probe_begin", C.c_int32),
+                ("probe_end", C.c_int32), ("spot_to_spot", C.c_int32)]
+
+
+class kp_probe_result(C.Structure):
+    _fields_ = [("decision", C.c_int32), ("valid", C.c_int32), ("all_scheduled", C.c_int32),
+                ("n_new_nodeclaims", C.c_int32), ("n_replacement_types", C.c_int32), ("n_pods", C.c_int32),
+                ("candidate_price", C.c_double), ("replacement_price", C.c_double)]
+
+
+PROBE_DTYPE = np.dtype([("decision", np.int32), ("valid", np.int32), ("all_scheduled", np.int32),
+                        ("n_new_nodeclaims", np.int32), ("n_replacement_types", np.int32), ("n_pods", np.int32),
+                        ("candidate_price", np.float64), ("replacement_price", np.float64)])
+assert PROBE_DTYPE.itemsize == C.sizeof(kp_probe_result)
+
+
 class kp_device_opts(C.Structure):
     _fields_ = [("device", C.c_int32), ("reserved0", C.c_int32)]
 

@@ -1,0 +1,149 @@
+"""Reference-shaped consolidation on the gfx950 library, sharded over ranks.
+
+Mirrors [core] sigs.k8s.io/karpenter pkg/controllers/disruption (recalled):
+  SingleNodeConsolidation.ComputeCommand — candidates in disruption-cost order, the first whose
+      computeConsolidation is not a no-op wins (singlenodeconsolidation.go);
+  MultiNodeConsolidation.firstNConsolidationOption — binary search over the prefix length, a prefix is kept when its
+      command is DELETE or a REPLACE whose options survive filterOutSameInstanceType (multinodeconsolidation.go).
+Every probe those loops could evaluate is independent, so the probes are evaluated in parallel (kp_consolidate; one
+wave per probe; one shard of probes per GPU) and the loops are replayed over the results: the decision is the one
+the sequential code would reach.  Across ranks the only exchange is the result vector: an all-reduce MIN of the first
+valid single-node index, or an all-gather of the multi-node prefix results.
+"""
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import abi, model, native
+
+
+@dataclass
+class Command:
+    decision: int                   # abi.KP_DECISION_*
+    candidates: list                # indices into ConsolidationProblem.candidates
+    n_replacement_types: int = 0
+    candidate_price: float = 0.0
+    replacement_price: float = 0.0
+
+
+NO_OP = Command(abi.KP_DECISION_NONE, [])
+
+
+def first_valid_single(results: np.ndarray, probe0: int = 0) -> int:
+    """Index (global probe id) of the first non-NONE single-node probe, or -1."""
+    idx = np.nonzero(results["decision"] != abi.KP_DECISION_NONE)[0]
+    return int(idx[0]) + probe0 if len(idx) else -1
+
+
+def replay_multi(results: np.ndarray, n_candidates: int, max_candidates: int = 100) -> int:
+    """firstNConsolidationOption's binary search over probe results (probe i = prefix of i+2 candidates).
+    Returns the chosen probe index or -1."""
+    if n_candidates < 2:
+        return -1
+    lo, hi = 1, max_candidates
+    if n_candidates <= hi:
+        hi = n_candidates - 1
+    best = -1
+    while lo <= hi:
+        mid = (lo + hi) // 2
+        r = results[mid - 1]
+        if r["valid"]:
+            best = mid - 1
+            lo = mid + 1
+        else:
+            hi = mid - 1
+    return best
+
+
+def _command(cp, results, probe, mode) -> Command:
+    if probe < 0:
+        return NO_OP
+    r = results[probe]
+    cands = [probe] if mode == abi.KP_CONSOLIDATE_SINGLE else list(range(probe + 2))
+    return Command(int(r["decision"]), cands, int(r["n_replacement_types"]), float(r["candidate_price"]),
+                   float(r["replacement_price"]))
+
+
+def shard_range(n_probes, rank, world):
+    """Contiguous probe shard of a rank (disruption-cost order is kept inside each shard)."""
+    per = (n_probes + world - 1) // world if world else n_probes
+    b0 = min(n_probes, rank * per)
+    return b0, min(n_probes, b0 + per)
+
+
+def compute_command(cp: model.ConsolidationProblem, mode, probe_fn, max_candidates=100, group=None) -> Command:
+    """ComputeCommand for one mode.  probe_fn(cp, mode, begin, end) evaluates probes [begin, end) (kp_consolidate on
+    this rank's GPU).  With a torch.distributed group the probes are sharded across its ranks and one collective
+    carries each rank's result: the first valid single-node probe of the shard, or the shard's multi-node rows."""
+    n = model.consolidation_probe_count(len(cp.candidates), mode, max_candidates)
+    if n == 0:
+        return NO_OP
+    if group is None and not _dist_on():
+        res = probe_fn(cp, mode, 0, 0)
+        probe = first_valid_single(res) if mode == abi.KP_CONSOLIDATE_SINGLE else \
+            replay_multi(res, len(cp.candidates), max_candidates)
+        return _command(cp, res, probe, mode)
+    import torch
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    b0, b1 = shard_range(n, rank, world)
+    res = probe_fn(cp, mode, b0, b1) if b1 > b0 else np.zeros(0, abi.PROBE_DTYPE)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else \
+        torch.device("cpu")
+    if mode == abi.KP_CONSOLIDATE_SINGLE:
+        loc = first_valid_single(res, b0)
+        row = np.zeros(1, abi.PROBE_DTYPE)
+        if loc >= 0:
+            row[0] = res[loc - b0]
+        msg = np.concatenate([np.array([loc if loc >= 0 else n], np.int64).view(np.uint8), row.view(np.uint8)])
+        t = torch.from_numpy(msg).to(dev)
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t, group=group)
+        best, best_row = n, None
+        for p_ in parts:
+            a = p_.cpu().numpy()
+            i = int(a[:8].view(np.int64)[0])
+            if i < best:
+                best, best_row = i, a[8:].view(abi.PROBE_DTYPE)
+        if best >= n:
+            return NO_OP
+        full = np.zeros(n, abi.PROBE_DTYPE)
+        full[best] = best_row[0]
+        return _command(cp, full, best, mode)
+    per = (n + world - 1) // world
+    pad = np.zeros(per, abi.PROBE_DTYPE)
+    pad[:len(res)] = res
+    loc = torch.from_numpy(pad.view(np.uint8).copy()).to(dev)
+    parts = [torch.empty_like(loc) for _ in range(world)]
+    dist.all_gather(parts, loc, group=group)
+    full = np.concatenate([p_.cpu().numpy().view(abi.PROBE_DTYPE) for p_ in parts])[:n]
+    probe = replay_multi(full, len(cp.candidates), max_candidates)
+    return _command(cp, full, probe, mode)
+
+
+def _dist_on():
+    try:
+        import torch.distributed as dist
+        return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    except Exception:
+        return False
+
+
+class Consolidator:
+    """Evaluates consolidation probes on one GPU (one kp_ctx); under torch.distributed, one rank of the pass."""
+
+    def __init__(self, catalog, device=0, ctx: Optional[native.Context] = None, spot_to_spot=False,
+                 max_candidates=100):
+        self.ctx = ctx or native.Context(device)
+        self.catalog_view = model.CatalogView(catalog)
+        self.ctx.upload_catalog(self.catalog_view)
+        self.spot_to_spot = spot_to_spot
+        self.max_candidates = max_candidates
+
+    def probes(self, cp: model.ConsolidationProblem, mode, begin=0, end=0, cluster_view=None) -> np.ndarray:
+        v = model.ConsolidateInputView(cp, mode, begin, end, self.spot_to_spot, self.max_candidates, cluster_view)
+        return self.ctx.consolidate(v)
+
+    def compute_command(self, cp: model.ConsolidationProblem, mode, group=None) -> Command:
+        return compute_command(cp, mode, lambda c, m, b0, b1: self.probes(c, m, b0, b1), self.max_candidates, group)

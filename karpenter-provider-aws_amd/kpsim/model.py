@@ -155,6 +155,37 @@ class Problem:
     min_values_policy: int = 0
 
 
+@dataclass
+class Candidate:
+    """disruption.Candidate: a state node considered for consolidation."""
+    node: int                       # index into ConsolidationProblem.cluster.existing
+    pods: np.ndarray                # reschedulable pods, indices into cluster.pods
+    price: float                    # cheapest offering of its instance type compatible with the node's labels
+    capacity_type: int = abi.KP_CT_ON_DEMAND
+    instance_type: int = -1         # catalog row
+    nodepool: int = -1              # index into cluster.nodepools
+    capacity: Optional[np.ndarray] = None  # [R] node capacity (returns to the NodePool's limits)
+
+
+@dataclass
+class ConsolidationProblem:
+    """Cluster state of one consolidation pass: the Problem's existing nodes are ALL state nodes in NewScheduler
+    order (initialized first, then by name); its pods are the pending pods plus every candidate's pods."""
+    cluster: Problem
+    candidates: List[Candidate]
+    pending: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int32))
+    initialized: Optional[np.ndarray] = None  # [E] uint8
+
+
+def consolidation_probe_count(n_candidates, mode, max_candidates=100):
+    """Same numbering as kp_consolidate_probe_count (include/kpsim.h)."""
+    if mode == abi.KP_CONSOLIDATE_SINGLE:
+        return n_candidates
+    if n_candidates < 2:
+        return 0
+    return n_candidates - 1 if n_candidates <= max_candidates else max_candidates
+
+
 # ------------------------------------------------------------------------------------------------
 # views
 # ------------------------------------------------------------------------------------------------
@@ -349,3 +380,38 @@ def parse_requirements_blob(s: str):
         key, comp, gt, lt, mn, vals = line.split("\t")
         out[key] = (comp == "1", gt, lt, mn, tuple(v for v in vals.split("\x1f") if v != "") if vals else ())
     return out
+
+
+class ConsolidateInputView:
+    """kp_consolidate_input for a ConsolidationProblem, probes [probe_begin, probe_end)."""
+
+    def __init__(self, cp: ConsolidationProblem, mode, probe_begin=0, probe_end=0, spot_to_spot=False,
+                 max_candidates=100, cluster_view: Optional[SolveInputView] = None):
+        self.cluster_view = cluster_view or SolveInputView(cp.cluster)
+        k = self.keep = abi.Keep()
+        v = self.view = abi.kp_consolidate_input()
+        v.cluster = self.cluster_view.view
+        if cp.initialized is not None:
+            v.initialized = k.ptr(cp.initialized, np.uint8, C.c_uint8)
+        v.n_pending = len(cp.pending)
+        v.pending = k.ptr(cp.pending, np.int32, C.c_int32)
+        cands = (abi.kp_candidate * max(1, len(cp.candidates)))()
+        for i, c in enumerate(cp.candidates):
+            x = cands[i]
+            x.node = int(c.node)
+            x.n_pods = len(c.pods)
+            x.pods = k.ptr(c.pods, np.int32, C.c_int32)
+            x.price = float(c.price)
+            x.capacity_type = int(c.capacity_type)
+            x.instance_type = int(c.instance_type)
+            x.nodepool = int(c.nodepool)
+            if c.capacity is not None:
+                x.capacity = k.ptr(c.capacity, np.int64, C.c_int64)
+        k.hold(cands)
+        v.n_candidates = len(cp.candidates)
+        v.candidates = cands
+        v.mode = int(mode)
+        v.max_candidates = int(max_candidates)
+        v.probe_begin = int(probe_begin)
+        v.probe_end = int(probe_end)
+        v.spot_to_spot = 1 if spot_to_spot else 0

@@ -10,7 +10,8 @@ LIB_PATH = os.path.join(PKG_DIR, "..", "lib", "libkpsim.so")
 EXPORTS = [
     "kp_ctx_create", "kp_ctx_destroy", "kp_last_error", "kp_version", "kp_catalog_upload", "kp_catalog_patch_avail",
     "kp_catalog_patch_price", "kp_solve", "kp_solve_prepare", "kp_solve_execute", "kp_solve_fetch",
-    "kp_result_nodeclaim_requirements", "kp_last_kernel_times",
+    "kp_result_nodeclaim_requirements", "kp_last_kernel_times", "kp_consolidate_probe_count", "kp_consolidate",
+    "kp_consolidate_stats",
 ]
 
 _lib = None
@@ -45,6 +46,10 @@ def load():
     L.kp_solve_fetch.argtypes = [C.c_void_p, C.POINTER(abi.kp_solve_output)]
     L.kp_result_nodeclaim_requirements.argtypes = [C.c_void_p, C.c_int32, C.c_char_p, C.c_int64, C.POINTER(C.c_int64)]
     L.kp_last_kernel_times.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_int32]
+    L.kp_consolidate_probe_count.argtypes = [C.POINTER(abi.kp_consolidate_input)]
+    L.kp_consolidate.argtypes = [C.c_void_p, C.POINTER(abi.kp_consolidate_input), C.POINTER(abi.kp_probe_result),
+                                 C.c_int32]
+    L.kp_consolidate_stats.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.c_int32]
     for f in EXPORTS:
         if f not in ("kp_last_error", "kp_version"):
             getattr(L, f).restype = C.c_int32
@@ -123,6 +128,25 @@ class Context:
         a = (C.c_double * 35)()
         self.check(self.L.kp_last_kernel_times(self.h, a, 35), "kp_last_kernel_times")
         return list(a)[5:]
+
+    def consolidate(self, cons_view):
+        """kp_consolidate over the view's probe range -> numpy array of abi.PROBE_DTYPE (one row per probe)."""
+        import numpy as np
+        v = cons_view.view
+        n = self.L.kp_consolidate_probe_count(C.byref(v))
+        b0 = max(0, v.probe_begin)
+        b1 = v.probe_end if 0 < v.probe_end < n else n
+        out = np.zeros(max(1, b1 - b0), abi.PROBE_DTYPE)
+        self.check(self.L.kp_consolidate(self.h, C.byref(v), out.ctypes.data_as(C.POINTER(abi.kp_probe_result)),
+                                         len(out)), "kp_consolidate")
+        return out[:max(0, b1 - b0)]
+
+    def consolidate_stats(self):
+        """(ms[prep, probe kernel, call], counters[8]) of the last kp_consolidate (kpsim.h kp_consolidate_stats)."""
+        ms = (C.c_double * 3)()
+        ct = (C.c_int64 * 8)()
+        self.check(self.L.kp_consolidate_stats(self.h, ms, ct, 8), "kp_consolidate_stats")
+        return list(ms), list(ct)
 
     def close(self):
         if getattr(self, "h", None):

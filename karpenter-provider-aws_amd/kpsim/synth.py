@@ -9,8 +9,9 @@ from typing import Dict, List, Optional
 import numpy as np
 
 from .catalog import golden_catalog, parse_quantity_milli
-from .model import (ARCH, CAPACITY_TYPE, R, RIDX, ZONE, NodePool, PodClass, Pods, Problem, Requirement, Taint,
-                    Toleration)
+from . import abi
+from .model import (ARCH, CAPACITY_TYPE, NODEPOOL, R, RIDX, ZONE, Candidate, ConsolidationProblem, ExistingNode,
+                    NodePool, PodClass, Pods, Problem, Requirement, Taint, Toleration)
 
 SEED = 20250912
 AWS = "karpenter.k8s.aws/"
@@ -139,3 +140,146 @@ def subsample(prob: Problem, n_pods: int, seed=SEED) -> Problem:
     pods = Pods(p.class_id[idx].copy(), p.requests[idx].copy(), p.creation_ns[idx].copy(), [p.uids[i] for i in idx])
     return Problem(prob.catalog, prob.nodepools, prob.classes, pods, prob.existing, prob.max_instance_types,
                    prob.min_values_policy)
+
+
+# ------------------------------------------------------------------------------------------------
+# consolidation (BASELINE configs[3])
+# ------------------------------------------------------------------------------------------------
+def node_labels(it, zone, capacity_type, nodepool=None):
+    """Labels of a launched node of type `it`: the type's single-valued labels plus zone / capacity-type."""
+    labels = {}
+    for k, v in it.labels.items():
+        if isinstance(v, (list, tuple)):
+            if len(v) == 1:
+                labels[k] = str(v[0])
+        elif v is not None:
+            labels[k] = str(v)
+    labels[ZONE] = zone
+    labels[CAPACITY_TYPE] = capacity_type
+    if nodepool:
+        labels[NODEPOOL] = nodepool
+    return labels
+
+
+def candidate_price(it, labels):
+    """getCandidatePrices term: Offerings.Compatible(NewLabelRequirements(node labels)).Cheapest().Price over ALL
+    offerings of the node's type (an offering matches on capacity-type and zone; reservation keys are DoesNotExist on
+    od/spot offerings, zone-id is well-known and undefined on the node).  None when nothing matches."""
+    best = None
+    for o in it.offerings:
+        if o.capacity_type != labels.get(CAPACITY_TYPE) or o.zone != labels.get(ZONE):
+            continue
+        if o.reservation_id and labels.get(abi_RESERVATION_ID) != o.reservation_id:
+            continue
+        best = o.price if best is None or o.price < best else best
+    return best
+
+
+abi_RESERVATION_ID = "karpenter.k8s.aws/capacity-reservation-id"
+
+
+def _selector_ok(req: Requirement, labels):
+    v = labels.get(req.key)
+    if req.op == "In":
+        return v is not None and v in req.values
+    if req.op == "NotIn":
+        return v is None or v not in req.values
+    if req.op == "Exists":
+        return v is not None
+    if req.op == "DoesNotExist":
+        return v is None
+    try:
+        x = int(v)
+    except (TypeError, ValueError):
+        return False
+    return x > int(req.values[0]) if req.op == "Gt" else x < int(req.values[0])
+
+
+def config4(n_nodes=5000, pods_per_node=(10, 30), n_classes=250, catalog=None, seed=SEED, n_pending=0,
+            util=(0.4, 0.6)) -> ConsolidationProblem:
+    """5k existing nodes with ~100k bound pods of config-2 classes at 40-60% utilisation (BASELINE configs[3]).
+
+    Each node: a NodePool (80% default spot/on-demand, 20% the tainted on-demand pool), a zone, a capacity type, then
+    the smallest catalog type (non-GPU, with an offering in that zone / capacity type) whose cpu and memory put the
+    node's pods at the drawn utilisation; its pods are drawn from the classes the node satisfies (selectors,
+    tolerations).  available = allocatable - bound pod requests.  Candidates = every node in disruption-cost order
+    (fewer pods first, then name); multi-node consolidation takes the first 100.  All nodes initialized."""
+    rng = np.random.Generator(np.random.PCG64(seed + 4))
+    catalog = catalog if catalog is not None else golden_catalog(seed=seed)
+    taint_key = "example.com/dedicated"
+    classes, creqs = _classes_config2(rng, n_classes, taint_key)
+    nodepools = [
+        default_nodepool("default", capacity_types=("spot", "on-demand"), weight=10),
+        NodePool(name="dedicated", weight=50, requirements=[Requirement(CAPACITY_TYPE, "In", ["on-demand"])],
+                 taints=[Taint(taint_key, "", "NoSchedule")]),
+    ]
+    creq_vec = np.zeros((n_classes, R), np.int64)
+    for c, r in enumerate(creqs):
+        for k, q in r.items():
+            creq_vec[c, RIDX[k]] = q
+        creq_vec[c, RIDX["pods"]] += 1000
+    gpu_free = [c for c in range(n_classes) if creq_vec[c, RIDX["nvidia.com/gpu"]] == 0]
+    w = rng.dirichlet(np.ones(n_classes) * 0.8)
+    types = [t for t, it in enumerate(catalog)
+             if it.allocatable[RIDX["nvidia.com/gpu"]] == 0 and it.allocatable[RIDX["cpu"]] >= 2000]
+    cpu_alloc = np.array([catalog[t].allocatable[RIDX["cpu"]] for t in types], np.int64)
+    mem_alloc = np.array([catalog[t].allocatable[RIDX["memory"]] for t in types], np.int64)
+    pods_alloc = np.array([catalog[t].allocatable[RIDX["pods"]] for t in types], np.int64)
+    by_cpu = np.lexsort((mem_alloc, cpu_alloc))
+    zones = ["test-zone-1a", "test-zone-1b", "test-zone-1c"]
+    nodes, specs, owner, cand_meta = [], [], [], []
+    for j in range(n_nodes):
+        dedicated = rng.random() < 0.2
+        pool = nodepools[1] if dedicated else nodepools[0]
+        ct = "on-demand" if dedicated or rng.random() < 0.5 else "spot"
+        zone = str(rng.choice(zones))
+        n = int(rng.integers(pods_per_node[0], pods_per_node[1] + 1))
+        u = float(rng.uniform(*util))
+        # draw classes tolerating the pool; selectors are checked once the type is known
+        pw = w[gpu_free] / w[gpu_free].sum()
+        cls = list(rng.choice(gpu_free, size=n, p=pw))
+        need_cpu = int(creq_vec[cls, RIDX["cpu"]].sum() / u)
+        need_mem = int(creq_vec[cls, RIDX["memory"]].sum() / u)
+        pick = None
+        for i in by_cpu:
+            if cpu_alloc[i] >= need_cpu and mem_alloc[i] >= need_mem and pods_alloc[i] >= n * 1000:
+                it = catalog[types[i]]
+                if any(o.zone == zone and o.capacity_type == ct and not o.reservation_id for o in it.offerings):
+                    pick = types[i]
+                    break
+        if pick is None:
+            pick = types[int(by_cpu[-1])]
+        it = catalog[pick]
+        labels = node_labels(it, zone, ct, pool.name)
+        ok = [c for c in gpu_free if all(_selector_ok(r, labels) for r in classes[c].requirements) and
+              (not dedicated or any(t.key == taint_key for t in classes[c].tolerations))]
+        okw = w[ok] / w[ok].sum()
+        for q in range(n):
+            c = cls[q]
+            if c not in ok:
+                cls[q] = int(rng.choice(ok, p=okw))
+        used = creq_vec[cls].sum(axis=0)
+        avail = np.array(it.allocatable, np.int64) - used
+        name = "node-%05d" % j
+        nodes.append(ExistingNode(name=name, labels=labels, available=avail, requests=np.zeros(R, np.int64),
+                                  taints=list(pool.taints)))
+        for c in cls:
+            specs.append((int(c), creqs[c]))
+            owner.append(j)
+        price = candidate_price(it, labels)
+        cand_meta.append((n, name, j, price, ct, pick, 1 if dedicated else 0, np.array(it.capacity, np.int64)))
+    # pending pods (unbound), created after the bound ones
+    for _ in range(n_pending):
+        c = int(rng.choice(gpu_free))
+        specs.append((c, creqs[c]))
+        owner.append(-1)
+    pods = _pods_from_milli(specs)
+    owner = np.array(owner, np.int64)
+    prob = Problem(catalog, nodepools, classes, pods, nodes)
+    order = np.argsort(owner[owner >= 0], kind="stable")
+    pods_of = np.split(np.nonzero(owner >= 0)[0][order], np.cumsum(np.bincount(owner[owner >= 0], minlength=n_nodes))[:-1])
+    cand_meta.sort(key=lambda m: (m[0], m[1]))
+    cands = [Candidate(node=m[2], pods=pods_of[m[2]].astype(np.int32), price=m[3],
+                       capacity_type=abi.KP_CT_SPOT if m[4] == "spot" else abi.KP_CT_ON_DEMAND, instance_type=m[5],
+                       nodepool=m[6], capacity=m[7]) for m in cand_meta]
+    return ConsolidationProblem(prob, cands, np.nonzero(owner < 0)[0].astype(np.int32), np.ones(n_nodes, np.uint8))

@@ -18,6 +18,12 @@ kp_status orc_solve(const kp_catalog_view* cat, const kp_solve_input* in, kp_sol
 kp_status orc_result_nodeclaim_requirements(const orc_result* res, int32_t nc, char* buf, int64_t cap, int64_t* needed);
 void orc_result_free(orc_result* res);
 
+/* Consolidation probes (SimulateScheduling + computeConsolidation), same probe numbering as kp_consolidate;
+ * probes are spread over n_threads std::threads (the cpu_baseline leg of config 4). */
+int32_t orc_consolidate_probe_count(const kp_consolidate_input* in);
+kp_status orc_consolidate(const kp_catalog_view* cat, const kp_consolidate_input* in, kp_probe_result* results,
+                          int32_t cap_results, int32_t n_threads);
+
 /* pkg/providers/instancetype/types.go:123-155,320-605 — capacity / overhead / allocatable arithmetic.
  * Resource axes (milli-units), fixed order ORC_R_*. */
 enum {

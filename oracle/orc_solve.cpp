@@ -18,12 +18,14 @@
 // pkg/providers/instancetype/offering/offering.go:103-196 (offering requirements) and
 // pkg/providers/instance/instance.go:62,293 (maxInstanceTypes = 60, Truncate).
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <cstdio>
 #include <cstring>
 #include <deque>
 #include <memory>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -130,20 +132,30 @@ struct Result {
 struct Solver {
     Dict& D;
     int R = 0;
-    std::vector<InstanceType> types;
+    std::vector<InstanceType> own_types;
+    const std::vector<InstanceType>* tp = &own_types;  // catalog rows (shared by consolidation probes)
     std::vector<Template> tmpls;
-    std::vector<PodClass> classes;
-    std::vector<Pod> pods;
-    std::vector<ExistingNode> existing;
-    std::vector<NodeClaim> ncs;       // creation order
+    std::vector<PodClass> own_classes;
+    const std::vector<PodClass>* cp = &own_classes;
+    std::vector<Pod> own_pods;
+    const std::vector<Pod>* pp = &own_pods;
+    std::vector<ExistingNode> own_existing;
+    const std::vector<ExistingNode>* ex_base = &own_existing;  // state nodes (shared by consolidation probes)
+    std::vector<int> ex_idx;                                 // existing nodes of this simulation, in order
+    std::unordered_map<int, ExistingNode> ex_mod;            // copy-on-write: nodes that received pods
+    std::vector<int> plist;           // pods of this simulation (indices into *pp); all per-pod state is by position
+    std::vector<NodeClaim> ncs;       // creation order; nc.pods holds positions in plist
     std::vector<int> newNodeClaims;   // s.newNodeClaims slice (indices into ncs)
-    std::vector<int> pod_result, pod_order;
+    std::vector<int> pod_result, pod_order;  // by position in plist
     int placements = 0;
     int hostname_key = -1;
-    int64_t nodeID = 0;
+    Req host_req;                     // hostname In [placeholder] of a new NodeClaim (no pod can select it)
     kp_solve_stats stats{};
 
     explicit Solver(Dict& d) : D(d) {}
+    const InstanceType& ty(int t) const { return (*tp)[t]; }
+    const Pod& pod_at(int li) const { return (*pp)[plist[li]]; }
+    const PodClass& cls_of(int li) const { return (*cp)[pod_at(li).cls]; }
 
     // compatible(it, reqs) = it.Requirements.Intersects(reqs) == nil
     bool compatible(const InstanceType& it, const Reqs& reqs) const { return reqs_intersects(D, it.reqs, reqs); }
@@ -152,35 +164,47 @@ struct Solver {
             if (o.available && reqs_compatible(D, reqs, o.reqs, true)) return true;
         return false;
     }
-    // InstanceTypes.SatisfiesMinValues(requirements) == nil
-    bool satisfies_min_values(const std::vector<int>& its, const Reqs& reqs) const {
-        for (auto& kv : reqs.m) {
-            if (!kv.second.has_min) continue;
-            std::vector<int> seen;
-            for (int t : its) {
-                Req r = types[t].reqs.get(kv.first);
-                for (int v : r.values) seen.push_back(v);
+    // InstanceTypes.SatisfiesMinValues(requirements): minNeededInstanceTypes (the shortest prefix that satisfies every
+    // minValues key) and whether the whole list satisfies them.
+    bool satisfies_min_values(const std::vector<int>& its, const Reqs& reqs, int* min_needed = nullptr) const {
+        if (min_needed) *min_needed = 0;
+        if (!reqs.has_min_values()) return true;
+        std::vector<std::pair<int, std::vector<int>>> seen;  // (key, sorted distinct values so far)
+        for (auto& kv : reqs.m)
+            if (kv.second.has_min) seen.push_back({kv.first, {}});
+        for (size_t i = 0; i < its.size(); i++) {
+            bool ok = true;
+            for (auto& sk : seen) {
+                Req r = ty(its[i]).reqs.get(sk.first);
+                for (int v : r.values) sk.second.push_back(v);
+                std::sort(sk.second.begin(), sk.second.end());
+                sk.second.erase(std::unique(sk.second.begin(), sk.second.end()), sk.second.end());
+                if ((int)sk.second.size() < reqs.m.at(sk.first).min_values) ok = false;
             }
-            std::sort(seen.begin(), seen.end());
-            seen.erase(std::unique(seen.begin(), seen.end()), seen.end());
-            if ((int)seen.size() < kv.second.min_values) return false;
+            if (ok) {
+                if (min_needed) *min_needed = (int)i + 1;
+                return true;
+            }
         }
+        if (min_needed) *min_needed = (int)its.size();
+        for (auto& sk : seen)
+            if ((int)sk.second.size() < reqs.m.at(sk.first).min_values) return false;
         return true;
     }
     // filterInstanceTypesByRequirements (MIN_VALUES_POLICY=Strict)
     std::vector<int> filter(const std::vector<int>& its, const Reqs& reqs, const std::vector<int64_t>& total) const {
         std::vector<int> out;
         for (int t : its) {
-            const InstanceType& it = types[t];
+            const InstanceType& it = ty(t);
             if (compatible(it, reqs) && fits(total, it.alloc) && has_offering(it, reqs)) out.push_back(t);
         }
         if (reqs.has_min_values() && !satisfies_min_values(out, reqs)) out.clear();
         return out;
     }
 
-    bool nodeclaim_add(NodeClaim& nc, int p) {
-        const Pod& pod = pods[p];
-        const PodClass& pc = classes[pod.cls];
+    bool nodeclaim_add(NodeClaim& nc, int li) {
+        const Pod& pod = pod_at(li);
+        const PodClass& pc = cls_of(li);
         const Template& tm = tmpls[nc.tmpl];
         if (!tolerates_all(tm.taints, pc.tols)) return false;
         Reqs r = nc.reqs;
@@ -192,16 +216,18 @@ struct Solver {
         for (int k = 0; k < R; k++) requests[k] = nc.requests[k] + pod.req[k];
         std::vector<int> remaining = filter(nc.options, r, requests);
         if (remaining.empty()) return false;
-        nc.pods.push_back(p);
+        nc.pods.push_back(li);
         nc.options.swap(remaining);
         nc.requests.swap(requests);
         nc.reqs = std::move(r);
         return true;
     }
 
-    bool existing_add(ExistingNode& n, int p) {
-        const Pod& pod = pods[p];
-        const PodClass& pc = classes[pod.cls];
+    // ExistingNode.Add: Taints.ToleratesPod, Fits(requests + pod, available), Compatible (no undefined-label
+    // allowance), then requirements.Add.  On success `out` is the updated node.
+    bool existing_try(const ExistingNode& n, int li, ExistingNode& out) {
+        const Pod& pod = pod_at(li);
+        const PodClass& pc = cls_of(li);
         if (!tolerates_all(n.taints, pc.tols)) return false;
         std::vector<int64_t> requests(R);
         for (int k = 0; k < R; k++) requests[k] = n.requests[k] + pod.req[k];
@@ -209,8 +235,10 @@ struct Solver {
         Reqs r = n.reqs;
         if (!reqs_compatible(D, r, pc.reqs, false)) return false;
         r.add_all(D, pc.reqs);
-        n.requests.swap(requests);
-        n.reqs = std::move(r);
+        out.taints = n.taints;
+        out.available = n.available;
+        out.requests.swap(requests);
+        out.reqs = std::move(r);
         return true;
     }
 
@@ -224,11 +252,15 @@ struct Solver {
         void swap(int i, int j) { std::swap(s->newNodeClaims[i], s->newNodeClaims[j]); }
     };
 
-    bool add(int p) {
-        for (size_t j = 0; j < existing.size(); j++) {
+    bool add(int li) {
+        for (int j : ex_idx) {
             stats.existing_evals++;
-            if (existing_add(existing[j], p)) {
-                pod_result[p] = KP_POD_EXISTING((int)j);
+            auto it = ex_mod.find(j);
+            const ExistingNode& n = it != ex_mod.end() ? it->second : (*ex_base)[j];
+            ExistingNode upd;
+            if (existing_try(n, li, upd)) {
+                ex_mod[j] = std::move(upd);
+                pod_result[li] = KP_POD_EXISTING(j);
                 return true;
             }
         }
@@ -237,8 +269,8 @@ struct Solver {
         stats.nodeclaim_candidates_scanned += (int64_t)newNodeClaims.size();
         for (int idx : newNodeClaims) {
             stats.nodeclaim_evals++;
-            if (nodeclaim_add(ncs[idx], p)) {
-                pod_result[p] = idx;
+            if (nodeclaim_add(ncs[idx], li)) {
+                pod_result[li] = idx;
                 return true;
             }
         }
@@ -249,7 +281,7 @@ struct Solver {
             for (int t : tm.options) {
                 bool viable = true;
                 for (int k = 0; k < R; k++)
-                    if (tm.limit_set[k] && types[t].cap[k] > tm.remaining[k]) viable = false;
+                    if (tm.limit_set[k] && ty(t).cap[k] > tm.remaining[k]) viable = false;
                 if (viable) its.push_back(t);
             }
             if (its.empty()) continue;
@@ -258,27 +290,25 @@ struct Solver {
             nc.id = (int)ncs.size();
             nc.tmpl = (int)ti;
             nc.reqs = tm.reqs;
-            char host[64];
-            snprintf(host, sizeof host, "hostname-placeholder-%04lld", (long long)(++nodeID));
-            nc.reqs.add(D, new_req(D, hostname_key, OP_IN, {host}, false, 0));
+            nc.reqs.add(D, host_req);
             nc.options = its;
             nc.requests = tm.daemon;
             stats.template_evals++;
-            if (!nodeclaim_add(nc, p)) continue;
+            if (!nodeclaim_add(nc, li)) continue;
             // subtractMax(remaining, nodeClaim.InstanceTypeOptions)
             for (int k = 0; k < R; k++) {
                 if (!tm.limit_set[k]) continue;
                 int64_t mx = 0;
                 bool first = true;
                 for (int t : nc.options) {
-                    if (first || types[t].cap[k] > mx) mx = types[t].cap[k];
+                    if (first || ty(t).cap[k] > mx) mx = ty(t).cap[k];
                     first = false;
                 }
                 tm.remaining[k] -= mx;
             }
             ncs.push_back(std::move(nc));
             newNodeClaims.push_back((int)ncs.size() - 1);
-            pod_result[p] = (int)ncs.size() - 1;
+            pod_result[li] = (int)ncs.size() - 1;
             return true;
         }
         return false;
@@ -286,11 +316,12 @@ struct Solver {
 
     void solve() {
         // NewQueue: sort.Slice(pods, byCPUAndMemoryDescending) — a total order (UIDs unique).
-        std::vector<int> order(pods.size());
-        for (size_t i = 0; i < pods.size(); i++) order[i] = (int)i;
+        const int n = (int)plist.size();
+        std::vector<int> order(n);
+        for (int i = 0; i < n; i++) order[i] = i;
         std::sort(order.begin(), order.end(), [&](int a, int b) {
-            const Pod& l = pods[a];
-            const Pod& r = pods[b];
+            const Pod& l = pod_at(a);
+            const Pod& r = pod_at(b);
             if (l.req[cpu_axis] != r.req[cpu_axis]) return l.req[cpu_axis] > r.req[cpu_axis];
             if (l.req[mem_axis] != r.req[mem_axis]) return l.req[mem_axis] > r.req[mem_axis];
             if (l.ts != r.ts) return l.ts < r.ts;
@@ -298,22 +329,60 @@ struct Solver {
         });
         std::deque<int> q(order.begin(), order.end());
         std::unordered_map<int, int> lastLen;
-        pod_result.assign(pods.size(), KP_POD_UNSCHEDULABLE);
-        pod_order.assign(pods.size(), -1);
+        pod_result.assign(n, KP_POD_UNSCHEDULABLE);
+        pod_order.assign(n, -1);
         for (;;) {
             if (q.empty()) break;
-            int p = q.front();
-            auto it = lastLen.find(p);
+            int li = q.front();
+            auto it = lastLen.find(li);
             if (it != lastLen.end() && it->second == (int)q.size()) break;
             q.pop_front();
             stats.pods_popped++;
-            if (add(p)) {
-                pod_order[p] = placements++;
+            if (add(li)) {
+                pod_order[li] = placements++;
                 continue;
             }
             // preferences.Relax: no preferred terms in this build's inputs → never relaxed
-            q.push_back(p);
-            lastLen[p] = (int)q.size();
+            q.push_back(li);
+            lastLen[li] = (int)q.size();
+        }
+    }
+
+    // Cheapest available offering compatible with reqs (OrderByPrice key); MaxFloat64 when none.
+    double cheapest(int t, const Reqs& reqs) const {
+        double price = DBL_MAX;
+        bool any = false;
+        for (auto& o : ty(t).offerings) {
+            if (!o.available || !reqs_compatible(D, reqs, o.reqs, true)) continue;
+            if (!any || o.price < price) price = o.price;
+            any = true;
+        }
+        return any ? price : DBL_MAX;
+    }
+
+    // Solve's FinalizeScheduling + Results.TruncateInstanceTypes(maxInstanceTypes): hostname removed,
+    // InstanceTypes.Truncate = OrderByPrice(reqs) then the first max types, SatisfiesMinValues on the kept list
+    // (a NodeClaim that fails it is dropped and its pods get errors).
+    void finalize(int max_types) {
+        for (auto& nc : ncs) {
+            nc.reqs.m.erase(hostname_key);
+            std::vector<std::pair<double, int>> keyed;
+            for (int t : nc.options) keyed.push_back({cheapest(t, nc.reqs), t});
+            std::sort(keyed.begin(), keyed.end(), [&](const std::pair<double, int>& a, const std::pair<double, int>& b) {
+                if (a.first == b.first) return ty(a.second).name < ty(b.second).name;
+                return a.first < b.first;
+            });
+            std::vector<int> tr;
+            for (auto& kv : keyed) tr.push_back(kv.second);
+            if (max_types > 0 && (int)tr.size() > max_types) tr.resize(max_types);
+            if (nc.reqs.has_min_values() && !satisfies_min_values(tr, nc.reqs)) {
+                nc.valid = false;
+                for (int li : nc.pods) {
+                    pod_result[li] = KP_POD_UNSCHEDULABLE;
+                    pod_order[li] = -1;
+                }
+            }
+            nc.truncated = tr;
         }
     }
     int cpu_axis = 0, mem_axis = 1;
@@ -344,13 +413,9 @@ struct orc_result {
     Dict D;
 };
 
-extern "C" kp_status orc_solve(const kp_catalog_view* cat, const kp_solve_input* in, kp_solve_output* out,
-                               orc_result** res_out) {
-    if (!cat || !in || !out) return KP_E_INVALID;
-    if (in->min_values_policy != KP_MIN_VALUES_STRICT) return KP_E_UNSUPPORTED;
-    auto res = std::make_unique<orc_result>();
-    Dict& D = res->D;
-    Solver s(D);
+// Input views → NewScheduler state (catalog rows, classes, pods, NodeClaimTemplates in weight order, existing nodes).
+static kp_status parse_into(Solver& s, const kp_catalog_view* cat, const kp_solve_input* in) {
+    Dict& D = s.D;
     const int T = cat->n_types, R = cat->n_resources;
     s.R = R;
     s.cpu_axis = s.mem_axis = -1;
@@ -360,10 +425,11 @@ extern "C" kp_status orc_solve(const kp_catalog_view* cat, const kp_solve_input*
     }
     if (s.cpu_axis < 0 || s.mem_axis < 0) return KP_E_INVALID;
     s.hostname_key = D.key("kubernetes.io/hostname");
+    s.host_req = new_req(D, s.hostname_key, OP_IN, {"hostname-placeholder"}, false, 0);
     // catalog → []*cloudprovider.InstanceType
-    s.types.resize(T);
+    s.own_types.resize(T);
     for (int t = 0; t < T; t++) {
-        InstanceType& it = s.types[t];
+        InstanceType& it = s.own_types[t];
         it.name = cat->type_names[t];
         it.cap.assign(cat->capacity + (size_t)t * R, cat->capacity + (size_t)(t + 1) * R);
         it.alloc.assign(cat->allocatable + (size_t)t * R, cat->allocatable + (size_t)(t + 1) * R);
@@ -395,27 +461,27 @@ extern "C" kp_status orc_solve(const kp_catalog_view* cat, const kp_solve_input*
             else
                 of.reqs.add(D, new_req(D, key, OP_IN, {cat->offering_label_values[(size_t)o * cat->n_offering_keys + k]}, false, 0));
         }
-        s.types[t].offerings.push_back(std::move(of));
+        s.own_types[t].offerings.push_back(std::move(of));
     }
     // pod classes
-    s.classes.resize(in->n_classes);
+    s.own_classes.resize(in->n_classes);
     for (int c = 0; c < in->n_classes; c++) {
         const kp_pod_class& pc = in->classes[c];
-        if (!build_reqs(D, pc.requirements, pc.n_requirements, s.classes[c].reqs)) return KP_E_INVALID;
+        if (!build_reqs(D, pc.requirements, pc.n_requirements, s.own_classes[c].reqs)) return KP_E_INVALID;
         for (int i = 0; i < pc.n_tolerations; i++) {
             Toleration t;
             t.key = pc.tolerations[i].key ? pc.tolerations[i].key : "";
             t.op = pc.tolerations[i].op;
             t.value = pc.tolerations[i].value ? pc.tolerations[i].value : "";
             t.effect = pc.tolerations[i].effect ? pc.tolerations[i].effect : "";
-            s.classes[c].tols.push_back(t);
+            s.own_classes[c].tols.push_back(t);
         }
     }
     // pods
     const kp_pods_view& pv = in->pods;
-    s.pods.resize(pv.n_pods);
+    s.own_pods.resize(pv.n_pods);
     for (int p = 0; p < pv.n_pods; p++) {
-        Pod& pod = s.pods[p];
+        Pod& pod = s.own_pods[p];
         pod.cls = pv.class_id[p];
         if (pod.cls < 0 || pod.cls >= in->n_classes) return KP_E_INVALID;
         pod.req.assign(pv.requests + (size_t)p * R, pv.requests + (size_t)(p + 1) * R);
@@ -477,42 +543,26 @@ extern "C" kp_status orc_solve(const kp_catalog_view* cat, const kp_solve_input*
         n.available.assign(en.available, en.available + R);
         n.requests.assign(R, 0);
         if (en.requests) n.requests.assign(en.requests, en.requests + R);
-        s.existing.push_back(std::move(n));
+        s.own_existing.push_back(std::move(n));
     }
+    return KP_OK;
+}
+
+extern "C" kp_status orc_solve(const kp_catalog_view* cat, const kp_solve_input* in, kp_solve_output* out,
+                               orc_result** res_out) {
+    if (!cat || !in || !out) return KP_E_INVALID;
+    if (in->min_values_policy != KP_MIN_VALUES_STRICT) return KP_E_UNSUPPORTED;
+    auto res = std::make_unique<orc_result>();
+    Solver s(res->D);
+    kp_status st = parse_into(s, cat, in);
+    if (st != KP_OK) return st;
+    for (int j = 0; j < (int)s.own_existing.size(); j++) s.ex_idx.push_back(j);
+    const kp_pods_view& pv = in->pods;
+    s.plist.resize(pv.n_pods);
+    for (int p = 0; p < pv.n_pods; p++) s.plist[p] = p;
 
     s.solve();
-
-    // FinalizeScheduling + Results.TruncateInstanceTypes(maxInstanceTypes)
-    for (auto& nc : s.ncs) {
-        nc.reqs.m.erase(s.hostname_key);
-        // OrderByPrice(reqs)
-        std::vector<std::pair<double, int>> keyed;
-        for (int t : nc.options) {
-            double price = DBL_MAX;
-            bool any = false;
-            for (auto& o : s.types[t].offerings) {
-                if (!o.available || !reqs_compatible(D, nc.reqs, o.reqs, true)) continue;
-                if (!any || o.price < price) price = o.price;
-                any = true;
-            }
-            keyed.push_back({any ? price : DBL_MAX, t});
-        }
-        std::sort(keyed.begin(), keyed.end(), [&](const std::pair<double, int>& a, const std::pair<double, int>& b) {
-            if (a.first == b.first) return s.types[a.second].name < s.types[b.second].name;
-            return a.first < b.first;
-        });
-        std::vector<int> tr;
-        for (auto& kv : keyed) tr.push_back(kv.second);
-        if (in->max_instance_types > 0 && (int)tr.size() > in->max_instance_types) tr.resize(in->max_instance_types);
-        if (nc.reqs.has_min_values() && !s.satisfies_min_values(tr, nc.reqs)) {
-            nc.valid = false;
-            for (int p : nc.pods) {
-                s.pod_result[p] = KP_POD_UNSCHEDULABLE;
-                s.pod_order[p] = -1;
-            }
-        }
-        nc.truncated = tr;
-    }
+    s.finalize(in->max_instance_types);
 
     // outputs
     int n_nc = (int)s.ncs.size();
@@ -543,6 +593,229 @@ extern "C" kp_status orc_solve(const kp_catalog_view* cat, const kp_solve_input*
         res->ncs = std::move(s.ncs);
         *res_out = res.release();
     }
+    return KP_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Consolidation ([core] pkg/controllers/disruption, recalled — DESIGN.md §7)
+// ------------------------------------------------------------------------------------------------
+namespace orc {
+
+struct ConsCtx {
+    Solver* base;
+    const kp_consolidate_input* in;
+    int ct_key = -1;
+    Reqs ct_reserved, ct_spot, ct_od;  // NewRequirements(capacity-type In [x])
+    Req spot_req;
+    int v_spot = -1, v_od = -1;        // value ids in the capacity-type dictionary
+};
+
+// Offerings.Available().WorstLaunchPrice(reqs) (cloudprovider/types.go): the first capacity type in the precedence
+// reserved, spot, on-demand with a compatible offering; the most expensive such offering.
+static double worst_launch_price(const ConsCtx& X, int t, const Reqs& reqs) {
+    const Solver& b = *X.base;
+    for (const Reqs* ct : {&X.ct_reserved, &X.ct_spot, &X.ct_od}) {
+        bool any = false;
+        double mx = 0;
+        for (auto& o : b.ty(t).offerings) {
+            if (!o.available || !reqs_compatible(b.D, reqs, o.reqs, true) || !reqs_compatible(b.D, *ct, o.reqs, true))
+                continue;
+            if (!any || o.price > mx) mx = o.price;
+            any = true;
+        }
+        if (any) return mx;
+    }
+    return DBL_MAX;
+}
+
+// requirement.Has(value) for a value that may be absent from the dictionary
+static bool req_has_vid(const Dict& D, const Reqs& reqs, int key, int vid) {
+    if (key < 0) return true;
+    auto it = reqs.m.find(key);
+    if (it == reqs.m.end()) return true;  // undefined key: Get() is Exists
+    const Req& r = it->second;
+    if (vid < 0) return r.complement && !r.has_gt && !r.has_lt;
+    return req_has(D, r, vid);
+}
+
+static int consolidate_probe_count(const kp_consolidate_input* in) {
+    const int n = in->n_candidates;
+    if (in->mode == KP_CONSOLIDATE_SINGLE) return n;
+    if (n < 2) return 0;
+    const int mx = in->max_candidates > 0 ? in->max_candidates : 100;
+    return n <= mx ? n - 1 : mx;  // firstNConsolidationOption: mid in [1, max], prefix candidates[0 : mid+1]
+}
+
+// One SimulateScheduling + computeConsolidation (+ the multi-node filterOutSameInstanceType test).
+static void run_probe(const ConsCtx& X, int probe, kp_probe_result& pr) {
+    const kp_consolidate_input* in = X.in;
+    const Solver& b = *X.base;
+    const int c0 = in->mode == KP_CONSOLIDATE_SINGLE ? probe : 0;
+    const int c1 = in->mode == KP_CONSOLIDATE_SINGLE ? probe + 1 : probe + 2;
+    pr = kp_probe_result{};
+    Solver s(b.D);
+    s.R = b.R;
+    s.cpu_axis = b.cpu_axis;
+    s.mem_axis = b.mem_axis;
+    s.hostname_key = b.hostname_key;
+    s.host_req = b.host_req;
+    s.tp = &b.own_types;
+    s.cp = &b.own_classes;
+    s.pp = &b.own_pods;
+    s.ex_base = &b.own_existing;
+    s.tmpls = b.tmpls;
+    // SimulateScheduling: state nodes minus the candidates; NewScheduler recomputes NodePool remaining resources over
+    // those nodes, i.e. the candidates' capacity returns to their NodePools.
+    std::vector<uint8_t> excluded(b.own_existing.size(), 0);
+    double cprice = 0;
+    bool all_spot = true;
+    for (int c = c0; c < c1; c++) {
+        const kp_candidate& cd = in->candidates[c];
+        excluded[cd.node] = 1;
+        cprice += cd.price;  // getCandidatePrices
+        if (cd.capacity_type != KP_CT_SPOT) all_spot = false;
+        if (cd.capacity && cd.nodepool >= 0)
+            for (auto& tm : s.tmpls)
+                if (tm.np_index == cd.nodepool)
+                    for (int r = 0; r < s.R; r++)
+                        if (tm.limit_set[r]) tm.remaining[r] += cd.capacity[r];
+    }
+    for (int j = 0; j < (int)b.own_existing.size(); j++)
+        if (!excluded[j]) s.ex_idx.push_back(j);
+    // pods = pending + candidates' reschedulable pods
+    for (int i = 0; i < in->n_pending; i++) s.plist.push_back(in->pending[i]);
+    const int n_pending = (int)s.plist.size();
+    for (int c = c0; c < c1; c++)
+        for (int i = 0; i < in->candidates[c].n_pods; i++) s.plist.push_back(in->candidates[c].pods[i]);
+    pr.n_pods = (int)s.plist.size();
+    pr.candidate_price = cprice;
+
+    s.solve();
+    s.finalize(in->cluster.max_instance_types);  // Solve(...).TruncateInstanceTypes(MaxInstanceTypes)
+
+    // Results.AllNonPendingPodsScheduled: pending pods may stay pending; a pod placed on an uninitialized existing
+    // node is an error (SimulateScheduling)
+    bool all = true;
+    for (int li = n_pending; li < (int)s.plist.size(); li++) {
+        const int r = s.pod_result[li];
+        if (r == KP_POD_UNSCHEDULABLE) all = false;
+        if (r <= -2 && in->initialized && !in->initialized[-2 - r]) all = false;
+    }
+    std::vector<int> valid;
+    for (int i = 0; i < (int)s.ncs.size(); i++)
+        if (s.ncs[i].valid) valid.push_back(i);
+    pr.all_scheduled = all ? 1 : 0;
+    pr.n_new_nodeclaims = valid.size() < 2 ? (int)valid.size() : 2;
+    if (!all) return;
+    if (valid.empty()) {
+        pr.decision = KP_DECISION_DELETE;
+        pr.valid = 1;
+        return;
+    }
+    if (valid.size() != 1) return;  // "we're not going to turn a single node into multiple candidates"
+    NodeClaim& nc = s.ncs[valid[0]];
+    Reqs reqs = nc.reqs;
+    std::vector<int> opts = nc.truncated;  // already OrderByPrice(reqs)
+    const int ncand = c1 - c0;
+    auto price_filter = [&](const Reqs& rq, double maxp) {  // RemoveInstanceTypeOptionsByPriceAndMinValues / filterByPrice
+        std::vector<int> o;
+        for (int t : opts)
+            if (worst_launch_price(X, t, rq) < maxp) o.push_back(t);
+        return o;
+    };
+    const bool has_spot = req_has_vid(b.D, reqs, X.ct_key, X.v_spot);
+    if (all_spot && has_spot) {
+        // computeSpotToSpotConsolidation
+        if (!in->spot_to_spot) return;
+        if (X.ct_key >= 0) reqs.add(b.D, X.spot_req);
+        opts = price_filter(reqs, cprice);
+        int need = 0;
+        if (!s.satisfies_min_values(opts, reqs, &need)) return;
+        if (opts.empty()) return;
+        if (ncand == 1) {
+            if ((int)opts.size() < 15) return;  // MinInstanceTypesForSpotToSpotConsolidation
+            const int keep = reqs.has_min_values() ? std::max(15, need) : 15;
+            if ((int)opts.size() > keep) opts.resize(keep);
+        }
+    } else {
+        opts = price_filter(reqs, cprice);
+        if (!s.satisfies_min_values(opts, reqs)) return;
+        if (opts.empty()) return;
+        if (has_spot && req_has_vid(b.D, reqs, X.ct_key, X.v_od) && X.ct_key >= 0) reqs.add(b.D, X.spot_req);
+    }
+    pr.decision = KP_DECISION_REPLACE;
+    if (in->mode == KP_CONSOLIDATE_MULTI) {
+        // filterOutSameInstanceType: the replacement must be cheaper than the cheapest candidate of a type it offers
+        double maxp = DBL_MAX;
+        for (int t : opts)
+            for (int c = c0; c < c1; c++) {
+                const kp_candidate& cd = in->candidates[c];
+                if (cd.instance_type == t && cd.price < maxp) maxp = cd.price;
+            }
+        opts = price_filter(reqs, maxp);
+    }
+    pr.valid = opts.empty() ? 0 : 1;
+    pr.n_replacement_types = (int)opts.size();
+    double best = 0;
+    for (size_t i = 0; i < opts.size(); i++) {
+        const double w = worst_launch_price(X, opts[i], reqs);
+        if (i == 0 || w < best) best = w;
+    }
+    pr.replacement_price = best;
+}
+
+}  // namespace orc
+
+extern "C" int32_t orc_consolidate_probe_count(const kp_consolidate_input* in) {
+    return in ? consolidate_probe_count(in) : 0;
+}
+
+extern "C" kp_status orc_consolidate(const kp_catalog_view* cat, const kp_consolidate_input* in,
+                                     kp_probe_result* results, int32_t cap_results, int32_t n_threads) {
+    if (!cat || !in) return KP_E_INVALID;
+    if (in->cluster.min_values_policy != KP_MIN_VALUES_STRICT) return KP_E_UNSUPPORTED;
+    if (in->mode != KP_CONSOLIDATE_SINGLE && in->mode != KP_CONSOLIDATE_MULTI) return KP_E_INVALID;
+    Dict D;
+    Solver base(D);
+    kp_status st = parse_into(base, cat, &in->cluster);
+    if (st != KP_OK) return st;
+    const int E = (int)base.own_existing.size(), P = (int)base.own_pods.size();
+    for (int i = 0; i < in->n_pending; i++)
+        if (in->pending[i] < 0 || in->pending[i] >= P) return KP_E_INVALID;
+    for (int c = 0; c < in->n_candidates; c++) {
+        const kp_candidate& cd = in->candidates[c];
+        if (cd.node < 0 || cd.node >= E || cd.n_pods < 0 || (cd.n_pods && !cd.pods) || !(cd.price >= 0)) return KP_E_INVALID;
+        for (int i = 0; i < cd.n_pods; i++)
+            if (cd.pods[i] < 0 || cd.pods[i] >= P) return KP_E_INVALID;
+    }
+    const int np = consolidate_probe_count(in);
+    const int b0 = in->probe_begin > 0 ? in->probe_begin : 0;
+    const int b1 = in->probe_end > 0 && in->probe_end < np ? in->probe_end : np;
+    if (b1 - b0 > cap_results) return KP_E_BUFFER;
+    ConsCtx X;
+    X.base = &base;
+    X.in = in;
+    X.ct_key = D.key("karpenter.sh/capacity-type");
+    X.ct_reserved.add(D, new_req(D, X.ct_key, OP_IN, {"reserved"}, false, 0));
+    X.ct_spot.add(D, new_req(D, X.ct_key, OP_IN, {"spot"}, false, 0));
+    X.ct_od.add(D, new_req(D, X.ct_key, OP_IN, {"on-demand"}, false, 0));
+    X.spot_req = new_req(D, X.ct_key, OP_IN, {"spot"}, false, 0);
+    X.v_spot = D.value(X.ct_key, "spot");
+    X.v_od = D.value(X.ct_key, "on-demand");
+    // the dictionary is frozen from here on: probes only read it
+    const int nt = n_threads > 1 ? n_threads : 1;
+    std::atomic<int> next{b0};
+    auto worker = [&]() {
+        for (;;) {
+            const int i = next.fetch_add(1);
+            if (i >= b1) break;
+            run_probe(X, i, results[i - b0]);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; t++) th.emplace_back(worker);
+    worker();
+    for (auto& t : th) t.join();
     return KP_OK;
 }
 

@@ -34,6 +34,11 @@ def lib():
         _lib.orc_result_free.argtypes = [C.c_void_p]
         _lib.orc_instance_type_resources.argtypes = [C.POINTER(OrcEc2Info), C.POINTER(OrcTypeOpts)] + \
             [C.POINTER(C.c_int64)] * 4
+        _lib.orc_consolidate_probe_count.argtypes = [C.POINTER(abi.kp_consolidate_input)]
+        _lib.orc_consolidate_probe_count.restype = C.c_int32
+        _lib.orc_consolidate.argtypes = [C.POINTER(abi.kp_catalog_view), C.POINTER(abi.kp_consolidate_input),
+                                         C.POINTER(abi.kp_probe_result), C.c_int32, C.c_int32]
+        _lib.orc_consolidate.restype = C.c_int32
         _lib.orc_go_sort_slice_ints.argtypes = [C.POINTER(C.c_int64), C.POINTER(C.c_int32), C.c_int32]
     return _lib
 
@@ -127,3 +132,21 @@ def solve(problem, catalog_view=None):
     if st != 0:
         raise RuntimeError("orc_solve failed: %d" % st)
     return OracleResult(ob.results(), h)
+
+
+def consolidate(cp, mode, probe_begin=0, probe_end=0, spot_to_spot=False, max_candidates=100, n_threads=1,
+                catalog_view=None):
+    """CPU oracle consolidation probes for a kpsim.model.ConsolidationProblem -> numpy array of abi.PROBE_DTYPE."""
+    from kpsim import abi, model
+    L = lib()
+    cv = catalog_view or model.CatalogView(cp.cluster.catalog)
+    iv = model.ConsolidateInputView(cp, mode, probe_begin, probe_end, spot_to_spot, max_candidates)
+    n = L.orc_consolidate_probe_count(C.byref(iv.view))
+    b0 = max(0, probe_begin)
+    b1 = probe_end if 0 < probe_end < n else n
+    out = np.zeros(max(1, b1 - b0), abi.PROBE_DTYPE)
+    st = L.orc_consolidate(C.byref(cv.view), C.byref(iv.view), out.ctypes.data_as(C.POINTER(abi.kp_probe_result)),
+                           len(out), n_threads)
+    if st != 0:
+        raise RuntimeError("orc_consolidate failed: %d" % st)
+    return out[:max(0, b1 - b0)]

@@ -147,3 +147,61 @@ def fuzz_problem(catalog, seed, n_pods=300, n_classes=12, n_pools=3, with_min=Tr
         pods.creation_ns[:] = pods.creation_ns[0]
     existing = existing_nodes(rng, catalog, n_existing) if n_existing else []
     return Problem(catalog, pools, classes, pods, existing)
+
+
+def _negative(r):
+    return r.op in ("NotIn", "DoesNotExist") and not (r.op == "NotIn" and not r.values)
+
+
+def drop_mutating_requirements(prob):
+    """Remove NotIn/DoesNotExist pod requirements that could change a node's requirements in a way a later pod sees
+    (a key some node lacks that another class selects positively): consolidation probes keep nodes immutable and the
+    library rejects such inputs (KP_E_UNSUPPORTED)."""
+    keys = set()
+    for pc in prob.classes:
+        keys |= {r.key for r in pc.requirements}
+    pos = {r.key for pc in prob.classes for r in pc.requirements if not _negative(r)}
+    undef = {k for k in keys if k != HOSTNAME and any(k not in n.labels for n in prob.existing)}
+    bad = pos & undef
+    for pc in prob.classes:
+        pc.requirements = [r for r in pc.requirements if not (_negative(r) and r.key in bad)]
+    return prob
+
+
+def fuzz_consolidation(catalog, seed, n_nodes=40, n_pods=200, n_candidates=None, with_min=False, pending_frac=0.15,
+                       all_spot=False, supported=False):
+    """A consolidation pass over random state: fuzz_problem's classes / pools / existing nodes, NewScheduler node order
+    (initialized first, then name), candidates with their bound pods, pending pods, candidate prices around their
+    offering price (so REPLACE, price-filtered NONE and DELETE all occur)."""
+    from kpsim import abi, synth
+    prob = fuzz_problem(catalog, seed, n_pods=n_pods, n_classes=12, with_min=with_min, n_existing=n_nodes)
+    if supported:
+        drop_mutating_requirements(prob)
+    rng = np.random.Generator(np.random.PCG64(seed + 7))
+    E = len(prob.existing)
+    init = (rng.random(E) < 0.9).astype(np.uint8)
+    order = sorted(range(E), key=lambda j: (0 if init[j] else 1, prob.existing[j].name))
+    prob.existing = [prob.existing[j] for j in order]
+    init = init[order]
+    by_name = {it.name: t for t, it in enumerate(catalog)}
+    nc = int(n_candidates or rng.integers(2, max(3, min(E, 30))))
+    cand_nodes = rng.choice(E, size=min(nc, E), replace=False)
+    P = prob.pods.n
+    owner = rng.integers(0, len(cand_nodes), size=P)
+    owner[rng.random(P) < pending_frac] = -1
+    cands = []
+    for i, j in enumerate(cand_nodes):
+        node = prob.existing[int(j)]
+        if all_spot:
+            node.labels[CAPACITY_TYPE] = "spot"
+        t = by_name.get(node.labels.get(INSTANCE_TYPE), -1)
+        price = synth.candidate_price(catalog[t], node.labels) if t >= 0 else None
+        if price is None:
+            price = float(rng.uniform(0.01, 3.0))
+        price *= float(rng.choice([0.3, 1.0, 1.0, 3.0, 20.0]))
+        ct = abi.KP_CT_SPOT if node.labels.get(CAPACITY_TYPE) == "spot" else abi.KP_CT_ON_DEMAND
+        npool = int(rng.integers(-1, len(prob.nodepools)))
+        cap = np.array(catalog[t].capacity, np.int64) if t >= 0 else None
+        cands.append(model.Candidate(node=int(j), pods=np.nonzero(owner == i)[0].astype(np.int32), price=price,
+                                     capacity_type=ct, instance_type=t, nodepool=npool, capacity=cap))
+    return model.ConsolidationProblem(prob, cands, np.nonzero(owner < 0)[0].astype(np.int32), init)

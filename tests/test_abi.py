@@ -12,7 +12,7 @@ LIB = os.path.join(ROOT, "karpenter-provider-aws_amd", "lib", "libkpsim.so")
 def declared_symbols():
     with open(os.path.join(ROOT, "include", "kpsim.h")) as f:
         text = f.read()
-    return sorted(set(re.findall(r"^\s*(?:kp_status|const char\*)\s+(kp_[a-z_]+)\(", text, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:kp_status|const char\*|int32_t)\s+(kp_[a-z_]+)\(", text, flags=re.M)))
 
 
 @pytest.fixture(scope="module")

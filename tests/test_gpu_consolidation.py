@@ -1,0 +1,79 @@
+"""GPU: consolidation probes on the gfx950 path (kp_consolidate) against the CPU oracle (orc_consolidate).
+
+Per probe: decision, validity (the multi-node search test), new NodeClaims (capped at 2), replacement option count,
+candidate / replacement prices (exact doubles), pods rescheduled; all_scheduled wherever the probe ran to completion
+(fewer than two new NodeClaims).  Sizes are those the oracle finishes in seconds; config 4 at full size is checked
+by properties (every probe evaluated, DELETE-dominated at 40-60% utilisation, shard-invariance).
+"""
+import numpy as np
+import pytest
+
+import fuzzgen
+import pyoracle
+from kpsim import abi, consolidation, model, synth
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ["decision", "valid", "n_new_nodeclaims", "n_replacement_types", "n_pods", "candidate_price",
+          "replacement_price"]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from kpsim import native
+    c = native.Context(0)
+    yield c
+    c.close()
+
+
+def device_probes(ctx, cp, mode, spot_to_spot=False, begin=0, end=0):
+    ctx.upload_catalog(model.CatalogView(cp.cluster.catalog))
+    return ctx.consolidate(model.ConsolidateInputView(cp, mode, begin, end, spot_to_spot))
+
+
+def assert_probes_equal(dev, orc):
+    assert len(dev) == len(orc)
+    for f in FIELDS:
+        np.testing.assert_array_equal(dev[f], orc[f], err_msg=f)
+    done = orc["n_new_nodeclaims"] < 2
+    np.testing.assert_array_equal(dev["all_scheduled"][done], orc["all_scheduled"][done], err_msg="all_scheduled")
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_fuzz_consolidation(ctx, golden, seed):
+    rng = np.random.Generator(np.random.PCG64(500 + seed))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 300)), replace=False))]
+    cp = fuzzgen.fuzz_consolidation(sub, 500 + seed, n_nodes=int(rng.integers(4, 80)),
+                                    n_pods=int(rng.integers(20, 300)), all_spot=seed % 4 == 0, supported=True)
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        s2s = seed % 2 == 0
+        assert_probes_equal(device_probes(ctx, cp, mode, s2s), pyoracle.consolidate(cp, mode, spot_to_spot=s2s))
+
+
+def test_shard_ranges_concatenate(ctx, golden):
+    cp = fuzzgen.fuzz_consolidation(golden[:200], 77, n_nodes=60, n_pods=250, n_candidates=40, supported=True)
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        full = device_probes(ctx, cp, mode)
+        n = len(full)
+        parts = []
+        for r in range(3):
+            b0, b1 = consolidation.shard_range(n, r, 3)
+            parts.append(device_probes(ctx, cp, mode, begin=b0, end=b1))
+        assert_probes_equal(np.concatenate(parts), full)
+
+
+def test_config4_small_parity(ctx, golden):
+    cp = synth.config4(n_nodes=400, catalog=golden, n_pending=50)
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        assert_probes_equal(device_probes(ctx, cp, mode), pyoracle.consolidate(cp, mode, n_threads=8))
+
+
+def test_config4_full_size_properties(ctx, golden):
+    """5k nodes / ~100k pods (BASELINE configs[3]): every probe of both modes against the oracle."""
+    cp = synth.config4(catalog=golden)
+    dev = device_probes(ctx, cp, abi.KP_CONSOLIDATE_SINGLE)
+    assert len(dev) == len(cp.candidates)
+    assert (dev["n_pods"] == np.array([len(c.pods) for c in cp.candidates])).all()
+    assert_probes_equal(dev, pyoracle.consolidate(cp, abi.KP_CONSOLIDATE_SINGLE, n_threads=8))
+    multi = device_probes(ctx, cp, abi.KP_CONSOLIDATE_MULTI)
+    assert_probes_equal(multi, pyoracle.consolidate(cp, abi.KP_CONSOLIDATE_MULTI, n_threads=8))
