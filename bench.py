@@ -33,6 +33,99 @@ def algorithmic_bytes(stats, n_nodeclaims, T, R=12, K_bytes=64):
     return stats["nodeclaim_candidates_scanned"] * s_nc + stats["pods_popped"] * s_pod + n_nodeclaims * T * s_type
 
 
+def consolidation_bytes(cst, A, R=12):
+    """Algorithmic bytes of the probe kernel: every existing-node slot examined reads its headroom on
+    the A active axes and one compatibility bit; every pod popped reads its requests, class and shape (S_pod); every
+    NodeClaim / template evaluation reads one NodeClaim row (S_nc = ceil(T/8) + 8R + 64, T = 918); the queue
+    bitmap scan reads and clears 8 B per word."""
+    s_nc = (918 + 7) // 8 + 8 * R + 64
+    s_pod = 8 * R + 64
+    return (cst[1] * (8 * A + 1 / 8) + cst[0] * s_pod + (cst[2] + cst[3]) * s_nc + cst[5] * 16)
+
+
+def consolidation_leg(a, cat, local, rank, world, dist, barrier):
+    """BASELINE configs[3]: single-node consolidation over every candidate of a 5k-node / ~100k-pod cluster plus the
+    multi-node prefix probes (first 100 by disruption cost).  Probes are sharded over ranks; one all-gather per mode
+    carries the results (kpsim.consolidation.compute_command)."""
+    from kpsim import abi, consolidation, model, native, synth
+    cp = synth.config4(n_nodes=a.nodes, catalog=cat)
+    ctx = native.Context(local)
+    ctx.upload_catalog(model.CatalogView(cat))
+    ctx.consolidate_prepare(model.ConsolidateInputView(cp, abi.KP_CONSOLIDATE_SINGLE))
+    n_s = model.consolidation_probe_count(len(cp.candidates), abi.KP_CONSOLIDATE_SINGLE)
+    n_m = model.consolidation_probe_count(len(cp.candidates), abi.KP_CONSOLIDATE_MULTI)
+
+    def probe_fn(c, mode, b0, b1):
+        return ctx.consolidate_execute(mode, n_s if mode == abi.KP_CONSOLIDATE_SINGLE else n_m, b0, b1)
+
+    def step():
+        cs = consolidation.compute_command(cp, abi.KP_CONSOLIDATE_SINGLE, probe_fn)
+        ms_s, cst_s = ctx.consolidate_stats()
+        cm = consolidation.compute_command(cp, abi.KP_CONSOLIDATE_MULTI, probe_fn)
+        ms_m, cst_m = ctx.consolidate_stats()
+        return cs, cm, (ms_s, cst_s), (ms_m, cst_m)
+
+    for _ in range(max(1, a.warmup)):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    kms, kcs = [], []
+    for _ in range(a.steps):
+        cs, cm, st_s, st_m = step()
+        kms.append([st_s[0][0], st_s[0][1], st_m[0][0], st_m[0][1]])
+        kcs.append(np.array(st_s[1]) + np.array(st_m[1]))
+    elapsed = time.perf_counter() - t0
+    barrier()
+    if dist is not None:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    km = np.array(kms).mean(axis=0)
+    cst = np.array(kcs).mean(axis=0)
+    A = int(np.any(cp.cluster.pods.requests != 0, axis=0).sum())  # active axes (no daemon overhead in config4)
+    B = consolidation_bytes(cst, A)
+    kern_s = (km[1] + km[3]) / 1e3
+    achieved = B / kern_s / 1e9 if kern_s > 0 else 0.0
+    out = {
+        "metric": "consolidation cands/sec",
+        "value": (n_s + n_m) * a.steps / elapsed,
+        "unit": "candidates/s",
+        "n_gpus": world,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "scaling": "strong",
+        "config": {"workload": "config4: %d existing nodes, %d bound pods (config2 classes), single-node probes over "
+                               "all %d candidates + %d multi-node prefix probes" % (len(cp.cluster.existing),
+                                                                                    cp.cluster.pods.n, n_s, n_m),
+                   "parallelism": "probe shards x%d" % world},
+        "decisions": {"single": [cs.decision, cs.candidates[:1]], "multi": [cm.decision, len(cm.candidates)]},
+        "kernel_ms_rank0": {"single_prep": km[0], "single_probes": km[1], "multi_prep": km[2], "multi_probes": km[3]},
+        "counters_per_step": dict(zip(["pods_popped", "existing_slots", "nodeclaim_evals", "template_evals", "probes",
+                                       "bitmap_words", "placed_existing", "new_nodeclaims"], [int(x) for x in cst])),
+        "roofline": {"bound": "hbm", "kernel": "consolidate_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes": int(B),
+                     "kernel_ms": float(km[1] + km[3])},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        import pyoracle
+        nthr = min(16, os.cpu_count() or 1)
+        t = time.perf_counter()
+        r1 = pyoracle.consolidate(cp, abi.KP_CONSOLIDATE_SINGLE, n_threads=nthr)
+        r2 = pyoracle.consolidate(cp, abi.KP_CONSOLIDATE_MULTI, n_threads=nthr)
+        cpu_s = time.perf_counter() - t
+        out["cpu_baseline"] = {"value": (n_s + n_m) / cpu_s, "unit": "candidates/s", "cores": nthr, "kind": "port",
+                               "sample": "oracle orc_consolidate (std::thread x %d) over the full pass, %.2f s incl. "
+                                         "cluster parse" % (nthr, cpu_s)}
+        d1 = ctx.consolidate_execute(abi.KP_CONSOLIDATE_SINGLE, n_s)
+        d2 = ctx.consolidate_execute(abi.KP_CONSOLIDATE_MULTI, n_m)
+        same = all((d1[f] == r1[f]).all() and (d2[f] == r2[f]).all() for f in
+                   ("decision", "valid", "n_new_nodeclaims", "n_replacement_types", "candidate_price", "replacement_price"))
+        out["parity_vs_cpu_baseline"] = bool(same)
+    ctx.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -41,6 +134,8 @@ def main():
     ap.add_argument("--pods", type=int, default=50_000)
     ap.add_argument("--cpu-sample", type=int, default=0, help="pods in the CPU-baseline sample (0 = the full workload)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-consolidation", action="store_true")
+    ap.add_argument("--nodes", type=int, default=5000, help="config4 cluster size (consolidation leg)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -109,6 +204,8 @@ def main():
         with open(pmc_path) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
 
+    cons = None if a.no_consolidation else consolidation_leg(a, cat, local, rank, world, dist, barrier)
+
     cpu = None
     parity_ok = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -164,6 +261,7 @@ def main():
             "nodeclaims": res.n_nodeclaims,
             "unschedulable": int((res.pod_result == -1).sum()),
             "solve_stats": {k: v for k, v in res.stats.items() if not k.startswith("ns_")},
+            "consolidation": cons,
         }
         print(json.dumps(line))
     ctx.close()

@@ -320,6 +320,13 @@ typedef struct kp_probe_result {
 int32_t kp_consolidate_probe_count(const kp_consolidate_input* in);
 /* Evaluates probes [probe_begin, probe_end) on the ctx's device; results[i] is probe probe_begin + i. */
 kp_status kp_consolidate(kp_ctx* ctx, const kp_consolidate_input* in, kp_probe_result* results, int32_t cap_results);
+/* Split form (inputs resident on the device between calls): prepare encodes and uploads the cluster and candidates
+ * of `in` (its mode and probe range are ignored); execute evaluates probes [probe_begin, probe_end) of `mode` over the
+ * prepared pass (probe_end <= 0: to the end).  kp_consolidate = prepare + execute of in->mode / in's range.
+ * Any kp_solve_prepare or catalog upload on the ctx invalidates the prepared pass (KP_E_STATE). */
+kp_status kp_consolidate_prepare(kp_ctx* ctx, const kp_consolidate_input* in);
+kp_status kp_consolidate_execute(kp_ctx* ctx, int32_t mode, int32_t probe_begin, int32_t probe_end,
+                                 kp_probe_result* results, int32_t cap_results);
 /* Diagnostics of the last kp_consolidate: ms[3] = {device prep (queue sort, masks), probe kernel, whole call};
  * counters[8] = {pods popped, existing-node slots examined, NodeClaim evaluations, template evaluations, probes,
  * queue-bitmap words scanned, existing-node placements, new NodeClaims}. */

@@ -28,7 +28,6 @@ hipError_t kp_launch_template_init(const KpDev& d, hipStream_t s);
 hipError_t kp_launch_existing(const KpDev& d, hipStream_t s);
 hipError_t kp_launch_ffd(const KpDev& d, hipStream_t s);
 hipError_t kp_launch_finalize(const KpDev& d, int n_nodeclaims, hipStream_t s);
-struct KpCons;
 bool kp_cons_plan_lds(const KpDev& d, KpCons& k, int max_bytes);
 hipError_t kp_launch_consolidate(const KpDev& d, const KpCons& k, int n_workers, hipStream_t s);
 hipError_t kp_launch_cons_prep(const int32_t* queue0, int P, int32_t* rank, const int32_t* pending, int n_pending,
@@ -241,6 +240,10 @@ struct kp_ctx {
     DBuf<uint64_t> d_pend_bits, d_pbits;
     DBuf<uint8_t> d_init;
     DBuf<kp_probe_result> d_probe_out;
+    KpCons cons{};                           // prepared consolidation pass (device pointers set per execute)
+    bool cons_prepared = false;
+    int cons_max_candidates = 100, cons_n_pending = 0;
+    std::vector<int32_t> cons_off;           // candidate pod CSR offsets
     double cons_ms[3] = {};                  // device prep (sort, masks), probe kernel, whole call
     int64_t cons_stats[CS_COUNT] = {};
     // last results (host)
@@ -550,6 +553,7 @@ extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, ui
     c->epoch = epoch;
     c->have_catalog = true;
     c->prepared = c->executed = false;
+    c->cons_prepared = false;
     return KP_OK;
 } catch (const std::exception& e) {
     return fail(ctx, KP_E_INVALID, e.what());
@@ -682,6 +686,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     HIPCHK(hipSetDevice(ctx->device));
     kp_ctx* c = ctx;
     c->prepared = c->executed = false;
+    c->cons_prepared = false;
     c->any_min_values = false;
     if (in->min_values_policy != KP_MIN_VALUES_STRICT)
         return fail(ctx, KP_E_UNSUPPORTED, "MIN_VALUES_POLICY=BestEffort is not supported by this build");
@@ -1362,17 +1367,11 @@ extern "C" int32_t kp_consolidate_probe_count(const kp_consolidate_input* in) {
     return n <= mx ? n - 1 : mx;  // firstNConsolidationOption: mid in [1, max], prefix candidates[0 : mid+1]
 }
 
-extern "C" kp_status kp_consolidate(kp_ctx* ctx, const kp_consolidate_input* in, kp_probe_result* results,
-                                    int32_t cap_results) try {
+extern "C" kp_status kp_consolidate_prepare(kp_ctx* ctx, const kp_consolidate_input* in) try {
     if (!ctx || !in) return KP_E_INVALID;
+    ctx->cons_prepared = false;
     if (in->mode != KP_CONSOLIDATE_SINGLE && in->mode != KP_CONSOLIDATE_MULTI)
         return fail(ctx, KP_E_INVALID, "unknown consolidation mode");
-    const int np = kp_consolidate_probe_count(in);
-    const int b0 = in->probe_begin > 0 ? in->probe_begin : 0;
-    const int b1 = in->probe_end > 0 && in->probe_end < np ? in->probe_end : np;
-    if (b0 > b1) return fail(ctx, KP_E_INVALID, "probe range outside the probe list");
-    const int nprobe = b1 - b0;
-    if (nprobe > cap_results || (nprobe > 0 && !results)) return fail(ctx, KP_E_BUFFER, "probe results buffer too small");
     const kp_solve_input& cl = in->cluster;
     const int P = cl.pods.n_pods, E = cl.n_existing, NC = in->n_candidates;
     // inputs: candidates on distinct nodes, each pod pending or owned by one candidate, prices >= 0
@@ -1393,12 +1392,10 @@ extern "C" kp_status kp_consolidate(kp_ctx* ctx, const kp_consolidate_input* in,
             }
         }
     }
-    if (nprobe == 0) return KP_OK;
     kp_status st = kp_solve_prepare(ctx, &cl);
     if (st != KP_OK) return st;
-    HIPCHK(hipSetDevice(ctx->device));
     kp_ctx* c = ctx;
-    KpDev d = c->dev;
+    const KpDev& d = c->dev;
     if (c->any_min_values) return fail(ctx, KP_E_UNSUPPORTED, "consolidation with minValues NodePools is not supported by this build");
     if (c->cons_mayfix)
         return fail(ctx, KP_E_UNSUPPORTED, "consolidation with NotIn/DoesNotExist pod requirements on keys some node lacks "
@@ -1406,16 +1403,13 @@ extern "C" kp_status kp_consolidate(kp_ctx* ctx, const kp_consolidate_input* in,
     if (d.n_active > KP_LDS_AXES) return fail(ctx, KP_E_UNSUPPORTED, "more than 6 requested resource axes");
     if (d.M <= 0 || d.M > 64) return fail(ctx, KP_E_UNSUPPORTED, "consolidation needs max_instance_types in 1..64");
     const int T = c->T, TW = c->TW, R = c->R, A = d.n_active;
-    d.lds_A = 0;  // no quick-accept witness in probes
-    d.lds_nstage = A;
-    d.profile = 0;
     hipStream_t s = c->stream;
-    KpCons k{};
-    k.n_probes = nprobe;
-    k.probe0 = b0;
-    k.mode = in->mode;
+    KpCons& k = c->cons;
+    k = KpCons{};
     k.n_cand = NC;
     k.spot_to_spot = in->spot_to_spot ? 1 : 0;
+    c->cons_max_candidates = in->max_candidates > 0 ? in->max_candidates : 100;
+    c->cons_n_pending = in->n_pending;
     k.v_spot = k.v_od = -1;
     if (c->key_ct >= 0) {
         k.v_spot = c->sol.keys[c->key_ct].find("spot");
@@ -1427,7 +1421,9 @@ extern "C" kp_status kp_consolidate(kp_ctx* ctx, const kp_consolidate_input* in,
     }
     std::vector<int> np_tmpl(cl.n_nodepools, -1);
     for (int j = 0; j < (int)c->tmpl_np.size(); j++) np_tmpl[c->tmpl_np[j]] = j;
-    std::vector<int32_t> ci((size_t)std::max(NC, 1) * 4, 0), coff(NC + 1, 0), cpods;
+    std::vector<int32_t> ci((size_t)std::max(NC, 1) * 4, 0), cpods;
+    std::vector<int32_t>& coff = c->cons_off;
+    coff.assign(NC + 1, 0);
     std::vector<double> cprice(std::max(NC, 1), 0.0);
     std::vector<int64_t> ccap((size_t)std::max(NC, 1) * R, 0);
     for (int i = 0; i < NC; i++) {
@@ -1443,14 +1439,6 @@ extern "C" kp_status kp_consolidate(kp_ctx* ctx, const kp_consolidate_input* in,
         for (int q = 0; q < cd.n_pods; q++) cpods.push_back(cd.pods[q]);
     }
     if (cpods.empty()) cpods.push_back(0);
-    // ring capacity: pods of the largest probe
-    int maxp = 0;
-    if (in->mode == KP_CONSOLIDATE_SINGLE) {
-        for (int i = b0; i < b1; i++) maxp = std::max(maxp, coff[i + 1] - coff[i]);
-    } else {
-        maxp = coff[std::min(NC, b1 + 1)];
-    }
-    k.ring_cap = std::max(1, in->n_pending + maxp);
     std::vector<int32_t> pend(in->pending, in->pending + in->n_pending);
     if (pend.empty()) pend.push_back(0);
     std::vector<uint8_t> init(std::max(E, 1), 1);
@@ -1461,31 +1449,77 @@ extern "C" kp_status kp_consolidate(kp_ctx* ctx, const kp_consolidate_input* in,
     for (int ai = 0; ai < A; ai++)
         for (int t = 0; t < T; t++) act[(size_t)ai * astride + t] = c->alloc_rt[(size_t)d.active_axes[ai] * T + t];
     k.PW = std::max(1, (P + 63) / 64);
-    if (!kp_cons_plan_lds(d, k, KP_LDS_BYTES)) return fail(ctx, KP_E_UNSUPPORTED, "consolidation LDS plan exceeds 160 KB");
-    int occ = std::max(1, std::min(8, KP_LDS_BYTES / std::max(k.lds_bytes, 1)));
-    int workers = std::min(nprobe, 256 * occ);
-    const auto t0 = clk::now();
+    k.astride = astride;
     HIPCHK(c->d_cand_i.upload(ci, s));
+    HIPCHK(c->d_cand_off.upload(coff, s));
     HIPCHK(c->d_cand_pods.upload(cpods, s));
+    HIPCHK(c->d_pending.upload(pend, s));
     HIPCHK(c->d_cand_price.upload(cprice, s));
     HIPCHK(c->d_cand_cap.upload(ccap, s));
     HIPCHK(c->d_init.upload(init, s));
     HIPCHK(c->d_alloc_act.upload(act, s));
-    HIPCHK(c->d_cand_off.upload(coff, s));
-    HIPCHK(c->d_pending.upload(pend, s));
     HIPCHK(c->d_next.ensure(1));
     HIPCHK(c->d_rank.ensure(std::max(P, 1)));
     HIPCHK(c->d_pend_bits.ensure(k.PW));
-    HIPCHK(hipMemsetAsync(c->d_pend_bits.p, 0, (size_t)k.PW * 8, s));
+    HIPCHK(c->d_cons_stats.ensure(CS_COUNT));
+    HIPCHK(hipStreamSynchronize(s));
+    c->cons_prepared = true;
+    return KP_OK;
+} catch (const std::exception& e) {
+    return fail(ctx, KP_E_INVALID, e.what());
+}
+
+extern "C" kp_status kp_consolidate_execute(kp_ctx* ctx, int32_t mode, int32_t probe_begin, int32_t probe_end,
+                                            kp_probe_result* results, int32_t cap_results) try {
+    if (!ctx) return KP_E_INVALID;
+    if (!ctx->cons_prepared) return fail(ctx, KP_E_STATE, "kp_consolidate_execute before kp_consolidate_prepare");
+    if (mode != KP_CONSOLIDATE_SINGLE && mode != KP_CONSOLIDATE_MULTI) return fail(ctx, KP_E_INVALID, "unknown consolidation mode");
+    kp_ctx* c = ctx;
+    HIPCHK(hipSetDevice(c->device));
+    KpCons k = c->cons;
+    const int NC = k.n_cand;
+    int np;
+    if (mode == KP_CONSOLIDATE_SINGLE) np = NC;
+    else np = NC < 2 ? 0 : (NC <= c->cons_max_candidates ? NC - 1 : c->cons_max_candidates);
+    const int b0 = probe_begin > 0 ? probe_begin : 0;
+    const int b1 = probe_end > 0 && probe_end < np ? probe_end : np;
+    if (b0 > b1) return fail(ctx, KP_E_INVALID, "probe range outside the probe list");
+    const int nprobe = b1 - b0;
+    if (nprobe > cap_results || (nprobe > 0 && !results)) return fail(ctx, KP_E_BUFFER, "probe results buffer too small");
+    if (nprobe == 0) return KP_OK;
+    KpDev d = c->dev;
+    const int P = d.P, E = d.E, A = d.n_active;
+    d.lds_A = 0;  // no quick-accept witness in probes
+    d.lds_nstage = A;
+    d.profile = 0;
+    hipStream_t s = c->stream;
+    const std::vector<int32_t>& coff = c->cons_off;
+    int maxp = 0;  // ring capacity: pods of the largest probe
+    if (mode == KP_CONSOLIDATE_SINGLE) {
+        for (int i = b0; i < b1; i++) maxp = std::max(maxp, coff[i + 1] - coff[i]);
+    } else {
+        maxp = coff[std::min(NC, b1 + 1)];
+    }
+    k.mode = mode;
+    k.n_probes = nprobe;
+    k.probe0 = b0;
+    k.ring_cap = std::max(1, c->cons_n_pending + maxp);
+    if (!kp_cons_plan_lds(d, k, KP_LDS_BYTES)) return fail(ctx, KP_E_UNSUPPORTED, "consolidation LDS plan exceeds 160 KB");
+    const int occ = std::max(1, std::min(8, KP_LDS_BYTES / std::max(k.lds_bytes, 1)));
+    const int workers = std::min(nprobe, 256 * occ);
+    const auto t0 = clk::now();
     HIPCHK(c->d_ring.ensure((size_t)workers * k.ring_cap));
     HIPCHK(c->d_ring_last.ensure((size_t)workers * k.ring_cap));
     HIPCHK(c->d_delta.ensure((size_t)workers * std::max(A, 1) * std::max(E, 1)));
-    HIPCHK(c->d_pbits.ensure((size_t)workers * k.PW));
-    HIPCHK(hipMemsetAsync(c->d_pbits.p, 0, (size_t)workers * k.PW * 8, s));
+    const size_t pb = (size_t)workers * k.PW;
+    if (c->d_pbits.n < pb) {  // kept all-zero between probes by the kernel
+        HIPCHK(c->d_pbits.ensure(pb));
+        HIPCHK(hipMemsetAsync(c->d_pbits.p, 0, pb * 8, s));
+    }
     HIPCHK(c->d_probe_out.ensure(nprobe));
-    HIPCHK(c->d_cons_stats.ensure(CS_COUNT));
     HIPCHK(hipMemsetAsync(c->d_cons_stats.p, 0, CS_COUNT * sizeof(int64_t), s));
     HIPCHK(hipMemsetAsync(c->d_next.p, 0, sizeof(int32_t), s));
+    HIPCHK(hipMemsetAsync(c->d_pend_bits.p, 0, (size_t)k.PW * 8, s));
     if (!c->h_remaining.empty())
         HIPCHK(hipMemcpyAsync(c->d_remaining.p, c->h_remaining.data(), c->h_remaining.size() * sizeof(int64_t),
                               hipMemcpyHostToDevice, s));
@@ -1497,7 +1531,7 @@ extern "C" kp_status kp_consolidate(kp_ctx* ctx, const kp_consolidate_input* in,
                              c->d_sort_temp.p, &tb, s, &q0));
     }
     d.queue0 = q0;
-    HIPCHK(kp_launch_cons_prep(q0, P, c->d_rank.p, c->d_pending.p, in->n_pending, c->d_pend_bits.p, s));
+    HIPCHK(kp_launch_cons_prep(q0, P, c->d_rank.p, c->d_pending.p, c->cons_n_pending, c->d_pend_bits.p, s));
     HIPCHK(kp_launch_class_mask(d, s));
     HIPCHK(kp_launch_template_init(d, s));
     HIPCHK(kp_launch_existing(d, s));
@@ -1511,7 +1545,6 @@ extern "C" kp_status kp_consolidate(kp_ctx* ctx, const kp_consolidate_input* in,
     k.pend_bits = c->d_pend_bits.p;
     k.initialized = c->d_init.p;
     k.alloc_act = c->d_alloc_act.p;
-    k.astride = astride;
     k.ring = c->d_ring.p;
     k.ring_last = c->d_ring_last.p;
     k.delta = c->d_delta.p;
@@ -1535,6 +1568,20 @@ extern "C" kp_status kp_consolidate(kp_ctx* ctx, const kp_consolidate_input* in,
     return KP_OK;
 } catch (const std::exception& e) {
     return fail(ctx, KP_E_INVALID, e.what());
+}
+
+extern "C" kp_status kp_consolidate(kp_ctx* ctx, const kp_consolidate_input* in, kp_probe_result* results,
+                                    int32_t cap_results) {
+    if (!ctx || !in) return KP_E_INVALID;
+    const int np = kp_consolidate_probe_count(in);
+    const int b0 = in->probe_begin > 0 ? in->probe_begin : 0;
+    const int b1 = in->probe_end > 0 && in->probe_end < np ? in->probe_end : np;
+    if (b0 > b1) return fail(ctx, KP_E_INVALID, "probe range outside the probe list");
+    if (b1 - b0 > cap_results || (b1 > b0 && !results)) return fail(ctx, KP_E_BUFFER, "probe results buffer too small");
+    kp_status st = kp_consolidate_prepare(ctx, in);
+    if (st != KP_OK) return st;
+    if (b1 == b0) return KP_OK;
+    return kp_consolidate_execute(ctx, in->mode, b0, b1, results, cap_results);
 }
 
 extern "C" kp_status kp_consolidate_stats(kp_ctx* ctx, double* ms, int64_t* counters, int32_t n_counters) {

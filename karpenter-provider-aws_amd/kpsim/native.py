@@ -11,7 +11,7 @@ EXPORTS = [
     "kp_ctx_create", "kp_ctx_destroy", "kp_last_error", "kp_version", "kp_catalog_upload", "kp_catalog_patch_avail",
     "kp_catalog_patch_price", "kp_solve", "kp_solve_prepare", "kp_solve_execute", "kp_solve_fetch",
     "kp_result_nodeclaim_requirements", "kp_last_kernel_times", "kp_consolidate_probe_count", "kp_consolidate",
-    "kp_consolidate_stats",
+    "kp_consolidate_stats", "kp_consolidate_prepare", "kp_consolidate_execute",
 ]
 
 _lib = None
@@ -49,6 +49,9 @@ def load():
     L.kp_consolidate_probe_count.argtypes = [C.POINTER(abi.kp_consolidate_input)]
     L.kp_consolidate.argtypes = [C.c_void_p, C.POINTER(abi.kp_consolidate_input), C.POINTER(abi.kp_probe_result),
                                  C.c_int32]
+    L.kp_consolidate_prepare.argtypes = [C.c_void_p, C.POINTER(abi.kp_consolidate_input)]
+    L.kp_consolidate_execute.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(abi.kp_probe_result),
+                                         C.c_int32]
     L.kp_consolidate_stats.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.c_int32]
     for f in EXPORTS:
         if f not in ("kp_last_error", "kp_version"):
@@ -140,6 +143,19 @@ class Context:
         self.check(self.L.kp_consolidate(self.h, C.byref(v), out.ctypes.data_as(C.POINTER(abi.kp_probe_result)),
                                          len(out)), "kp_consolidate")
         return out[:max(0, b1 - b0)]
+
+    def consolidate_prepare(self, cons_view):
+        self.check(self.L.kp_consolidate_prepare(self.h, C.byref(cons_view.view)), "kp_consolidate_prepare")
+
+    def consolidate_execute(self, mode, n_probes, begin=0, end=0):
+        """Probes [begin, end) of `mode` over the prepared pass; n_probes = the mode's probe count."""
+        import numpy as np
+        b1 = end if 0 < end < n_probes else n_probes
+        out = np.zeros(max(1, b1 - begin), abi.PROBE_DTYPE)
+        self.check(self.L.kp_consolidate_execute(self.h, mode, begin, end,
+                                                 out.ctypes.data_as(C.POINTER(abi.kp_probe_result)), len(out)),
+                   "kp_consolidate_execute")
+        return out[:max(0, b1 - begin)]
 
     def consolidate_stats(self):
         """(ms[prep, probe kernel, call], counters[8]) of the last kp_consolidate (kpsim.h kp_consolidate_stats)."""
