@@ -101,7 +101,11 @@ def consolidation_leg(a, cat, local, rank, world, dist, barrier):
         "decisions": {"single": [cs.decision, cs.candidates[:1]], "multi": [cm.decision, len(cm.candidates)]},
         "kernel_ms_rank0": {"single_prep": km[0], "single_probes": km[1], "multi_prep": km[2], "multi_probes": km[3]},
         "counters_per_step": dict(zip(["pods_popped", "existing_slots", "nodeclaim_evals", "template_evals", "probes",
-                                       "bitmap_words", "placed_existing", "new_nodeclaims"], [int(x) for x in cst])),
+                                       "bitmap_words", "placed_existing", "new_nodeclaims", "chunk_loads", "chunk_hits",
+                                       "cyc_build", "cyc_scan", "cyc_nodeclaim", "cyc_decide", "cyc_total"],
+                                      [int(x) for x in cst])),
+        "counters_multi": dict(zip(["pods_popped", "existing_slots", "chunk_loads", "chunk_hits", "cyc_build",
+                                    "cyc_scan", "cyc_total"], [int(st_m[1][i]) for i in (0, 1, 8, 9, 10, 11, 14)])),
         "roofline": {"bound": "hbm", "kernel": "consolidate_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes": int(B),
                      "kernel_ms": float(km[1] + km[3])},

@@ -328,8 +328,10 @@ kp_status kp_consolidate_prepare(kp_ctx* ctx, const kp_consolidate_input* in);
 kp_status kp_consolidate_execute(kp_ctx* ctx, int32_t mode, int32_t probe_begin, int32_t probe_end,
                                  kp_probe_result* results, int32_t cap_results);
 /* Diagnostics of the last kp_consolidate: ms[3] = {device prep (queue sort, masks), probe kernel, whole call};
- * counters[8] = {pods popped, existing-node slots examined, NodeClaim evaluations, template evaluations, probes,
- * queue-bitmap words scanned, existing-node placements, new NodeClaims}. */
+ * counters[16] = {pods popped, existing-node slots examined, NodeClaim evaluations, template evaluations, probes,
+ * queue-bitmap words scanned, existing-node placements, new NodeClaims, node chunks loaded, cached-chunk hits, then
+ * with KPSIM_PROFILE set: s_memtime cycles of queue build, existing-node scans, NodeClaim/template evaluation,
+ * decision, whole probe (summed over probes)}. */
 kp_status kp_consolidate_stats(kp_ctx* ctx, double* ms, int64_t* counters, int32_t n_counters);
 
 /*

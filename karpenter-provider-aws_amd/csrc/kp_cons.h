@@ -11,7 +11,10 @@
 #include "kp_layout.h"
 
 enum { CS_POPS = 0, CS_EX_NODES, CS_NC_EVALS, CS_TMPL_EVALS, CS_PROBES, CS_BITMAP_WORDS, CS_PLACED_EXISTING,
-       CS_NEW_NC, CS_COUNT = 8 };
+       CS_NEW_NC, CS_CHUNK_LOADS, CS_CACHE_HITS, CS_CYC_BUILD, CS_CYC_SCAN, CS_CYC_NODECLAIM, CS_CYC_DECIDE,
+       CS_CYC_TOTAL, CS_COUNT = 16 };
+
+#define KP_CONS_XTC 1024  // pod classes whose XT column of the cached node chunk is kept in LDS
 
 struct KpCons {
     int32_t n_probes;           // probes of this call: global probe ids probe0 .. probe0 + n_probes - 1
@@ -30,7 +33,8 @@ struct KpCons {
     const int32_t* rank;        // [P] queue position of each pod (NewQueue order)
     const uint64_t* pend_bits;  // [PW] pending pods by queue position
     int32_t PW;
-    const uint8_t* initialized; // [E] StateNode.Initialized()
+    const uint64_t* init_bits;  // [EW] StateNode.Initialized() by node
+    int32_t n_pending;
     const int64_t* alloc_act;   // [n_active][astride] allocatable of the active axes (EvalEnv.alloc)
     int32_t astride;
     // per-worker scratch
@@ -39,9 +43,12 @@ struct KpCons {
     int32_t* ring_last;         // [workers][ring_cap] Queue.lastLen of the entry (-1: never pushed)
     int64_t* delta;             // [workers][n_active][E] requests added to node j by this probe (valid: mod bit)
     uint64_t* pbits;            // [workers][PW] probe pods by queue position (all zero between probes)
-    int32_t* next_probe;        // [1] work counter
+    int32_t* next_probe;        // [3] work counters: fast variant, full variant, probes handed to the full variant
+    int32_t* retry;             // [n_probes] probes the fast variant handed over
     kp_probe_result* out;       // [n_probes]
     int64_t* stats;             // [CS_COUNT]
+    int32_t profile;            // s_memtime stage cycles (KPSIM_PROFILE)
+    int32_t no_fast;            // diagnostics: every probe on the FULL variant (KPSIM_CONS_NOFAST)
     // dynamic LDS plan (kp_cons_plan_lds)
-    int32_t off_hdr, off_words, off_rem, off_excl, off_mod, lds_bytes;
+    int32_t off_hdr, off_words, off_rem, off_excl, off_mod, off_init, off_xtc, lds_bytes;
 };

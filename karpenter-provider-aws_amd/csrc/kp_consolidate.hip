@@ -31,6 +31,7 @@ struct ConsShared {
     WaveScratch ws;
     Roles roles;
     int64_t nc_req[KP_MAX_R];
+    int64_t st[CS_COUNT];
 };
 
 __device__ __forceinline__ int32_t ld32(const int32_t* p) {
@@ -88,6 +89,9 @@ __device__ inline double worst_launch_price(const KpDev& d, const KpCons& k, int
 
 }  // namespace
 
+// FULL = false: the fast variant handles probes whose pods all fit existing nodes (no NodeClaim code, a small register
+// footprint); a probe that needs a NodeClaim is handed to the FULL variant through k.retry.
+template <bool FULL>
 __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     ConsShared& S = *reinterpret_cast<ConsShared*>(smem);
@@ -96,6 +100,8 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
     int64_t* rem = reinterpret_cast<int64_t*>(smem + k.off_rem);
     uint64_t* excl = reinterpret_cast<uint64_t*>(smem + k.off_excl);
     uint64_t* modb = reinterpret_cast<uint64_t*>(smem + k.off_mod);
+    uint64_t* initb = reinterpret_cast<uint64_t*>(smem + k.off_init);
+    uint64_t* xtc = reinterpret_cast<uint64_t*>(smem + k.off_xtc);  // XT column of the cached chunk, by class
     const int lane = threadIdx.x;
     const int wid = blockIdx.x;
     const int E = d.E, EW = d.EW, A = d.n_active, R = d.R, K = d.K, TW = d.TW, T = d.T, NT = d.NT;
@@ -112,6 +118,8 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
         S.roles.nw[lane] = rk >= 0 ? d.nw[rk] : 0;
     }
     if (lane == 0) S.CC.cls = -1;
+    if (lane < CS_COUNT) S.st[lane] = 0;
+    for (int w = lane; w < EW; w += 64) initb[w] = k.init_bits[w];
     __syncthreads();
     EvalEnv Ev;
     Ev.alloc = k.alloc_act;
@@ -124,15 +132,29 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
     Ev.roles = &S.roles;
     Ev.min_tmpl_mask = 0;  // minValues templates are rejected by kp_consolidate
 
-    for (;;) {
+    for (int it = 0;; it++) {
         int probe = 0;
-        if (lane == 0) probe = atomicAdd(k.next_probe, 1);
-        probe = __builtin_amdgcn_readfirstlane(__shfl(probe, 0));
+        if (!FULL) {  // static stride: a shared work counter serialises in L2 at thousands of probes
+            probe = wid + it * (int)gridDim.x;
+        } else {
+            if (lane == 0) {
+                if (k.no_fast == 1) {
+                    probe = atomicAdd(&k.next_probe[0], 1);
+                } else {
+                    const int i = atomicAdd(&k.next_probe[1], 1);
+                    probe = i < ld32(&k.next_probe[2]) ? k.retry[i] : k.n_probes;
+                }
+            }
+            probe = __builtin_amdgcn_readfirstlane(__shfl(probe, 0));
+        }
         if (probe >= k.n_probes) break;
         const int gp = k.probe0 + probe;
         const bool single = k.mode == KP_CONSOLIDATE_SINGLE;
         const int c0 = single ? gp : 0, c1 = single ? gp + 1 : gp + 2;
-        int64_t st_pops = 0, st_nodes = 0, st_nc = 0, st_tmpl = 0, st_words = 0, st_placed = 0;
+        int64_t st_pops = 0, st_nodes = 0, st_nc = 0, st_tmpl = 0, st_words = 0, st_placed = 0, st_loads = 0, st_hits = 0;
+        long long cy_build = 0, cy_scan = 0, cy_nc = 0, cy_dec = 0;
+        const bool prof = k.profile != 0;
+        const long long cy0 = prof ? __builtin_amdgcn_s_memtime() : 0;
 
         // ---- probe state: excluded candidates, modified nodes, NodePool limits + candidate capacity ----
         for (int w = lane; w < EW; w += 64) {
@@ -156,7 +178,35 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             if (j >= 0 && lane < R && d.limit_set[(size_t)j * R + lane])
                 rem[j * R + lane] += k.cand_cap[(size_t)c * R + lane];
         }
-        // ---- the probe's pods in queue order: mark queue positions, then scan the bitmap with the pending pods ----
+        // ---- the probe's pods in queue order ----
+        int n = 0;
+        if (k.n_pending == 0 && n_np <= 64) {
+            // at most one pod per lane: bitonic sort of (queue position, pod) across the wave
+            int myp = -1;
+            {
+                int i = lane;
+                for (int c = c0; c < c1 && myp < 0; c++) {
+                    const int cnt = k.cand_off[c + 1] - k.cand_off[c];
+                    if (i < cnt) myp = k.cand_pods[k.cand_off[c] + i];
+                    else i -= cnt;
+                }
+            }
+            uint64_t key = myp >= 0 ? ((uint64_t)(uint32_t)k.rank[myp] << 32) | (uint32_t)myp : ~0ull;
+            for (int kk = 2; kk <= 64; kk <<= 1)
+                for (int j = kk >> 1; j > 0; j >>= 1) {
+                    const uint64_t o = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(key >> 32), j) << 32) |
+                                       (uint32_t)__shfl_xor((int)(uint32_t)key, j);
+                    const bool up = (lane & kk) == 0, lower = (lane & j) == 0;
+                    const uint64_t mn = o < key ? o : key, mx = o < key ? key : o;
+                    key = (lower == up) ? mn : mx;
+                }
+            if (lane < n_np) {
+                ring[lane] = (int32_t)(uint32_t)key;
+                rlast[lane] = -1;
+            }
+            n = n_np;
+        } else {
+        // mark queue positions, then scan the bitmap with the pending pods
         for (int c = c0; c < c1; c++) {
             const int o0 = k.cand_off[c], o1 = k.cand_off[c + 1];
             for (int i = o0 + lane; i < o1; i += 64) {
@@ -166,7 +216,6 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        int n = 0;
         for (int wb = 0; wb < k.PW; wb += 64) {
             const int w = wb + lane;
             uint64_t mine = 0, pend = 0;
@@ -195,9 +244,11 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             n += total;
         }
         st_words += k.PW;
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
 
+        if (prof) cy_build = __builtin_amdgcn_s_memtime() - cy0;
         // ---- Solve: queue with lastLen termination; existing nodes, the in-flight NodeClaim, the templates ----
         int head = 0, count = n, wbase = -64;
         int vpod = -1, vlast = -1, vc = 0, vshape = -1;
@@ -224,6 +275,12 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             }
         };
         int n_nc = 0, nc_tmpl = -1, prev_shape = -1, xstart = 0, ok_np = 0;
+        bool aborted = false;
+        int cbase = -1, ccls = -1;  // cached node chunk (wave-uniform)
+        uint64_t cx = 0;
+        int64_t ch[KP_LDS_AXES], cd[KP_LDS_AXES];
+#pragma unroll
+        for (int ai = 0; ai < KP_LDS_AXES; ai++) ch[ai] = cd[ai] = 0;
         bool bad = false, stop = false;
         uint64_t nc_opts = 0;
         while (count > 0) {
@@ -249,56 +306,107 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 prev_shape = shape;
                 xstart = 0;
             }
-            // ExistingNode.Add in scheduling order (candidates excluded)
+            // ExistingNode.Add in scheduling order (candidates excluded), 64-node aligned chunks; the chunk of the last
+            // placement stays in registers (effective headroom and this probe's added requests per lane)
             int jf = -1;
-            for (int base = xstart; base < E; base += 64) {
+            const long long cs0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+            for (int base = xstart & ~63; base < E; base += 64) {
+                const int w = base >> 6;
                 const int j = base + lane;
-                bool cand = false;
-                if (j < E) {
-                    const uint64_t xw = d.XT[(size_t)c * EW + (j >> 6)] & ~excl[j >> 6];
-                    cand = (xw >> (j & 63)) & 1ull;
-                    if (cand) {
-                        const bool md = (modb[j >> 6] >> (j & 63)) & 1ull;
+                const uint64_t ge = xstart > base ? (~0ull << (xstart - base)) : ~0ull;
+                uint64_t xw;
+                int64_t h[KP_LDS_AXES], dl[KP_LDS_AXES];
+                if (base == cbase) {
+                    st_hits++;
+                    if (ccls != c) {
+                        cx = (d.C <= KP_CONS_XTC) ? xtc[c] : (d.XT[(size_t)c * EW + w] & ~excl[w]);
+                        ccls = c;
+                    }
+                    xw = cx;
 #pragma unroll
-                        for (int ai = 0; ai < KP_LDS_AXES; ai++) {
-                            if (ai < A) {
-                                int64_t h = d.ex_head[(size_t)ai * E + j];
-                                if (md) h -= ld_req(&delta[(size_t)ai * E + j]);
-                                cand &= q[ai] <= h;
-                            }
+                    for (int ai = 0; ai < KP_LDS_AXES; ai++) {
+                        h[ai] = ch[ai];
+                        dl[ai] = cd[ai];
+                    }
+                } else {
+                    xw = d.XT[(size_t)c * EW + w] & ~excl[w];
+                    if (!(xw & ge)) {
+                        st_nodes += 64;
+                        continue;
+                    }
+                    st_loads++;
+                    const uint64_t mw = modb[w];
+                    if (mw & xw) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this probe's delta stores landed
+                    const bool md = (mw >> lane) & 1ull;
+#pragma unroll
+                    for (int ai = 0; ai < KP_LDS_AXES; ai++) {
+                        h[ai] = 0;
+                        dl[ai] = 0;
+                        if (ai < A && j < E) {
+                            h[ai] = d.ex_head[(size_t)ai * E + j];
+                            if (md) dl[ai] = ld_req(&delta[(size_t)ai * E + j]);
+                            h[ai] -= dl[ai];
                         }
                     }
                 }
+                bool cand = (xw & ge) >> lane & 1ull;
+#pragma unroll
+                for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                    if (ai < A) cand &= q[ai] <= h[ai];
                 st_nodes += 64;
                 const uint64_t m = ballot(cand);
                 if (m) {
                     jf = base + __ffsll((unsigned long long)m) - 1;
+                    if (base != cbase) {
+                        // evict: this probe's requests on the old chunk go to the delta slab (read back past L1)
+                        if (cbase >= 0 && ((modb[cbase >> 6] >> lane) & 1ull)) {
+#pragma unroll
+                            for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                                if (ai < A)
+                                    __hip_atomic_store(&delta[(size_t)ai * E + cbase + lane], cd[ai], __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                        if (d.C <= KP_CONS_XTC)
+                            for (int cc = lane; cc < d.C; cc += 64) xtc[cc] = d.XT[(size_t)cc * EW + w] & ~excl[w];
+                        cbase = base;
+                        cx = xw;
+                        ccls = c;
+#pragma unroll
+                        for (int ai = 0; ai < KP_LDS_AXES; ai++) {
+                            ch[ai] = h[ai];
+                            cd[ai] = dl[ai];
+                        }
+                    }
                     break;
                 }
             }
+            if (prof) cy_scan += __builtin_amdgcn_s_memtime() - cs0;
             if (jf >= 0) {
-                const bool md = (modb[jf >> 6] >> (jf & 63)) & 1ull;
-                if (lane < A) {
-                    int64_t qq = 0;
+                if (lane == jf - cbase) {
 #pragma unroll
-                    for (int ai = 0; ai < KP_LDS_AXES; ai++)
-                        if (lane == ai) qq = q[ai];
-                    int64_t* dp = &delta[(size_t)lane * E + jf];
-                    __hip_atomic_store(dp, md ? ld_req(dp) + qq : qq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    for (int ai = 0; ai < KP_LDS_AXES; ai++) {
+                        if (ai < A) {
+                            ch[ai] -= q[ai];
+                            cd[ai] += q[ai];
+                        }
+                    }
                 }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0 && !md) modb[jf >> 6] |= 1ull << (jf & 63);
-                __syncthreads();
+                if (lane == 0) modb[jf >> 6] |= 1ull << (jf & 63);
                 xstart = jf;
                 st_placed++;
                 if (!pend) {
-                    if (k.initialized[jf]) ok_np++;
+                    if ((initb[jf >> 6] >> (jf & 63)) & 1ull) ok_np++;
                     else bad = true;  // SimulateScheduling: uninitialized-node placement is an error
                 }
                 continue;
             }
             xstart = E;
+            if constexpr (!FULL) {
+                aborted = true;  // needs a NodeClaim: the FULL variant redoes this probe
+                break;
+            }
             bool placed = false;
+            const long long cn0 = prof ? __builtin_amdgcn_s_memtime() : 0;
             const int64_t* preq = d.pod_req + (size_t)p * R;
             if (n_nc == 1) {  // NodeClaim.Add on the in-flight NodeClaim
                 if (S.CC.cls != c) fill_class_cache(d, c, S.CC, lane, 64);
@@ -378,6 +486,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     break;
                 }
             }
+            if (prof) cy_nc += __builtin_amdgcn_s_memtime() - cn0;
             if (stop) break;
             if (placed) {
                 if (!pend) ok_np++;
@@ -401,14 +510,21 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
 
+        if (!FULL && aborted) {
+            if (lane == 0) {
+                const int slot = atomicAdd(&k.next_probe[2], 1);
+                k.retry[slot] = probe;
+            }
+        } else {
         // ---- computeConsolidation ----
+        const long long cd0 = prof ? __builtin_amdgcn_s_memtime() : 0;
         int decision = KP_DECISION_NONE, valid = 0, nrep = 0;
         double rprice = 0.0;
         const bool all = !stop && !bad && ok_np == n_np;
         if (all && n_nc == 0) {
             decision = KP_DECISION_DELETE;
             valid = 1;
-        } else if (all) {
+        } else if (FULL && all) {
             // Offerings.Available().Compatible(NodeClaim requirements) over zone × capacity-type slots
             bool okslot = false;
             if (lane < d.n_slots) {
@@ -537,6 +653,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 rprice = nrep ? wave_min_f64(keep ? wl : DBL_MAX) : 0.0;
             }
         }
+        if (prof) cy_dec = __builtin_amdgcn_s_memtime() - cd0;
         if (lane == 0) {
             kp_probe_result o;
             o.decision = decision;
@@ -548,18 +665,29 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             o.candidate_price = cprice;
             o.replacement_price = rprice;
             k.out[probe] = o;
-            atomicAdd((unsigned long long*)&k.stats[CS_POPS], (unsigned long long)st_pops);
-            atomicAdd((unsigned long long*)&k.stats[CS_EX_NODES], (unsigned long long)st_nodes);
-            atomicAdd((unsigned long long*)&k.stats[CS_NC_EVALS], (unsigned long long)st_nc);
-            atomicAdd((unsigned long long*)&k.stats[CS_TMPL_EVALS], (unsigned long long)st_tmpl);
-            atomicAdd((unsigned long long*)&k.stats[CS_PROBES], 1ull);
-            atomicAdd((unsigned long long*)&k.stats[CS_BITMAP_WORDS], (unsigned long long)st_words);
-            atomicAdd((unsigned long long*)&k.stats[CS_PLACED_EXISTING], (unsigned long long)st_placed);
-            atomicAdd((unsigned long long*)&k.stats[CS_NEW_NC], (unsigned long long)(stop ? 2 : n_nc));
+            // counters stay in LDS until the worker exits (per-probe global atomics on 16 words serialise in L2)
+            S.st[CS_POPS] += st_pops;
+            S.st[CS_EX_NODES] += st_nodes;
+            S.st[CS_NC_EVALS] += st_nc;
+            S.st[CS_TMPL_EVALS] += st_tmpl;
+            S.st[CS_PROBES] += 1;
+            S.st[CS_BITMAP_WORDS] += st_words;
+            S.st[CS_PLACED_EXISTING] += st_placed;
+            S.st[CS_NEW_NC] += stop ? 2 : n_nc;
+            S.st[CS_CHUNK_LOADS] += st_loads;
+            S.st[CS_CACHE_HITS] += st_hits;
+            if (prof) {
+                S.st[CS_CYC_BUILD] += cy_build;
+                S.st[CS_CYC_SCAN] += cy_scan;
+                S.st[CS_CYC_NODECLAIM] += cy_nc;
+                S.st[CS_CYC_DECIDE] += cy_dec;
+                S.st[CS_CYC_TOTAL] += __builtin_amdgcn_s_memtime() - cy0;
+            }
         }
-        if (lane == 0) S.CC.cls = -1;  // the class cache is refilled lazily per probe
+        }
         __syncthreads();
     }
+    if (lane < CS_COUNT && S.st[lane]) atomicAdd((unsigned long long*)&k.stats[lane], (unsigned long long)S.st[lane]);
 }
 
 // queue position of each pod: rank[queue0[i]] = i
@@ -590,6 +718,10 @@ bool kp_cons_plan_lds(const KpDev& d, KpCons& k, int max_bytes) {
     off = al(off + 8 * (size_t)(d.EW > 0 ? d.EW : 1));
     k.off_mod = (int)off;
     off = al(off + 8 * (size_t)(d.EW > 0 ? d.EW : 1));
+    k.off_init = (int)off;
+    off = al(off + 8 * (size_t)(d.EW > 0 ? d.EW : 1));
+    k.off_xtc = (int)off;
+    off = al(off + 8 * (size_t)(d.C < KP_CONS_XTC ? (d.C > 0 ? d.C : 1) : KP_CONS_XTC));
     k.lds_bytes = (int)off;
     return (int)off <= max_bytes;
 }
@@ -597,13 +729,17 @@ bool kp_cons_plan_lds(const KpDev& d, KpCons& k, int max_bytes) {
 hipError_t kp_launch_consolidate(const KpDev& d, const KpCons& k, int n_workers, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)consolidate_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           KP_LDS_BYTES);
+        hipError_t e = hipFuncSetAttribute((const void*)consolidate_kernel<false>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, KP_LDS_BYTES);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)consolidate_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    KP_LDS_BYTES);
         if (e != hipSuccess) return e;
         attr = true;
     }
     if (n_workers <= 0 || k.n_probes <= 0) return hipSuccess;
-    hipLaunchKernelGGL(consolidate_kernel, dim3(n_workers), dim3(64), (size_t)k.lds_bytes, s, d, k);
+    if (k.no_fast != 1) hipLaunchKernelGGL(consolidate_kernel<false>, dim3(n_workers), dim3(64), (size_t)k.lds_bytes, s, d, k);
+    if (k.no_fast != 2) hipLaunchKernelGGL(consolidate_kernel<true>, dim3(n_workers), dim3(64), (size_t)k.lds_bytes, s, d, k);
     return hipGetLastError();
 }
 

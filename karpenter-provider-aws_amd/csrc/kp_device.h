@@ -23,6 +23,23 @@ __device__ __forceinline__ uint64_t rl64(uint64_t x, int lane) {
 __device__ __forceinline__ int rl32(int x, int lane) { return __builtin_amdgcn_readlane(x, lane); }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
+// KpDev's small arrays are read with constant indices only: a runtime index into the by-value kernel argument makes
+// the compiler copy the whole struct to scratch.  These select the element through a compare chain instead.
+__device__ __forceinline__ int act_axis(const KpDev& d, int ai) {
+    int r = 0;
+#pragma unroll
+    for (int i = 0; i < KP_MAX_R; i++)
+        if (i == ai) r = d.active_axes[i];
+    return r;
+}
+__device__ __forceinline__ int qshift_of(const KpDev& d, int ai) {
+    int r = 0;
+#pragma unroll
+    for (int i = 0; i < KP_LDS_AXES; i++)
+        if (i == ai) r = d.qshift[i];
+    return r;
+}
+
 // Requirement.Operator() of a DEFINED requirement with `nvals` values
 __device__ __forceinline__ int req_op(uint32_t flags, int nvals) {
     if (flags & RF_CMP) return nvals > 0 ? OP_NOTIN : OP_EXISTS;

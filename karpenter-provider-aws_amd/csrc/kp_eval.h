@@ -219,7 +219,7 @@ struct WitnessAcc {
             if (lane == ai) my = tot[ai];
         if (lane < A) {
             const int64_t h = E.alloc[lane * E.astride + bt] - my;
-            ws.hr[lane] = h < 0 ? -1 : (int32_t)(h >> d.qshift[lane]);
+            ws.hr[lane] = h < 0 ? -1 : (int32_t)(h >> qshift_of(d, lane));
         }
     }
 };
@@ -353,7 +353,7 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
             }
         }
         for (int x = 0; x < n_extra; x++) {
-            const int r = d.active_axes[KP_LDS_AXES + x];
+            const int r = act_axis(d, KP_LDS_AXES + x);
             const int64_t tr = (a.base_req ? ld_req(a.base_req + r) : 0) + (a.pod_req ? a.pod_req[r] : 0);
             if (tr > 0) fit &= tr <= d.alloc[(size_t)r * T + (t < T ? t : 0)];
         }
@@ -468,7 +468,7 @@ __device__ __forceinline__ bool eval_fits_only(const KpDev& d, const EvalEnv& E,
             keep &= !(tot[ai] > 0) | (tot[ai] <= av[ai]);
         }
         for (int x = 0; x < n_extra; x++) {
-            const int r = d.active_axes[KP_LDS_AXES + x];
+            const int r = act_axis(d, KP_LDS_AXES + x);
             const int64_t tr = ld_req(a.base_req + r) + a.pod_req[r];
             if (tr > 0) keep &= tr <= d.alloc[(size_t)r * T + (t < T ? t : 0)];
         }

@@ -234,11 +234,11 @@ struct kp_ctx {
     bool any_min_values = false;             // some template requirement carries minValues
     bool cons_mayfix = false;                // a pod's NotIn/DoesNotExist merge can change a later Compatible
     // consolidation probes
-    DBuf<int32_t> d_rank, d_cand_i, d_cand_off, d_cand_pods, d_pending, d_ring, d_ring_last, d_next;
+    DBuf<int32_t> d_retry, d_rank, d_cand_i, d_cand_off, d_cand_pods, d_pending, d_ring, d_ring_last, d_next;
     DBuf<double> d_cand_price;
     DBuf<int64_t> d_cand_cap, d_delta, d_alloc_act, d_cons_stats;
     DBuf<uint64_t> d_pend_bits, d_pbits;
-    DBuf<uint8_t> d_init;
+    DBuf<uint64_t> d_init;
     DBuf<kp_probe_result> d_probe_out;
     KpCons cons{};                           // prepared consolidation pass (device pointers set per execute)
     bool cons_prepared = false;
@@ -318,7 +318,7 @@ extern "C" kp_status kp_ctx_destroy(kp_ctx* ctx) {
     ctx->d_nc_count.release(); ctx->d_nc_npods.release(); ctx->d_nc_slice_pos.release(); ctx->d_nc_nopts.release();
     ctx->d_nc_valid.release(); ctx->d_nc_types.release(); ctx->d_nc_ntypes.release(); ctx->d_err.release();
     ctx->d_sort_temp.release();
-    ctx->d_rank.release(); ctx->d_cand_i.release(); ctx->d_cand_off.release(); ctx->d_pending.release(); ctx->d_cand_pods.release(); ctx->d_ring.release();
+    ctx->d_retry.release(); ctx->d_rank.release(); ctx->d_cand_i.release(); ctx->d_cand_off.release(); ctx->d_pending.release(); ctx->d_cand_pods.release(); ctx->d_ring.release();
     ctx->d_ring_last.release(); ctx->d_next.release(); ctx->d_cand_price.release(); ctx->d_cand_cap.release();
     ctx->d_delta.release(); ctx->d_alloc_act.release(); ctx->d_cons_stats.release(); ctx->d_pend_bits.release();
     ctx->d_pbits.release(); ctx->d_init.release(); ctx->d_probe_out.release();
@@ -1441,9 +1441,9 @@ extern "C" kp_status kp_consolidate_prepare(kp_ctx* ctx, const kp_consolidate_in
     if (cpods.empty()) cpods.push_back(0);
     std::vector<int32_t> pend(in->pending, in->pending + in->n_pending);
     if (pend.empty()) pend.push_back(0);
-    std::vector<uint8_t> init(std::max(E, 1), 1);
-    if (in->initialized)
-        for (int j = 0; j < E; j++) init[j] = in->initialized[j] ? 1 : 0;
+    std::vector<uint64_t> init(std::max(d.EW, 1), 0);
+    for (int j = 0; j < E; j++)
+        if (!in->initialized || in->initialized[j]) init[j >> 6] |= 1ull << (j & 63);
     const int astride = TW * 64;
     std::vector<int64_t> act((size_t)std::max(A, 1) * astride, 0);
     for (int ai = 0; ai < A; ai++)
@@ -1458,7 +1458,7 @@ extern "C" kp_status kp_consolidate_prepare(kp_ctx* ctx, const kp_consolidate_in
     HIPCHK(c->d_cand_cap.upload(ccap, s));
     HIPCHK(c->d_init.upload(init, s));
     HIPCHK(c->d_alloc_act.upload(act, s));
-    HIPCHK(c->d_next.ensure(1));
+    HIPCHK(c->d_next.ensure(3));
     HIPCHK(c->d_rank.ensure(std::max(P, 1)));
     HIPCHK(c->d_pend_bits.ensure(k.PW));
     HIPCHK(c->d_cons_stats.ensure(CS_COUNT));
@@ -1518,7 +1518,8 @@ extern "C" kp_status kp_consolidate_execute(kp_ctx* ctx, int32_t mode, int32_t p
     }
     HIPCHK(c->d_probe_out.ensure(nprobe));
     HIPCHK(hipMemsetAsync(c->d_cons_stats.p, 0, CS_COUNT * sizeof(int64_t), s));
-    HIPCHK(hipMemsetAsync(c->d_next.p, 0, sizeof(int32_t), s));
+    HIPCHK(hipMemsetAsync(c->d_next.p, 0, 3 * sizeof(int32_t), s));
+    HIPCHK(c->d_retry.ensure(nprobe));
     HIPCHK(hipMemsetAsync(c->d_pend_bits.p, 0, (size_t)k.PW * 8, s));
     if (!c->h_remaining.empty())
         HIPCHK(hipMemcpyAsync(c->d_remaining.p, c->h_remaining.data(), c->h_remaining.size() * sizeof(int64_t),
@@ -1543,15 +1544,19 @@ extern "C" kp_status kp_consolidate_execute(kp_ctx* ctx, int32_t mode, int32_t p
     k.cand_cap = c->d_cand_cap.p;
     k.rank = c->d_rank.p;
     k.pend_bits = c->d_pend_bits.p;
-    k.initialized = c->d_init.p;
+    k.init_bits = c->d_init.p;
+    k.n_pending = c->cons_n_pending;
     k.alloc_act = c->d_alloc_act.p;
     k.ring = c->d_ring.p;
     k.ring_last = c->d_ring_last.p;
     k.delta = c->d_delta.p;
     k.pbits = c->d_pbits.p;
     k.next_probe = c->d_next.p;
+    k.retry = c->d_retry.p;
     k.out = c->d_probe_out.p;
     k.stats = c->d_cons_stats.p;
+    k.profile = getenv("KPSIM_PROFILE") ? 1 : 0;
+    k.no_fast = getenv("KPSIM_CONS_NOFAST") ? atoi(getenv("KPSIM_CONS_NOFAST")) : 0;  // 1: FULL only, 2: fast only
     HIPCHK(kp_launch_consolidate(d, k, workers, s));
     HIPCHK(hipEventRecord(c->ev[2], s));
     HIPCHK(hipMemcpyAsync(results, c->d_probe_out.p, (size_t)nprobe * sizeof(kp_probe_result), hipMemcpyDeviceToHost, s));

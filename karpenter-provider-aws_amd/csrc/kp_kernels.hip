@@ -54,12 +54,12 @@ __global__ __launch_bounds__(256) void existing_init_kernel(KpDev d) {
     for (int r = 0; r < d.R; r++) {
         const int64_t av = d.ex_avail[(size_t)j * d.R + r], rq = d.ex_req[(size_t)j * d.R + r];
         bool act = false;
-        for (int ai = 0; ai < d.n_active; ai++) act |= d.active_axes[ai] == r;
+        for (int ai = 0; ai < d.n_active; ai++) act |= act_axis(d, ai) == r;
         if (av < 0 || (!act && rq > av)) ok = false;
     }
     d.ex_static[j] = ok ? 1 : 0;
     for (int ai = 0; ai < d.n_active; ai++) {
-        const int r = d.active_axes[ai];
+        const int r = act_axis(d, ai);
         d.ex_head[(size_t)ai * d.E + j] = d.ex_avail[(size_t)j * d.R + r] - d.ex_req[(size_t)j * d.R + r];
     }
 }
@@ -242,7 +242,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
     // ---- stage the type tables in LDS ----
     for (int i = tid; i < d.lds_nstage * TP; i += nthr) {
         const int ai = i / TP, t = i % TP;
-        sAlloc[i] = t < T ? d.alloc[(size_t)d.active_axes[ai] * T + t] : 0;
+        sAlloc[i] = t < T ? d.alloc[(size_t)act_axis(d, ai) * T + t] : 0;
     }
     for (int t = tid; t < TP; t += nthr) sAvail[t] = t < T ? d.avail_zc[t] : 0;
     if (d.multi16)
@@ -485,10 +485,13 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                             const uint64_t xw = __hip_atomic_load(&d.XT[(size_t)c * d.EW + (j >> 6)], __ATOMIC_RELAXED,
                                                                   __HIP_MEMORY_SCOPE_AGENT);
                             cand = (xw >> (j & 63)) & 1ull;
-                            for (int ai = 0; ai < d.n_active; ai++) {
-                                const int64_t pr = S.shape_req[d.active_axes[ai]];
-                                const int64_t h = ld_req(&d.ex_head[(size_t)ai * d.E + j]) - (j == xj ? pr * xcnt : 0);
-                                cand &= pr <= h;
+#pragma unroll
+                            for (int ai = 0; ai < KP_MAX_R; ai++) {
+                                if (ai < d.n_active) {
+                                    const int64_t pr = S.shape_req[d.active_axes[ai]];
+                                    const int64_t h = ld_req(&d.ex_head[(size_t)ai * d.E + j]) - (j == xj ? pr * xcnt : 0);
+                                    cand &= pr <= h;
+                                }
                             }
                         }
                         const uint64_t m = ballot(cand);
@@ -1052,7 +1055,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(KpDev d) {
         // Fits(final requests, Allocatable): the quick-accept path applies Fits lazily (pick_witness)
         bool fit = true;
         for (int ai = 0; ai < d.n_active; ai++) {
-            const int r = d.active_axes[ai];
+            const int r = act_axis(d, ai);
             const int64_t tr = s_tot[r];
             if (tr > 0 && tr > d.alloc[(size_t)r * T + t]) fit = false;
         }

@@ -158,10 +158,10 @@ class Context:
         return out[:max(0, b1 - begin)]
 
     def consolidate_stats(self):
-        """(ms[prep, probe kernel, call], counters[8]) of the last kp_consolidate (kpsim.h kp_consolidate_stats)."""
+        """(ms[prep, probe kernel, call], counters[16]) of the last kp_consolidate (kpsim.h kp_consolidate_stats)."""
         ms = (C.c_double * 3)()
-        ct = (C.c_int64 * 8)()
-        self.check(self.L.kp_consolidate_stats(self.h, ms, ct, 8), "kp_consolidate_stats")
+        ct = (C.c_int64 * 16)()
+        self.check(self.L.kp_consolidate_stats(self.h, ms, ct, 16), "kp_consolidate_stats")
         return list(ms), list(ct)
 
     def close(self):
