@@ -335,6 +335,53 @@ kp_status kp_consolidate_execute(kp_ctx* ctx, int32_t mode, int32_t probe_begin,
 kp_status kp_consolidate_stats(kp_ctx* ctx, double* ms, int64_t* counters, int32_t n_counters);
 
 /*
+ * Launch-time instance-type selection — replaces the pure-function part of CloudProvider.Create
+ * (pkg/cloudprovider/cloudprovider.go:90-137) → instance.DefaultProvider.Create (pkg/providers/instance/instance.go:132-137):
+ *   filterInstanceTypes (instance.go:270-298): the filter chain of pkg/providers/instance/filter/filter.go
+ *     CompatibleAvailableFilter :39-64, CapacityReservationTypeFilter :73-157, CapacityBlockFilter :163-221,
+ *     ReservedOfferingFilter :230-270, ExoticInstanceTypeFilter :279-318, SpotInstanceFilter :328-386
+ *     (a filter leaving no type → KP_E_INSUFFICIENT_CAPACITY, instance.go:281-284), then
+ *     [core] InstanceTypes.Truncate(reqs, max_instance_types) (instance.go:293; minValues failure → KP_E_CREATE :295);
+ *   getCapacityType (instance.go:532-546): reserved > spot > on-demand;
+ *   the offering side of getOverrides (instance.go:420-467): per kept type, its Available offerings Compatible with the
+ *     requirements narrowed to the chosen capacity type (the caller maps each offering's zone to a subnet).
+ * One request = one NodeClaim (Spec.Requirements with minValues, Spec.Resources.Requests) against the whole uploaded
+ * catalog (instanceTypeProvider.List, cloudprovider.go:116).  Requests are independent: a batch is evaluated in parallel.
+ * Order conventions where the reference iterates Go maps (filter.go:115,156,263: lo.Values): catalog row order for
+ * types and view row order for offerings.  The truncated list is ordered by (cheapest compatible available price, name).
+ */
+enum {
+    KP_FILTER_COMPATIBLE_AVAILABLE = 0, KP_FILTER_CAPACITY_RESERVATION_TYPE = 1, KP_FILTER_CAPACITY_BLOCK = 2,
+    KP_FILTER_RESERVED_OFFERING = 3, KP_FILTER_EXOTIC = 4, KP_FILTER_SPOT = 5, KP_N_FILTERS = 6
+};
+
+typedef struct kp_launch_request {
+    int32_t n_requirements;                  /* NodeClaim.Spec.Requirements (NewNodeSelectorRequirementsWithMinValues) */
+    const kp_requirement* requirements;
+    const int64_t* requests;                 /* [R] Spec.Resources.Requests (milli); 0 = resource not requested */
+} kp_launch_request;
+
+typedef struct kp_launch_result {
+    int32_t status;                          /* KP_OK | KP_E_INSUFFICIENT_CAPACITY | KP_E_CREATE */
+    int32_t failed_filter;                   /* KP_FILTER_* that left no type (ICE), else -1 */
+    int32_t capacity_type;                   /* KP_CT_* (getCapacityType) */
+    int32_t n_types;                         /* truncated, price-ordered types */
+    int32_t type_offset;                     /* into type_ids */
+    int32_t n_overrides;                     /* offering rows (catalog view order) of the kept types */
+    int32_t override_offset;                 /* into override_offerings */
+    int32_t n_options;                       /* types left by the filter chain, before Truncate */
+    int32_t rejected[KP_N_FILTERS];          /* types each filter rejected */
+} kp_launch_result;
+
+/* Evaluates n requests on the ctx's device.  type_ids / override_offerings receive the concatenated lists
+ * (KP_E_BUFFER with results[*] offsets still valid up to the capacity when a buffer is too small). */
+kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_request* requests, int32_t max_instance_types,
+                           kp_launch_result* results, int32_t* type_ids, int32_t cap_type_ids,
+                           int32_t* override_offerings, int32_t cap_overrides);
+/* ms[0] = launch kernel (HIP events on the ctx stream), ms[1] = whole kp_launch_select call, of the last call. */
+kp_status kp_launch_stats(kp_ctx* ctx, double* ms, int32_t n);
+
+/*
  * Requirements of NodeClaim `nc` from the last kp_solve on this ctx (hostname removed as in
  * FinalizeScheduling), one line per key, lines sorted:
  *   "key \t complement(0|1) \t gt|- \t lt|- \t minValues|- \t v1 \x1f v2 ..."   (values sorted)

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <set>
 #include <memory>
 #include <string>
 #include <unordered_map>
@@ -19,6 +20,7 @@
 
 #include "../../include/kpsim.h"
 #include "kp_cons.h"
+#include "kp_launch.h"
 #include "kp_layout.h"
 
 size_t kp_ffd_shared_bytes();
@@ -29,6 +31,7 @@ hipError_t kp_launch_existing(const KpDev& d, hipStream_t s);
 hipError_t kp_launch_ffd(const KpDev& d, hipStream_t s);
 hipError_t kp_launch_finalize(const KpDev& d, int n_nodeclaims, hipStream_t s);
 bool kp_cons_plan_lds(const KpDev& d, KpCons& k, int max_bytes);
+hipError_t kp_launch_select_kernel(const KpLaunch& g, hipStream_t s);
 hipError_t kp_launch_consolidate(const KpDev& d, const KpCons& k, int n_workers, hipStream_t s);
 hipError_t kp_launch_cons_prep(const int32_t* queue0, int P, int32_t* rank, const int32_t* pending, int n_pending,
                                uint64_t* pend_bits, hipStream_t s);
@@ -246,6 +249,21 @@ struct kp_ctx {
     std::vector<int32_t> cons_off;           // candidate pod CSR offsets
     double cons_ms[3] = {};                  // device prep (sort, masks), probe kernel, whole call
     int64_t cons_stats[CS_COUNT] = {};
+    // launch selection (kp_launch_select): raw offering rows, incl. reserved offerings
+    bool has_reserved = false, launch_ok = true;
+    std::string launch_err;
+    std::vector<int32_t> l_off_begin, l_off_val, l_ct, l_rt, l_rcap;
+    std::vector<double> l_price;
+    std::vector<uint8_t> l_avail, l_exotic;
+    DBuf<int32_t> d_l_off_begin, d_l_off_val, d_l_ct, d_l_rt, d_l_rcap, d_l_hdr, d_l_types, d_l_over;
+    DBuf<double> d_l_price;
+    DBuf<uint8_t> d_l_avail, d_l_exotic;
+    DBuf<KlReq> d_l_req;
+    DBuf<KlKey> d_l_keys;
+    DBuf<KlMinKey> d_l_mins;
+    DBuf<uint64_t> d_l_words;
+    DBuf<int64_t> d_l_rq;
+    double launch_ms[2] = {};                // launch kernel, whole call
     // last results (host)
     int last_N = 0, M = 0;
     std::vector<int32_t> h_nc_tmpl;
@@ -338,6 +356,8 @@ static void rebuild_avail(kp_ctx* c, const std::vector<uint8_t>& avail) {
         if (c->off_slot[o] >= 0 && avail[o]) c->avail_zc[c->off_type[o]] |= 1ull << c->off_slot[o];
 }
 
+static kp_status upload_launch_tables(kp_ctx* c, const kp_catalog_view* v, const std::vector<uint8_t>& avail);
+
 extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, uint64_t epoch) try {
     if (!ctx || !v) return KP_E_INVALID;
     HIPCHK(hipSetDevice(ctx->device));
@@ -352,6 +372,7 @@ extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, ui
     c->resource_names.assign(v->resource_names, v->resource_names + R);
     c->type_names.assign(v->type_names, v->type_names + T);
     c->cat = Dicts();
+    c->has_reserved = false;
     // label keys (type requirements) then offering keys
     std::vector<int> lk(KL), ok(v->n_offering_keys);
     for (int k = 0; k < KL; k++) lk[k] = c->cat.key(normalize(v->label_keys[k]));
@@ -435,8 +456,12 @@ extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, ui
         lab(kri, sri);
         lab(krt, srt);
         if (sz != KP_LABEL_IN || sc != KP_LABEL_IN) return fail(ctx, KP_E_UNSUPPORTED, "offering without zone / capacity-type");
-        if (sri == KP_LABEL_IN || srt == KP_LABEL_IN)
-            return fail(ctx, KP_E_UNSUPPORTED, "reserved (capacity-reservation) offerings are not supported by this build");
+        if (sri == KP_LABEL_IN || srt == KP_LABEL_IN || !strcmp(ct, "reserved")) {
+            // reserved offerings (offering.go:164-194) feed kp_launch_select only; Solve / consolidation reject the catalog
+            c->has_reserved = true;
+            off_zone[o] = off_ct[o] = -1;
+            continue;
+        }
         if (sri == KP_LABEL_ABSENT || srt == KP_LABEL_ABSENT)
             return fail(ctx, KP_E_UNSUPPORTED, "od/spot offerings must carry reservation keys as DoesNotExist (offering.go:144-145)");
         const int zv = c->cat.keys[c->key_zone].id(z), cv = c->cat.keys[c->key_ct].id(ct);
@@ -468,6 +493,7 @@ extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, ui
         }
     c->slot_price.assign((size_t)T * KP_MAX_SLOTS, 1.7976931348623157e308);
     for (int o = 0; o < O; o++) {
+        if (off_zone[o] < 0) continue;
         const int s = off_zone[o] * NC + off_ct[o];
         c->off_slot[o] = s;
         c->slot_price[(size_t)c->off_type[o] * KP_MAX_SLOTS + s] = v->offering_price[o];
@@ -549,6 +575,10 @@ extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, ui
     HIPCHK(c->d_slot_zoneid.upload(c->slot_zoneid, s));
     HIPCHK(c->d_name_rank.upload(rank, s));
     HIPCHK(c->d_nonneg.upload(nonneg, s));
+    {
+        kp_status lst = upload_launch_tables(c, v, avail);
+        if (lst != KP_OK) return lst;
+    }
     HIPCHK(hipStreamSynchronize(s));
     c->epoch = epoch;
     c->have_catalog = true;
@@ -566,6 +596,8 @@ extern "C" kp_status kp_catalog_patch_avail(kp_ctx* ctx, const uint8_t* availabl
     HIPCHK(hipSetDevice(ctx->device));
     rebuild_avail(ctx, std::vector<uint8_t>(available, available + n));
     HIPCHK(ctx->d_avail_zc.upload(ctx->avail_zc, ctx->stream));
+    for (int o = 0; o < n; o++) ctx->l_avail[o] = available[o] ? 1 : 0;
+    HIPCHK(ctx->d_l_avail.upload(ctx->l_avail, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     ctx->epoch = epoch;
     return KP_OK;
@@ -578,9 +610,12 @@ extern "C" kp_status kp_catalog_patch_price(kp_ctx* ctx, const int32_t* idx, con
     HIPCHK(hipSetDevice(ctx->device));
     for (int i = 0; i < n; i++) {
         if (idx[i] < 0 || idx[i] >= (int)ctx->off_type.size()) return fail(ctx, KP_E_INVALID, "offering index");
-        ctx->slot_price[(size_t)ctx->off_type[idx[i]] * KP_MAX_SLOTS + ctx->off_slot[idx[i]]] = price[i];
+        if (ctx->off_slot[idx[i]] >= 0)
+            ctx->slot_price[(size_t)ctx->off_type[idx[i]] * KP_MAX_SLOTS + ctx->off_slot[idx[i]]] = price[i];
+        ctx->l_price[idx[i]] = price[i];
     }
     HIPCHK(ctx->d_slot_price.upload(ctx->slot_price, ctx->stream));
+    HIPCHK(ctx->d_l_price.upload(ctx->l_price, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     ctx->epoch = epoch;
     return KP_OK;
@@ -682,6 +717,8 @@ static bool tolerates(const kp_taint& taint, const kp_toleration* tols, int n) {
 extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try {
     if (!ctx || !in) return KP_E_INVALID;
     if (!ctx->have_catalog) return fail(ctx, KP_E_STATE, "kp_solve before kp_catalog_upload");
+    if (ctx->has_reserved)
+        return fail(ctx, KP_E_UNSUPPORTED, "Solve over a catalog with reserved offerings is not supported by this build");
     const auto t0 = clk::now();
     HIPCHK(hipSetDevice(ctx->device));
     kp_ctx* c = ctx;
@@ -1370,6 +1407,8 @@ extern "C" int32_t kp_consolidate_probe_count(const kp_consolidate_input* in) {
 extern "C" kp_status kp_consolidate_prepare(kp_ctx* ctx, const kp_consolidate_input* in) try {
     if (!ctx || !in) return KP_E_INVALID;
     ctx->cons_prepared = false;
+    if (ctx->has_reserved)
+        return fail(ctx, KP_E_UNSUPPORTED, "consolidation over a catalog with reserved offerings is not supported by this build");
     if (in->mode != KP_CONSOLIDATE_SINGLE && in->mode != KP_CONSOLIDATE_MULTI)
         return fail(ctx, KP_E_INVALID, "unknown consolidation mode");
     const kp_solve_input& cl = in->cluster;
@@ -1595,5 +1634,357 @@ extern "C" kp_status kp_consolidate_stats(kp_ctx* ctx, double* ms, int64_t* coun
         for (int i = 0; i < 3; i++) ms[i] = ctx->cons_ms[i];
     if (counters)
         for (int i = 0; i < n_counters && i < CS_COUNT; i++) counters[i] = ctx->cons_stats[i];
+    return KP_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// launch selection (kp_launch_select): filter.go chain + Truncate + getCapacityType + getOverrides' offering side
+// ---------------------------------------------------------------------------------------------
+static kp_status upload_launch_tables(kp_ctx* c, const kp_catalog_view* v, const std::vector<uint8_t>& avail) {
+    kp_ctx* ctx = c;  // HIPCHK reports through ctx
+    const int T = c->T, O = v->n_offerings, KO = v->n_offering_keys;
+    c->launch_ok = true;
+    c->launch_err.clear();
+    c->l_off_begin.assign(T + 1, 0);
+    for (int o = 0; o < O; o++) {
+        if (o > 0 && v->offering_type[o] < v->offering_type[o - 1])
+            return fail(c, KP_E_INVALID, "offering rows must be grouped by type (offering_type non-decreasing)");
+        c->l_off_begin[v->offering_type[o] + 1]++;
+    }
+    for (int t = 0; t < T; t++) {
+        if (c->l_off_begin[t + 1] > KL_MAX_OFF) {
+            c->launch_ok = false;
+            c->launch_err = "more than 64 offerings on one instance type";
+        }
+        c->l_off_begin[t + 1] += c->l_off_begin[t];
+    }
+    const int roles[KL_ROLES] = {c->key_zone, c->key_ct, c->key_zoneid, c->key_resvid, c->key_resvtype};
+    c->l_off_val.assign((size_t)KL_ROLES * O, KL_V_ABSENT);
+    c->l_ct.assign(O, KP_CT_ON_DEMAND);
+    c->l_rt.assign(O, -1);
+    c->l_rcap.assign(O, 0);
+    c->l_price.assign(O, 0.0);
+    c->l_avail = avail;
+    for (int o = 0; o < O; o++) {
+        c->l_price[o] = v->offering_price[o];
+        c->l_rcap[o] = v->offering_reservation_capacity ? v->offering_reservation_capacity[o] : 0;
+        for (int k = 0; k < KO; k++) {
+            const int key = c->cat.find_key(normalize(v->offering_keys[k]));
+            int r = -1;
+            for (int j = 0; j < KL_ROLES; j++)
+                if (roles[j] == key && key >= 0) r = j;
+            if (r < 0) continue;
+            const int st = v->offering_label_state[(size_t)o * KO + k];
+            int val = KL_V_ABSENT;
+            if (st == KP_LABEL_DOES_NOT_EXIST) val = KL_V_DNE;
+            else if (st == KP_LABEL_IN) val = c->cat.keys[key].id(v->offering_label_values[(size_t)o * KO + k]);
+            c->l_off_val[(size_t)r * O + o] = val;
+            if (st != KP_LABEL_IN) continue;
+            const char* s = v->offering_label_values[(size_t)o * KO + k];
+            if (r == KL_ROLE_CT) {
+                if (!strcmp(s, "on-demand")) c->l_ct[o] = KP_CT_ON_DEMAND;
+                else if (!strcmp(s, "spot")) c->l_ct[o] = KP_CT_SPOT;
+                else if (!strcmp(s, "reserved")) c->l_ct[o] = KP_CT_RESERVED;
+                else return fail(c, KP_E_INVALID, "unknown capacity type on an offering");
+            } else if (r == KL_ROLE_RESVTYPE) {
+                // v1.CapacityReservationType("").Values(); filter.go:148 panics on anything else
+                if (!strcmp(s, "default")) c->l_rt[o] = 0;
+                else if (!strcmp(s, "capacity-block")) c->l_rt[o] = 1;
+                else return fail(c, KP_E_INVALID, "unknown capacity-reservation-type on an offering");
+            }
+        }
+    }
+    // ExoticInstanceTypeFilter's per-type test (filter.go:294-312): a "metal" size, or accelerator capacity
+    c->l_exotic.assign(T, 0);
+    const int ksize = c->cat.find_key("karpenter.k8s.aws/instance-size");
+    const char* accel[] = {"aws.amazon.com/neuron", "aws.amazon.com/neuroncore", "amd.com/gpu", "nvidia.com/gpu",
+                           "habana.ai/gaudi"};
+    const int KL = v->n_label_keys;
+    for (int t = 0; t < T; t++) {
+        bool ex = false;
+        for (int k = 0; k < KL && !ex; k++) {
+            if (ksize < 0 || c->cat.find_key(normalize(v->label_keys[k])) != ksize) continue;
+            if (v->label_state[(size_t)t * KL + k] != KP_LABEL_IN) continue;
+            for (int i = v->label_offsets[(size_t)t * KL + k]; i < v->label_offsets[(size_t)t * KL + k + 1]; i++)
+                if (strstr(v->label_values[i], "metal")) ex = true;
+        }
+        for (int r = 0; r < c->R && !ex; r++)
+            for (auto* a : accel)
+                if (c->resource_names[r] == a && v->capacity[(size_t)t * c->R + r] != 0) ex = true;
+        c->l_exotic[t] = ex;
+    }
+    hipStream_t s = c->stream;
+    HIPCHK(c->d_l_off_begin.upload(c->l_off_begin, s));
+    HIPCHK(c->d_l_off_val.upload(c->l_off_val, s));
+    HIPCHK(c->d_l_ct.upload(c->l_ct, s));
+    HIPCHK(c->d_l_rt.upload(c->l_rt, s));
+    HIPCHK(c->d_l_rcap.upload(c->l_rcap, s));
+    HIPCHK(c->d_l_price.upload(c->l_price, s));
+    HIPCHK(c->d_l_avail.upload(c->l_avail, s));
+    HIPCHK(c->d_l_exotic.upload(c->l_exotic, s));
+    return KP_OK;
+}
+
+namespace {
+// scheduling.Requirement in string space (requirement.go: NewRequirementWithFlexibility, Intersection, Has, Operator)
+struct SReq {
+    bool complement = false;
+    std::set<std::string> vals;
+    bool has_gt = false, has_lt = false;
+    int64_t gt = 0, lt = 0;
+    bool has_min = false;
+    int minv = 0;
+    bool within(const std::string& v) const {
+        if (!has_gt && !has_lt) return true;
+        int64_t x = 0;
+        if (!go_atoi(v.c_str(), x)) return false;
+        if (has_gt && gt >= x) return false;
+        if (has_lt && lt <= x) return false;
+        return true;
+    }
+    bool has(const std::string& v) const { return (complement ? !vals.count(v) : vals.count(v) > 0) && within(v); }
+    int op() const {  // 0 In, 1 NotIn, 2 Exists, 3 DoesNotExist
+        if (complement) return vals.empty() ? 2 : 1;
+        return vals.empty() ? 3 : 0;
+    }
+};
+SReq sreq_new(const kp_requirement& r) {
+    SReq q;
+    q.complement = !(r.op == KP_OP_IN || r.op == KP_OP_DOES_NOT_EXIST);
+    if (r.op == KP_OP_IN || r.op == KP_OP_NOT_IN)
+        for (int j = 0; j < r.n_values; j++) q.vals.insert(r.values[j] ? r.values[j] : "");
+    if (r.op == KP_OP_GT || r.op == KP_OP_LT) {
+        int64_t x = 0;
+        go_atoi(r.n_values > 0 && r.values[0] ? r.values[0] : "", x);
+        (r.op == KP_OP_GT ? q.has_gt : q.has_lt) = true;
+        (r.op == KP_OP_GT ? q.gt : q.lt) = x;
+    }
+    q.has_min = r.min_values >= 0;
+    q.minv = r.min_values;
+    return q;
+}
+SReq sreq_intersection(const SReq& a, const SReq& b) {
+    SReq o;
+    o.complement = a.complement && b.complement;
+    o.has_gt = a.has_gt || b.has_gt;
+    o.gt = (a.has_gt && b.has_gt) ? std::max(a.gt, b.gt) : (a.has_gt ? a.gt : b.gt);
+    o.has_lt = a.has_lt || b.has_lt;
+    o.lt = (a.has_lt && b.has_lt) ? std::min(a.lt, b.lt) : (a.has_lt ? a.lt : b.lt);
+    o.has_min = a.has_min || b.has_min;
+    o.minv = (a.has_min && b.has_min) ? std::max(a.minv, b.minv) : (a.has_min ? a.minv : b.minv);
+    if (o.has_gt && o.has_lt && o.gt >= o.lt) {
+        SReq d;
+        d.has_min = o.has_min;
+        d.minv = o.minv;
+        return d;
+    }
+    std::set<std::string> vs;
+    if (a.complement && b.complement) {
+        vs = a.vals;
+        vs.insert(b.vals.begin(), b.vals.end());
+    } else if (a.complement) {
+        for (auto& x : b.vals)
+            if (!a.vals.count(x)) vs.insert(x);
+    } else if (b.complement) {
+        for (auto& x : a.vals)
+            if (!b.vals.count(x)) vs.insert(x);
+    } else {
+        for (auto& x : a.vals)
+            if (b.vals.count(x)) vs.insert(x);
+    }
+    for (auto& x : vs)
+        if (o.within(x)) o.vals.insert(x);
+    if (!o.complement) o.has_gt = o.has_lt = false;
+    return o;
+}
+}  // namespace
+
+extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_request* requests,
+                                      int32_t max_instance_types, kp_launch_result* results, int32_t* type_ids,
+                                      int32_t cap_type_ids, int32_t* override_offerings, int32_t cap_overrides) try {
+    if (!ctx || n < 0 || (n > 0 && (!requests || !results))) return KP_E_INVALID;
+    if (!ctx->have_catalog) return fail(ctx, KP_E_STATE, "kp_launch_select before kp_catalog_upload");
+    if (!ctx->launch_ok) return fail(ctx, KP_E_UNSUPPORTED, ctx->launch_err);
+    const int M = max_instance_types;
+    if (M < 1 || M > 64) return fail(ctx, KP_E_UNSUPPORTED, "max_instance_types must be in 1..64 (instance.go:62 uses 60)");
+    const auto t0 = clk::now();
+    HIPCHK(hipSetDevice(ctx->device));
+    kp_ctx* c = ctx;
+    const int T = c->T, R = c->R, Kc = c->Kcat;
+    std::vector<KlReq> reqs(n);
+    std::vector<KlKey> keys;
+    std::vector<KlMinKey> mins;
+    std::vector<uint64_t> words;
+    std::vector<int64_t> rq((size_t)std::max(1, n) * R, 0);
+    const int roles[KL_ROLES] = {c->key_zone, c->key_ct, c->key_zoneid, c->key_resvid, c->key_resvtype};
+    for (int i = 0; i < n; i++) {
+        const kp_launch_request& lr = requests[i];
+        if (lr.n_requirements < 0 || (lr.n_requirements > 0 && !lr.requirements)) return fail(c, KP_E_INVALID, "bad request");
+        std::map<std::string, SReq> m;  // NewNodeSelectorRequirementsWithMinValues: Add = intersect per key
+        for (int j = 0; j < lr.n_requirements; j++) {
+            const kp_requirement& r = lr.requirements[j];
+            if (!r.key || r.op < 0 || r.op > 5) return fail(c, KP_E_INVALID, "bad requirement");
+            const std::string key = normalize(r.key);
+            SReq q = sreq_new(r);
+            auto it = m.find(key);
+            if (it == m.end()) m.emplace(key, q);
+            else it->second = sreq_intersection(q, it->second);
+        }
+        if (lr.requests)
+            for (int r = 0; r < R; r++) rq[(size_t)i * R + r] = lr.requests[r];
+        KlReq& q = reqs[i];
+        q = KlReq{};
+        q.key_off = (int)keys.size();
+        std::map<int, int> woff_of;  // catalog key → word offset of its value bitset
+        for (auto& kv : m) {
+            const int kc = c->cat.find_key(kv.first);
+            if (kc < 0) continue;  // no type or offering carries the key: absent on both sides, never constrains
+            const auto& vals = c->cat.keys[kc].vals;
+            const int woff = (int)words.size();
+            words.resize(words.size() + std::max<size_t>(1, (vals.size() + 63) / 64), 0ull);
+            for (size_t vv = 0; vv < vals.size(); vv++)
+                if (kv.second.has(vals[vv])) words[woff + vv / 64] |= 1ull << (vv % 64);
+            woff_of[kc] = woff;
+            const int op = kv.second.op();
+            KlKey kk{kc, c->cat_multi[kc], 0u, woff};
+            kk.flags = (c->cat_kflags[kc] & KF_CAT_MULTI) ? KLK_MULTI : KLK_SINGLE;
+            if (op == 1 || op == 3) kk.flags |= KLK_DNE_OK;
+            if (c->cat_kflags[kc] != 0) keys.push_back(kk);
+        }
+        q.n_keys = (int)keys.size() - q.key_off;
+        q.und_off = (int)keys.size();
+        for (int kc = 0; kc < Kc; kc++) {
+            if (c->cat_kflags[kc] == 0 || woff_of.count(kc) || well_known(c->cat.keys[kc].name)) continue;
+            KlKey kk{kc, c->cat_multi[kc], (c->cat_kflags[kc] & KF_CAT_MULTI) ? KLK_MULTI : KLK_SINGLE, 0};
+            keys.push_back(kk);
+        }
+        q.n_und = (int)keys.size() - q.und_off;
+        for (int r = 0; r < KL_ROLES; r++) {
+            const int kc = roles[r];
+            KlRole& ro = q.role[r];
+            ro = KlRole{KLR_PASS, 0u, 0, 0};
+            if (kc < 0) continue;
+            auto it = woff_of.find(kc);
+            if (it != woff_of.end()) {
+                ro.mode = KLR_CONSTRAINED;
+                ro.woff = it->second;
+                const int op = m[c->cat.keys[kc].name].op();
+                if (op == 1 || op == 3) ro.flags = KLK_DNE_OK;
+            } else if (!well_known(c->cat.keys[kc].name)) {
+                ro.mode = KLR_FAIL_IN;
+            }
+        }
+        auto ct = m.find("karpenter.sh/capacity-type");
+        const char* cts[3] = {"on-demand", "spot", "reserved"};
+        for (int x = 0; x < 3; x++) q.ct_has[x] = ct == m.end() ? 1 : (ct->second.has(cts[x]) ? 1 : 0);
+        q.min_off = (int)mins.size();
+        for (auto& kv : m) {
+            if (!kv.second.has_min) continue;
+            q.has_min = 1;
+            const int kc = c->cat.find_key(kv.first);
+            KlMinKey mk{-1, -1, 0, kv.second.minv};
+            if (kc >= 0 && c->cat_kflags[kc] != 0) {
+                mk.k = kc;
+                mk.mi = (c->cat_kflags[kc] & KF_CAT_MULTI) ? c->cat_multi[kc] : -1;
+                mk.nvals = (int)c->cat.keys[kc].vals.size();
+                if (mk.nvals > KP_MAX_MIN_WORDS * 64) return fail(c, KP_E_UNSUPPORTED, "minValues key with > 4096 values");
+            } else {
+                mk.k = 0;  // no type carries the key: zero distinct values
+                mk.mi = -1;
+                mk.nvals = 0;
+                if (mk.minv > 0) mk.minv = INT32_MAX;
+            }
+            mins.push_back(mk);
+        }
+        q.n_min = (int)mins.size() - q.min_off;
+    }
+    hipStream_t s = c->stream;
+    if (n > 0) {
+        HIPCHK(c->d_l_req.upload(reqs, s));
+        HIPCHK(c->d_l_keys.upload(keys.empty() ? std::vector<KlKey>(1) : keys, s));
+        HIPCHK(c->d_l_mins.upload(mins.empty() ? std::vector<KlMinKey>(1) : mins, s));
+        HIPCHK(c->d_l_words.upload(words.empty() ? std::vector<uint64_t>(1) : words, s));
+        HIPCHK(c->d_l_rq.upload(rq, s));
+        HIPCHK(c->d_l_hdr.ensure((size_t)n * KL_HDR));
+        HIPCHK(c->d_l_types.ensure((size_t)n * M));
+        HIPCHK(c->d_l_over.ensure((size_t)n * M * KL_MAX_OFF));
+    }
+    KpLaunch g{};
+    g.T = T;
+    g.TW = c->TW;
+    g.R = R;
+    g.M = M;
+    g.type_val = c->d_type_val.p;
+    g.multi_mask = c->d_multi_mask.p;
+    g.dne_mask = c->d_dne_mask.p;
+    g.alloc = c->d_alloc.p;
+    g.name_rank = c->d_name_rank.p;
+    g.exotic = c->d_l_exotic.p;
+    g.off_begin = c->d_l_off_begin.p;
+    g.off_val = c->d_l_off_val.p;
+    g.ct_code = c->d_l_ct.p;
+    g.rt_code = c->d_l_rt.p;
+    g.off_price = c->d_l_price.p;
+    g.off_avail = c->d_l_avail.p;
+    g.off_rcap = c->d_l_rcap.p;
+    g.L = n;
+    g.req = c->d_l_req.p;
+    g.keys = c->d_l_keys.p;
+    g.mins = c->d_l_mins.p;
+    g.words = c->d_l_words.p;
+    g.requests = c->d_l_rq.p;
+    g.out_hdr = c->d_l_hdr.p;
+    g.out_types = c->d_l_types.p;
+    g.out_over = c->d_l_over.p;
+    HIPCHK(hipEventRecord(c->ev[0], s));
+    HIPCHK(kp_launch_select_kernel(g, s));
+    HIPCHK(hipEventRecord(c->ev[1], s));
+    std::vector<int32_t> hdr((size_t)n * KL_HDR), tys((size_t)n * M), ov((size_t)n * M * KL_MAX_OFF);
+    if (n > 0) {
+        HIPCHK(hipMemcpyAsync(hdr.data(), c->d_l_hdr.p, hdr.size() * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(tys.data(), c->d_l_types.p, tys.size() * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(ov.data(), c->d_l_over.p, ov.size() * 4, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    float kms = 0.f;
+    HIPCHK(hipEventElapsedTime(&kms, c->ev[0], c->ev[1]));
+    c->launch_ms[0] = kms;
+    int tpos = 0, opos = 0;
+    bool short_buf = false;
+    for (int i = 0; i < n; i++) {
+        const int32_t* h = &hdr[(size_t)i * KL_HDR];
+        kp_launch_result& r = results[i];
+        r.status = h[0];
+        r.failed_filter = h[1];
+        r.capacity_type = h[2];
+        r.n_types = h[3];
+        r.n_options = h[5];
+        for (int f = 0; f < KP_N_FILTERS; f++) r.rejected[f] = h[8 + f];
+        r.type_offset = tpos;
+        r.override_offset = opos;
+        r.n_overrides = 0;
+        for (int k = 0; k < r.n_types; k++) {
+            if (type_ids && tpos < cap_type_ids) type_ids[tpos] = tys[(size_t)i * M + k];
+            else short_buf = true;
+            tpos++;
+            const int32_t* ol = &ov[((size_t)i * M + k) * KL_MAX_OFF];
+            for (int j = 0; j < KL_MAX_OFF && ol[j] >= 0; j++) {
+                if (override_offerings && opos < cap_overrides) override_offerings[opos] = ol[j];
+                else short_buf = true;
+                opos++;
+                r.n_overrides++;
+            }
+        }
+    }
+    c->launch_ms[1] = ns_since(t0) / 1e6;
+    if (short_buf) return fail(c, KP_E_BUFFER, "type_ids / override_offerings too small");
+    return KP_OK;
+} catch (const std::exception& e) {
+    return fail(ctx, KP_E_INVALID, e.what());
+}
+
+extern "C" kp_status kp_launch_stats(kp_ctx* ctx, double* ms, int32_t n) {
+    if (!ctx || !ms) return KP_E_INVALID;
+    for (int i = 0; i < n && i < 2; i++) ms[i] = ctx->launch_ms[i];
     return KP_OK;
 }

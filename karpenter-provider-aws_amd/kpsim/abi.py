@@ -133,6 +133,30 @@ PROBE_DTYPE = np.dtype([("decision", np.int32), ("valid", np.int32), ("all_sched
 assert PROBE_DTYPE.itemsize == C.sizeof(kp_probe_result)
 
 
+KP_FILTER_NAMES = ["compatible-available-filter", "capacity-reservation-type-filter", "capacity-block-filter",
+                   "reserved-offering-filter", "exotic-instance-filter", "spot-instance-filter"]  # filter.go Name()
+KP_N_FILTERS = 6
+(KP_FILTER_COMPATIBLE_AVAILABLE, KP_FILTER_CAPACITY_RESERVATION_TYPE, KP_FILTER_CAPACITY_BLOCK,
+ KP_FILTER_RESERVED_OFFERING, KP_FILTER_EXOTIC, KP_FILTER_SPOT) = range(6)
+
+
+class kp_launch_request(C.Structure):
+    _fields_ = [("n_requirements", C.c_int32), ("requirements", C.POINTER(kp_requirement)),
+                ("requests", C.POINTER(C.c_int64))]
+
+
+class kp_launch_result(C.Structure):
+    _fields_ = [("status", C.c_int32), ("failed_filter", C.c_int32), ("capacity_type", C.c_int32),
+                ("n_types", C.c_int32), ("type_offset", C.c_int32), ("n_overrides", C.c_int32),
+                ("override_offset", C.c_int32), ("n_options", C.c_int32), ("rejected", C.c_int32 * KP_N_FILTERS)]
+
+
+LAUNCH_DTYPE = np.dtype([("status", np.int32), ("failed_filter", np.int32), ("capacity_type", np.int32),
+                         ("n_types", np.int32), ("type_offset", np.int32), ("n_overrides", np.int32),
+                         ("override_offset", np.int32), ("n_options", np.int32), ("rejected", np.int32, KP_N_FILTERS)])
+assert LAUNCH_DTYPE.itemsize == C.sizeof(kp_launch_result)
+
+
 class kp_device_opts(C.Structure):
     _fields_ = [("device", C.c_int32), ("reserved0", C.c_int32)]
 

@@ -415,3 +415,58 @@ class ConsolidateInputView:
         v.probe_begin = int(probe_begin)
         v.probe_end = int(probe_end)
         v.spot_to_spot = 1 if spot_to_spot else 0
+
+
+@dataclass
+class LaunchRequest:
+    """A NodeClaim as CloudProvider.Create sees it (pkg/providers/instance/instance.go:132): Spec.Requirements (with
+    minValues) and Spec.Resources.Requests (milli, RESOURCES order; 0 = not requested)."""
+    requirements: List[Requirement]
+    requests: np.ndarray
+
+
+class LaunchBatchView:
+    """kp_launch_request[n] (buffers owned by self.keep)."""
+
+    def __init__(self, reqs: List[LaunchRequest]):
+        k = self.keep = abi.Keep()
+        self.n = len(reqs)
+        arr = (abi.kp_launch_request * max(1, self.n))()
+        for i, lr in enumerate(reqs):
+            nr, ra = abi.requirement_array(k, lr.requirements)
+            arr[i].n_requirements = nr
+            arr[i].requirements = ra
+            arr[i].requests = k.ptr(np.asarray(lr.requests, np.int64), np.int64, C.c_int64)
+        k.hold(arr)
+        self.array = arr
+
+
+@dataclass
+class LaunchResults:
+    """Per request: LAUNCH_DTYPE rows, plus the concatenated type ids and override offering rows."""
+    rows: np.ndarray
+    type_ids: np.ndarray
+    overrides: np.ndarray
+
+    def types(self, i):
+        r = self.rows[i]
+        return self.type_ids[r["type_offset"]:r["type_offset"] + r["n_types"]]
+
+    def offerings(self, i):
+        r = self.rows[i]
+        return self.overrides[r["override_offset"]:r["override_offset"] + r["n_overrides"]]
+
+
+def launch_buffers(n, M, catalog_view):
+    rows = np.zeros(max(1, n), abi.LAUNCH_DTYPE)
+    tids = np.zeros(max(1, n * M), np.int32)
+    ovs = np.zeros(max(1, n * M * 64), np.int32)
+    return rows, tids, ovs
+
+
+def launch_call(fn, cv, batch: LaunchBatchView, M):
+    """Runs fn(n, requests, M, results, type_ids, cap, overrides, cap) (kp_launch_select or its oracle)."""
+    rows, tids, ovs = launch_buffers(batch.n, M, cv)
+    st = fn(batch.n, batch.array, M, rows.ctypes.data_as(C.POINTER(abi.kp_launch_result)),
+            tids.ctypes.data_as(C.POINTER(C.c_int32)), len(tids), ovs.ctypes.data_as(C.POINTER(C.c_int32)), len(ovs))
+    return st, LaunchResults(rows[:batch.n], tids, ovs)

@@ -11,7 +11,7 @@ EXPORTS = [
     "kp_ctx_create", "kp_ctx_destroy", "kp_last_error", "kp_version", "kp_catalog_upload", "kp_catalog_patch_avail",
     "kp_catalog_patch_price", "kp_solve", "kp_solve_prepare", "kp_solve_execute", "kp_solve_fetch",
     "kp_result_nodeclaim_requirements", "kp_last_kernel_times", "kp_consolidate_probe_count", "kp_consolidate",
-    "kp_consolidate_stats", "kp_consolidate_prepare", "kp_consolidate_execute",
+    "kp_consolidate_stats", "kp_consolidate_prepare", "kp_consolidate_execute", "kp_launch_select", "kp_launch_stats",
 ]
 
 _lib = None
@@ -53,6 +53,10 @@ def load():
     L.kp_consolidate_execute.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(abi.kp_probe_result),
                                          C.c_int32]
     L.kp_consolidate_stats.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.c_int32]
+    L.kp_launch_select.argtypes = [C.c_void_p, C.c_int32, C.POINTER(abi.kp_launch_request), C.c_int32,
+                                   C.POINTER(abi.kp_launch_result), C.POINTER(C.c_int32), C.c_int32,
+                                   C.POINTER(C.c_int32), C.c_int32]
+    L.kp_launch_stats.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_int32]
     for f in EXPORTS:
         if f not in ("kp_last_error", "kp_version"):
             getattr(L, f).restype = C.c_int32
@@ -95,6 +99,18 @@ class Context:
         self.check(self.L.kp_catalog_patch_price(self.h, i.ctypes.data_as(C.POINTER(C.c_int32)),
                                                  p.ctypes.data_as(C.POINTER(C.c_double)), len(i), epoch),
                    "kp_catalog_patch_price")
+
+    def launch_select(self, batch, M=60):
+        """kp_launch_select over a model.LaunchBatchView → model.LaunchResults (instance.go:132-137 per request)."""
+        from kpsim import model
+        st, res = model.launch_call(lambda *a: self.L.kp_launch_select(self.h, *a), self._catalog, batch, M)
+        self.check(st, "kp_launch_select")
+        return res
+
+    def launch_stats(self):
+        ms = (C.c_double * 2)()
+        self.check(self.L.kp_launch_stats(self.h, ms, 2), "kp_launch_stats")
+        return list(ms)
 
     def prepare(self, input_view):
         self.check(self.L.kp_solve_prepare(self.h, C.byref(input_view.view)), "kp_solve_prepare")

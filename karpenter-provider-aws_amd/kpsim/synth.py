@@ -9,7 +9,7 @@ from typing import Dict, List, Optional
 import numpy as np
 
 from .catalog import golden_catalog, parse_quantity_milli
-from . import abi
+from . import abi, model
 from .model import (ARCH, CAPACITY_TYPE, NODEPOOL, R, RIDX, ZONE, Candidate, ConsolidationProblem, ExistingNode,
                     NodePool, PodClass, Pods, Problem, Requirement, Taint, Toleration)
 
@@ -283,3 +283,74 @@ def config4(n_nodes=5000, pods_per_node=(10, 30), n_classes=250, catalog=None, s
                        capacity_type=abi.KP_CT_SPOT if m[4] == "spot" else abi.KP_CT_ON_DEMAND, instance_type=m[5],
                        nodepool=m[6], capacity=m[7]) for m in cand_meta]
     return ConsolidationProblem(prob, cands, np.nonzero(owner < 0)[0].astype(np.int32), np.ones(n_nodes, np.uint8))
+
+
+def config5_catalog(catalog, n_default=40, n_block=20, seed=SEED, expiring_frac=0.10):
+    """BASELINE configs[4]'s catalog: the golden catalog plus reserved offerings (offering.go:164-194) for 60 types —
+    40 ODCR-default and 20 capacity-block, ReservationCapacity in [1, 20], price = odPrice / 1e7 (offering.go:176),
+    10% of reservations expiring (Available = false, offering.go:187).  Returns a new catalog list (types copied)."""
+    import copy
+    rng = np.random.Generator(np.random.PCG64(seed + 5))
+    cat = copy.deepcopy(catalog)
+    idx = rng.choice(len(cat), size=n_default + n_block, replace=False)
+    for j, t in enumerate(idx):
+        it = cat[int(t)]
+        od = [o for o in it.offerings if o.capacity_type == "on-demand"]
+        if not od:
+            continue
+        z = od[int(rng.integers(len(od)))]
+        rcap = int(rng.integers(1, 21))
+        expiring = rng.random() < expiring_frac
+        it.offerings.append(model.Offering(
+            capacity_type="reserved", zone=z.zone, price=z.price / 10_000_000.0, available=not expiring,
+            zone_id=z.zone_id, reservation_id="cr-%05d" % j,
+            reservation_type="default" if j < n_default else "capacity-block", reservation_capacity=rcap))
+    return cat
+
+
+def launch_requests(catalog, n=1000, seed=SEED, with_min_values=True):
+    """Seeded NodeClaims for kp_launch_select: requirement mixes a Solve produces (NodePool capacity types, zones,
+    arch, categories, instance-type In [≤ 60 names], occasional minValues) and request totals."""
+    rng = np.random.Generator(np.random.PCG64(seed + 6))
+    names = [it.name for it in catalog]
+    fams = sorted({it.labels.get("karpenter.k8s.aws/instance-family", [None])[0] or "" for it in catalog} - {""})
+    ct_sets = [["on-demand"], ["spot"], ["spot", "on-demand"], ["reserved"], ["reserved", "on-demand"],
+               ["reserved", "spot", "on-demand"], None]
+    out = []
+    R = len(model.RESOURCES)
+    for i in range(n):
+        reqs = []
+        cts = ct_sets[int(rng.integers(len(ct_sets)))]
+        if cts is not None:
+            reqs.append(model.Requirement(model.CAPACITY_TYPE, "In", list(cts)))
+        u = rng.random()
+        if u < 0.6:
+            k = int(rng.integers(5, 120))
+            reqs.append(model.Requirement(model.INSTANCE_TYPE, "In",
+                                          [names[int(x)] for x in rng.choice(len(names), size=k, replace=False)]))
+        elif u < 0.8:
+            reqs.append(model.Requirement("karpenter.k8s.aws/instance-family", "In",
+                                          [fams[int(x)] for x in rng.choice(len(fams), size=int(rng.integers(1, 12)),
+                                                                            replace=False)]))
+        if rng.random() < 0.3:
+            reqs.append(model.Requirement(model.ZONE, "In", ["test-zone-1%s" % c for c in
+                                                             rng.choice(list("abc"), size=int(rng.integers(1, 3)),
+                                                                        replace=False)]))
+        if rng.random() < 0.3:
+            reqs.append(model.Requirement(model.ARCH, "In", [["amd64", "arm64"][int(rng.integers(2))]]))
+        if rng.random() < 0.2:
+            reqs.append(model.Requirement("karpenter.k8s.aws/instance-category", "NotIn", ["g", "p", "inf", "trn"]))
+        if rng.random() < 0.15:
+            reqs.append(model.Requirement("karpenter.k8s.aws/instance-generation", "Gt", [str(int(rng.integers(2, 7)))]))
+        if with_min_values and rng.random() < 0.1:
+            reqs.append(model.Requirement("karpenter.k8s.aws/instance-family", "Exists", [],
+                                          min_values=int(rng.integers(1, 40))))
+        rq = np.zeros(R, np.int64)
+        cpu = int(rng.choice([250, 500, 1000, 2000, 4000, 8000, 16000, 64000]))
+        rq[0] = cpu
+        rq[1] = cpu * int(rng.choice([1, 2, 4, 8])) * (1 << 30)  # cpu cores x GiB/core, milli-bytes
+        rq[3] = int(rng.integers(1, 40)) * 1000
+        if rng.random() < 0.03:
+            rq[5] = int(rng.choice([1, 2, 4, 8])) * 1000
+        out.append(model.LaunchRequest(reqs, rq))
+    return out

@@ -24,6 +24,12 @@ int32_t orc_consolidate_probe_count(const kp_consolidate_input* in);
 kp_status orc_consolidate(const kp_catalog_view* cat, const kp_consolidate_input* in, kp_probe_result* results,
                           int32_t cap_results, int32_t n_threads);
 
+/* Launch-time selection (filter.go chain + Truncate + getCapacityType + getOverrides' offering side), same
+ * contract as kp_launch_select. */
+kp_status orc_launch_select(const kp_catalog_view* cat, int32_t n, const kp_launch_request* requests, int32_t M,
+                            kp_launch_result* results, int32_t* type_ids, int32_t cap_type_ids,
+                            int32_t* override_offerings, int32_t cap_overrides);
+
 /* pkg/providers/instancetype/types.go:123-155,320-605 — capacity / overhead / allocatable arithmetic.
  * Resource axes (milli-units), fixed order ORC_R_*. */
 enum {

@@ -39,6 +39,10 @@ def lib():
         _lib.orc_consolidate.argtypes = [C.POINTER(abi.kp_catalog_view), C.POINTER(abi.kp_consolidate_input),
                                          C.POINTER(abi.kp_probe_result), C.c_int32, C.c_int32]
         _lib.orc_consolidate.restype = C.c_int32
+        _lib.orc_launch_select.argtypes = [C.POINTER(abi.kp_catalog_view), C.c_int32, C.POINTER(abi.kp_launch_request),
+                                           C.c_int32, C.POINTER(abi.kp_launch_result), C.POINTER(C.c_int32), C.c_int32,
+                                           C.POINTER(C.c_int32), C.c_int32]
+        _lib.orc_launch_select.restype = C.c_int32
         _lib.orc_go_sort_slice_ints.argtypes = [C.POINTER(C.c_int64), C.POINTER(C.c_int32), C.c_int32]
     return _lib
 
@@ -150,3 +154,10 @@ def consolidate(cp, mode, probe_begin=0, probe_end=0, spot_to_spot=False, max_ca
     if st != 0:
         raise RuntimeError("orc_consolidate failed: %d" % st)
     return out[:max(0, b1 - b0)]
+
+
+def launch_select(catalog_view, batch, M=60):
+    """orc_launch_select over a kpsim.model.LaunchBatchView → (status, model.LaunchResults)."""
+    from kpsim import model
+    L = lib()
+    return model.launch_call(lambda *a: L.orc_launch_select(C.byref(catalog_view.view), *a), catalog_view, batch, M)

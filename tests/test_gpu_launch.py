@@ -1,0 +1,86 @@
+"""GPU parity of kp_launch_select (launch-time filter chain + Truncate + getCapacityType + overrides) against the
+oracle: the ported filter_test.go cases, a seeded config-5 batch over the golden catalog with reserved offerings, and
+ICE / price deltas applied through kp_catalog_patch_*."""
+import numpy as np
+import pytest
+
+import launch_cases as LC
+import pyoracle
+from kpsim import abi, model, native, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = native.Context(0)
+    yield c
+    c.close()
+
+
+def _both(ctx, cat, reqs, M=60):
+    cv = model.CatalogView(cat)
+    ctx.upload_catalog(cv)
+    b = model.LaunchBatchView(reqs)
+    dev = ctx.launch_select(b, M)
+    st, orc = pyoracle.launch_select(cv, b, M)
+    assert st == abi.KP_OK
+    return dev, orc
+
+
+@pytest.mark.parametrize("mk", LC.CASES, ids=[getattr(c, "__name__", "case%d" % i) for i, c in enumerate(LC.CASES)])
+def test_filter_cases(ctx, mk):
+    cat, reqs, expect = mk()
+    dev, orc = _both(ctx, cat, reqs)
+    LC.check(cat, dev, expect)
+    LC.assert_same(dev, orc)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_config5_batch_parity(ctx, golden, seed):
+    cat = synth.config5_catalog(golden, seed=synth.SEED + seed)
+    reqs = synth.launch_requests(cat, n=600, seed=synth.SEED + seed)
+    dev, orc = _both(ctx, cat, reqs)
+    LC.assert_same(dev, orc)
+    assert (dev.rows["capacity_type"] == abi.KP_CT_RESERVED).sum() > 0
+    assert (dev.rows["status"] == abi.KP_E_INSUFFICIENT_CAPACITY).sum() > 0
+
+
+def test_patches_reach_launch(ctx, golden):
+    """ICE marks and price refreshes (kp_catalog_patch_avail / _price) change the launch result like a re-List."""
+    cat = synth.config5_catalog(golden)
+    cv = model.CatalogView(cat)
+    ctx.upload_catalog(cv)
+    reqs = synth.launch_requests(cat, n=200, seed=7)
+    b = model.LaunchBatchView(reqs)
+    rng = np.random.Generator(np.random.PCG64(3))
+    avail = np.array([o.available for it in cat for o in it.offerings], np.uint8)
+    avail[rng.random(len(avail)) < 0.3] = 0
+    ctx.patch_avail(avail, 2)
+    idx = rng.choice(len(avail), size=500, replace=False).astype(np.int32)
+    price = rng.random(500) * 3
+    ctx.patch_price(idx, price, 3)
+    dev = ctx.launch_select(b, 60)
+    flat = [o for it in cat for o in it.offerings]
+    for j, o in enumerate(flat):
+        o.available = bool(avail[j])
+    for i, p in zip(idx, price):
+        flat[int(i)].price = float(p)
+    st, orc = pyoracle.launch_select(model.CatalogView(cat), b, 60)
+    assert st == abi.KP_OK
+    LC.assert_same(dev, orc)
+
+
+def test_solve_rejects_reserved_catalog(ctx, golden):
+    cat = synth.config5_catalog(golden)
+    ctx.upload_catalog(model.CatalogView(cat))
+    prob = synth.config2(n_pods=200, catalog=cat)
+    with pytest.raises(native.KpError) as e:
+        ctx.prepare(model.SolveInputView(prob))
+    assert e.value.status == abi.KP_E_UNSUPPORTED
+
+
+def test_empty_batch(ctx, golden):
+    ctx.upload_catalog(model.CatalogView(golden))
+    res = ctx.launch_select(model.LaunchBatchView([]), 60)
+    assert len(res.rows) == 0
