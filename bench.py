@@ -130,6 +130,88 @@ def consolidation_leg(a, cat, local, rank, world, dist, barrier):
     return out
 
 
+def launch_bytes(T, R=12, K=32, O=6):
+    """SURVEY §8d S_type = 8R + 2K + 16·O per instance type; one launch request sweeps every type of the catalog."""
+    return T * (8 * R + 2 * K + 16 * O)
+
+
+def launch_leg(a, golden, local, rank, world, dist, barrier):
+    """BASELINE configs[4] launch side: CloudProvider.Create's instance-type selection (filter.go chain, Truncate(60),
+    getCapacityType, override offerings) for a batch of NodeClaims over the catalog with 60 reserved types (40 ODCR
+    default + 20 capacity-block, 10% expiring).  200k pods at ~20 pods/node → a 10k-NodeClaim batch.  Requests are
+    independent, so ranks take contiguous slices of one fixed batch (strong scaling, no data-path collective)."""
+    from kpsim import abi, model, native, synth
+    import launch_cases as LC
+    cat = synth.config5_catalog(golden)
+    reqs_all = synth.launch_requests(cat, n=a.launch_batch)
+    b0 = a.launch_batch * rank // world
+    b1 = a.launch_batch * (rank + 1) // world
+    batch = model.LaunchBatchView(reqs_all[b0:b1])
+    ctx = native.Context(local)
+    cv = model.CatalogView(cat)
+    ctx.upload_catalog(cv)
+    for _ in range(max(1, a.warmup)):
+        res = ctx.launch_select(batch, 60)
+    barrier()
+    kms, cms = [], []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        res = ctx.launch_select(batch, 60)
+        k, c = ctx.launch_stats()
+        kms.append(k)
+        cms.append(c)
+    elapsed = time.perf_counter() - t0
+    barrier()
+    kern = float(np.mean(kms))
+    if dist is not None:
+        import torch
+        tt = torch.tensor([elapsed, kern], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, kern = float(tt[0].item()), float(tt[1].item())
+    T = len(cat)
+    B = launch_bytes(T) * batch.n
+    achieved = B / (kern / 1e3) / 1e9 if kern > 0 else 0.0
+    st = res.rows["status"]
+    out = {
+        "metric": "launch selections/sec (filter chain + Truncate(60) per NodeClaim)",
+        "value": a.launch_batch / (kern / 1e3) if kern > 0 else 0.0,
+        "unit": "nodeclaims/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "kernel_ms": kern,
+        "call_ms": float(np.mean(cms)),
+        "call_rate_pcie_inclusive": a.launch_batch * a.steps / elapsed,
+        "scaling": "strong",
+        "config": {"workload": "config5 launch batch: %d NodeClaims x %d types (%d reserved offerings)" % (
+            a.launch_batch, T, sum(o.capacity_type == "reserved" for it in cat for o in it.offerings)),
+            "parallelism": "batch slices x%d" % world},
+        "outcomes": {"ok": int((st == abi.KP_OK).sum()), "ice": int((st == abi.KP_E_INSUFFICIENT_CAPACITY).sum()),
+                     "reserved": int((res.rows["capacity_type"] == abi.KP_CT_RESERVED).sum())},
+        "roofline": {"bound": "hbm", "kernel": "launch_select_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes": int(B)},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        import pyoracle
+        n = min(batch.n, 1000)
+        sb = model.LaunchBatchView(reqs_all[:n])
+        t = time.perf_counter()
+        stc, orc = pyoracle.launch_select(cv, sb, 60)
+        cpu_s = time.perf_counter() - t
+        out["cpu_baseline"] = {"value": n / cpu_s, "unit": "nodeclaims/s", "cores": 1, "kind": "port",
+                               "sample": "oracle orc_launch_select, 1 thread, first %d requests of the batch: %.2f s"
+                                         % (n, cpu_s)}
+        dev = ctx.launch_select(sb, 60)
+        try:
+            assert stc == abi.KP_OK
+            LC.assert_same(dev, orc)
+            out["parity_vs_cpu_baseline"] = True
+        except AssertionError:
+            out["parity_vs_cpu_baseline"] = False
+    ctx.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -140,6 +222,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-consolidation", action="store_true")
     ap.add_argument("--nodes", type=int, default=5000, help="config4 cluster size (consolidation leg)")
+    ap.add_argument("--launch-batch", type=int, default=10_000, help="config5 launch batch (NodeClaims)")
+    ap.add_argument("--no-launch", action="store_true")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -209,6 +293,7 @@ def main():
             traffic = json.load(f).get("hbm_bytes_per_launch")
 
     cons = None if a.no_consolidation else consolidation_leg(a, cat, local, rank, world, dist, barrier)
+    launch = None if a.no_launch else launch_leg(a, cat, local, rank, world, dist, barrier)
 
     cpu = None
     parity_ok = None
@@ -266,6 +351,7 @@ def main():
             "unschedulable": int((res.pod_result == -1).sum()),
             "solve_stats": {k: v for k, v in res.stats.items() if not k.startswith("ns_")},
             "consolidation": cons,
+            "launch": launch,
         }
         print(json.dumps(line))
     ctx.close()

@@ -255,7 +255,8 @@ struct kp_ctx {
     std::vector<int32_t> l_off_begin, l_off_val, l_ct, l_rt, l_rcap;
     std::vector<double> l_price;
     std::vector<uint8_t> l_avail, l_exotic;
-    DBuf<int32_t> d_l_off_begin, d_l_off_val, d_l_ct, d_l_rt, d_l_rcap, d_l_hdr, d_l_types, d_l_over;
+    DBuf<int32_t> d_l_off_begin, d_l_off_val, d_l_ct, d_l_rt, d_l_rcap, d_l_hdr, d_l_types;
+    DBuf<uint64_t> d_l_over;
     DBuf<double> d_l_price;
     DBuf<uint8_t> d_l_avail, d_l_exotic;
     DBuf<KlReq> d_l_req;
@@ -1839,11 +1840,26 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
         for (auto& kv : m) {
             const int kc = c->cat.find_key(kv.first);
             if (kc < 0) continue;  // no type or offering carries the key: absent on both sides, never constrains
-            const auto& vals = c->cat.keys[kc].vals;
+            const KeyDict& kd = c->cat.keys[kc];
+            const auto& vals = kd.vals;
             const int woff = (int)words.size();
             words.resize(words.size() + std::max<size_t>(1, (vals.size() + 63) / 64), 0ull);
-            for (size_t vv = 0; vv < vals.size(); vv++)
-                if (kv.second.has(vals[vv])) words[woff + vv / 64] |= 1ull << (vv % 64);
+            // bit v ⇔ Has(vals[v]); In sets visit only their own values, complements start full and clear theirs
+            const SReq& sq = kv.second;
+            if (!sq.complement) {
+                for (const auto& x : sq.vals) {
+                    const int v = kd.find(x);
+                    if (v >= 0 && sq.within(x)) words[woff + v / 64] |= 1ull << (v % 64);
+                }
+            } else {
+                const bool bounded = sq.has_gt || sq.has_lt;
+                for (size_t vv = 0; vv < vals.size(); vv++)
+                    if (!bounded || sq.within(vals[vv])) words[woff + vv / 64] |= 1ull << (vv % 64);
+                for (const auto& x : sq.vals) {
+                    const int v = kd.find(x);
+                    if (v >= 0) words[woff + v / 64] &= ~(1ull << (v % 64));
+                }
+            }
             woff_of[kc] = woff;
             const int op = kv.second.op();
             KlKey kk{kc, c->cat_multi[kc], 0u, woff};
@@ -1907,7 +1923,7 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
         HIPCHK(c->d_l_rq.upload(rq, s));
         HIPCHK(c->d_l_hdr.ensure((size_t)n * KL_HDR));
         HIPCHK(c->d_l_types.ensure((size_t)n * M));
-        HIPCHK(c->d_l_over.ensure((size_t)n * M * KL_MAX_OFF));
+        HIPCHK(c->d_l_over.ensure((size_t)n * M));
     }
     KpLaunch g{};
     g.T = T;
@@ -1939,11 +1955,12 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
     HIPCHK(hipEventRecord(c->ev[0], s));
     HIPCHK(kp_launch_select_kernel(g, s));
     HIPCHK(hipEventRecord(c->ev[1], s));
-    std::vector<int32_t> hdr((size_t)n * KL_HDR), tys((size_t)n * M), ov((size_t)n * M * KL_MAX_OFF);
+    std::vector<int32_t> hdr((size_t)n * KL_HDR), tys((size_t)n * M);
+    std::vector<uint64_t> ov((size_t)n * M);
     if (n > 0) {
         HIPCHK(hipMemcpyAsync(hdr.data(), c->d_l_hdr.p, hdr.size() * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(tys.data(), c->d_l_types.p, tys.size() * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(ov.data(), c->d_l_over.p, ov.size() * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(ov.data(), c->d_l_over.p, ov.size() * 8, hipMemcpyDeviceToHost, s));
     }
     HIPCHK(hipStreamSynchronize(s));
     float kms = 0.f;
@@ -1964,12 +1981,14 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
         r.override_offset = opos;
         r.n_overrides = 0;
         for (int k = 0; k < r.n_types; k++) {
-            if (type_ids && tpos < cap_type_ids) type_ids[tpos] = tys[(size_t)i * M + k];
+            const int32_t t = tys[(size_t)i * M + k];
+            if (type_ids && tpos < cap_type_ids) type_ids[tpos] = t;
             else short_buf = true;
             tpos++;
-            const int32_t* ol = &ov[((size_t)i * M + k) * KL_MAX_OFF];
-            for (int j = 0; j < KL_MAX_OFF && ol[j] >= 0; j++) {
-                if (override_offerings && opos < cap_overrides) override_offerings[opos] = ol[j];
+            // override offerings of slot k: bit j = offering row off_begin[t] + j, ascending
+            for (uint64_t m = ov[(size_t)i * M + k]; m; m &= m - 1) {
+                if (override_offerings && opos < cap_overrides)
+                    override_offerings[opos] = c->l_off_begin[t] + __builtin_ctzll(m);
                 else short_buf = true;
                 opos++;
                 r.n_overrides++;

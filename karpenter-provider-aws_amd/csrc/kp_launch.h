@@ -78,7 +78,7 @@ struct KpLaunch {
     // outputs (fixed stride)
     int32_t* out_hdr;                // [L][8 + KP_N_FILTERS]: status, failed, ct, n_types, n_over, n_options, -, -, rejected
     int32_t* out_types;              // [L][M]
-    int32_t* out_over;               // [L][M * KL_MAX_OFF]
+    uint64_t* out_over;              // [L][M] override offering mask per kept slot (bit j = row off_begin[t] + j)
 };
 
 #define KL_HDR 14

@@ -464,15 +464,8 @@ __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
                 if (S.pos[t] < 0) continue;
                 const int o0 = g.off_begin[t];
                 uint64_t m = S.lv[t] & S.am[t] & S.cmn[t] & ct_mask(g, o0, S.lv[t], ct_sel);
-                int32_t* dst = g.out_over + ((size_t)i * M + S.pos[t]) * KL_MAX_OFF;
-                int c = 0;
-                while (m) {
-                    const int j = __ffsll((unsigned long long)m) - 1;
-                    m &= m - 1;
-                    dst[c++] = o0 + j;
-                }
-                if (c < KL_MAX_OFF) dst[c] = -1;
-                n_over += c;
+                g.out_over[(size_t)i * M + S.pos[t]] = m;  // the host expands bit j to offering row o0 + j
+                n_over += __popcll(m);
             }
             n_over = bsum(n_over, S);
         }
