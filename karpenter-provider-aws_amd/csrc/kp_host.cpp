@@ -15,6 +15,7 @@
 #include <set>
 #include <memory>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -1812,19 +1813,35 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
     HIPCHK(hipSetDevice(ctx->device));
     kp_ctx* c = ctx;
     const int T = c->T, R = c->R, Kc = c->Kcat;
+    // Requests are encoded independently (NewNodeSelectorRequirementsWithMinValues + digest per NodeClaim), so the
+    // batch is split over host threads into chunk-local tables that are concatenated with their offsets rebased.
     std::vector<KlReq> reqs(n);
-    std::vector<KlKey> keys;
-    std::vector<KlMinKey> mins;
-    std::vector<uint64_t> words;
     std::vector<int64_t> rq((size_t)std::max(1, n) * R, 0);
     const int roles[KL_ROLES] = {c->key_zone, c->key_ct, c->key_zoneid, c->key_resvid, c->key_resvtype};
-    for (int i = 0; i < n; i++) {
+    struct Chunk {
+        std::vector<KlKey> keys;
+        std::vector<KlMinKey> mins;
+        std::vector<uint64_t> words;
+        kp_status st = KP_OK;
+        std::string msg;
+    };
+    const int nthr = std::max(1, std::min<int>({8, (int)std::thread::hardware_concurrency(), (n + 255) / 256}));
+    std::vector<Chunk> chunks(nthr);
+    auto encode_one = [&](int i, Chunk& ch) -> bool {
+        std::vector<KlKey>& keys = ch.keys;
+        std::vector<KlMinKey>& mins = ch.mins;
+        std::vector<uint64_t>& words = ch.words;
+        auto err = [&](kp_status st, const char* m) {
+            ch.st = st;
+            ch.msg = m;
+            return false;
+        };
         const kp_launch_request& lr = requests[i];
-        if (lr.n_requirements < 0 || (lr.n_requirements > 0 && !lr.requirements)) return fail(c, KP_E_INVALID, "bad request");
+        if (lr.n_requirements < 0 || (lr.n_requirements > 0 && !lr.requirements)) return err(KP_E_INVALID, "bad request");
         std::map<std::string, SReq> m;  // NewNodeSelectorRequirementsWithMinValues: Add = intersect per key
         for (int j = 0; j < lr.n_requirements; j++) {
             const kp_requirement& r = lr.requirements[j];
-            if (!r.key || r.op < 0 || r.op > 5) return fail(c, KP_E_INVALID, "bad requirement");
+            if (!r.key || r.op < 0 || r.op > 5) return err(KP_E_INVALID, "bad requirement");
             const std::string key = normalize(r.key);
             SReq q = sreq_new(r);
             auto it = m.find(key);
@@ -1903,7 +1920,7 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
                 mk.k = kc;
                 mk.mi = (c->cat_kflags[kc] & KF_CAT_MULTI) ? c->cat_multi[kc] : -1;
                 mk.nvals = (int)c->cat.keys[kc].vals.size();
-                if (mk.nvals > KP_MAX_MIN_WORDS * 64) return fail(c, KP_E_UNSUPPORTED, "minValues key with > 4096 values");
+                if (mk.nvals > KP_MAX_MIN_WORDS * 64) return err(KP_E_UNSUPPORTED, "minValues key with > 4096 values");
             } else {
                 mk.k = 0;  // no type carries the key: zero distinct values
                 mk.mi = -1;
@@ -1913,6 +1930,42 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
             mins.push_back(mk);
         }
         q.n_min = (int)mins.size() - q.min_off;
+        return true;
+    };
+    auto run_chunk = [&](int ti) {
+        const int i0 = (int)((int64_t)n * ti / nthr), i1 = (int)((int64_t)n * (ti + 1) / nthr);
+        for (int i = i0; i < i1; i++)
+            if (!encode_one(i, chunks[ti])) return;
+    };
+    if (nthr == 1) {
+        run_chunk(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int ti = 0; ti < nthr; ti++) th.emplace_back(run_chunk, ti);
+        for (auto& x : th) x.join();
+    }
+    std::vector<KlKey> keys;
+    std::vector<KlMinKey> mins;
+    std::vector<uint64_t> words;
+    for (int ti = 0; ti < nthr; ti++) {
+        Chunk& ch = chunks[ti];
+        if (ch.st != KP_OK) return fail(c, ch.st, ch.msg);
+        const int kb = (int)keys.size(), mb = (int)mins.size(), wbase = (int)words.size();
+        const int i0 = (int)((int64_t)n * ti / nthr), i1 = (int)((int64_t)n * (ti + 1) / nthr);
+        for (int i = i0; i < i1; i++) {
+            KlReq& q = reqs[i];
+            q.key_off += kb;
+            q.und_off += kb;
+            q.min_off += mb;
+            for (int r = 0; r < KL_ROLES; r++)
+                if (q.role[r].mode == KLR_CONSTRAINED) q.role[r].woff += wbase;
+        }
+        for (KlKey kk : ch.keys) {
+            kk.woff += wbase;  // undefined-key entries carry no bitset; their woff is never read
+            keys.push_back(kk);
+        }
+        mins.insert(mins.end(), ch.mins.begin(), ch.mins.end());
+        words.insert(words.end(), ch.words.begin(), ch.words.end());
     }
     hipStream_t s = c->stream;
     if (n > 0) {

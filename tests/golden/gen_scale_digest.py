@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Full-size oracle fixtures too slow to recompute inside a GPU test (~2 min of single-thread oracle time): runs the
+CPU oracle on seeded BASELINE workloads and writes per-field sha256 digests of its Solve output to
+tests/golden/scale_digests.json.  tests/test_gpu_parity.py::test_scale_digest compares the device result with them.
+
+    python tests/golden/gen_scale_digest.py
+"""
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [os.path.join(ROOT, "karpenter-provider-aws_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
+
+from kpsim import catalog, synth  # noqa: E402
+import parity  # noqa: E402
+
+CASES = {"config2_200k": dict(n_pods=200_000)}  # BASELINE configs[4]'s pod count over the config-2 pod mix
+
+
+def main():
+    cat = catalog.golden_catalog(fx=catalog.load_fixtures())
+    out = {}
+    for name, kw in CASES.items():
+        prob = synth.config2(catalog=cat, **kw)
+        t = time.time()
+        out[name] = dict(kw, **parity.result_digest(parity.run_oracle(prob)))
+        print(name, "%.1f s" % (time.time() - t), out[name]["n_nodeclaims"])
+    with open(os.path.join(HERE, "scale_digests.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -40,3 +40,22 @@ def assert_same(dev, orc, check_reqs=True):
     if check_reqs:
         for i in range(rd.n_nodeclaims):
             assert qd[i] == qo[i], (i, qd[i], qo[i])
+
+
+def result_digest(res):
+    """sha256 per output field of a Solve result ((Results, requirements) as returned by run_device / run_oracle), so
+    a full-size oracle run can be committed as a small fixture (tests/golden/gen_scale_digest.py)."""
+    import hashlib
+    r, q = res
+    h = lambda b: hashlib.sha256(b).hexdigest()  # noqa: E731
+    return {
+        "n_nodeclaims": int(r.n_nodeclaims),
+        "pod_result": h(np.ascontiguousarray(r.pod_result, np.int64).tobytes()),
+        "pod_order": h(np.ascontiguousarray(r.pod_order, np.int64).tobytes()),
+        "nodeclaim_nodepool": h(np.ascontiguousarray(r.nodeclaim_nodepool, np.int64).tobytes()),
+        "nodeclaim_n_pods": h(np.ascontiguousarray(r.nodeclaim_n_pods, np.int64).tobytes()),
+        "nodeclaim_slice_pos": h(np.ascontiguousarray(r.nodeclaim_slice_pos, np.int64).tobytes()),
+        "nodeclaim_n_options": h(np.ascontiguousarray(r.nodeclaim_n_options, np.int64).tobytes()),
+        "nodeclaim_types": h(repr([list(map(int, r.nodeclaim_types[i])) for i in range(r.n_nodeclaims)]).encode()),
+        "requirements": h(repr(q).encode()),
+    }

@@ -113,6 +113,19 @@ def test_config2_full_parity(ctx, golden):
     parity.assert_same(parity.run_device(ctx, prob), parity.run_oracle(prob))
 
 
+@pytest.mark.parametrize("name", ["config2_200k"])
+def test_scale_digest(ctx, golden, name):
+    """200k pods (BASELINE configs[4]'s pod count, config-2 pod mix): every output field's digest equals the oracle's,
+    committed by tests/golden/gen_scale_digest.py (the oracle needs ~2 min for this size, too long to rerun here)."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "scale_digests.json")) as f:
+        want = json.load(f)[name]
+    prob = synth.config2(catalog=golden, n_pods=want["n_pods"])
+    got = parity.result_digest(parity.run_device(ctx, prob))
+    assert got == {k: v for k, v in want.items() if k != "n_pods"}
+
+
 def test_config2_full_properties(ctx, golden):
     """Full 50k-pod config 2: size-independent properties of the device result on its own."""
     prob = synth.config2(catalog=golden)
