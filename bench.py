@@ -108,7 +108,8 @@ def consolidation_leg(a, cat, local, rank, world, dist, barrier):
                                     "cyc_scan", "cyc_total"], [int(st_m[1][i]) for i in (0, 1, 8, 9, 10, 11, 14)])),
         "roofline": {"bound": "hbm", "kernel": "consolidate_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes": int(B),
-                     "kernel_ms": float(km[1] + km[3])},
+                     "kernel_ms": float(km[1] + km[3]),
+                     "traffic_per_launch": pmc_traffic("consolidate")},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -133,6 +134,15 @@ def consolidation_leg(a, cat, local, rank, world, dist, barrier):
 def launch_bytes(T, R=12, K=32, O=6):
     """SURVEY §8d S_type = 8R + 2K + 16·O per instance type; one launch request sweeps every type of the catalog."""
     return T * (8 * R + 2 * K + 16 * O)
+
+
+def pmc_traffic(short):
+    """HBM bytes per launch of a kernel from the committed PMC pass (tools/pmc_summary.py), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_%s.json" % short)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get("hbm_bytes_per_launch")
 
 
 def launch_leg(a, golden, local, rank, world, dist, barrier):
@@ -187,8 +197,9 @@ def launch_leg(a, golden, local, rank, world, dist, barrier):
             "parallelism": "batch slices x%d" % world},
         "outcomes": {"ok": int((st == abi.KP_OK).sum()), "ice": int((st == abi.KP_E_INSUFFICIENT_CAPACITY).sum()),
                      "reserved": int((res.rows["capacity_type"] == abi.KP_CT_RESERVED).sum())},
-        "roofline": {"bound": "hbm", "kernel": "launch_select_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes": int(B)},
+        "roofline": {"bound": "hbm", "kernel": "launch_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes": int(B),
+                     "traffic": pmc_traffic("launch")},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -286,11 +297,7 @@ def main():
     B = algorithmic_bytes(res.stats, res.n_nodeclaims, T)
     ffd_s = kt[3] / 1e3
     achieved = B / ffd_s / 1e9
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_ffd.json")
-    if os.path.exists(pmc_path):
-        with open(pmc_path) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+    traffic = pmc_traffic("ffd")
 
     cons = None if a.no_consolidation else consolidation_leg(a, cat, local, rank, world, dist, barrier)
     launch = None if a.no_launch else launch_leg(a, cat, local, rank, world, dist, barrier)

@@ -1,5 +1,5 @@
 """Summarise a tools/profile_round.sh run into profiles/: the kernel-trace stats CSV (copied as-is) and
-profiles/pmc_ffd.json with the HBM bytes per ffd_kernel launch (MI355X_MICROARCH.md: FETCH_SIZE is doubled on
+profiles/pmc_<kernel>.json with the HBM bytes per launch of ffd_kernel, consolidate_kernel and launch_kernel (MI355X_MICROARCH.md: FETCH_SIZE is doubled on
 gfx950 for wide streaming reads; WRITE_SIZE taken as is).  Usage: python tools/pmc_summary.py <outdir> <tag>"""
 import csv
 import glob
@@ -36,27 +36,31 @@ def main():
     os.makedirs(prof, exist_ok=True)
     stats = find(os.path.join(out, "trace"), "*kernel_stats.csv")
     shutil.copy(stats, os.path.join(prof, "%s_kernel_stats.csv" % tag))
-    fetch_kb, nf = counter_per_launch(os.path.join(out, "fetch"), "FETCH_SIZE")
-    write_kb, nw = counter_per_launch(os.path.join(out, "write"), "WRITE_SIZE")
-    # rocprofv3 FETCH_SIZE / WRITE_SIZE are in KiB
-    fetch_b, write_b = fetch_kb * 1024.0, write_kb * 1024.0
-    rec = {
-        "kernel": "ffd_kernel",
-        "round": tag,
-        "command": "python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 (config2, 50k pods)",
-        "fetch_size_bytes_raw": fetch_b,
-        "write_size_bytes": write_b,
-        "hbm_bytes_per_launch": 2.0 * fetch_b + write_b,
-        "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section); WRITE_SIZE as reported",
-        "launches": {"fetch_pass": nf, "write_pass": nw},
-    }
-    with open(os.path.join(prof, "pmc_ffd.json"), "w") as f:
-        json.dump(rec, f, indent=1)
-    with open(os.path.join(prof, "%s_pmc_ffd.json" % tag), "w") as f:
-        json.dump(rec, f, indent=1)
+    recs = []
+    # per kernel: profiles/pmc_<short>.json (bench.py reads hbm_bytes_per_launch as roofline.traffic)
+    for kernel, short in (("ffd_kernel", "ffd"), ("consolidate_kernel", "consolidate"), ("launch_kernel", "launch")):
+        fetch_kb, nf = counter_per_launch(os.path.join(out, "fetch"), "FETCH_SIZE", kernel)
+        write_kb, nw = counter_per_launch(os.path.join(out, "write"), "WRITE_SIZE", kernel)
+        # rocprofv3 FETCH_SIZE / WRITE_SIZE are in KiB
+        fetch_b, write_b = fetch_kb * 1024.0, write_kb * 1024.0
+        rec = {
+            "kernel": kernel,
+            "round": tag,
+            "command": "python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 (config2 50k pods; config4; config5 launch)",
+            "fetch_size_bytes_raw": fetch_b,
+            "write_size_bytes": write_b,
+            "hbm_bytes_per_launch": 2.0 * fetch_b + write_b,
+            "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section); WRITE_SIZE as reported",
+            "launches": {"fetch_pass": nf, "write_pass": nw},
+        }
+        for name in ("pmc_%s.json" % short, "%s_pmc_%s.json" % (tag, short)):
+            with open(os.path.join(prof, name), "w") as f:
+                json.dump(rec, f, indent=1)
+        recs.append(rec)
     with open(stats) as f:
         print(f.read())
-    print(json.dumps(rec))
+    for rec in recs:
+        print(json.dumps(rec))
 
 
 if __name__ == "__main__":
