@@ -21,7 +21,9 @@
 #define KP_MAX_CLASS_KEYS 32         // label keys constrained by one pod class / template
 #define KP_MAX_SLOTS 64              // zone slots × capacity-type slots
 #define KP_MAX_R 16                  // resource axes
+#ifndef KP_NWAVES
 #define KP_NWAVES 8                  // waves in the single-workgroup FFD kernel
+#endif
 #define KP_LDS_AXES 6                // allocatable axes staged in LDS
 #define KP_MAX_SCR_WORDS 64          // value-bitset words of one class's keys (per-wave LDS scratch)
 #define KP_MAX_MIN_WORDS 64          // value bitset for a minValues distinct count (4096 values)
