@@ -36,6 +36,7 @@ struct LShared {
     uint64_t minbits[KP_MAX_MIN_WORDS];
     double redd[NWV];
     int redi[NWV];
+    int ncomp;
 };
 
 __device__ __forceinline__ bool wbit(const uint64_t* w, int off, int v) { return (w[off + (v >> 6)] >> (v & 63)) & 1ull; }
@@ -387,8 +388,11 @@ __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
     int status = failed >= 0 ? KP_E_INSUFFICIENT_CAPACITY : KP_OK;
     int ct_sel = KP_CT_ON_DEMAND, n_types = 0, n_over = 0;
     if (failed < 0) {
+        // compact the kept types: S.key[u] = cheapest compatible available price, S.tmp[u] = name_rank << 32 | t
+        // (order of u is irrelevant: the rank below is a pure count over the (price, name, index) order)
+        if (tid == 0) S.ncomp = 0;
+        __syncthreads();
         for (int t = tid; t < T; t += NT) {
-            S.pos[t] = -1;
             if (!S.keep[t]) continue;
             const int o0 = g.off_begin[t];
             uint64_t m = S.lv[t] & S.am[t] & S.cmn[t] & S.ctok[t];
@@ -398,25 +402,38 @@ __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
                 m &= m - 1;
                 p = g.off_price[o0 + j] < p ? g.off_price[o0 + j] : p;
             }
-            S.key[t] = p;
+            const int u = atomicAdd(&S.ncomp, 1);
+            S.key[u] = p;
+            S.tmp[u] = ((uint64_t)g.name_rank[t] << 32) | (uint32_t)t;
         }
         __syncthreads();
-        for (int t = tid; t < T; t += NT) {
-            if (!S.keep[t]) continue;
-            const double kt = S.key[t];
-            const uint32_t nt = g.name_rank[t];
+        const int nc = S.ncomp;
+        constexpr int PER = (KP_MAX_TYPES + NT - 1) / NT;
+        int my_t[PER], my_r[PER];
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            my_t[k] = -1;
+            my_r[k] = M;
+            const int u = tid + k * NT;
+            if (u >= nc) continue;
+            const double kt = S.key[u];
+            const uint64_t pt = S.tmp[u];
             int rank = 0;
-            for (int u = 0; u < T && rank < M; u++) {
-                if (!S.keep[u] || u == t) continue;
-                const double ku = S.key[u];
-                const uint32_t nu = g.name_rank[u];
-                rank += (ku < kt) || (ku == kt && (nu < nt || (nu == nt && u < t)));
+            for (int v = 0; v < nc && rank < M; v++) {
+                const double kv = S.key[v];
+                rank += (kv < kt) || (kv == kt && S.tmp[v] < pt);
             }
-            if (rank < M) {
-                S.pos[t] = (int16_t)rank;
-                g.out_types[(size_t)i * M + rank] = t;
-            }
+            my_t[k] = (int)(uint32_t)pt;
+            my_r[k] = rank;
         }
+        for (int t = tid; t < T; t += NT) S.pos[t] = -1;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < PER; k++)
+            if (my_t[k] >= 0 && my_r[k] < M) {
+                S.pos[my_t[k]] = (int16_t)my_r[k];
+                g.out_types[(size_t)i * M + my_r[k]] = my_t[k];
+            }
         n_types = n < M ? n : M;
         __syncthreads();
         // SatisfiesMinValues over the truncated list (monotone in the prefix, so the full list decides)
