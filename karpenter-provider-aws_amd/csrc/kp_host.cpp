@@ -246,6 +246,10 @@ struct kp_ctx {
     DBuf<kp_probe_result> d_probe_out;
     KpCons cons{};                           // prepared consolidation pass (device pointers set per execute)
     bool cons_prepared = false;
+    // device prep of the prepared cluster (queue sort, ranks, pending bits, class / template / existing-node masks)
+    // is reused by later kp_consolidate_execute calls until any entry point that rewrites device tables runs
+    bool cons_prep_valid = false;
+    int32_t* cons_q0 = nullptr;
     int cons_max_candidates = 100, cons_n_pending = 0;
     std::vector<int32_t> cons_off;           // candidate pod CSR offsets
     double cons_ms[3] = {};                  // device prep (sort, masks), probe kernel, whole call
@@ -362,6 +366,7 @@ static kp_status upload_launch_tables(kp_ctx* c, const kp_catalog_view* v, const
 
 extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, uint64_t epoch) try {
     if (!ctx || !v) return KP_E_INVALID;
+    ctx->cons_prep_valid = false;
     HIPCHK(hipSetDevice(ctx->device));
     const int T = v->n_types, R = v->n_resources, KL = v->n_label_keys;
     if (T <= 0 || R <= 0 || R > KP_MAX_R) return fail(ctx, KP_E_INVALID, "bad n_types / n_resources");
@@ -593,6 +598,7 @@ extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, ui
 
 extern "C" kp_status kp_catalog_patch_avail(kp_ctx* ctx, const uint8_t* available, int32_t n, uint64_t epoch) {
     if (!ctx || !available) return KP_E_INVALID;
+    ctx->cons_prep_valid = false;
     if (!ctx->have_catalog) return fail(ctx, KP_E_STATE, "no catalog");
     if (n != (int)ctx->off_type.size()) return fail(ctx, KP_E_INVALID, "offering count mismatch");
     HIPCHK(hipSetDevice(ctx->device));
@@ -608,6 +614,7 @@ extern "C" kp_status kp_catalog_patch_avail(kp_ctx* ctx, const uint8_t* availabl
 extern "C" kp_status kp_catalog_patch_price(kp_ctx* ctx, const int32_t* idx, const double* price, int32_t n,
                                             uint64_t epoch) {
     if (!ctx || (n > 0 && (!idx || !price))) return KP_E_INVALID;
+    ctx->cons_prep_valid = false;
     if (!ctx->have_catalog) return fail(ctx, KP_E_STATE, "no catalog");
     HIPCHK(hipSetDevice(ctx->device));
     for (int i = 0; i < n; i++) {
@@ -718,6 +725,7 @@ static bool tolerates(const kp_taint& taint, const kp_toleration* tols, int n) {
 
 extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try {
     if (!ctx || !in) return KP_E_INVALID;
+    ctx->cons_prep_valid = false;
     if (!ctx->have_catalog) return fail(ctx, KP_E_STATE, "kp_solve before kp_catalog_upload");
     if (ctx->has_reserved)
         return fail(ctx, KP_E_UNSUPPORTED, "Solve over a catalog with reserved offerings is not supported by this build");
@@ -1215,6 +1223,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
 // ---------------------------------------------------------------------------------------------
 extern "C" kp_status kp_solve_execute(kp_ctx* ctx) {
     if (!ctx) return KP_E_INVALID;
+    ctx->cons_prep_valid = false;
     if (!ctx->prepared) return fail(ctx, KP_E_STATE, "kp_solve_execute before kp_solve_prepare");
     HIPCHK(hipSetDevice(ctx->device));
     kp_ctx* c = ctx;
@@ -1409,6 +1418,7 @@ extern "C" int32_t kp_consolidate_probe_count(const kp_consolidate_input* in) {
 extern "C" kp_status kp_consolidate_prepare(kp_ctx* ctx, const kp_consolidate_input* in) try {
     if (!ctx || !in) return KP_E_INVALID;
     ctx->cons_prepared = false;
+    ctx->cons_prep_valid = false;
     if (ctx->has_reserved)
         return fail(ctx, KP_E_UNSUPPORTED, "consolidation over a catalog with reserved offerings is not supported by this build");
     if (in->mode != KP_CONSOLIDATE_SINGLE && in->mode != KP_CONSOLIDATE_MULTI)
@@ -1561,22 +1571,27 @@ extern "C" kp_status kp_consolidate_execute(kp_ctx* ctx, int32_t mode, int32_t p
     HIPCHK(hipMemsetAsync(c->d_cons_stats.p, 0, CS_COUNT * sizeof(int64_t), s));
     HIPCHK(hipMemsetAsync(c->d_next.p, 0, 3 * sizeof(int32_t), s));
     HIPCHK(c->d_retry.ensure(nprobe));
-    HIPCHK(hipMemsetAsync(c->d_pend_bits.p, 0, (size_t)k.PW * 8, s));
-    if (!c->h_remaining.empty())
-        HIPCHK(hipMemcpyAsync(c->d_remaining.p, c->h_remaining.data(), c->h_remaining.size() * sizeof(int64_t),
-                              hipMemcpyHostToDevice, s));
     HIPCHK(hipEventRecord(c->ev[0], s));
-    int32_t* q0 = nullptr;
-    if (P > 0) {
-        size_t tb = c->sort_temp_bytes;
-        HIPCHK(kp_queue_sort(c->d_sort_fields.p, P, c->d_perm_a.p, c->d_perm_b.p, c->d_keys_a.p, c->d_keys_b.p,
-                             c->d_sort_temp.p, &tb, s, &q0));
+    if (!c->cons_prep_valid) {
+        HIPCHK(hipMemsetAsync(c->d_pend_bits.p, 0, (size_t)k.PW * 8, s));
+        if (!c->h_remaining.empty())
+            HIPCHK(hipMemcpyAsync(c->d_remaining.p, c->h_remaining.data(), c->h_remaining.size() * sizeof(int64_t),
+                                  hipMemcpyHostToDevice, s));
+        int32_t* q0 = nullptr;
+        if (P > 0) {
+            size_t tb = c->sort_temp_bytes;
+            HIPCHK(kp_queue_sort(c->d_sort_fields.p, P, c->d_perm_a.p, c->d_perm_b.p, c->d_keys_a.p, c->d_keys_b.p,
+                                 c->d_sort_temp.p, &tb, s, &q0));
+        }
+        d.queue0 = q0;
+        HIPCHK(kp_launch_cons_prep(q0, P, c->d_rank.p, c->d_pending.p, c->cons_n_pending, c->d_pend_bits.p, s));
+        HIPCHK(kp_launch_class_mask(d, s));
+        HIPCHK(kp_launch_template_init(d, s));
+        HIPCHK(kp_launch_existing(d, s));
+        c->cons_q0 = q0;
+        c->cons_prep_valid = true;
     }
-    d.queue0 = q0;
-    HIPCHK(kp_launch_cons_prep(q0, P, c->d_rank.p, c->d_pending.p, c->cons_n_pending, c->d_pend_bits.p, s));
-    HIPCHK(kp_launch_class_mask(d, s));
-    HIPCHK(kp_launch_template_init(d, s));
-    HIPCHK(kp_launch_existing(d, s));
+    d.queue0 = c->cons_q0;
     HIPCHK(hipEventRecord(c->ev[1], s));
     k.cand_i = c->d_cand_i.p;
     k.cand_off = c->d_cand_off.p;
