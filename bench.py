@@ -154,8 +154,8 @@ def launch_leg(a, golden, local, rank, world, dist, barrier):
     import launch_cases as LC
     cat = synth.config5_catalog(golden)
     reqs_all = synth.launch_requests(cat, n=a.launch_batch)
-    b0 = a.launch_batch * rank // world
-    b1 = a.launch_batch * (rank + 1) // world
+    from kpsim.consolidation import shard_range
+    b0, b1 = shard_range(a.launch_batch, rank, world)  # the slice kpsim.launch.select_sharded gives this rank
     batch = model.LaunchBatchView(reqs_all[b0:b1])
     ctx = native.Context(local)
     cv = model.CatalogView(cat)

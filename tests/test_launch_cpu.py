@@ -41,3 +41,43 @@ def test_oracle_config5_batch_runs(golden):
     assert st == abi.KP_OK
     assert (res.rows["status"] == abi.KP_OK).sum() > 20
     assert (res.rows["capacity_type"] == abi.KP_CT_RESERVED).sum() > 0
+
+
+def _launch_rank_main(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    from kpsim import catalog, launch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cat = synth.config5_catalog(catalog.golden_catalog())
+        cv = model.CatalogView(cat)
+        reqs = synth.launch_requests(cat, n=45, seed=11)
+        fn = lambda b: pyoracle.launch_select(cv, b, 60)[1]  # noqa: E731
+        q.put((rank, launch.select_sharded(reqs, fn, group=dist.group.WORLD)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_launch_equals_single_rank_gloo(golden):
+    """Rank slices of a launch batch (bench.py's launch leg at N>1) gathered over gloo equal the whole-batch result."""
+    import multiprocessing as mp
+    import socket
+    from kpsim import launch
+    cat = synth.config5_catalog(golden)
+    cv = model.CatalogView(cat)
+    reqs = synth.launch_requests(cat, n=45, seed=11)
+    want = launch.select_sharded(reqs, lambda b: pyoracle.launch_select(cv, b, 60)[1])
+    assert len(want) == 45 and any(r[0] == abi.KP_OK for r in want)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_launch_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert got[0] == want and got[1] == want
