@@ -191,7 +191,8 @@ struct WitnessAcc {
         float sc = 3.0e38f;
 #pragma unroll
         for (int ai = 0; ai < KP_LDS_AXES; ai++)
-            if (inv[ai] > 0.0f) sc = fminf(sc, (float)(av[ai] - tot[ai]) * inv[ai]);
+            // i64 → f64 → f32: four VALU ops instead of the expanded i64 → f32 sequence (the score is a heuristic)
+            if (inv[ai] > 0.0f) sc = fminf(sc, (float)(double)(av[ai] - tot[ai]) * inv[ai]);
         if (sc > best) {
             best = sc;
             bt = t;
