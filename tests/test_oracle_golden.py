@@ -140,3 +140,27 @@ def test_gosort_restatement_sorts(fx):
         assert (np.diff(keys[out]) >= 0).all()
         # deterministic
         assert (pyoracle.go_sort_slice_ints(keys, perm) == out).all()
+
+
+def test_scale_digest_fixture_shape():
+    """tests/golden/scale_digests.json (oracle digests for the 200k-pod GPU parity test) is complete and well-formed."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "scale_digests.json")) as f:
+        fx_ = json.load(f)
+    want = {"n_pods", "n_nodeclaims", "pod_result", "pod_order", "nodeclaim_nodepool", "nodeclaim_n_pods",
+            "nodeclaim_slice_pos", "nodeclaim_n_options", "nodeclaim_types", "requirements"}
+    for name, rec in fx_.items():
+        assert set(rec) == want, name
+        assert rec["n_pods"] >= 200_000 and rec["n_nodeclaims"] > 0
+        for k in want - {"n_pods", "n_nodeclaims"}:
+            assert len(rec[k]) == 64 and int(rec[k], 16) >= 0
+
+
+def test_result_digest_deterministic(golden):
+    """The digest the 200k fixture relies on is a pure function of the Solve output (two oracle runs agree)."""
+    import parity
+    prob = synth.config2(n_pods=800, catalog=golden)
+    a = parity.result_digest(parity.run_oracle(prob))
+    b = parity.result_digest(parity.run_oracle(prob))
+    assert a == b and a["n_nodeclaims"] > 0
