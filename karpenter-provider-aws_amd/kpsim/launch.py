@@ -35,3 +35,49 @@ def select_sharded(requests: List[model.LaunchRequest], select_fn: Callable[[mod
     parts: List[Optional[list]] = [None] * world
     dist.all_gather_object(parts, part, group=group)
     return [row for p in parts for row in p]
+
+
+# ---- Fleet emulation: the kwok fake EC2's CreateFleet override pick ----
+
+MAX_FLOAT64 = 1.7976931348623157e308
+
+
+def min_by_score(scores: List[float]) -> int:
+    """Index lo.MinBy picks in kwok/ec2/ec2.go:432-461: min starts at item 0 and item i replaces it when
+    comparison(item, min) holds, where comparison is true if min's score is 0 (lo.IsEmpty), false if the item's score
+    is 0, else item < min.  Ties keep the earlier override."""
+    if not scores:
+        return -1
+    best = 0
+    for i in range(1, len(scores)):
+        a, b = scores[i], scores[best]
+        if b == 0.0 or (a != 0.0 and a < b):
+            best = i
+    return best
+
+
+def fleet_pick(catalog, res: model.LaunchResults, i: int):
+    """(type index, offering row) CreateFleet would launch for request i in the kwok provider, or None.
+
+    Overrides come in getOverrides order (instance.go:420-467: kept types in Truncate order, then each type's
+    Available ∧ Compatible offerings; every zone is assumed to have a subnet).  The fleet's target capacity type is spot
+    for a spot launch and on-demand otherwise (reserved launches are on-demand fleets); kwok/strategy/strategy.go:45-60
+    scores an override by SpotPrice(type, zone) or OnDemandPrice(type), MaxFloat64 when there is no price."""
+    r = res.rows[i]
+    if int(r["status"]) != 0:
+        return None
+    from kpsim import abi
+    spot = int(r["capacity_type"]) == abi.KP_CT_SPOT
+    owner = [t for t, it in enumerate(catalog) for _ in it.offerings]
+    flat = [o for it in catalog for o in it.offerings]
+    rows = [int(x) for x in res.offerings(i)]
+
+    def score(row):
+        it = catalog[owner[row]]
+        if spot:
+            return next((o.price for o in it.offerings if o.capacity_type == "spot" and o.zone == flat[row].zone),
+                        MAX_FLOAT64)
+        return next((o.price for o in it.offerings if o.capacity_type == "on-demand"), MAX_FLOAT64)
+
+    k = min_by_score([score(row) for row in rows])
+    return None if k < 0 else (owner[rows[k]], rows[k])

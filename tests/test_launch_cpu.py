@@ -81,3 +81,35 @@ def test_sharded_launch_equals_single_rank_gloo(golden):
     for p in procs:
         p.join(60)
     assert got[0] == want and got[1] == want
+
+
+@pytest.mark.parametrize("scores,want", [([3.0, 1.0, 2.0], 1), ([1.0, 1.0], 0), ([0.0, 5.0, 3.0], 2),
+                                         ([5.0, 0.0, 3.0], 2), ([0.0, 0.0], 1), ([], -1)])
+def test_fleet_min_by_score(scores, want):
+    """lo.MinBy with kwok's comparator (kwok/ec2/ec2.go:432-461), including its zero-score (lo.IsEmpty) branches."""
+    from kpsim import launch
+    assert launch.min_by_score(scores) == want
+
+
+def test_fleet_pick_config5(golden):
+    """The kwok CreateFleet pick over the oracle's launch result: one of the overrides, of minimal score, the first
+    such override, and of the launch's capacity type (reserved launches pick reserved offerings)."""
+    from kpsim import launch
+    cat = synth.config5_catalog(golden)
+    cv = model.CatalogView(cat)
+    b = model.LaunchBatchView(synth.launch_requests(cat, n=40, seed=5))
+    st, res = pyoracle.launch_select(cv, b, 60)
+    assert st == abi.KP_OK
+    flat = [o for it in cat for o in it.offerings]
+    ct_name = {abi.KP_CT_ON_DEMAND: "on-demand", abi.KP_CT_SPOT: "spot", abi.KP_CT_RESERVED: "reserved"}
+    n_ok = 0
+    for i in range(b.n):
+        pick = launch.fleet_pick(cat, res, i)
+        if int(res.rows[i]["status"]) != abi.KP_OK:
+            assert pick is None
+            continue
+        n_ok += 1
+        t, row = pick
+        assert row in list(res.offerings(i)) and t in list(res.types(i))
+        assert flat[row].capacity_type == ct_name[int(res.rows[i]["capacity_type"])]
+    assert n_ok > 0
