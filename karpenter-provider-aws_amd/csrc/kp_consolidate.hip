@@ -726,17 +726,17 @@ bool kp_cons_plan_lds(const KpDev& d, KpCons& k, int max_bytes) {
     return (int)off <= max_bytes;
 }
 
+// Per-device kernel attributes, set by kp_ctx_create with the ctx's device current (see kp_ffd_set_attributes).
+hipError_t kp_cons_set_attributes() {
+    hipError_t e = hipFuncSetAttribute((const void*)consolidate_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       KP_LDS_BYTES);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void*)consolidate_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                KP_LDS_BYTES);
+    return e;
+}
+
 hipError_t kp_launch_consolidate(const KpDev& d, const KpCons& k, int n_workers, hipStream_t s) {
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)consolidate_kernel<false>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, KP_LDS_BYTES);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)consolidate_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    KP_LDS_BYTES);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
     if (n_workers <= 0 || k.n_probes <= 0) return hipSuccess;
     if (k.no_fast != 1) hipLaunchKernelGGL(consolidate_kernel<false>, dim3(n_workers), dim3(64), (size_t)k.lds_bytes, s, d, k);
     if (k.no_fast != 2) hipLaunchKernelGGL(consolidate_kernel<true>, dim3(n_workers), dim3(64), (size_t)k.lds_bytes, s, d, k);

@@ -30,6 +30,8 @@ hipError_t kp_launch_class_mask(const KpDev& d, hipStream_t s);
 hipError_t kp_launch_template_init(const KpDev& d, hipStream_t s);
 hipError_t kp_launch_existing(const KpDev& d, hipStream_t s);
 hipError_t kp_launch_ffd(const KpDev& d, hipStream_t s);
+hipError_t kp_ffd_set_attributes();
+hipError_t kp_cons_set_attributes();
 hipError_t kp_launch_finalize(const KpDev& d, int n_nodeclaims, hipStream_t s);
 bool kp_cons_plan_lds(const KpDev& d, KpCons& k, int max_bytes);
 hipError_t kp_launch_select_kernel(const KpLaunch& g, hipStream_t s);
@@ -153,9 +155,13 @@ struct HReq {
 };
 
 template <class T>
-struct DBuf {  // device buffer, grow-only
+struct DBuf {  // device buffer, grow-only; freed by its destructor (the owning ctx sets the device first)
     T* p = nullptr;
     size_t n = 0;
+    DBuf() = default;
+    DBuf(const DBuf&) = delete;
+    DBuf& operator=(const DBuf&) = delete;
+    ~DBuf() { release(); }
     hipError_t ensure(size_t count) {
         if (count <= n && p) return hipSuccess;
         if (p) hipFree(p);
@@ -304,6 +310,7 @@ extern "C" kp_status kp_ctx_create(const kp_device_opts* opts, kp_ctx** out) try
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) return KP_E_DEVICE;
     for (auto& e : ctx->ev)
         if (hipEventCreate(&e) != hipSuccess) return KP_E_DEVICE;
+    if (kp_ffd_set_attributes() != hipSuccess || kp_cons_set_attributes() != hipSuccess) return KP_E_DEVICE;
     *out = ctx.release();
     return KP_OK;
 } catch (...) {
@@ -314,42 +321,10 @@ extern "C" kp_status kp_ctx_destroy(kp_ctx* ctx) {
     if (!ctx) return KP_OK;
     hipSetDevice(ctx->device);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
-    // buffers are released with the process / device reset; explicit frees for long-lived processes
-    ctx->d_type_val.release();
-    ctx->d_multi16.release();
-    ctx->d_multi_mask.release();
-    ctx->d_dne_mask.release();
-    ctx->d_avail_zc.release();
-    ctx->d_nonneg.release();
-    ctx->d_alloc.release();
-    ctx->d_cap.release();
-    ctx->d_slot_price.release();
-    ctx->d_slot_zone.release();
-    ctx->d_slot_ct.release();
-    ctx->d_slot_zoneid.release();
-    ctx->d_name_rank.release();
-    ctx->d_kflags.release(); ctx->d_cls_flags.release(); ctx->d_tol.release();
-    ctx->d_kcat.release(); ctx->d_kmulti.release(); ctx->d_woff.release(); ctx->d_nw.release(); ctx->d_nval.release();
-    ctx->d_vbase.release(); ctx->d_cls_koff.release(); ctx->d_cls_keys.release(); ctx->d_cls_wsoff.release();
-    ctx->d_min_keys.release(); ctx->d_val_isint.release(); ctx->d_limit_set.release(); ctx->d_val_int.release();
-    ctx->d_daemon.release(); ctx->d_remaining.release(); ctx->d_pod_req.release(); ctx->d_sort_fields.release();
-    ctx->d_nc_req.release(); ctx->d_stats.release(); ctx->d_cls_hdr.release(); ctx->d_nc_hdr.release();
-    ctx->d_empty_hdr.release(); ctx->d_cls_words.release(); ctx->d_V.release(); ctx->d_tmpl_rows.release();
-    ctx->d_tmpl_opts.release(); ctx->d_nc_words.release(); ctx->d_nc_opts.release(); ctx->d_empty_words.release();
-    ctx->d_keys_a.release(); ctx->d_keys_b.release(); ctx->d_tmpl_ok.release(); ctx->d_pod_cls.release();
-    ctx->d_pod_shape.release(); ctx->d_perm_a.release(); ctx->d_perm_b.release(); ctx->d_nc_tmpl.release();
-    ctx->d_qbuf.release(); ctx->d_last_len.release(); ctx->d_pod_result.release(); ctx->d_pod_order.release();
-    ctx->d_nc_count.release(); ctx->d_nc_npods.release(); ctx->d_nc_slice_pos.release(); ctx->d_nc_nopts.release();
-    ctx->d_nc_valid.release(); ctx->d_nc_types.release(); ctx->d_nc_ntypes.release(); ctx->d_err.release();
-    ctx->d_sort_temp.release();
-    ctx->d_retry.release(); ctx->d_rank.release(); ctx->d_cand_i.release(); ctx->d_cand_off.release(); ctx->d_pending.release(); ctx->d_cand_pods.release(); ctx->d_ring.release();
-    ctx->d_ring_last.release(); ctx->d_next.release(); ctx->d_cand_price.release(); ctx->d_cand_cap.release();
-    ctx->d_delta.release(); ctx->d_alloc_act.release(); ctx->d_cons_stats.release(); ctx->d_pend_bits.release();
-    ctx->d_pbits.release(); ctx->d_init.release(); ctx->d_probe_out.release();
     for (auto& e : ctx->ev)
         if (e) hipEventDestroy(e);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
-    delete ctx;
+    delete ctx;  // every DBuf member frees its device memory (on the device set above)
     return KP_OK;
 }
 
@@ -366,7 +341,11 @@ static kp_status upload_launch_tables(kp_ctx* c, const kp_catalog_view* v, const
 
 extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, uint64_t epoch) try {
     if (!ctx || !v) return KP_E_INVALID;
-    ctx->cons_prep_valid = false;
+    // every prepared solve / consolidation pass captured device pointers and sizes of the previous catalog, and the
+    // tables below may be reallocated: nothing prepared survives an upload, successful or not
+    ctx->have_catalog = false;
+    ctx->prepared = ctx->executed = false;
+    ctx->cons_prepared = ctx->cons_prep_valid = false;
     HIPCHK(hipSetDevice(ctx->device));
     const int T = v->n_types, R = v->n_resources, KL = v->n_label_keys;
     if (T <= 0 || R <= 0 || R > KP_MAX_R) return fail(ctx, KP_E_INVALID, "bad n_types / n_resources");
@@ -967,6 +946,8 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     uidseen.reserve((size_t)P * 2);
     bool uid_collision = false;
     const kp_pods_view& pv = in->pods;
+    // kp_pods_view.uids is optional (NULL, or NULL entries): a missing UID is the empty string
+    auto uid_of = [&](int p) -> const char* { return pv.uids && pv.uids[p] ? pv.uids[p] : ""; };
     for (int p = 0; p < P; p++) {
         const int cl = pv.class_id[p];
         if (cl < 0 || cl >= C) return fail(ctx, KP_E_INVALID, "pod class out of range");
@@ -982,7 +963,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         pshape[p] = it->second;
         // NewQueue key: cpu desc, memory desc, creation asc, UID asc.  The UID enters as its first 8 bytes
         // (big-endian, order-preserving); if two distinct UIDs share that prefix, exact string ranks are used.
-        const char* u = pv.uids && pv.uids[p] ? pv.uids[p] : "";
+        const char* u = uid_of(p);
         uint64_t uk = 0;
         const char* q = u;
         for (int i = 0; i < 8; i++) {
@@ -994,15 +975,15 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         fields[(size_t)p * 4 + 2] = pv.creation_ns ? pv.creation_ns[p] : 0;
         fields[(size_t)p * 4 + 3] = (int64_t)(uk ^ 0x8000000000000000ull);
         auto ins = uidseen.emplace(uk, p);
-        if (!ins.second && strcmp(pv.uids[ins.first->second] ? pv.uids[ins.first->second] : "", u) != 0) uid_collision = true;
+        if (!ins.second && strcmp(uid_of(ins.first->second), u) != 0) uid_collision = true;
     }
     if (uid_collision) {
         std::vector<int> idx(P);
         for (int p = 0; p < P; p++) idx[p] = p;
-        std::sort(idx.begin(), idx.end(), [&](int a, int b) { return strcmp(pv.uids[a], pv.uids[b]) < 0; });
+        std::sort(idx.begin(), idx.end(), [&](int a, int b) { return strcmp(uid_of(a), uid_of(b)) < 0; });
         int rank = 0;
         for (int i = 0; i < P; i++) {
-            if (i > 0 && strcmp(pv.uids[idx[i]], pv.uids[idx[i - 1]]) != 0) rank = i;
+            if (i > 0 && strcmp(uid_of(idx[i]), uid_of(idx[i - 1])) != 0) rank = i;
             fields[(size_t)idx[i] * 4 + 3] = (int64_t)((uint64_t)rank ^ 0x8000000000000000ull);
         }
     }
@@ -1224,7 +1205,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
 extern "C" kp_status kp_solve_execute(kp_ctx* ctx) {
     if (!ctx) return KP_E_INVALID;
     ctx->cons_prep_valid = false;
-    if (!ctx->prepared) return fail(ctx, KP_E_STATE, "kp_solve_execute before kp_solve_prepare");
+    if (!ctx->prepared || !ctx->have_catalog) return fail(ctx, KP_E_STATE, "kp_solve_execute before kp_solve_prepare");
     HIPCHK(hipSetDevice(ctx->device));
     kp_ctx* c = ctx;
     KpDev& d = c->dev;
@@ -1523,7 +1504,8 @@ extern "C" kp_status kp_consolidate_prepare(kp_ctx* ctx, const kp_consolidate_in
 extern "C" kp_status kp_consolidate_execute(kp_ctx* ctx, int32_t mode, int32_t probe_begin, int32_t probe_end,
                                             kp_probe_result* results, int32_t cap_results) try {
     if (!ctx) return KP_E_INVALID;
-    if (!ctx->cons_prepared) return fail(ctx, KP_E_STATE, "kp_consolidate_execute before kp_consolidate_prepare");
+    if (!ctx->cons_prepared || !ctx->have_catalog)
+        return fail(ctx, KP_E_STATE, "kp_consolidate_execute before kp_consolidate_prepare");
     if (mode != KP_CONSOLIDATE_SINGLE && mode != KP_CONSOLIDATE_MULTI) return fail(ctx, KP_E_INVALID, "unknown consolidation mode");
     kp_ctx* c = ctx;
     HIPCHK(hipSetDevice(c->device));

@@ -1204,14 +1204,13 @@ hipError_t kp_launch_template_init(const KpDev& d, hipStream_t s) {
     hipLaunchKernelGGL(template_init_kernel, dim3(d.NT), dim3(64), 0, s, d);
     return hipGetLastError();
 }
+// Per-device kernel attributes: called by kp_ctx_create with the ctx's device current (every ctx, so a second ctx on
+// another device of the same process gets them too; the call is idempotent and needs no process-wide flag).
+hipError_t kp_ffd_set_attributes() {
+    return hipFuncSetAttribute((const void*)ffd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, KP_LDS_BYTES);
+}
 hipError_t kp_launch_ffd(const KpDev& d, hipStream_t s) {
-    static bool attr = false;
     const size_t bytes = (size_t)d.lds_bytes;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)ffd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, KP_LDS_BYTES);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
     hipLaunchKernelGGL(ffd_kernel, dim3(1), dim3(KP_NWAVES * 64), bytes, s, d);
     return hipGetLastError();
 }

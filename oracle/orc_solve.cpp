@@ -315,11 +315,12 @@ struct Solver {
     }
 
     void solve() {
-        // NewQueue: sort.Slice(pods, byCPUAndMemoryDescending) — a total order (UIDs unique).
+        // NewQueue: sort.Slice(pods, byCPUAndMemoryDescending) — a total order (Kubernetes UIDs are unique).  Inputs
+        // without UIDs (kp_pods_view.uids NULL) keep their input order on ties, as the device's stable radix passes do.
         const int n = (int)plist.size();
         std::vector<int> order(n);
         for (int i = 0; i < n; i++) order[i] = i;
-        std::sort(order.begin(), order.end(), [&](int a, int b) {
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
             const Pod& l = pod_at(a);
             const Pod& r = pod_at(b);
             if (l.req[cpu_axis] != r.req[cpu_axis]) return l.req[cpu_axis] > r.req[cpu_axis];

@@ -110,6 +110,53 @@ def test_fleet_pick_config5(golden):
             continue
         n_ok += 1
         t, row = pick
-        assert row in list(res.offerings(i)) and t in list(res.types(i))
+        rows = [int(x) for x in res.offerings(i)]
+        assert row in rows and t in list(res.types(i))
         assert flat[row].capacity_type == ct_name[int(res.rows[i]["capacity_type"])]
+        # the pick is the first override of minimal LowestPrice score (kwok/strategy/strategy.go:45-60)
+        scores = [_lowest_price_score(cat, r, int(res.rows[i]["capacity_type"]) == abi.KP_CT_SPOT) for r in rows]
+        k = rows.index(row)
+        assert scores[k] == min(scores)
+        assert all(s != scores[k] for s in scores[:k])
     assert n_ok > 0
+
+
+def _lowest_price_score(cat, row, spot):
+    """strategy.go LowestPrice score of an offering row: SpotPrice(type, zone) for spot fleets, OnDemandPrice(type)
+    otherwise, MaxFloat64 when the pricing provider has no price."""
+    from kpsim import launch
+    owner = [(t, o) for t, it in enumerate(cat) for o in it.offerings]
+    t, o = owner[row]
+    want = "spot" if spot else "on-demand"
+    for x in cat[t].offerings:
+        if x.capacity_type == want and (not spot or x.zone == o.zone):
+            return x.price
+    return launch.MAX_FLOAT64
+
+
+def _one_request_result(overrides, ct):
+    rows = np.zeros(1, abi.LAUNCH_DTYPE)
+    rows[0]["status"] = abi.KP_OK
+    rows[0]["capacity_type"] = ct
+    rows[0]["n_overrides"] = len(overrides)
+    return model.LaunchResults(rows, np.zeros(1, np.int32), np.array(overrides, np.int32))
+
+
+def test_fleet_pick_hand_cases():
+    """Hand-computed picks (kwok/ec2/ec2.go:432-461 + strategy.go:45-60): a spot price tie across zones keeps the
+    earlier override; a type without a spot price in that zone scores MaxFloat64 and loses to any priced override; an
+    on-demand fleet scores every zone of a type with the same OD price, so the first override of the cheapest type wins."""
+    from kpsim import launch
+    O = model.Offering
+    mk = lambda name, offs: model.InstanceType(name, {}, np.zeros(model.R, np.int64), np.zeros(model.R, np.int64), offs)  # noqa: E731
+    cat = [mk("a.large", [O("spot", "z1", 0.05, True), O("spot", "z2", 0.05, True), O("on-demand", "z1", 0.2, True)]),
+           mk("b.large", [O("on-demand", "z1", 0.1, True), O("on-demand", "z2", 0.1, True)]),
+           mk("c.large", [O("spot", "z3", 0.01, True)])]
+    # rows: a/z1-spot 0, a/z2-spot 1, a/z1-od 2, b/z1-od 3, b/z2-od 4, c/z3-spot 5
+    assert launch.fleet_pick(cat, _one_request_result([1, 0], abi.KP_CT_SPOT), 0) == (0, 1)   # tie: first listed
+    assert launch.fleet_pick(cat, _one_request_result([3, 0, 5], abi.KP_CT_SPOT), 0) == (2, 5)  # b has no spot price
+    assert launch.fleet_pick(cat, _one_request_result([3, 1], abi.KP_CT_SPOT), 0) == (0, 1)
+    assert launch.fleet_pick(cat, _one_request_result([2, 4, 3], abi.KP_CT_ON_DEMAND), 0) == (1, 4)
+    # c.large has no on-demand price: MaxFloat64 never beats a priced override, and only it → it is still picked
+    assert launch.fleet_pick(cat, _one_request_result([5, 3], abi.KP_CT_ON_DEMAND), 0) == (1, 3)
+    assert launch.fleet_pick(cat, _one_request_result([5], abi.KP_CT_ON_DEMAND), 0) == (2, 5)
