@@ -140,12 +140,42 @@ typedef struct kp_nodepool {
     const int32_t* type_index;
 } kp_nodepool;
 
-/* A pod class: pods that share scheduling constraints (podData.Requirements, tolerations). */
+/*
+ * Topology terms of a pod class: corev1.TopologySpreadConstraint and PodAffinityTerm as [core]
+ * scheduling/topology.go (newForTopologies / newForAffinities / updateInverseAntiAffinity) turns them into
+ * TopologyGroups (topologygroup.go).  Semantics restated in oracle/orc_solve.cpp (Topology) and DESIGN.md §4.
+ */
+enum { KP_TOPO_SPREAD = 0, KP_TOPO_AFFINITY = 1, KP_TOPO_ANTI_AFFINITY = 2 };
+enum { KP_POLICY_IGNORE = 0, KP_POLICY_HONOR = 1 };        /* corev1.NodeInclusionPolicy */
+enum { KP_DO_NOT_SCHEDULE = 0, KP_SCHEDULE_ANYWAY = 1 };   /* corev1.UnsatisfiableConstraintAction */
+typedef struct kp_topology_term {
+    int32_t type;                            /* KP_TOPO_* */
+    const char* topology_key;                /* e.g. topology.kubernetes.io/zone, kubernetes.io/hostname */
+    int32_t max_skew;                        /* spread */
+    int32_t min_domains;                     /* spread; <= 0: nil */
+    int32_t when_unsatisfiable;              /* spread: KP_DO_NOT_SCHEDULE, or KP_SCHEDULE_ANYWAY (a preference) */
+    int32_t node_affinity_policy;            /* spread: KP_POLICY_* (Kubernetes default Honor) */
+    int32_t node_taints_policy;              /* spread: KP_POLICY_* (Kubernetes default Ignore) */
+    int32_t weight;                          /* (anti-)affinity: 0 = requiredDuringScheduling, > 0 = preferred weight */
+    int32_t n_selector;                      /* LabelSelector over pod labels as requirements (matchLabels k=v → In [v];
+                                                matchExpressions In/NotIn/Exists/DoesNotExist); < 0: nil (selects nothing) */
+    const kp_requirement* selector;
+    int32_t n_namespaces;                    /* (anti-)affinity term namespaces; 0: the pod's own namespace */
+    const char* const* namespaces;
+} kp_topology_term;
+
+/* A pod class: pods that share scheduling constraints (podData.Requirements, tolerations, labels, topology). */
 typedef struct kp_pod_class {
     int32_t n_requirements;                  /* nodeSelector ∪ requiredDuringScheduling term[0] */
     const kp_requirement* requirements;
     int32_t n_tolerations;
     const kp_toleration* tolerations;
+    const char* namespace_name;              /* metadata.namespace (NULL: "default") */
+    int32_t n_labels;                        /* metadata.labels (topology selectors match these) */
+    const char* const* label_keys;
+    const char* const* label_values;
+    int32_t n_topology;
+    const kp_topology_term* topology;
 } kp_pod_class;
 
 typedef struct kp_pods_view {
@@ -178,6 +208,11 @@ typedef struct kp_solve_input {
     const kp_existing_node* existing;        /* in scheduling order (initialized first, core sorts stably) */
     int32_t max_instance_types;              /* 60 (instance.go:62); <= 0 disables truncation */
     int32_t min_values_policy;               /* KP_MIN_VALUES_* */
+    /* pods already bound to existing nodes: topology.go countDomains (spread / affinity counts) and
+       updateInverseAffinities (their required anti-affinity terms); pods being scheduled must not be listed */
+    int32_t n_bound;
+    const int32_t* bound_node;               /* [n_bound] index into existing */
+    const int32_t* bound_class;              /* [n_bound] index into classes (labels, namespace, terms) */
 } kp_solve_input;
 
 /* Per-solve counters: evaluation counts feed the algorithmic-bytes roofline. */
@@ -217,9 +252,18 @@ typedef struct kp_solve_output {
     kp_solve_stats stats;
 } kp_solve_output;
 
+/* core PREFERENCE_POLICY (website/content/en/preview/reference/settings.md:40) */
+enum { KP_PREFERENCE_RESPECT = 0, KP_PREFERENCE_IGNORE = 1 };
+
+/* Context options: devices and the solver parameters core reads from its operator options
+   (settings.md:13-42, pkg/operator/options/options.go:36-58). */
 typedef struct kp_device_opts {
-    int32_t device;                          /* HIP device ordinal */
-    int32_t reserved0;
+    int32_t device;                          /* HIP device ordinal (the ctx's primary device) */
+    int32_t n_devices;                       /* > 1: kp_consolidate shards probes over devices[0..n) */
+    const int32_t* devices;
+    int32_t preference_policy;               /* KP_PREFERENCE_*: Respect relaxes preferences (ScheduleAnyway spreads,
+                                                preferred affinities); Ignore drops them before scheduling */
+    int32_t reserved_capacity;               /* feature gate ReservedCapacity: reserved offerings join Solve */
 } kp_device_opts;
 
 typedef struct kp_ctx kp_ctx;

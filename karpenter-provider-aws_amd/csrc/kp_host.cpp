@@ -717,6 +717,8 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     if (in->min_values_policy != KP_MIN_VALUES_STRICT)
         return fail(ctx, KP_E_UNSUPPORTED, "MIN_VALUES_POLICY=BestEffort is not supported by this build");
     const int T = c->T, TW = c->TW, R = c->R, P = in->pods.n_pods, C = in->n_classes;
+    for (int i = 0; i < C; i++)
+        if (in->classes[i].n_topology > 0) return fail(ctx, KP_E_UNSUPPORTED, "topology terms (device path pending)");
     // ---- dictionaries: catalog ∪ solve strings ----
     c->sol = c->cat;
     std::vector<std::map<int, HReq>> creq(C);

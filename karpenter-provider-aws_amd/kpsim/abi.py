@@ -64,9 +64,24 @@ class kp_nodepool(C.Structure):
     ]
 
 
+KP_TOPO_SPREAD, KP_TOPO_AFFINITY, KP_TOPO_ANTI_AFFINITY = 0, 1, 2
+KP_POLICY_IGNORE, KP_POLICY_HONOR = 0, 1
+KP_DO_NOT_SCHEDULE, KP_SCHEDULE_ANYWAY = 0, 1
+KP_PREFERENCE_RESPECT, KP_PREFERENCE_IGNORE = 0, 1
+
+
+class kp_topology_term(C.Structure):
+    _fields_ = [("type", C.c_int32), ("topology_key", C.c_char_p), ("max_skew", C.c_int32), ("min_domains", C.c_int32),
+                ("when_unsatisfiable", C.c_int32), ("node_affinity_policy", C.c_int32),
+                ("node_taints_policy", C.c_int32), ("weight", C.c_int32), ("n_selector", C.c_int32),
+                ("selector", C.POINTER(kp_requirement)), ("n_namespaces", C.c_int32), ("namespaces", c_char_pp)]
+
+
 class kp_pod_class(C.Structure):
     _fields_ = [("n_requirements", C.c_int32), ("requirements", C.POINTER(kp_requirement)),
-                ("n_tolerations", C.c_int32), ("tolerations", C.POINTER(kp_toleration))]
+                ("n_tolerations", C.c_int32), ("tolerations", C.POINTER(kp_toleration)),
+                ("namespace_name", C.c_char_p), ("n_labels", C.c_int32), ("label_keys", c_char_pp),
+                ("label_values", c_char_pp), ("n_topology", C.c_int32), ("topology", C.POINTER(kp_topology_term))]
 
 
 class kp_pods_view(C.Structure):
@@ -85,7 +100,8 @@ class kp_solve_input(C.Structure):
                 ("n_classes", C.c_int32), ("classes", C.POINTER(kp_pod_class)),
                 ("pods", kp_pods_view),
                 ("n_existing", C.c_int32), ("existing", C.POINTER(kp_existing_node)),
-                ("max_instance_types", C.c_int32), ("min_values_policy", C.c_int32)]
+                ("max_instance_types", C.c_int32), ("min_values_policy", C.c_int32),
+                ("n_bound", C.c_int32), ("bound_node", c_int32_p), ("bound_class", c_int32_p)]
 
 
 class kp_solve_stats(C.Structure):
@@ -158,7 +174,8 @@ assert LAUNCH_DTYPE.itemsize == C.sizeof(kp_launch_result)
 
 
 class kp_device_opts(C.Structure):
-    _fields_ = [("device", C.c_int32), ("reserved0", C.c_int32)]
+    _fields_ = [("device", C.c_int32), ("n_devices", C.c_int32), ("devices", c_int32_p),
+                ("preference_policy", C.c_int32), ("reserved_capacity", C.c_int32)]
 
 
 # ------------------------------------------------------------------------------------------------
@@ -221,3 +238,31 @@ def toleration_array(keep, tols):
         arr[i].effect = (t.effect or "").encode()
     keep.hold(arr)
     return len(tols), arr
+
+
+def topology_array(keep, terms):
+    """terms: iterable of model.TopologyTerm -> (n, POINTER(kp_topology_term))"""
+    from kpsim.model import TOPO_KIND
+    terms = list(terms)
+    arr = (kp_topology_term * max(1, len(terms)))()
+    pol = {"Ignore": KP_POLICY_IGNORE, "Honor": KP_POLICY_HONOR}
+    for i, t in enumerate(terms):
+        x = arr[i]
+        x.type = TOPO_KIND[t.kind]
+        x.topology_key = t.key.encode()
+        x.max_skew = int(t.max_skew)
+        x.min_domains = int(t.min_domains) if t.min_domains else 0
+        x.when_unsatisfiable = KP_SCHEDULE_ANYWAY if t.when_unsatisfiable == "ScheduleAnyway" else KP_DO_NOT_SCHEDULE
+        x.node_affinity_policy = pol[t.node_affinity_policy]
+        x.node_taints_policy = pol[t.node_taints_policy]
+        x.weight = int(t.weight)
+        if t.selector is None:
+            x.n_selector = -1
+            x.selector = (kp_requirement * 1)()
+            keep.hold(x.selector)
+        else:
+            x.n_selector, x.selector = requirement_array(keep, t.selector)
+        x.n_namespaces = len(t.namespaces)
+        x.namespaces = keep.cstrs(list(t.namespaces))
+    keep.hold(arr)
+    return len(terms), arr

@@ -118,9 +118,32 @@ class NodePool:
 
 
 @dataclass
+class TopologyTerm:
+    """corev1.TopologySpreadConstraint (kind "spread") or a pod (anti-)affinity term (kind "affinity" / "anti"), as
+    [core] scheduling/topology.go reads them.  selector: LabelSelector as Requirements over pod labels (None = nil)."""
+    kind: str                                   # spread | affinity | anti
+    key: str                                    # topologyKey
+    selector: Optional[List[Requirement]] = field(default_factory=list)
+    max_skew: int = 1
+    min_domains: Optional[int] = None
+    when_unsatisfiable: str = "DoNotSchedule"   # | ScheduleAnyway
+    node_affinity_policy: str = "Honor"
+    node_taints_policy: str = "Ignore"
+    weight: int = 0                             # (anti-)affinity: 0 = required
+    namespaces: List[str] = field(default_factory=list)
+
+
+TOPO_KIND = {"spread": 0, "affinity": 1, "anti": 2}
+HOSTNAME = "kubernetes.io/hostname"
+
+
+@dataclass
 class PodClass:
     requirements: List[Requirement] = field(default_factory=list)
     tolerations: List[Toleration] = field(default_factory=list)
+    labels: Dict[str, str] = field(default_factory=dict)
+    namespace: str = "default"
+    topology: List[TopologyTerm] = field(default_factory=list)
 
 
 @dataclass
@@ -153,6 +176,7 @@ class Problem:
     existing: List[ExistingNode] = field(default_factory=list)
     max_instance_types: int = 60
     min_values_policy: int = 0
+    bound: List[tuple] = field(default_factory=list)   # (existing node, class) of pods already bound (topology counts)
 
 
 @dataclass
@@ -288,6 +312,11 @@ class SolveInputView:
         for i, pc in enumerate(prob.classes):
             cls[i].n_requirements, cls[i].requirements = abi.requirement_array(k, pc.requirements)
             cls[i].n_tolerations, cls[i].tolerations = abi.toleration_array(k, pc.tolerations)
+            cls[i].namespace_name = pc.namespace.encode()
+            cls[i].n_labels = len(pc.labels)
+            cls[i].label_keys = k.cstrs(list(pc.labels.keys()))
+            cls[i].label_values = k.cstrs(list(pc.labels.values()))
+            cls[i].n_topology, cls[i].topology = abi.topology_array(k, pc.topology)
         k.hold(cls)
         ex = (abi.kp_existing_node * max(1, len(prob.existing)))()
         for i, e in enumerate(prob.existing):
@@ -315,6 +344,11 @@ class SolveInputView:
         v.existing = ex
         v.max_instance_types = prob.max_instance_types
         v.min_values_policy = prob.min_values_policy
+        v.n_bound = len(prob.bound)
+        if prob.bound:
+            b = np.array(prob.bound, np.int32).reshape(-1, 2)
+            v.bound_node = k.ptr(b[:, 0].copy(), np.int32, C.c_int32)
+            v.bound_class = k.ptr(b[:, 1].copy(), np.int32, C.c_int32)
 
 
 @dataclass

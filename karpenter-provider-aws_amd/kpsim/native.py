@@ -67,11 +67,16 @@ def load():
 class Context:
     """One kp_ctx (device stream + buffers).  Not thread-safe; use one per thread."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, preference_policy=abi.KP_PREFERENCE_RESPECT, devices=None, reserved_capacity=1):
         L = load()
         self.L = L
         h = C.c_void_p()
-        opts = abi.kp_device_opts(device=device)
+        opts = abi.kp_device_opts(device=device, preference_policy=preference_policy, reserved_capacity=reserved_capacity)
+        if devices:
+            import numpy as np
+            self._devs = np.ascontiguousarray(devices, np.int32)
+            opts.n_devices = len(self._devs)
+            opts.devices = self._devs.ctypes.data_as(C.POINTER(C.c_int32))
         st = L.kp_ctx_create(C.byref(opts), C.byref(h))
         if st != 0:
             raise KpError(st, "kp_ctx_create(device=%d) — a gfx950 device is required" % device)

@@ -115,6 +115,59 @@ def config2(n_pods=50_000, n_classes=250, catalog=None, seed=SEED, deployments=T
     return Problem(catalog, nodepools, classes, pods)
 
 
+def config3_topology(rng, classes, zonal=0.40, hostname=0.20, anti=0.10):
+    """Give every class a Deployment label (app=class-N) and draw its topology terms independently: zonal spread
+    (maxSkew 1, DoNotSchedule), hostname spread (maxSkew 1) and required hostname anti-affinity, each selecting the
+    class's own pods (the Deployment pattern the reference's scale suite uses, test/suites/scale/provisioning_test.go:91-101)."""
+    for c, pc in enumerate(classes):
+        app = "class-%d" % c
+        pc.labels = {"app": app}
+        sel = [Requirement("app", "In", [app])]
+        if rng.random() < zonal:
+            pc.topology.append(model.TopologyTerm("spread", ZONE, list(sel), max_skew=1))
+        if rng.random() < hostname:
+            pc.topology.append(model.TopologyTerm("spread", model.HOSTNAME, list(sel), max_skew=1))
+        if rng.random() < anti:
+            pc.topology.append(model.TopologyTerm("anti", model.HOSTNAME, list(sel)))
+    return classes
+
+
+def config3_nodepools(taint_key="example.com/dedicated"):
+    """Five weighted NodePools (weights 100/80/50/20/0) with overlapping requirements and cpu limits
+    500 / 2000 / 5000 cores / none / none."""
+    AWS_ = AWS
+    return [
+        NodePool(name="np-100", weight=100, requirements=[Requirement(CAPACITY_TYPE, "In", ["on-demand"]),
+                                                         Requirement(AWS_ + "instance-category", "In", ["c", "m"])],
+                 limits_remaining={"cpu": 500 * 1000}),
+        NodePool(name="np-80", weight=80, requirements=[Requirement(CAPACITY_TYPE, "In", ["spot"]),
+                                                       Requirement(AWS_ + "instance-category", "In", ["m", "r"])],
+                 limits_remaining={"cpu": 2000 * 1000}),
+        NodePool(name="np-50", weight=50, requirements=[Requirement(CAPACITY_TYPE, "In", ["spot", "on-demand"]),
+                                                       Requirement(AWS_ + "instance-generation", "Gt", ["5"])],
+                 limits_remaining={"cpu": 5000 * 1000}),
+        NodePool(name="np-20", weight=20, requirements=[Requirement(CAPACITY_TYPE, "In", ["on-demand"])],
+                 taints=[Taint(taint_key, "", "NoSchedule")]),
+        default_nodepool("np-0", capacity_types=("spot", "on-demand"), weight=0),
+    ]
+
+
+def config3(n_pods=50_000, n_classes=250, catalog=None, seed=SEED) -> Problem:
+    """BASELINE configs[2]: config 2's pod mix with zonal + hostname topology spread and hostname anti-affinity
+    (config3_topology) over five weighted NodePools with limits (config3_nodepools)."""
+    rng = np.random.Generator(np.random.PCG64(seed + 3))
+    catalog = catalog if catalog is not None else golden_catalog(seed=seed)
+    taint_key = "example.com/dedicated"
+    classes, creqs = _classes_config2(rng, n_classes, taint_key)
+    config3_topology(rng, classes)
+    w = rng.dirichlet(np.ones(n_classes) * 0.8)
+    counts = rng.multinomial(n_pods, w)
+    specs = []
+    for c in rng.permutation(n_classes):
+        specs += [(int(c), creqs[c])] * int(counts[c])
+    return Problem(catalog, config3_nodepools(taint_key), classes, _pods_from_milli(specs))
+
+
 def _pods_from_milli(specs, t0=1_700_000_000 * 10 ** 9):
     n = len(specs)
     cls = np.array([c for c, _ in specs], np.int32)
@@ -139,7 +192,7 @@ def subsample(prob: Problem, n_pods: int, seed=SEED) -> Problem:
     idx = np.sort(np.random.Generator(np.random.PCG64(seed)).choice(p.n, size=min(n_pods, p.n), replace=False))
     pods = Pods(p.class_id[idx].copy(), p.requests[idx].copy(), p.creation_ns[idx].copy(), [p.uids[i] for i in idx])
     return Problem(prob.catalog, prob.nodepools, prob.classes, pods, prob.existing, prob.max_instance_types,
-                   prob.min_values_policy)
+                   prob.min_values_policy, list(prob.bound))
 
 
 # ------------------------------------------------------------------------------------------------

@@ -15,6 +15,9 @@ extern "C" {
 typedef struct orc_result orc_result;
 
 kp_status orc_solve(const kp_catalog_view* cat, const kp_solve_input* in, kp_solve_output* out, orc_result** res);
+/* orc_solve with the context's solver parameters (kp_device_opts.preference_policy); opts NULL = defaults */
+kp_status orc_solve_opts(const kp_catalog_view* cat, const kp_solve_input* in, const kp_device_opts* opts,
+                         kp_solve_output* out, orc_result** res);
 kp_status orc_result_nodeclaim_requirements(const orc_result* res, int32_t nc, char* buf, int64_t cap, int64_t* needed);
 void orc_result_free(orc_result* res);
 

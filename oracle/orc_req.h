@@ -136,10 +136,11 @@ struct Req {
     bool has_value(int v) const { return std::binary_search(values.begin(), values.end(), v); }
 };
 
-// withinIntPtrs(value, gt, lt)
+// withinIntPtrs(value, gt, lt).  Negative value ids are NodeClaim hostname placeholders
+// ("hostname-placeholder-NNNN", never an integer).
 inline bool within(const Dict& D, int key, int v, bool has_gt, int64_t gt, bool has_lt, int64_t lt) {
     if (!has_gt && !has_lt) return true;
-    if (!D.val_isint[key][v]) return false;
+    if (v < 0 || !D.val_isint[key][v]) return false;
     int64_t x = D.val_int[key][v];
     if (has_gt && gt >= x) return false;
     if (has_lt && lt <= x) return false;

@@ -84,9 +84,59 @@ static bool fits(const std::vector<int64_t>& candidate, const std::vector<int64_
     return true;
 }
 
+// metav1.LabelSelector over pod labels (labels.Selector semantics: In / NotIn / Exists / DoesNotExist)
+struct LabelSel {
+    bool nil = false;  // a nil selector selects nothing
+    struct Term {
+        std::string key;
+        int op = 0;
+        std::vector<std::string> values;
+    };
+    std::vector<Term> terms;
+    bool matches(const std::map<std::string, std::string>& labels) const {
+        if (nil) return false;
+        for (auto& t : terms) {
+            auto it = labels.find(t.key);
+            const bool present = it != labels.end();
+            const bool in = present && std::find(t.values.begin(), t.values.end(), it->second) != t.values.end();
+            if (t.op == KP_OP_IN && !in) return false;
+            if (t.op == KP_OP_NOT_IN && in) return false;
+            if (t.op == KP_OP_EXISTS && !present) return false;
+            if (t.op == KP_OP_DOES_NOT_EXIST && present) return false;
+        }
+        return true;
+    }
+};
+
+// One topology term of a pod class (kp_topology_term)
+struct TopoTerm {
+    int type = 0, key = -1, max_skew = 1, min_domains = -1, aff_pol = KP_POLICY_HONOR, taint_pol = KP_POLICY_IGNORE;
+    LabelSel sel;
+    std::vector<std::string> namespaces;
+};
+
 struct PodClass {
     Reqs reqs;
     std::vector<Toleration> tols;
+    std::string ns = "default";
+    std::map<std::string, std::string> labels;
+    std::vector<TopoTerm> terms;
+};
+
+// [core] scheduling/topologygroup.go TopologyGroup.  One group per (pod class, term): Go shares a group between pods
+// whose terms hash equal, but groups that share a hash count the same pods, so per-class groups decide identically.
+// `cnt` is the domains map (domain value id → count; emptyDomains = the domains with count 0, since counts only grow
+// within a Solve).  Hostname groups know every registered host implicitly (NewNodeClaim and NewExistingNode
+// Register their hostnames in every hostname group), so only recorded hosts are stored.
+struct TopoGroup {
+    int type = 0, key = -1;
+    bool host = false;
+    bool inverse = false;      // inverseTopologyGroups (updateInverseAntiAffinity): constrains the pods it selects
+    int owner = -1;            // class that owns the term
+    int max_skew = 0, min_domains = -1;
+    int aff_pol = KP_POLICY_IGNORE, taint_pol = KP_POLICY_IGNORE;  // TopologyNodeFilter (spread only)
+    std::vector<uint8_t> sel;  // per class: selects(pod) = namespace ∈ namespaces ∧ selector matches labels
+    std::map<int, int> cnt;
 };
 struct Pod {
     int cls = 0;
@@ -110,6 +160,7 @@ struct Template {
 struct NodeClaim {
     int id = 0;
     int tmpl = 0;
+    int host = 0;  // hostname-placeholder value id (negative)
     Reqs reqs;
     std::vector<int> options;
     std::vector<int64_t> requests;
@@ -122,6 +173,14 @@ struct ExistingNode {
     Reqs reqs;
     std::vector<Taint> taints;
     std::vector<int64_t> available, requests;
+    int host = 0;  // hostname value id
+};
+
+// A NodePool as buildDomainGroups sees it (every NodePool, also those whose options end up empty)
+struct PoolDomains {
+    Reqs reqs;
+    std::vector<Taint> taints;
+    std::vector<int> rows;
 };
 
 struct Result {
@@ -150,6 +209,9 @@ struct Solver {
     int placements = 0;
     int hostname_key = -1;
     Req host_req;                     // hostname In [placeholder] of a new NodeClaim (no pod can select it)
+    int next_host = 0;                // NewNodeClaim's hostname-placeholder counter (value id -2 - n)
+    std::vector<TopoGroup> groups;    // Topology.topologyGroups ∪ inverseTopologyGroups
+    std::vector<std::vector<int>> t_cons, t_rec;  // per class: groups that constrain / count its pods
     kp_solve_stats stats{};
 
     explicit Solver(Dict& d) : D(d) {}
@@ -202,6 +264,151 @@ struct Solver {
         return out;
     }
 
+    // ------------------------------------------------------------------------------------------------
+    // Topology ([core] scheduling/topology.go, topologygroup.go; recalled).  Go iterates maps when it
+    // picks a domain among equal counts (nextDomainTopologySpread's `count < minCount`, nextDomainAffinity's first
+    // match), so any tied domain is a valid Go outcome; this restatement (and the device) takes the smallest domain name.
+    // ------------------------------------------------------------------------------------------------
+    std::string dom_name(int key, int v) const {
+        if (v >= 0) return D.vals[key][v];
+        char b[48];
+        snprintf(b, sizeof b, "hostname-placeholder-%04d", -2 - v);
+        return b;
+    }
+    bool dom_less(int key, int a, int b) const { return dom_name(key, a) < dom_name(key, b); }
+    static int count_of(const TopoGroup& g, int d, bool& known) {
+        auto it = g.cnt.find(d);
+        if (it != g.cnt.end()) {
+            known = true;
+            return it->second;
+        }
+        known = g.host;  // every registered host is a known (empty) domain
+        return 0;
+    }
+    // domainMinCount(podDomains): hostname topologies have a min of 0; minDomains above the supported domain count → 0
+    int64_t domain_min_count(const TopoGroup& g, const Req& podDom) const {
+        if (g.host) return 0;
+        int64_t mn = INT32_MAX;
+        int num = 0;
+        for (auto& kv : g.cnt)
+            if (req_has(D, podDom, kv.first)) {
+                num++;
+                mn = std::min<int64_t>(mn, kv.second);
+            }
+        if (g.min_domains > 0 && num < g.min_domains) mn = 0;
+        return mn;
+    }
+    // TopologyGroup.Get(pod, podDomains, nodeDomains) → the allowed domains (an In requirement; empty = DoesNotExist)
+    Req topo_get(const TopoGroup& g, int cls, const Req& podDom, const Req& nodeDom) const {
+        Req out;
+        out.key = g.key;
+        out.complement = false;
+        // the domains examined: nodeDomains' values on the In path, else every known domain in nodeDomains.  (A
+        // hostname nodeDomains is always In [the node's host]: NodeClaims and existing nodes carry hostname In [name].)
+        std::vector<int> cand;
+        const bool in_path = nodeDom.Operator() == OP_IN;
+        if (in_path) {
+            cand = nodeDom.values;
+        } else {
+            for (auto& kv : g.cnt)
+                if (req_has(D, nodeDom, kv.first)) cand.push_back(kv.first);
+        }
+        if (g.type == KP_TOPO_SPREAD) {  // nextDomainTopologySpread
+            const int64_t mn = domain_min_count(g, podDom);
+            const int self = g.sel[cls];
+            int best = 0;
+            int64_t bc = INT32_MAX;
+            bool found = false;
+            for (int d : cand) {
+                bool known;
+                const int64_t c = (int64_t)count_of(g, d, known) + self;
+                if (!known) continue;
+                if (c - mn <= g.max_skew && (c < bc || (c == bc && found && dom_less(g.key, d, best)))) {
+                    best = d;
+                    bc = c;
+                    found = true;
+                }
+            }
+            if (found) out.values.push_back(best);
+            return out;
+        }
+        if (g.type == KP_TOPO_ANTI_AFFINITY) {  // nextDomainAntiAffinity: empty domains the pod and node allow
+            for (int d : cand) {
+                bool known;
+                const int c = count_of(g, d, known);
+                if (known && c == 0 && req_has(D, podDom, d)) out.values.push_back(d);
+            }
+            std::sort(out.values.begin(), out.values.end());
+            return out;
+        }
+        // nextDomainAffinity: domains the pod allows that hold a selected pod; a self-selecting pod with none
+        // bootstraps a domain (first one compatible with the node domains, else any the pod allows)
+        std::vector<int> known_doms;
+        for (auto& kv : g.cnt) known_doms.push_back(kv.first);
+        if (g.host && in_path)
+            for (int d : nodeDom.values)
+                if (!g.cnt.count(d)) known_doms.push_back(d);
+        for (int d : known_doms) {
+            bool k;
+            if (count_of(g, d, k) > 0 && req_has(D, podDom, d)) out.values.push_back(d);
+        }
+        if (out.values.empty() && g.sel[cls]) {
+            int pick = 0;
+            bool found = false;
+            for (int pass = 0; pass < 2 && !found; pass++)
+                for (int d : known_doms)
+                    if (req_has(D, podDom, d) && (pass == 1 || req_has(D, nodeDom, d)) &&
+                        (!found || dom_less(g.key, d, pick))) {
+                        pick = d;
+                        found = true;
+                    }
+            if (found) out.values.push_back(pick);
+        }
+        std::sort(out.values.begin(), out.values.end());
+        return out;
+    }
+    // Topology.AddRequirements + NodeClaim.Add's Compatible(nodeClaimRequirements, topologyRequirements) + Add:
+    // every group that constrains the pod contributes its domains computed from the same nodeRequirements.
+    bool topo_add(int li, Reqs& r, bool allow_wk) const {
+        const int c = pod_at(li).cls;
+        if (t_cons.empty() || t_cons[c].empty()) return true;
+        const PodClass& pc = (*cp)[c];
+        Reqs topo = r;
+        for (int gi : t_cons[c]) {
+            const TopoGroup& g = groups[gi];
+            const Req podDom = pc.reqs.get(g.key);  // Exists when the pod does not constrain the key
+            const Req nodeDom = r.get(g.key);
+            const Req dom = topo_get(g, c, podDom, nodeDom);
+            if (dom.Len() == 0) return false;  // topologyError
+            topo.add(D, dom);
+        }
+        if (!reqs_compatible(D, r, topo, allow_wk)) return false;
+        r.add_all(D, topo);
+        return true;
+    }
+    // Topology.Record(pod, taints, requirements): every group whose Counts(pod) holds records the domain(s) the pod
+    // lands in; inverse groups owned by the pod record every value of the requirement.
+    void topo_record(int li, const Reqs& r, const std::vector<Taint>& taints, bool allow_wk) {
+        const int c = pod_at(li).cls;
+        if (t_rec.empty()) return;
+        for (int gi : t_rec[c]) {
+            TopoGroup& g = groups[gi];
+            const Req dom = r.get(g.key);
+            if (!g.inverse) {
+                if (g.type == KP_TOPO_SPREAD) {  // TopologyNodeFilter.Matches
+                    const PodClass& fc = (*cp)[g.owner];
+                    if (g.aff_pol == KP_POLICY_HONOR && !reqs_compatible(D, r, fc.reqs, allow_wk)) continue;
+                    if (g.taint_pol == KP_POLICY_HONOR && !tolerates_all(taints, fc.tols)) continue;
+                }
+                if (g.type != KP_TOPO_ANTI_AFFINITY) {  // the domain is recorded only once it is a single value
+                    if (!dom.complement && dom.values.size() == 1) g.cnt[dom.values[0]]++;
+                    continue;
+                }
+            }
+            for (int v : dom.values) g.cnt[v]++;  // Values(): the excluded set of a complement
+        }
+    }
+
     bool nodeclaim_add(NodeClaim& nc, int li) {
         const Pod& pod = pod_at(li);
         const PodClass& pc = cls_of(li);
@@ -210,8 +417,7 @@ struct Solver {
         Reqs r = nc.reqs;
         if (!reqs_compatible(D, r, pc.reqs, true)) return false;
         r.add_all(D, pc.reqs);
-        // topology.AddRequirements: no topology groups in this build's inputs → the requirements themselves;
-        // Compatible(r, r) always holds and Add(r) is idempotent.
+        if (!topo_add(li, r, true)) return false;  // topology.AddRequirements
         std::vector<int64_t> requests(R);
         for (int k = 0; k < R; k++) requests[k] = nc.requests[k] + pod.req[k];
         std::vector<int> remaining = filter(nc.options, r, requests);
@@ -220,11 +426,12 @@ struct Solver {
         nc.options.swap(remaining);
         nc.requests.swap(requests);
         nc.reqs = std::move(r);
+        topo_record(li, nc.reqs, tm.taints, true);
         return true;
     }
 
     // ExistingNode.Add: Taints.ToleratesPod, Fits(requests + pod, available), Compatible (no undefined-label
-    // allowance), then requirements.Add.  On success `out` is the updated node.
+    // allowance), then requirements.Add and topology.  On success `out` is the updated node (the caller records it).
     bool existing_try(const ExistingNode& n, int li, ExistingNode& out) {
         const Pod& pod = pod_at(li);
         const PodClass& pc = cls_of(li);
@@ -235,8 +442,10 @@ struct Solver {
         Reqs r = n.reqs;
         if (!reqs_compatible(D, r, pc.reqs, false)) return false;
         r.add_all(D, pc.reqs);
+        if (!topo_add(li, r, false)) return false;
         out.taints = n.taints;
         out.available = n.available;
+        out.host = n.host;
         out.requests.swap(requests);
         out.reqs = std::move(r);
         return true;
@@ -259,6 +468,7 @@ struct Solver {
             const ExistingNode& n = it != ex_mod.end() ? it->second : (*ex_base)[j];
             ExistingNode upd;
             if (existing_try(n, li, upd)) {
+                topo_record(li, upd.reqs, upd.taints, false);
                 ex_mod[j] = std::move(upd);
                 pod_result[li] = KP_POD_EXISTING(j);
                 return true;
@@ -290,7 +500,10 @@ struct Solver {
             nc.id = (int)ncs.size();
             nc.tmpl = (int)ti;
             nc.reqs = tm.reqs;
-            nc.reqs.add(D, host_req);
+            nc.host = -2 - next_host++;  // hostname-placeholder-%04d (registered in every hostname group)
+            Req hr = host_req;
+            hr.values = {nc.host};
+            nc.reqs.add(D, hr);
             nc.options = its;
             nc.requests = tm.daemon;
             stats.template_evals++;
@@ -414,8 +627,11 @@ struct orc_result {
     Dict D;
 };
 
-// Input views → NewScheduler state (catalog rows, classes, pods, NodeClaimTemplates in weight order, existing nodes).
-static kp_status parse_into(Solver& s, const kp_catalog_view* cat, const kp_solve_input* in) {
+// Input views → NewScheduler state (catalog rows, classes, pods, NodeClaimTemplates in weight order, existing nodes),
+// then NewTopology (domain groups, topology groups, counts of the bound pods).
+static kp_status build_topology(Solver& s, const kp_solve_input* in, const std::vector<PoolDomains>& pools);
+
+static kp_status parse_into(Solver& s, const kp_catalog_view* cat, const kp_solve_input* in, int pref_policy) {
     Dict& D = s.D;
     const int T = cat->n_types, R = cat->n_resources;
     s.R = R;
@@ -468,14 +684,50 @@ static kp_status parse_into(Solver& s, const kp_catalog_view* cat, const kp_solv
     s.own_classes.resize(in->n_classes);
     for (int c = 0; c < in->n_classes; c++) {
         const kp_pod_class& pc = in->classes[c];
-        if (!build_reqs(D, pc.requirements, pc.n_requirements, s.own_classes[c].reqs)) return KP_E_INVALID;
+        PodClass& oc = s.own_classes[c];
+        if (!build_reqs(D, pc.requirements, pc.n_requirements, oc.reqs)) return KP_E_INVALID;
         for (int i = 0; i < pc.n_tolerations; i++) {
             Toleration t;
             t.key = pc.tolerations[i].key ? pc.tolerations[i].key : "";
             t.op = pc.tolerations[i].op;
             t.value = pc.tolerations[i].value ? pc.tolerations[i].value : "";
             t.effect = pc.tolerations[i].effect ? pc.tolerations[i].effect : "";
-            s.own_classes[c].tols.push_back(t);
+            oc.tols.push_back(t);
+        }
+        if (pc.namespace_name) oc.ns = pc.namespace_name;
+        for (int l = 0; l < pc.n_labels; l++)
+            oc.labels[pc.label_keys[l] ? pc.label_keys[l] : ""] = pc.label_values[l] ? pc.label_values[l] : "";
+        for (int i = 0; i < pc.n_topology; i++) {
+            const kp_topology_term& x = pc.topology[i];
+            if (x.type < KP_TOPO_SPREAD || x.type > KP_TOPO_ANTI_AFFINITY || !x.topology_key) return KP_E_INVALID;
+            const bool preferred = x.type == KP_TOPO_SPREAD ? x.when_unsatisfiable == KP_SCHEDULE_ANYWAY : x.weight > 0;
+            if (preferred) {
+                // PREFERENCE_POLICY=Ignore drops preferences; Respect relaxes them on failure (preferences.go), which
+                // this restatement does not implement
+                if (pref_policy == KP_PREFERENCE_IGNORE) continue;
+                return KP_E_UNSUPPORTED;
+            }
+            TopoTerm t;
+            t.type = x.type;
+            t.key = D.key(normalize_label(x.topology_key));
+            t.max_skew = x.type == KP_TOPO_SPREAD ? x.max_skew : INT32_MAX;
+            if (x.type == KP_TOPO_SPREAD && x.max_skew <= 0) return KP_E_INVALID;
+            t.min_domains = x.type == KP_TOPO_SPREAD && x.min_domains > 0 ? x.min_domains : -1;
+            t.aff_pol = x.type == KP_TOPO_SPREAD ? x.node_affinity_policy : KP_POLICY_IGNORE;
+            t.taint_pol = x.type == KP_TOPO_SPREAD ? x.node_taints_policy : KP_POLICY_IGNORE;
+            t.sel.nil = x.n_selector < 0;
+            for (int j = 0; j < x.n_selector; j++) {
+                const kp_requirement& q = x.selector[j];
+                if (!q.key || q.op < KP_OP_IN || q.op > KP_OP_DOES_NOT_EXIST) return KP_E_INVALID;
+                LabelSel::Term st;
+                st.key = q.key;
+                st.op = q.op;
+                st.values = strs(q.values, q.n_values);
+                t.sel.terms.push_back(st);
+            }
+            if (x.type == KP_TOPO_SPREAD || x.n_namespaces <= 0) t.namespaces = {oc.ns};
+            else t.namespaces = strs(x.namespaces, x.n_namespaces);
+            oc.terms.push_back(t);
         }
     }
     // pods
@@ -498,6 +750,7 @@ static kp_status parse_into(Solver& s, const kp_catalog_view* cat, const kp_solv
         if (x.weight != y.weight) return x.weight > y.weight;
         return strcmp(x.name, y.name) < 0;
     });
+    std::vector<PoolDomains> pools(in->n_nodepools);
     for (int i : npo) {
         const kp_nodepool& np = in->nodepools[i];
         Template tm;
@@ -508,6 +761,8 @@ static kp_status parse_into(Solver& s, const kp_catalog_view* cat, const kp_solv
         for (int j = 0; j < np.n_taints; j++)
             tm.taints.push_back({np.taints[j].key ? np.taints[j].key : "", np.taints[j].value ? np.taints[j].value : "",
                                  np.taints[j].effect ? np.taints[j].effect : ""});
+        pools[i].reqs = tm.reqs;
+        pools[i].taints = tm.taints;
         tm.daemon.assign(R, 0);
         if (np.daemon_overhead) tm.daemon.assign(np.daemon_overhead, np.daemon_overhead + R);
         tm.limit_set.assign(R, 0);
@@ -522,6 +777,7 @@ static kp_status parse_into(Solver& s, const kp_catalog_view* cat, const kp_solv
         } else {
             for (int j = 0; j < np.n_types; j++) rows.push_back(np.type_index[j]);
         }
+        pools[i].rows = rows;
         // NewScheduler: nct.InstanceTypeOptions = filterInstanceTypesByRequirements(its, nct.Requirements, {}, {}, {})
         std::vector<int64_t> zero(R, 0);
         // Fits({}, alloc) only rejects negative allocatable; emulate with an all-zero request
@@ -538,6 +794,7 @@ static kp_status parse_into(Solver& s, const kp_catalog_view* cat, const kp_solv
             n.reqs.add(D, new_req(D, k, OP_IN, {en.label_values[l]}, false, 0));
         }
         n.reqs.add(D, new_req(D, s.hostname_key, OP_IN, {en.name ? en.name : ""}, false, 0));
+        n.host = D.value(s.hostname_key, en.name ? en.name : "");
         for (int l = 0; l < en.n_taints; l++)
             n.taints.push_back({en.taints[l].key ? en.taints[l].key : "", en.taints[l].value ? en.taints[l].value : "",
                                 en.taints[l].effect ? en.taints[l].effect : ""});
@@ -546,16 +803,122 @@ static kp_status parse_into(Solver& s, const kp_catalog_view* cat, const kp_solv
         if (en.requests) n.requests.assign(en.requests, en.requests + R);
         s.own_existing.push_back(std::move(n));
     }
+    return build_topology(s, in, pools);
+}
+
+// NewTopology: buildDomainGroups over every NodePool × its instance types, one forward group per topology term of a
+// class (newForTopologies / newForAffinities) and one inverse group per required anti-affinity term
+// (updateInverseAntiAffinity), then countDomains over the bound pods and the bound pods' inverse anti-affinities.
+static kp_status build_topology(Solver& s, const kp_solve_input* in, const std::vector<PoolDomains>& pools) {
+    Dict& D = s.D;
+    const int C = (int)s.own_classes.size();
+    bool any = false;
+    for (auto& pc : s.own_classes) any = any || !pc.terms.empty();
+    if (!any) return KP_OK;
+    // buildDomainGroups: key → domain → taint sets of the NodePools that offer it
+    std::map<int, std::map<int, std::vector<int>>> dg;  // key → domain → pools
+    auto domains_of = [&](int key) -> const std::map<int, std::vector<int>>& {
+        auto it = dg.find(key);
+        if (it != dg.end()) return it->second;
+        std::map<int, std::vector<int>>& m = dg[key];
+        for (int p = 0; p < (int)pools.size(); p++) {
+            const PoolDomains& pd = pools[p];
+            for (int t : pd.rows) {
+                // requirements = NodePool requirements (+ template labels), Add(it.Requirements)
+                const InstanceType& it = s.ty(t);
+                const bool hp = pd.reqs.has(key), ht = it.reqs.has(key);
+                if (!hp && !ht) continue;
+                Req x = hp && ht ? req_intersection(D, it.reqs.m.at(key), pd.reqs.m.at(key)) : (hp ? pd.reqs.m.at(key) : it.reqs.m.at(key));
+                for (int v : x.values) m[v].push_back(p);  // requirement.Values()
+            }
+            if (pd.reqs.has(key) && pd.reqs.m.at(key).Operator() == OP_IN)
+                for (int v : pd.reqs.m.at(key).values) m[v].push_back(p);
+        }
+        return m;
+    };
+    auto tolerated_domain = [&](const std::vector<int>& ps, int cls) {  // ForEachDomain with NodeTaintsPolicy Honor
+        for (int p : ps)
+            if (tolerates_all(pools[p].taints, s.own_classes[cls].tols)) return true;
+        return false;
+    };
+    for (int c = 0; c < C; c++) {
+        const PodClass& pc = s.own_classes[c];
+        for (const TopoTerm& t : pc.terms) {
+            for (int inv = 0; inv < 2; inv++) {
+                if (inv && t.type != KP_TOPO_ANTI_AFFINITY) break;
+                TopoGroup g;
+                g.type = t.type;
+                g.key = t.key;
+                g.host = t.key == s.hostname_key;
+                g.inverse = inv == 1;
+                g.owner = c;
+                g.max_skew = t.max_skew;
+                g.min_domains = t.min_domains;
+                g.aff_pol = t.aff_pol;
+                g.taint_pol = t.taint_pol;
+                g.sel.assign(C, 0);
+                for (int o = 0; o < C; o++) {
+                    const PodClass& q = s.own_classes[o];
+                    g.sel[o] = std::find(t.namespaces.begin(), t.namespaces.end(), q.ns) != t.namespaces.end() &&
+                               t.sel.matches(q.labels);
+                }
+                if (!g.host)
+                    for (auto& kv : domains_of(t.key))
+                        if (t.type != KP_TOPO_SPREAD || t.taint_pol != KP_POLICY_HONOR || tolerated_domain(kv.second, c))
+                            g.cnt[kv.first] = 0;
+                s.groups.push_back(std::move(g));
+            }
+        }
+    }
+    s.t_cons.assign(C, {});
+    s.t_rec.assign(C, {});
+    for (int gi = 0; gi < (int)s.groups.size(); gi++) {
+        const TopoGroup& g = s.groups[gi];
+        for (int c = 0; c < C; c++) {
+            if (g.inverse) {
+                if (g.sel[c]) s.t_cons[c].push_back(gi);  // getMatchingTopologies: inverse groups that select the pod
+                if (g.owner == c) s.t_rec[c].push_back(gi);
+            } else {
+                if (g.owner == c) s.t_cons[c].push_back(gi);
+                if (g.sel[c]) s.t_rec[c].push_back(gi);
+            }
+        }
+    }
+    // bound pods: countDomains (forward groups; node filter against the node's labels and taints) and the inverse
+    // anti-affinity of bound pods (recorded at their node's domain)
+    const int E = (int)s.own_existing.size();
+    for (int i = 0; i < in->n_bound; i++) {
+        const int j = in->bound_node[i], b = in->bound_class[i];
+        if (j < 0 || j >= E || b < 0 || b >= C) return KP_E_INVALID;
+        const ExistingNode& n = s.own_existing[j];
+        for (TopoGroup& g : s.groups) {
+            if (g.inverse ? g.owner != b : !g.sel[b]) continue;
+            if (!g.inverse && g.type == KP_TOPO_SPREAD) {
+                const PodClass& fc = s.own_classes[g.owner];
+                if (g.aff_pol == KP_POLICY_HONOR && !reqs_compatible(D, n.reqs, fc.reqs, false)) continue;
+                if (g.taint_pol == KP_POLICY_HONOR && !tolerates_all(n.taints, fc.tols)) continue;
+            }
+            int dom;
+            if (g.host) {
+                dom = n.host;
+            } else {
+                auto it = n.reqs.m.find(g.key);
+                if (it == n.reqs.m.end() || it->second.complement || it->second.values.size() != 1) continue;  // unlabeled
+                dom = it->second.values[0];
+            }
+            g.cnt[dom]++;
+        }
+    }
     return KP_OK;
 }
 
-extern "C" kp_status orc_solve(const kp_catalog_view* cat, const kp_solve_input* in, kp_solve_output* out,
-                               orc_result** res_out) {
+extern "C" kp_status orc_solve_opts(const kp_catalog_view* cat, const kp_solve_input* in, const kp_device_opts* opts,
+                                    kp_solve_output* out, orc_result** res_out) {
     if (!cat || !in || !out) return KP_E_INVALID;
     if (in->min_values_policy != KP_MIN_VALUES_STRICT) return KP_E_UNSUPPORTED;
     auto res = std::make_unique<orc_result>();
     Solver s(res->D);
-    kp_status st = parse_into(s, cat, in);
+    kp_status st = parse_into(s, cat, in, opts ? opts->preference_policy : KP_PREFERENCE_RESPECT);
     if (st != KP_OK) return st;
     for (int j = 0; j < (int)s.own_existing.size(); j++) s.ex_idx.push_back(j);
     const kp_pods_view& pv = in->pods;
@@ -595,6 +958,11 @@ extern "C" kp_status orc_solve(const kp_catalog_view* cat, const kp_solve_input*
         *res_out = res.release();
     }
     return KP_OK;
+}
+
+extern "C" kp_status orc_solve(const kp_catalog_view* cat, const kp_solve_input* in, kp_solve_output* out,
+                               orc_result** res_out) {
+    return orc_solve_opts(cat, in, nullptr, out, res_out);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -778,8 +1146,11 @@ extern "C" kp_status orc_consolidate(const kp_catalog_view* cat, const kp_consol
     if (in->mode != KP_CONSOLIDATE_SINGLE && in->mode != KP_CONSOLIDATE_MULTI) return KP_E_INVALID;
     Dict D;
     Solver base(D);
-    kp_status st = parse_into(base, cat, &in->cluster);
+    kp_status st = parse_into(base, cat, &in->cluster, KP_PREFERENCE_RESPECT);
     if (st != KP_OK) return st;
+    // consolidation over topology-constrained pods (topology counts of the remaining cluster, excluded candidate pods)
+    // is not restated yet
+    if (!base.groups.empty()) return KP_E_UNSUPPORTED;
     const int E = (int)base.own_existing.size(), P = (int)base.own_pods.size();
     for (int i = 0; i < in->n_pending; i++)
         if (in->pending[i] < 0 || in->pending[i] >= P) return KP_E_INVALID;

@@ -28,6 +28,10 @@ def lib():
         _lib.orc_solve.argtypes = [C.POINTER(abi.kp_catalog_view), C.POINTER(abi.kp_solve_input),
                                    C.POINTER(abi.kp_solve_output), C.POINTER(C.c_void_p)]
         _lib.orc_solve.restype = C.c_int32
+        _lib.orc_solve_opts.argtypes = [C.POINTER(abi.kp_catalog_view), C.POINTER(abi.kp_solve_input),
+                                        C.POINTER(abi.kp_device_opts), C.POINTER(abi.kp_solve_output),
+                                        C.POINTER(C.c_void_p)]
+        _lib.orc_solve_opts.restype = C.c_int32
         _lib.orc_result_nodeclaim_requirements.argtypes = [C.c_void_p, C.c_int32, C.c_char_p, C.c_int64,
                                                            C.POINTER(C.c_int64)]
         _lib.orc_result_nodeclaim_requirements.restype = C.c_int32
@@ -123,16 +127,17 @@ class OracleResult:
             self._h = None
 
 
-def solve(problem, catalog_view=None):
-    """Run the CPU oracle on a kpsim.model.Problem.  Returns OracleResult."""
-    from kpsim import model
+def solve(problem, catalog_view=None, preference_policy=0):
+    """Run the CPU oracle on a kpsim.model.Problem (solver parameters as kp_device_opts).  Returns OracleResult."""
+    from kpsim import abi, model
     L = lib()
+    opts = abi.kp_device_opts(preference_policy=preference_policy)
     cv = catalog_view or model.CatalogView(problem.catalog)
     iv = model.SolveInputView(problem)
     cap_nc = max(16, problem.pods.n + 1)
     ob = model.OutputBuffers(problem.pods.n, cap_nc, cap_nc * max(1, problem.max_instance_types or len(problem.catalog)))
     h = C.c_void_p()
-    st = L.orc_solve(C.byref(cv.view), C.byref(iv.view), C.byref(ob.view), C.byref(h))
+    st = L.orc_solve_opts(C.byref(cv.view), C.byref(iv.view), C.byref(opts), C.byref(ob.view), C.byref(h))
     if st != 0:
         raise RuntimeError("orc_solve failed: %d" % st)
     return OracleResult(ob.results(), h)
