@@ -420,6 +420,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 a.compat = true;
                 a.force_off = false;
                 a.prof = nullptr;
+                a.host = 0;
                 st_nc++;
                 if (eval_wave(d, Ev, S.CC, a, S.ws, lane)) {
                     if (lane < S.CC.nck) {
@@ -449,6 +450,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     a.compat = true;
                     a.force_off = false;
                     a.prof = nullptr;
+                    a.host = 0;
                     st_tmpl++;
                     if (!eval_wave(d, Ev, S.CC, a, S.ws, lane)) continue;
                     if (n_nc == 1) {  // a second NodeClaim: computeConsolidation returns NONE

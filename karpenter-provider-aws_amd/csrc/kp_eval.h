@@ -29,6 +29,8 @@ struct WaveScratch {
     uint64_t opts[KP_TW_MAX];
     uint64_t minbits[KP_MAX_MIN_WORDS];
     int32_t hr[KP_LDS_AXES];   // quick-accept headroom of the chosen witness type (scaled, lower bound)
+    int32_t memo_ok;           // a failed evaluation may be memoised for the shape (it did not depend on topology
+                               // counts: see topo_narrow)
 };
 
 // Class-side operands of the evaluation, cached in LDS while consecutive pods share a class.
@@ -51,6 +53,12 @@ struct ClassCache {
     uint64_t words[KP_MAX_SCR_WORDS];
     uint64_t V[KP_TW_MAX];
     uint64_t dne[KP_MAX_CLASS_KEYS][KP_TW_MAX];
+    uint32_t kneutral;          // class keys present only for topology narrowing (bit per class-key index)
+    int ntc, ntr;               // topology groups constraining / recording the class
+    int tc[KP_MAX_TOPO];        // group | self << 30
+    int tc_ki[KP_MAX_TOPO];     // class-key index of a value-keyed group's key (-1 for hostname groups)
+    int tr[KP_MAX_TOPO_REC];
+    int tr_ki[KP_MAX_TOPO_REC]; // class-key index of the group's key, -1 when the class does not constrain it
 };
 
 // Offering-role keys (zone, capacity-type, zone-id, reservation-id, reservation-type) of the solve.
@@ -103,6 +111,12 @@ __device__ inline void fill_class_cache(const KpDev& d, int c, ClassCache& CC, i
         CC.nck = nck;
         CC.tol = c < d.C ? d.tol[c] : 0xFFFFFFFFu;
         CC.flags = d.cls_flags[c];
+        uint32_t kn = 0;
+        if (d.cls_kneutral)
+            for (int i = 0; i < nck; i++) kn |= d.cls_kneutral[k0 + i] ? (1u << i) : 0u;
+        CC.kneutral = kn;
+        CC.ntc = (c < d.C && d.G > 0) ? d.cls_tcoff[c + 1] - d.cls_tcoff[c] : 0;
+        CC.ntr = (c < d.C && d.G > 0) ? d.cls_troff[c + 1] - d.cls_troff[c] : 0;
     }
     __syncthreads();
     if (tid < 5) {
@@ -111,6 +125,23 @@ __device__ inline void fill_class_cache(const KpDev& d, int c, ClassCache& CC, i
         for (int i = 0; i < nck; i++)
             if (CC.key[i] == rk && rk >= 0) idx = i;
         CC.role[tid] = idx;
+    }
+    // topology group lists with the class-key index of each group's key
+    if (tid < CC.ntc + CC.ntr) {
+        const bool cons = tid < CC.ntc;
+        const int e = cons ? d.cls_tc[d.cls_tcoff[c] + tid] : d.cls_tr[d.cls_troff[c] + tid - CC.ntc];
+        const int4 info = d.tg_info[e & 0x3FFFFFFF];
+        int ki = -1;
+        if (!(info.x & TG_HOST))
+            for (int i = 0; i < nck; i++)
+                if (CC.key[i] == info.y) ki = i;
+        if (cons) {
+            CC.tc[tid] = e;
+            CC.tc_ki[tid] = ki;
+        } else {
+            CC.tr[tid - CC.ntc] = e;
+            CC.tr_ki[tid - CC.ntc] = ki;
+        }
     }
     __syncthreads();
 }
@@ -235,7 +266,200 @@ struct EvalIn {
     bool compat;              // taints + Requirements.Compatible
     bool force_off;           // always apply the offering test (template filter)
     long long* prof;          // LDS stage-cycle counters (diagnostics) or null
+    int host;                 // topology hostname domain of the candidate (E + NodeClaim id)
 };
+
+__device__ __forceinline__ int ld_i32(const int32_t* p) {
+    return __hip_atomic_load(const_cast<int32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_u64(const uint64_t* p) {
+    return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint32_t y = __shfl_xor(x, o);
+        x = y < x ? y : x;
+    }
+    return x;
+}
+__device__ __forceinline__ int wave_min_i32(int x) {
+    for (int o = 32; o >= 1; o >>= 1) {
+        const int y = __shfl_xor(x, o);
+        x = y < x ? y : x;
+    }
+    return x;
+}
+
+// Topology.AddRequirements ([core] scheduling/topology.go) for one candidate, after the requirement merge: every group
+// that constrains the pod's class yields its allowed domains (TopologyGroup.Get: nextDomainTopologySpread /
+// nextDomainAffinity / nextDomainAntiAffinity), all computed from the same merged requirements (nodeDomains) and
+// intersected per key, then Compatible(nodeClaimRequirements, topologyRequirements) and Add narrow the scratch.
+// Value-keyed groups: lane v examines value id v of the key (<= 64 values).  Go picks among equal counts by map
+// iteration order; the smallest value name (vrank) is the canonical choice (oracle/orc_solve.cpp topo_get).
+// Hostname groups: the candidate's own host is the only domain its requirements allow (hostname In [host]).
+// ws.memo_ok is cleared when the outcome depends on counts (a count check failed or a key was narrowed).
+__device__ __forceinline__ bool topo_narrow(const KpDev& d, const ClassCache& CC, WaveScratch& ws, int host, bool allow_wk,
+                                         int lane) {
+    int nk = 0;
+    int kidx[KP_MAX_TOPO];
+    uint64_t kmask[KP_MAX_TOPO];
+    for (int e = 0; e < CC.ntc; e++) {
+        const int g = CC.tc[e] & 0x3FFFFFFF, self = (CC.tc[e] >> 30) & 1, ki = CC.tc_ki[e];
+        const int4 info = d.tg_info[g];
+        const int type = info.x & TG_TYPE;
+        if (info.x & TG_HOST) {
+            const int cnt = ld_i32(&d.tg_hcnt[(size_t)d.tg_hrow[g] * d.HN + host]);
+            bool ok;
+            if (type == 0) ok = cnt + self <= info.z;             // spread: hostname domainMinCount is 0
+            else if (type == 2) ok = cnt == 0;                    // anti-affinity: an empty domain
+            else ok = cnt > 0 || (self && ld_i32(&d.tg_pos[g]) == 0);  // affinity (self-selecting bootstrap)
+            if (!ok) {
+                ws.memo_ok = 0;
+                return false;
+            }
+            continue;
+        }
+        const int k = info.y;
+        const bool valid = lane < CC.nval[ki];
+        const uint64_t known = ld_u64(&d.tg_known[g]);
+        const bool kn = valid && ((known >> lane) & 1ull);
+        const int cnt = kn ? ld_i32(&d.tg_cnt[(size_t)g * 64 + lane]) : 0;
+        const bool pod_has = valid && req_has(d, k, lane, CC.hdr[ki], CC.words + CC.wsoff[ki]);
+        const ReqHdr nh = ws.hdr[ki];
+        const bool node_has = valid && (!(nh.flags & RF_DEF) || req_has(d, k, lane, nh, ws.words + CC.wsoff[ki]));
+        const uint32_t rk = valid ? d.vrank[(size_t)k * 64 + lane] : 0xFFu;
+        uint64_t mask = 0;
+        if (type == 0) {  // nextDomainTopologySpread: min count over the pod's domains, then the least-loaded node domain
+            const uint64_t sup = ballot(kn && pod_has);
+            int mn = wave_min_i32((kn && pod_has) ? cnt : INT32_MAX);
+            if (info.w > 0 && __popcll(sup) < info.w) mn = 0;
+            const int64_t c = (int64_t)cnt + self;
+            const bool el = kn && node_has && c - (int64_t)mn <= (int64_t)info.z;
+            const uint32_t key = el ? ((uint32_t)c << 8) | rk : 0xFFFFFFFFu;
+            const uint32_t best = wave_min_u32(key);
+            mask = best == 0xFFFFFFFFu ? 0ull : ballot(el && key == best);
+        } else if (type == 2) {  // nextDomainAntiAffinity: empty domains allowed by pod and node
+            mask = ballot(kn && cnt == 0 && pod_has && node_has);
+        } else {  // nextDomainAffinity
+            mask = ballot(kn && cnt > 0 && pod_has);
+            if (!mask && self) {
+                for (int pass = 0; pass < 2 && !mask; pass++) {
+                    const bool c = kn && pod_has && (pass == 1 || node_has);
+                    const uint32_t best = wave_min_u32(c ? rk : 0xFFFFFFFFu);
+                    if (best != 0xFFFFFFFFu) mask = ballot(c && rk == best);
+                }
+            }
+        }
+        if (!mask) {
+            ws.memo_ok = 0;
+            return false;
+        }
+        int j = 0;
+        while (j < nk && kidx[j] != ki) j++;
+        if (j == nk) {
+            kidx[nk] = ki;
+            kmask[nk] = ~0ull;
+            nk++;
+        }
+        kmask[j] &= mask;
+    }
+    // Compatible(r, topo) + Add: r[k] ∩ In[mask]
+    bool fail = false, changed = false;
+    for (int j = 0; j < nk; j++) {
+        const int ki = kidx[j], k = CC.key[ki];
+        if (lane == 0) {
+            const ReqHdr A = ws.hdr[ki];
+            uint64_t* aw = ws.words + CC.wsoff[ki];
+            if (!(A.flags & RF_DEF)) {
+                // undefined on the node: topo's In needs AllowUndefinedWellKnownLabels (an empty topo is DoesNotExist)
+                if (kmask[j] != 0 && !(allow_wk && (CC.kflags[ki] & KF_WELL_KNOWN))) fail = true;
+                ReqHdr o{};
+                o.flags = RF_DEF;
+                ws.hdr[ki] = o;
+                aw[0] = kmask[j];
+                changed = true;
+            } else {
+                ReqHdr B{};
+                B.flags = RF_DEF;
+                const uint64_t bw = kmask[j];
+                ReqHdr O;
+                uint64_t ow;
+                const int cnt = req_intersect(d, k, A, aw, B, &bw, O, &ow);
+                if (cnt == 0 && !op_notin_or_dne(req_op(A.flags, popc_words(aw, 1)))) fail = true;
+                changed |= O.flags != A.flags || ow != aw[0];
+                ws.hdr[ki] = O;
+                aw[0] = ow;
+            }
+        }
+    }
+    fail = __shfl(fail ? 1 : 0, 0) != 0;
+    changed = __shfl(changed ? 1 : 0, 0) != 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (changed || fail) ws.memo_ok = 0;
+    return !fail;
+}
+
+// Topology.Record for a committed placement (one wave).  The merged requirements are ws for the class's keys and the
+// candidate's base digest (Ahdr / Aw) for the others; `host` is its hostname domain and `tmpl` its template (taints).
+// Counts(pod): forward groups selecting the class, through the spread node filter (owner's requirements with the
+// AllowUndefinedWellKnownLabels option when allow_wk, owner's tolerations); spread / affinity record a single-valued
+// domain, anti-affinity and inverse groups record every value (requirement.Values(), the excluded set of a complement).
+__device__ inline bool topo_filter_compatible(const KpDev& d, const ClassCache& CC, const WaveScratch& ws,
+                                              const ReqHdr* Ahdr, const uint64_t* Aw, int owner, bool allow_wk, int lane) {
+    bool ok = true;
+    for (int i = d.cls_xkoff[owner] + lane; i < d.cls_xkoff[owner + 1]; i += 64) {
+        const int k = d.cls_xkeys[i];
+        const ReqHdr B = d.cls_hdr[(size_t)owner * d.K + k];
+        const uint64_t* bw = d.cls_words + (size_t)owner * d.DW + d.woff[k];
+        const bool bno = op_notin_or_dne(req_op(B.flags, popc_words(bw, d.nw[k])));
+        if (k == d.key_host) {  // NodeClaim hostname In [placeholder]: only a complement without bounds admits it
+            if (!((B.flags & RF_CMP) && !(B.flags & (RF_GT | RF_LT)))) ok = false;
+            continue;
+        }
+        int ci = -1;
+        for (int q = 0; q < CC.nck; q++)
+            if (CC.key[q] == k) ci = q;
+        const ReqHdr A = ci >= 0 ? ws.hdr[ci] : Ahdr[k];
+        const uint64_t* aw = ci >= 0 ? ws.words + CC.wsoff[ci] : Aw + d.woff[k];
+        if (!(A.flags & RF_DEF)) {
+            if (!bno && !(allow_wk && (d.kflags[k] & KF_WELL_KNOWN))) ok = false;
+            continue;
+        }
+        if (req_intersect_empty(d, k, A, aw, B, bw) && !(bno && op_notin_or_dne(req_op(A.flags, popc_words(aw, d.nw[k])))))
+            ok = false;
+    }
+    return ballot(!ok) == 0;
+}
+
+__device__ __forceinline__ void topo_record(const KpDev& d, const ClassCache& CC, const WaveScratch& ws, const ReqHdr* Ahdr,
+                                         const uint64_t* Aw, int host, int tmpl, bool allow_wk, int lane) {
+    for (int e = 0; e < CC.ntr; e++) {
+        const int g = CC.tr[e], ki = CC.tr_ki[e];
+        const int4 info = d.tg_info[g];
+        const int type = info.x & TG_TYPE;
+        const bool inv = info.x & TG_INVERSE;
+        if (!inv && type == 0) {  // TopologyNodeFilter.Matches
+            const int pol = d.tg_pol[g], owner = d.tg_owner[g];
+            if ((pol & 2) && !((d.tol[owner] >> tmpl) & 1u)) continue;
+            if ((pol & 1) && owner != CC.cls && !topo_filter_compatible(d, CC, ws, Ahdr, Aw, owner, allow_wk, lane)) continue;
+        }
+        if (info.x & TG_HOST) {
+            if (lane == 0) {
+                const int old = atomicAdd(&d.tg_hcnt[(size_t)d.tg_hrow[g] * d.HN + host], 1);
+                if (old == 0) atomicAdd(&d.tg_pos[g], 1);
+            }
+            continue;
+        }
+        const int k = info.y;
+        const ReqHdr h = ki >= 0 ? ws.hdr[ki] : Ahdr[k];
+        const uint64_t w = ki >= 0 ? ws.words[CC.wsoff[ki]] : ld_u64(Aw + d.woff[k]);
+        if (!(h.flags & RF_DEF)) continue;  // Get() of an undefined key is Exists: no values
+        if (!inv && type != 2 && ((h.flags & RF_CMP) || __popcll(w) != 1)) continue;
+        if ((w >> lane) & 1ull) atomicAdd(&d.tg_cnt[(size_t)g * 64 + lane], 1);
+        if (lane == 0 && w) atomicOr((unsigned long long*)&d.tg_known[g], (unsigned long long)w);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 #define EV_STAMP(slot)                                                           \
     do {                                                                         \
         if (a.prof) {                                                            \
@@ -258,6 +482,7 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
     bool fail = false, kill = false;
     uint64_t adm = ~0ull;
     int kmul = -1;
+    ws.memo_ok = 1;
     if (lane < nck) {
         const int k = CC.key[lane];
         const int n = CC.nw[lane];
@@ -267,24 +492,37 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         const uint64_t* bw = CC.words + CC.wsoff[lane];
         uint64_t* ow = ws.words + CC.wsoff[lane];
         ReqHdr O;
-        int cnt;
         const int nb = CC.nbB[lane];
-        if (!(A.flags & RF_DEF)) {
+        if ((CC.kneutral >> lane) & 1u) {
+            // key present only for topology: the pod does not constrain it, the merge keeps the base requirement
+            O = A;
+            for (int i = 0; i < n; i++) ow[i] = (A.flags & RF_DEF) ? aw[i] : 0ull;
+        } else if (!(A.flags & RF_DEF)) {
             if (a.compat && !op_notin_or_dne(req_op(B.flags, nb)) && !(CC.kflags[lane] & KF_WELL_KNOWN)) fail = true;
             O = B;
             for (int i = 0; i < n; i++) ow[i] = bw[i];
-            cnt = nb;
         } else {
-            cnt = req_intersect(d, k, A, aw, B, bw, O, ow);
+            const int cnt = req_intersect(d, k, A, aw, B, bw, O, ow);
             if (a.compat && !(O.flags & RF_CMP) && cnt == 0) {
                 const int na = popc_words(aw, n);
                 if (!(op_notin_or_dne(req_op(B.flags, nb)) && op_notin_or_dne(req_op(A.flags, na)))) fail = true;
             }
         }
         ws.hdr[lane] = O;
+    }
+    if (ballot(fail)) return false;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (CC.flags & CF_TOPO_CONS) {
+        if (!topo_narrow(d, CC, ws, a.host, a.compat, lane)) return false;
+    }
+    if (lane < nck) {
+        const int k = CC.key[lane];
+        const ReqHdr O = ws.hdr[lane];
+        const uint64_t* ow = ws.words + CC.wsoff[lane];
         const uint32_t kf = CC.kflags[lane];
-        if (kf & (KF_CAT_SINGLE | KF_CAT_MULTI)) kill = !op_notin_or_dne(req_op(O.flags, cnt));
-        if (kf & KF_CAT_MULTI) {
+        if ((kf & (KF_CAT_SINGLE | KF_CAT_MULTI)) && (O.flags & RF_DEF))
+            kill = !op_notin_or_dne(req_op(O.flags, popc_words(ow, CC.nw[lane])));
+        if ((kf & KF_CAT_MULTI) && (O.flags & RF_DEF)) {
             kmul = CC.kmulti[lane];
             adm = 0;
             const int nv = CC.nval[lane] < 64 ? CC.nval[lane] : 64;
@@ -292,7 +530,6 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
                 if (req_has(d, k, v, O, ow)) adm |= 1ull << v;
         }
     }
-    if (ballot(fail)) return false;
     EV_STAMP(0);
 
     // ---- options ∧ V[class] ∧ ¬DoesNotExist-types of keys whose merged operator is In/Exists ----

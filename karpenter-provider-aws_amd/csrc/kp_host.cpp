@@ -193,6 +193,8 @@ struct kp_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
+    int pref_policy = KP_PREFERENCE_RESPECT;  // kp_device_opts solver parameters
+    int reserved_capacity = 1;
     // catalog (host copies)
     bool have_catalog = false;
     uint64_t epoch = 0;
@@ -206,6 +208,8 @@ struct kp_ctx {
     std::vector<int> off_type, off_slot;     // per offering row
     std::vector<double> slot_price;          // [T][KP_MAX_SLOTS]
     std::vector<int32_t> slot_zone, slot_ct, slot_zoneid;
+    std::vector<uint64_t> h_multi_mask;      // [n_multi][T] value masks of the multi-valued keys (topology domains)
+    std::vector<uint8_t> h_multi_state;      // [n_multi][T] KP_LABEL_* of those keys
     int key_zone = -1, key_ct = -1, key_zoneid = -1, key_resvid = -1, key_resvtype = -1;
     // catalog device tables
     DBuf<uint16_t> d_type_val, d_multi16;
@@ -276,6 +280,13 @@ struct kp_ctx {
     DBuf<uint64_t> d_l_words;
     DBuf<int64_t> d_l_rq;
     double launch_ms[2] = {};                // launch kernel, whole call
+    // topology (kp_solve_prepare encodes the groups; execute resets the counts from the *0 copies)
+    int tg_G = 0, tg_HG = 0;
+    DBuf<int4> d_tg_info;
+    DBuf<int32_t> d_tg_hrow, d_tg_owner, d_tg_pol, d_tg_cnt0, d_tg_cnt, d_tg_hcnt0, d_tg_hcnt, d_tg_pos0, d_tg_pos,
+        d_cls_tcoff, d_cls_tc, d_cls_troff, d_cls_tr;
+    DBuf<uint64_t> d_tg_known0, d_tg_known;
+    DBuf<uint8_t> d_cls_kneutral, d_vrank;
     // last results (host)
     int last_N = 0, M = 0;
     std::vector<int32_t> h_nc_tmpl;
@@ -302,6 +313,12 @@ extern "C" kp_status kp_ctx_create(const kp_device_opts* opts, kp_ctx** out) try
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return KP_E_DEVICE;
     auto ctx = std::make_unique<kp_ctx>();
     ctx->device = opts ? opts->device : 0;
+    if (opts) {
+        if (opts->preference_policy != KP_PREFERENCE_RESPECT && opts->preference_policy != KP_PREFERENCE_IGNORE)
+            return KP_E_INVALID;
+        ctx->pref_policy = opts->preference_policy;
+        ctx->reserved_capacity = opts->reserved_capacity ? 1 : 0;
+    }
     if (ctx->device < 0 || ctx->device >= n) return KP_E_DEVICE;
     if (hipSetDevice(ctx->device) != hipSuccess) return KP_E_DEVICE;
     hipDeviceProp_t prop;
@@ -505,6 +522,7 @@ extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, ui
     const int TW = c->TW;
     std::vector<uint16_t> tval((size_t)Kc * T, VAL_ABSENT);
     std::vector<uint64_t> mmask((size_t)std::max(1, c->n_multi) * T, 0), dne((size_t)Kc * TW, 0);
+    c->h_multi_state.assign((size_t)std::max(1, c->n_multi) * T, KP_LABEL_ABSENT);
     for (int k = 0; k < Kc; k++) {
         for (int t = 0; t < T; t++) {
             const int8_t s = st[(size_t)t * Kc + k];
@@ -518,6 +536,7 @@ extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, ui
                 if (s == KP_LABEL_IN)
                     for (int id : tv[(size_t)t * Kc + k]) m |= 1ull << id;
                 mmask[(size_t)c->cat_multi[k] * T + t] = m;
+                c->h_multi_state[(size_t)c->cat_multi[k] * T + t] = (uint8_t)s;
             }
         }
     }
@@ -540,6 +559,7 @@ extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, ui
     for (int i = 0; i < T; i++) {
         rank[idx[i]] = (i > 0 && c->type_names[idx[i]] == c->type_names[idx[i - 1]]) ? rank[idx[i - 1]] : (uint32_t)i;
     }
+    c->h_multi_mask = mmask;
     hipStream_t s = c->stream;
     HIPCHK(c->d_type_val.upload(tval, s));
     HIPCHK(c->d_multi_mask.upload(mmask, s));
@@ -702,6 +722,130 @@ static bool tolerates(const kp_taint& taint, const kp_toleration* tols, int n) {
     return false;
 }
 
+// ---------------------------------------------------------------------------------------------
+// topology encoding ([core] scheduling/topology.go NewTopology, topologygroup.go)
+// ---------------------------------------------------------------------------------------------
+namespace {
+struct HGroup {
+    int type = 0, key = -1, owner = -1, skew = 0, mindom = 0, pol = 0, hrow = -1;
+    bool host = false, inverse = false;
+    std::vector<uint8_t> sel;  // per class: namespace ∈ namespaces ∧ the label selector matches
+};
+struct TopoHost {
+    std::vector<HGroup> g;
+    std::vector<std::vector<int>> cons, rec;  // per class: constraining groups (| self << 30), recording groups
+    std::vector<std::vector<int>> neutral;    // per class: keys added to its digest only for narrowing
+    int key_host = -1;
+    int n_host = 0;
+};
+
+// labels.Selector over pod labels (metav1.LabelSelector: matchLabels as In, matchExpressions In/NotIn/Exists/DNE)
+bool selector_matches(const kp_topology_term& t, const kp_pod_class& pc) {
+    if (t.n_selector < 0) return false;  // nil selector
+    for (int i = 0; i < t.n_selector; i++) {
+        const kp_requirement& q = t.selector[i];
+        const char* v = nullptr;
+        for (int l = 0; l < pc.n_labels; l++)
+            if (pc.label_keys[l] && !strcmp(pc.label_keys[l], q.key)) v = pc.label_values[l] ? pc.label_values[l] : "";
+        bool in = false;
+        for (int j = 0; v && j < q.n_values; j++) in = in || !strcmp(q.values[j] ? q.values[j] : "", v);
+        if ((q.op == KP_OP_IN && !in) || (q.op == KP_OP_NOT_IN && in) || (q.op == KP_OP_EXISTS && !v) ||
+            (q.op == KP_OP_DOES_NOT_EXIST && v))
+            return false;
+    }
+    return true;
+}
+const char* ns_of(const kp_pod_class& pc) { return pc.namespace_name ? pc.namespace_name : "default"; }
+}  // namespace
+
+// One forward group per (class, term) and one inverse group per required anti-affinity term (per-class groups decide
+// exactly like Go's hash-shared ones: groups that share a hash count the same pods).  Interns the topology keys.
+static kp_status topo_build(kp_ctx* c, const kp_solve_input* in, const std::vector<std::map<int, HReq>>& creq,
+                            TopoHost& th, std::string& err) {
+    const int C = in->n_classes;
+    th = TopoHost();
+    th.cons.assign(C, {});
+    th.rec.assign(C, {});
+    th.neutral.assign(C, {});
+    for (int i = 0; i < C; i++) {
+        const kp_pod_class& pc = in->classes[i];
+        for (int q = 0; q < pc.n_topology; q++) {
+            const kp_topology_term& x = pc.topology[q];
+            if (x.type < KP_TOPO_SPREAD || x.type > KP_TOPO_ANTI_AFFINITY || !x.topology_key) {
+                err = "bad topology term";
+                return KP_E_INVALID;
+            }
+            const bool preferred = x.type == KP_TOPO_SPREAD ? x.when_unsatisfiable == KP_SCHEDULE_ANYWAY : x.weight > 0;
+            if (preferred) {
+                if (c->pref_policy == KP_PREFERENCE_IGNORE) continue;  // PREFERENCE_POLICY=Ignore drops preferences
+                err = "preferred topology terms need preference relaxation (PREFERENCE_POLICY=Respect), not supported";
+                return KP_E_UNSUPPORTED;
+            }
+            if (x.type == KP_TOPO_SPREAD && x.max_skew <= 0) {
+                err = "maxSkew must be positive";
+                return KP_E_INVALID;
+            }
+            for (int j = 0; j < x.n_selector; j++)
+                if (!x.selector[j].key || x.selector[j].op < KP_OP_IN || x.selector[j].op > KP_OP_DOES_NOT_EXIST) {
+                    err = "label selector operators are In / NotIn / Exists / DoesNotExist";
+                    return KP_E_INVALID;
+                }
+            const int key = c->sol.key(normalize(x.topology_key));
+            for (int inv = 0; inv < 2; inv++) {
+                if (inv && x.type != KP_TOPO_ANTI_AFFINITY) break;
+                HGroup g;
+                g.type = x.type;
+                g.key = key;
+                g.inverse = inv == 1;
+                g.owner = i;
+                g.skew = x.type == KP_TOPO_SPREAD ? x.max_skew : INT32_MAX;
+                g.mindom = x.type == KP_TOPO_SPREAD && x.min_domains > 0 ? x.min_domains : 0;
+                if (x.type == KP_TOPO_SPREAD)
+                    g.pol = (x.node_affinity_policy == KP_POLICY_HONOR ? 1 : 0) | (x.node_taints_policy == KP_POLICY_HONOR ? 2 : 0);
+                g.sel.assign(C, 0);
+                for (int o = 0; o < C; o++) {
+                    const kp_pod_class& oc = in->classes[o];
+                    bool ns_ok = false;
+                    if (x.type == KP_TOPO_SPREAD || x.n_namespaces <= 0) ns_ok = !strcmp(ns_of(oc), ns_of(pc));
+                    else
+                        for (int n = 0; n < x.n_namespaces; n++) ns_ok = ns_ok || (x.namespaces[n] && !strcmp(x.namespaces[n], ns_of(oc)));
+                    g.sel[o] = ns_ok && selector_matches(x, oc);
+                }
+                th.g.push_back(std::move(g));
+            }
+        }
+    }
+    if (th.g.empty()) return KP_OK;
+    th.key_host = c->sol.key("kubernetes.io/hostname");
+    for (int gi = 0; gi < (int)th.g.size(); gi++) {
+        HGroup& g = th.g[gi];
+        g.host = g.key == th.key_host;
+        if (g.host) g.hrow = th.n_host++;
+        for (int o = 0; o < C; o++) {
+            if (g.inverse) {
+                if (g.sel[o]) th.cons[o].push_back(gi | (g.sel[o] << 30));
+                if (g.owner == o) th.rec[o].push_back(gi);
+            } else {
+                if (g.owner == o) th.cons[o].push_back(gi | (g.sel[o] << 30));
+                if (g.sel[o]) th.rec[o].push_back(gi);
+            }
+        }
+    }
+    for (int o = 0; o < C; o++) {
+        if (th.cons[o].size() > KP_MAX_TOPO || th.rec[o].size() > KP_MAX_TOPO_REC) {
+            err = "a pod class is constrained or counted by too many topology groups";
+            return KP_E_UNSUPPORTED;
+        }
+        for (int e : th.cons[o]) {
+            const HGroup& g = th.g[e & 0x3FFFFFFF];
+            if (!g.host && !creq[o].count(g.key) &&
+                std::find(th.neutral[o].begin(), th.neutral[o].end(), g.key) == th.neutral[o].end())
+                th.neutral[o].push_back(g.key);
+        }
+    }
+    return KP_OK;
+}
+
 extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try {
     if (!ctx || !in) return KP_E_INVALID;
     ctx->cons_prep_valid = false;
@@ -717,8 +861,6 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     if (in->min_values_policy != KP_MIN_VALUES_STRICT)
         return fail(ctx, KP_E_UNSUPPORTED, "MIN_VALUES_POLICY=BestEffort is not supported by this build");
     const int T = c->T, TW = c->TW, R = c->R, P = in->pods.n_pods, C = in->n_classes;
-    for (int i = 0; i < C; i++)
-        if (in->classes[i].n_topology > 0) return fail(ctx, KP_E_UNSUPPORTED, "topology terms (device path pending)");
     // ---- dictionaries: catalog ∪ solve strings ----
     c->sol = c->cat;
     std::vector<std::map<int, HReq>> creq(C);
@@ -743,6 +885,13 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     for (int i = 0; i < C; i++)
         for (auto& kv : creq[i])
             if (kv.second.has_min) return fail(ctx, KP_E_INVALID, "pod requirements cannot carry minValues");
+    TopoHost th;
+    {
+        const kp_status ts = topo_build(c, in, creq, th, err);
+        if (ts != KP_OK) return fail(ctx, ts, err);
+        if (!th.g.empty() && in->n_existing > 0)
+            return fail(ctx, KP_E_UNSUPPORTED, "topology with existing nodes (device path pending)");
+    }
     // existing nodes (ExistingNode, [core] scheduling/existingnode.go NewExistingNode): requirements =
     // NewLabelRequirements(node labels) + hostname In [name].  Only label keys some pod class constrains can
     // influence Compatible (it iterates the pod's keys), so only those are interned.
@@ -811,11 +960,20 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         if ((kflags[k] & KF_CAT_MULTI) && nval[k] > 64)
             return fail(ctx, KP_E_UNSUPPORTED, "multi-valued label with > 64 values after adding pod values");
     }
+    // topology keys the device narrows per value: multi-valued catalog labels (zone, capacity-type, zone-id, ...) and
+    // labels no instance type carries, each with at most 64 values; hostname is handled per host
+    for (const HGroup& g : th.g) {
+        if (g.host) continue;
+        if ((kflags[g.key] & KF_CAT_SINGLE) || nval[g.key] > 64)
+            return fail(ctx, KP_E_UNSUPPORTED, "topology key " + c->sol.keys[g.key].name +
+                                                   ": single-valued instance-type labels or > 64 values are not supported");
+    }
     // ---- class digests: pod classes then templates ----
     const int CT = C + NT;
     std::vector<ReqHdr> chdr((size_t)CT * K);
     std::vector<uint64_t> cwords((size_t)CT * DW, 0);
     std::vector<int32_t> koff(CT + 1, 0), ckeys, cwsoff;
+    std::vector<uint8_t> ckneu;  // parallel to ckeys: key added for topology narrowing only
     std::vector<uint32_t> cflags(CT, 0);
     std::vector<int32_t> min_keys((size_t)NT * KP_MAX_CLASS_KEYS, -1);
     std::vector<int32_t> xkoff(C + 1, 0), xkeys;
@@ -845,13 +1003,32 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
             }
             nk++;
             ckeys.push_back(q.key);
+            ckneu.push_back(0);
             cwsoff.push_back(so);
             so += nw[q.key];
             if (q.key == c->key_zone || q.key == c->key_ct || q.key == c->key_zoneid || q.key == c->key_resvid ||
                 q.key == c->key_resvtype)
-                cflags[row] |= 1u;
+                cflags[row] |= CF_OFFERING;
         }
-        if (nk == 0) cflags[row] |= 4u;  // no requirement keys: NodeClaim.Add = tolerations + Fits (+ minValues)
+        if (row < C && !th.g.empty()) {
+            // keys the class's topology groups narrow (AddRequirements adds zone In [domain] even when the pod does
+            // not constrain the zone): carried as Exists, skipped by Compatible, merged as the base requirement
+            for (int k : th.neutral[row]) {
+                ReqHdr h{};
+                h.flags = RF_DEF | RF_CMP;
+                chdr[(size_t)row * K + k] = h;
+                nk++;
+                ckeys.push_back(k);
+                ckneu.push_back(1);
+                cwsoff.push_back(so);
+                so += nw[k];
+                if (k == c->key_zone || k == c->key_ct || k == c->key_zoneid || k == c->key_resvid || k == c->key_resvtype)
+                    cflags[row] |= CF_OFFERING;
+            }
+            if (!th.cons[row].empty() || !th.rec[row].empty()) cflags[row] |= CF_TOPO;
+            if (!th.cons[row].empty()) cflags[row] |= CF_TOPO_CONS;
+        }
+        if (nk == 0) cflags[row] |= CF_NOKEYS;  // no requirement keys: NodeClaim.Add = tolerations + Fits (+ minValues)
         if (nk > KP_MAX_CLASS_KEYS || so > KP_MAX_SCR_WORDS) return false;
         koff[row + 1] = (int)ckeys.size();
         if (row < C) xkoff[row + 1] = (int)xkeys.size();
@@ -1016,7 +1193,9 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     if (ckeys.empty()) {
         ckeys.push_back(0);
         cwsoff.push_back(0);
+        ckneu.push_back(0);
     }
+    HIPCHK(c->d_cls_kneutral.upload(ckneu, s));
     HIPCHK(c->d_cls_keys.upload(ckeys, s));
     HIPCHK(c->d_cls_wsoff.upload(cwsoff, s));
     HIPCHK(c->d_cls_hdr.upload(chdr, s));
@@ -1075,6 +1254,115 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     const int M = in->max_instance_types > 0 ? std::min(in->max_instance_types, T) : T;
     HIPCHK(c->d_nc_types.ensure((size_t)NCcap * M));
     HIPCHK(c->d_stats.ensure(ST_COUNT));
+    // ---- topology: groups, initial domains (buildDomainGroups), per-class group lists, tie-break ranks ----
+    const int G = (int)th.g.size();
+    c->tg_G = G;
+    c->tg_HG = th.n_host;
+    {
+        const int G1 = std::max(G, 1);
+        std::vector<int4> tinfo(G1);
+        std::vector<int32_t> thr_row(G1, -1), towner(G1, 0), tpol(G1, 0), tcnt0((size_t)G1 * 64, 0), tpos0(G1, 0);
+        std::vector<uint64_t> tknown0(G1, 0);
+        std::vector<int32_t> tcoff(C + 1, 0), tcl, troff(C + 1, 0), trl;
+        std::vector<uint8_t> vrank((size_t)K * 64, 0xFF);
+        if (G > 0) {
+            auto hreq_has = [&](const HReq& q, int v) {
+                const bool in = std::binary_search(q.vals.begin(), q.vals.end(), v);
+                if (!q.complement) return in;
+                if (in) return false;
+                if (!q.has_gt && !q.has_lt) return true;
+                int64_t x = 0;
+                if (!go_atoi(c->sol.keys[q.key].vals[v].c_str(), x)) return false;
+                return !((q.has_gt && q.gt >= x) || (q.has_lt && q.lt <= x));
+            };
+            // buildDomainGroups: value → the NodePools (templates) offering it, over every NodePool × its types
+            std::map<int, std::map<int, std::vector<int>>> dg;
+            auto domains_of = [&](int k) -> const std::map<int, std::vector<int>>& {
+                auto it = dg.find(k);
+                if (it != dg.end()) return it->second;
+                std::map<int, std::vector<int>>& m = dg[k];
+                const int mi = k < c->Kcat ? c->cat_multi[k] : -1;
+                for (int j = 0; j < NT; j++) {
+                    auto npit = treq[j].find(k);
+                    const bool hp = npit != treq[j].end();
+                    for (int t = 0; t < T; t++) {
+                        if (!((rows[(size_t)j * TW + t / 64] >> (t % 64)) & 1ull)) continue;
+                        const int st = mi >= 0 ? c->h_multi_state[(size_t)mi * T + t] : KP_LABEL_ABSENT;
+                        const bool ht = st != KP_LABEL_ABSENT;
+                        if (!hp && !ht) continue;
+                        const uint64_t tm = st == KP_LABEL_IN ? c->h_multi_mask[(size_t)mi * T + t] : 0ull;
+                        if (hp && ht) {
+                            for (uint64_t x = tm; x; x &= x - 1) {
+                                const int v = __builtin_ctzll(x);
+                                if (hreq_has(npit->second, v)) m[v].push_back(j);
+                            }
+                        } else if (hp) {
+                            for (int v : npit->second.vals) m[v].push_back(j);  // requirement.Values()
+                        } else {
+                            for (uint64_t x = tm; x; x &= x - 1) m[__builtin_ctzll(x)].push_back(j);
+                        }
+                    }
+                    if (hp && !npit->second.complement && !npit->second.vals.empty())  // NodePool In requirements
+                        for (int v : npit->second.vals) m[v].push_back(j);
+                }
+                return m;
+            };
+            auto owner_tolerates = [&](int owner, int j) {
+                const kp_nodepool& np = in->nodepools[npo[j]];
+                for (int q = 0; q < np.n_taints; q++)
+                    if (!tolerates(np.taints[q], in->classes[owner].tolerations, in->classes[owner].n_tolerations)) return false;
+                return true;
+            };
+            for (int gi = 0; gi < G; gi++) {
+                const HGroup& g = th.g[gi];
+                tinfo[gi] = make_int4(g.type | (g.inverse ? TG_INVERSE : 0) | (g.host ? TG_HOST : 0), g.key, g.skew, g.mindom);
+                thr_row[gi] = g.hrow;
+                towner[gi] = g.owner;
+                tpol[gi] = g.pol;
+                if (g.host) continue;
+                for (auto& kv : domains_of(g.key)) {
+                    bool ok = !(g.type == KP_TOPO_SPREAD && (g.pol & 2));
+                    for (size_t q = 0; q < kv.second.size() && !ok; q++) ok = owner_tolerates(g.owner, kv.second[q]);
+                    if (ok) tknown0[gi] |= 1ull << kv.first;
+                }
+                // value ranks by name (the canonical pick among equal counts)
+                const auto& vals = c->sol.keys[g.key].vals;
+                std::vector<int> idx(vals.size());
+                for (size_t v = 0; v < vals.size(); v++) idx[v] = (int)v;
+                std::sort(idx.begin(), idx.end(), [&](int a, int b) { return vals[a] < vals[b]; });
+                for (size_t r = 0; r < idx.size(); r++) vrank[(size_t)g.key * 64 + idx[r]] = (uint8_t)r;
+            }
+            for (int i = 0; i < C; i++) {
+                for (int e : th.cons[i]) tcl.push_back(e);
+                for (int e : th.rec[i]) trl.push_back(e);
+                tcoff[i + 1] = (int)tcl.size();
+                troff[i + 1] = (int)trl.size();
+            }
+            if (in->n_bound > 0) return fail(ctx, KP_E_UNSUPPORTED, "bound pods with topology (device path pending)");
+        }
+        if (tcl.empty()) tcl.push_back(0);
+        if (trl.empty()) trl.push_back(0);
+        const int HN = E + NCcap;
+        HIPCHK(c->d_tg_info.upload(tinfo, s));
+        HIPCHK(c->d_tg_hrow.upload(thr_row, s));
+        HIPCHK(c->d_tg_owner.upload(towner, s));
+        HIPCHK(c->d_tg_pol.upload(tpol, s));
+        HIPCHK(c->d_tg_cnt0.upload(tcnt0, s));
+        HIPCHK(c->d_tg_cnt.ensure(tcnt0.size()));
+        HIPCHK(c->d_tg_known0.upload(tknown0, s));
+        HIPCHK(c->d_tg_known.ensure(tknown0.size()));
+        HIPCHK(c->d_tg_pos0.upload(tpos0, s));
+        HIPCHK(c->d_tg_pos.ensure(tpos0.size()));
+        std::vector<int32_t> hc0((size_t)std::max(1, th.n_host) * HN, 0);
+        HIPCHK(c->d_tg_hcnt0.upload(hc0, s));
+        HIPCHK(c->d_tg_hcnt.ensure(hc0.size()));
+        HIPCHK(c->d_cls_tcoff.upload(tcoff, s));
+        HIPCHK(c->d_cls_tc.upload(tcl, s));
+        HIPCHK(c->d_cls_troff.upload(troff, s));
+        HIPCHK(c->d_cls_tr.upload(trl, s));
+        HIPCHK(c->d_vrank.upload(vrank, s));
+        d.HN = HN;
+    }
     if (P > 0) {
         size_t tb = 0;
         HIPCHK(kp_queue_sort(nullptr, P, c->d_perm_a.p, c->d_perm_b.p, c->d_keys_a.p, c->d_keys_b.p, nullptr, &tb, s, nullptr));
@@ -1176,6 +1464,22 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.stats = c->d_stats.p;
     d.err = c->d_err.p;
     d.profile = getenv("KPSIM_PROFILE") ? 1 : 0;
+    d.G = G;
+    d.key_host = th.key_host;
+    d.tg_info = c->d_tg_info.p;
+    d.tg_hrow = c->d_tg_hrow.p;
+    d.tg_owner = c->d_tg_owner.p;
+    d.tg_pol = c->d_tg_pol.p;
+    d.tg_cnt = c->d_tg_cnt.p;
+    d.tg_known = c->d_tg_known.p;
+    d.tg_hcnt = c->d_tg_hcnt.p;
+    d.tg_pos = c->d_tg_pos.p;
+    d.cls_tcoff = c->d_cls_tcoff.p;
+    d.cls_tc = c->d_cls_tc.p;
+    d.cls_troff = c->d_cls_troff.p;
+    d.cls_tr = c->d_cls_tr.p;
+    d.cls_kneutral = c->d_cls_kneutral.p;
+    d.vrank = c->d_vrank.p;
     // quick-accept headroom scale per active axis: every allocatable value >> qshift fits in 30 bits
     for (int ai = 0; ai < KP_LDS_AXES; ai++) {
         int sh = 0;
@@ -1219,6 +1523,13 @@ extern "C" kp_status kp_solve_execute(kp_ctx* ctx) {
     if (!c->h_remaining.empty())
         HIPCHK(hipMemcpyAsync(c->d_remaining.p, c->h_remaining.data(), c->h_remaining.size() * sizeof(int64_t),
                               hipMemcpyHostToDevice, s));
+    if (c->tg_G > 0) {  // topology counts start from the bound pods' counts (TopologyGroup state per Solve)
+        HIPCHK(hipMemcpyAsync(c->d_tg_cnt.p, c->d_tg_cnt0.p, (size_t)c->tg_G * 64 * 4, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->d_tg_known.p, c->d_tg_known0.p, (size_t)c->tg_G * 8, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->d_tg_pos.p, c->d_tg_pos0.p, (size_t)c->tg_G * 4, hipMemcpyDeviceToDevice, s));
+        if (c->tg_HG > 0)
+            HIPCHK(hipMemcpyAsync(c->d_tg_hcnt.p, c->d_tg_hcnt0.p, (size_t)c->tg_HG * d.HN * 4, hipMemcpyDeviceToDevice, s));
+    }
     int32_t* q0 = nullptr;
     HIPCHK(hipEventRecord(c->ev[0], s));
     if (d.P > 0) {

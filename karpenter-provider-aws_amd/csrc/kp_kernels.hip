@@ -135,6 +135,7 @@ __global__ __launch_bounds__(64) void template_init_kernel(KpDev d) {
     a.compat = false;
     a.force_off = true;
     a.prof = nullptr;
+    a.host = 0;
     const bool ok = eval_wave(d, E, CC, a, ws, lane);
     if (lane < d.TW) d.tmpl_opts[(size_t)j * d.TW + lane] = ok ? ws.opts[lane] : 0;
     if (lane == 0) d.tmpl_ok[j] = ok ? 1 : 0;
@@ -352,6 +353,8 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
             };
             int done = 0, err = S.err;
             int c = S.cur_cls;
+            // the current shape's class carries topology: never quick-accepted, every pod goes to the block
+            bool ctopo = c >= 0 && (d.cls_flags[c] & CF_TOPO);
             uint32_t tl = S.cur_tol;
             int pq[KP_LDS_AXES];
 #pragma unroll
@@ -466,6 +469,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                         any_rej = 0;
                     }
                     c = rl32(vc, off);
+                    ctopo = (d.cls_flags[c] & CF_TOPO) != 0;
                     tl = (uint32_t)rl32((int)vtol, off);
 #pragma unroll
                     for (int ai = 0; ai < KP_LDS_AXES; ai++) pq[ai] = rl32(vq[ai], off);
@@ -618,7 +622,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                 }
                 const long long t_d = prof_clock(d);
                 cqscan += t_d - t_c;
-                if (f < N) {
+                if (f < N && !ctopo) {
                     const int fl = f - wb;
                     bool ok = wa;
 #pragma unroll
@@ -842,14 +846,18 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                 a.compat = true;
                 a.force_off = false;
                 a.prof = d.profile ? &S.st[ST_EV_REQ] : nullptr;
-                const bool fast = slast[nc] == (uint16_t)S.cur_cls ||
-                                  ((S.CC.flags & 4u) && ((S.CC.tol >> a.tmpl) & 1u));
+                a.host = d.E + nc;
+                const bool fast = !(S.CC.flags & CF_TOPO) &&
+                                  (slast[nc] == (uint16_t)S.cur_cls || ((S.CC.flags & CF_NOKEYS) && ((S.CC.tol >> a.tmpl) & 1u)));
+                if (fast && lane == 0) S.ws[wave].memo_ok = 1;
                 const bool ok = fast ? eval_fits_only(d, E, a, S.ws[wave], lane) : eval_wave(d, E, S.CC, a, S.ws[wave], lane);
                 if (lane == 0) {
                     S.fastp[b][wave] = fast;
                     S.acc[b][wave] = ok;
-                    if (!ok) {
-                        skey[S.cand_pos[b][wave]] |= 0x80000000u;  // rejected this shape (positions are stable here)
+                    if (!ok && S.ws[wave].memo_ok) {
+                        // rejected this shape for good (positions are stable here); a rejection that depended on
+                        // topology counts is not memoised
+                        skey[S.cand_pos[b][wave]] |= 0x80000000u;
                         S.any_rej = 1;
                     }
                     if (fast) atomicAdd((unsigned long long*)&S.st[ST_WITNESS_MISS], 1ull);
@@ -877,6 +885,9 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                 const int pos = S.cand_pos[round & 1][win];
                 const int nc = sord[pos];
                 if (!S.fastp[round & 1][win]) commit_reqs(d, S.CC, S.ws[win], nc, lane);
+                if (S.CC.flags & CF_TOPO)
+                    topo_record(d, S.CC, S.ws[win], d.nc_hdr + (size_t)nc * K, d.nc_words + (size_t)nc * d.DW,
+                                d.E + nc, d.nc_tmpl[nc], true, lane);
                 if (lane < TW) d.nc_opts[(size_t)nc * TW + lane] = S.ws[win].opts[lane];
                 if (lane < R && S.pod_req[lane])
                     atomicAdd((unsigned long long*)&d.nc_req[(size_t)nc * R + lane], (unsigned long long)S.pod_req[lane]);
@@ -886,7 +897,9 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                     skey[pos]++;
                     S.dirty_kind = 1;
                     S.dirty_pos = pos;
-                    S.scan_start = pos;  // every position before the winner rejected this shape
+                    // every position before the winner rejected this shape for good, unless rejections depended on
+                    // topology counts (not memoised; the next pod of the shape rescans them)
+                    S.scan_start = (S.CC.flags & CF_TOPO) ? 0 : pos;
                     d.pod_result[pod] = nc;
                     d.pod_order[pod] = S.seq++;
                 }
@@ -913,6 +926,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                         a.compat = true;
                         a.force_off = false;
                         a.prof = nullptr;
+                        a.host = d.E + S.N;  // NewNodeClaim's fresh hostname (no pod counted there yet)
                         ok = eval_wave(d, E, S.CC, a, S.ws[wave], lane);
                     }
                     if (lane == 0) S.tacc[wave] = ok;
@@ -939,6 +953,9 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                             d.nc_words[(size_t)n * d.DW + i] = d.cls_words[(size_t)(d.C + jj) * d.DW + i];
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         commit_reqs(d, S.CC, S.ws[wave], n, lane);
+                        if (S.CC.flags & CF_TOPO)
+                            topo_record(d, S.CC, S.ws[wave], d.cls_hdr + (size_t)(d.C + jj) * K,
+                                        d.cls_words + (size_t)(d.C + jj) * d.DW, d.E + n, jj, true, lane);
                         if (lane < TW) d.nc_opts[(size_t)n * TW + lane] = S.ws[wave].opts[lane];
                         for (int r = lane; r < R; r += 64)
                             __hip_atomic_store(&d.nc_req[(size_t)n * R + r], d.daemon[(size_t)jj * R + r] + S.pod_req[r],

@@ -28,6 +28,20 @@
 #define KP_MAX_SCR_WORDS 64          // value-bitset words of one class's keys (per-wave LDS scratch)
 #define KP_MAX_MIN_WORDS 64          // value bitset for a minValues distinct count (4096 values)
 #define KP_LDS_BYTES (160 * 1024)    // LDS per workgroup on gfx950
+#define KP_MAX_TOPO 8                // topology groups constraining one pod class
+#define KP_MAX_TOPO_REC 16           // topology groups recording one pod class's placements
+
+// cls_flags bits
+#define CF_OFFERING 1u               // constrains an offering key
+#define CF_MINV 2u                   // carries minValues
+#define CF_NOKEYS 4u                 // no requirement keys
+#define CF_TOPO 8u                   // topology: constrained by or recorded into some group (never quick-accepted)
+#define CF_TOPO_CONS 16u             // constrained by some group (AddRequirements runs in NodeClaim.Add)
+
+// tg_info.x
+#define TG_TYPE 3                    // KP_TOPO_SPREAD / AFFINITY / ANTI_AFFINITY
+#define TG_INVERSE 4
+#define TG_HOST 8
 
 // ReqHdr.flags
 #define RF_DEF 1u                    // key present in the Requirements map
@@ -157,6 +171,28 @@ struct KpDev {
     const int32_t* cls_xkoff;        // [C+1] CSR of every key a pod class constrains (incl. hostname)
     const int32_t* cls_xkeys;
     int32_t ex_mayfix;               // some class has a NotIn/DoesNotExist key: Add may change node requirements
+
+    // ---------------- topology ([core] scheduling/topology.go, topologygroup.go) ----------------
+    // One group per (pod class, topology term) plus one inverse group per required anti-affinity term.  Value-keyed
+    // groups (zone, capacity-type, ... : <= 64 dictionary values) count per value id; hostname groups count per host
+    // domain h = existing node j, or E + n for in-flight NodeClaim n.  Counts only grow during a Solve.
+    int32_t G;                       // groups
+    int32_t HN;                      // hostname-count row length (E + NCcap)
+    int32_t key_host;                // kubernetes.io/hostname solve key or -1
+    const int4* tg_info;             // [G] {type | inverse << 2 | hostname << 3, key, max_skew, min_domains (0 nil)}
+    const int32_t* tg_hrow;          // [G] row of tg_hcnt (hostname groups), else -1
+    const int32_t* tg_owner;         // [G] class owning the term (spread node filter)
+    const int32_t* tg_pol;           // [G] spread node filter: bit0 nodeAffinityPolicy Honor, bit1 nodeTaintsPolicy Honor
+    int32_t* tg_cnt;                 // [G][64] counts by value id (value-keyed groups)
+    uint64_t* tg_known;              // [G] value ids present in the group's domains map
+    int32_t* tg_hcnt;                // [hostname groups][HN]
+    int32_t* tg_pos;                 // [G] hostname domains with a positive count (affinity bootstrap)
+    const int32_t* cls_tcoff;        // [C+1] CSR: groups that constrain the class (owned forward, selecting inverse)
+    const int32_t* cls_tc;           //   entry: group | self-selecting << 30
+    const int32_t* cls_troff;        // [C+1] CSR: groups that record the class's placements
+    const int32_t* cls_tr;
+    const uint8_t* cls_kneutral;     // parallel to cls_keys: 1 = key added only so topology can narrow it
+    const uint8_t* vrank;            // [K][64] rank of value id v among the key's values by name (tie-break)
 
     // ---------------- FFD kernel LDS plan (kp_ffd_plan_lds) ----------------
     // Dynamic LDS after the fixed FfdShared block: slice arrays sized by lds_ncmax, the staged type tables

@@ -149,6 +149,55 @@ def fuzz_problem(catalog, seed, n_pods=300, n_classes=12, n_pools=3, with_min=Tr
     return Problem(catalog, pools, classes, pods, existing)
 
 
+TOPO_KEYS = [ZONE, HOSTNAME, CAPACITY_TYPE]
+
+
+def _rand_selector(rng, apps):
+    kind = int(rng.integers(0, 6))
+    if kind == 0:
+        return None  # nil selector: selects nothing
+    if kind == 1:
+        return []    # empty selector: selects every pod of the namespace(s)
+    if kind == 2:
+        return [Requirement("app", "NotIn", [str(rng.choice(apps))])]
+    if kind == 3:
+        return [Requirement("tier", str(rng.choice(["Exists", "DoesNotExist"])))]
+    return [Requirement("app", "In", sorted(set(rng.choice(apps, size=int(rng.integers(1, 3))).tolist())))]
+
+
+def add_topology(rng, prob, p_term=0.6, namespaces=("default", "team-b")):
+    """Labels, namespaces and random topology terms on a problem's classes: zonal / hostname / capacity-type spread
+    (maxSkew 1-3, minDomains, node-affinity / taint policies), required pod affinity and anti-affinity, selectors that
+    match the class itself, other classes, everything or nothing."""
+    apps = ["a%d" % i for i in range(max(2, len(prob.classes) // 2))]
+    for pc in prob.classes:
+        pc.labels = {"app": str(rng.choice(apps))}
+        if rng.random() < 0.5:
+            pc.labels["tier"] = str(rng.choice(["web", "db"]))
+        pc.namespace = str(rng.choice(namespaces)) if rng.random() < 0.25 else "default"
+    for pc in prob.classes:
+        while rng.random() < p_term and len(pc.topology) < 3:
+            key = str(rng.choice(TOPO_KEYS, p=[0.5, 0.35, 0.15]))
+            sel = [Requirement("app", "In", [pc.labels["app"]])] if rng.random() < 0.6 else _rand_selector(rng, apps)
+            kind = str(rng.choice(["spread", "spread", "anti", "affinity"]))
+            if kind == "spread":
+                pc.topology.append(model.TopologyTerm(
+                    "spread", key, sel, max_skew=int(rng.integers(1, 4)),
+                    min_domains=int(rng.integers(1, 5)) if rng.random() < 0.2 else None,
+                    node_affinity_policy=str(rng.choice(["Honor", "Honor", "Ignore"])),
+                    node_taints_policy=str(rng.choice(["Ignore", "Ignore", "Honor"]))))
+            else:
+                ns = [str(x) for x in rng.choice(namespaces, size=2, replace=False)] if rng.random() < 0.2 else []
+                pc.topology.append(model.TopologyTerm(kind, key, sel, namespaces=ns))
+    return prob
+
+
+def fuzz_topology_problem(catalog, seed, n_pods=200, n_classes=10):
+    """fuzz_problem (requirements, taints, pools, limits, minValues) plus topology terms on its classes."""
+    prob = fuzz_problem(catalog, seed, n_pods=n_pods, n_classes=n_classes)
+    return add_topology(np.random.Generator(np.random.PCG64(seed + 99)), prob)
+
+
 def _negative(r):
     return r.op in ("NotIn", "DoesNotExist") and not (r.op == "NotIn" and not r.values)
 

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
-"""Full-size oracle fixtures too slow to recompute inside a GPU test (~2 min of single-thread oracle time): runs the
-CPU oracle on seeded BASELINE workloads and writes per-field sha256 digests of its Solve output to
-tests/golden/scale_digests.json.  tests/test_gpu_parity.py::test_scale_digest compares the device result with them.
+"""Full-size oracle fixtures too slow to recompute inside a GPU test (one to two minutes of single-thread oracle time):
+runs the CPU oracle on seeded BASELINE workloads and writes per-field sha256 digests of its Solve output to
+tests/golden/scale_digests.json.  tests/test_gpu_parity.py::test_scale_digest and tests/test_gpu_topology.py compare
+the device result with them.
 
-    python tests/golden/gen_scale_digest.py
+    python tests/golden/gen_scale_digest.py [case ...]     (default: every case; others keep their committed digests)
 """
 import json
 import os
@@ -17,18 +18,26 @@ sys.path[:0] = [os.path.join(ROOT, "karpenter-provider-aws_amd"), os.path.join(R
 from kpsim import catalog, synth  # noqa: E402
 import parity  # noqa: E402
 
-CASES = {"config2_200k": dict(n_pods=200_000)}  # BASELINE configs[4]'s pod count over the config-2 pod mix
+CASES = {
+    "config2_200k": ("config2", dict(n_pods=200_000)),  # BASELINE configs[4]'s pod count over the config-2 pod mix
+    "config3_50k": ("config3", dict(n_pods=50_000)),    # BASELINE configs[2]: topology + five weighted NodePools
+}
 
 
 def main():
     cat = catalog.golden_catalog(fx=catalog.load_fixtures())
+    path = os.path.join(HERE, "scale_digests.json")
     out = {}
-    for name, kw in CASES.items():
-        prob = synth.config2(catalog=cat, **kw)
+    if os.path.exists(path):
+        with open(path) as f:
+            out = json.load(f)
+    for name in sys.argv[1:] or list(CASES):
+        gen, kw = CASES[name]
+        prob = getattr(synth, gen)(catalog=cat, **kw)
         t = time.time()
         out[name] = dict(kw, **parity.result_digest(parity.run_oracle(prob)))
         print(name, "%.1f s" % (time.time() - t), out[name]["n_nodeclaims"])
-    with open(os.path.join(HERE, "scale_digests.json"), "w") as f:
+    with open(path, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
 
 

@@ -1,0 +1,129 @@
+"""GPU: topology spread, pod affinity and anti-affinity on the device (topo_narrow / topo_record in csrc/kp_eval.h)
+against the oracle's restatement of [core] topology.go — bit-exact, plus the reference's own expectations.
+
+Reference-pinned: test/suites/scheduling/suite_test.go:421-470 (self-affinity → 1 node, zonal spread → 3 nodes) and
+test/suites/scale/provisioning_test.go:76-214 (node-dense 500 nodes with and without minValues, pod-dense 60 nodes).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import fuzzgen
+import parity
+from kpsim import abi, model, synth
+import test_topology_cpu as TC
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from kpsim import native
+    c = native.Context(0)
+    yield c
+    c.close()
+
+
+def same(ctx, prob):
+    dev = parity.run_device(ctx, prob)
+    parity.assert_same(dev, parity.run_oracle(prob))
+    return dev
+
+
+def test_zonal_spread_three_nodes(ctx, golden):
+    lab = {"test": "zonal-spread"}
+    pc, pods = TC.deployment(3, lab, [model.TopologyTerm("spread", model.ZONE, TC.sel(lab), max_skew=1, min_domains=3)])
+    r, q = same(ctx, model.Problem(golden, [synth.default_nodepool()], [pc], pods))
+    assert r.n_nodeclaims == 3
+    assert sorted(TC.zone_of(x) for x in q) == [("test-zone-1a",), ("test-zone-1b",), ("test-zone-1c",)]
+
+
+def test_self_affinity_one_node(ctx, golden):
+    lab = {"test": "self-affinity"}
+    pc, pods = TC.deployment(2, lab, [model.TopologyTerm("affinity", model.HOSTNAME, TC.sel(lab))])
+    r, _ = same(ctx, model.Problem(golden, [synth.default_nodepool()], [pc], pods))
+    assert r.n_nodeclaims == 1
+
+
+@pytest.mark.parametrize("min_values", [None, 30])
+def test_node_dense(ctx, golden, min_values):
+    lab = {"app": "node-dense"}
+    pc, pods = TC.deployment(500, lab, [model.TopologyTerm("anti", model.HOSTNAME, TC.sel(lab))])
+    r, _ = same(ctx, model.Problem(golden, [TC.e2e_nodepool(min_values)], [pc], pods))
+    assert r.n_nodeclaims == 500 and (r.nodeclaim_n_pods == 1).all()
+
+
+def test_hostname_spread_and_inverse_anti_affinity(ctx, golden):
+    lab = {"app": "h"}
+    pc, pods = TC.deployment(10, lab, [model.TopologyTerm("spread", model.HOSTNAME, TC.sel(lab), max_skew=2)])
+    r, _ = same(ctx, model.Problem(golden, [synth.default_nodepool()], [pc], pods))
+    assert r.n_nodeclaims == 5
+    a = model.PodClass(labels={"app": "a"}, topology=[model.TopologyTerm("anti", model.HOSTNAME, TC.sel({"app": "b"}))])
+    b = model.PodClass(labels={"app": "b"})
+    pods = synth.pods_from_specs([(0, {"cpu": "2", "memory": "1Gi"}), (1, {"cpu": "1", "memory": "1Gi"}),
+                                  (1, {"cpu": "1", "memory": "1Gi"})])
+    r, _ = same(ctx, model.Problem(golden, [synth.default_nodepool()], [a, b], pods))
+    assert list(r.pod_result) == [0, 1, 1]
+
+
+def test_zonal_anti_affinity_and_foreign_selector(ctx, golden):
+    lab = {"app": "za"}
+    pc, pods = TC.deployment(4, lab, [model.TopologyTerm("anti", model.ZONE, TC.sel(lab))])
+    r, _ = same(ctx, model.Problem(golden, [synth.default_nodepool()], [pc], pods))
+    assert r.n_nodeclaims == 1 and int((r.pod_result == -1).sum()) == 3
+    other = model.PodClass(labels={"app": "web"}, requirements=[model.Requirement(model.ZONE, "In", ["test-zone-1a"])])
+    owner = model.PodClass(labels={"app": "probe"},
+                           topology=[model.TopologyTerm("spread", model.ZONE, TC.sel({"app": "web"}), max_skew=1)])
+    pods = synth.pods_from_specs([(0, {"cpu": "2", "memory": "1Gi"})] * 2 + [(1, {"cpu": "1", "memory": "1Gi"})])
+    r, _ = same(ctx, model.Problem(golden, [synth.default_nodepool()], [other, owner], pods))
+    assert r.n_nodeclaims == 2
+
+
+def test_preference_policy_ignore(golden):
+    """PREFERENCE_POLICY=Ignore (kp_device_opts.preference_policy) drops ScheduleAnyway spreads; Respect is rejected."""
+    from kpsim import native
+    lab = {"app": "p"}
+    pc, pods = TC.deployment(6, lab, [model.TopologyTerm("spread", model.HOSTNAME, TC.sel(lab),
+                                                         when_unsatisfiable="ScheduleAnyway")])
+    prob = model.Problem(golden, [synth.default_nodepool()], [pc], pods)
+    c = native.Context(0, preference_policy=abi.KP_PREFERENCE_IGNORE)
+    try:
+        dev = parity.run_device(c, prob)
+        o = __import__("pyoracle").solve(prob, preference_policy=abi.KP_PREFERENCE_IGNORE)
+        np.testing.assert_array_equal(dev[0].pod_result, o.results.pod_result)
+    finally:
+        c.close()
+    r = native.Context(0)
+    try:
+        with pytest.raises(native.KpError) as e:
+            parity.run_device(r, prob)
+        assert e.value.status == abi.KP_E_UNSUPPORTED
+    finally:
+        r.close()
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_fuzz_topology(ctx, golden, seed):
+    """Random spread / affinity / anti-affinity terms (zone, hostname, capacity-type; selectors on the class itself,
+    other classes, everything or nothing; namespaces; minDomains; node filter policies) over fuzzed requirements,
+    taints, weighted NodePools with limits and minValues."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=160, replace=False))]
+    same(ctx, fuzzgen.fuzz_topology_problem(sub, seed, n_pods=int(rng.integers(50, 300))))
+
+
+@pytest.mark.parametrize("n", [500, 3000])
+def test_config3_sample(ctx, golden, n):
+    same(ctx, synth.subsample(synth.config3(catalog=golden), n))
+
+
+def test_config3_full_digest(ctx, golden):
+    """BASELINE configs[2] at full size (50k pods): every output field equals the oracle's committed digest
+    (tests/golden/gen_scale_digest.py config3_50k; the oracle needs ~1 min here)."""
+    with open(os.path.join(os.path.dirname(__file__), "golden", "scale_digests.json")) as f:
+        want = json.load(f)["config3_50k"]
+    prob = synth.config3(catalog=golden, n_pods=want["n_pods"])
+    got = parity.result_digest(parity.run_device(ctx, prob))
+    assert got == {k: v for k, v in want.items() if k != "n_pods"}
