@@ -223,6 +223,82 @@ def launch_leg(a, golden, local, rank, world, dist, barrier):
     return out
 
 
+def topology_leg(a, cat, local, rank, world, dist, barrier):
+    """BASELINE configs[2]: 50k pods with zonal + hostname topology spread and hostname anti-affinity over five weighted
+    NodePools with cpu limits (synth.config3).  Same step as the headline leg: one kp_solve_execute with HBM-resident
+    inputs; replicas across ranks (weak scaling, no collective)."""
+    from kpsim import model, native, synth
+    prob = synth.config3(n_pods=a.pods, catalog=cat)
+    ctx = native.Context(local)
+    ctx.upload_catalog(model.CatalogView(cat))
+    iv = model.SolveInputView(prob)
+    cap_nc = max(16, prob.pods.n + 1)
+    out = model.OutputBuffers(prob.pods.n, cap_nc, cap_nc * 60)
+    t = time.perf_counter()
+    ctx.solve(iv, out)
+    e2e_ms = (time.perf_counter() - t) * 1e3
+    res = out.results()
+    ctx.prepare(iv)
+    for _ in range(a.warmup):
+        ctx.execute()
+    barrier()
+    kts = []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ctx.execute()
+        kts.append(ctx.kernel_times_ms())
+    elapsed = time.perf_counter() - t0
+    barrier()
+    if dist is not None:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    kt = np.array(kts).mean(axis=0)
+    P, T = prob.pods.n, len(cat)
+    B = algorithmic_bytes(res.stats, res.n_nodeclaims, T)
+    achieved = B / (kt[3] / 1e3) / 1e9
+    n_topo = int(sum(1 for c in prob.pods.class_id if prob.classes[int(c)].topology))
+    line = {
+        "metric": "pods scheduled/sec (Solve, config3: topology spread + anti-affinity, 5 weighted NodePools)",
+        "value": P * a.steps * world / elapsed,
+        "unit": "pods/s",
+        "n_gpus": world,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "scaling": "weak",
+        "config": {"workload": "config3: %d pods (%d with topology terms), 250 classes x %d types, 5 NodePools" %
+                               (P, n_topo, T), "parallelism": "replicas" if world > 1 else "single"},
+        "kernel_ms": {"queue_sort": float(kt[0]), "class_mask": float(kt[1]), "template_init": float(kt[2]),
+                      "ffd": float(kt[3]), "finalize": float(kt[4])},
+        "end_to_end_ms": e2e_ms,
+        "nodeclaims": res.n_nodeclaims,
+        "unschedulable": int((res.pod_result == -1).sum()),
+        "roofline": {"bound": "hbm", "kernel": "ffd_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes": int(B), "kernel_ms": float(kt[3])},
+        "solve_stats": {k: v for k, v in res.stats.items() if not k.startswith("ns_")},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        import parity
+        import pyoracle
+        sample = synth.subsample(prob, min(P, a.topo_cpu_sample))
+        t = time.perf_counter()
+        orc = pyoracle.solve(sample)
+        cpu_s = time.perf_counter() - t
+        line["cpu_baseline"] = {"value": sample.pods.n / cpu_s, "unit": "pods/s", "cores": 1, "kind": "port",
+                                "sample": "oracle (1 thread) on a seeded %d-pod subsample of config3: %.2f s"
+                                          % (sample.pods.n, cpu_s)}
+        try:
+            parity.assert_same(parity.run_device(ctx, sample),
+                               (orc.results, [model.parse_requirements_blob(orc.requirements(i))
+                                              for i in range(orc.results.n_nodeclaims)]))
+            line["parity_vs_cpu_baseline"] = True
+        except AssertionError:
+            line["parity_vs_cpu_baseline"] = False
+    ctx.close()
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -235,6 +311,8 @@ def main():
     ap.add_argument("--nodes", type=int, default=5000, help="config4 cluster size (consolidation leg)")
     ap.add_argument("--launch-batch", type=int, default=10_000, help="config5 launch batch (NodeClaims)")
     ap.add_argument("--no-launch", action="store_true")
+    ap.add_argument("--no-topology", action="store_true")
+    ap.add_argument("--topo-cpu-sample", type=int, default=12_000, help="pods in config3's CPU-baseline sample")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -301,6 +379,7 @@ def main():
 
     cons = None if a.no_consolidation else consolidation_leg(a, cat, local, rank, world, dist, barrier)
     launch = None if a.no_launch else launch_leg(a, cat, local, rank, world, dist, barrier)
+    topo = None if a.no_topology else topology_leg(a, cat, local, rank, world, dist, barrier)
 
     cpu = None
     parity_ok = None
@@ -359,6 +438,7 @@ def main():
             "solve_stats": {k: v for k, v in res.stats.items() if not k.startswith("ns_")},
             "consolidation": cons,
             "launch": launch,
+            "topology": topo,
         }
         print(json.dumps(line))
     ctx.close()

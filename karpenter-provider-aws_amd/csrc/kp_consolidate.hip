@@ -422,7 +422,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 a.prof = nullptr;
                 a.host = 0;
                 st_nc++;
-                if (eval_wave(d, Ev, S.CC, a, S.ws, lane)) {
+                if (eval_wave<false>(d, Ev, S.CC, a, S.ws, lane)) {
                     if (lane < S.CC.nck) {
                         const int kk = S.CC.key[lane];
                         nch[kk] = S.ws.hdr[lane];
@@ -452,7 +452,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     a.prof = nullptr;
                     a.host = 0;
                     st_tmpl++;
-                    if (!eval_wave(d, Ev, S.CC, a, S.ws, lane)) continue;
+                    if (!eval_wave<false>(d, Ev, S.CC, a, S.ws, lane)) continue;
                     if (n_nc == 1) {  // a second NodeClaim: computeConsolidation returns NONE
                         stop = true;
                         break;

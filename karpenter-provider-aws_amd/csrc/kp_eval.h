@@ -470,6 +470,10 @@ __device__ __forceinline__ void topo_record(const KpDev& d, const ClassCache& CC
     } while (0)
 
 // Wave-uniform result: does NodeClaim.Add(pod) succeed?  On success ws.opts / ws.hdr / ws.words hold the new state.
+// TOPO: the class is constrained by topology groups (CF_TOPO_CONS): topo_narrow runs between the requirement merge
+// and the type sweep, and keys carried only for narrowing (kneutral) merge as the base requirement.  The two
+// instantiations keep the topology code out of the common path.
+template <bool TOPO>
 __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, const ClassCache& CC, const EvalIn& a,
                                           WaveScratch& ws, int lane) {
     const int TW = d.TW, T = d.T;
@@ -482,7 +486,20 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
     bool fail = false, kill = false;
     uint64_t adm = ~0ull;
     int kmul = -1;
-    ws.memo_ok = 1;
+    if (lane == 0) ws.memo_ok = 1;
+    // DoesNotExist-type elimination and the admissible value mask of a multi-valued key, from the merged requirement
+    auto classify = [&](int k, const ReqHdr& O, const uint64_t* ow, int cnt) {
+        const uint32_t kf = CC.kflags[lane];
+        if (!(O.flags & RF_DEF)) return;
+        if (kf & (KF_CAT_SINGLE | KF_CAT_MULTI)) kill = !op_notin_or_dne(req_op(O.flags, cnt));
+        if (kf & KF_CAT_MULTI) {
+            kmul = CC.kmulti[lane];
+            adm = 0;
+            const int nv = CC.nval[lane] < 64 ? CC.nval[lane] : 64;
+            for (int v = 0; v < nv; v++)
+                if (req_has(d, k, v, O, ow)) adm |= 1ull << v;
+        }
+    };
     if (lane < nck) {
         const int k = CC.key[lane];
         const int n = CC.nw[lane];
@@ -492,42 +509,36 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         const uint64_t* bw = CC.words + CC.wsoff[lane];
         uint64_t* ow = ws.words + CC.wsoff[lane];
         ReqHdr O;
+        int cnt;
         const int nb = CC.nbB[lane];
-        if ((CC.kneutral >> lane) & 1u) {
+        if (TOPO && ((CC.kneutral >> lane) & 1u)) {
             // key present only for topology: the pod does not constrain it, the merge keeps the base requirement
             O = A;
             for (int i = 0; i < n; i++) ow[i] = (A.flags & RF_DEF) ? aw[i] : 0ull;
+            cnt = 0;
         } else if (!(A.flags & RF_DEF)) {
             if (a.compat && !op_notin_or_dne(req_op(B.flags, nb)) && !(CC.kflags[lane] & KF_WELL_KNOWN)) fail = true;
             O = B;
             for (int i = 0; i < n; i++) ow[i] = bw[i];
+            cnt = nb;
         } else {
-            const int cnt = req_intersect(d, k, A, aw, B, bw, O, ow);
+            cnt = req_intersect(d, k, A, aw, B, bw, O, ow);
             if (a.compat && !(O.flags & RF_CMP) && cnt == 0) {
                 const int na = popc_words(aw, n);
                 if (!(op_notin_or_dne(req_op(B.flags, nb)) && op_notin_or_dne(req_op(A.flags, na)))) fail = true;
             }
         }
         ws.hdr[lane] = O;
+        if (!TOPO) classify(k, O, ow, cnt);
     }
     if (ballot(fail)) return false;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    if (CC.flags & CF_TOPO_CONS) {
+    if (TOPO) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         if (!topo_narrow(d, CC, ws, a.host, a.compat, lane)) return false;
-    }
-    if (lane < nck) {
-        const int k = CC.key[lane];
-        const ReqHdr O = ws.hdr[lane];
-        const uint64_t* ow = ws.words + CC.wsoff[lane];
-        const uint32_t kf = CC.kflags[lane];
-        if ((kf & (KF_CAT_SINGLE | KF_CAT_MULTI)) && (O.flags & RF_DEF))
-            kill = !op_notin_or_dne(req_op(O.flags, popc_words(ow, CC.nw[lane])));
-        if ((kf & KF_CAT_MULTI) && (O.flags & RF_DEF)) {
-            kmul = CC.kmulti[lane];
-            adm = 0;
-            const int nv = CC.nval[lane] < 64 ? CC.nval[lane] : 64;
-            for (int v = 0; v < nv; v++)
-                if (req_has(d, k, v, O, ow)) adm |= 1ull << v;
+        if (lane < nck) {
+            const ReqHdr O = ws.hdr[lane];
+            const uint64_t* ow = ws.words + CC.wsoff[lane];
+            classify(CC.key[lane], O, ow, popc_words(ow, CC.nw[lane]));
         }
     }
     EV_STAMP(0);

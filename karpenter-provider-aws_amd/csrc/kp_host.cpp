@@ -244,7 +244,7 @@ struct kp_ctx {
     double ns_prep = 0, ns_exec = 0, ns_fin = 0;
     hipEvent_t ev[6] = {};
     double kernel_ms[5] = {};
-    int64_t cycles[30] = {};  // FFD phases (s_memtime): pop, sort, scan+eval, templates, commit, full pdqsort
+    int64_t cycles[33] = {};  // FFD phases (s_memtime): pop, sort, scan+eval, templates, commit, full pdqsort
     bool any_min_values = false;             // some template requirement carries minValues
     bool cons_mayfix = false;                // a pod's NotIn/DoesNotExist merge can change a later Compatible
     // consolidation probes
@@ -1027,6 +1027,12 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
             }
             if (!th.cons[row].empty() || !th.rec[row].empty()) cflags[row] |= CF_TOPO;
             if (!th.cons[row].empty()) cflags[row] |= CF_TOPO_CONS;
+            bool qrec = true;
+            for (int gi : th.rec[row]) {
+                const HGroup& g = th.g[gi];
+                if (!g.inverse && g.type == KP_TOPO_SPREAD && (g.pol & 1) && g.owner != row) qrec = false;
+            }
+            if (qrec) cflags[row] |= CF_TOPO_QREC;
         }
         if (nk == 0) cflags[row] |= CF_NOKEYS;  // no requirement keys: NodeClaim.Add = tolerations + Fits (+ minValues)
         if (nk > KP_MAX_CLASS_KEYS || so > KP_MAX_SCR_WORDS) return false;
@@ -1612,6 +1618,7 @@ extern "C" kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out) {
     for (int i = 0; i < 6; i++) c->cycles[6 + i] = st[ST_EV_REQ + i];
     for (int i = 0; i < 7; i++) c->cycles[12 + i] = st[ST_QUICK + i];
     for (int i = 0; i < 11; i++) c->cycles[19 + i] = st[ST_N_NOINV + i];
+    for (int i = 0; i < 3; i++) c->cycles[30 + i] = st[ST_TOPO_QUICK + i];
     so.ns_host_prep = c->ns_prep;
     so.ns_device_solve = c->ns_exec;
     if (N > out->cap_nodeclaims || n_ids > out->cap_type_ids) return fail(ctx, KP_E_BUFFER, "output buffers too small");
@@ -1644,7 +1651,7 @@ extern "C" kp_status kp_last_kernel_times(kp_ctx* ctx, double* ms, int32_t n) {
     if (!ctx || !ms) return KP_E_INVALID;
     if (!ctx->executed) return fail(ctx, KP_E_STATE, "no execute yet");
     for (int i = 0; i < n && i < 5; i++) ms[i] = ctx->kernel_ms[i];
-    for (int i = 5; i < n && i < 35; i++) ms[i] = (double)ctx->cycles[i - 5];
+    for (int i = 5; i < n && i < 38; i++) ms[i] = (double)ctx->cycles[i - 5];
     return KP_OK;
 }
 

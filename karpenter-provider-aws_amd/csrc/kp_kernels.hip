@@ -136,7 +136,7 @@ __global__ __launch_bounds__(64) void template_init_kernel(KpDev d) {
     a.force_off = true;
     a.prof = nullptr;
     a.host = 0;
-    const bool ok = eval_wave(d, E, CC, a, ws, lane);
+    const bool ok = eval_wave<false>(d, E, CC, a, ws, lane);
     if (lane < d.TW) d.tmpl_opts[(size_t)j * d.TW + lane] = ok ? ws.opts[lane] : 0;
     if (lane == 0) d.tmpl_ok[j] = ok ? 1 : 0;
 }
@@ -168,16 +168,200 @@ struct FfdShared {
     int32_t cur_pq[KP_LDS_AXES];   // scaled quick-accept requests of the current shape
     int64_t shape_req[KP_MAX_R];   // requests of the current shape (pending-total flush)
     long long st[ST_COUNT];
+    // topology prefilter of the current pod (topo_prefilter_setup): a NodeClaim whose own requirements admit no
+    // domain a constraining group allows cannot accept the pod, and is skipped without an evaluation
+    int tp_n, topo_pod, topo_quick;
+    int tp_k[KP_MAX_TOPO];         // value-keyed group: key; hostname group: -1 - row of tg_hcnt
+    int tp_lo[KP_MAX_TOPO], tp_hi[KP_MAX_TOPO];  // hostname group: the host's count must lie in [lo, hi]
+    int tp_cmp[KP_MAX_TOPO];       // value-keyed: a complement (NotIn) NodeClaim requirement is not prefiltered
+    uint64_t tp_elig[KP_MAX_TOPO]; // value-keyed: allowed domains ∩ the pod's domains
 };
 
-// wave 0: collect up to KP_NWAVES slice positions >= start whose NodeClaim has not rejected the current shape
-__device__ inline void collect_candidates(FfdShared& S, const uint32_t* key, const uint16_t* ord, int N, int start,
-                                          int buf, int lane) {
-    (void)ord;
+// wave 0, once per pod of a class with constraining topology groups: the per-group conditions topo_narrow applies,
+// reduced to what depends on the candidate (its host's count, or its own domains of the key).  Exact up to the
+// NotIn/DoesNotExist Compatible exception, which the prefilter leaves to the evaluation.
+__device__ inline void topo_prefilter_setup(const KpDev& d, FfdShared& S, int c, int lane) {
+    const int t0 = d.cls_tcoff[c], nt = d.cls_tcoff[c + 1] - t0;
+    for (int e = 0; e < nt; e++) {
+        const int ent = d.cls_tc[t0 + e], g = ent & 0x3FFFFFFF, self = (ent >> 30) & 1;
+        const int4 info = d.tg_info[g];
+        const int type = info.x & TG_TYPE;
+        int k = -1, lo = 0, hi = INT32_MAX, cmp = 0;
+        uint64_t elig = 0;
+        if (info.x & TG_HOST) {
+            k = -1 - d.tg_hrow[g];
+            if (type == 0) hi = info.z - self;
+            else if (type == 2) hi = 0;
+            else lo = (self && ld_i32(&d.tg_pos[g]) == 0) ? 0 : 1;
+        } else {
+            k = info.y;
+            // the pod's domains: its requirement for the key, or every value when it does not constrain it
+            const ReqHdr ph = d.cls_hdr[(size_t)c * d.K + k];
+            const bool valid = lane < d.nval[k];
+            const bool pod_has =
+                valid && (!(ph.flags & RF_DEF) || req_has(d, k, lane, ph, d.cls_words + (size_t)c * d.DW + d.woff[k]));
+            const bool kn = valid && ((ld_u64(&d.tg_known[g]) >> lane) & 1ull);
+            const int cnt = kn ? ld_i32(&d.tg_cnt[(size_t)g * 64 + lane]) : 0;
+            if (type == 0) {
+                const uint64_t sup = ballot(kn && pod_has);
+                int mn = wave_min_i32((kn && pod_has) ? cnt : INT32_MAX);
+                if (info.w > 0 && __popcll(sup) < info.w) mn = 0;
+                elig = ballot(kn && pod_has && (int64_t)cnt + self - (int64_t)mn <= (int64_t)info.z);
+            } else if (type == 2) {
+                elig = ballot(kn && cnt == 0 && pod_has);
+            } else {
+                elig = ballot(kn && cnt > 0 && pod_has);
+                cmp = 1;
+                if (!elig) {
+                    if (self) elig = ballot(kn && pod_has);
+                    else cmp = 0;  // no domain at all: Get is empty whatever the node requirement
+                }
+            }
+        }
+        if (lane == 0) {
+            S.tp_k[e] = k;
+            S.tp_lo[e] = lo;
+            S.tp_hi[e] = hi;
+            S.tp_cmp[e] = cmp;
+            S.tp_elig[e] = elig;
+        }
+    }
+    if (lane == 0) S.tp_n = nt;
+}
+
+__device__ __forceinline__ bool topo_prefilter_pass(const KpDev& d, const FfdShared& S, int nc) {
+    bool ok = true;
+    for (int e = 0; e < S.tp_n && ok; e++) {
+        const int k = S.tp_k[e];
+        if (k < 0) {
+            const int cnt = ld_i32(&d.tg_hcnt[(size_t)(-1 - k) * d.HN + d.E + nc]);
+            ok = cnt >= S.tp_lo[e] && cnt <= S.tp_hi[e];
+        } else {
+            const uint32_t fl = d.nc_hdr[(size_t)nc * d.K + k].flags;
+            const uint64_t w = d.nc_words[(size_t)nc * d.DW + d.woff[k]];
+            if (!(fl & RF_DEF)) ok = S.tp_elig[e] != 0;
+            else if (fl & RF_CMP) ok = S.tp_cmp[e] || (~w & S.tp_elig[e]) != 0;
+            else ok = (w & S.tp_elig[e]) != 0;
+        }
+    }
+    return ok;
+}
+
+// wave 0: the first slice position in [start, N) that has not rejected the shape and passes the topology prefilter
+// (N if none).  Four 64-position chunks per round so the prefilter's global loads of 256 NodeClaims overlap.
+__device__ inline int topo_scan(const KpDev& d, const FfdShared& S, const uint32_t* skey, const uint16_t* sord, int N,
+                                int start, int lane) {
+    for (int base = start; base < N; base += 256) {
+        bool ok[4];
+        int nc[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int p = base + u * 64 + lane;
+            ok[u] = p < N && !(skey[p] >> 31);
+            nc[u] = ok[u] ? (int)sord[p] : 0;
+        }
+        for (int e = 0; e < S.tp_n; e++) {
+            const int k = S.tp_k[e];
+            if (k < 0) {
+                const int32_t* row = d.tg_hcnt + (size_t)(-1 - k) * d.HN + d.E;
+                const int lo = S.tp_lo[e], hi = S.tp_hi[e];
+                int cnt[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) cnt[u] = ok[u] ? ld_i32(row + nc[u]) : 0;
+#pragma unroll
+                for (int u = 0; u < 4; u++) ok[u] = ok[u] && cnt[u] >= lo && cnt[u] <= hi;
+            } else {
+                const uint64_t el = S.tp_elig[e];
+                const bool cmp = S.tp_cmp[e];
+                uint32_t fl[4];
+                uint64_t w[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    fl[u] = ok[u] ? d.nc_hdr[(size_t)nc[u] * d.K + k].flags : 0u;
+                    w[u] = ok[u] ? d.nc_words[(size_t)nc[u] * d.DW + d.woff[k]] : 0ull;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const bool pass = !(fl[u] & RF_DEF) ? el != 0 : (fl[u] & RF_CMP) ? (cmp || (~w[u] & el) != 0)
+                                                                                       : (w[u] & el) != 0;
+                    ok[u] = ok[u] && pass;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint64_t m = ballot(ok[u]);
+            if (m) return base + u * 64 + __ffsll((unsigned long long)m) - 1;
+        }
+    }
+    return N;
+}
+
+// Every value-keyed group of the pod already sees a single domain on NodeClaim nc (its requirement for the key is
+// In [one value]), so AddRequirements cannot narrow it (the prefilter has admitted that value).
+__device__ inline bool topo_pinned(const KpDev& d, const FfdShared& S, int nc) {
+    for (int e = 0; e < S.tp_n; e++) {
+        const int k = S.tp_k[e];
+        if (k < 0) continue;
+        const uint32_t fl = d.nc_hdr[(size_t)nc * d.K + k].flags;
+        const uint64_t w = d.nc_words[(size_t)nc * d.DW + d.woff[k]];
+        if (!(fl & RF_DEF) || (fl & RF_CMP) || __popcll(w) != 1) return false;
+    }
+    return true;
+}
+
+// Topology.Record of a quick accept onto NodeClaim nc (template tmpl): its requirements are unchanged by the Add, so
+// every recorded domain comes from its digest (hostname groups: its host E + nc).  CF_TOPO_QREC guarantees that no
+// recording group needs the node-affinity filter of another class.
+__device__ inline void topo_record_quick(const KpDev& d, int c, int nc, int tmpl, int lane) {
+    for (int i = d.cls_troff[c]; i < d.cls_troff[c + 1]; i++) {
+        const int g = d.cls_tr[i];
+        const int4 info = d.tg_info[g];
+        const int type = info.x & TG_TYPE;
+        const bool inv = info.x & TG_INVERSE;
+        if (!inv && type == 0 && (d.tg_pol[g] & 2) && !((d.tol[d.tg_owner[g]] >> tmpl) & 1u)) continue;
+        if (info.x & TG_HOST) {
+            if (lane == 0) {
+                const int old = atomicAdd(&d.tg_hcnt[(size_t)d.tg_hrow[g] * d.HN + d.E + nc], 1);
+                if (old == 0) atomicAdd(&d.tg_pos[g], 1);
+            }
+            continue;
+        }
+        const int k = info.y;
+        const ReqHdr h = d.nc_hdr[(size_t)nc * d.K + k];
+        const uint64_t w = d.nc_words[(size_t)nc * d.DW + d.woff[k]];
+        if (!(h.flags & RF_DEF)) continue;
+        if (!inv && type != 2 && ((h.flags & RF_CMP) || __popcll(w) != 1)) continue;
+        if ((w >> lane) & 1ull) atomicAdd(&d.tg_cnt[(size_t)g * 64 + lane], 1);
+        if (lane == 0 && w) atomicOr((unsigned long long*)&d.tg_known[g], (unsigned long long)w);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// wave 0: collect up to KP_NWAVES slice positions >= start whose NodeClaim has not rejected the current shape (and
+// passes the topology prefilter of the current pod)
+__device__ inline void collect_candidates(const KpDev& d, FfdShared& S, const uint32_t* key, const uint16_t* ord, int N,
+                                          int start, int buf, int lane) {
     int cnt = 0, pos = start, next = N;
     while (pos < N) {
         const int p = pos + lane;
-        const bool c = p < N && !(key[p] >> 31);
+        bool c = p < N && !(key[p] >> 31);
+        if (S.tp_n && c) c = topo_prefilter_pass(d, S, ord[p]);
+        const uint64_t m0 = __ballot(c);
+        if (S.tp_n && m0 && cnt + __popcll(m0) < KP_NWAVES) {
+            // topology pods: the first prefilter survivor usually accepts; end the round with this window rather than
+            // paying the prefilter's loads for up to 8 candidates (the next round continues after it)
+            const int rank = cnt + __popcll(m0 & ((1ull << lane) - 1ull));
+            if (c) S.cand_pos[buf][rank] = p;
+            cnt += __popcll(m0);
+            pos += 64;
+            if (lane == 0) {
+                S.n_cand[buf] = cnt;
+                S.scan_next[buf] = pos < N ? pos : N;
+                S.scan_done[buf] = pos >= N;
+            }
+            return;
+        }
         const uint64_t m = __ballot(c);
         const int rank = cnt + __popcll(m & ((1ull << lane) - 1ull));
         if (c && rank < KP_NWAVES) S.cand_pos[buf][rank] = p;
@@ -270,6 +454,9 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
     }
     if (tid == 0) {
         S.N = 0;
+        S.tp_n = 0;
+        S.topo_pod = 0;
+        S.topo_quick = 0;
         S.qhead = 0;
         S.qcount = P;
         S.done = 0;
@@ -353,7 +540,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
             };
             int done = 0, err = S.err;
             int c = S.cur_cls;
-            // the current shape's class carries topology: never quick-accepted, every pod goes to the block
+            // the current shape's class carries topology (CF_TOPO): such pods are handled by the block
             bool ctopo = c >= 0 && (d.cls_flags[c] & CF_TOPO);
             uint32_t tl = S.cur_tol;
             int pq[KP_LDS_AXES];
@@ -363,6 +550,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
             long long cqpop = 0, cqscan = 0, cqcheck = 0, cqcommit = 0;
             long long n_noinv = 0, n_winmove = 0, n_ldssort = 0, n_pivot = 0, n_winload = 0, n_flush = 0, n_shape = 0;
             long long n_r2 = 0, n_rwb = 0, n_rout = 0, n_batch = 0;
+
             // ---- slice window: lane i mirrors slice position wb + i and its NodeClaim (authoritative while valid) ----
             int wb = -1;
             uint32_t wk = 0xFFFFFFFFu, wo = 0, wm = 0xFFFFu;  // key|rejected, NodeClaim id, lastClass | template << 16
@@ -604,6 +792,19 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                     if (dkind == 2 || how == 2 || sstart > dpos) sstart = 0;
                     dkind = 0;
                 }
+                if (ctopo) {
+                    // a pod with topology terms: the block handles it (topology prefilter, quick accept with
+                    // recording, or the evaluation of candidates); counts change with every placement
+                    win_flush();
+                    wb = -1;
+                    if (lane < R) S.pod_req[lane] = S.qw_req[off][lane];
+                    if (lane == 0) {
+                        S.cur_pod = p;
+                        S.cls_fill = S.CC.cls != c;
+                        S.topo_pod = 1;
+                    }
+                    break;
+                }
                 // first NodeClaim in slice order (from sstart) that has not rejected this shape
                 const long long t_c = prof_clock(d);
                 int f = N;
@@ -622,9 +823,9 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                 }
                 const long long t_d = prof_clock(d);
                 cqscan += t_d - t_c;
-                if (f < N && !ctopo) {
+                if (f < N) {
                     const int fl = f - wb;
-                    bool ok = wa;
+                    bool ok = wa && A > 0;  // no witness table (A == 0): every pod is evaluated
 #pragma unroll
                     for (int ai = 0; ai < KP_LDS_AXES; ai++)
                         if (ai < A) ok &= pq[ai] <= wh[ai];
@@ -645,7 +846,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                             // the run leaves the window: re-base the window at f to batch over up to 64 of its elements
                             win_flush();
                             win_load(f);
-                            bool ok2 = wa;
+                            bool ok2 = wa && A > 0;
 #pragma unroll
                             for (int ai = 0; ai < KP_LDS_AXES; ai++)
                                 if (ai < A) ok2 &= pq[ai] <= wh[ai];
@@ -771,8 +972,9 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                 if (lane == 0) {
                     S.cur_pod = p;
                     S.cls_fill = S.CC.cls != c;  // decided before the barrier: fill_class_cache rewrites CC.cls
+                    S.topo_pod = 0;
                 }
-                collect_candidates(S, skey, sord, N, f, 0, lane);
+                collect_candidates(d, S, skey, sord, N, f, 0, lane);
                 break;
             }
             win_flush();
@@ -815,6 +1017,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                 S.st[ST_N_SHAPE + 2] += n_rwb;
                 S.st[ST_N_SHAPE + 3] += n_rout;
                 S.st[ST_N_SHAPE + 4] += n_batch;
+
                 S.st[ST_CYC_POP] += prof_clock(d) - c_in;
             }
             if (lane < KP_LDS_AXES) {
@@ -828,6 +1031,64 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
         if (S.done) break;
         const long long c_slow = prof_clock(d);
         const int pod = S.cur_pod;
+        if (S.topo_pod) {
+            // ================= a pod with topology terms (wave 0) =================
+            // prefilter of this pod's groups, first surviving NodeClaim in slice order; quick accept when it has
+            // absorbed the class, every narrowed key is a single admitted domain and the witness fits; otherwise
+            // the block evaluates candidates from there
+            if (wave == 0) {
+                const long long t0 = prof_clock(d);
+                const int c = S.cur_cls, N = S.N;
+                const uint32_t cfl = d.cls_flags[c];
+                if (lane == 0) S.tp_n = 0;
+                if (cfl & CF_TOPO_CONS) topo_prefilter_setup(d, S, c, lane);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                const long long t1 = prof_clock(d);
+                const int f = topo_scan(d, S, skey, sord, N, S.scan_start, lane);
+                const long long t2 = prof_clock(d);
+                bool quick = false;
+                if (f < N && (cfl & CF_TOPO_QREC) && A > 0) {
+                    const int nc = sord[f], tm = stmpl[nc];
+                    bool ok = nc < NQ && (slast[nc] == (uint16_t)c || ((cfl & CF_NOKEYS) && ((d.tol[c] >> tm) & 1u)));
+                    for (int ai = 0; ai < A && ok; ai++) ok = S.cur_pq[ai] <= shr[ai * NQ + nc];
+                    quick = ok && topo_pinned(d, S, nc);
+                    if (quick) {
+                        if (lane < A) shr[lane * NQ + nc] -= S.cur_pq[lane];
+                        if (lane < R && S.pod_req[lane])
+                            atomicAdd((unsigned long long*)&d.nc_req[(size_t)nc * R + lane], (unsigned long long)S.pod_req[lane]);
+                        topo_record_quick(d, c, nc, tm, lane);
+                        if (lane == 0) {
+                            skey[f]++;
+                            d.pod_result[pod] = nc;
+                            d.pod_order[pod] = S.seq++;
+                            S.dirty_kind = 1;
+                            S.dirty_pos = f;
+                            S.scan_start = 0;
+                            S.st[ST_TOPO_QUICK]++;
+                            S.st[ST_QUICK]++;
+                        }
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    }
+                }
+                if (!quick) collect_candidates(d, S, skey, sord, N, f, 0, lane);
+                if (lane == 0) {
+                    S.topo_quick = quick;
+                    if (d.profile) {
+                        S.st[ST_CYC_TSETUP] += t1 - t0;
+                        S.st[ST_CYC_TSCAN] += t2 - t1;
+                    }
+                }
+            }
+            __syncthreads();
+            if (S.topo_quick) {
+                if (tid == 0) {
+                    S.tp_n = 0;
+                    S.topo_pod = 0;
+                }
+                __syncthreads();
+                continue;
+            }
+        }
         if (S.cls_fill) fill_class_cache(d, S.cur_cls, S.CC, tid, nthr);
 
         // ================= in-flight NodeClaims in slice order: first whose Add succeeds =================
@@ -850,7 +1111,9 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                 const bool fast = !(S.CC.flags & CF_TOPO) &&
                                   (slast[nc] == (uint16_t)S.cur_cls || ((S.CC.flags & CF_NOKEYS) && ((S.CC.tol >> a.tmpl) & 1u)));
                 if (fast && lane == 0) S.ws[wave].memo_ok = 1;
-                const bool ok = fast ? eval_fits_only(d, E, a, S.ws[wave], lane) : eval_wave(d, E, S.CC, a, S.ws[wave], lane);
+                const bool ok = fast ? eval_fits_only(d, E, a, S.ws[wave], lane)
+                                : (S.CC.flags & CF_TOPO_CONS) ? eval_wave<true>(d, E, S.CC, a, S.ws[wave], lane)
+                                                              : eval_wave<false>(d, E, S.CC, a, S.ws[wave], lane);
                 if (lane == 0) {
                     S.fastp[b][wave] = fast;
                     S.acc[b][wave] = ok;
@@ -872,7 +1135,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                 }
             if (tid == 0) S.st[ST_NC_EVALS] += nc_;
             if (win >= 0 || S.scan_done[b]) break;
-            if (wave == 0) collect_candidates(S, skey, sord, S.N, S.scan_next[b], b ^ 1, lane);
+            if (wave == 0) collect_candidates(d, S, skey, sord, S.N, S.scan_next[b], b ^ 1, lane);
             __syncthreads();
             round++;
         }
@@ -927,7 +1190,8 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                         a.force_off = false;
                         a.prof = nullptr;
                         a.host = d.E + S.N;  // NewNodeClaim's fresh hostname (no pod counted there yet)
-                        ok = eval_wave(d, E, S.CC, a, S.ws[wave], lane);
+                        ok = (S.CC.flags & CF_TOPO_CONS) ? eval_wave<true>(d, E, S.CC, a, S.ws[wave], lane)
+                                                         : eval_wave<false>(d, E, S.CC, a, S.ws[wave], lane);
                     }
                     if (lane == 0) S.tacc[wave] = ok;
                 }
@@ -1002,6 +1266,10 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                     d.last_len[pod] = S.qcount;
                 }
             }
+        }
+        if (tid == 0) {
+            S.tp_n = 0;
+            S.topo_pod = 0;
         }
         __syncthreads();
     }

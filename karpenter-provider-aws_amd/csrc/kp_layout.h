@@ -37,6 +37,8 @@
 #define CF_NOKEYS 4u                 // no requirement keys
 #define CF_TOPO 8u                   // topology: constrained by or recorded into some group (never quick-accepted)
 #define CF_TOPO_CONS 16u             // constrained by some group (AddRequirements runs in NodeClaim.Add)
+#define CF_TOPO_QREC 32u             // every recording group's node filter is decidable from a NodeClaim's template
+                                     // alone (no node-affinity filter owned by another class): quick accepts record
 
 // tg_info.x
 #define TG_TYPE 3                    // KP_TOPO_SPREAD / AFFINITY / ANTI_AFFINITY
@@ -213,5 +215,6 @@ enum {
     ST_MEMO_SKIPS, ST_CYC_POP, ST_CYC_SORT, ST_CYC_SCAN, ST_CYC_TMPL, ST_CYC_COMMIT, ST_CYC_SORT_FULL,
     ST_EV_REQ = 16, ST_EV_MASK, ST_EV_OFF, ST_EV_TYPES, ST_EV_MIN, ST_EV_CALLS,
     ST_QUICK = 24, ST_SLOW, ST_WITNESS_MISS, ST_CYC_QPOP, ST_CYC_QSCAN, ST_CYC_QCHECK, ST_CYC_QCOMMIT,
-    ST_N_NOINV = 32, ST_N_WINMOVE, ST_N_LDSSORT, ST_N_PIVOT, ST_N_WINLOAD, ST_N_FLUSH, ST_N_SHAPE, ST_EXIST_PLACED = 44, ST_COUNT = 48
+    ST_N_NOINV = 32, ST_N_WINMOVE, ST_N_LDSSORT, ST_N_PIVOT, ST_N_WINLOAD, ST_N_FLUSH, ST_N_SHAPE, ST_EXIST_PLACED = 44,
+    ST_TOPO_QUICK = 45, ST_CYC_TSETUP, ST_CYC_TSCAN, ST_COUNT = 48
 };
