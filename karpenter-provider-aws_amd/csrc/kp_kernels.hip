@@ -21,6 +21,12 @@
 #include "kp_gosort.h"
 #include "kp_layout.h"
 
+#ifdef KP_NO_TOPO
+#define KP_TOPO_ON 0  // A/B builds only (tools/ab_variants.sh): topology code compiled out
+#else
+#define KP_TOPO_ON 1
+#endif
+
 // ------------------------------------------------------------------------------------------------
 // class × type label compatibility
 // ------------------------------------------------------------------------------------------------
@@ -792,7 +798,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                     if (dkind == 2 || how == 2 || sstart > dpos) sstart = 0;
                     dkind = 0;
                 }
-                if (ctopo) {
+                if (KP_TOPO_ON && ctopo) {
                     // a pod with topology terms: the block handles it (topology prefilter, quick accept with
                     // recording, or the evaluation of candidates); counts change with every placement
                     win_flush();
@@ -1031,7 +1037,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
         if (S.done) break;
         const long long c_slow = prof_clock(d);
         const int pod = S.cur_pod;
-        if (S.topo_pod) {
+        if (KP_TOPO_ON && S.topo_pod) {
             // ================= a pod with topology terms (wave 0) =================
             // prefilter of this pod's groups, first surviving NodeClaim in slice order; quick accept when it has
             // absorbed the class, every narrowed key is a single admitted domain and the witness fits; otherwise
@@ -1112,7 +1118,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                                   (slast[nc] == (uint16_t)S.cur_cls || ((S.CC.flags & CF_NOKEYS) && ((S.CC.tol >> a.tmpl) & 1u)));
                 if (fast && lane == 0) S.ws[wave].memo_ok = 1;
                 const bool ok = fast ? eval_fits_only(d, E, a, S.ws[wave], lane)
-                                : (S.CC.flags & CF_TOPO_CONS) ? eval_wave<true>(d, E, S.CC, a, S.ws[wave], lane)
+                                : (KP_TOPO_ON && (S.CC.flags & CF_TOPO_CONS)) ? eval_wave<true>(d, E, S.CC, a, S.ws[wave], lane)
                                                               : eval_wave<false>(d, E, S.CC, a, S.ws[wave], lane);
                 if (lane == 0) {
                     S.fastp[b][wave] = fast;
@@ -1148,7 +1154,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                 const int pos = S.cand_pos[round & 1][win];
                 const int nc = sord[pos];
                 if (!S.fastp[round & 1][win]) commit_reqs(d, S.CC, S.ws[win], nc, lane);
-                if (S.CC.flags & CF_TOPO)
+                if (KP_TOPO_ON && (S.CC.flags & CF_TOPO))
                     topo_record(d, S.CC, S.ws[win], d.nc_hdr + (size_t)nc * K, d.nc_words + (size_t)nc * d.DW,
                                 d.E + nc, d.nc_tmpl[nc], true, lane);
                 if (lane < TW) d.nc_opts[(size_t)nc * TW + lane] = S.ws[win].opts[lane];
@@ -1190,7 +1196,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                         a.force_off = false;
                         a.prof = nullptr;
                         a.host = d.E + S.N;  // NewNodeClaim's fresh hostname (no pod counted there yet)
-                        ok = (S.CC.flags & CF_TOPO_CONS) ? eval_wave<true>(d, E, S.CC, a, S.ws[wave], lane)
+                        ok = (KP_TOPO_ON && (S.CC.flags & CF_TOPO_CONS)) ? eval_wave<true>(d, E, S.CC, a, S.ws[wave], lane)
                                                          : eval_wave<false>(d, E, S.CC, a, S.ws[wave], lane);
                     }
                     if (lane == 0) S.tacc[wave] = ok;
@@ -1217,7 +1223,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                             d.nc_words[(size_t)n * d.DW + i] = d.cls_words[(size_t)(d.C + jj) * d.DW + i];
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         commit_reqs(d, S.CC, S.ws[wave], n, lane);
-                        if (S.CC.flags & CF_TOPO)
+                        if (KP_TOPO_ON && (S.CC.flags & CF_TOPO))
                             topo_record(d, S.CC, S.ws[wave], d.cls_hdr + (size_t)(d.C + jj) * K,
                                         d.cls_words + (size_t)(d.C + jj) * d.DW, d.E + n, jj, true, lane);
                         if (lane < TW) d.nc_opts[(size_t)n * TW + lane] = S.ws[wave].opts[lane];

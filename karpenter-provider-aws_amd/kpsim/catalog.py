@@ -368,8 +368,9 @@ def fake_catalog(opts: TypeOptions = None, zones=("test-zone-1a", "test-zone-1b"
         by_type.setdefault(t, []).append(z)
         if z not in all_zones:
             all_zones.append(z)
-    subnet_info = [{"zone": z, "zone_id": ""} for z in zones]  # suite subnets carry no ZoneID
-    zone_ids = {z: "" for z in zones}
+    # the suite's EC2NodeClass status subnets (pkg/test/nodeclass.go:103-119): test-zone-1x ↔ tstz1-1x
+    subnet_info = [{"zone": z, "zone_id": "tstz1-" + z.rsplit("-", 1)[-1]} for z in zones]
+    zone_ids = {s["zone"]: s["zone_id"] for s in subnet_info}
     out = []
     for info in infos:
         it = new_instance_type(info, opts, "us-west-2", by_type.get(info["name"], []), subnet_info, fx["bandwidth"],
