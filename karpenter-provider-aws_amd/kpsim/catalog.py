@@ -51,6 +51,7 @@ TYPE_LABEL_KEYS = [
     AWS + "instance-accelerator-manufacturer", AWS + "instance-accelerator-count", AWS + "instance-hypervisor",
     AWS + "instance-encryption-in-transit-supported", RESERVATION_ID, RESERVATION_TYPE,
 ]
+WINDOWS_BUILDS = {"Windows2019": "10.0.17763", "Windows2022": "10.0.20348"}   # pkg/apis/v1/labels.go:112-113
 INSTANCE_TYPE_SCHEME = re.compile(r"(^[a-z]+)(\-[0-9]+tb)?([0-9]+).*\.")
 
 
@@ -217,6 +218,8 @@ def compute_requirements(info, region, offering_zones, subnet_zone_info, opts: T
         labels[AWS + "instance-accelerator-name"] = [_lower_kabob(nd[0]["name"])]
         labels[AWS + "instance-accelerator-manufacturer"] = ["aws"]
         labels[AWS + "instance-accelerator-count"] = [str(nd[0]["count"])]
+    if opts.ami_family in WINDOWS_BUILDS:   # types.go:281-284
+        labels[WINDOWS_BUILD] = [WINDOWS_BUILDS[opts.ami_family]]
     labels[AWS + "instance-cpu-manufacturer"] = [_lower_kabob(info.get("cpu_manufacturer"))]
     ghz = float(info.get("sustained_clock_ghz") or 0.0)
     labels[AWS + "instance-cpu-sustained-clock-speed-mhz"] = [str(_go_round(ghz * 1000))]
@@ -226,8 +229,9 @@ def compute_requirements(info, region, offering_zones, subnet_zone_info, opts: T
     return {k: (v if v else None) if v is not None else None for k, v in labels.items()}
 
 
-def new_instance_type(info, opts: TypeOptions, region, offering_zones, subnet_zone_info, bandwidth, vpclimits):
-    labels = compute_requirements(info, region, offering_zones, subnet_zone_info, opts, bandwidth)
+def new_instance_type(info, opts: TypeOptions, region, offering_zones, subnet_zone_info, bandwidth, vpclimits,
+                      capacity_reservations=()):
+    labels = compute_requirements(info, region, offering_zones, subnet_zone_info, opts, bandwidth, capacity_reservations)
     cap, kube, ev = instance_resources(info, opts, vpclimits)
     return InstanceType(info["name"], labels, cap, cap - kube - ev, [])
 
@@ -354,9 +358,13 @@ def golden_catalog(zones=("test-zone-1a", "test-zone-1b", "test-zone-1c"),
 
 
 def fake_catalog(opts: TypeOptions = None, zones=("test-zone-1a", "test-zone-1b", "test-zone-1c"), fx=None,
-                 extra_infos=(), extra_offerings=()) -> List[InstanceType]:
+                 extra_infos=(), extra_offerings=(), ice=(), spot_prices=None, reservations=None) -> List[InstanceType]:
     """The envtest catalog: pkg/fake 17 types, subnets test-zone-1a/1b/1c (instancetype/suite_test.go:119-137),
-    static us-east-1 prices with spot = on-demand until a spot refresh (pricing.go:443-455)."""
+    static us-east-1 prices with spot = on-demand until a spot refresh (pricing.go:443-455).
+
+    ice: {(capacity type, type name, zone)} marked unavailable (the UnavailableOfferings cache after an ICE,
+    fake.CapacityPool).  spot_prices: {(type name, zone): price} after UpdateSpotPricing — pairs without an entry have
+    no spot price and so no available spot offering (offering.go:148).  reservations: {type name: [cr dicts]}."""
     fx = fx or load_fixtures()
     opts = opts or TypeOptions()
     fake = fx["fake"]
@@ -371,12 +379,20 @@ def fake_catalog(opts: TypeOptions = None, zones=("test-zone-1a", "test-zone-1b"
     # the suite's EC2NodeClass status subnets (pkg/test/nodeclass.go:103-119): test-zone-1x ↔ tstz1-1x
     subnet_info = [{"zone": z, "zone_id": "tstz1-" + z.rsplit("-", 1)[-1]} for z in zones]
     zone_ids = {s["zone"]: s["zone_id"] for s in subnet_info}
+    ice = set(ice)
     out = []
     for info in infos:
-        it = new_instance_type(info, opts, "us-west-2", by_type.get(info["name"], []), subnet_info, fx["bandwidth"],
-                               fx["vpclimits"])
-        od = fx["prices"].get(info["name"])
+        name = info["name"]
+        crs = (reservations or {}).get(name, [])
+        it = new_instance_type(info, opts, "us-west-2", by_type.get(name, []), subnet_info, fx["bandwidth"],
+                               fx["vpclimits"], capacity_reservations=crs)
+        od = fx["prices"].get(name)
         od = float(od) if od is not None else None
-        inject_offerings(it, all_zones, zone_ids, od, lambda z, od=od: od)
+        if spot_prices is None:
+            spot = lambda z, od=od: od   # noqa: E731
+        else:
+            spot = lambda z, name=name: spot_prices.get((name, z))   # noqa: E731
+        inject_offerings(it, all_zones, zone_ids, od, spot, unavailable=lambda ct, z, name=name: (ct, name, z) in ice,
+                         reservations=crs)
         out.append(it)
     return out
