@@ -230,6 +230,86 @@ def capacity_type_preference():  # getCapacityType: reserved > spot > on-demand 
         {"types": ["a", "b"], "ct": abi.KP_CT_ON_DEMAND}]
 
 
+for _sel in ("default", "capacity-block"):
+    def _crt_pins(sel=_sel):  # filter_test.go:213-243 (chain: a capacity-block pin is then narrowed to the cheapest type)
+        cat = [it("pin-instance", offerings=[off("reserved", crt=sel, price=1.0, rid="pin")]),
+               it("filter-instance", offerings=[off("reserved", crt=t, price=5.0, rid="f-" + t)
+                                                for t in ("default", "capacity-block")])]
+        want = ["pin-instance"] + (["filter-instance"] if sel == "default" else [])
+        rids = ["pin"] + (["f-" + sel] if sel == "default" else [])
+        return cat, [req(ct("reserved"))], [{"types": want, "ct": abi.KP_CT_RESERVED, "offer_rids": rids}]
+    _crt_pins.__name__ = "crt_pins_selected_" + _sel.replace("-", "_")
+    CASES.append(_crt_pins)
+
+
+@case
+def reserved_filter_not_reserved():  # filter_test.go:373-397 (NotIn reserved: both types kept, od+spot offerings)
+    cat = [it("non-reserved-instance", offerings=[off("on-demand"), off("spot")]),
+           it("reserved-instance", offerings=[off("on-demand"), off("spot"), off("reserved", zone="1", crt="default")])]
+    return cat, [req(ct("reserved", op="NotIn"))], [{"types": ["non-reserved-instance", "reserved-instance"],
+                                                     "ct": abi.KP_CT_SPOT}]
+
+
+def _spot_zones(with_reserved):  # filter_test.go:513-583
+    zs = lambda *o: list(o)  # noqa: E731
+    kept = [it("expensive-od-instance", offerings=zs(off("on-demand", price=15.0, zone="zone-1a"),
+                                                     off("on-demand", price=15.0, zone="zone-1b"))),
+            it("od-instance", offerings=zs(off("on-demand", price=5.0, zone="zone-1a"),
+                                           off("on-demand", price=10.0, zone="zone-1b"))),
+            it("cheap-spot-instance", offerings=zs(off("spot", price=1.0, zone="zone-1a"),
+                                                   off("spot", price=2.0, zone="zone-1b"))),
+            it("mixed-spot-instance", offerings=zs(off("spot", price=1.0, zone="zone-1a"),
+                                                   off("spot", price=10.0, zone="zone-1b"))),
+            it("mixed-compatible-available-spot-instance", offerings=zs(off("spot", price=1.0, zone="zone-1a"),
+                                                                        off("spot", price=10.0, zone="zone-1c")))]
+    rejected = [it("mixed-unavailable-spot-instance", offerings=zs(off("spot", False, price=1.0, zone="zone-1a"),
+                                                                   off("spot", price=10.0, zone="zone-1b"))),
+                it("mixed-compatible-unavailable-spot-instance", offerings=zs(off("spot", price=10.0, zone="zone-1a"),
+                                                                              off("spot", price=1.0, zone="zone-1c"))),
+                it("expensive-spot-instance", offerings=zs(off("spot", price=10.0, zone="zone-1a"),
+                                                           off("spot", price=10.0, zone="zone-1b")))]
+    cat = kept + rejected
+    r = req(Requirement(CAPACITY_TYPE, "Exists"), Requirement(ZONE, "In", ["zone-1a", "zone-1b"]))
+    if not with_reserved:
+        return cat, [r], [{"type_set": [x.name for x in kept], "ct": abi.KP_CT_SPOT}]
+    # the single-filter It also keeps a type with a reserved offering; in the chain the reserved-offering filter runs
+    # before the spot filter (instance.go:270-298) and keeps only that type
+    cat.append(it("reserved-instance", offerings=zs(off("spot", price=10.0, zone="zone-1a"),
+                                                     off("spot", price=10.0, zone="zone-1b"),
+                                                     off("reserved", zone="zone-1b", crt="default"))))
+    return cat, [r], [{"types": ["reserved-instance"], "ct": abi.KP_CT_RESERVED}]
+
+
+@case
+def spot_filter_compatible_zones():
+    return _spot_zones(False)
+
+
+@case
+def spot_filter_compatible_zones_with_reserved():
+    return _spot_zones(True)
+
+
+def _three_spot():
+    # the instance-type label (absent on filter_test's mocks) lets the chain's Truncate count minValues
+    return [it(n, {"node.kubernetes.io/instance-type": [n]}, offerings=[off(c, price=p)])
+            for n, c, p in (("od-instance", "on-demand", 5.0), ("cheap-spot-instance", "spot", 1.0),
+                            ("expensive-spot-instance", "spot", 10.0))]
+
+
+@case
+def spot_filter_only_spot_compatible():  # filter_test.go:584-603 (od-instance then fails the compatible filter)
+    return _three_spot(), [req(ct("spot"))], [{"types": ["cheap-spot-instance", "expensive-spot-instance"],
+                                               "ct": abi.KP_CT_SPOT}]
+
+
+@case
+def spot_filter_min_values():  # filter_test.go:604-631
+    r = req(Requirement(CAPACITY_TYPE, "Exists"), Requirement("node.kubernetes.io/instance-type", "Exists", [], min_values=2))
+    return _three_spot(), [r], [{"types": ["cheap-spot-instance", "od-instance", "expensive-spot-instance"],
+                                 "ct": abi.KP_CT_SPOT}]
+
+
 def check(cat, res, expect):
     """Asserts a model.LaunchResults against a case's expectations."""
     for i, e in enumerate(expect):
@@ -237,6 +317,8 @@ def check(cat, res, expect):
         assert int(row["status"]) == e.get("status", abi.KP_OK), (i, row)
         if "failed" in e:
             assert int(row["failed_filter"]) == e["failed"]
+        if "type_set" in e:
+            assert sorted(cat[int(t)].name for t in res.types(i)) == sorted(e["type_set"]), i
         if e.get("types") is not None:
             assert [cat[int(t)].name for t in res.types(i)] == e["types"], (i, [cat[int(t)].name for t in res.types(i)])
         if "ct" in e:
