@@ -40,6 +40,7 @@ struct Offering {
     Reqs reqs;
     double price = 0;
     bool available = false;
+    int rid = -1;  // reserved offerings: dense index of the reservation ID (Solver::rid_names)
 };
 
 struct InstanceType {
@@ -167,6 +168,7 @@ struct NodeClaim {
     std::vector<int> pods;
     bool valid = true;
     std::vector<int> truncated;
+    std::vector<int> held;  // reservedOfferings: reservation IDs this NodeClaim holds (sorted rid indices)
 };
 
 struct ExistingNode {
@@ -213,6 +215,13 @@ struct Solver {
     std::vector<TopoGroup> groups;    // Topology.topologyGroups ∪ inverseTopologyGroups
     std::vector<std::vector<int>> t_cons, t_rec;  // per class: groups that constrain / count its pods
     kp_solve_stats stats{};
+    // ReservationManager ([core] scheduling/reservationmanager.go): capacity per reservation ID, the least
+    // ReservationCapacity among the offerings that carry the ID; NodeClaims hold IDs (NodeClaim.reservedOfferings).
+    std::vector<std::string> rid_names;
+    std::vector<int> rcap;
+    int resv_key = -1;         // karpenter.k8s.aws/capacity-reservation-id (cloudprovider.ReservationIDLabel)
+    bool resv_on = false;      // ReservedCapacity feature gate ∧ the catalog has reserved offerings
+    bool resv_strict = true;   // ReservedOfferingModeStrict (provisioning); Fallback in disruption simulations
 
     explicit Solver(Dict& d) : D(d) {}
     const InstanceType& ty(int t) const { return (*tp)[t]; }
@@ -422,12 +431,48 @@ struct Solver {
         for (int k = 0; k < R; k++) requests[k] = nc.requests[k] + pod.req[k];
         std::vector<int> remaining = filter(nc.options, r, requests);
         if (remaining.empty()) return false;
+        std::vector<int> held;
+        if (resv_on && !offerings_to_reserve(nc, remaining, r, held)) return false;
         nc.pods.push_back(li);
         nc.options.swap(remaining);
         nc.requests.swap(requests);
         nc.reqs = std::move(r);
+        if (resv_on) commit_reservations(nc, held);
         topo_record(li, nc.reqs, tm.taints, true);
         return true;
+    }
+
+    // NodeClaim.Add's reservation step: every available reserved offering of the remaining instance types that the
+    // updated requirements are compatible with is reserved for this NodeClaim's hostname (Reserve is idempotent for an
+    // ID the host already holds; otherwise it takes one unit of the ID's capacity, if any is left).  Strict mode fails
+    // the Add when a compatible reserved offering exists but none can be reserved, or when the NodeClaim held
+    // reservations and the updated constraints leave none (ReservedOfferingError).  Read-only: the IDs the Add would
+    // hold are returned, commit_reservations applies them.
+    bool offerings_to_reserve(const NodeClaim& nc, const std::vector<int>& remaining, const Reqs& r,
+                              std::vector<int>& held) const {
+        bool has = false;
+        for (int t : remaining)
+            for (auto& o : ty(t).offerings) {
+                if (o.rid < 0 || !o.available) continue;
+                if (!reqs_compatible(D, r, o.reqs, true)) continue;
+                has = true;
+                if (std::binary_search(nc.held.begin(), nc.held.end(), o.rid) || rcap[o.rid] > 0) held.push_back(o.rid);
+            }
+        std::sort(held.begin(), held.end());
+        held.erase(std::unique(held.begin(), held.end()), held.end());
+        if (resv_strict) {
+            if (has && held.empty()) return false;
+            if (!nc.held.empty() && held.empty()) return false;
+        }
+        return true;
+    }
+    // Reserve the newly held IDs, Release the IDs no longer compatible.
+    void commit_reservations(NodeClaim& nc, std::vector<int>& held) {
+        for (int id : held)
+            if (!std::binary_search(nc.held.begin(), nc.held.end(), id)) rcap[id]--;
+        for (int id : nc.held)
+            if (!std::binary_search(held.begin(), held.end(), id)) rcap[id]++;
+        nc.held.swap(held);
     }
 
     // ExistingNode.Add: Taints.ToleratesPod, Fits(requests + pod, available), Compatible (no undefined-label
@@ -580,6 +625,12 @@ struct Solver {
     void finalize(int max_types) {
         for (auto& nc : ncs) {
             nc.reqs.m.erase(hostname_key);
+            // FinalizeScheduling: a NodeClaim holding reservations gets ReservationIDLabel In [held IDs]
+            if (!nc.held.empty()) {
+                std::vector<std::string> ids;
+                for (int id : nc.held) ids.push_back(rid_names[id]);
+                nc.reqs.add(D, new_req(D, resv_key, OP_IN, ids, false, 0));
+            }
             std::vector<std::pair<double, int>> keyed;
             for (int t : nc.options) keyed.push_back({cheapest(t, nc.reqs), t});
             std::sort(keyed.begin(), keyed.end(), [&](const std::pair<double, int>& a, const std::pair<double, int>& b) {
@@ -643,6 +694,7 @@ static kp_status parse_into(Solver& s, const kp_catalog_view* cat, const kp_solv
     if (s.cpu_axis < 0 || s.mem_axis < 0) return KP_E_INVALID;
     s.hostname_key = D.key("kubernetes.io/hostname");
     s.host_req = new_req(D, s.hostname_key, OP_IN, {"hostname-placeholder"}, false, 0);
+    s.resv_key = D.key("karpenter.k8s.aws/capacity-reservation-id");
     // catalog → []*cloudprovider.InstanceType
     s.own_types.resize(T);
     for (int t = 0; t < T; t++) {
@@ -678,8 +730,27 @@ static kp_status parse_into(Solver& s, const kp_catalog_view* cat, const kp_solv
             else
                 of.reqs.add(D, new_req(D, key, OP_IN, {cat->offering_label_values[(size_t)o * cat->n_offering_keys + k]}, false, 0));
         }
+        // reserved offerings (offering.go:164-194) carry ReservationIDLabel In [id]; NewReservationManager keeps the
+        // least ReservationCapacity per ID
+        auto rit = of.reqs.m.find(s.resv_key);
+        if (rit != of.reqs.m.end() && !rit->second.complement && rit->second.values.size() == 1) {
+            const std::string id = D.vals[s.resv_key][rit->second.values[0]];
+            const int rc = cat->offering_reservation_capacity ? cat->offering_reservation_capacity[o] : 0;
+            int ix = -1;
+            for (size_t i = 0; i < s.rid_names.size(); i++)
+                if (s.rid_names[i] == id) ix = (int)i;
+            if (ix < 0) {
+                ix = (int)s.rid_names.size();
+                s.rid_names.push_back(id);
+                s.rcap.push_back(rc);
+            } else {
+                s.rcap[ix] = std::min(s.rcap[ix], rc);
+            }
+            of.rid = ix;
+        }
         s.own_types[t].offerings.push_back(std::move(of));
     }
+    s.resv_on = s.resv_on && !s.rid_names.empty();
     // pod classes
     s.own_classes.resize(in->n_classes);
     for (int c = 0; c < in->n_classes; c++) {
@@ -918,6 +989,8 @@ extern "C" kp_status orc_solve_opts(const kp_catalog_view* cat, const kp_solve_i
     if (in->min_values_policy != KP_MIN_VALUES_STRICT) return KP_E_UNSUPPORTED;
     auto res = std::make_unique<orc_result>();
     Solver s(res->D);
+    s.resv_on = opts ? opts->reserved_capacity != 0 : true;  // FEATURE_GATES ReservedCapacity (default on)
+    s.resv_strict = true;  // provisioning: scheduling.DisableReservedCapacityFallback
     kp_status st = parse_into(s, cat, in, opts ? opts->preference_policy : KP_PREFERENCE_RESPECT);
     if (st != KP_OK) return st;
     for (int j = 0; j < (int)s.own_existing.size(); j++) s.ex_idx.push_back(j);
@@ -1028,6 +1101,11 @@ static void run_probe(const ConsCtx& X, int probe, kp_probe_result& pr) {
     s.mem_axis = b.mem_axis;
     s.hostname_key = b.hostname_key;
     s.host_req = b.host_req;
+    s.rid_names = b.rid_names;
+    s.rcap = b.rcap;
+    s.resv_key = b.resv_key;
+    s.resv_on = b.resv_on;
+    s.resv_strict = b.resv_strict;
     s.tp = &b.own_types;
     s.cp = &b.own_classes;
     s.pp = &b.own_pods;
@@ -1146,6 +1224,8 @@ extern "C" kp_status orc_consolidate(const kp_catalog_view* cat, const kp_consol
     if (in->mode != KP_CONSOLIDATE_SINGLE && in->mode != KP_CONSOLIDATE_MULTI) return KP_E_INVALID;
     Dict D;
     Solver base(D);
+    base.resv_on = true;        // ReservedCapacity gate on; disruption simulations use ReservedOfferingModeFallback
+    base.resv_strict = false;
     kp_status st = parse_into(base, cat, &in->cluster, KP_PREFERENCE_RESPECT);
     if (st != KP_OK) return st;
     // consolidation over topology-constrained pods (topology counts of the remaining cluster, excluded candidate pods)

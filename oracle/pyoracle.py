@@ -127,11 +127,11 @@ class OracleResult:
             self._h = None
 
 
-def solve(problem, catalog_view=None, preference_policy=0):
+def solve(problem, catalog_view=None, preference_policy=0, reserved_capacity=1):
     """Run the CPU oracle on a kpsim.model.Problem (solver parameters as kp_device_opts).  Returns OracleResult."""
     from kpsim import abi, model
     L = lib()
-    opts = abi.kp_device_opts(preference_policy=preference_policy)
+    opts = abi.kp_device_opts(preference_policy=preference_policy, reserved_capacity=reserved_capacity)
     cv = catalog_view or model.CatalogView(problem.catalog)
     iv = model.SolveInputView(problem)
     cap_nc = max(16, problem.pods.n + 1)

@@ -593,3 +593,164 @@ def ids():
 
 def clone_problem(prob):
     return copy.deepcopy(prob)
+
+
+# ----------------------------------------------------------------------------------------------------------------------
+# reserved capacity in Solve: ReservationManager + FinalizeScheduling's reservation-id requirement
+# ----------------------------------------------------------------------------------------------------------------------
+RESV_CASES: List[Callable] = []
+
+
+def resv_case(fn):
+    RESV_CASES.append(fn)
+    return fn
+
+
+RESVID = "karpenter.k8s.aws/capacity-reservation-id"
+RESVTYPE = "karpenter.k8s.aws/capacity-reservation-type"
+
+
+def _cp_reservations_catalog(fx):
+    """cloudprovider/suite_test.go:1444-1465: one m5.large reservation per reservation type in test-zone-1a, 10 each."""
+    crs = {"m5.large": [{"id": "cr-m5.large-1a-" + t, "zone": Z1A, "type": t, "capacity": 10, "state": "active"}
+                        for t in ("default", "capacity-block")]}
+    return catalog.fake_catalog(fx=fx, reservations=crs)
+
+
+def _reserved_pool():
+    return model.NodePool("default", requirements=[Requirement(CAPACITY_TYPE, "In", ["reserved"])])
+
+
+def _launch_reserved(cat, lres, i, rid):
+    ov = overrides(cat, lres, i)
+    assert int(lres.rows[i]["capacity_type"]) == abi.KP_CT_RESERVED, lres.rows[i]
+    fo = flat_offerings(cat)
+    rids = {fo[int(j)][1].reservation_id for j in lres.offerings(i)}
+    assert rids == {rid} and ov, (rids, rid)
+
+
+@resv_case
+def resv_marks_launched(fx):
+    cat = _cp_reservations_catalog(fx)
+    prob = problem(cat, [_reserved_pool()], [PodClass()], [(0, {})])
+    ids = ("cr-m5.large-1a-capacity-block", "cr-m5.large-1a-default")
+
+    def check(prob, res, reqs):
+        _all_scheduled(prob, res, reqs)
+        assert res.n_nodeclaims == 1 and names(cat, res.nodeclaim_types[0]) == ["m5.large"]
+        assert reqs[0][RESVID][0] is False and reqs[0][RESVID][4] == ids
+
+    def launch_check(cat, lreqs, lres):
+        # both reservations are held; the launch's reservation-type filter prefers default on a price tie
+        _launch_reserved(cat, lres, 0, "cr-m5.large-1a-default")
+    return Kat("resv_marks_launched", "pkg/cloudprovider/suite_test.go:1472-1480", prob, check, launch_check)
+
+
+def _resv_labels(fx, crt):
+    cat = _cp_reservations_catalog(fx)
+    prob = problem(cat, [_reserved_pool()], [PodClass(sel(**{RESVTYPE: crt}))], [(0, {})])
+    rid = "cr-m5.large-1a-" + crt
+
+    def check(prob, res, reqs):
+        _all_scheduled(prob, res, reqs)
+        assert reqs[0][RESVID][4] == (rid,)
+
+    def launch_check(cat, lreqs, lres):
+        _launch_reserved(cat, lres, 0, rid)
+    return Kat("resv_labels_" + crt, "pkg/cloudprovider/suite_test.go:1501-1524", prob, check, launch_check)
+
+
+@resv_case
+def resv_labels_default(fx):
+    return _resv_labels(fx, "default")
+
+
+@resv_case
+def resv_labels_capacity_block(fx):
+    return _resv_labels(fx, "capacity-block")
+
+
+def e2e_reservations(fx, large_cap=1, xlarge_cap=2):
+    """test/suites/scheduling/suite_test.go:771-823: m5.large (1 instance) and m5.xlarge (2) ODCRs in the first zone,
+    NodePool capacity-type In [on-demand, reserved], os In [linux]."""
+    crs = {"m5.large": [{"id": "cr-large", "zone": Z1A, "type": "default", "capacity": large_cap,
+                         "state": "active"}],
+           "m5.xlarge": [{"id": "cr-xlarge", "zone": Z1A, "type": "default", "capacity": xlarge_cap,
+                          "state": "active"}]}
+    cat = catalog.fake_catalog(fx=fx, reservations=crs)
+    np_ = model.NodePool("default", requirements=[Requirement(CAPACITY_TYPE, "In", ["on-demand", "reserved"]),
+                                                  Requirement("kubernetes.io/os", "In", ["linux"])])
+    return cat, np_
+
+
+@resv_case
+def resv_specific_id(fx):
+    cat, np_ = e2e_reservations(fx)
+    prob = problem(cat, [np_], [PodClass([Requirement(RESVID, "In", ["cr-xlarge"])])], [(0, {})])
+
+    def check(prob, res, reqs):
+        _all_scheduled(prob, res, reqs)
+        assert reqs[0][RESVID][4] == ("cr-xlarge",)
+        assert names(cat, res.nodeclaim_types[0]) == ["m5.xlarge"]
+
+    def launch_check(cat, lreqs, lres):
+        _launch_reserved(cat, lres, 0, "cr-xlarge")
+    return Kat("resv_specific_id", "test/suites/scheduling/suite_test.go:824-847", prob, check, launch_check)
+
+
+@resv_case
+def resv_specific_type(fx):
+    cat, np_ = e2e_reservations(fx)
+    cls = PodClass([Requirement(RESVTYPE, "In", ["default"]), Requirement(INSTANCE_TYPE, "In", ["m5.xlarge"])])
+    prob = problem(cat, [np_], [cls], [(0, {})])
+
+    def check(prob, res, reqs):
+        _all_scheduled(prob, res, reqs)
+        assert reqs[0][RESVID][4] == ("cr-xlarge",) and reqs[0][RESVTYPE][4] == ("default",)
+
+    def launch_check(cat, lreqs, lres):
+        _launch_reserved(cat, lres, 0, "cr-xlarge")
+    return Kat("resv_specific_type", "test/suites/scheduling/suite_test.go:850-883", prob, check, launch_check)
+
+
+def _fallback_pods(cat, np_):
+    anti = model.TopologyTerm("anti", model.HOSTNAME, selector=[Requirement("foo", "In", ["bar"])])
+    cls = PodClass([Requirement(INSTANCE_TYPE, "In", ["m5.large"])], labels={"foo": "bar"}, topology=[anti])
+    return problem(cat, [np_], [cls], [(0, {})] * 2)
+
+
+@resv_case
+def resv_fallback_first_solve(fx):
+    """:884-920, first provisioning loop: the first pod reserves the single m5.large instance; the second pod's new
+    NodeClaim has a compatible reserved offering it cannot reserve (ReservedOfferingModeStrict) and waits."""
+    cat, np_ = e2e_reservations(fx)
+    prob = _fallback_pods(cat, np_)
+
+    def check(prob, res, reqs):
+        assert res.n_nodeclaims == 1 and sorted(res.pod_result.tolist()) == [-1, 0]
+        assert reqs[0][RESVID][4] == ("cr-large",)
+
+    def launch_check(cat, lreqs, lres):
+        _launch_reserved(cat, lres, 0, "cr-large")
+    return Kat("resv_fallback_first_solve", "test/suites/scheduling/suite_test.go:884-920", prob, check, launch_check)
+
+
+@resv_case
+def resv_fallback_second_solve(fx):
+    """:884-920, the next loop: the reservation's available count is 0 (offering.go:187, Available = false), so the
+    waiting pod gets an on-demand NodeClaim without a reservation requirement."""
+    cat, np_ = e2e_reservations(fx, large_cap=0)
+    prob = _fallback_pods(cat, np_)
+    prob.pods = synth.pods_from_specs([(0, {})])
+
+    def check(prob, res, reqs):
+        _all_scheduled(prob, res, reqs)
+        assert RESVID not in reqs[0] or reqs[0][RESVID][0] is True or reqs[0][RESVID][4] != ("cr-large",)
+
+    def launch_check(cat, lreqs, lres):
+        assert int(lres.rows[0]["capacity_type"]) == abi.KP_CT_ON_DEMAND
+    return Kat("resv_fallback_second_solve", "test/suites/scheduling/suite_test.go:884-920", prob, check, launch_check)
+
+
+def resv_ids():
+    return [c.__name__ for c in RESV_CASES]

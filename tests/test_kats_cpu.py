@@ -98,3 +98,8 @@ def test_capacity_block_launch_oracle(fx, state):
         assert [(n, z, ct) for n, z, ct, _ in KC.overrides(cat, lres, 0)] == [("c6g.large", KC.Z1A, "reserved")]
     else:
         assert int(row["status"]) == abi.KP_E_INSUFFICIENT_CAPACITY
+
+
+@pytest.mark.parametrize("mk", KC.RESV_CASES, ids=KC.resv_ids())
+def test_kat_reserved_oracle(fx, mk):
+    run_kat_oracle(mk(fx))
