@@ -131,6 +131,10 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
     Ev.slot_zoneid = d.slot_zoneid;
     Ev.roles = &S.roles;
     Ev.min_tmpl_mask = 0;  // minValues templates are rejected by kp_consolidate
+    Ev.ro = nullptr;       // catalogs with reserved offerings are rejected by kp_consolidate
+    Ev.type_ro = nullptr;
+    Ev.rcap = nullptr;
+    Ev.resv_on = 0;
 
     for (int it = 0;; it++) {
         int probe = 0;
@@ -421,6 +425,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 a.force_off = false;
                 a.prof = nullptr;
                 a.host = 0;
+                a.held = 0;
                 st_nc++;
                 if (eval_wave<false>(d, Ev, S.CC, a, S.ws, lane)) {
                     if (lane < S.CC.nck) {
@@ -451,6 +456,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     a.force_off = false;
                     a.prof = nullptr;
                     a.host = 0;
+                    a.held = 0;
                     st_tmpl++;
                     if (!eval_wave<false>(d, Ev, S.CC, a, S.ws, lane)) continue;
                     if (n_nc == 1) {  // a second NodeClaim: computeConsolidation returns NONE

@@ -30,7 +30,9 @@ struct WaveScratch {
     uint64_t minbits[KP_MAX_MIN_WORDS];
     int32_t hr[KP_LDS_AXES];   // quick-accept headroom of the chosen witness type (scaled, lower bound)
     int32_t memo_ok;           // a failed evaluation may be memoised for the shape (it did not depend on topology
-                               // counts: see topo_narrow)
+                               // counts: see topo_narrow, or on reservation capacity: see the reservation step)
+    int32_t rlive;             // success: the new options keep a compatible available reserved offering
+    uint64_t held;             // success: reservation IDs the NodeClaim holds after the Add
 };
 
 // Class-side operands of the evaluation, cached in LDS while consecutive pods share a class.
@@ -79,6 +81,10 @@ struct EvalEnv {
     const int* slot_zoneid;
     const Roles* roles;
     uint32_t min_tmpl_mask;    // templates whose requirements carry minValues
+    const ResvTab* ro;         // reserved offerings (null: none)
+    const uint64_t* type_ro;   // [T] the type's reserved offerings (bits over ro index)
+    const int32_t* rcap;       // ReservationManager capacity by reservation-id value id (FFD kernel LDS)
+    int resv_on;               // run the reservation step of NodeClaim.Add (ReservedOfferingModeStrict)
 };
 
 // Cooperative fill by all threads of the block; contains two __syncthreads().
@@ -194,6 +200,21 @@ __device__ __forceinline__ bool role_dneok(const KpDev& d, const EvalEnv& E, con
     return op_notin_or_dne(req_op(h.flags, popc_words(w, n)));
 }
 
+// Offerings.Available() ∧ reqs.IsCompatible(offering.Requirements) for the reserved offerings (lane i = offering i):
+// capacity-type In [reserved], zone, zone-id, reservation-id In [id], reservation-type In [type] (offering.go:178-186).
+__device__ __forceinline__ uint64_t resv_adm(const KpDev& d, const EvalEnv& E, const ClassCache& CC, const WaveScratch& ws,
+                                             const ReqHdr* Ahdr, const uint64_t* Aw, int lane) {
+    const ResvTab& X = *E.ro;
+    bool ok = false;
+    if (lane < X.n && ((X.avail >> lane) & 1ull)) {
+        const int zid = X.zid[lane], rt = X.rtype[lane];
+        ok = role_adm(d, E, CC, ws, Ahdr, Aw, 1, X.ctv) && role_adm(d, E, CC, ws, Ahdr, Aw, 0, X.zone[lane]) &&
+             (zid < 0 || role_adm(d, E, CC, ws, Ahdr, Aw, 2, zid)) && role_adm(d, E, CC, ws, Ahdr, Aw, 3, X.rid[lane]) &&
+             (rt < 0 ? role_dneok(d, E, CC, ws, Ahdr, Aw, 4) : role_adm(d, E, CC, ws, Ahdr, Aw, 4, rt));
+    }
+    return ballot(ok);
+}
+
 // Quick-accept witness for the NodeClaim state an evaluation produces (options `newword`, totals `tot`).
 // Lazy Fits: request totals only grow, so filterInstanceTypesByRequirements' Fits term applied at every Add equals
 // Fits against the final totals; a NodeClaim whose absorbed class repeats accepts the pod iff SOME option still fits.
@@ -267,6 +288,7 @@ struct EvalIn {
     bool force_off;           // always apply the offering test (template filter)
     long long* prof;          // LDS stage-cycle counters (diagnostics) or null
     int host;                 // topology hostname domain of the candidate (E + NodeClaim id)
+    uint64_t held;            // reservation IDs the candidate holds (0 for a new NodeClaim)
 };
 
 __device__ __forceinline__ int ld_i32(const int32_t* p) {
@@ -471,9 +493,10 @@ __device__ __forceinline__ void topo_record(const KpDev& d, const ClassCache& CC
 
 // Wave-uniform result: does NodeClaim.Add(pod) succeed?  On success ws.opts / ws.hdr / ws.words hold the new state.
 // TOPO: the class is constrained by topology groups (CF_TOPO_CONS): topo_narrow runs between the requirement merge
-// and the type sweep, and keys carried only for narrowing (kneutral) merge as the base requirement.  The two
-// instantiations keep the topology code out of the common path.
-template <bool TOPO>
+// and the type sweep, and keys carried only for narrowing (kneutral) merge as the base requirement.  RESV: the catalog
+// has reserved offerings (offering compatibility over them, and the reservation step when E.resv_on).  The
+// instantiations keep the topology and reservation code out of the common path.
+template <bool TOPO, bool RESV = false>
 __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, const ClassCache& CC, const EvalIn& a,
                                           WaveScratch& ws, int lane) {
     const int TW = d.TW, T = d.T;
@@ -569,6 +592,9 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         }
         mzc = ballot(ok);
     }
+    // reserved offerings: a type also has an offering when one of its reserved offerings is compatible
+    const uint64_t mro =
+        (RESV && E.ro && E.ro->n > 0 && (need_off || E.resv_on)) ? resv_adm(d, E, CC, ws, a.Ahdr, a.Aw, lane) : 0ull;
     EV_STAMP(2);
 
     // ---- request totals over the active axes (the first KP_LDS_AXES live in registers) ----
@@ -617,7 +643,11 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
                                           : d.multi_mask[(size_t)m * T + (t < T ? t : 0)];
             keep &= (tm == 0) | ((tm & am) != 0);
         }
-        if (need_off) keep &= (E.avail[t] & mzc) != 0;
+        if (need_off) {
+            bool off = (E.avail[t] & mzc) != 0;
+            if (RESV && mro) off |= (E.type_ro[t < T ? t : 0] & mro) != 0;
+            keep &= off;
+        }
         if (keep && wit.on) wit.add(av, tot, t);
         const uint64_t nb = ballot(keep);
         if (lane == w) newword = nb;
@@ -669,8 +699,35 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
             if (count < h.minv) return false;
         }
     }
+    // ---- reservations (NodeClaim.Add's offeringsToReserve, ReservedOfferingModeStrict) ----
+    // Every available reserved offering of a remaining type that the updated requirements are compatible with is
+    // reserved for this NodeClaim: an ID it already holds, or one with capacity left.  The Add fails when a compatible
+    // reserved offering exists but none can be reserved, or when the NodeClaim held reservations and none remain
+    // (ReservedOfferingError).  Both depend on the manager's counts, so such a rejection is never memoised.  Read-only
+    // here: the winner's commit takes / releases the capacity.
+    bool rlive = false;
+    if (RESV && E.resv_on) {
+        const ResvTab& X = *E.ro;
+        const int tt = lane < X.n ? X.type[lane] : 0;
+        const uint64_t wd = __shfl(newword, tt >> 6);
+        const bool comp = lane < X.n && ((mro >> lane) & 1ull) && ((wd >> (tt & 63)) & 1ull);
+        const int rid = lane < X.n ? X.rid[lane] : 0;
+        const bool res = comp && (((a.held >> rid) & 1ull) || E.rcap[rid] > 0);
+        const uint64_t cm = ballot(comp), rm = ballot(res);
+        if ((cm && !rm) || (a.held && !rm)) {
+            if (lane == 0) ws.memo_ok = 0;
+            return false;
+        }
+        rlive = cm != 0;
+        const uint64_t nh = wave_or64(res ? (1ull << rid) : 0ull);
+        if (lane == 0) {
+            ws.held = nh;
+            ws.rlive = rlive ? 1 : 0;
+        }
+    }
     if (lane < TW) ws.opts[lane] = newword;
-    wit.finish(d, E, tot, a.tmpl >= 0 && ((E.min_tmpl_mask >> a.tmpl) & 1u), ws, lane);
+    // a NodeClaim that keeps reserved offerings is never quick-accepted (hr = -1): every Add recomputes its reservations
+    wit.finish(d, E, tot, rlive || (a.tmpl >= 0 && ((E.min_tmpl_mask >> a.tmpl) & 1u)), ws, lane);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     EV_STAMP(4);
     return true;

@@ -266,6 +266,18 @@ struct kp_ctx {
     int64_t cons_stats[CS_COUNT] = {};
     // launch selection (kp_launch_select): raw offering rows, incl. reserved offerings
     bool has_reserved = false, launch_ok = true;
+    // reserved offerings in Solve (ReservationManager): <= 64 per catalog
+    bool ro_ok = true;
+    ResvTab h_ro{};
+    std::vector<ResvTab> h_ro_up;            // upload staging of h_ro (outlives the async copy)
+    std::vector<int32_t> ro_off;             // offering row of reserved offering i
+    std::vector<uint64_t> type_ro;           // [T]
+    std::vector<int32_t> rcap0;              // [64]
+    std::vector<double> ro_price;            // [KP_MAX_RO]
+    DBuf<ResvTab> d_ro;
+    DBuf<uint64_t> d_type_ro, d_nc_held;
+    DBuf<int32_t> d_rcap0, d_nc_rlive;
+    DBuf<double> d_ro_price;
     std::string launch_err;
     std::vector<int32_t> l_off_begin, l_off_val, l_ct, l_rt, l_rcap;
     std::vector<double> l_price;
@@ -439,6 +451,7 @@ extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, ui
     c->off_slot.assign(O, -1);
     std::vector<int> off_zone(O), off_ct(O);
     std::vector<uint8_t> avail(O);
+    std::vector<int> ro_rows;
     for (int o = 0; o < O; o++) {
         const int t = v->offering_type[o];
         if (t < 0 || t >= T) return fail(ctx, KP_E_INVALID, "offering_type out of range");
@@ -460,9 +473,11 @@ extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, ui
         lab(krt, srt);
         if (sz != KP_LABEL_IN || sc != KP_LABEL_IN) return fail(ctx, KP_E_UNSUPPORTED, "offering without zone / capacity-type");
         if (sri == KP_LABEL_IN || srt == KP_LABEL_IN || !strcmp(ct, "reserved")) {
-            // reserved offerings (offering.go:164-194) feed kp_launch_select only; Solve / consolidation reject the catalog
+            // reserved offerings (offering.go:164-194): the ResvTab of Solve and the launch tables; consolidation
+            // rejects the catalog
             c->has_reserved = true;
             off_zone[o] = off_ct[o] = -1;
+            ro_rows.push_back(o);
             continue;
         }
         if (sri == KP_LABEL_ABSENT || srt == KP_LABEL_ABSENT)
@@ -503,6 +518,49 @@ extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, ui
     }
     c->avail_zc.assign(T, 0);
     rebuild_avail(c, avail);
+    // reserved offerings: ResvTab (ordered by type), the ReservationManager's initial capacity per reservation ID
+    // (NewReservationManager: the least ReservationCapacity among the offerings carrying the ID)
+    c->ro_ok = (int)ro_rows.size() <= KP_MAX_RO;
+    c->h_ro = ResvTab{};
+    c->ro_off.clear();
+    c->type_ro.assign(T, 0);
+    c->rcap0.assign(64, 0);
+    c->ro_price.assign(KP_MAX_RO, 0.0);
+    if (c->ro_ok && !ro_rows.empty()) {
+        std::stable_sort(ro_rows.begin(), ro_rows.end(), [&](int a, int b) { return c->off_type[a] < c->off_type[b]; });
+        std::vector<uint8_t> seen(64, 0);
+        ResvTab& X = c->h_ro;
+        X.n = (int)ro_rows.size();
+        X.ctv = c->cat.keys[c->key_ct].id("reserved");
+        for (int i = 0; i < X.n; i++) {
+            const int o = ro_rows[i];
+            auto lab = [&](int k, int& state) -> const char* {
+                state = k < 0 ? KP_LABEL_ABSENT : v->offering_label_state[(size_t)o * KO + k];
+                return k < 0 ? nullptr : v->offering_label_values[(size_t)o * KO + k];
+            };
+            int sz, sc, szi, sri, srt;
+            const char* z = lab(kz, sz);
+            const char* ct = lab(kc, sc);
+            const char* zi = lab(kzi, szi);
+            const char* ri = lab(kri, sri);
+            const char* rt = lab(krt, srt);
+            if (strcmp(ct, "reserved") != 0 || sri != KP_LABEL_IN)
+                return fail(ctx, KP_E_UNSUPPORTED, "reserved offering without capacity-type reserved / reservation-id");
+            X.type[i] = c->off_type[o];
+            X.zone[i] = c->cat.keys[c->key_zone].id(z);
+            X.zid[i] = szi == KP_LABEL_IN ? c->cat.keys[c->key_zoneid].id(zi) : -1;
+            X.rid[i] = c->cat.keys[c->key_resvid].id(ri);
+            X.rtype[i] = srt == KP_LABEL_IN ? c->cat.keys[c->key_resvtype].id(rt) : -1;
+            if (X.rid[i] >= 64) return fail(ctx, KP_E_UNSUPPORTED, "more than 64 capacity reservation IDs");
+            if (avail[o]) X.avail |= 1ull << i;
+            const int rc = v->offering_reservation_capacity ? v->offering_reservation_capacity[o] : 0;
+            c->rcap0[X.rid[i]] = seen[X.rid[i]] ? std::min(c->rcap0[X.rid[i]], rc) : rc;
+            seen[X.rid[i]] = 1;
+            c->type_ro[X.type[i]] |= 1ull << i;
+            c->ro_price[i] = v->offering_price[o];
+            c->ro_off.push_back(o);
+        }
+    }
     // multi-valued keys: value masks (<= 64 values)
     c->cat_kflags.assign(Kc, 0);
     c->cat_multi.assign(Kc, -1);
@@ -581,6 +639,11 @@ extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, ui
     HIPCHK(c->d_slot_zoneid.upload(c->slot_zoneid, s));
     HIPCHK(c->d_name_rank.upload(rank, s));
     HIPCHK(c->d_nonneg.upload(nonneg, s));
+    c->h_ro_up.assign(1, c->h_ro);
+    HIPCHK(c->d_ro.upload(c->h_ro_up, s));
+    HIPCHK(c->d_type_ro.upload(c->type_ro, s));
+    HIPCHK(c->d_rcap0.upload(c->rcap0, s));
+    HIPCHK(c->d_ro_price.upload(c->ro_price, s));
     {
         kp_status lst = upload_launch_tables(c, v, avail);
         if (lst != KP_OK) return lst;
@@ -603,6 +666,11 @@ extern "C" kp_status kp_catalog_patch_avail(kp_ctx* ctx, const uint8_t* availabl
     HIPCHK(hipSetDevice(ctx->device));
     rebuild_avail(ctx, std::vector<uint8_t>(available, available + n));
     HIPCHK(ctx->d_avail_zc.upload(ctx->avail_zc, ctx->stream));
+    ctx->h_ro.avail = 0;
+    for (size_t i = 0; i < ctx->ro_off.size(); i++)
+        if (available[ctx->ro_off[i]]) ctx->h_ro.avail |= 1ull << i;
+    ctx->h_ro_up.assign(1, ctx->h_ro);
+    HIPCHK(ctx->d_ro.upload(ctx->h_ro_up, ctx->stream));
     for (int o = 0; o < n; o++) ctx->l_avail[o] = available[o] ? 1 : 0;
     HIPCHK(ctx->d_l_avail.upload(ctx->l_avail, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -620,8 +688,11 @@ extern "C" kp_status kp_catalog_patch_price(kp_ctx* ctx, const int32_t* idx, con
         if (idx[i] < 0 || idx[i] >= (int)ctx->off_type.size()) return fail(ctx, KP_E_INVALID, "offering index");
         if (ctx->off_slot[idx[i]] >= 0)
             ctx->slot_price[(size_t)ctx->off_type[idx[i]] * KP_MAX_SLOTS + ctx->off_slot[idx[i]]] = price[i];
+        for (size_t r = 0; r < ctx->ro_off.size(); r++)
+            if (ctx->ro_off[r] == idx[i]) ctx->ro_price[r] = price[i];
         ctx->l_price[idx[i]] = price[i];
     }
+    HIPCHK(ctx->d_ro_price.upload(ctx->ro_price, ctx->stream));
     HIPCHK(ctx->d_slot_price.upload(ctx->slot_price, ctx->stream));
     HIPCHK(ctx->d_l_price.upload(ctx->l_price, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -850,8 +921,8 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     if (!ctx || !in) return KP_E_INVALID;
     ctx->cons_prep_valid = false;
     if (!ctx->have_catalog) return fail(ctx, KP_E_STATE, "kp_solve before kp_catalog_upload");
-    if (ctx->has_reserved)
-        return fail(ctx, KP_E_UNSUPPORTED, "Solve over a catalog with reserved offerings is not supported by this build");
+    if (ctx->has_reserved && !ctx->ro_ok)
+        return fail(ctx, KP_E_UNSUPPORTED, "Solve over a catalog with more than 64 reserved offerings");
     const auto t0 = clk::now();
     HIPCHK(hipSetDevice(ctx->device));
     kp_ctx* c = ctx;
@@ -1242,6 +1313,8 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     HIPCHK(c->d_nc_opts.ensure((size_t)NCcap * TW));
     HIPCHK(c->d_nc_req.ensure((size_t)NCcap * R));
     HIPCHK(c->d_nc_tmpl.ensure(NCcap));
+    HIPCHK(c->d_nc_held.ensure(NCcap));
+    HIPCHK(c->d_nc_rlive.ensure(NCcap));
     HIPCHK(c->d_qbuf.ensure(std::max(P, 1)));
     HIPCHK(c->d_last_len.ensure(std::max(P, 1)));
     HIPCHK(c->d_pod_result.ensure(std::max(P, 1)));
@@ -1496,6 +1569,13 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         }
         d.qshift[ai] = sh;
     }
+    d.ro = c->h_ro.n > 0 ? c->d_ro.p : nullptr;
+    d.type_ro = c->d_type_ro.p;
+    d.ro_price = c->d_ro_price.p;
+    d.resv_on = (c->reserved_capacity && c->h_ro.n > 0) ? 1 : 0;
+    d.rcap0 = c->d_rcap0.p;
+    d.nc_held = c->d_nc_held.p;
+    d.nc_rlive = c->d_nc_rlive.p;
     if (!kp_ffd_plan_lds(d, KP_LDS_BYTES)) return fail(ctx, KP_E_UNSUPPORTED, "FFD kernel LDS plan exceeds 160 KB");
     c->P = P;
     c->C = C;

@@ -131,6 +131,10 @@ __global__ __launch_bounds__(64) void template_init_kernel(KpDev d) {
     E.slot_zoneid = d.slot_zoneid;
     E.roles = &roles;
     E.min_tmpl_mask = d.min_keys[(size_t)j * KP_MAX_CLASS_KEYS] >= 0 ? (1u << j) : 0u;
+    E.ro = d.ro;
+    E.type_ro = d.type_ro;
+    E.rcap = nullptr;
+    E.resv_on = 0;  // NewScheduler's option filter: offerings only, no reservations
     EvalIn a;
     a.Ahdr = d.empty_hdr;
     a.Aw = d.empty_words;
@@ -142,7 +146,8 @@ __global__ __launch_bounds__(64) void template_init_kernel(KpDev d) {
     a.force_off = true;
     a.prof = nullptr;
     a.host = 0;
-    const bool ok = eval_wave<false>(d, E, CC, a, ws, lane);
+    a.held = 0;
+    const bool ok = d.ro ? eval_wave<false, true>(d, E, CC, a, ws, lane) : eval_wave<false>(d, E, CC, a, ws, lane);
     if (lane < d.TW) d.tmpl_opts[(size_t)j * d.TW + lane] = ok ? ws.opts[lane] : 0;
     if (lane == 0) d.tmpl_ok[j] = ok ? 1 : 0;
 }
@@ -169,6 +174,8 @@ struct FfdShared {
     // control state: owned by wave 0 inside its fast loop, by the block between the slow-path barriers
     int N, qhead, qcount, done, cur_pod, cur_cls, cur_shape, prev_shape;
     int dirty_kind, dirty_pos, seq, err, cls_fill, scan_start, any_rej;
+    int rej_volatile;              // a candidate of the current pod was rejected for a reason that may not last
+                                   // (reservation capacity): the next pod of the shape rescans from the start
     int xstart;                    // every existing node < xstart has rejected the current shape
     uint32_t cur_tol;              // tolerations word of the current shape's class (bit 31: no requirement keys)
     int32_t cur_pq[KP_LDS_AXES];   // scaled quick-accept requests of the current shape
@@ -412,10 +419,22 @@ __device__ inline uint64_t limit_filter(const KpDev& d, int j, uint64_t o, int l
 
 __device__ __forceinline__ long long prof_clock(const KpDev& d) { return d.profile ? __builtin_amdgcn_s_memtime() : 0; }
 
+// The winner's reservations (one lane): ReservationManager.Reserve for the IDs newly held, Release for the IDs the
+// Add no longer holds (NodeClaim.Add's reservedOfferings update), then the NodeClaim's held set and liveness.
+__device__ __forceinline__ void commit_reservations(const KpDev& d, int32_t* rcap, const WaveScratch& ws, int nc,
+                                                    uint64_t old) {
+    const uint64_t nh = ws.held;
+    for (uint64_t x = nh & ~old; x; x &= x - 1) rcap[__ffsll((unsigned long long)x) - 1]--;
+    for (uint64_t x = old & ~nh; x; x &= x - 1) rcap[__ffsll((unsigned long long)x) - 1]++;
+    __hip_atomic_store(&d.nc_held[nc], nh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&d.nc_rlive[nc], ws.rlive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Scheduler.Solve.  Wave 0 runs the queue, the sort.Slice emulation and the first-fit scan for as many pods as it
 // can resolve alone: a pod whose first non-rejected NodeClaim (slice order) has already absorbed the pod's class
 // and whose witness type still fits is placed without an evaluation (exact: see pick_witness).  Any other pod is
 // handed to all 8 waves (the slow path: NodeClaim.Add of up to 8 candidates at once, or the templates).
+template <bool RESV>
 __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     FfdShared& S = *reinterpret_cast<FfdShared*>(smem);
@@ -427,6 +446,9 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
     uint64_t* const sAvail = reinterpret_cast<uint64_t*>(smem + d.off_avail);
     uint16_t* const sMulti = reinterpret_cast<uint16_t*>(smem + d.off_multi);
     int32_t* const shr = reinterpret_cast<int32_t*>(smem + d.off_hr);       // [A][NQ] witness headroom
+    // reserved offerings and the ReservationManager's capacities (RESV instantiation: the catalog has reserved offerings)
+    ResvTab* const sRo = RESV ? reinterpret_cast<ResvTab*>(smem + d.off_ro) : nullptr;
+    int32_t* const sRcap = RESV ? reinterpret_cast<int32_t*>(smem + d.off_ro + sizeof(ResvTab)) : nullptr;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nthr = blockDim.x;
     const int T = d.T, TW = d.TW, K = d.K, R = d.R, P = d.P;
     const int TP = d.lds_tpad, NQ = d.lds_nq, A = d.lds_A, NCMAX = d.lds_ncmax;
@@ -452,6 +474,12 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
         S.roles.woff[tid] = rk >= 0 ? d.woff[rk] : 0;
         S.roles.nw[tid] = rk >= 0 ? d.nw[rk] : 0;
     }
+    if (RESV) {
+        const int32_t* src = reinterpret_cast<const int32_t*>(d.ro);
+        int32_t* dst = reinterpret_cast<int32_t*>(sRo);
+        for (int i = tid; i < (int)(sizeof(ResvTab) / 4); i += nthr) dst[i] = src[i];
+        for (int i = tid; i < 64; i += nthr) sRcap[i] = d.rcap0[i];  // NewReservationManager
+    }
     for (int p = tid; p < P; p += nthr) {
         d.qbuf[p] = d.queue0[p];
         d.last_len[p] = 0;
@@ -471,6 +499,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
         S.dirty_pos = 0;
         S.scan_start = 0;
         S.any_rej = 0;
+        S.rej_volatile = 0;
         S.xstart = 0;
         S.seq = 0;
         S.err = 0;
@@ -491,6 +520,10 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
     E.slot_ct = S.slot_ct;
     E.slot_zoneid = S.slot_zoneid;
     E.roles = &S.roles;
+    E.ro = sRo;
+    E.type_ro = d.type_ro;
+    E.rcap = sRcap;
+    E.resv_on = RESV ? d.resv_on : 0;
     {
         uint32_t mmask = 0;
         for (int j = 0; j < d.NT; j++)
@@ -1114,21 +1147,24 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                 a.force_off = false;
                 a.prof = d.profile ? &S.st[ST_EV_REQ] : nullptr;
                 a.host = d.E + nc;
-                const bool fast = !(S.CC.flags & CF_TOPO) &&
+                a.held = (RESV && d.resv_on) ? ld_u64(&d.nc_held[nc]) : 0ull;
+                // a NodeClaim that keeps reserved offerings re-runs the whole Add (its reservations are recomputed)
+                const bool fast = !(S.CC.flags & CF_TOPO) && !(RESV && d.resv_on && ld_i32(&d.nc_rlive[nc])) &&
                                   (slast[nc] == (uint16_t)S.cur_cls || ((S.CC.flags & CF_NOKEYS) && ((S.CC.tol >> a.tmpl) & 1u)));
                 if (fast && lane == 0) S.ws[wave].memo_ok = 1;
                 const bool ok = fast ? eval_fits_only(d, E, a, S.ws[wave], lane)
-                                : (KP_TOPO_ON && (S.CC.flags & CF_TOPO_CONS)) ? eval_wave<true>(d, E, S.CC, a, S.ws[wave], lane)
-                                                              : eval_wave<false>(d, E, S.CC, a, S.ws[wave], lane);
+                                : (KP_TOPO_ON && (S.CC.flags & CF_TOPO_CONS)) ? eval_wave<true, RESV>(d, E, S.CC, a, S.ws[wave], lane)
+                                                              : eval_wave<false, RESV>(d, E, S.CC, a, S.ws[wave], lane);
                 if (lane == 0) {
                     S.fastp[b][wave] = fast;
                     S.acc[b][wave] = ok;
                     if (!ok && S.ws[wave].memo_ok) {
                         // rejected this shape for good (positions are stable here); a rejection that depended on
-                        // topology counts is not memoised
+                        // topology counts or reservation capacity is not memoised
                         skey[S.cand_pos[b][wave]] |= 0x80000000u;
                         S.any_rej = 1;
                     }
+                    if (!ok && !S.ws[wave].memo_ok) S.rej_volatile = 1;
                     if (fast) atomicAdd((unsigned long long*)&S.st[ST_WITNESS_MISS], 1ull);
                 }
             }
@@ -1153,7 +1189,10 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
             if (wave == win) {
                 const int pos = S.cand_pos[round & 1][win];
                 const int nc = sord[pos];
-                if (!S.fastp[round & 1][win]) commit_reqs(d, S.CC, S.ws[win], nc, lane);
+                if (!S.fastp[round & 1][win]) {
+                    commit_reqs(d, S.CC, S.ws[win], nc, lane);
+                    if (RESV && d.resv_on && lane == 0) commit_reservations(d, sRcap, S.ws[win], nc, ld_u64(&d.nc_held[nc]));
+                }
                 if (KP_TOPO_ON && (S.CC.flags & CF_TOPO))
                     topo_record(d, S.CC, S.ws[win], d.nc_hdr + (size_t)nc * K, d.nc_words + (size_t)nc * d.DW,
                                 d.E + nc, d.nc_tmpl[nc], true, lane);
@@ -1168,7 +1207,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                     S.dirty_pos = pos;
                     // every position before the winner rejected this shape for good, unless rejections depended on
                     // topology counts (not memoised; the next pod of the shape rescans them)
-                    S.scan_start = (S.CC.flags & CF_TOPO) ? 0 : pos;
+                    S.scan_start = ((S.CC.flags & CF_TOPO) || S.rej_volatile) ? 0 : pos;
                     d.pod_result[pod] = nc;
                     d.pod_order[pod] = S.seq++;
                 }
@@ -1196,8 +1235,9 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                         a.force_off = false;
                         a.prof = nullptr;
                         a.host = d.E + S.N;  // NewNodeClaim's fresh hostname (no pod counted there yet)
-                        ok = (KP_TOPO_ON && (S.CC.flags & CF_TOPO_CONS)) ? eval_wave<true>(d, E, S.CC, a, S.ws[wave], lane)
-                                                         : eval_wave<false>(d, E, S.CC, a, S.ws[wave], lane);
+                        a.held = 0;
+                        ok = (KP_TOPO_ON && (S.CC.flags & CF_TOPO_CONS)) ? eval_wave<true, RESV>(d, E, S.CC, a, S.ws[wave], lane)
+                                                         : eval_wave<false, RESV>(d, E, S.CC, a, S.ws[wave], lane);
                     }
                     if (lane == 0) S.tacc[wave] = ok;
                 }
@@ -1223,6 +1263,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                             d.nc_words[(size_t)n * d.DW + i] = d.cls_words[(size_t)(d.C + jj) * d.DW + i];
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         commit_reqs(d, S.CC, S.ws[wave], n, lane);
+                        if (RESV && d.resv_on && lane == 0) commit_reservations(d, sRcap, S.ws[wave], n, 0ull);
                         if (KP_TOPO_ON && (S.CC.flags & CF_TOPO))
                             topo_record(d, S.CC, S.ws[wave], d.cls_hdr + (size_t)(d.C + jj) * K,
                                         d.cls_words + (size_t)(d.C + jj) * d.DW, d.E + n, jj, true, lane);
@@ -1276,6 +1317,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
         if (tid == 0) {
             S.tp_n = 0;
             S.topo_pod = 0;
+            S.rej_volatile = 0;
         }
         __syncthreads();
     }
@@ -1300,7 +1342,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(KpDev d) {
     __shared__ uint64_t s_key[KP_MAX_TYPES];
     __shared__ uint32_t s_rank[KP_MAX_TYPES];
     __shared__ uint16_t s_t[KP_MAX_TYPES];
-    __shared__ uint64_t s_mzc;
+    __shared__ uint64_t s_mzc, s_mro;
     __shared__ int s_n;
     __shared__ uint64_t s_bits[KP_MAX_MIN_WORDS];
     __shared__ int s_ok;
@@ -1313,7 +1355,21 @@ __global__ __launch_bounds__(256) void finalize_kernel(KpDev d) {
     if (tid == 0) {
         s_n = 0;
         s_ok = 1;
+        // FinalizeScheduling: a NodeClaim holding reservations gets ReservationIDLabel In [held IDs] (Requirements.Add:
+        // the held IDs are admitted by the NodeClaim's requirement, so the intersection is In [held], minValues kept)
+        const uint64_t held = d.resv_on ? d.nc_held[nc] : 0ull;
+        if (held && d.key_resvid >= 0) {
+            ReqHdr* hp = d.nc_hdr + (size_t)nc * d.K + d.key_resvid;
+            uint64_t* wp = d.nc_words + (size_t)nc * d.DW + d.woff[d.key_resvid];
+            ReqHdr o{};
+            o.flags = RF_DEF | (hp->flags & RF_MIN);
+            o.minv = hp->minv;
+            *hp = o;
+            wp[0] = held;
+            for (int i = 1; i < d.nw[d.key_resvid]; i++) wp[i] = 0;
+        }
     }
+    __syncthreads();
     if (wave == 0) {
         // Offerings.Available().Compatible(reqs) over slots, reqs = NodeClaim requirements (hostname removed)
         bool ok = false;
@@ -1336,10 +1392,33 @@ __global__ __launch_bounds__(256) void finalize_kernel(KpDev d) {
         }
         const uint64_t m = ballot(ok);
         if (lane == 0) s_mzc = m;
+        // the reserved offerings
+        bool rok = false;
+        if (d.ro && lane < d.ro->n && ((d.ro->avail >> lane) & 1ull)) {
+            auto adm = [&](int k, int v) -> bool {
+                if (k < 0) return true;
+                const ReqHdr h = H[k];
+                if (!(h.flags & RF_DEF)) return true;
+                return req_has(d, k, v, h, W + d.woff[k]);
+            };
+            const int zid = d.ro->zid[lane], rt = d.ro->rtype[lane];
+            bool rtok;
+            if (rt >= 0) {
+                rtok = adm(d.key_resvtype, rt);
+            } else {
+                const ReqHdr h = d.key_resvtype >= 0 ? H[d.key_resvtype] : ReqHdr{};
+                rtok = !(h.flags & RF_DEF) ||
+                       op_notin_or_dne(req_op(h.flags, popc_words(W + d.woff[d.key_resvtype], d.nw[d.key_resvtype])));
+            }
+            rok = adm(d.key_ct, d.ro->ctv) && adm(d.key_zone, d.ro->zone[lane]) && (zid < 0 || adm(d.key_zoneid, zid)) &&
+                  adm(d.key_resvid, d.ro->rid[lane]) && rtok;
+        }
+        const uint64_t rm = ballot(rok);
+        if (lane == 0) s_mro = rm;
     }
     if (tid < d.R) s_tot[tid] = d.nc_req[(size_t)nc * d.R + tid];
     __syncthreads();
-    const uint64_t mzc = s_mzc;
+    const uint64_t mzc = s_mzc, mro = s_mro;
     for (int t = tid; t < TW * 64; t += blockDim.x) {
         if (t >= T) continue;
         if (!((d.nc_opts[(size_t)nc * TW + (t >> 6)] >> (t & 63)) & 1ull)) continue;
@@ -1357,6 +1436,10 @@ __global__ __launch_bounds__(256) void finalize_kernel(KpDev d) {
             const int s = __ffsll((unsigned long long)m) - 1;
             m &= m - 1;
             const double p = d.slot_price[(size_t)t * KP_MAX_SLOTS + s];
+            price = p < price ? p : price;
+        }
+        for (uint64_t rmk = mro ? d.type_ro[t] & mro : 0ull; rmk; rmk &= rmk - 1) {
+            const double p = d.ro_price[__ffsll((unsigned long long)rmk) - 1];
             price = p < price ? p : price;
         }
         const int i = atomicAdd(&s_n, 1);
@@ -1464,6 +1547,8 @@ bool kp_ffd_plan_lds(KpDev& d, int max_bytes) {
     off = al(off + 8 * (size_t)tp);
     d.off_multi = (int)off;
     if (d.multi16) off = al(off + 2 * (size_t)d.n_multi * tp);
+    d.off_ro = (int)off;
+    if (d.ro) off = al(off + sizeof(ResvTab) + 4 * 64);
     d.off_hr = (int)off;
     if ((int)off > max_bytes) return false;
     d.lds_A = d.n_active <= KP_LDS_AXES ? d.n_active : 0;
@@ -1498,11 +1583,14 @@ hipError_t kp_launch_template_init(const KpDev& d, hipStream_t s) {
 // Per-device kernel attributes: called by kp_ctx_create with the ctx's device current (every ctx, so a second ctx on
 // another device of the same process gets them too; the call is idempotent and needs no process-wide flag).
 hipError_t kp_ffd_set_attributes() {
-    return hipFuncSetAttribute((const void*)ffd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, KP_LDS_BYTES);
+    hipError_t e = hipFuncSetAttribute((const void*)ffd_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, KP_LDS_BYTES);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute((const void*)ffd_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, KP_LDS_BYTES);
 }
 hipError_t kp_launch_ffd(const KpDev& d, hipStream_t s) {
     const size_t bytes = (size_t)d.lds_bytes;
-    hipLaunchKernelGGL(ffd_kernel, dim3(1), dim3(KP_NWAVES * 64), bytes, s, d);
+    if (d.ro) hipLaunchKernelGGL(ffd_kernel<true>, dim3(1), dim3(KP_NWAVES * 64), bytes, s, d);
+    else hipLaunchKernelGGL(ffd_kernel<false>, dim3(1), dim3(KP_NWAVES * 64), bytes, s, d);
     return hipGetLastError();
 }
 hipError_t kp_launch_finalize(const KpDev& d, int n_nodeclaims, hipStream_t s) {

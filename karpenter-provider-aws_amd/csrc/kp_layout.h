@@ -68,6 +68,21 @@ struct ReqHdr {
     int64_t lt;
 };
 
+// Reserved offerings of the catalog (offering.go:164-194), at most 64, as one evaluation reads them (LDS copy in the
+// FFD kernel).  Requirement values are value ids of the offering-role keys; `rid` (the reservation-id value id, < 64
+// because the key is multi-valued) is also the ReservationManager slot.
+#define KP_MAX_RO 64
+struct ResvTab {
+    int32_t n;                       // reserved offerings
+    int32_t ctv;                     // capacity-type value id of "reserved"
+    int32_t type[KP_MAX_RO];         // instance type row
+    int32_t zone[KP_MAX_RO];         // zone value id
+    int32_t zid[KP_MAX_RO];          // zone-id value id or -1 (no zone-id requirement)
+    int32_t rid[KP_MAX_RO];          // reservation-id value id
+    int32_t rtype[KP_MAX_RO];        // reservation-type value id or -1 (DoesNotExist)
+    uint64_t avail;                  // bit i: Offering.Available
+};
+
 // Device pointers and sizes for one solve (catalog tables + solve tables + state + outputs).
 struct KpDev {
     // ---------------- catalog (uploaded once per epoch) ----------------
@@ -204,9 +219,18 @@ struct KpDev {
     int32_t lds_nstage;              // allocatable axes staged in LDS
     int32_t lds_A;                   // quick-accept axes (= n_active when n_active <= KP_LDS_AXES, else 0)
     int32_t lds_nq;                  // NodeClaims with a quick-accept headroom row (ids < lds_nq)
-    int32_t off_key, off_ord, off_last, off_tmpl, off_alloc, off_avail, off_multi, off_hr;
+    int32_t off_key, off_ord, off_last, off_tmpl, off_alloc, off_avail, off_multi, off_ro, off_hr;
     int32_t lds_bytes;
     int32_t qshift[KP_LDS_AXES];     // headroom scale per quick axis: value >> qshift fits 30 bits
+
+    // ---------------- reserved capacity ([core] scheduling/reservationmanager.go, nodeclaim.go) ----------------
+    const ResvTab* ro;               // reserved offerings (global copy)
+    const uint64_t* type_ro;         // [T] bits over ro index: the type's reserved offerings
+    const double* ro_price;          // [KP_MAX_RO]
+    int32_t resv_on;                 // ReservedCapacity gate ∧ reserved offerings exist: NodeClaim.Add reserves
+    const int32_t* rcap0;            // [64] ReservationManager capacity per reservation-id value id (least over offerings)
+    uint64_t* nc_held;               // [NCcap] reservation IDs a NodeClaim holds (NodeClaim.reservedOfferings' IDs)
+    int32_t* nc_rlive;               // [NCcap] the NodeClaim's options keep a compatible available reserved offering
 };
 
 // stats slots

@@ -358,7 +358,33 @@ def config5_catalog(catalog, n_default=40, n_block=20, seed=SEED, expiring_frac=
             capacity_type="reserved", zone=z.zone, price=z.price / 10_000_000.0, available=not expiring,
             zone_id=z.zone_id, reservation_id="cr-%05d" % j,
             reservation_type="default" if j < n_default else "capacity-block", reservation_capacity=rcap))
+        # computeRequirements for a type with capacity reservations (types.go:181-234): capacity-type gains
+        # "reserved", and the reservation ID / type labels list the type's reservations
+        res = [o for o in it.offerings if o.capacity_type == "reserved"]
+        cts = list(it.labels.get(CAPACITY_TYPE) or [])
+        if "reserved" not in cts:
+            it.labels[CAPACITY_TYPE] = cts + ["reserved"]
+        it.labels[model.RESERVATION_ID] = sorted({o.reservation_id for o in res})
+        it.labels[model.RESERVATION_TYPE] = sorted({o.reservation_type for o in res})
     return cat
+
+
+def config5(n_pods=200_000, n_classes=250, catalog=None, golden=None, seed=SEED) -> Problem:
+    """BASELINE configs[4] as a Solve: config-2 pods over the reserved-offering catalog (config5_catalog), with the
+    ODCR NodePool patterns of designs/odcr.md:140-180 — an ODCR-only NodePool first (capacity-type In [reserved],
+    weight 100), a tainted NodePool with on-demand fallback (In [on-demand, reserved]) and the spot/on-demand
+    default.  Provisioning runs the ReservationManager in strict mode."""
+    if catalog is None:
+        catalog = config5_catalog(golden if golden is not None else golden_catalog(seed=seed), seed=seed)
+    prob = config2(n_pods=n_pods, n_classes=n_classes, catalog=catalog, seed=seed)
+    taint_key = "example.com/dedicated"
+    prob.nodepools = [
+        NodePool(name="odcr", weight=100, requirements=[Requirement(CAPACITY_TYPE, "In", ["reserved"])]),
+        NodePool(name="dedicated", weight=50, requirements=[Requirement(CAPACITY_TYPE, "In", ["on-demand", "reserved"])],
+                 taints=[Taint(taint_key, "", "NoSchedule")]),
+        default_nodepool("default", capacity_types=("spot", "on-demand"), weight=10),
+    ]
+    return prob
 
 
 def launch_requests(catalog, n=1000, seed=SEED, with_min_values=True):

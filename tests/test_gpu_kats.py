@@ -19,7 +19,7 @@ def ctx():
     c.close()
 
 
-@pytest.mark.parametrize("mk", KC.CASES, ids=KC.ids())
+@pytest.mark.parametrize("mk", KC.CASES + KC.RESV_CASES, ids=KC.ids() + KC.resv_ids())
 def test_kat_device(ctx, fx, mk):
     k = mk(fx)
     cv = model.CatalogView(k.problem.catalog)

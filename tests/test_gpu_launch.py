@@ -71,8 +71,10 @@ def test_patches_reach_launch(ctx, golden):
     LC.assert_same(dev, orc)
 
 
-def test_solve_rejects_reserved_catalog(ctx, golden):
-    cat = synth.config5_catalog(golden)
+def test_solve_rejects_over_64_reserved_offerings(ctx, golden):
+    """Solve keeps the reserved offerings in one 64-bit table (ResvTab); a larger catalog is refused loudly (the launch
+    path has no such limit)."""
+    cat = synth.config5_catalog(golden, n_default=50, n_block=20)
     ctx.upload_catalog(model.CatalogView(cat))
     prob = synth.config2(n_pods=200, catalog=cat)
     with pytest.raises(native.KpError) as e:
