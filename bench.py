@@ -21,7 +21,13 @@ for p in (os.path.join(ROOT, "karpenter-provider-aws_amd"), os.path.join(ROOT, "
 
 import numpy as np  # noqa: E402
 
+T_START = time.perf_counter()
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+
+
+def log(msg):
+    """Progress to stderr (a long silent run looks hung to the GPU harness)."""
+    print("[bench %.0fs] %s" % (time.perf_counter() - T_START, msg), file=sys.stderr, flush=True)
 
 
 def algorithmic_bytes(stats, n_nodeclaims, T, R=12, K_bytes=64):
@@ -223,12 +229,10 @@ def launch_leg(a, golden, local, rank, world, dist, barrier):
     return out
 
 
-def topology_leg(a, cat, local, rank, world, dist, barrier):
-    """BASELINE configs[2]: 50k pods with zonal + hostname topology spread and hostname anti-affinity over five weighted
-    NodePools with cpu limits (synth.config3).  Same step as the headline leg: one kp_solve_execute with HBM-resident
-    inputs; replicas across ranks (weak scaling, no collective)."""
+def solve_leg(a, cat, prob, metric, workload, cpu_sample, local, rank, world, dist, barrier):
+    """A further Solve workload, same step as the headline leg: one kp_solve_execute with HBM-resident inputs; replicas
+    across ranks (weak scaling, no collective); CPU baseline on a seeded subsample, with device parity on it."""
     from kpsim import model, native, synth
-    prob = synth.config3(n_pods=a.pods, catalog=cat)
     ctx = native.Context(local)
     ctx.upload_catalog(model.CatalogView(cat))
     iv = model.SolveInputView(prob)
@@ -237,6 +241,7 @@ def topology_leg(a, cat, local, rank, world, dist, barrier):
     t = time.perf_counter()
     ctx.solve(iv, out)
     e2e_ms = (time.perf_counter() - t) * 1e3
+    log("%s: first solve %.1f ms" % (workload.split(":")[0], e2e_ms))
     res = out.results()
     ctx.prepare(iv)
     for _ in range(a.warmup):
@@ -258,16 +263,14 @@ def topology_leg(a, cat, local, rank, world, dist, barrier):
     P, T = prob.pods.n, len(cat)
     B = algorithmic_bytes(res.stats, res.n_nodeclaims, T)
     achieved = B / (kt[3] / 1e3) / 1e9
-    n_topo = int(sum(1 for c in prob.pods.class_id if prob.classes[int(c)].topology))
     line = {
-        "metric": "pods scheduled/sec (Solve, config3: topology spread + anti-affinity, 5 weighted NodePools)",
+        "metric": metric,
         "value": P * a.steps * world / elapsed,
         "unit": "pods/s",
         "n_gpus": world,
         "ms_per_step": elapsed / a.steps * 1e3,
         "scaling": "weak",
-        "config": {"workload": "config3: %d pods (%d with topology terms), 250 classes x %d types, 5 NodePools" %
-                               (P, n_topo, T), "parallelism": "replicas" if world > 1 else "single"},
+        "config": {"workload": workload, "parallelism": "replicas" if world > 1 else "single"},
         "kernel_ms": {"queue_sort": float(kt[0]), "class_mask": float(kt[1]), "template_init": float(kt[2]),
                       "ffd": float(kt[3]), "finalize": float(kt[4])},
         "end_to_end_ms": e2e_ms,
@@ -281,12 +284,13 @@ def topology_leg(a, cat, local, rank, world, dist, barrier):
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         import parity
         import pyoracle
-        sample = synth.subsample(prob, min(P, a.topo_cpu_sample))
+        sample = synth.subsample(prob, min(P, cpu_sample))
+        log("cpu baseline: oracle on %d pods" % sample.pods.n)
         t = time.perf_counter()
         orc = pyoracle.solve(sample)
         cpu_s = time.perf_counter() - t
         line["cpu_baseline"] = {"value": sample.pods.n / cpu_s, "unit": "pods/s", "cores": 1, "kind": "port",
-                                "sample": "oracle (1 thread) on a seeded %d-pod subsample of config3: %.2f s"
+                                "sample": "oracle (1 thread) on a seeded %d-pod subsample: %.2f s"
                                           % (sample.pods.n, cpu_s)}
         try:
             parity.assert_same(parity.run_device(ctx, sample),
@@ -297,6 +301,28 @@ def topology_leg(a, cat, local, rank, world, dist, barrier):
             line["parity_vs_cpu_baseline"] = False
     ctx.close()
     return line
+
+
+def topology_leg(a, cat, local, rank, world, dist, barrier):
+    """BASELINE configs[2]: 50k pods with zonal + hostname topology spread and hostname anti-affinity over five weighted
+    NodePools with cpu limits (synth.config3)."""
+    from kpsim import synth
+    prob = synth.config3(n_pods=a.pods, catalog=cat)
+    n_topo = int(sum(1 for c in prob.pods.class_id if prob.classes[int(c)].topology))
+    return solve_leg(a, cat, prob, "pods scheduled/sec (Solve, config3: topology spread + anti-affinity, 5 weighted NodePools)",
+                     "config3: %d pods (%d with topology terms), 250 classes x %d types, 5 NodePools"
+                     % (prob.pods.n, n_topo, len(cat)), a.topo_cpu_sample, local, rank, world, dist, barrier)
+
+
+def reserved_leg(a, cat, local, rank, world, dist, barrier):
+    """BASELINE configs[4] as a Solve: config-2 pods over the catalog with 60 reserved offerings (40 ODCR, 20 capacity
+    blocks), ODCR-first NodePools; the ReservationManager runs in strict mode (synth.config5)."""
+    from kpsim import synth
+    cat5 = synth.config5_catalog(cat)
+    prob = synth.config5(n_pods=a.resv_pods, catalog=cat5)
+    return solve_leg(a, cat5, prob, "pods scheduled/sec (Solve, config5: reserved offerings, ODCR-first NodePools)",
+                     "config5: %d pods, 250 classes x %d types (60 reserved offerings), 3 NodePools"
+                     % (prob.pods.n, len(cat5)), a.resv_cpu_sample, local, rank, world, dist, barrier)
 
 
 def main():
@@ -313,6 +339,9 @@ def main():
     ap.add_argument("--no-launch", action="store_true")
     ap.add_argument("--no-topology", action="store_true")
     ap.add_argument("--topo-cpu-sample", type=int, default=12_000, help="pods in config3's CPU-baseline sample")
+    ap.add_argument("--no-reserved", action="store_true")
+    ap.add_argument("--resv-pods", type=int, default=200_000, help="config5 Solve pods")
+    ap.add_argument("--resv-cpu-sample", type=int, default=40_000, help="pods in config5's CPU-baseline sample")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -377,9 +406,15 @@ def main():
     achieved = B / ffd_s / 1e9
     traffic = pmc_traffic("ffd")
 
+    log("config2 solve leg done: %.1f ms/step" % (elapsed / a.steps * 1e3))
     cons = None if a.no_consolidation else consolidation_leg(a, cat, local, rank, world, dist, barrier)
+    log("consolidation leg done")
     launch = None if a.no_launch else launch_leg(a, cat, local, rank, world, dist, barrier)
+    log("launch leg done")
     topo = None if a.no_topology else topology_leg(a, cat, local, rank, world, dist, barrier)
+    log("topology leg done")
+    resv = None if a.no_reserved else reserved_leg(a, cat, local, rank, world, dist, barrier)
+    log("reserved leg done")
 
     cpu = None
     parity_ok = None
@@ -388,6 +423,7 @@ def main():
         import pyoracle
         full = a.cpu_sample <= 0 or a.cpu_sample >= prob.pods.n
         sample = prob if full else synth.subsample(prob, a.cpu_sample)
+        log("cpu baseline: oracle on %d pods" % sample.pods.n)
         t = time.perf_counter()
         orc = pyoracle.solve(sample)
         cpu_s = time.perf_counter() - t
@@ -439,6 +475,7 @@ def main():
             "consolidation": cons,
             "launch": launch,
             "topology": topo,
+            "reserved": resv,
         }
         print(json.dumps(line))
     ctx.close()

@@ -703,8 +703,8 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
     // Every available reserved offering of a remaining type that the updated requirements are compatible with is
     // reserved for this NodeClaim: an ID it already holds, or one with capacity left.  The Add fails when a compatible
     // reserved offering exists but none can be reserved, or when the NodeClaim held reservations and none remain
-    // (ReservedOfferingError).  Both depend on the manager's counts, so such a rejection is never memoised.  Read-only
-    // here: the winner's commit takes / releases the capacity.
+    // (ReservedOfferingError).  A rejection that depends on the manager's counts is never memoised.  Read-only here:
+    // the winner's commit takes / releases the capacity.
     bool rlive = false;
     if (RESV && E.resv_on) {
         const ResvTab& X = *E.ro;
@@ -715,7 +715,9 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         const bool res = comp && (((a.held >> rid) & 1ull) || E.rcap[rid] > 0);
         const uint64_t cm = ballot(comp), rm = ballot(res);
         if ((cm && !rm) || (a.held && !rm)) {
-            if (lane == 0) ws.memo_ok = 0;
+            // with no compatible reserved offering at all (cm == 0) the outcome does not depend on the manager's
+            // counts, and a NodeClaim's compatible set only shrinks while its held set stays non-empty: for good
+            if (lane == 0 && cm) ws.memo_ok = 0;
             return false;
         }
         rlive = cm != 0;

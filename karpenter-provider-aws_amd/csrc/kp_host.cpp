@@ -266,6 +266,7 @@ struct kp_ctx {
     int64_t cons_stats[CS_COUNT] = {};
     // launch selection (kp_launch_select): raw offering rows, incl. reserved offerings
     bool has_reserved = false, launch_ok = true;
+    std::string solve_unsupported;           // catalog the Solve tables cannot hold (launch selection still works)
     // reserved offerings in Solve (ReservationManager): <= 64 per catalog
     bool ro_ok = true;
     ResvTab h_ro{};
@@ -278,6 +279,7 @@ struct kp_ctx {
     DBuf<uint64_t> d_type_ro, d_nc_held;
     DBuf<int32_t> d_rcap0, d_nc_rlive;
     DBuf<double> d_ro_price;
+    DBuf<int32_t> d_trace;                   // KPSIM_TRACE_POD diagnostics
     std::string launch_err;
     std::vector<int32_t> l_off_begin, l_off_val, l_ct, l_rt, l_rcap;
     std::vector<double> l_price;
@@ -388,6 +390,7 @@ extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, ui
     c->type_names.assign(v->type_names, v->type_names + T);
     c->cat = Dicts();
     c->has_reserved = false;
+    c->solve_unsupported.clear();
     // label keys (type requirements) then offering keys
     std::vector<int> lk(KL), ok(v->n_offering_keys);
     for (int k = 0; k < KL; k++) lk[k] = c->cat.key(normalize(v->label_keys[k]));
@@ -551,7 +554,10 @@ extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, ui
             X.zid[i] = szi == KP_LABEL_IN ? c->cat.keys[c->key_zoneid].id(zi) : -1;
             X.rid[i] = c->cat.keys[c->key_resvid].id(ri);
             X.rtype[i] = srt == KP_LABEL_IN ? c->cat.keys[c->key_resvtype].id(rt) : -1;
-            if (X.rid[i] >= 64) return fail(ctx, KP_E_UNSUPPORTED, "more than 64 capacity reservation IDs");
+            if (X.rid[i] >= 64) {  // more than 64 reservation IDs: Solve refuses the catalog (solve_unsupported)
+                c->ro_ok = false;
+                break;
+            }
             if (avail[o]) X.avail |= 1ull << i;
             const int rc = v->offering_reservation_capacity ? v->offering_reservation_capacity[o] : 0;
             c->rcap0[X.rid[i]] = seen[X.rid[i]] ? std::min(c->rcap0[X.rid[i]], rc) : rc;
@@ -559,6 +565,12 @@ extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, ui
             c->type_ro[X.type[i]] |= 1ull << i;
             c->ro_price[i] = v->offering_price[o];
             c->ro_off.push_back(o);
+        }
+        if (!c->ro_ok) {
+            c->h_ro = ResvTab{};
+            c->ro_off.clear();
+            c->type_ro.assign(T, 0);
+            c->rcap0.assign(64, 0);
         }
     }
     // multi-valued keys: value masks (<= 64 values)
@@ -570,7 +582,11 @@ extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, ui
         for (int t = 0; t < T && !present; t++) present = st[(size_t)t * Kc + k] != KP_LABEL_ABSENT;
         if (!present && !multi[k]) continue;  // offering-only key absent from every type
         if (multi[k]) {
-            if (c->cat.keys[k].vals.size() > 64) return fail(ctx, KP_E_UNSUPPORTED, "multi-valued label with > 64 values");
+            if (c->cat.keys[k].vals.size() > 64) {
+                // the Solve tables hold a multi-valued label as a 64-bit value mask; the launch path has no such limit
+                c->solve_unsupported = "multi-valued label " + c->cat.keys[k].name + " with > 64 values";
+                continue;
+            }
             c->cat_kflags[k] = KF_CAT_MULTI;
             c->cat_multi[k] = c->n_multi++;
         } else {
@@ -921,6 +937,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     if (!ctx || !in) return KP_E_INVALID;
     ctx->cons_prep_valid = false;
     if (!ctx->have_catalog) return fail(ctx, KP_E_STATE, "kp_solve before kp_catalog_upload");
+    if (!ctx->solve_unsupported.empty()) return fail(ctx, KP_E_UNSUPPORTED, "Solve: " + ctx->solve_unsupported);
     if (ctx->has_reserved && !ctx->ro_ok)
         return fail(ctx, KP_E_UNSUPPORTED, "Solve over a catalog with more than 64 reserved offerings");
     const auto t0 = clk::now();
@@ -1543,6 +1560,15 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.stats = c->d_stats.p;
     d.err = c->d_err.p;
     d.profile = getenv("KPSIM_PROFILE") ? 1 : 0;
+    // KPSIM_TRACE_POD=p traces pod p; KPSIM_TRACE_CLASS=c traces every slow-path pod of class c (trace_pod = -2 - c)
+    d.trace_pod = getenv("KPSIM_TRACE_POD") ? atoi(getenv("KPSIM_TRACE_POD"))
+                  : getenv("KPSIM_TRACE_CLASS") ? -2 - atoi(getenv("KPSIM_TRACE_CLASS")) : -1;
+    d.trace_max = getenv("KPSIM_TRACE_MAXPOD") ? atoi(getenv("KPSIM_TRACE_MAXPOD")) : INT32_MAX;
+    d.trace = nullptr;
+    if (d.trace_pod != -1) {
+        HIPCHK(c->d_trace.ensure(1 + 6 * KP_TRACE_N + 3 + 2 * 4096));
+        d.trace = c->d_trace.p;
+    }
     d.G = G;
     d.key_host = th.key_host;
     d.tg_info = c->d_tg_info.p;
@@ -1624,6 +1650,7 @@ extern "C" kp_status kp_solve_execute(kp_ctx* ctx) {
                              c->d_sort_temp.p, &tb, s, &q0));
     }
     d.queue0 = q0;
+    if (d.trace) HIPCHK(hipMemsetAsync(d.trace, 0, sizeof(int32_t), s));
     HIPCHK(hipEventRecord(c->ev[1], s));
     HIPCHK(kp_launch_class_mask(d, s));
     HIPCHK(hipEventRecord(c->ev[2], s));
@@ -1639,6 +1666,21 @@ extern "C" kp_status kp_solve_execute(kp_ctx* ctx) {
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]));
         c->kernel_ms[i] = ms;
+    }
+    if (d.trace) {  // KPSIM_TRACE_POD diagnostics
+        std::vector<int32_t> tr(1 + 6 * KP_TRACE_N + 3 + 2 * 4096);
+        HIPCHK(hipMemcpy(tr.data(), d.trace, tr.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+        fprintf(stderr, "[kpsim trace] pod %d: %d evaluations\n", d.trace_pod, tr[0]);
+        for (int i = std::max(0, tr[0] - KP_TRACE_N); i < tr[0]; i++) {  // ring: the last KP_TRACE_N entries
+            const int32_t* e = &tr[1 + 6 * (i % KP_TRACE_N)];
+            fprintf(stderr, "[kpsim trace]   pod %d nc %d ok %d flags %d pos %d held %08x\n", e[0], e[1], e[2], e[3],
+                    e[4], (unsigned)e[5]);
+        }
+        const int32_t* sl = &tr[1 + 6 * KP_TRACE_N];
+        fprintf(stderr, "[kpsim trace] slice N %d scan_start %d first candidate pos %d\n", sl[0], sl[1], sl[2]);
+        for (int i = 0; i < std::min(sl[0], 4096); i++)
+            fprintf(stderr, "[kpsim trace]   pos %d nc %d pods %d rej %d\n", i, sl[3 + 2 * i], sl[4 + 2 * i] & 0x7FFFFFFF,
+                    (int)(((uint32_t)sl[4 + 2 * i]) >> 31));
     }
     c->ns_exec = ns_since(t0);
     c->executed = true;
@@ -1802,6 +1844,7 @@ extern "C" kp_status kp_consolidate_prepare(kp_ctx* ctx, const kp_consolidate_in
     ctx->cons_prep_valid = false;
     if (ctx->has_reserved)
         return fail(ctx, KP_E_UNSUPPORTED, "consolidation over a catalog with reserved offerings is not supported by this build");
+    if (!ctx->solve_unsupported.empty()) return fail(ctx, KP_E_UNSUPPORTED, "consolidation: " + ctx->solve_unsupported);
     if (in->mode != KP_CONSOLIDATE_SINGLE && in->mode != KP_CONSOLIDATE_MULTI)
         return fail(ctx, KP_E_INVALID, "unknown consolidation mode");
     const kp_solve_input& cl = in->cluster;

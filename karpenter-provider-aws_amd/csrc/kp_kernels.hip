@@ -434,8 +434,9 @@ __device__ __forceinline__ void commit_reservations(const KpDev& d, int32_t* rca
 // can resolve alone: a pod whose first non-rejected NodeClaim (slice order) has already absorbed the pod's class
 // and whose witness type still fits is placed without an evaluation (exact: see pick_witness).  Any other pod is
 // handed to all 8 waves (the slow path: NodeClaim.Add of up to 8 candidates at once, or the templates).
-template <bool RESV>
+template <bool RESV, bool TOPO>
 __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
+    constexpr bool TOPO_ON = KP_TOPO_ON && TOPO;  // the solve has topology groups
     extern __shared__ __attribute__((aligned(16))) char smem[];
     FfdShared& S = *reinterpret_cast<FfdShared*>(smem);
     uint32_t* const skey = reinterpret_cast<uint32_t*>(smem + d.off_key);   // len(Pods) by slice position
@@ -580,7 +581,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
             int done = 0, err = S.err;
             int c = S.cur_cls;
             // the current shape's class carries topology (CF_TOPO): such pods are handled by the block
-            bool ctopo = c >= 0 && (d.cls_flags[c] & CF_TOPO);
+            bool ctopo = TOPO_ON && c >= 0 && (d.cls_flags[c] & CF_TOPO);
             uint32_t tl = S.cur_tol;
             int pq[KP_LDS_AXES];
 #pragma unroll
@@ -696,7 +697,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                         any_rej = 0;
                     }
                     c = rl32(vc, off);
-                    ctopo = (d.cls_flags[c] & CF_TOPO) != 0;
+                    ctopo = TOPO_ON && (d.cls_flags[c] & CF_TOPO) != 0;
                     tl = (uint32_t)rl32((int)vtol, off);
 #pragma unroll
                     for (int ai = 0; ai < KP_LDS_AXES; ai++) pq[ai] = rl32(vq[ai], off);
@@ -831,7 +832,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                     if (dkind == 2 || how == 2 || sstart > dpos) sstart = 0;
                     dkind = 0;
                 }
-                if (KP_TOPO_ON && ctopo) {
+                if (TOPO_ON && ctopo) {
                     // a pod with topology terms: the block handles it (topology prefilter, quick accept with
                     // recording, or the evaluation of candidates); counts change with every placement
                     win_flush();
@@ -1029,6 +1030,9 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                 S.dirty_pos = dpos;
                 S.scan_start = sstart;
                 S.any_rej = any_rej;
+                // reset here, behind the barrier that opens the slow path: the winner wave reads it at its commit,
+                // which no barrier separates from the end of the iteration
+                S.rej_volatile = 0;
                 S.done = done;
                 S.err = err;
                 S.cur_cls = c;
@@ -1070,7 +1074,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
         if (S.done) break;
         const long long c_slow = prof_clock(d);
         const int pod = S.cur_pod;
-        if (KP_TOPO_ON && S.topo_pod) {
+        if (TOPO_ON && S.topo_pod) {
             // ================= a pod with topology terms (wave 0) =================
             // prefilter of this pod's groups, first surviving NodeClaim in slice order; quick accept when it has
             // absorbed the class, every narrowed key is a single admitted domain and the witness fits; otherwise
@@ -1132,6 +1136,18 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
 
         // ================= in-flight NodeClaims in slice order: first whose Add succeeds =================
         int round = 0, win = -1;
+        if (d.trace && pod == d.trace_pod && wave == 0) {  // diagnostics: the slice as the slow path sees it
+            int* sl = d.trace + 1 + 6 * KP_TRACE_N;
+            if (lane == 0) {
+                sl[0] = S.N;
+                sl[1] = S.scan_start;
+                sl[2] = S.cand_pos[0][0];
+            }
+            for (int i = lane; i < S.N && i < 4096; i += 64) {
+                sl[3 + 2 * i] = sord[i];
+                sl[4 + 2 * i] = (int)skey[i];
+            }
+        }
         for (;;) {
             const int b = round & 1;
             if (wave < S.n_cand[b]) {
@@ -1153,8 +1169,20 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                                   (slast[nc] == (uint16_t)S.cur_cls || ((S.CC.flags & CF_NOKEYS) && ((S.CC.tol >> a.tmpl) & 1u)));
                 if (fast && lane == 0) S.ws[wave].memo_ok = 1;
                 const bool ok = fast ? eval_fits_only(d, E, a, S.ws[wave], lane)
-                                : (KP_TOPO_ON && (S.CC.flags & CF_TOPO_CONS)) ? eval_wave<true, RESV>(d, E, S.CC, a, S.ws[wave], lane)
+                                : (TOPO_ON && (S.CC.flags & CF_TOPO_CONS)) ? eval_wave<true, RESV>(d, E, S.CC, a, S.ws[wave], lane)
                                                               : eval_wave<false, RESV>(d, E, S.CC, a, S.ws[wave], lane);
+                if (d.trace && (pod == d.trace_pod || (S.cur_cls == -2 - d.trace_pod && pod <= d.trace_max)) && lane == 0) {
+                    const int i = atomicAdd(&d.trace[0], 1);
+                    {  // ring of the last KP_TRACE_N entries
+                        int* e = d.trace + 1 + 6 * (i % KP_TRACE_N);
+                        e[0] = pod;
+                        e[1] = nc;
+                        e[2] = ok;
+                        e[3] = S.ws[wave].memo_ok | (fast << 1) | ((RESV ? ld_i32(&d.nc_rlive[nc]) : 0) << 2);
+                        e[4] = S.cand_pos[b][wave];
+                        e[5] = (int)(a.held & 0xFFFFFFFFu);
+                    }
+                }
                 if (lane == 0) {
                     S.fastp[b][wave] = fast;
                     S.acc[b][wave] = ok;
@@ -1193,7 +1221,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                     commit_reqs(d, S.CC, S.ws[win], nc, lane);
                     if (RESV && d.resv_on && lane == 0) commit_reservations(d, sRcap, S.ws[win], nc, ld_u64(&d.nc_held[nc]));
                 }
-                if (KP_TOPO_ON && (S.CC.flags & CF_TOPO))
+                if (TOPO_ON && (S.CC.flags & CF_TOPO))
                     topo_record(d, S.CC, S.ws[win], d.nc_hdr + (size_t)nc * K, d.nc_words + (size_t)nc * d.DW,
                                 d.E + nc, d.nc_tmpl[nc], true, lane);
                 if (lane < TW) d.nc_opts[(size_t)nc * TW + lane] = S.ws[win].opts[lane];
@@ -1208,6 +1236,18 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                     // every position before the winner rejected this shape for good, unless rejections depended on
                     // topology counts (not memoised; the next pod of the shape rescans them)
                     S.scan_start = ((S.CC.flags & CF_TOPO) || S.rej_volatile) ? 0 : pos;
+                    if (d.trace && S.cur_cls == -2 - d.trace_pod && pod <= d.trace_max) {
+                        const int i = atomicAdd(&d.trace[0], 1);
+                        {
+                            int* e = d.trace + 1 + 6 * (i % KP_TRACE_N);
+                            e[0] = pod;
+                            e[1] = -1000 - nc;
+                            e[2] = S.scan_start;
+                            e[3] = S.rej_volatile;
+                            e[4] = pos;
+                            e[5] = 0;
+                        }
+                    }
                     d.pod_result[pod] = nc;
                     d.pod_order[pod] = S.seq++;
                 }
@@ -1236,8 +1276,19 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                         a.prof = nullptr;
                         a.host = d.E + S.N;  // NewNodeClaim's fresh hostname (no pod counted there yet)
                         a.held = 0;
-                        ok = (KP_TOPO_ON && (S.CC.flags & CF_TOPO_CONS)) ? eval_wave<true, RESV>(d, E, S.CC, a, S.ws[wave], lane)
+                        ok = (TOPO_ON && (S.CC.flags & CF_TOPO_CONS)) ? eval_wave<true, RESV>(d, E, S.CC, a, S.ws[wave], lane)
                                                          : eval_wave<false, RESV>(d, E, S.CC, a, S.ws[wave], lane);
+                    }
+                    if (d.trace && pod == d.trace_pod && lane == 0) {
+                        const int i = atomicAdd(&d.trace[0], 1);
+                        {
+                            int* e = d.trace + 1 + 6 * (i % KP_TRACE_N);
+                            e[0] = -1;
+                            e[1] = -1 - j;
+                            e[2] = ok;
+                            e[3] = S.ws[wave].memo_ok;
+                            e[4] = e[5] = 0;
+                        }
                     }
                     if (lane == 0) S.tacc[wave] = ok;
                 }
@@ -1264,7 +1315,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         commit_reqs(d, S.CC, S.ws[wave], n, lane);
                         if (RESV && d.resv_on && lane == 0) commit_reservations(d, sRcap, S.ws[wave], n, 0ull);
-                        if (KP_TOPO_ON && (S.CC.flags & CF_TOPO))
+                        if (TOPO_ON && (S.CC.flags & CF_TOPO))
                             topo_record(d, S.CC, S.ws[wave], d.cls_hdr + (size_t)(d.C + jj) * K,
                                         d.cls_words + (size_t)(d.C + jj) * d.DW, d.E + n, jj, true, lane);
                         if (lane < TW) d.nc_opts[(size_t)n * TW + lane] = S.ws[wave].opts[lane];
@@ -1317,7 +1368,6 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
         if (tid == 0) {
             S.tp_n = 0;
             S.topo_pod = 0;
-            S.rej_volatile = 0;
         }
         __syncthreads();
     }
@@ -1583,14 +1633,22 @@ hipError_t kp_launch_template_init(const KpDev& d, hipStream_t s) {
 // Per-device kernel attributes: called by kp_ctx_create with the ctx's device current (every ctx, so a second ctx on
 // another device of the same process gets them too; the call is idempotent and needs no process-wide flag).
 hipError_t kp_ffd_set_attributes() {
-    hipError_t e = hipFuncSetAttribute((const void*)ffd_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, KP_LDS_BYTES);
-    if (e != hipSuccess) return e;
-    return hipFuncSetAttribute((const void*)ffd_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, KP_LDS_BYTES);
+    const void* ks[4] = {(const void*)ffd_kernel<false, false>, (const void*)ffd_kernel<false, true>,
+                         (const void*)ffd_kernel<true, false>, (const void*)ffd_kernel<true, true>};
+    for (const void* k : ks) {
+        const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, KP_LDS_BYTES);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 hipError_t kp_launch_ffd(const KpDev& d, hipStream_t s) {
     const size_t bytes = (size_t)d.lds_bytes;
-    if (d.ro) hipLaunchKernelGGL(ffd_kernel<true>, dim3(1), dim3(KP_NWAVES * 64), bytes, s, d);
-    else hipLaunchKernelGGL(ffd_kernel<false>, dim3(1), dim3(KP_NWAVES * 64), bytes, s, d);
+    // instantiation by solve features: reserved offerings (RESV), topology groups (TOPO)
+    const dim3 g(1), b(KP_NWAVES * 64);
+    if (d.ro && d.G > 0) hipLaunchKernelGGL((ffd_kernel<true, true>), g, b, bytes, s, d);
+    else if (d.ro) hipLaunchKernelGGL((ffd_kernel<true, false>), g, b, bytes, s, d);
+    else if (d.G > 0) hipLaunchKernelGGL((ffd_kernel<false, true>), g, b, bytes, s, d);
+    else hipLaunchKernelGGL((ffd_kernel<false, false>), g, b, bytes, s, d);
     return hipGetLastError();
 }
 hipError_t kp_launch_finalize(const KpDev& d, int n_nodeclaims, hipStream_t s) {

@@ -29,7 +29,8 @@
 #define KP_MAX_MIN_WORDS 64          // value bitset for a minValues distinct count (4096 values)
 #define KP_LDS_BYTES (160 * 1024)    // LDS per workgroup on gfx950
 #define KP_MAX_TOPO 8                // topology groups constraining one pod class
-#define KP_MAX_TOPO_REC 16           // topology groups recording one pod class's placements
+#define KP_MAX_TOPO_REC 16
+#define KP_TRACE_N 16384             // diagnostics ring (KPSIM_TRACE_*)           // topology groups recording one pod class's placements
 
 // cls_flags bits
 #define CF_OFFERING 1u               // constrains an offering key
@@ -172,6 +173,9 @@ struct KpDev {
     int64_t* stats;                  // [16]
     int32_t* err;                    // [1] device-side error code (capacity overflow etc.)
     int32_t profile;                 // accumulate per-stage evaluation cycles (diagnostics)
+    int32_t trace_pod;               // diagnostics (KPSIM_TRACE_POD): the slow path logs this pod's evaluations
+    int32_t trace_max;               //   KPSIM_TRACE_CLASS: only pods with index <= KPSIM_TRACE_MAXPOD
+    int32_t* trace;                  //   [1 + 6 * KP_TRACE_N]: count, then {round, nodeclaim (-1-j: template j), ok, flags, held lo/hi}
 
     // ---------------- existing nodes (ExistingNode, [core] scheduling/existingnode.go) ----------------
     int32_t E, EW;                   // existing nodes in scheduling order; words of an E-bit row

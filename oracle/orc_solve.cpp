@@ -21,6 +21,7 @@
 #include <atomic>
 #include <cfloat>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -222,6 +223,8 @@ struct Solver {
     int resv_key = -1;         // karpenter.k8s.aws/capacity-reservation-id (cloudprovider.ReservationIDLabel)
     bool resv_on = false;      // ReservedCapacity feature gate ∧ the catalog has reserved offerings
     bool resv_strict = true;   // ReservedOfferingModeStrict (provisioning); Fallback in disruption simulations
+    int trace_pod = getenv("ORC_TRACE_POD") ? atoi(getenv("ORC_TRACE_POD")) : -1;
+    int trace_cls = getenv("ORC_TRACE_CLASS") ? atoi(getenv("ORC_TRACE_CLASS")) : -1;
 
     explicit Solver(Dict& d) : D(d) {}
     const InstanceType& ty(int t) const { return (*tp)[t]; }
@@ -522,9 +525,18 @@ struct Solver {
         SliceAdaptor sa{this};
         go_sort_slice(sa);
         stats.nodeclaim_candidates_scanned += (int64_t)newNodeClaims.size();
+        const bool tr = (trace_pod >= 0 && plist[li] == trace_pod) ||
+                        (trace_cls >= 0 && pod_at(li).cls == trace_cls);  // ORC_TRACE_POD / ORC_TRACE_CLASS diagnostics
         for (int idx : newNodeClaims) {
             stats.nodeclaim_evals++;
+            if (tr) {
+                std::string h;
+                for (int id : ncs[idx].held) h += rid_names[id] + "(" + std::to_string(rcap[id]) + ") ";
+                fprintf(stderr, "[orc trace] pod %d nc %d pods %zu opts %zu held %s\n", plist[li], idx,
+                        ncs[idx].pods.size(), ncs[idx].options.size(), h.c_str());
+            }
             if (nodeclaim_add(ncs[idx], li)) {
+                if (tr) fprintf(stderr, "[orc trace]   -> accepted by nc %d\n", idx);
                 pod_result[li] = idx;
                 return true;
             }
