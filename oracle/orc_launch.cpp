@@ -53,13 +53,20 @@ struct L {
     bool has_value(const Reqs& r, int key, const std::string& v) {
         return req_has(D, r.get(key), D.value(key, v));
     }
-    // Offerings.Available().Compatible(reqs)
-    std::vector<const Off*> avail_compat(const IT& it, const Reqs& reqs) const {
+    // Offerings.Available().Compatible(reqs) over a candidate's current offering list
+    std::vector<const Off*> avail_compat(const std::vector<const Off*>& offs, const Reqs& reqs) const {
         std::vector<const Off*> o;
-        for (auto& f : it.offs)
-            if (f.available && reqs_compatible(D, reqs, f.reqs, true)) o.push_back(&f);
+        for (auto* f : offs)
+            if (f->available && reqs_compatible(D, reqs, f->reqs, true)) o.push_back(f);
         return o;
     }
+};
+
+// One element of the filters' []*InstanceType: the catalog type and its (possibly replaced) offering slice.  Types are
+// shared, never copied per request.
+struct Cand {
+    const IT* it;
+    std::vector<const Off*> offs;
 };
 
 bool fits(const std::vector<int64_t>& req, const std::vector<int64_t>& alloc) {
@@ -141,25 +148,28 @@ extern "C" kp_status orc_launch_select(const kp_catalog_view* cat, int32_t n, co
         res.override_offset = opos;
         const bool has_min = reqs.has_min_values();
         const bool has_reserved = X.has_value(reqs, X.kct, "reserved");
-        std::vector<IT> its = all;
+        std::vector<Cand> its;
         auto ice = [&](int f) {
             res.status = KP_E_INSUFFICIENT_CAPACITY;
             res.failed_filter = f;
         };
         // CompatibleAvailableFilter (filter.go:51-64)
         {
-            std::vector<IT> kept;
-            for (auto& it : its) {
+            for (auto& it : all) {
                 if (!reqs_compatible(D, reqs, it.reqs, true)) continue;
                 if (!fits(rq, it.alloc)) continue;
                 bool any = false;
                 for (auto& f : it.offs)
-                    if (reqs_compatible(D, reqs, f.reqs, true) && f.available) any = true;
+                    if (f.available && reqs_compatible(D, reqs, f.reqs, true)) {
+                        any = true;
+                        break;
+                    }
                 if (!any) continue;
-                kept.push_back(it);
+                Cand c{&it, {}};
+                for (auto& f : it.offs) c.offs.push_back(&f);
+                its.push_back(std::move(c));
             }
-            res.rejected[0] = (int)(its.size() - kept.size());
-            its.swap(kept);
+            res.rejected[0] = (int)(all.size() - its.size());
             if (its.empty()) ice(KP_FILTER_COMPATIBLE_AVAILABLE);
         }
         // CapacityReservationTypeFilter (filter.go:83-157)
@@ -168,7 +178,7 @@ extern "C" kp_status orc_launch_select(const kp_catalog_view* cat, int32_t n, co
             std::vector<int> member[2];
             for (size_t x = 0; x < its.size(); x++) {
                 bool in[2] = {false, false};
-                for (auto* o : X.avail_compat(its[x], reqs)) {
+                for (auto* o : X.avail_compat(its[x].offs, reqs)) {
                     if (X.ct(*o) != "reserved") continue;
                     const std::string t = X.rtype(*o);
                     const int p = t == "default" ? 0 : (t == "capacity-block" ? 1 : -1);
@@ -181,14 +191,12 @@ extern "C" kp_status orc_launch_select(const kp_catalog_view* cat, int32_t n, co
             }
             const int sel = cheapest[1] < cheapest[0] ? 1 : 0;  // lo.MinBy: price, then priority default < capacity-block
             if (!member[sel].empty()) {
-                std::vector<IT> kept;
+                std::vector<Cand> kept;
                 for (int x : member[sel]) {
-                    IT it = its[x];
-                    std::vector<Off> offs;
-                    for (auto& f : it.offs)
-                        if (X.ct(f) == "reserved" && X.rtype(f) == (sel ? "capacity-block" : "default")) offs.push_back(f);
-                    it.offs = offs;
-                    kept.push_back(it);
+                    Cand c{its[x].it, {}};
+                    for (auto* f : its[x].offs)
+                        if (X.ct(*f) == "reserved" && X.rtype(*f) == (sel ? "capacity-block" : "default")) c.offs.push_back(f);
+                    kept.push_back(std::move(c));
                 }
                 res.rejected[1] = (int)(its.size() - kept.size());
                 its.swap(kept);
@@ -197,10 +205,10 @@ extern "C" kp_status orc_launch_select(const kp_catalog_view* cat, int32_t n, co
         // CapacityBlockFilter (filter.go:173-221)
         if (res.status == KP_OK && has_reserved) {
             bool should = false, decided = false;
-            for (auto& it : its) {
-                for (auto& f : it.offs) {
-                    if (!f.reqs.has(X.krt)) continue;
-                    should = X.rtype(f) == "capacity-block";
+            for (auto& c : its) {
+                for (auto* f : c.offs) {
+                    if (!f->reqs.has(X.krt)) continue;
+                    should = X.rtype(*f) == "capacity-block";
                     decided = true;
                     break;
                 }
@@ -208,47 +216,45 @@ extern "C" kp_status orc_launch_select(const kp_catalog_view* cat, int32_t n, co
             }
             if (should) {
                 int sel = -1;
-                Off selo{};
+                const Off* selo = nullptr;
                 for (size_t x = 0; x < its.size(); x++) {
                     const Off* so = nullptr;
-                    for (auto& f : its[x].offs) {
-                        if (X.ct(f) != "reserved" || X.rtype(f) != "capacity-block") continue;
-                        if (!so || so->price > f.price) so = &f;
+                    for (auto* f : its[x].offs) {
+                        if (X.ct(*f) != "reserved" || X.rtype(*f) != "capacity-block") continue;
+                        if (!so || so->price > f->price) so = f;
                     }
-                    if (so && (sel < 0 || selo.price > so->price)) {
-                        selo = *so;
+                    if (so && (sel < 0 || selo->price > so->price)) {
+                        selo = so;
                         sel = (int)x;
                     }
                 }
-                IT it = its[sel];
-                it.offs = {selo};
+                Cand c{its[sel].it, {selo}};
                 res.rejected[2] = (int)its.size() - 1;
-                its = {it};
+                its.clear();
+                its.push_back(std::move(c));
             }
         }
         // ReservedOfferingFilter (filter.go:240-270)
         if (res.status == KP_OK && has_reserved) {
-            std::vector<IT> remaining;
-            for (auto& it : its) {
+            std::vector<Cand> remaining;
+            for (auto& c : its) {
                 std::vector<std::string> zones;
-                std::vector<Off> zo;
-                for (auto* o : X.avail_compat(it, reqs)) {
+                std::vector<const Off*> zo;
+                for (auto* o : X.avail_compat(c.offs, reqs)) {
                     if (X.ct(*o) != "reserved") continue;
                     const std::string z = X.zone(*o);
                     size_t k = 0;
                     while (k < zones.size() && zones[k] != z) k++;
                     if (k == zones.size()) {
                         zones.push_back(z);
-                        zo.push_back(*o);
-                    } else if (o->rcap > zo[k].rcap) {
-                        zo[k] = *o;
+                        zo.push_back(o);
+                    } else if (o->rcap > zo[k]->rcap) {
+                        zo[k] = o;
                     }
                 }
                 if (zo.empty()) continue;
-                IT k2 = it;
-                std::sort(zo.begin(), zo.end(), [](const Off& a, const Off& b) { return a.row < b.row; });
-                k2.offs = zo;
-                remaining.push_back(k2);
+                std::sort(zo.begin(), zo.end(), [](const Off* a, const Off* b) { return a->row < b->row; });
+                remaining.push_back(Cand{c.it, zo});
             }
             if (!remaining.empty()) {
                 res.rejected[3] = (int)(its.size() - remaining.size());
@@ -257,17 +263,17 @@ extern "C" kp_status orc_launch_select(const kp_catalog_view* cat, int32_t n, co
         }
         // ExoticInstanceTypeFilter (filter.go:289-318)
         if (res.status == KP_OK && !has_min) {
-            std::vector<IT> generic;
-            for (auto& it : its) {
+            std::vector<Cand> generic;
+            for (auto& c : its) {
                 bool exotic = false;
-                const Req sz = it.reqs.get(X.ksize);
+                const Req sz = c.it->reqs.get(X.ksize);
                 if (!sz.complement)
                     for (int v : sz.values)
                         if (D.vals[X.ksize][v].find("metal") != std::string::npos) exotic = true;
                 for (int r = 0; r < R; r++)
                     for (auto* a : accel)
-                        if (X.res[r] == a && it.cap[r] != 0) exotic = true;
-                if (!exotic) generic.push_back(it);
+                        if (X.res[r] == a && c.it->cap[r] != 0) exotic = true;
+                if (!exotic) generic.push_back(c);
             }
             if (!generic.empty()) {
                 res.rejected[4] = (int)(its.size() - generic.size());
@@ -278,27 +284,27 @@ extern "C" kp_status orc_launch_select(const kp_catalog_view* cat, int32_t n, co
         if (res.status == KP_OK && !has_min && X.has_value(reqs, X.kct, "on-demand") && X.has_value(reqs, X.kct, "spot")) {
             double cod = DBL_MAX;
             bool has_spot = false, has_od = false;
-            for (auto& it : its)
-                for (auto* o : X.avail_compat(it, reqs)) {
-                    const std::string c = X.ct(*o);
-                    if (c == "on-demand") {
+            for (auto& c : its)
+                for (auto* o : X.avail_compat(c.offs, reqs)) {
+                    const std::string ctv = X.ct(*o);
+                    if (ctv == "on-demand") {
                         has_od = true;
                         if (o->price < cod) cod = o->price;
-                    } else if (c == "spot") {
+                    } else if (ctv == "spot") {
                         has_spot = true;
                     }
                 }
             if (has_od && has_spot) {
-                std::vector<IT> kept;
-                for (auto& it : its) {
+                std::vector<Cand> kept;
+                for (auto& c : its) {
                     bool keep = false, decided = false, spot = false;
-                    for (auto* o : X.avail_compat(it, reqs)) {
-                        const std::string c = X.ct(*o);
-                        if (c == "reserved") {
+                    for (auto* o : X.avail_compat(c.offs, reqs)) {
+                        const std::string ctv = X.ct(*o);
+                        if (ctv == "reserved") {
                             keep = decided = true;
                             break;
                         }
-                        if (c == "spot") {
+                        if (ctv == "spot") {
                             spot = true;
                             if (o->price <= cod) {
                                 keep = decided = true;
@@ -307,7 +313,7 @@ extern "C" kp_status orc_launch_select(const kp_catalog_view* cat, int32_t n, co
                         }
                     }
                     if (!decided) keep = !spot;
-                    if (keep) kept.push_back(it);
+                    if (keep) kept.push_back(c);
                 }
                 res.rejected[5] = (int)(its.size() - kept.size());
                 its.swap(kept);
@@ -320,14 +326,14 @@ extern "C" kp_status orc_launch_select(const kp_catalog_view* cat, int32_t n, co
         std::vector<std::pair<double, int>> key;
         for (size_t x = 0; x < its.size(); x++) {
             double p = DBL_MAX;
-            for (auto* o : X.avail_compat(its[x], reqs))
+            for (auto* o : X.avail_compat(its[x].offs, reqs))
                 if (o->price < p) p = o->price;
             key.emplace_back(p, (int)x);
         }
         std::sort(key.begin(), key.end(), [&](const std::pair<double, int>& a, const std::pair<double, int>& b) {
             if (a.first != b.first) return a.first < b.first;
-            if (its[a.second].name != its[b.second].name) return its[a.second].name < its[b.second].name;
-            return its[a.second].row < its[b.second].row;
+            if (its[a.second].it->name != its[b.second].it->name) return its[a.second].it->name < its[b.second].it->name;
+            return its[a.second].it->row < its[b.second].it->row;
         });
         if ((int)key.size() > M) key.resize(M);
         if (has_min) {
@@ -335,7 +341,7 @@ extern "C" kp_status orc_launch_select(const kp_catalog_view* cat, int32_t n, co
                 if (!kv.second.has_min) continue;
                 std::vector<int> seen;
                 for (auto& k : key) {
-                    const Req r = its[k.second].reqs.get(kv.first);
+                    const Req r = its[k.second].it->reqs.get(kv.first);
                     if (r.complement) continue;
                     for (int v : r.values)
                         if (std::find(seen.begin(), seen.end(), v) == seen.end()) seen.push_back(v);
@@ -353,7 +359,10 @@ extern "C" kp_status orc_launch_select(const kp_catalog_view* cat, int32_t n, co
             r2.m[X.kct] = new_req(D, X.kct, OP_IN, {names[c]}, false, 0);
             bool any = false;
             for (auto& k : key)
-                if (!X.avail_compat(its[k.second], r2).empty()) any = true;
+                if (!X.avail_compat(its[k.second].offs, r2).empty()) {
+                    any = true;
+                    break;
+                }
             if (any) {
                 ct = c;
                 break;
@@ -364,10 +373,10 @@ extern "C" kp_status orc_launch_select(const kp_catalog_view* cat, int32_t n, co
         r3.m[X.kct] = new_req(D, X.kct, OP_IN, {names[ct]}, false, 0);
         res.n_types = (int)key.size();
         for (auto& k : key) {
-            if (type_ids && tpos < cap_type_ids) type_ids[tpos] = its[k.second].row;
+            if (type_ids && tpos < cap_type_ids) type_ids[tpos] = its[k.second].it->row;
             else short_buf = true;
             tpos++;
-            for (auto* o : X.avail_compat(its[k.second], r3)) {
+            for (auto* o : X.avail_compat(its[k.second].offs, r3)) {
                 if (override_offerings && opos < cap_overrides) override_offerings[opos] = o->row;
                 else short_buf = true;
                 opos++;

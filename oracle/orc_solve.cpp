@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cfloat>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -999,6 +1000,8 @@ extern "C" kp_status orc_solve_opts(const kp_catalog_view* cat, const kp_solve_i
                                     kp_solve_output* out, orc_result** res_out) {
     if (!cat || !in || !out) return KP_E_INVALID;
     if (in->min_values_policy != KP_MIN_VALUES_STRICT) return KP_E_UNSUPPORTED;
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     auto res = std::make_unique<orc_result>();
     Solver s(res->D);
     s.resv_on = opts ? opts->reserved_capacity != 0 : true;  // FEATURE_GATES ReservedCapacity (default on)
@@ -1010,8 +1013,17 @@ extern "C" kp_status orc_solve_opts(const kp_catalog_view* cat, const kp_solve_i
     s.plist.resize(pv.n_pods);
     for (int p = 0; p < pv.n_pods; p++) s.plist[p] = p;
 
+    const auto t1 = clk::now();
     s.solve();
+    const auto t2 = clk::now();
     s.finalize(in->max_instance_types);
+    const auto t3 = clk::now();
+    // the oracle's phases in the device's stats fields: input parsing, the Solve loop, FinalizeScheduling + Truncate
+    auto ns = [](clk::time_point a, clk::time_point b) { return (double)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count(); };
+    s.stats.ns_host_prep = ns(t0, t1);
+    s.stats.ns_device_solve = ns(t1, t2);
+    s.stats.ns_device_finalize = ns(t2, t3);
+    s.stats.ns_total = ns(t0, t3);
 
     // outputs
     int n_nc = (int)s.ncs.size();

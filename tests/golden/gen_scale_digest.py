@@ -21,6 +21,7 @@ import parity  # noqa: E402
 CASES = {
     "config2_200k": ("config2", dict(n_pods=200_000)),  # BASELINE configs[4]'s pod count over the config-2 pod mix
     "config3_50k": ("config3", dict(n_pods=50_000)),    # BASELINE configs[2]: topology + five weighted NodePools
+    "config5_200k": ("config5", dict(n_pods=200_000)),  # BASELINE configs[4]: reserved offerings, ODCR-first NodePools
 }
 
 
@@ -33,7 +34,7 @@ def main():
             out = json.load(f)
     for name in sys.argv[1:] or list(CASES):
         gen, kw = CASES[name]
-        prob = getattr(synth, gen)(catalog=cat, **kw)
+        prob = synth.config5(golden=cat, **kw) if gen == "config5" else getattr(synth, gen)(catalog=cat, **kw)
         t = time.time()
         out[name] = dict(kw, **parity.result_digest(parity.run_oracle(prob)))
         print(name, "%.1f s" % (time.time() - t), out[name]["n_nodeclaims"])

@@ -76,3 +76,16 @@ def test_reserved_capacity_gate_off(golden):
     orc = (o.results, [model.parse_requirements_blob(o.requirements(i)) for i in range(o.results.n_nodeclaims)])
     parity.assert_same(dev, orc)
     assert _held(dev[1]) == 0
+
+
+def test_config5_200k_digest(ctx, golden):
+    """BASELINE configs[4] at full size (200k pods): every output field equals the committed oracle digest
+    (tests/golden/gen_scale_digest.py config5_200k; the oracle needs ~15 min at this size)."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "scale_digests.json")) as f:
+        want = json.load(f)["config5_200k"]
+    prob = synth.config5(n_pods=want["n_pods"], golden=golden)
+    got = parity.result_digest(parity.run_device(ctx, prob))
+    for k, v in got.items():
+        assert v == want[k], k
