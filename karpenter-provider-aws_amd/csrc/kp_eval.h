@@ -30,7 +30,8 @@ struct WaveScratch {
     uint64_t minbits[KP_MAX_MIN_WORDS];
     int32_t hr[KP_LDS_AXES];   // quick-accept headroom of the chosen witness type (scaled, lower bound)
     int32_t memo_ok;           // a failed evaluation may be memoised for the shape (it did not depend on topology
-                               // counts: see topo_narrow, or on reservation capacity: see the reservation step)
+                               // counts: see topo_narrow; one that depended on reservation capacity is memoised
+                               // until a capacity comes back from 0, see the reservation step)
     int32_t rlive;             // success: the new options keep a compatible available reserved offering
     uint64_t held;             // success: reservation IDs the NodeClaim holds after the Add
 };
@@ -703,8 +704,9 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
     // Every available reserved offering of a remaining type that the updated requirements are compatible with is
     // reserved for this NodeClaim: an ID it already holds, or one with capacity left.  The Add fails when a compatible
     // reserved offering exists but none can be reserved, or when the NodeClaim held reservations and none remain
-    // (ReservedOfferingError).  A rejection that depends on the manager's counts is never memoised.  Read-only here:
-    // the winner's commit takes / releases the capacity.
+    // (ReservedOfferingError).  Read-only here: the winner's commit takes / releases the capacity.  A rejection of
+    // this kind needs every compatible ID the NodeClaim does not hold to be at capacity 0, and only a release can lift
+    // a capacity from 0: such rejections stay memoised until commit_reservations reports one (FfdShared::rel_flag).
     bool rlive = false;
     if (RESV && E.resv_on) {
         const ResvTab& X = *E.ro;
@@ -714,12 +716,7 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         const int rid = lane < X.n ? X.rid[lane] : 0;
         const bool res = comp && (((a.held >> rid) & 1ull) || E.rcap[rid] > 0);
         const uint64_t cm = ballot(comp), rm = ballot(res);
-        if ((cm && !rm) || (a.held && !rm)) {
-            // with no compatible reserved offering at all (cm == 0) the outcome does not depend on the manager's
-            // counts, and a NodeClaim's compatible set only shrinks while its held set stays non-empty: for good
-            if (lane == 0 && cm) ws.memo_ok = 0;
-            return false;
-        }
+        if ((cm && !rm) || (a.held && !rm)) return false;
         rlive = cm != 0;
         const uint64_t nh = wave_or64(res ? (1ull << rid) : 0ull);
         if (lane == 0) {

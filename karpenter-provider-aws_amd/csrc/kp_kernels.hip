@@ -175,7 +175,9 @@ struct FfdShared {
     int N, qhead, qcount, done, cur_pod, cur_cls, cur_shape, prev_shape;
     int dirty_kind, dirty_pos, seq, err, cls_fill, scan_start, any_rej;
     int rej_volatile;              // a candidate of the current pod was rejected for a reason that may not last
-                                   // (reservation capacity): the next pod of the shape rescans from the start
+                                   // (topology counts): the next pod of the shape rescans from the start
+    int rel_flag;                  // a reservation ID's capacity came back from 0 (commit_reservations): the
+                                   // reservation-dependent rejections memoised so far may no longer hold
     int xstart;                    // every existing node < xstart has rejected the current shape
     uint32_t cur_tol;              // tolerations word of the current shape's class (bit 31: no requirement keys)
     int32_t cur_pq[KP_LDS_AXES];   // scaled quick-accept requests of the current shape
@@ -422,10 +424,11 @@ __device__ __forceinline__ long long prof_clock(const KpDev& d) { return d.profi
 // The winner's reservations (one lane): ReservationManager.Reserve for the IDs newly held, Release for the IDs the
 // Add no longer holds (NodeClaim.Add's reservedOfferings update), then the NodeClaim's held set and liveness.
 __device__ __forceinline__ void commit_reservations(const KpDev& d, int32_t* rcap, const WaveScratch& ws, int nc,
-                                                    uint64_t old) {
+                                                    uint64_t old, int* rel_flag) {
     const uint64_t nh = ws.held;
     for (uint64_t x = nh & ~old; x; x &= x - 1) rcap[__ffsll((unsigned long long)x) - 1]--;
-    for (uint64_t x = old & ~nh; x; x &= x - 1) rcap[__ffsll((unsigned long long)x) - 1]++;
+    for (uint64_t x = old & ~nh; x; x &= x - 1)
+        if (rcap[__ffsll((unsigned long long)x) - 1]++ == 0) *rel_flag = 1;
     __hip_atomic_store(&d.nc_held[nc], nh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&d.nc_rlive[nc], ws.rlive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -501,6 +504,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
         S.scan_start = 0;
         S.any_rej = 0;
         S.rej_volatile = 0;
+        S.rel_flag = 0;
         S.xstart = 0;
         S.seq = 0;
         S.err = 0;
@@ -561,6 +565,15 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
             int seq = S.seq, prev_shape = S.prev_shape, dkind = S.dirty_kind, dpos = S.dirty_pos;
             int sstart = S.scan_start;  // every slice position < sstart has rejected the current shape
             int any_rej = S.any_rej;
+            if (RESV && S.rel_flag) {
+                // a reservation capacity came back from 0: forget the shape's memoised rejections (a reservation-
+                // dependent one may now succeed; the others are re-derived on the next scan)
+                for (int i = lane; i < N; i += 64) skey[i] &= KEYMASK;
+                any_rej = 0;
+                sstart = 0;
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                if (lane == 0) S.rel_flag = 0;
+            }
             int xstart = S.xstart;
             long long nexist = 0;
             // pods of the current shape placed on existing node xj whose headroom update is still pending (flushed
@@ -1188,7 +1201,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                     S.acc[b][wave] = ok;
                     if (!ok && S.ws[wave].memo_ok) {
                         // rejected this shape for good (positions are stable here); a rejection that depended on
-                        // topology counts or reservation capacity is not memoised
+                        // topology counts is not memoised, one that depended on reservation capacity until rel_flag
                         skey[S.cand_pos[b][wave]] |= 0x80000000u;
                         S.any_rej = 1;
                     }
@@ -1219,7 +1232,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                 const int nc = sord[pos];
                 if (!S.fastp[round & 1][win]) {
                     commit_reqs(d, S.CC, S.ws[win], nc, lane);
-                    if (RESV && d.resv_on && lane == 0) commit_reservations(d, sRcap, S.ws[win], nc, ld_u64(&d.nc_held[nc]));
+                    if (RESV && d.resv_on && lane == 0) commit_reservations(d, sRcap, S.ws[win], nc, ld_u64(&d.nc_held[nc]), &S.rel_flag);
                 }
                 if (TOPO_ON && (S.CC.flags & CF_TOPO))
                     topo_record(d, S.CC, S.ws[win], d.nc_hdr + (size_t)nc * K, d.nc_words + (size_t)nc * d.DW,
@@ -1314,7 +1327,7 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
                             d.nc_words[(size_t)n * d.DW + i] = d.cls_words[(size_t)(d.C + jj) * d.DW + i];
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         commit_reqs(d, S.CC, S.ws[wave], n, lane);
-                        if (RESV && d.resv_on && lane == 0) commit_reservations(d, sRcap, S.ws[wave], n, 0ull);
+                        if (RESV && d.resv_on && lane == 0) commit_reservations(d, sRcap, S.ws[wave], n, 0ull, &S.rel_flag);
                         if (TOPO_ON && (S.CC.flags & CF_TOPO))
                             topo_record(d, S.CC, S.ws[wave], d.cls_hdr + (size_t)(d.C + jj) * K,
                                         d.cls_words + (size_t)(d.C + jj) * d.DW, d.E + n, jj, true, lane);

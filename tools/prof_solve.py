@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """FFD-kernel phase profile of one Solve (KPSIM_PROFILE=1: s_memtime cycle counters inside ffd_kernel).
 
-    KPSIM_PROFILE=1 python tools/prof_solve.py [config2|config3] [n_pods]
+    KPSIM_PROFILE=1 python tools/prof_solve.py [config2|config3|config5] [n_pods]
 """
 import json
 import os
@@ -23,15 +23,20 @@ def main():
     which = sys.argv[1] if len(sys.argv) > 1 else "config3"
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 50_000
     cat = catalog.golden_catalog()
+    if which == "config5":
+        cat = synth.config5_catalog(cat)
     prob = getattr(synth, which)(n_pods=n, catalog=cat)
     ctx = native.Context(0)
     ctx.upload_catalog(model.CatalogView(cat))
     iv = model.SolveInputView(prob)
     out = model.OutputBuffers(prob.pods.n, prob.pods.n + 16, (prob.pods.n + 16) * 60)
+    import time
+    t = time.perf_counter()
     ctx.solve(iv, out)
+    wall = (time.perf_counter() - t) * 1e3
     r = out.results()
     kt = ctx.kernel_times_ms()
-    print(json.dumps({"config": which, "pods": n, "kernel_ms": kt, "stats": r.stats,
+    print(json.dumps({"config": which, "pods": n, "wall_ms": wall, "kernel_ms": kt, "nodeclaims": r.n_nodeclaims, "stats": r.stats,
                       "ffd": dict(zip(NAMES, ctx.ffd_cycles()))}, indent=1))
     ctx.close()
 
