@@ -57,35 +57,43 @@ def consolidation_bytes(cst, A, R=12):
 
 def consolidation_leg(a, cat, local, rank, world, dist, barrier):
     """BASELINE configs[3]: single-node consolidation over every candidate of a 5k-node / ~100k-pod cluster plus the
-    multi-node prefix probes (first 100 by disruption cost).  Probes are sharded over ranks; one all-gather per mode
-    carries the results (kpsim.consolidation.compute_command)."""
+    multi-node prefix probes (first 100 by disruption cost).  With N GPUs the library shards the probes itself: rank 0
+    opens one multi-device ctx over devices 0..N-1 (kp_device_opts.devices), which evaluates one
+    contiguous probe shard per device on its own host thread and gathers the results in-process; the other ranks only
+    join the barriers.  The decision (kpsim.consolidation.compute_command) replays over the gathered vector."""
     from kpsim import abi, consolidation, model, native, synth
     cp = synth.config4(n_nodes=a.nodes, catalog=cat)
-    ctx = native.Context(local)
-    ctx.upload_catalog(model.CatalogView(cat))
-    ctx.consolidate_prepare(model.ConsolidateInputView(cp, abi.KP_CONSOLIDATE_SINGLE))
     n_s = model.consolidation_probe_count(len(cp.candidates), abi.KP_CONSOLIDATE_SINGLE)
     n_m = model.consolidation_probe_count(len(cp.candidates), abi.KP_CONSOLIDATE_MULTI)
+    ctx = None
+    if rank == 0:
+        ctx = native.Context(local) if world == 1 else native.Context(devices=list(range(world)))
+        ctx.upload_catalog(model.CatalogView(cat))
+        ctx.consolidate_prepare(model.ConsolidateInputView(cp, abi.KP_CONSOLIDATE_SINGLE))
 
     def probe_fn(c, mode, b0, b1):
         return ctx.consolidate_execute(mode, n_s if mode == abi.KP_CONSOLIDATE_SINGLE else n_m, b0, b1)
 
     def step():
-        cs = consolidation.compute_command(cp, abi.KP_CONSOLIDATE_SINGLE, probe_fn)
+        # the library's own sharding: one call per mode over the whole probe range (no torch.distributed collective)
+        cs = consolidation.compute_command(cp, abi.KP_CONSOLIDATE_SINGLE, probe_fn, distributed=False)
         ms_s, cst_s = ctx.consolidate_stats()
-        cm = consolidation.compute_command(cp, abi.KP_CONSOLIDATE_MULTI, probe_fn)
+        cm = consolidation.compute_command(cp, abi.KP_CONSOLIDATE_MULTI, probe_fn, distributed=False)
         ms_m, cst_m = ctx.consolidate_stats()
         return cs, cm, (ms_s, cst_s), (ms_m, cst_m)
 
-    for _ in range(max(1, a.warmup)):
-        step()
+    if rank == 0:
+        for _ in range(max(1, a.warmup)):
+            step()
     barrier()
     t0 = time.perf_counter()
     kms, kcs = [], []
-    for _ in range(a.steps):
-        cs, cm, st_s, st_m = step()
-        kms.append([st_s[0][0], st_s[0][1], st_m[0][0], st_m[0][1]])
-        kcs.append(np.array(st_s[1]) + np.array(st_m[1]))
+    cs = cm = None
+    if rank == 0:
+        for _ in range(a.steps):
+            cs, cm, st_s, st_m = step()
+            kms.append([st_s[0][0], st_s[0][1], st_m[0][0], st_m[0][1]])
+            kcs.append(np.array(st_s[1]) + np.array(st_m[1]))
     elapsed = time.perf_counter() - t0
     barrier()
     if dist is not None:
@@ -93,6 +101,8 @@ def consolidation_leg(a, cat, local, rank, world, dist, barrier):
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+    if rank != 0:
+        return None
     km = np.array(kms).mean(axis=0)
     cst = np.array(kcs).mean(axis=0)
     A = int(np.any(cp.cluster.pods.requests != 0, axis=0).sum())  # active axes (no daemon overhead in config4)
@@ -109,7 +119,7 @@ def consolidation_leg(a, cat, local, rank, world, dist, barrier):
         "config": {"workload": "config4: %d existing nodes, %d bound pods (config2 classes), single-node probes over "
                                "all %d candidates + %d multi-node prefix probes" % (len(cp.cluster.existing),
                                                                                     cp.cluster.pods.n, n_s, n_m),
-                   "parallelism": "probe shards x%d" % world},
+                   "parallelism": "probe shards x%d (one multi-device ctx, in-library gather)" % world},
         "decisions": {"single": [cs.decision, cs.candidates[:1]], "multi": [cm.decision, len(cm.candidates)]},
         "kernel_ms_rank0": {"single_prep": km[0], "single_probes": km[1], "multi_prep": km[2], "multi_probes": km[3]},
         "counters_per_step": dict(zip(["pods_popped", "existing_slots", "nodeclaim_evals", "template_evals", "probes",

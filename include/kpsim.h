@@ -259,7 +259,13 @@ enum { KP_PREFERENCE_RESPECT = 0, KP_PREFERENCE_IGNORE = 1 };
    (settings.md:13-42, pkg/operator/options/options.go:36-58). */
 typedef struct kp_device_opts {
     int32_t device;                          /* HIP device ordinal (the ctx's primary device) */
-    int32_t n_devices;                       /* > 1: kp_consolidate shards probes over devices[0..n) */
+    int32_t n_devices;                       /* > 1: a multi-device ctx over devices[0..n) (devices[0] is the primary;
+                                                `device` is ignored).  Catalog uploads / patches and
+                                                kp_consolidate_prepare are applied on every device (one host thread
+                                                each); kp_consolidate_execute / kp_consolidate split the probe range into
+                                                one contiguous shard per device and gather the results (SURVEY §8b(4):
+                                                kp_consolidate runs multi-GPU internally).  Solve and launch selection
+                                                run on the primary. */
     const int32_t* devices;
     int32_t preference_policy;               /* KP_PREFERENCE_*: Respect relaxes preferences (ScheduleAnyway spreads,
                                                 preferred affinities); Ignore drops them before scheduling */

@@ -192,6 +192,11 @@ struct DBuf {  // device buffer, grow-only; freed by its destructor (the owning 
 struct kp_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // kp_device_opts.devices[1..n): one ctx per further device (own stream, own copies of the catalog and of the
+    // prepared consolidation pass).  Catalog uploads / patches and kp_consolidate_prepare run on every device (one host
+    // thread each); kp_consolidate_execute splits the probe range into one contiguous shard per device and gathers the
+    // shards' results into the caller's buffer (≤ 40 B per probe, an in-process host gather).
+    std::vector<kp_ctx*> peers;
     std::string err;
     int pref_policy = KP_PREFERENCE_RESPECT;  // kp_device_opts solver parameters
     int reserved_capacity = 1;
@@ -316,6 +321,26 @@ static kp_status fail(kp_ctx* c, kp_status st, const std::string& msg) {
         if (_e != hipSuccess) return fail(ctx, KP_E_DEVICE, std::string(#expr ": ") + hipGetErrorString(_e)); \
     } while (0)
 
+// Runs f on the ctx and, concurrently (one host thread each), on its peer ctxs.  The primary's status wins; otherwise
+// the first failing peer's status is returned with its message.
+template <class F>
+static kp_status fan_out(kp_ctx* ctx, F f) {
+    if (ctx->peers.empty()) return f(ctx);
+    const size_t G = ctx->peers.size();
+    std::vector<kp_status> st(G, KP_OK);
+    std::vector<std::thread> th;
+    th.reserve(G);
+    for (size_t i = 0; i < G; i++) th.emplace_back([&st, &f, ctx, i] { st[i] = f(ctx->peers[i]); });
+    const kp_status s0 = f(ctx);
+    for (auto& t : th) t.join();
+    if (s0 != KP_OK) return s0;
+    for (size_t i = 0; i < G; i++)
+        if (st[i] != KP_OK)
+            return fail(ctx, st[i], "device " + std::to_string(ctx->peers[i]->device) + " (peer " + std::to_string(i + 1) +
+                                        "): " + ctx->peers[i]->err);
+    return KP_OK;
+}
+
 extern "C" const char* kp_version(void) { return "kpsim 0.1 (gfx950)"; }
 
 extern "C" const char* kp_last_error(const kp_ctx* ctx) { return ctx ? ctx->err.c_str() : "null ctx"; }
@@ -325,6 +350,32 @@ extern "C" kp_status kp_ctx_create(const kp_device_opts* opts, kp_ctx** out) try
     *out = nullptr;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return KP_E_DEVICE;
+    if (opts && opts->n_devices > 1) {
+        // multi-device ctx: the primary is devices[0], each further entry gets a peer ctx (the same ordinal may repeat:
+        // two streams on one device)
+        if (!opts->devices) return KP_E_INVALID;
+        for (int i = 0; i < opts->n_devices; i++)
+            if (opts->devices[i] < 0 || opts->devices[i] >= n) return KP_E_DEVICE;
+        kp_device_opts one = *opts;
+        one.n_devices = 0;
+        one.devices = nullptr;
+        one.device = opts->devices[0];
+        kp_ctx* primary = nullptr;
+        kp_status st = kp_ctx_create(&one, &primary);
+        if (st != KP_OK) return st;
+        for (int i = 1; i < opts->n_devices && st == KP_OK; i++) {
+            one.device = opts->devices[i];
+            kp_ctx* peer = nullptr;
+            st = kp_ctx_create(&one, &peer);
+            if (st == KP_OK) primary->peers.push_back(peer);
+        }
+        if (st != KP_OK) {
+            kp_ctx_destroy(primary);
+            return st;
+        }
+        *out = primary;
+        return KP_OK;
+    }
     auto ctx = std::make_unique<kp_ctx>();
     ctx->device = opts ? opts->device : 0;
     if (opts) {
@@ -350,6 +401,8 @@ extern "C" kp_status kp_ctx_create(const kp_device_opts* opts, kp_ctx** out) try
 
 extern "C" kp_status kp_ctx_destroy(kp_ctx* ctx) {
     if (!ctx) return KP_OK;
+    for (kp_ctx* p : ctx->peers) kp_ctx_destroy(p);
+    ctx->peers.clear();
     hipSetDevice(ctx->device);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
     for (auto& e : ctx->ev)
@@ -370,7 +423,7 @@ static void rebuild_avail(kp_ctx* c, const std::vector<uint8_t>& avail) {
 
 static kp_status upload_launch_tables(kp_ctx* c, const kp_catalog_view* v, const std::vector<uint8_t>& avail);
 
-extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, uint64_t epoch) try {
+static kp_status catalog_upload_one(kp_ctx* ctx, const kp_catalog_view* v, uint64_t epoch) try {
     if (!ctx || !v) return KP_E_INVALID;
     // every prepared solve / consolidation pass captured device pointers and sizes of the previous catalog, and the
     // tables below may be reallocated: nothing prepared survives an upload, successful or not
@@ -674,7 +727,14 @@ extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, ui
     return fail(ctx, KP_E_INVALID, e.what());
 }
 
-extern "C" kp_status kp_catalog_patch_avail(kp_ctx* ctx, const uint8_t* available, int32_t n, uint64_t epoch) {
+extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, uint64_t epoch) try {
+    if (!ctx || !v) return KP_E_INVALID;
+    return fan_out(ctx, [&](kp_ctx* c) { return catalog_upload_one(c, v, epoch); });
+} catch (...) {
+    return fail(ctx, KP_E_INVALID, "kp_catalog_upload: host error");
+}
+
+static kp_status patch_avail_one(kp_ctx* ctx, const uint8_t* available, int32_t n, uint64_t epoch) {
     if (!ctx || !available) return KP_E_INVALID;
     ctx->cons_prep_valid = false;
     if (!ctx->have_catalog) return fail(ctx, KP_E_STATE, "no catalog");
@@ -694,8 +754,14 @@ extern "C" kp_status kp_catalog_patch_avail(kp_ctx* ctx, const uint8_t* availabl
     return KP_OK;
 }
 
-extern "C" kp_status kp_catalog_patch_price(kp_ctx* ctx, const int32_t* idx, const double* price, int32_t n,
-                                            uint64_t epoch) {
+extern "C" kp_status kp_catalog_patch_avail(kp_ctx* ctx, const uint8_t* available, int32_t n, uint64_t epoch) try {
+    if (!ctx || !available) return KP_E_INVALID;
+    return fan_out(ctx, [&](kp_ctx* c) { return patch_avail_one(c, available, n, epoch); });
+} catch (...) {
+    return fail(ctx, KP_E_INVALID, "kp_catalog_patch_avail: host error");
+}
+
+static kp_status patch_price_one(kp_ctx* ctx, const int32_t* idx, const double* price, int32_t n, uint64_t epoch) {
     if (!ctx || (n > 0 && (!idx || !price))) return KP_E_INVALID;
     ctx->cons_prep_valid = false;
     if (!ctx->have_catalog) return fail(ctx, KP_E_STATE, "no catalog");
@@ -714,6 +780,14 @@ extern "C" kp_status kp_catalog_patch_price(kp_ctx* ctx, const int32_t* idx, con
     HIPCHK(hipStreamSynchronize(ctx->stream));
     ctx->epoch = epoch;
     return KP_OK;
+}
+
+extern "C" kp_status kp_catalog_patch_price(kp_ctx* ctx, const int32_t* idx, const double* price, int32_t n,
+                                            uint64_t epoch) try {
+    if (!ctx || (n > 0 && (!idx || !price))) return KP_E_INVALID;
+    return fan_out(ctx, [&](kp_ctx* c) { return patch_price_one(c, idx, price, n, epoch); });
+} catch (...) {
+    return fail(ctx, KP_E_INVALID, "kp_catalog_patch_price: host error");
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1838,7 +1912,7 @@ extern "C" int32_t kp_consolidate_probe_count(const kp_consolidate_input* in) {
     return n <= mx ? n - 1 : mx;  // firstNConsolidationOption: mid in [1, max], prefix candidates[0 : mid+1]
 }
 
-extern "C" kp_status kp_consolidate_prepare(kp_ctx* ctx, const kp_consolidate_input* in) try {
+static kp_status cons_prepare_one(kp_ctx* ctx, const kp_consolidate_input* in) try {
     if (!ctx || !in) return KP_E_INVALID;
     ctx->cons_prepared = false;
     ctx->cons_prep_valid = false;
@@ -1944,8 +2018,15 @@ extern "C" kp_status kp_consolidate_prepare(kp_ctx* ctx, const kp_consolidate_in
     return fail(ctx, KP_E_INVALID, e.what());
 }
 
-extern "C" kp_status kp_consolidate_execute(kp_ctx* ctx, int32_t mode, int32_t probe_begin, int32_t probe_end,
-                                            kp_probe_result* results, int32_t cap_results) try {
+extern "C" kp_status kp_consolidate_prepare(kp_ctx* ctx, const kp_consolidate_input* in) try {
+    if (!ctx || !in) return KP_E_INVALID;
+    return fan_out(ctx, [&](kp_ctx* c) { return cons_prepare_one(c, in); });
+} catch (...) {
+    return fail(ctx, KP_E_INVALID, "kp_consolidate_prepare: host error");
+}
+
+static kp_status cons_execute_one(kp_ctx* ctx, int32_t mode, int32_t probe_begin, int32_t probe_end,
+                                  kp_probe_result* results, int32_t cap_results) try {
     if (!ctx) return KP_E_INVALID;
     if (!ctx->cons_prepared || !ctx->have_catalog)
         return fail(ctx, KP_E_STATE, "kp_consolidate_execute before kp_consolidate_prepare");
@@ -2051,6 +2132,65 @@ extern "C" kp_status kp_consolidate_execute(kp_ctx* ctx, int32_t mode, int32_t p
     c->cons_ms[1] = ms;
     c->cons_ms[2] = ns_since(t0) * 1e-6;
     for (int i = 0; i < CS_COUNT; i++) c->cons_stats[i] = cst[i];
+    return KP_OK;
+} catch (const std::exception& e) {
+    return fail(ctx, KP_E_INVALID, e.what());
+}
+
+// Multi-device: probes [b0, b1) split into one contiguous shard per device (equal probe counts), each evaluated on its
+// device by its own host thread into its slice of `results`; counters are summed, device times are the max over
+// devices.  Probes are independent, so the gathered vector equals a single-device evaluation of the whole range.
+extern "C" kp_status kp_consolidate_execute(kp_ctx* ctx, int32_t mode, int32_t probe_begin, int32_t probe_end,
+                                            kp_probe_result* results, int32_t cap_results) try {
+    if (!ctx) return KP_E_INVALID;
+    if (ctx->peers.empty()) return cons_execute_one(ctx, mode, probe_begin, probe_end, results, cap_results);
+    if (!ctx->cons_prepared || !ctx->have_catalog)
+        return fail(ctx, KP_E_STATE, "kp_consolidate_execute before kp_consolidate_prepare");
+    for (kp_ctx* p : ctx->peers)
+        if (!p->cons_prepared || !p->have_catalog)
+            return fail(ctx, KP_E_STATE, "kp_consolidate_execute: a peer device has no prepared pass");
+    if (mode != KP_CONSOLIDATE_SINGLE && mode != KP_CONSOLIDATE_MULTI) return fail(ctx, KP_E_INVALID, "unknown consolidation mode");
+    const int NC = ctx->cons.n_cand;
+    const int np = mode == KP_CONSOLIDATE_SINGLE ? NC : (NC < 2 ? 0 : (NC <= ctx->cons_max_candidates ? NC - 1 : ctx->cons_max_candidates));
+    const int b0 = probe_begin > 0 ? probe_begin : 0;
+    const int b1 = probe_end > 0 && probe_end < np ? probe_end : np;
+    if (b0 > b1) return fail(ctx, KP_E_INVALID, "probe range outside the probe list");
+    const int nprobe = b1 - b0;
+    if (nprobe > cap_results || (nprobe > 0 && !results)) return fail(ctx, KP_E_BUFFER, "probe results buffer too small");
+    if (nprobe == 0) return KP_OK;
+    const auto t0 = clk::now();
+    const int G = 1 + (int)ctx->peers.size();
+    std::vector<kp_ctx*> dev(1, ctx);
+    dev.insert(dev.end(), ctx->peers.begin(), ctx->peers.end());
+    std::vector<int> lo(G), hi(G);
+    for (int g = 0; g < G; g++) {
+        lo[g] = b0 + (int)((int64_t)nprobe * g / G);
+        hi[g] = b0 + (int)((int64_t)nprobe * (g + 1) / G);
+    }
+    std::vector<kp_status> st(G, KP_OK);
+    auto run = [&](int g) {
+        if (hi[g] > lo[g]) st[g] = cons_execute_one(dev[g], mode, lo[g], hi[g], results + (lo[g] - b0), hi[g] - lo[g]);
+    };
+    std::vector<std::thread> th;
+    th.reserve(G - 1);
+    for (int g = 1; g < G; g++) th.emplace_back(run, g);
+    run(0);
+    for (auto& t : th) t.join();
+    for (int g = 0; g < G; g++)
+        if (st[g] != KP_OK)
+            return g == 0 ? st[0] : fail(ctx, st[g], "device " + std::to_string(dev[g]->device) + ": " + dev[g]->err);
+    int64_t sum[CS_COUNT] = {};
+    double ms0 = 0, ms1 = 0;
+    for (int g = 0; g < G; g++) {
+        if (hi[g] <= lo[g]) continue;
+        for (int i = 0; i < CS_COUNT; i++) sum[i] += dev[g]->cons_stats[i];
+        ms0 = std::max(ms0, dev[g]->cons_ms[0]);
+        ms1 = std::max(ms1, dev[g]->cons_ms[1]);
+    }
+    for (int i = 0; i < CS_COUNT; i++) ctx->cons_stats[i] = sum[i];
+    ctx->cons_ms[0] = ms0;
+    ctx->cons_ms[1] = ms1;
+    ctx->cons_ms[2] = ns_since(t0) * 1e-6;
     return KP_OK;
 } catch (const std::exception& e) {
     return fail(ctx, KP_E_INVALID, e.what());

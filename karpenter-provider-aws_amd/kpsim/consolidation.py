@@ -72,14 +72,16 @@ def shard_range(n_probes, rank, world):
     return b0, min(n_probes, b0 + per)
 
 
-def compute_command(cp: model.ConsolidationProblem, mode, probe_fn, max_candidates=100, group=None) -> Command:
+def compute_command(cp: model.ConsolidationProblem, mode, probe_fn, max_candidates=100, group=None,
+                    distributed=True) -> Command:
     """ComputeCommand for one mode.  probe_fn(cp, mode, begin, end) evaluates probes [begin, end) (kp_consolidate on
     this rank's GPU).  With a torch.distributed group the probes are sharded across its ranks and one collective
-    carries each rank's result: the first valid single-node probe of the shard, or the shard's multi-node rows."""
+    carries each rank's result: the first valid single-node probe of the shard, or the shard's multi-node rows.
+    distributed=False: probe_fn covers the whole range in this process (a multi-device kp_ctx shards internally)."""
     n = model.consolidation_probe_count(len(cp.candidates), mode, max_candidates)
     if n == 0:
         return NO_OP
-    if group is None and not _dist_on():
+    if not distributed or (group is None and not _dist_on()):
         res = probe_fn(cp, mode, 0, 0)
         probe = first_valid_single(res) if mode == abi.KP_CONSOLIDATE_SINGLE else \
             replay_multi(res, len(cp.candidates), max_candidates)

@@ -77,3 +77,47 @@ def test_config4_full_size_properties(ctx, golden):
     assert_probes_equal(dev, pyoracle.consolidate(cp, abi.KP_CONSOLIDATE_SINGLE, n_threads=8))
     multi = device_probes(ctx, cp, abi.KP_CONSOLIDATE_MULTI)
     assert_probes_equal(multi, pyoracle.consolidate(cp, abi.KP_CONSOLIDATE_MULTI, n_threads=8))
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_multi_device_ctx(golden, devices):
+    """kp_device_opts.devices: one ctx over several device streams (the same ordinal repeated on a
+    one-GPU box) shards the probe range internally and gathers the shards; equal to the single-device evaluation,
+    also over a sub-range, and the summed counters cover every probe."""
+    from kpsim import native
+    cp = synth.config4(n_nodes=400, catalog=golden, n_pending=50)
+    one = native.Context(0)
+    multi = native.Context(devices=devices)
+    try:
+        for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+            want = device_probes(one, cp, mode)
+            got = device_probes(multi, cp, mode)
+            assert_probes_equal(got, want)
+            _, cst = multi.consolidate_stats()
+            assert cst[4] == len(want)  # probes evaluated, summed over the devices
+            n = len(want)
+            assert_probes_equal(device_probes(multi, cp, mode, begin=n // 3, end=n - 2), want[n // 3:n - 2])
+        # split form: prepare once (every device), execute twice
+        multi.consolidate_prepare(model.ConsolidateInputView(cp, abi.KP_CONSOLIDATE_SINGLE))
+        n_s = model.consolidation_probe_count(len(cp.candidates), abi.KP_CONSOLIDATE_SINGLE)
+        a = multi.consolidate_execute(abi.KP_CONSOLIDATE_SINGLE, n_s)
+        assert_probes_equal(a, device_probes(one, cp, abi.KP_CONSOLIDATE_SINGLE))
+    finally:
+        multi.close()
+        one.close()
+
+
+def test_multi_device_state_errors(golden):
+    """A solve prepare on the primary invalidates the multi-device pass (KP_E_STATE), like the single-device ctx."""
+    from kpsim import native
+    cp = synth.config4(n_nodes=100, catalog=golden, n_pending=0)
+    multi = native.Context(devices=[0, 0])
+    try:
+        multi.upload_catalog(model.CatalogView(cp.cluster.catalog))
+        multi.consolidate_prepare(model.ConsolidateInputView(cp, abi.KP_CONSOLIDATE_SINGLE))
+        multi.prepare(model.SolveInputView(cp.cluster))
+        with pytest.raises(native.KpError) as e:
+            multi.consolidate_execute(abi.KP_CONSOLIDATE_SINGLE, len(cp.candidates))
+        assert e.value.status == abi.KP_E_STATE
+    finally:
+        multi.close()
