@@ -438,7 +438,7 @@ __device__ __forceinline__ void commit_reservations(const KpDev& d, int32_t* rca
 // and whose witness type still fits is placed without an evaluation (exact: see pick_witness).  Any other pod is
 // handed to all 8 waves (the slow path: NodeClaim.Add of up to 8 candidates at once, or the templates).
 template <bool RESV, bool TOPO>
-__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
+__device__ __forceinline__ void ffd_solve(KpDev d) {
     constexpr bool TOPO_ON = KP_TOPO_ON && TOPO;  // the solve has topology groups
     extern __shared__ __attribute__((aligned(16))) char smem[];
     FfdShared& S = *reinterpret_cast<FfdShared*>(smem);
@@ -1398,6 +1398,13 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) {
     }
 }
 
+// One named entry point per feature instantiation, so kernel traces (rocprofv3 --stats) report the common case
+// (ffd_kernel: no topology groups, no reserved offerings) separately from the topology / reservation variants.
+__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) { ffd_solve<false, false>(d); }
+__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_topo_kernel(KpDev d) { ffd_solve<false, true>(d); }
+__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_resv_kernel(KpDev d) { ffd_solve<true, false>(d); }
+__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_resv_topo_kernel(KpDev d) { ffd_solve<true, true>(d); }
+
 // ------------------------------------------------------------------------------------------------
 // FinalizeScheduling + Truncate(OrderByPrice, maxInstanceTypes) + SatisfiesMinValues
 // ------------------------------------------------------------------------------------------------
@@ -1646,8 +1653,8 @@ hipError_t kp_launch_template_init(const KpDev& d, hipStream_t s) {
 // Per-device kernel attributes: called by kp_ctx_create with the ctx's device current (every ctx, so a second ctx on
 // another device of the same process gets them too; the call is idempotent and needs no process-wide flag).
 hipError_t kp_ffd_set_attributes() {
-    const void* ks[4] = {(const void*)ffd_kernel<false, false>, (const void*)ffd_kernel<false, true>,
-                         (const void*)ffd_kernel<true, false>, (const void*)ffd_kernel<true, true>};
+    const void* ks[4] = {(const void*)ffd_kernel, (const void*)ffd_topo_kernel, (const void*)ffd_resv_kernel,
+                         (const void*)ffd_resv_topo_kernel};
     for (const void* k : ks) {
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, KP_LDS_BYTES);
         if (e != hipSuccess) return e;
@@ -1658,10 +1665,10 @@ hipError_t kp_launch_ffd(const KpDev& d, hipStream_t s) {
     const size_t bytes = (size_t)d.lds_bytes;
     // instantiation by solve features: reserved offerings (RESV), topology groups (TOPO)
     const dim3 g(1), b(KP_NWAVES * 64);
-    if (d.ro && d.G > 0) hipLaunchKernelGGL((ffd_kernel<true, true>), g, b, bytes, s, d);
-    else if (d.ro) hipLaunchKernelGGL((ffd_kernel<true, false>), g, b, bytes, s, d);
-    else if (d.G > 0) hipLaunchKernelGGL((ffd_kernel<false, true>), g, b, bytes, s, d);
-    else hipLaunchKernelGGL((ffd_kernel<false, false>), g, b, bytes, s, d);
+    if (d.ro && d.G > 0) hipLaunchKernelGGL(ffd_resv_topo_kernel, g, b, bytes, s, d);
+    else if (d.ro) hipLaunchKernelGGL(ffd_resv_kernel, g, b, bytes, s, d);
+    else if (d.G > 0) hipLaunchKernelGGL(ffd_topo_kernel, g, b, bytes, s, d);
+    else hipLaunchKernelGGL(ffd_kernel, g, b, bytes, s, d);
     return hipGetLastError();
 }
 hipError_t kp_launch_finalize(const KpDev& d, int n_nodeclaims, hipStream_t s) {

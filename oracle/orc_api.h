@@ -26,6 +26,7 @@ void orc_result_free(orc_result* res);
 int32_t orc_consolidate_probe_count(const kp_consolidate_input* in);
 kp_status orc_consolidate(const kp_catalog_view* cat, const kp_consolidate_input* in, kp_probe_result* results,
                           int32_t cap_results, int32_t n_threads);
+double orc_consolidate_last_probe_seconds(void);
 
 /* Launch-time selection (filter.go chain + Truncate + getCapacityType + getOverrides' offering side), same
  * contract as kp_launch_select. */

@@ -1241,6 +1241,8 @@ extern "C" int32_t orc_consolidate_probe_count(const kp_consolidate_input* in) {
     return in ? consolidate_probe_count(in) : 0;
 }
 
+static std::atomic<double> g_last_probe_seconds{0.0};
+
 extern "C" kp_status orc_consolidate(const kp_catalog_view* cat, const kp_consolidate_input* in,
                                      kp_probe_result* results, int32_t cap_results, int32_t n_threads) {
     if (!cat || !in) return KP_E_INVALID;
@@ -1280,6 +1282,7 @@ extern "C" kp_status orc_consolidate(const kp_catalog_view* cat, const kp_consol
     X.v_od = D.value(X.ct_key, "on-demand");
     // the dictionary is frozen from here on: probes only read it
     const int nt = n_threads > 1 ? n_threads : 1;
+    const auto tp0 = std::chrono::steady_clock::now();
     std::atomic<int> next{b0};
     auto worker = [&]() {
         for (;;) {
@@ -1292,8 +1295,12 @@ extern "C" kp_status orc_consolidate(const kp_catalog_view* cat, const kp_consol
     for (int t = 1; t < nt; t++) th.emplace_back(worker);
     worker();
     for (auto& t : th) t.join();
+    g_last_probe_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - tp0).count();
     return KP_OK;
 }
+
+// Wall time of the probe phase of the last orc_consolidate (input parsing excluded): bench.py's CPU baseline.
+extern "C" double orc_consolidate_last_probe_seconds(void) { return g_last_probe_seconds; }
 
 extern "C" kp_status orc_result_nodeclaim_requirements(const orc_result* res, int32_t nc, char* buf, int64_t cap,
                                                        int64_t* needed) {

@@ -161,6 +161,13 @@ def consolidate(cp, mode, probe_begin=0, probe_end=0, spot_to_spot=False, max_ca
     return out[:max(0, b1 - b0)]
 
 
+def last_consolidate_seconds():
+    """Probe-phase wall time of the last consolidate() call (the oracle's input parsing excluded)."""
+    L = lib()
+    L.orc_consolidate_last_probe_seconds.restype = C.c_double
+    return float(L.orc_consolidate_last_probe_seconds())
+
+
 def launch_select(catalog_view, batch, M=60):
     """orc_launch_select over a kpsim.model.LaunchBatchView → (status, model.LaunchResults)."""
     from kpsim import model
