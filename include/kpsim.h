@@ -164,9 +164,25 @@ typedef struct kp_topology_term {
     const char* const* namespaces;
 } kp_topology_term;
 
-/* A pod class: pods that share scheduling constraints (podData.Requirements, tolerations, labels, topology). */
+/* corev1.NodeSelectorTerm (required node affinity) or PreferredSchedulingTerm (preferred node affinity). */
+typedef struct kp_node_selector_term {
+    int32_t weight;                          /* PreferredSchedulingTerm.Weight (required terms: ignored) */
+    int32_t n_requirements;                  /* MatchExpressions */
+    const kp_requirement* requirements;
+} kp_node_selector_term;
+
+/*
+ * A pod class: pods that share scheduling constraints (podData.Requirements, tolerations, labels, topology).
+ * Preferences ([core] scheduling/preferences.go Relax, applied per pod when it fails to schedule, PREFERENCE_POLICY
+ * Respect): the heaviest preferred node-affinity term and every preferred pod (anti-)affinity / ScheduleAnyway spread
+ * constrain the pod until relaxed one at a time, in the order: the first of several required node-affinity terms,
+ * the heaviest preferred pod-affinity term, the heaviest preferred anti-affinity term, the heaviest preferred
+ * node-affinity term, the first ScheduleAnyway spread, then (when a NodePool carries a PreferNoSchedule taint) a
+ * toleration of PreferNoSchedule taints.  A relaxed pod is re-queued with Queue.Push(pod, relaxed = true).
+ */
 typedef struct kp_pod_class {
-    int32_t n_requirements;                  /* nodeSelector ∪ requiredDuringScheduling term[0] */
+    int32_t n_requirements;                  /* nodeSelector ∪ requiredDuringScheduling term[0]; with n_required_terms
+                                                > 0: the nodeSelector only */
     const kp_requirement* requirements;
     int32_t n_tolerations;
     const kp_toleration* tolerations;
@@ -176,6 +192,11 @@ typedef struct kp_pod_class {
     const char* const* label_values;
     int32_t n_topology;
     const kp_topology_term* topology;
+    int32_t n_required_terms;                /* nodeAffinity.requiredDuringScheduling NodeSelectorTerms (ORed; tried in
+                                                order as relaxation removes the first); 0: folded into requirements */
+    const kp_node_selector_term* required_terms;
+    int32_t n_preferred_terms;               /* nodeAffinity.preferredDuringScheduling terms (<= 12) */
+    const kp_node_selector_term* preferred_terms;
 } kp_pod_class;
 
 typedef struct kp_pods_view {

@@ -68,6 +68,7 @@ KP_TOPO_SPREAD, KP_TOPO_AFFINITY, KP_TOPO_ANTI_AFFINITY = 0, 1, 2
 KP_POLICY_IGNORE, KP_POLICY_HONOR = 0, 1
 KP_DO_NOT_SCHEDULE, KP_SCHEDULE_ANYWAY = 0, 1
 KP_PREFERENCE_RESPECT, KP_PREFERENCE_IGNORE = 0, 1
+KP_MIN_VALUES_STRICT, KP_MIN_VALUES_BEST_EFFORT = 0, 1
 
 
 class kp_topology_term(C.Structure):
@@ -77,11 +78,17 @@ class kp_topology_term(C.Structure):
                 ("selector", C.POINTER(kp_requirement)), ("n_namespaces", C.c_int32), ("namespaces", c_char_pp)]
 
 
+class kp_node_selector_term(C.Structure):
+    _fields_ = [("weight", C.c_int32), ("n_requirements", C.c_int32), ("requirements", C.POINTER(kp_requirement))]
+
+
 class kp_pod_class(C.Structure):
     _fields_ = [("n_requirements", C.c_int32), ("requirements", C.POINTER(kp_requirement)),
                 ("n_tolerations", C.c_int32), ("tolerations", C.POINTER(kp_toleration)),
                 ("namespace_name", C.c_char_p), ("n_labels", C.c_int32), ("label_keys", c_char_pp),
-                ("label_values", c_char_pp), ("n_topology", C.c_int32), ("topology", C.POINTER(kp_topology_term))]
+                ("label_values", c_char_pp), ("n_topology", C.c_int32), ("topology", C.POINTER(kp_topology_term)),
+                ("n_required_terms", C.c_int32), ("required_terms", C.POINTER(kp_node_selector_term)),
+                ("n_preferred_terms", C.c_int32), ("preferred_terms", C.POINTER(kp_node_selector_term))]
 
 
 class kp_pods_view(C.Structure):
@@ -215,6 +222,17 @@ def requirement_array(keep, reqs):
         arr[i].min_values = -1 if r.min_values is None else int(r.min_values)
     keep.hold(arr)
     return len(reqs), arr
+
+
+def node_term_array(keep, terms):
+    """terms: iterable of (weight, [model.Requirement]) -> (n, POINTER(kp_node_selector_term))"""
+    terms = list(terms)
+    arr = (kp_node_selector_term * max(1, len(terms)))()
+    for i, (w, reqs) in enumerate(terms):
+        arr[i].weight = int(w)
+        arr[i].n_requirements, arr[i].requirements = requirement_array(keep, reqs)
+    keep.hold(arr)
+    return len(terms), arr
 
 
 def taint_array(keep, taints):

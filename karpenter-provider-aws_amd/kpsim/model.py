@@ -10,7 +10,7 @@ Types mirror the Go types they stand for:
 """
 import ctypes as C
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 
@@ -139,11 +139,16 @@ HOSTNAME = "kubernetes.io/hostname"
 
 @dataclass
 class PodClass:
+    """requirements: nodeSelector ∪ required node-affinity term[0], or the nodeSelector alone when required_terms is
+    given (the ORed NodeSelectorTerms, relaxed from the front).  preferred_terms: (weight, requirements) of the
+    preferred node affinity (kpsim.h kp_pod_class)."""
     requirements: List[Requirement] = field(default_factory=list)
     tolerations: List[Toleration] = field(default_factory=list)
     labels: Dict[str, str] = field(default_factory=dict)
     namespace: str = "default"
     topology: List[TopologyTerm] = field(default_factory=list)
+    required_terms: List[List[Requirement]] = field(default_factory=list)
+    preferred_terms: List[Tuple[int, List[Requirement]]] = field(default_factory=list)
 
 
 @dataclass
@@ -317,6 +322,8 @@ class SolveInputView:
             cls[i].label_keys = k.cstrs(list(pc.labels.keys()))
             cls[i].label_values = k.cstrs(list(pc.labels.values()))
             cls[i].n_topology, cls[i].topology = abi.topology_array(k, pc.topology)
+            cls[i].n_required_terms, cls[i].required_terms = abi.node_term_array(k, [(0, t) for t in pc.required_terms])
+            cls[i].n_preferred_terms, cls[i].preferred_terms = abi.node_term_array(k, pc.preferred_terms)
         k.hold(cls)
         ex = (abi.kp_existing_node * max(1, len(prob.existing)))()
         for i, e in enumerate(prob.existing):

@@ -114,6 +114,7 @@ struct LabelSel {
 // One topology term of a pod class (kp_topology_term)
 struct TopoTerm {
     int type = 0, key = -1, max_skew = 1, min_domains = -1, aff_pol = KP_POLICY_HONOR, taint_pol = KP_POLICY_IGNORE;
+    bool preferred = false;  // ScheduleAnyway spread / weighted (anti-)affinity: no inverse group (only required terms)
     LabelSel sel;
     std::vector<std::string> namespaces;
 };
@@ -230,7 +231,12 @@ struct Solver {
     explicit Solver(Dict& d) : D(d) {}
     const InstanceType& ty(int t) const { return (*tp)[t]; }
     const Pod& pod_at(int li) const { return (*pp)[plist[li]]; }
-    const PodClass& cls_of(int li) const { return (*cp)[pod_at(li).cls]; }
+    // the pod's class as preferences.Relax left it (a relaxed pod moves to its class's next relaxation stage)
+    std::vector<int> pcls;            // by position in plist
+    std::vector<int> relax_next;      // per class: the class after one Relax step, -1 when nothing is left to relax
+    bool best_effort = false;         // MIN_VALUES_POLICY=BestEffort
+    int cls_id(int li) const { return pcls.empty() ? pod_at(li).cls : pcls[li]; }
+    const PodClass& cls_of(int li) const { return (*cp)[cls_id(li)]; }
 
     // compatible(it, reqs) = it.Requirements.Intersects(reqs) == nil
     bool compatible(const InstanceType& it, const Reqs& reqs) const { return reqs_intersects(D, it.reqs, reqs); }
@@ -266,14 +272,32 @@ struct Solver {
             if ((int)sk.second.size() < reqs.m.at(sk.first).min_values) return false;
         return true;
     }
-    // filterInstanceTypesByRequirements (MIN_VALUES_POLICY=Strict)
-    std::vector<int> filter(const std::vector<int>& its, const Reqs& reqs, const std::vector<int64_t>& total) const {
+    // filterInstanceTypesByRequirements.  MIN_VALUES_POLICY=Strict: a remaining list that fails SatisfiesMinValues is
+    // emptied.  BestEffort: the list is kept and, when `relax` is given (NodeClaim.Add), every unsatisfied minValues
+    // key is relaxed to the number of distinct values the list offers (SatisfiesMinValues' unsatisfiableKeys; the
+    // NodeClaim's requirements carry the relaxed minValues from then on).
+    std::vector<int> filter(const std::vector<int>& its, const Reqs& reqs, const std::vector<int64_t>& total,
+                            Reqs* relax = nullptr) const {
         std::vector<int> out;
         for (int t : its) {
             const InstanceType& it = ty(t);
             if (compatible(it, reqs) && fits(total, it.alloc) && has_offering(it, reqs)) out.push_back(t);
         }
-        if (reqs.has_min_values() && !satisfies_min_values(out, reqs)) out.clear();
+        if (reqs.has_min_values() && !satisfies_min_values(out, reqs)) {
+            if (!best_effort) {
+                out.clear();
+            } else if (relax && !out.empty()) {
+                for (auto& kv : relax->m) {
+                    if (!kv.second.has_min) continue;
+                    std::vector<int> vals;
+                    for (int t : out)
+                        for (int v : ty(t).reqs.get(kv.first).values) vals.push_back(v);
+                    std::sort(vals.begin(), vals.end());
+                    vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
+                    if ((int)vals.size() < kv.second.min_values) kv.second.min_values = (int)vals.size();
+                }
+            }
+        }
         return out;
     }
 
@@ -383,7 +407,7 @@ struct Solver {
     // Topology.AddRequirements + NodeClaim.Add's Compatible(nodeClaimRequirements, topologyRequirements) + Add:
     // every group that constrains the pod contributes its domains computed from the same nodeRequirements.
     bool topo_add(int li, Reqs& r, bool allow_wk) const {
-        const int c = pod_at(li).cls;
+        const int c = cls_id(li);
         if (t_cons.empty() || t_cons[c].empty()) return true;
         const PodClass& pc = (*cp)[c];
         Reqs topo = r;
@@ -402,7 +426,7 @@ struct Solver {
     // Topology.Record(pod, taints, requirements): every group whose Counts(pod) holds records the domain(s) the pod
     // lands in; inverse groups owned by the pod record every value of the requirement.
     void topo_record(int li, const Reqs& r, const std::vector<Taint>& taints, bool allow_wk) {
-        const int c = pod_at(li).cls;
+        const int c = cls_id(li);
         if (t_rec.empty()) return;
         for (int gi : t_rec[c]) {
             TopoGroup& g = groups[gi];
@@ -433,7 +457,7 @@ struct Solver {
         if (!topo_add(li, r, true)) return false;  // topology.AddRequirements
         std::vector<int64_t> requests(R);
         for (int k = 0; k < R; k++) requests[k] = nc.requests[k] + pod.req[k];
-        std::vector<int> remaining = filter(nc.options, r, requests);
+        std::vector<int> remaining = filter(nc.options, r, requests, &r);
         if (remaining.empty()) return false;
         std::vector<int> held;
         if (resv_on && !offerings_to_reserve(nc, remaining, r, held)) return false;
@@ -527,7 +551,7 @@ struct Solver {
         go_sort_slice(sa);
         stats.nodeclaim_candidates_scanned += (int64_t)newNodeClaims.size();
         const bool tr = (trace_pod >= 0 && plist[li] == trace_pod) ||
-                        (trace_cls >= 0 && pod_at(li).cls == trace_cls);  // ORC_TRACE_POD / ORC_TRACE_CLASS diagnostics
+                        (trace_cls >= 0 && cls_id(li) == trace_cls);  // ORC_TRACE_POD / ORC_TRACE_CLASS diagnostics
         for (int idx : newNodeClaims) {
             stats.nodeclaim_evals++;
             if (tr) {
@@ -601,6 +625,8 @@ struct Solver {
         });
         std::deque<int> q(order.begin(), order.end());
         std::unordered_map<int, int> lastLen;
+        pcls.resize(n);
+        for (int i = 0; i < n; i++) pcls[i] = pod_at(i).cls;
         pod_result.assign(n, KP_POD_UNSCHEDULABLE);
         pod_order.assign(n, -1);
         for (;;) {
@@ -614,9 +640,16 @@ struct Solver {
                 pod_order[li] = placements++;
                 continue;
             }
-            // preferences.Relax: no preferred terms in this build's inputs → never relaxed
+            // preferences.Relax, then Queue.Push(pod, relaxed): a relaxed pod clears lastLen (and Topology.Update /
+            // updateCachedPodData take its new spec: the next relaxation stage of its class)
+            const int nx = relax_next.empty() ? -1 : relax_next[cls_id(li)];
             q.push_back(li);
-            lastLen[li] = (int)q.size();
+            if (nx >= 0) {
+                pcls[li] = nx;
+                lastLen.clear();
+            } else {
+                lastLen[li] = (int)q.size();
+            }
         }
     }
 
@@ -764,56 +797,181 @@ static kp_status parse_into(Solver& s, const kp_catalog_view* cat, const kp_solv
         s.own_types[t].offerings.push_back(std::move(of));
     }
     s.resv_on = s.resv_on && !s.rid_names.empty();
-    // pod classes
-    s.own_classes.resize(in->n_classes);
-    for (int c = 0; c < in->n_classes; c++) {
+    // pod classes, expanded into preferences.Relax stages: stage 0 of class c is own_classes[c]; further stages are
+    // appended, relax_next links them (kp_pod_class comment in kpsim.h; preferences.go, recalled)
+    bool tol_pns = false;  // NewScheduler: some NodePool template carries a PreferNoSchedule taint
+    for (int i = 0; i < in->n_nodepools; i++)
+        for (int j = 0; j < in->nodepools[i].n_taints; j++)
+            if (in->nodepools[i].taints[j].effect && !strcmp(in->nodepools[i].taints[j].effect, "PreferNoSchedule"))
+                tol_pns = true;
+    std::vector<std::string> topo_keys;  // every topology key of the input (strict pod requirements, see below)
+    for (int c = 0; c < in->n_classes; c++)
+        for (int i = 0; i < in->classes[c].n_topology; i++)
+            if (in->classes[c].topology[i].topology_key) topo_keys.push_back(normalize_label(in->classes[c].topology[i].topology_key));
+    auto parse_term = [&](const kp_topology_term& x, const std::string& ns, TopoTerm& t) -> kp_status {
+        if (x.type < KP_TOPO_SPREAD || x.type > KP_TOPO_ANTI_AFFINITY || !x.topology_key) return KP_E_INVALID;
+        t.type = x.type;
+        t.key = D.key(normalize_label(x.topology_key));
+        t.max_skew = x.type == KP_TOPO_SPREAD ? x.max_skew : INT32_MAX;
+        if (x.type == KP_TOPO_SPREAD && x.max_skew <= 0) return KP_E_INVALID;
+        t.min_domains = x.type == KP_TOPO_SPREAD && x.min_domains > 0 ? x.min_domains : -1;
+        t.aff_pol = x.type == KP_TOPO_SPREAD ? x.node_affinity_policy : KP_POLICY_IGNORE;
+        t.taint_pol = x.type == KP_TOPO_SPREAD ? x.node_taints_policy : KP_POLICY_IGNORE;
+        t.preferred = x.type == KP_TOPO_SPREAD ? x.when_unsatisfiable == KP_SCHEDULE_ANYWAY : x.weight > 0;
+        t.sel.nil = x.n_selector < 0;
+        for (int j = 0; j < x.n_selector; j++) {
+            const kp_requirement& q = x.selector[j];
+            if (!q.key || q.op < KP_OP_IN || q.op > KP_OP_DOES_NOT_EXIST) return KP_E_INVALID;
+            LabelSel::Term st;
+            st.key = q.key;
+            st.op = q.op;
+            st.values = strs(q.values, q.n_values);
+            t.sel.terms.push_back(st);
+        }
+        if (x.type == KP_TOPO_SPREAD || x.n_namespaces <= 0) t.namespaces = {ns};
+        else t.namespaces = strs(x.namespaces, x.n_namespaces);
+        return KP_OK;
+    };
+    // The spec state a pod's Relax steps walk through.
+    struct Spec {
+        int req_first = 0;           // first remaining required node-affinity term
+        std::vector<int> pnode;      // remaining preferred node-affinity terms, heaviest first (stable)
+        std::vector<int> paff, panti;  // remaining preferred pod (anti-)affinity terms, heaviest first (SliceStable)
+        std::vector<int> spreads;    // TopologySpreadConstraints in spec order (swap-with-last removal)
+        bool pns = false;            // the PreferNoSchedule toleration was added
+    };
+    const int C0 = in->n_classes;
+    s.own_classes.clear();
+    s.own_classes.resize(C0);
+    s.relax_next.assign(C0, -1);
+    bool any_relax = false;
+    std::vector<std::pair<int, Spec>> work;  // (class id, spec) whose Relax step is still to be derived
+    for (int c = 0; c < C0; c++) {
         const kp_pod_class& pc = in->classes[c];
-        PodClass& oc = s.own_classes[c];
-        if (!build_reqs(D, pc.requirements, pc.n_requirements, oc.reqs)) return KP_E_INVALID;
+        if (pc.n_preferred_terms > 12) return KP_E_UNSUPPORTED;  // newPodRequirements' sort.Slice is stable only up to 12
+        Spec sp;
+        for (int i = 0; i < pc.n_preferred_terms; i++) sp.pnode.push_back(i);
+        std::stable_sort(sp.pnode.begin(), sp.pnode.end(), [&](int a, int b) {
+            return pc.preferred_terms[a].weight > pc.preferred_terms[b].weight;
+        });
+        for (int i = 0; i < pc.n_topology; i++) {
+            const kp_topology_term& x = pc.topology[i];
+            if (x.type == KP_TOPO_SPREAD) sp.spreads.push_back(i);
+            else if (x.weight > 0) (x.type == KP_TOPO_AFFINITY ? sp.paff : sp.panti).push_back(i);
+        }
+        for (auto* v : {&sp.paff, &sp.panti})
+            std::stable_sort(v->begin(), v->end(), [&](int a, int b) { return pc.topology[a].weight > pc.topology[b].weight; });
+        // restrictions shared with the device build: the topology node filter takes the nodeSelector and EVERY required
+        // term (ORed) but no preference, and pod domains come from the strict requirements (no preferred term)
+        bool honor_spread = false;
+        for (int i = 0; i < pc.n_topology; i++)
+            honor_spread |= pc.topology[i].type == KP_TOPO_SPREAD && pc.topology[i].node_affinity_policy == KP_POLICY_HONOR;
+        if (honor_spread && pc.n_required_terms > 1) return KP_E_UNSUPPORTED;
+        if (pref_policy == KP_PREFERENCE_RESPECT && pc.n_preferred_terms > 0) {
+            if (honor_spread) return KP_E_UNSUPPORTED;
+            for (int i = 0; i < pc.n_preferred_terms; i++)
+                for (int j = 0; j < pc.preferred_terms[i].n_requirements; j++) {
+                    const char* k = pc.preferred_terms[i].requirements[j].key;
+                    if (k && std::find(topo_keys.begin(), topo_keys.end(), normalize_label(k)) != topo_keys.end())
+                        return KP_E_UNSUPPORTED;
+                }
+        }
+        work.push_back({c, sp});
+    }
+    auto has_pns_tol = [](const kp_pod_class& pc) {  // Toleration.MatchToleration of {Exists, PreferNoSchedule}
+        for (int i = 0; i < pc.n_tolerations; i++) {
+            const kp_toleration& t = pc.tolerations[i];
+            if (t.op == KP_TOL_EXISTS && (!t.key || !*t.key) && (!t.value || !*t.value) && t.effect &&
+                !strcmp(t.effect, "PreferNoSchedule"))
+                return true;
+        }
+        return false;
+    };
+    std::vector<int> origin(C0);  // class id -> input class
+    for (int c = 0; c < C0; c++) origin[c] = c;
+    for (size_t w = 0; w < work.size(); w++) {
+        const int id = work[w].first;
+        const Spec sp = work[w].second;
+        const int oc = origin[id];
+        const kp_pod_class& pc = in->classes[oc];
+        // the effective PodClass of this spec
+        PodClass& out = s.own_classes[id];
+        if (!build_reqs(D, pc.requirements, pc.n_requirements, out.reqs)) return KP_E_INVALID;
+        if (pc.n_required_terms > 0 &&
+            !build_reqs(D, pc.required_terms[sp.req_first].requirements, pc.required_terms[sp.req_first].n_requirements, out.reqs))
+            return KP_E_INVALID;
+        if (pref_policy == KP_PREFERENCE_RESPECT && !sp.pnode.empty() &&
+            !build_reqs(D, pc.preferred_terms[sp.pnode[0]].requirements, pc.preferred_terms[sp.pnode[0]].n_requirements, out.reqs))
+            return KP_E_INVALID;
         for (int i = 0; i < pc.n_tolerations; i++) {
             Toleration t;
             t.key = pc.tolerations[i].key ? pc.tolerations[i].key : "";
             t.op = pc.tolerations[i].op;
             t.value = pc.tolerations[i].value ? pc.tolerations[i].value : "";
             t.effect = pc.tolerations[i].effect ? pc.tolerations[i].effect : "";
-            oc.tols.push_back(t);
+            out.tols.push_back(t);
         }
-        if (pc.namespace_name) oc.ns = pc.namespace_name;
+        if (sp.pns) {
+            Toleration t;
+            t.op = KP_TOL_EXISTS;
+            t.effect = "PreferNoSchedule";
+            out.tols.push_back(t);
+        }
+        if (pc.namespace_name) out.ns = pc.namespace_name;
         for (int l = 0; l < pc.n_labels; l++)
-            oc.labels[pc.label_keys[l] ? pc.label_keys[l] : ""] = pc.label_values[l] ? pc.label_values[l] : "";
-        for (int i = 0; i < pc.n_topology; i++) {
+            out.labels[pc.label_keys[l] ? pc.label_keys[l] : ""] = pc.label_values[l] ? pc.label_values[l] : "";
+        auto add_term = [&](int i) -> kp_status {
             const kp_topology_term& x = pc.topology[i];
-            if (x.type < KP_TOPO_SPREAD || x.type > KP_TOPO_ANTI_AFFINITY || !x.topology_key) return KP_E_INVALID;
             const bool preferred = x.type == KP_TOPO_SPREAD ? x.when_unsatisfiable == KP_SCHEDULE_ANYWAY : x.weight > 0;
-            if (preferred) {
-                // PREFERENCE_POLICY=Ignore drops preferences; Respect relaxes them on failure (preferences.go), which
-                // this restatement does not implement
-                if (pref_policy == KP_PREFERENCE_IGNORE) continue;
-                return KP_E_UNSUPPORTED;
-            }
+            if (preferred && pref_policy == KP_PREFERENCE_IGNORE) return KP_OK;  // Ignore drops preferences
             TopoTerm t;
-            t.type = x.type;
-            t.key = D.key(normalize_label(x.topology_key));
-            t.max_skew = x.type == KP_TOPO_SPREAD ? x.max_skew : INT32_MAX;
-            if (x.type == KP_TOPO_SPREAD && x.max_skew <= 0) return KP_E_INVALID;
-            t.min_domains = x.type == KP_TOPO_SPREAD && x.min_domains > 0 ? x.min_domains : -1;
-            t.aff_pol = x.type == KP_TOPO_SPREAD ? x.node_affinity_policy : KP_POLICY_IGNORE;
-            t.taint_pol = x.type == KP_TOPO_SPREAD ? x.node_taints_policy : KP_POLICY_IGNORE;
-            t.sel.nil = x.n_selector < 0;
-            for (int j = 0; j < x.n_selector; j++) {
-                const kp_requirement& q = x.selector[j];
-                if (!q.key || q.op < KP_OP_IN || q.op > KP_OP_DOES_NOT_EXIST) return KP_E_INVALID;
-                LabelSel::Term st;
-                st.key = q.key;
-                st.op = q.op;
-                st.values = strs(q.values, q.n_values);
-                t.sel.terms.push_back(st);
+            kp_status st = parse_term(x, out.ns, t);
+            if (st == KP_OK) out.terms.push_back(t);
+            return st;
+        };
+        for (int i : sp.spreads)
+            if (kp_status st = add_term(i)) return st;
+        for (int i = 0; i < pc.n_topology; i++)
+            if (pc.topology[i].type != KP_TOPO_SPREAD && pc.topology[i].weight <= 0)
+                if (kp_status st = add_term(i)) return st;
+        for (auto* v : {&sp.paff, &sp.panti})
+            for (int i : *v)
+                if (kp_status st = add_term(i)) return st;
+        // Preferences.Relax: the first relaxation that applies
+        Spec nx = sp;
+        bool relaxed = true;
+        if (pc.n_required_terms - sp.req_first > 1) {
+            nx.req_first++;                                  // removeRequiredNodeAffinityTerm
+        } else if (!sp.paff.empty()) {
+            nx.paff.erase(nx.paff.begin());                  // removePreferredPodAffinityTerm
+        } else if (!sp.panti.empty()) {
+            nx.panti.erase(nx.panti.begin());                // removePreferredPodAntiAffinityTerm
+        } else if (!sp.pnode.empty()) {
+            nx.pnode.erase(nx.pnode.begin());                // removePreferredNodeAffinityTerm
+        } else {
+            relaxed = false;
+            for (size_t i = 0; i < sp.spreads.size() && !relaxed; i++)
+                if (pc.topology[sp.spreads[i]].when_unsatisfiable == KP_SCHEDULE_ANYWAY) {  // removeTopologySpreadScheduleAnyway
+                    nx.spreads[i] = nx.spreads.back();
+                    nx.spreads.pop_back();
+                    relaxed = true;
+                }
+            if (!relaxed && tol_pns && !sp.pns && !has_pns_tol(pc)) {  // toleratePreferNoScheduleTaints
+                nx.pns = true;
+                relaxed = true;
             }
-            if (x.type == KP_TOPO_SPREAD || x.n_namespaces <= 0) t.namespaces = {oc.ns};
-            else t.namespaces = strs(x.namespaces, x.n_namespaces);
-            oc.terms.push_back(t);
+        }
+        if (relaxed) {
+            const int nid = (int)s.own_classes.size();
+            s.own_classes.emplace_back();
+            s.relax_next.push_back(-1);
+            origin.push_back(oc);
+            s.relax_next[id] = nid;
+            work.push_back({nid, nx});
+            any_relax = true;
         }
     }
+    if (!any_relax) s.relax_next.clear();
     // pods
     const kp_pods_view& pv = in->pods;
     s.own_pods.resize(pv.n_pods);
@@ -929,7 +1087,8 @@ static kp_status build_topology(Solver& s, const kp_solve_input* in, const std::
         const PodClass& pc = s.own_classes[c];
         for (const TopoTerm& t : pc.terms) {
             for (int inv = 0; inv < 2; inv++) {
-                if (inv && t.type != KP_TOPO_ANTI_AFFINITY) break;
+                // updateInverseAntiAffinity: only required anti-affinity terms get an inverse group
+                if (inv && (t.type != KP_TOPO_ANTI_AFFINITY || t.preferred)) break;
                 TopoGroup g;
                 g.type = t.type;
                 g.key = t.key;
@@ -999,13 +1158,15 @@ static kp_status build_topology(Solver& s, const kp_solve_input* in, const std::
 extern "C" kp_status orc_solve_opts(const kp_catalog_view* cat, const kp_solve_input* in, const kp_device_opts* opts,
                                     kp_solve_output* out, orc_result** res_out) {
     if (!cat || !in || !out) return KP_E_INVALID;
-    if (in->min_values_policy != KP_MIN_VALUES_STRICT) return KP_E_UNSUPPORTED;
+    if (in->min_values_policy != KP_MIN_VALUES_STRICT && in->min_values_policy != KP_MIN_VALUES_BEST_EFFORT)
+        return KP_E_INVALID;
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     auto res = std::make_unique<orc_result>();
     Solver s(res->D);
     s.resv_on = opts ? opts->reserved_capacity != 0 : true;  // FEATURE_GATES ReservedCapacity (default on)
     s.resv_strict = true;  // provisioning: scheduling.DisableReservedCapacityFallback
+    s.best_effort = in->min_values_policy == KP_MIN_VALUES_BEST_EFFORT;
     kp_status st = parse_into(s, cat, in, opts ? opts->preference_policy : KP_PREFERENCE_RESPECT);
     if (st != KP_OK) return st;
     for (int j = 0; j < (int)s.own_existing.size(); j++) s.ex_idx.push_back(j);
@@ -1254,6 +1415,7 @@ extern "C" kp_status orc_consolidate(const kp_catalog_view* cat, const kp_consol
     base.resv_strict = false;
     kp_status st = parse_into(base, cat, &in->cluster, KP_PREFERENCE_RESPECT);
     if (st != KP_OK) return st;
+    if (!base.relax_next.empty()) return KP_E_UNSUPPORTED;  // preference relaxation inside probes: not restated
     // consolidation over topology-constrained pods (topology counts of the remaining cluster, excluded candidate pods)
     // is not restated yet
     if (!base.groups.empty()) return KP_E_UNSUPPORTED;

@@ -171,14 +171,14 @@ def test_spread_selecting_another_class(golden):
         assert zone_of(q[r.pod_result[-1]]) == (("test-zone-1a",) if want == 1 else ("test-zone-1b",))
 
 
-def test_preferences_respect_unsupported_ignore_drops(golden):
+def test_preferences_respect_spreads_ignore_drops(golden):
     """ScheduleAnyway spreads are preferences: PREFERENCE_POLICY=Ignore drops them (same result as no term); Respect
-    needs preference relaxation, which the restatement rejects explicitly."""
+    treats them as DoNotSchedule until relaxed (one pod per NodeClaim here, every NodeClaim unconstrained)."""
     lab = {"app": "p"}
     pc, pods = deployment(6, lab, [TopologyTerm("spread", HOSTNAME, sel(lab), when_unsatisfiable="ScheduleAnyway")])
     prob = model.Problem(golden, [synth.default_nodepool()], [pc], pods)
-    with pytest.raises(RuntimeError):
-        solve(prob)
+    resp, _ = solve(prob)
+    assert resp.n_nodeclaims == 6 and (resp.pod_result >= 0).all()
     ign, _ = solve(prob, preference_policy=abi.KP_PREFERENCE_IGNORE)
     plain, _ = solve(model.Problem(golden, [synth.default_nodepool()], [PodClass(labels=lab)], pods))
     np.testing.assert_array_equal(ign.pod_result, plain.pod_result)
