@@ -34,7 +34,28 @@ struct WaveScratch {
                                // until a capacity comes back from 0, see the reservation step)
     int32_t rlive;             // success: the new options keep a compatible available reserved offering
     uint64_t held;             // success: reservation IDs the NodeClaim holds after the Add
+    // success under MIN_VALUES_POLICY=BestEffort: keys whose minValues the Add relaxes to the distinct values the
+    // remaining options offer (SatisfiesMinValues' unsatisfiable keys); the commit writes them into the NodeClaim
+    int32_t n_minrel;
+    int32_t minrel_k[KP_MAX_CLASS_KEYS];
+    int32_t minrel_v[KP_MAX_CLASS_KEYS];
 };
+
+// An unmet minValues key: Strict fails the Add; BestEffort records the relaxation (wave-uniform).
+__device__ __forceinline__ bool min_values_unmet(const KpDev& d, WaveScratch& ws, int k, int count, int lane) {
+    if (!d.best_effort) return false;
+    if (lane == 0 && ws.n_minrel < KP_MAX_CLASS_KEYS) {
+        ws.minrel_k[ws.n_minrel] = k;
+        ws.minrel_v[ws.n_minrel] = count;
+        ws.n_minrel++;
+    }
+    return true;
+}
+
+// Apply an Add's BestEffort minValues relaxations to NodeClaim slot n (after commit_reqs).
+__device__ __forceinline__ void commit_min_relax(const KpDev& d, const WaveScratch& ws, int n, int lane) {
+    if (lane < ws.n_minrel) d.nc_hdr[(size_t)n * d.K + ws.minrel_k[lane]].minv = ws.minrel_v[lane];
+}
 
 // Class-side operands of the evaluation, cached in LDS while consecutive pods share a class.
 struct ClassCache {
@@ -510,7 +531,10 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
     bool fail = false, kill = false;
     uint64_t adm = ~0ull;
     int kmul = -1;
-    if (lane == 0) ws.memo_ok = 1;
+    if (lane == 0) {
+        ws.memo_ok = 1;
+        ws.n_minrel = 0;
+    }
     // DoesNotExist-type elimination and the admissible value mask of a multi-valued key, from the merged requirement
     auto classify = [&](int k, const ReqHdr& O, const uint64_t* ow, int cnt) {
         const uint32_t kf = CC.kflags[lane];
@@ -697,7 +721,7 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
                 for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
                 count = c;
             }
-            if (count < h.minv) return false;
+            if (count < h.minv && !min_values_unmet(d, ws, k, count, lane)) return false;
         }
     }
     // ---- reservations (NodeClaim.Add's offeringsToReserve, ReservedOfferingModeStrict) ----
@@ -748,6 +772,7 @@ __device__ __forceinline__ void commit_reqs(const KpDev& d, const ClassCache& CC
 __device__ __forceinline__ bool eval_fits_only(const KpDev& d, const EvalEnv& E, const EvalIn& a, WaveScratch& ws,
                                                int lane) {
     const int TW = d.TW, T = d.T;
+    if (lane == 0) ws.n_minrel = 0;
     int64_t tot[KP_LDS_AXES];
 #pragma unroll
     for (int ai = 0; ai < KP_LDS_AXES; ai++) {
@@ -817,7 +842,7 @@ __device__ __forceinline__ bool eval_fits_only(const KpDev& d, const EvalEnv& E,
                 for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
                 count = c;
             }
-            if (count < h.minv) return false;
+            if (count < h.minv && !min_values_unmet(d, ws, k, count, lane)) return false;
         }
     }
     if (lane < TW) ws.opts[lane] = newword;

@@ -184,6 +184,16 @@ struct DBuf {  // device buffer, grow-only; freed by its destructor (the owning 
     }
 };
 
+struct PrefExpansion {
+    std::vector<kp_pod_class> classes;
+    std::vector<int32_t> relax_next;  // per expanded class; empty when no class can relax
+    kp_solve_input in{};
+    // storage of the stage classes' arrays (pointers are set once every stage exists)
+    std::vector<std::vector<kp_requirement>> reqs;
+    std::vector<std::vector<kp_toleration>> tols;
+    std::vector<std::vector<kp_topology_term>> terms;
+};
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
@@ -306,6 +316,10 @@ struct kp_ctx {
         d_cls_tcoff, d_cls_tc, d_cls_troff, d_cls_tr;
     DBuf<uint64_t> d_tg_known0, d_tg_known;
     DBuf<uint8_t> d_cls_kneutral, d_vrank;
+    // preference relaxation stages of the prepared solve (expand_preferences) and MIN_VALUES_POLICY
+    PrefExpansion pref;
+    bool best_effort = false;
+    DBuf<int32_t> d_relax_next, d_shape_next, d_pod_cls0, d_pod_shape0, d_last_ep;
     // last results (host)
     int last_N = 0, M = 0;
     std::vector<int32_t> h_nc_tmpl;
@@ -919,6 +933,179 @@ bool selector_matches(const kp_topology_term& t, const kp_pod_class& pc) {
 const char* ns_of(const kp_pod_class& pc) { return pc.namespace_name ? pc.namespace_name : "default"; }
 }  // namespace
 
+// ---------------------------------------------------------------------------------------------
+// preferences ([core] scheduling/preferences.go Relax; kpsim.h kp_pod_class).  Every input class becomes a chain of
+// effective classes, one per spec state a pod's Relax steps walk through: stage 0 keeps the input class id, further
+// stages are appended and linked by relax_next.  The device switches a failed pod to relax_next[class] and re-queues
+// it with Queue.Push(pod, relaxed = true).
+// ---------------------------------------------------------------------------------------------
+static kp_status expand_preferences(const kp_solve_input* in, int pref_policy, PrefExpansion& X, std::string& err) {
+    const int C0 = in->n_classes;
+    bool tol_pns = false;  // NewScheduler: a NodePool template carries a PreferNoSchedule taint
+    for (int i = 0; i < in->n_nodepools; i++)
+        for (int j = 0; j < in->nodepools[i].n_taints; j++) {
+            const char* e = in->nodepools[i].taints[j].effect;
+            tol_pns |= e && !strcmp(e, "PreferNoSchedule");
+        }
+    std::set<std::string> topo_keys;
+    for (int c = 0; c < C0; c++)
+        for (int i = 0; i < in->classes[c].n_topology; i++)
+            if (in->classes[c].topology[i].topology_key) topo_keys.insert(normalize(in->classes[c].topology[i].topology_key));
+    struct St {
+        int cls, origin, req_first;
+        std::vector<int> pnode, paff, panti, spreads;
+        bool pns;
+    };
+    std::vector<St> st;
+    bool any = false;
+    for (int c = 0; c < C0; c++) {
+        const kp_pod_class& pc = in->classes[c];
+        St x{c, c, 0, {}, {}, {}, {}, false};
+        if (pc.n_preferred_terms > 12) {
+            err = "more than 12 preferred node-affinity terms (newPodRequirements' sort.Slice order)";
+            return KP_E_UNSUPPORTED;
+        }
+        if ((pc.n_required_terms > 0 && !pc.required_terms) || (pc.n_preferred_terms > 0 && !pc.preferred_terms) ||
+            (pc.n_topology > 0 && !pc.topology)) {
+            err = "pod class arrays";
+            return KP_E_INVALID;
+        }
+        for (int i = 0; i < pc.n_preferred_terms; i++) x.pnode.push_back(i);
+        std::stable_sort(x.pnode.begin(), x.pnode.end(),
+                         [&](int a, int b) { return pc.preferred_terms[a].weight > pc.preferred_terms[b].weight; });
+        bool honor = false;
+        for (int i = 0; i < pc.n_topology; i++) {
+            const kp_topology_term& t = pc.topology[i];
+            if (t.type == KP_TOPO_SPREAD) {
+                x.spreads.push_back(i);
+                honor |= t.node_affinity_policy == KP_POLICY_HONOR;
+            } else if (t.weight > 0) {
+                (t.type == KP_TOPO_AFFINITY ? x.paff : x.panti).push_back(i);
+            }
+        }
+        for (auto* v : {&x.paff, &x.panti})
+            std::stable_sort(v->begin(), v->end(), [&](int a, int b) { return pc.topology[a].weight > pc.topology[b].weight; });
+        // the topology node filter takes the nodeSelector with EVERY required term (ORed) and no preference; pod domains
+        // come from the strict requirements: combinations that would need those apart are refused, not approximated
+        if (honor && pc.n_required_terms > 1) {
+            err = "a spread with nodeAffinityPolicy Honor on a pod with several required node-affinity terms";
+            return KP_E_UNSUPPORTED;
+        }
+        if (pref_policy == KP_PREFERENCE_RESPECT && pc.n_preferred_terms > 0) {
+            if (honor) {
+                err = "a spread with nodeAffinityPolicy Honor on a pod with preferred node affinity";
+                return KP_E_UNSUPPORTED;
+            }
+            for (int i = 0; i < pc.n_preferred_terms; i++)
+                for (int j = 0; j < pc.preferred_terms[i].n_requirements; j++) {
+                    const char* k = pc.preferred_terms[i].requirements[j].key;
+                    if (k && topo_keys.count(normalize(k))) {
+                        err = "a preferred node-affinity term on a topology key";
+                        return KP_E_UNSUPPORTED;
+                    }
+                }
+        }
+        st.push_back(std::move(x));
+    }
+    X.relax_next.assign(C0, -1);
+    for (size_t w = 0; w < st.size(); w++) {
+        const St cur = st[w];
+        const kp_pod_class& pc = in->classes[cur.origin];
+        St nx = cur;
+        bool relaxed = true;
+        if (pc.n_required_terms - cur.req_first > 1) {
+            nx.req_first++;                       // removeRequiredNodeAffinityTerm
+        } else if (!cur.paff.empty()) {
+            nx.paff.erase(nx.paff.begin());       // removePreferredPodAffinityTerm (heaviest)
+        } else if (!cur.panti.empty()) {
+            nx.panti.erase(nx.panti.begin());     // removePreferredPodAntiAffinityTerm (heaviest)
+        } else if (!cur.pnode.empty()) {
+            nx.pnode.erase(nx.pnode.begin());     // removePreferredNodeAffinityTerm (heaviest)
+        } else {
+            relaxed = false;
+            for (size_t i = 0; i < cur.spreads.size() && !relaxed; i++)
+                if (pc.topology[cur.spreads[i]].when_unsatisfiable == KP_SCHEDULE_ANYWAY) {
+                    nx.spreads[i] = nx.spreads.back();  // removeTopologySpreadScheduleAnyway: swap with the last
+                    nx.spreads.pop_back();
+                    relaxed = true;
+                }
+            if (!relaxed && tol_pns && !cur.pns) {
+                bool has = false;  // Toleration.MatchToleration of {Exists, effect PreferNoSchedule}
+                for (int i = 0; i < pc.n_tolerations; i++) {
+                    const kp_toleration& t = pc.tolerations[i];
+                    has |= t.op == KP_TOL_EXISTS && (!t.key || !*t.key) && (!t.value || !*t.value) && t.effect &&
+                           !strcmp(t.effect, "PreferNoSchedule");
+                }
+                if (!has) {
+                    nx.pns = true;                // toleratePreferNoScheduleTaints
+                    relaxed = true;
+                }
+            }
+        }
+        if (!relaxed) continue;
+        nx.cls = C0 + (int)(st.size() - C0);
+        X.relax_next[cur.cls] = nx.cls;
+        X.relax_next.push_back(-1);
+        st.push_back(std::move(nx));
+        any = true;
+    }
+    const int CX = (int)st.size();
+    if (CX + 64 >= 65535) {
+        err = "too many pod classes after preference expansion";
+        return KP_E_UNSUPPORTED;
+    }
+    X.classes.assign(CX, kp_pod_class{});
+    X.reqs.assign(CX, {});
+    X.tols.assign(CX, {});
+    X.terms.assign(CX, {});
+    static const kp_toleration pns_tol = {"", KP_TOL_EXISTS, "", "PreferNoSchedule"};
+    for (const St& x : st) {
+        const kp_pod_class& pc = in->classes[x.origin];
+        kp_pod_class& o = X.classes[x.cls];
+        o = pc;
+        auto& rq = X.reqs[x.cls];
+        rq.assign(pc.requirements, pc.requirements + pc.n_requirements);
+        if (pc.n_required_terms > 0) {
+            const kp_node_selector_term& t = pc.required_terms[x.req_first];
+            rq.insert(rq.end(), t.requirements, t.requirements + t.n_requirements);
+        }
+        if (pref_policy == KP_PREFERENCE_RESPECT && !x.pnode.empty()) {
+            const kp_node_selector_term& t = pc.preferred_terms[x.pnode[0]];
+            rq.insert(rq.end(), t.requirements, t.requirements + t.n_requirements);
+        }
+        auto& tl = X.tols[x.cls];
+        tl.assign(pc.tolerations, pc.tolerations + pc.n_tolerations);
+        if (x.pns) tl.push_back(pns_tol);
+        auto& tm = X.terms[x.cls];
+        auto keep = [&](int i) {
+            const kp_topology_term& t = pc.topology[i];
+            const bool pref = t.type == KP_TOPO_SPREAD ? t.when_unsatisfiable == KP_SCHEDULE_ANYWAY : t.weight > 0;
+            if (!(pref && pref_policy == KP_PREFERENCE_IGNORE)) tm.push_back(t);
+        };
+        for (int i : x.spreads) keep(i);
+        for (int i = 0; i < pc.n_topology; i++)
+            if (pc.topology[i].type != KP_TOPO_SPREAD && pc.topology[i].weight <= 0) keep(i);
+        for (int i : x.paff) keep(i);
+        for (int i : x.panti) keep(i);
+        o.n_required_terms = o.n_preferred_terms = 0;
+        o.required_terms = o.preferred_terms = nullptr;
+    }
+    for (int c = 0; c < CX; c++) {
+        kp_pod_class& o = X.classes[c];
+        o.n_requirements = (int32_t)X.reqs[c].size();
+        o.requirements = X.reqs[c].data();
+        o.n_tolerations = (int32_t)X.tols[c].size();
+        o.tolerations = X.tols[c].data();
+        o.n_topology = (int32_t)X.terms[c].size();
+        o.topology = X.terms[c].data();
+    }
+    if (!any) X.relax_next.clear();
+    X.in = *in;
+    X.in.n_classes = CX;
+    X.in.classes = X.classes.data();
+    return KP_OK;
+}
+
 // One forward group per (class, term) and one inverse group per required anti-affinity term (per-class groups decide
 // exactly like Go's hash-shared ones: groups that share a hash count the same pods).  Interns the topology keys.
 static kp_status topo_build(kp_ctx* c, const kp_solve_input* in, const std::vector<std::map<int, HReq>>& creq,
@@ -936,12 +1123,10 @@ static kp_status topo_build(kp_ctx* c, const kp_solve_input* in, const std::vect
                 err = "bad topology term";
                 return KP_E_INVALID;
             }
+            // preferred terms reach here only under PREFERENCE_POLICY=Respect (expand_preferences drops them under
+            // Ignore): they constrain like required ones until the pod's Relax removes them
             const bool preferred = x.type == KP_TOPO_SPREAD ? x.when_unsatisfiable == KP_SCHEDULE_ANYWAY : x.weight > 0;
-            if (preferred) {
-                if (c->pref_policy == KP_PREFERENCE_IGNORE) continue;  // PREFERENCE_POLICY=Ignore drops preferences
-                err = "preferred topology terms need preference relaxation (PREFERENCE_POLICY=Respect), not supported";
-                return KP_E_UNSUPPORTED;
-            }
+            if (preferred && c->pref_policy == KP_PREFERENCE_IGNORE) continue;
             if (x.type == KP_TOPO_SPREAD && x.max_skew <= 0) {
                 err = "maxSkew must be positive";
                 return KP_E_INVALID;
@@ -953,7 +1138,7 @@ static kp_status topo_build(kp_ctx* c, const kp_solve_input* in, const std::vect
                 }
             const int key = c->sol.key(normalize(x.topology_key));
             for (int inv = 0; inv < 2; inv++) {
-                if (inv && x.type != KP_TOPO_ANTI_AFFINITY) break;
+                if (inv && (x.type != KP_TOPO_ANTI_AFFINITY || preferred)) break;  // inverse: required anti-affinity only
                 HGroup g;
                 g.type = x.type;
                 g.key = key;
@@ -1020,8 +1205,19 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     c->prepared = c->executed = false;
     c->cons_prepared = false;
     c->any_min_values = false;
-    if (in->min_values_policy != KP_MIN_VALUES_STRICT)
-        return fail(ctx, KP_E_UNSUPPORTED, "MIN_VALUES_POLICY=BestEffort is not supported by this build");
+    if (in->min_values_policy != KP_MIN_VALUES_STRICT && in->min_values_policy != KP_MIN_VALUES_BEST_EFFORT)
+        return fail(ctx, KP_E_INVALID, "unknown MIN_VALUES_POLICY");
+    c->best_effort = in->min_values_policy == KP_MIN_VALUES_BEST_EFFORT;
+    if (in->n_classes < 0 || (in->n_classes > 0 && !in->classes)) return fail(ctx, KP_E_INVALID, "pod classes");
+    for (int i = 0; i < in->pods.n_pods; i++)
+        if (in->pods.class_id[i] < 0 || in->pods.class_id[i] >= in->n_classes)
+            return fail(ctx, KP_E_INVALID, "pod class out of range");
+    {
+        std::string perr;
+        kp_status pst = expand_preferences(in, c->pref_policy, c->pref, perr);
+        if (pst != KP_OK) return fail(ctx, pst, perr);
+    }
+    in = &c->pref.in;  // from here on: the expanded classes (stage 0 of input class i is class i)
     const int T = c->T, TW = c->TW, R = c->R, P = in->pods.n_pods, C = in->n_classes;
     // ---- dictionaries: catalog ∪ solve strings ----
     c->sol = c->cat;
@@ -1334,6 +1530,26 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
             fields[(size_t)idx[i] * 4 + 3] = (int64_t)((uint64_t)rank ^ 0x8000000000000000ull);
         }
     }
+    // relaxation stages of every shape: shape_next[s] = the shape of (relax_next[class of s], the same requests)
+    std::vector<int32_t> shape_next;
+    if (!c->pref.relax_next.empty()) {
+        std::vector<const ShapeKey*> by_id(shapes.size());
+        for (auto& kv : shapes) by_id[kv.second] = &kv.first;  // std::map nodes do not move
+        for (size_t sid = 0; sid < by_id.size(); sid++) {
+            const int nx = c->pref.relax_next[by_id[sid]->cls];
+            int id = -1;
+            if (nx >= 0) {
+                ShapeKey sk{nx, by_id[sid]->req};
+                auto it = shapes.find(sk);
+                if (it == shapes.end()) {
+                    it = shapes.emplace(std::move(sk), (int)shapes.size()).first;
+                    by_id.push_back(&it->first);
+                }
+                id = it->second;
+            }
+            shape_next.push_back(id);
+        }
+    }
     KpDev& d = c->dev;
     d = KpDev{};
     d.n_active = 0;
@@ -1394,6 +1610,13 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     HIPCHK(c->d_XT.ensure(extol.size()));
     HIPCHK(c->d_pod_cls.upload(pcls, s));
     HIPCHK(c->d_pod_shape.upload(pshape, s));
+    if (!shape_next.empty()) {
+        HIPCHK(c->d_pod_cls0.upload(pcls, s));
+        HIPCHK(c->d_pod_shape0.upload(pshape, s));
+        HIPCHK(c->d_relax_next.upload(c->pref.relax_next, s));
+        HIPCHK(c->d_shape_next.upload(shape_next, s));
+        HIPCHK(c->d_last_ep.ensure(std::max(P, 1)));
+    }
     HIPCHK(c->d_pod_req.upload(preq, s));
     HIPCHK(c->d_sort_fields.upload(fields, s));
     HIPCHK(c->d_empty_hdr.upload(empty_hdr, s));
@@ -1609,6 +1832,13 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.P = P;
     d.pod_cls = c->d_pod_cls.p;
     d.pod_shape = c->d_pod_shape.p;
+    const bool relax = !c->pref.relax_next.empty();
+    d.relax_next = relax ? c->d_relax_next.p : nullptr;
+    d.shape_next = relax ? c->d_shape_next.p : nullptr;
+    d.pod_cls0 = relax ? c->d_pod_cls0.p : nullptr;
+    d.pod_shape0 = relax ? c->d_pod_shape0.p : nullptr;
+    d.last_ep = relax ? c->d_last_ep.p : nullptr;
+    d.best_effort = c->best_effort ? 1 : 0;
     d.pod_req = c->d_pod_req.p;
     d.queue0 = nullptr;  // set by execute (sort output)
     d.NCcap = NCcap;
@@ -1944,6 +2174,9 @@ static kp_status cons_prepare_one(kp_ctx* ctx, const kp_consolidate_input* in) t
     kp_status st = kp_solve_prepare(ctx, &cl);
     if (st != KP_OK) return st;
     kp_ctx* c = ctx;
+    if (!c->pref.relax_next.empty())
+        return fail(ctx, KP_E_UNSUPPORTED, "consolidation over pods with preferences to relax is not supported by this build");
+    if (c->best_effort) return fail(ctx, KP_E_UNSUPPORTED, "consolidation with MIN_VALUES_POLICY=BestEffort is not supported by this build");
     const KpDev& d = c->dev;
     if (c->any_min_values) return fail(ctx, KP_E_UNSUPPORTED, "consolidation with minValues NodePools is not supported by this build");
     if (c->cons_mayfix)

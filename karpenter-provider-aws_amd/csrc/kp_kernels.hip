@@ -178,6 +178,8 @@ struct FfdShared {
                                    // (topology counts): the next pod of the shape rescans from the start
     int rel_flag;                  // a reservation ID's capacity came back from 0 (commit_reservations): the
                                    // reservation-dependent rejections memoised so far may no longer hold
+    int epoch;                     // lastLen generation: Queue.Push(pod, relaxed = true) clears lastLen
+    int relaxed;                   // a pod relaxed since wave 0 last loaded its queue window (its lastLens are stale)
     int xstart;                    // every existing node < xstart has rejected the current shape
     uint32_t cur_tol;              // tolerations word of the current shape's class (bit 31: no requirement keys)
     int32_t cur_pq[KP_LDS_AXES];   // scaled quick-accept requests of the current shape
@@ -490,6 +492,12 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
         d.pod_result[p] = -1;
         d.pod_order[p] = -1;
     }
+    if (d.relax_next)  // a previous execute may have relaxed pods: every pod starts from its input class
+        for (int p = tid; p < P; p += nthr) {
+            d.pod_cls[p] = d.pod_cls0[p];
+            d.pod_shape[p] = d.pod_shape0[p];
+            d.last_ep[p] = -1;
+        }
     if (tid == 0) {
         S.N = 0;
         S.tp_n = 0;
@@ -505,6 +513,8 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
         S.any_rej = 0;
         S.rej_volatile = 0;
         S.rel_flag = 0;
+        S.epoch = 0;
+        S.relaxed = 0;
         S.xstart = 0;
         S.seq = 0;
         S.err = 0;
@@ -565,6 +575,12 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
             int seq = S.seq, prev_shape = S.prev_shape, dkind = S.dirty_kind, dpos = S.dirty_pos;
             int sstart = S.scan_start;  // every slice position < sstart has rejected the current shape
             int any_rej = S.any_rej;
+            const int ep = S.epoch;
+            if (d.relax_next && S.relaxed) {
+                vlast = -1;  // Queue.Push(pod, relaxed): every lastLen read into the window is gone
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                if (lane == 0) S.relaxed = 0;
+            }
             if (RESV && S.rel_flag) {
                 // a reservation capacity came back from 0: forget the shape's memoised rejections (a reservation-
                 // dependent one may now succeed; the others are re-derived on the next scan)
@@ -673,7 +689,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                         vp = d.qbuf[pos];
                         vc = d.pod_cls[vp];
                         vshape = d.pod_shape[vp];
-                        vlast = d.last_len[vp];
+                        vlast = (d.last_ep && d.last_ep[vp] != ep) ? -1 : d.last_len[vp];
                         vtol = (d.tol[vc] & 0x7FFFFFFFu) | ((d.cls_flags[vc] & 4u) ? 0x80000000u : 0u);
                         for (int r = 0; r < R; r++) S.qw_req[lane][r] = d.pod_req[(size_t)vp * R + r];
 #pragma unroll
@@ -1234,6 +1250,10 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                     commit_reqs(d, S.CC, S.ws[win], nc, lane);
                     if (RESV && d.resv_on && lane == 0) commit_reservations(d, sRcap, S.ws[win], nc, ld_u64(&d.nc_held[nc]), &S.rel_flag);
                 }
+                if (d.best_effort) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // commit_reqs' header rows have landed
+                    commit_min_relax(d, S.ws[win], nc, lane);
+                }
                 if (TOPO_ON && (S.CC.flags & CF_TOPO))
                     topo_record(d, S.CC, S.ws[win], d.nc_hdr + (size_t)nc * K, d.nc_words + (size_t)nc * d.DW,
                                 d.E + nc, d.nc_tmpl[nc], true, lane);
@@ -1327,6 +1347,10 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                             d.nc_words[(size_t)n * d.DW + i] = d.cls_words[(size_t)(d.C + jj) * d.DW + i];
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         commit_reqs(d, S.CC, S.ws[wave], n, lane);
+                        if (d.best_effort) {
+                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the header rows above have landed
+                            commit_min_relax(d, S.ws[wave], n, lane);
+                        }
                         if (RESV && d.resv_on && lane == 0) commit_reservations(d, sRcap, S.ws[wave], n, 0ull, &S.rel_flag);
                         if (TOPO_ON && (S.CC.flags & CF_TOPO))
                             topo_record(d, S.CC, S.ws[wave], d.cls_hdr + (size_t)(d.C + jj) * K,
@@ -1370,11 +1394,22 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
             }
             if (tid == 0) {
                 if (d.profile) S.st[ST_CYC_TMPL] += __builtin_amdgcn_s_memtime() - c_t;
-                if (twin < 0) {  // Queue.Push(pod, relaxed=false)
+                if (twin < 0) {  // preferences.Relax, then Queue.Push(pod, relaxed)
                     const int tail = (S.qhead + S.qcount) % P;
                     d.qbuf[tail] = pod;
                     S.qcount++;
-                    d.last_len[pod] = S.qcount;
+                    const int nx = d.relax_next ? d.relax_next[S.cur_cls] : -1;
+                    if (nx >= 0) {
+                        // the pod takes its class's next relaxation stage (Topology.Update / updateCachedPodData) and
+                        // lastLen is cleared: a new epoch
+                        d.pod_cls[pod] = nx;
+                        d.pod_shape[pod] = d.shape_next[S.prev_shape];
+                        S.epoch++;
+                        S.relaxed = 1;
+                    } else {
+                        d.last_len[pod] = S.qcount;
+                        if (d.last_ep) d.last_ep[pod] = S.epoch;
+                    }
                 }
             }
         }

@@ -140,8 +140,15 @@ struct KpDev {
 
     // ---------------- pods ----------------
     int32_t P;
-    const int32_t* pod_cls;          // [P]
-    const int32_t* pod_shape;        // [P] id of (class, requests)
+    int32_t* pod_cls;                // [P] (rewritten by the FFD kernel when a pod relaxes)
+    int32_t* pod_shape;              // [P] id of (class, requests)
+    // preference relaxation (kp_host.cpp expand_preferences); relax_next == nullptr: no class can relax
+    const int32_t* relax_next;       // [C] the class after one preferences.Relax step, -1 when none is left
+    const int32_t* shape_next;       // [shapes] the shape of (relax_next[class], same requests)
+    const int32_t* pod_cls0;         // [P] input classes / shapes, restored into pod_cls / pod_shape per execute
+    const int32_t* pod_shape0;
+    int32_t* last_ep;                // [P] epoch of last_len (Queue.Push(pod, relaxed) clears lastLen: a new epoch)
+    int32_t best_effort;             // MIN_VALUES_POLICY=BestEffort: unmet minValues relax instead of failing
     const int64_t* pod_req;          // [P][R]
     const int32_t* queue0;           // [P] queue order (NewQueue sort), device-sorted
     int32_t active_axes[KP_MAX_R];   // axes any pod/daemon requests, LDS-staged first

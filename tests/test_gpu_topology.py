@@ -82,7 +82,8 @@ def test_zonal_anti_affinity_and_foreign_selector(ctx, golden):
 
 
 def test_preference_policy_ignore(golden):
-    """PREFERENCE_POLICY=Ignore (kp_device_opts.preference_policy) drops ScheduleAnyway spreads; Respect is rejected."""
+    """PREFERENCE_POLICY=Ignore (kp_device_opts.preference_policy) drops ScheduleAnyway spreads; Respect honours them
+    until relaxed (one pod per NodeClaim here), both bit-exact with the oracle."""
     from kpsim import native
     lab = {"app": "p"}
     pc, pods = TC.deployment(6, lab, [model.TopologyTerm("spread", model.HOSTNAME, TC.sel(lab),
@@ -97,9 +98,10 @@ def test_preference_policy_ignore(golden):
         c.close()
     r = native.Context(0)
     try:
-        with pytest.raises(native.KpError) as e:
-            parity.run_device(r, prob)
-        assert e.value.status == abi.KP_E_UNSUPPORTED
+        dev = parity.run_device(r, prob)
+        o = __import__("pyoracle").solve(prob)
+        np.testing.assert_array_equal(dev[0].pod_result, o.results.pod_result)
+        assert dev[0].n_nodeclaims == 6
     finally:
         r.close()
 
