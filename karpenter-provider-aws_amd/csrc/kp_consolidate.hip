@@ -87,6 +87,47 @@ __device__ inline double worst_launch_price(const KpDev& d, const KpCons& k, int
     return mx;
 }
 
+// minValues over an ordered option list held one type per lane (lane i = the i-th cheapest, lanes in `m` kept):
+// the distinct values of single-valued catalog key k (a type without the label contributes none, like
+// Requirements.Get(k).Values()).  Returns the lanes holding a first occurrence, in lane order.
+__device__ inline uint64_t first_values(const KpDev& d, int k, int my_t, uint64_t m, int lane) {
+    const int kc = d.kcat[k];
+    int v = -1;
+    if (((m >> lane) & 1ull) && kc >= 0 && my_t >= 0) {
+        const uint16_t x = d.type_val[(size_t)kc * d.T + my_t];
+        if (x < VAL_ABSENT) v = x;
+    }
+    bool first = v >= 0;
+    for (int j = 0; j < 63; j++) {
+        const int vj = __shfl(v, j);
+        if (j < lane && vj == v) first = false;
+    }
+    return ballot(first);
+}
+
+// InstanceTypes.SatisfiesMinValues over the kept lanes m of NodeClaim template j's minValues keys (header nch):
+// *need = minNeededInstanceTypes, the shortest kept prefix that satisfies every key.
+__device__ inline bool min_values_ok(const KpDev& d, const ReqHdr* nch, int j, int my_t, uint64_t m, int lane, int* need) {
+    const int* mk = d.min_keys + (size_t)j * KP_MAX_CLASS_KEYS;
+    int nd = 0;
+    for (int q = 0; q < KP_MAX_CLASS_KEYS; q++) {
+        const int k = mk[q];
+        if (k < 0) break;
+        const ReqHdr h = nch[k];
+        if (!(h.flags & RF_MIN) || h.minv <= 0) continue;
+        const uint64_t f = first_values(d, k, my_t, m, lane);
+        if (__popcll(f) < h.minv) return false;
+        // the kept lane at which the count reaches minv, as a position in the kept list
+        uint64_t x = f;
+        for (int i = 1; i < h.minv; i++) x &= x - 1;
+        const int L = __ffsll((unsigned long long)x) - 1;
+        const int pos = __popcll(m & ((L >= 63) ? ~0ull : ((2ull << L) - 1)));
+        nd = pos > nd ? pos : nd;
+    }
+    if (need) *need = nd;
+    return true;
+}
+
 }  // namespace
 
 // FULL = false: the fast variant handles probes whose pods all fit existing nodes (no NodeClaim code, a small register
@@ -130,7 +171,12 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
     Ev.slot_ct = d.slot_ct;
     Ev.slot_zoneid = d.slot_zoneid;
     Ev.roles = &S.roles;
-    Ev.min_tmpl_mask = 0;  // minValues templates are rejected by kp_consolidate
+    {
+        uint32_t mmask = 0;  // templates whose requirements carry minValues (single-valued keys, kp_consolidate_prepare)
+        for (int j = 0; j < d.NT; j++)
+            if (d.min_keys[(size_t)j * KP_MAX_CLASS_KEYS] >= 0) mmask |= 1u << j;
+        Ev.min_tmpl_mask = mmask;
+    }
     Ev.ro = nullptr;       // catalogs with reserved offerings are rejected by kp_consolidate
     Ev.type_ro = nullptr;
     Ev.rcap = nullptr;
@@ -278,7 +324,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     vq[ai] = ai < A ? d.pod_req[(size_t)p * R + d.active_axes[ai]] : 0;
             }
         };
-        int n_nc = 0, nc_tmpl = -1, prev_shape = -1, xstart = 0, ok_np = 0;
+        int n_nc = 0, nc_tmpl = -1, prev_shape = -1, xstart = 0, ok_np = 0, nc_nonpend = 0;
         bool aborted = false;
         int cbase = -1, ccls = -1;  // cached node chunk (wave-uniform)
         uint64_t cx = 0;
@@ -497,7 +543,10 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             if (prof) cy_nc += __builtin_amdgcn_s_memtime() - cn0;
             if (stop) break;
             if (placed) {
-                if (!pend) ok_np++;
+                if (!pend) {
+                    ok_np++;
+                    nc_nonpend++;
+                }
                 continue;
             }
             // Queue.Push(pod, relaxed=false): lastLen = len after the append
@@ -528,6 +577,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
         const long long cd0 = prof ? __builtin_amdgcn_s_memtime() : 0;
         int decision = KP_DECISION_NONE, valid = 0, nrep = 0;
         double rprice = 0.0;
+        bool truncated_out = false;  // the NodeClaim failed TruncateInstanceTypes' minValues check
         const bool all = !stop && !bad && ok_np == n_np;
         if (all && n_nc == 0) {
             decision = KP_DECISION_DELETE;
@@ -582,6 +632,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 }
             }
             const int nsel = n_opt < d.M ? n_opt : d.M;
+            const bool has_min = (Ev.min_tmpl_mask >> nc_tmpl) & 1u;
             int my_t = -1;
             for (int i = 0; i < nsel; i++) {
                 double bp = DBL_MAX;
@@ -612,6 +663,10 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 if (lane == i) my_t = gw * 64 + gl;
                 if (lane == gl) present &= ~(1u << gw);
             }
+            // Results.TruncateInstanceTypes: a NodeClaim whose first M options miss its minValues is dropped and its pods
+            // get errors (not every non-pending pod scheduled; no valid new NodeClaim)
+            const uint64_t msel = nsel >= 64 ? ~0ull : ((1ull << nsel) - 1);
+            const bool trunc_ok = !has_min || min_values_ok(d, nch, nc_tmpl, my_t, msel, lane, nullptr);
             // capacity-type requirement of the NodeClaim: Has(spot) / Has(on-demand)
             auto ct_has = [&](int vid) -> bool {
                 const int kk = d.key_ct;
@@ -624,26 +679,40 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             const bool has_spot = ct_has(k.v_spot), has_od = ct_has(k.v_od);
             const uint64_t mt = my_t >= 0 ? d.avail_zc[my_t] & mzc : 0;
             bool keep = false, none = false, spot_only = false;
-            if (all_spot && has_spot) {  // computeSpotToSpotConsolidation
+            if (!trunc_ok) {
+                // the dropped NodeClaim's pods get errors: if one of them is not pending, not all non-pending pods
+                // scheduled (NONE); otherwise no new NodeClaim is left and the candidates' pods all landed: DELETE
+                none = true;
+                truncated_out = true;
+            } else if (all_spot && has_spot) {  // computeSpotToSpotConsolidation
                 if (!k.spot_to_spot) {
                     none = true;
                 } else {
                     spot_only = true;  // Requirements.Add(capacity-type In [spot])
                     keep = my_t >= 0 && worst_launch_price(d, k, my_t, mt & k.spot_slots) < cprice;
                     const uint64_t km = ballot(keep);
-                    if (!km) {
+                    int need = 0;
+                    if (has_min && !min_values_ok(d, nch, nc_tmpl, my_t, km, lane, &need)) {
+                        none = true;  // RemoveInstanceTypeOptionsByPriceAndMinValues keeps minValues
+                    } else if (!km) {
                         none = true;
                     } else if (c1 - c0 == 1) {
-                        if (__popcll(km) < 15) none = true;  // MinInstanceTypesForSpotToSpotConsolidation
-                        else keep = keep && __popcll(km & ((1ull << lane) - 1)) < 15;
+                        // MinInstanceTypesForSpotToSpotConsolidation; the kept list is cut to max(15, minNeeded)
+                        const int cut = has_min && need > 15 ? need : 15;
+                        if (__popcll(km) < 15) none = true;
+                        else keep = keep && __popcll(km & ((1ull << lane) - 1)) < cut;
                     }
                 }
             } else {  // RemoveInstanceTypeOptionsByPriceAndMinValues
                 keep = my_t >= 0 && worst_launch_price(d, k, my_t, mt) < cprice;
-                if (!ballot(keep)) none = true;
+                const uint64_t km = ballot(keep);
+                if (!km || (has_min && !min_values_ok(d, nch, nc_tmpl, my_t, km, lane, nullptr))) none = true;
                 spot_only = has_spot && has_od;  // spot/on-demand flexible replacement narrowed to spot
             }
-            if (!none) {
+            if (truncated_out && nc_nonpend == 0) {
+                decision = KP_DECISION_DELETE;
+                valid = 1;
+            } else if (!none) {
                 decision = KP_DECISION_REPLACE;
                 const uint64_t mr = spot_only ? (mt & k.spot_slots) : mt;
                 const double wl = keep ? worst_launch_price(d, k, my_t, mr) : DBL_MAX;
@@ -666,8 +735,8 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             kp_probe_result o;
             o.decision = decision;
             o.valid = valid;
-            o.all_scheduled = all ? 1 : 0;
-            o.n_new_nodeclaims = stop ? 2 : n_nc;
+            o.all_scheduled = (all && !(truncated_out && nc_nonpend > 0)) ? 1 : 0;
+            o.n_new_nodeclaims = stop ? 2 : (truncated_out ? 0 : n_nc);
             o.n_replacement_types = nrep;
             o.n_pods = n;
             o.candidate_price = cprice;
@@ -681,7 +750,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             S.st[CS_PROBES] += 1;
             S.st[CS_BITMAP_WORDS] += st_words;
             S.st[CS_PLACED_EXISTING] += st_placed;
-            S.st[CS_NEW_NC] += stop ? 2 : n_nc;
+            S.st[CS_NEW_NC] += o.n_new_nodeclaims;
             S.st[CS_CHUNK_LOADS] += st_loads;
             S.st[CS_CACHE_HITS] += st_hits;
             if (prof) {

@@ -261,6 +261,7 @@ struct kp_ctx {
     double kernel_ms[5] = {};
     int64_t cycles[33] = {};  // FFD phases (s_memtime): pop, sort, scan+eval, templates, commit, full pdqsort
     bool any_min_values = false;             // some template requirement carries minValues
+    bool min_multi = false;                  // ... on a multi-valued catalog key (zone, capacity type, ...)
     bool cons_mayfix = false;                // a pod's NotIn/DoesNotExist merge can change a later Compatible
     // consolidation probes
     DBuf<int32_t> d_retry, d_rank, d_cand_i, d_cand_off, d_cand_pods, d_pending, d_ring, d_ring_last, d_next;
@@ -1205,6 +1206,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     c->prepared = c->executed = false;
     c->cons_prepared = false;
     c->any_min_values = false;
+    c->min_multi = false;
     if (in->min_values_policy != KP_MIN_VALUES_STRICT && in->min_values_policy != KP_MIN_VALUES_BEST_EFFORT)
         return fail(ctx, KP_E_INVALID, "unknown MIN_VALUES_POLICY");
     c->best_effort = in->min_values_policy == KP_MIN_VALUES_BEST_EFFORT;
@@ -1407,6 +1409,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
             if (kv.second.has_min) {
                 min_keys[(size_t)j * KP_MAX_CLASS_KEYS + q++] = kv.first;
                 c->any_min_values = true;
+                if (kv.first < c->Kcat && (c->cat_kflags[kv.first] & KF_CAT_MULTI)) c->min_multi = true;
             }
     }
     // ---- templates: taints, daemon overhead, limits, instance-type rows ----
@@ -2178,7 +2181,9 @@ static kp_status cons_prepare_one(kp_ctx* ctx, const kp_consolidate_input* in) t
         return fail(ctx, KP_E_UNSUPPORTED, "consolidation over pods with preferences to relax is not supported by this build");
     if (c->best_effort) return fail(ctx, KP_E_UNSUPPORTED, "consolidation with MIN_VALUES_POLICY=BestEffort is not supported by this build");
     const KpDev& d = c->dev;
-    if (c->any_min_values) return fail(ctx, KP_E_UNSUPPORTED, "consolidation with minValues NodePools is not supported by this build");
+    // minValues NodePools: the probe kernel counts distinct values of single-valued catalog keys only
+    if (c->min_multi)
+        return fail(ctx, KP_E_UNSUPPORTED, "consolidation with minValues on a multi-valued label is not supported by this build");
     if (c->cons_mayfix)
         return fail(ctx, KP_E_UNSUPPORTED, "consolidation with NotIn/DoesNotExist pod requirements on keys some node lacks "
                                            "and other pods select positively is not supported by this build");

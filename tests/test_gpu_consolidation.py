@@ -50,6 +50,25 @@ def test_fuzz_consolidation(ctx, golden, seed):
         assert_probes_equal(device_probes(ctx, cp, mode, s2s), pyoracle.consolidate(cp, mode, spot_to_spot=s2s))
 
 
+@pytest.mark.parametrize("seed", range(16))
+def test_fuzz_consolidation_min_values(ctx, golden, seed):
+    """NodePools with minValues on instance-family: the probes' NodeClaim.Add minValues filter, TruncateInstanceTypes'
+    minValues check (a dropped NodeClaim: NONE, or DELETE when only pending pods rode on it) and
+    RemoveInstanceTypeOptionsByPriceAndMinValues / the spot-to-spot max(15, minNeeded) cut, against the oracle."""
+    rng = np.random.Generator(np.random.PCG64(900 + seed))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 300)), replace=False))]
+    cp = fuzzgen.fuzz_consolidation(sub, 900 + seed, n_nodes=int(rng.integers(4, 80)),
+                                    n_pods=int(rng.integers(20, 300)), all_spot=seed % 3 == 0, supported=True,
+                                    with_min=True)
+    for np_ in cp.cluster.nodepools:  # minValues on every pool, sometimes beyond what a truncated list can hold
+        if not any(r.min_values for r in np_.requirements):
+            np_.requirements.append(model.Requirement("karpenter.k8s.aws/instance-family", "Exists", [],
+                                                      int(rng.choice([1, 2, 5, 20, 40]))))
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        s2s = seed % 2 == 0
+        assert_probes_equal(device_probes(ctx, cp, mode, s2s), pyoracle.consolidate(cp, mode, spot_to_spot=s2s))
+
+
 def test_shard_ranges_concatenate(ctx, golden):
     cp = fuzzgen.fuzz_consolidation(golden[:200], 77, n_nodes=60, n_pods=250, n_candidates=40, supported=True)
     for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
