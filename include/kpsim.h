@@ -453,6 +453,24 @@ kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_request* requ
 kp_status kp_launch_stats(kp_ctx* ctx, double* ms, int32_t n);
 
 /*
+ * NodeClaim write-back for a launched instance — replaces CloudProvider.instanceToNodeClaim's label and status-resource
+ * rules (pkg/cloudprovider/cloudprovider.go:381-444) for an instance of catalog row type_index launched through offering
+ * row `offering` (CreateFleet's pick among kp_launch_select's overrides: the instance's zone, capacity type and
+ * capacity reservation):
+ *   labels: every single-valued requirement of the instance type (Requirement.Len() == 1) except the
+ *           capacity-reservation id / type keys; topology.kubernetes.io/zone; topology.k8s.aws/zone-id (zone_id, the
+ *           EC2NodeClass subnet's ZoneID, or when NULL the offering's own zone-id); karpenter.sh/capacity-type; for a
+ *           reserved instance its reservation id and type; karpenter.sh/nodepool (nodepool, the instance tag, if given).
+ *           Written as "key 	 value 
+" lines sorted by key (*needed = bytes incl. NUL).
+ *   capacity / allocatable [R] (optional): InstanceType.Capacity / Allocatable() with zero quantities dropped (0) and
+ *           vpc.amazonaws.com/efa kept only when efa_enabled (the launch asked for EFA interfaces).
+ */
+kp_status kp_nodeclaim_labels(kp_ctx* ctx, int32_t type_index, int32_t offering, const char* zone_id,
+                              const char* nodepool, int32_t efa_enabled, char* buf, int64_t cap, int64_t* needed,
+                              int64_t* capacity, int64_t* allocatable);
+
+/*
  * Requirements of NodeClaim `nc` from the last kp_solve on this ctx (hostname removed as in
  * FinalizeScheduling), one line per key, lines sorted:
  *   "key \t complement(0|1) \t gt|- \t lt|- \t minValues|- \t v1 \x1f v2 ..."   (values sorted)

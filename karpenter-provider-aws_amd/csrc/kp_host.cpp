@@ -297,6 +297,7 @@ struct kp_ctx {
     DBuf<double> d_ro_price;
     DBuf<int32_t> d_trace;                   // KPSIM_TRACE_POD diagnostics
     std::string launch_err;
+    std::vector<std::vector<std::pair<int, int>>> type_single;  // [T] (catalog key, value id) with Len() == 1
     std::vector<int32_t> l_off_begin, l_off_val, l_ct, l_rt, l_rcap;
     std::vector<double> l_price;
     std::vector<uint8_t> l_avail, l_exotic;
@@ -490,6 +491,11 @@ static kp_status catalog_upload_one(kp_ctx* ctx, const kp_catalog_view* v, uint6
             if (ids.size() > 1) multi[key] = 1;
         }
     }
+    // single-valued requirements of each type (Requirement.Len() == 1): instanceToNodeClaim's labels
+    c->type_single.assign(T, {});
+    for (int t = 0; t < T; t++)
+        for (int key = 0; key < Kc; key++)
+            if (tv[(size_t)t * Kc + key].size() == 1) c->type_single[t].push_back({key, tv[(size_t)t * Kc + key][0]});
     // offering-role keys are multi-valued on the type side in AWS (zone, capacity-type, ...): treat every key
     // that appears in offerings as multi so their value masks exist
     for (int k = 0; k < v->n_offering_keys; k++) multi[ok[k]] = 1;
@@ -2868,6 +2874,60 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
     }
     c->launch_ms[1] = ns_since(t0) / 1e6;
     if (short_buf) return fail(c, KP_E_BUFFER, "type_ids / override_offerings too small");
+    return KP_OK;
+} catch (const std::exception& e) {
+    return fail(ctx, KP_E_INVALID, e.what());
+}
+
+// instanceToNodeClaim (pkg/cloudprovider/cloudprovider.go:381-444) for an instance launched from catalog row
+// type_index through offering row `offering` (its zone, capacity type and reservation are the instance's).
+extern "C" kp_status kp_nodeclaim_labels(kp_ctx* ctx, int32_t type_index, int32_t offering, const char* zone_id,
+                                         const char* nodepool, int32_t efa_enabled, char* buf, int64_t cap,
+                                         int64_t* needed, int64_t* capacity, int64_t* allocatable) try {
+    if (!ctx) return KP_E_INVALID;
+    if (!ctx->have_catalog) return fail(ctx, KP_E_STATE, "kp_nodeclaim_labels before kp_catalog_upload");
+    kp_ctx* c = ctx;
+    const int T = c->T, O = (int)c->l_ct.size(), R = c->R;
+    if (type_index < 0 || type_index >= T) return fail(c, KP_E_INVALID, "type_index out of range");
+    if (offering < 0 || offering >= O) return fail(c, KP_E_INVALID, "offering out of range");
+    if (c->off_type[offering] != type_index) return fail(c, KP_E_INVALID, "offering is not an offering of type_index");
+    std::map<std::string, std::string> labels;
+    // labels of the type's single-valued requirements, except the reservation keys (present for every capacity type)
+    for (const auto& kv : c->type_single[type_index]) {
+        if (kv.first == c->key_resvid || kv.first == c->key_resvtype) continue;
+        const KeyDict& kd = c->cat.keys[kv.first];
+        labels[kd.name] = kd.vals[kv.second];
+    }
+    auto role_val = [&](int role, int key) -> const std::string* {
+        const int v = c->l_off_val[(size_t)role * O + offering];
+        if (key < 0 || v < 0 || v >= (int)c->cat.keys[key].vals.size()) return nullptr;
+        return &c->cat.keys[key].vals[v];
+    };
+    if (const std::string* z = role_val(KL_ROLE_ZONE, c->key_zone)) labels["topology.kubernetes.io/zone"] = *z;
+    // zone-id: the EC2NodeClass subnet of the zone (the caller's), else the offering's own zone-id requirement
+    if (zone_id && *zone_id) labels["topology.k8s.aws/zone-id"] = zone_id;
+    else if (const std::string* zi = role_val(KL_ROLE_ZONEID, c->key_zoneid)) labels["topology.k8s.aws/zone-id"] = *zi;
+    const int ct = c->l_ct[offering];
+    labels["karpenter.sh/capacity-type"] = ct == KP_CT_SPOT ? "spot" : ct == KP_CT_RESERVED ? "reserved" : "on-demand";
+    if (ct == KP_CT_RESERVED) {
+        if (const std::string* r = role_val(KL_ROLE_RESVID, c->key_resvid)) labels["karpenter.k8s.aws/capacity-reservation-id"] = *r;
+        if (const std::string* r = role_val(KL_ROLE_RESVTYPE, c->key_resvtype))
+            labels["karpenter.k8s.aws/capacity-reservation-type"] = *r;
+    }
+    if (nodepool && *nodepool) labels["karpenter.sh/nodepool"] = nodepool;  // the instance's NodePool tag
+    std::string out;
+    for (auto& kv : labels) out += kv.first + "\t" + kv.second + "\n";
+    if (needed) *needed = (int64_t)out.size() + 1;
+    // Status.Capacity / Allocatable: non-zero quantities; EFA only when the launch requested EFA interfaces
+    for (int r = 0; r < R; r++) {
+        const bool efa = c->resource_names[r] == "vpc.amazonaws.com/efa";
+        const int64_t cv = c->cap_rt[(size_t)r * T + type_index], av = c->alloc_rt[(size_t)r * T + type_index];
+        const bool keep_c = cv != 0 && (!efa || efa_enabled), keep_a = av != 0 && (!efa || efa_enabled);
+        if (capacity) capacity[r] = keep_c ? cv : 0;
+        if (allocatable) allocatable[r] = keep_a ? av : 0;
+    }
+    if (!buf || cap < (int64_t)out.size() + 1) return fail(c, KP_E_BUFFER, "label buffer too small");
+    memcpy(buf, out.c_str(), out.size() + 1);
     return KP_OK;
 } catch (const std::exception& e) {
     return fail(ctx, KP_E_INVALID, e.what());

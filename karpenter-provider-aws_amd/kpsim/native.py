@@ -12,6 +12,7 @@ EXPORTS = [
     "kp_catalog_patch_price", "kp_solve", "kp_solve_prepare", "kp_solve_execute", "kp_solve_fetch",
     "kp_result_nodeclaim_requirements", "kp_last_kernel_times", "kp_consolidate_probe_count", "kp_consolidate",
     "kp_consolidate_stats", "kp_consolidate_prepare", "kp_consolidate_execute", "kp_launch_select", "kp_launch_stats",
+    "kp_nodeclaim_labels",
 ]
 
 _lib = None
@@ -57,6 +58,8 @@ def load():
                                    C.POINTER(abi.kp_launch_result), C.POINTER(C.c_int32), C.c_int32,
                                    C.POINTER(C.c_int32), C.c_int32]
     L.kp_launch_stats.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_int32]
+    L.kp_nodeclaim_labels.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_char_p, C.c_char_p, C.c_int32, C.c_char_p,
+                                      C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     for f in EXPORTS:
         if f not in ("kp_last_error", "kp_version"):
             getattr(L, f).restype = C.c_int32
@@ -111,6 +114,22 @@ class Context:
         st, res = model.launch_call(lambda *a: self.L.kp_launch_select(self.h, *a), self._catalog, batch, M)
         self.check(st, "kp_launch_select")
         return res
+
+    def nodeclaim_labels(self, type_index, offering, zone_id=None, nodepool=None, efa_enabled=False):
+        """kp_nodeclaim_labels (instanceToNodeClaim, cloudprovider.go:381-444) → (labels dict, capacity[R],
+        allocatable[R]) for an instance of catalog row type_index launched through offering row `offering`."""
+        import numpy as np
+        from kpsim import model
+        need = C.c_int64(0)
+        buf = C.create_string_buffer(1 << 14)
+        cap = np.zeros(model.R, np.int64)
+        alloc = np.zeros(model.R, np.int64)
+        self.check(self.L.kp_nodeclaim_labels(self.h, type_index, offering, zone_id.encode() if zone_id else None,
+                                              nodepool.encode() if nodepool else None, 1 if efa_enabled else 0, buf,
+                                              len(buf), C.byref(need), cap.ctypes.data_as(C.POINTER(C.c_int64)),
+                                              alloc.ctypes.data_as(C.POINTER(C.c_int64))), "kp_nodeclaim_labels")
+        labels = dict(line.split("\t", 1) for line in buf.value.decode().splitlines() if line)
+        return labels, cap, alloc
 
     def launch_stats(self):
         ms = (C.c_double * 2)()

@@ -232,6 +232,17 @@ int worker(const Catalog& cat, const Problem& pb, int id, int iters, std::vector
         if (it == 0) *sig = so.pres;
         else CHECK(*sig == so.pres);
     }
+    // instanceToNodeClaim write-back: offering row 1 of type 0 is (zone-a, spot)
+    char lab[4096];
+    int64_t need = 0, capv[3], allocv[3];
+    CHECK(kp_nodeclaim_labels(ctx, 0, 1, nullptr, "default", 0, lab, sizeof lab, &need, capv, allocv) == KP_OK);
+    const std::string ls(lab);
+    CHECK(ls.find("karpenter.sh/capacity-type\tspot\n") != std::string::npos);
+    CHECK(ls.find("topology.kubernetes.io/zone\tzone-a\n") != std::string::npos);
+    CHECK(ls.find("node.kubernetes.io/instance-type\tm9.1xlarge\n") != std::string::npos);
+    CHECK(ls.find("karpenter.sh/nodepool\tdefault\n") != std::string::npos);
+    CHECK(capv[0] == 1000 && allocv[0] == 920);
+    CHECK(kp_nodeclaim_labels(ctx, 1, 1, nullptr, nullptr, 0, lab, sizeof lab, &need, nullptr, nullptr) == KP_E_INVALID);
     CHECK(kp_ctx_destroy(ctx) == KP_OK);
     return 0;
 }
