@@ -187,11 +187,13 @@ def launch_leg(a, golden, local, rank, world, dist, barrier):
     barrier()
     kms, cms = [], []
     t0 = time.perf_counter()
+    phases = []
     for _ in range(a.steps):
         res = ctx.launch_select(batch, 60)
-        k, c = ctx.launch_stats()
-        kms.append(k)
-        cms.append(c)
+        st6 = ctx.launch_stats(6)
+        kms.append(st6[0])
+        cms.append(st6[1])
+        phases.append(st6[2:])
     elapsed = time.perf_counter() - t0
     barrier()
     kern = float(np.mean(kms))
@@ -212,6 +214,8 @@ def launch_leg(a, golden, local, rank, world, dist, barrier):
         "steps": a.steps,
         "kernel_ms": kern,
         "call_ms": float(np.mean(cms)),
+        "call_phases_ms": dict(zip(["encode", "merge_upload", "kernel_download", "expand"],
+                                   [float(x) for x in np.mean(phases, axis=0)])),
         "call_rate_pcie_inclusive": a.launch_batch * a.steps / elapsed,
         "scaling": "strong",
         "config": {"workload": "config5 launch batch: %d NodeClaims x %d types (%d reserved offerings)" % (

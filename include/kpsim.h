@@ -449,7 +449,8 @@ typedef struct kp_launch_result {
 kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_request* requests, int32_t max_instance_types,
                            kp_launch_result* results, int32_t* type_ids, int32_t cap_type_ids,
                            int32_t* override_offerings, int32_t cap_overrides);
-/* ms[0] = launch kernel (HIP events on the ctx stream), ms[1] = whole kp_launch_select call, of the last call. */
+/* Of the last kp_launch_select: ms[0] = launch kernel (HIP events on the ctx stream), ms[1] = whole call; host phases
+ * ms[2] = request encoding, ms[3] = table merge + upload, ms[4] = kernel + result download, ms[5] = result expansion. */
 kp_status kp_launch_stats(kp_ctx* ctx, double* ms, int32_t n);
 
 /*

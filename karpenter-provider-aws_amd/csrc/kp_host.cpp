@@ -15,6 +15,9 @@
 #include <set>
 #include <memory>
 #include <string>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -117,11 +120,39 @@ struct KeyDict {
         int i = (int)vals.size();
         ids.emplace(v, i);
         vals.push_back(v);
+        slots.clear();  // the fast index no longer covers every value: find_fast falls back to find
         return i;
     }
     int find(const std::string& v) const {
         auto it = ids.find(v);
         return it == ids.end() ? -1 : it->second;
+    }
+    // open-addressing FNV-1a index over vals for C-string lookups without std::string temporaries (launch-request
+    // encoding); rebuilt by freeze() after the dictionary stops growing (catalog upload)
+    std::vector<int32_t> slots;
+    static uint64_t hash(const char* s) {
+        uint64_t h = 1469598103934665603ull;
+        for (; *s; s++) h = (h ^ (uint8_t)*s) * 1099511628211ull;
+        return h;
+    }
+    void freeze() {
+        size_t cap = 16;
+        while (cap < vals.size() * 2) cap <<= 1;
+        slots.assign(cap, -1);
+        for (int i = 0; i < (int)vals.size(); i++) {
+            size_t h = hash(vals[i].c_str()) & (cap - 1);
+            while (slots[h] >= 0) h = (h + 1) & (cap - 1);
+            slots[h] = i;
+        }
+    }
+    int find_fast(const char* v) const {
+        if (slots.empty()) return find(v);
+        const size_t mask = slots.size() - 1;
+        for (size_t h = hash(v) & mask;; h = (h + 1) & mask) {
+            const int i = slots[h];
+            if (i < 0) return -1;
+            if (!strcmp(vals[i].c_str(), v)) return i;
+        }
     }
 };
 
@@ -192,6 +223,101 @@ struct PrefExpansion {
     std::vector<std::vector<kp_requirement>> reqs;
     std::vector<std::vector<kp_toleration>> tols;
     std::vector<std::vector<kp_topology_term>> terms;
+};
+
+// Persistent worker threads of a ctx for the host-side batch work of kp_launch_select (request encoding, result
+// expansion): run(k, fn) calls fn(0..k-1) across the workers and the calling thread and returns when all are done.
+class WorkerPool {
+  public:
+    ~WorkerPool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    int size() const { return (int)th_.size() + 1; }
+    void grow(int n) {  // at most n - 1 workers (the caller is the n-th)
+        while ((int)th_.size() < n - 1) th_.emplace_back([this] { loop(); });
+    }
+    void run(int k, const std::function<void(int)>& fn) {
+        if (k <= 1 || th_.empty()) {
+            for (int i = 0; i < k; i++) fn(i);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            fn_ = &fn;
+            next_ = 0;
+            tasks_ = k;
+            left_ = k;
+            gen_++;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> g(mu_);
+        done_.wait(g, [this] { return left_ == 0; });
+        fn_ = nullptr;
+    }
+
+  private:
+    void work() {
+        for (;;) {
+            int i;
+            const std::function<void(int)>* f;
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                if (!fn_ || next_ >= tasks_) return;
+                i = next_++;
+                f = fn_;
+            }
+            (*f)(i);
+            std::lock_guard<std::mutex> g(mu_);
+            if (--left_ == 0) done_.notify_all();
+        }
+    }
+    void loop() {
+        int seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+            }
+            work();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)>* fn_ = nullptr;
+    int next_ = 0, tasks_ = 0, left_ = 0, gen_ = 0;
+    bool stop_ = false;
+};
+
+// Pinned host staging buffer, grow-only (launch-request tables: DMA without the pageable-copy staging).
+template <class T>
+struct PinBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    PinBuf() = default;
+    PinBuf(const PinBuf&) = delete;
+    PinBuf& operator=(const PinBuf&) = delete;
+    ~PinBuf() {
+        if (p) hipHostFree(p);
+    }
+    hipError_t ensure(size_t count) {
+        if (count <= n && p) return hipSuccess;
+        if (p) hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        const size_t c = count ? count : 1;
+        hipError_t e = hipHostMalloc((void**)&p, c * sizeof(T), hipHostMallocDefault);
+        if (e == hipSuccess) n = c;
+        return e;
+    }
 };
 
 }  // namespace
@@ -298,6 +424,7 @@ struct kp_ctx {
     DBuf<int32_t> d_trace;                   // KPSIM_TRACE_POD diagnostics
     std::string launch_err;
     std::vector<std::vector<std::pair<int, int>>> type_single;  // [T] (catalog key, value id) with Len() == 1
+    int ct_vid[3] = {-1, -1, -1};            // value ids of on-demand / spot / reserved in the capacity-type dictionary
     std::vector<int32_t> l_off_begin, l_off_val, l_ct, l_rt, l_rcap;
     std::vector<double> l_price;
     std::vector<uint8_t> l_avail, l_exotic;
@@ -310,7 +437,15 @@ struct kp_ctx {
     DBuf<KlMinKey> d_l_mins;
     DBuf<uint64_t> d_l_words;
     DBuf<int64_t> d_l_rq;
-    double launch_ms[2] = {};                // launch kernel, whole call
+    PinBuf<KlReq> p_l_req;                   // pinned staging of the launch tables and results
+    PinBuf<int64_t> p_l_rq;
+    PinBuf<KlKey> p_l_keys;
+    PinBuf<KlMinKey> p_l_mins;
+    PinBuf<uint64_t> p_l_words, p_l_over;
+    PinBuf<int32_t> p_l_hdr, p_l_types;
+    WorkerPool pool;                         // host threads of kp_launch_select's batch work
+    double launch_ms[6] = {};                // launch kernel, whole call; host phases: encode, merge + upload,
+                                             // kernel + download, result expansion
     // topology (kp_solve_prepare encodes the groups; execute resets the counts from the *0 copies)
     int tg_G = 0, tg_HG = 0;
     DBuf<int4> d_tg_info;
@@ -740,6 +875,7 @@ static kp_status catalog_upload_one(kp_ctx* ctx, const kp_catalog_view* v, uint6
     }
     HIPCHK(hipStreamSynchronize(s));
     c->epoch = epoch;
+    for (auto& kd : c->cat.keys) kd.freeze();  // the catalog dictionaries are complete: index them for lookups
     c->have_catalog = true;
     c->prepared = c->executed = false;
     c->cons_prepared = false;
@@ -2623,6 +2759,123 @@ SReq sreq_intersection(const SReq& a, const SReq& b) {
     if (!o.complement) o.has_gt = o.has_lt = false;
     return o;
 }
+
+// The same requirement in the catalog's value-id space (launch-request encoding): `ids` are the values the catalog
+// dictionary of key kc knows (sorted), `unk` the others (kept by name only — they decide whether a set is empty).
+struct IReq {
+    int kc = -1;          // catalog key, -1 when no type or offering carries it
+    std::string name;     // normalised key
+    bool comp = false;
+    std::vector<int> ids;
+    std::vector<std::string> unk;
+    bool has_gt = false, has_lt = false;
+    int64_t gt = 0, lt = 0;
+    bool has_min = false;
+    int minv = 0;
+    int op() const {  // 0 In, 1 NotIn, 2 Exists, 3 DoesNotExist
+        const bool empty = ids.empty() && unk.empty();
+        if (comp) return empty ? 2 : 1;
+        return empty ? 3 : 0;
+    }
+};
+const char* const kCtNames[3] = {"on-demand", "spot", "reserved"};
+bool ireq_within(const IReq& q, const std::string& v) {
+    if (!q.has_gt && !q.has_lt) return true;
+    int64_t x = 0;
+    if (!go_atoi(v.c_str(), x)) return false;
+    if (q.has_gt && q.gt >= x) return false;
+    if (q.has_lt && q.lt <= x) return false;
+    return true;
+}
+IReq ireq_new(const kp_ctx* c, const kp_requirement& r) {
+    IReq q;
+    q.name = normalize(r.key);
+    q.kc = c->cat.find_key(q.name);
+    q.comp = !(r.op == KP_OP_IN || r.op == KP_OP_DOES_NOT_EXIST);
+    if (r.op == KP_OP_IN || r.op == KP_OP_NOT_IN) {
+        const KeyDict* kd = q.kc >= 0 ? &c->cat.keys[q.kc] : nullptr;
+        q.ids.reserve(r.n_values);
+        for (int j = 0; j < r.n_values; j++) {
+            const char* v = r.values[j] ? r.values[j] : "";
+            const int id = kd ? kd->find_fast(v) : -1;
+            if (id >= 0) q.ids.push_back(id);
+            else q.unk.emplace_back(v);
+        }
+        std::sort(q.ids.begin(), q.ids.end());
+        q.ids.erase(std::unique(q.ids.begin(), q.ids.end()), q.ids.end());
+        std::sort(q.unk.begin(), q.unk.end());
+        q.unk.erase(std::unique(q.unk.begin(), q.unk.end()), q.unk.end());
+    }
+    if (r.op == KP_OP_GT || r.op == KP_OP_LT) {
+        int64_t x = 0;
+        go_atoi(r.n_values > 0 && r.values[0] ? r.values[0] : "", x);
+        (r.op == KP_OP_GT ? q.has_gt : q.has_lt) = true;
+        (r.op == KP_OP_GT ? q.gt : q.lt) = x;
+    }
+    q.has_min = r.min_values >= 0;
+    q.minv = r.min_values;
+    return q;
+}
+template <class V>
+V set_op(const V& a, const V& b, int how) {  // 0 union, 1 a \ b, 2 a ∩ b (sorted inputs)
+    V o;
+    if (how == 0) std::set_union(a.begin(), a.end(), b.begin(), b.end(), std::back_inserter(o));
+    else if (how == 1) std::set_difference(a.begin(), a.end(), b.begin(), b.end(), std::back_inserter(o));
+    else std::set_intersection(a.begin(), a.end(), b.begin(), b.end(), std::back_inserter(o));
+    return o;
+}
+// Requirement.Intersection (same rules as sreq_intersection, in value-id space)
+IReq ireq_intersection(const kp_ctx* c, const IReq& a, const IReq& b) {
+    IReq o;
+    o.kc = a.kc;
+    o.name = a.name;
+    o.comp = a.comp && b.comp;
+    o.has_gt = a.has_gt || b.has_gt;
+    o.gt = (a.has_gt && b.has_gt) ? std::max(a.gt, b.gt) : (a.has_gt ? a.gt : b.gt);
+    o.has_lt = a.has_lt || b.has_lt;
+    o.lt = (a.has_lt && b.has_lt) ? std::min(a.lt, b.lt) : (a.has_lt ? a.lt : b.lt);
+    o.has_min = a.has_min || b.has_min;
+    o.minv = (a.has_min && b.has_min) ? std::max(a.minv, b.minv) : (a.has_min ? a.minv : b.minv);
+    if (o.has_gt && o.has_lt && o.gt >= o.lt) {
+        IReq d;
+        d.kc = a.kc;
+        d.name = a.name;
+        d.has_min = o.has_min;
+        d.minv = o.minv;
+        return d;
+    }
+    const int how = (a.comp && b.comp) ? 0 : 2;
+    if (a.comp && !b.comp) {
+        o.ids = set_op(b.ids, a.ids, 1);
+        o.unk = set_op(b.unk, a.unk, 1);
+    } else if (b.comp && !a.comp) {
+        o.ids = set_op(a.ids, b.ids, 1);
+        o.unk = set_op(a.unk, b.unk, 1);
+    } else {
+        o.ids = set_op(a.ids, b.ids, how);
+        o.unk = set_op(a.unk, b.unk, how);
+    }
+    if (o.has_gt || o.has_lt) {  // values outside the bounds are dropped
+        const std::vector<std::string>* vals = o.kc >= 0 ? &c->cat.keys[o.kc].vals : nullptr;
+        std::vector<int> ids;
+        for (int v : o.ids)
+            if (ireq_within(o, (*vals)[v])) ids.push_back(v);
+        o.ids.swap(ids);
+        std::vector<std::string> unk;
+        for (auto& x : o.unk)
+            if (ireq_within(o, x)) unk.push_back(x);
+        o.unk.swap(unk);
+    }
+    if (!o.comp) o.has_gt = o.has_lt = false;
+    return o;
+}
+// Requirement.Has for a value given by id (or by name when the dictionary does not know it, id < 0)
+bool ireq_has(const kp_ctx* c, const IReq& q, int id, const char* name) {
+    bool in;
+    if (id >= 0) in = std::binary_search(q.ids.begin(), q.ids.end(), id);
+    else in = std::binary_search(q.unk.begin(), q.unk.end(), std::string(name));
+    return (q.comp ? !in : in) && ireq_within(q, name);
+}
 }  // namespace
 
 extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_request* requests,
@@ -2639,18 +2892,28 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
     const int T = c->T, R = c->R, Kc = c->Kcat;
     // Requests are encoded independently (NewNodeSelectorRequirementsWithMinValues + digest per NodeClaim), so the
     // batch is split over host threads into chunk-local tables that are concatenated with their offsets rebased.
-    std::vector<KlReq> reqs(n);
-    std::vector<int64_t> rq((size_t)std::max(1, n) * R, 0);
+    HIPCHK(c->p_l_req.ensure(std::max(1, n)));
+    HIPCHK(c->p_l_rq.ensure((size_t)std::max(1, n) * R));
+    KlReq* const reqs = c->p_l_req.p;
+    int64_t* const rq = c->p_l_rq.p;
+    memset(rq, 0, (size_t)std::max(1, n) * R * sizeof(int64_t));
     const int roles[KL_ROLES] = {c->key_zone, c->key_ct, c->key_zoneid, c->key_resvid, c->key_resvtype};
     struct Chunk {
         std::vector<KlKey> keys;
         std::vector<KlMinKey> mins;
         std::vector<uint64_t> words;
+        std::vector<IReq> scratch;
+        std::vector<uint8_t> constrained;
         kp_status st = KP_OK;
         std::string msg;
     };
-    const int nthr = std::max(1, std::min<int>({8, (int)std::thread::hardware_concurrency(), (n + 255) / 256}));
+    for (int x = 0; x < 3; x++) c->ct_vid[x] = c->key_ct >= 0 ? c->cat.keys[c->key_ct].find(kCtNames[x]) : -1;
+    int nthr = std::max(1, std::min<int>({16, (int)std::thread::hardware_concurrency(), (n + 255) / 256}));
+    if (const char* e = getenv("KPSIM_LAUNCH_THREADS")) nthr = std::max(1, std::min(nthr, atoi(e)));  // diagnostics
     std::vector<Chunk> chunks(nthr);
+    // catalog keys that are well-known labels (undefined on a request: no constraint), computed once per call
+    std::vector<uint8_t> wk(Kc, 0);
+    for (int kc = 0; kc < Kc; kc++) wk[kc] = well_known(c->cat.keys[kc].name) ? 1 : 0;
     auto encode_one = [&](int i, Chunk& ch) -> bool {
         std::vector<KlKey>& keys = ch.keys;
         std::vector<KlMinKey>& mins = ch.mins;
@@ -2662,56 +2925,63 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
         };
         const kp_launch_request& lr = requests[i];
         if (lr.n_requirements < 0 || (lr.n_requirements > 0 && !lr.requirements)) return err(KP_E_INVALID, "bad request");
-        std::map<std::string, SReq> m;  // NewNodeSelectorRequirementsWithMinValues: Add = intersect per key
+        // NewNodeSelectorRequirementsWithMinValues: Add = intersect per key, in catalog value-id space (values no type
+        // or offering carries are kept by name only: they decide whether a set is empty)
+        std::vector<IReq>& m = ch.scratch;
+        m.clear();
         for (int j = 0; j < lr.n_requirements; j++) {
             const kp_requirement& r = lr.requirements[j];
             if (!r.key || r.op < 0 || r.op > 5) return err(KP_E_INVALID, "bad requirement");
-            const std::string key = normalize(r.key);
-            SReq q = sreq_new(r);
-            auto it = m.find(key);
-            if (it == m.end()) m.emplace(key, q);
-            else it->second = sreq_intersection(q, it->second);
+            IReq q = ireq_new(c, r);
+            IReq* hit = nullptr;
+            for (IReq& x : m)
+                if (x.kc == q.kc && (q.kc >= 0 || x.name == q.name)) hit = &x;
+            if (hit) *hit = ireq_intersection(c, q, *hit);
+            else m.push_back(std::move(q));
         }
+        std::sort(m.begin(), m.end(), [](const IReq& a, const IReq& b) { return a.name < b.name; });
         if (lr.requests)
             for (int r = 0; r < R; r++) rq[(size_t)i * R + r] = lr.requests[r];
         KlReq& q = reqs[i];
         q = KlReq{};
         q.key_off = (int)keys.size();
-        std::map<int, int> woff_of;  // catalog key → word offset of its value bitset
-        for (auto& kv : m) {
-            const int kc = c->cat.find_key(kv.first);
+        int woff_of[KL_ROLES];
+        for (int r = 0; r < KL_ROLES; r++) woff_of[r] = -1;
+        const IReq* role_req[KL_ROLES] = {};
+        std::vector<uint8_t>& constrained = ch.constrained;
+        constrained.assign(Kc, 0);
+        for (const IReq& sq : m) {
+            const int kc = sq.kc;
             if (kc < 0) continue;  // no type or offering carries the key: absent on both sides, never constrains
+            constrained[kc] = 1;
             const KeyDict& kd = c->cat.keys[kc];
-            const auto& vals = kd.vals;
+            const int nv = (int)kd.vals.size();
             const int woff = (int)words.size();
-            words.resize(words.size() + std::max<size_t>(1, (vals.size() + 63) / 64), 0ull);
+            words.resize(words.size() + std::max<size_t>(1, (nv + 63) / 64), 0ull);
             // bit v ⇔ Has(vals[v]); In sets visit only their own values, complements start full and clear theirs
-            const SReq& sq = kv.second;
-            if (!sq.complement) {
-                for (const auto& x : sq.vals) {
-                    const int v = kd.find(x);
-                    if (v >= 0 && sq.within(x)) words[woff + v / 64] |= 1ull << (v % 64);
-                }
+            if (!sq.comp) {
+                for (int v : sq.ids) words[woff + v / 64] |= 1ull << (v % 64);
             } else {
                 const bool bounded = sq.has_gt || sq.has_lt;
-                for (size_t vv = 0; vv < vals.size(); vv++)
-                    if (!bounded || sq.within(vals[vv])) words[woff + vv / 64] |= 1ull << (vv % 64);
-                for (const auto& x : sq.vals) {
-                    const int v = kd.find(x);
-                    if (v >= 0) words[woff + v / 64] &= ~(1ull << (v % 64));
-                }
+                for (int vv = 0; vv < nv; vv++)
+                    if (!bounded || ireq_within(sq, kd.vals[vv])) words[woff + vv / 64] |= 1ull << (vv % 64);
+                for (int v : sq.ids) words[woff + v / 64] &= ~(1ull << (v % 64));
             }
-            woff_of[kc] = woff;
-            const int op = kv.second.op();
+            const int op = sq.op();
             KlKey kk{kc, c->cat_multi[kc], 0u, woff};
             kk.flags = (c->cat_kflags[kc] & KF_CAT_MULTI) ? KLK_MULTI : KLK_SINGLE;
             if (op == 1 || op == 3) kk.flags |= KLK_DNE_OK;
             if (c->cat_kflags[kc] != 0) keys.push_back(kk);
+            for (int r = 0; r < KL_ROLES; r++)
+                if (roles[r] == kc) {
+                    woff_of[r] = woff;
+                    role_req[r] = &sq;
+                }
         }
         q.n_keys = (int)keys.size() - q.key_off;
         q.und_off = (int)keys.size();
         for (int kc = 0; kc < Kc; kc++) {
-            if (c->cat_kflags[kc] == 0 || woff_of.count(kc) || well_known(c->cat.keys[kc].name)) continue;
+            if (c->cat_kflags[kc] == 0 || constrained[kc] || wk[kc]) continue;
             KlKey kk{kc, c->cat_multi[kc], (c->cat_kflags[kc] & KF_CAT_MULTI) ? KLK_MULTI : KLK_SINGLE, 0};
             keys.push_back(kk);
         }
@@ -2721,25 +2991,25 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
             KlRole& ro = q.role[r];
             ro = KlRole{KLR_PASS, 0u, 0, 0};
             if (kc < 0) continue;
-            auto it = woff_of.find(kc);
-            if (it != woff_of.end()) {
+            if (woff_of[r] >= 0) {
                 ro.mode = KLR_CONSTRAINED;
-                ro.woff = it->second;
-                const int op = m[c->cat.keys[kc].name].op();
+                ro.woff = woff_of[r];
+                const int op = role_req[r]->op();
                 if (op == 1 || op == 3) ro.flags = KLK_DNE_OK;
-            } else if (!well_known(c->cat.keys[kc].name)) {
+            } else if (!wk[kc]) {
                 ro.mode = KLR_FAIL_IN;
             }
         }
-        auto ct = m.find("karpenter.sh/capacity-type");
-        const char* cts[3] = {"on-demand", "spot", "reserved"};
-        for (int x = 0; x < 3; x++) q.ct_has[x] = ct == m.end() ? 1 : (ct->second.has(cts[x]) ? 1 : 0);
+        const IReq* ct = nullptr;
+        for (const IReq& x : m)
+            if (x.name == "karpenter.sh/capacity-type") ct = &x;
+        for (int x = 0; x < 3; x++) q.ct_has[x] = ct == nullptr ? 1 : (ireq_has(c, *ct, c->ct_vid[x], kCtNames[x]) ? 1 : 0);
         q.min_off = (int)mins.size();
-        for (auto& kv : m) {
-            if (!kv.second.has_min) continue;
+        for (const IReq& sq : m) {
+            if (!sq.has_min) continue;
             q.has_min = 1;
-            const int kc = c->cat.find_key(kv.first);
-            KlMinKey mk{-1, -1, 0, kv.second.minv};
+            const int kc = sq.kc;
+            KlMinKey mk{-1, -1, 0, sq.minv};
             if (kc >= 0 && c->cat_kflags[kc] != 0) {
                 mk.k = kc;
                 mk.mi = (c->cat_kflags[kc] & KF_CAT_MULTI) ? c->cat_multi[kc] : -1;
@@ -2761,43 +3031,57 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
         for (int i = i0; i < i1; i++)
             if (!encode_one(i, chunks[ti])) return;
     };
-    if (nthr == 1) {
-        run_chunk(0);
-    } else {
-        std::vector<std::thread> th;
-        for (int ti = 0; ti < nthr; ti++) th.emplace_back(run_chunk, ti);
-        for (auto& x : th) x.join();
-    }
-    std::vector<KlKey> keys;
-    std::vector<KlMinKey> mins;
-    std::vector<uint64_t> words;
+    c->pool.grow(nthr);
+    c->pool.run(nthr, run_chunk);
+    const auto t_enc = clk::now();
+    // chunk tables concatenated straight into pinned staging, offsets rebased per chunk
+    size_t nk = 0, nm = 0, nw = 0;
     for (int ti = 0; ti < nthr; ti++) {
-        Chunk& ch = chunks[ti];
-        if (ch.st != KP_OK) return fail(c, ch.st, ch.msg);
-        const int kb = (int)keys.size(), mb = (int)mins.size(), wbase = (int)words.size();
-        const int i0 = (int)((int64_t)n * ti / nthr), i1 = (int)((int64_t)n * (ti + 1) / nthr);
-        for (int i = i0; i < i1; i++) {
-            KlReq& q = reqs[i];
-            q.key_off += kb;
-            q.und_off += kb;
-            q.min_off += mb;
-            for (int r = 0; r < KL_ROLES; r++)
-                if (q.role[r].mode == KLR_CONSTRAINED) q.role[r].woff += wbase;
+        if (chunks[ti].st != KP_OK) return fail(c, chunks[ti].st, chunks[ti].msg);
+        nk += chunks[ti].keys.size();
+        nm += chunks[ti].mins.size();
+        nw += chunks[ti].words.size();
+    }
+    HIPCHK(c->p_l_keys.ensure(std::max<size_t>(nk, 1)));
+    HIPCHK(c->p_l_mins.ensure(std::max<size_t>(nm, 1)));
+    HIPCHK(c->p_l_words.ensure(std::max<size_t>(nw, 1)));
+    {
+        size_t kb = 0, mb = 0, wbase = 0;
+        for (int ti = 0; ti < nthr; ti++) {
+            Chunk& ch = chunks[ti];
+            const int i0 = (int)((int64_t)n * ti / nthr), i1 = (int)((int64_t)n * (ti + 1) / nthr);
+            for (int i = i0; i < i1; i++) {
+                KlReq& q = reqs[i];
+                q.key_off += (int)kb;
+                q.und_off += (int)kb;
+                q.min_off += (int)mb;
+                for (int r = 0; r < KL_ROLES; r++)
+                    if (q.role[r].mode == KLR_CONSTRAINED) q.role[r].woff += (int)wbase;
+            }
+            KlKey* kd = c->p_l_keys.p + kb;
+            for (size_t j = 0; j < ch.keys.size(); j++) {
+                kd[j] = ch.keys[j];
+                kd[j].woff += (int)wbase;  // undefined-key entries carry no bitset; their woff is never read
+            }
+            if (!ch.mins.empty()) memcpy(c->p_l_mins.p + mb, ch.mins.data(), ch.mins.size() * sizeof(KlMinKey));
+            if (!ch.words.empty()) memcpy(c->p_l_words.p + wbase, ch.words.data(), ch.words.size() * sizeof(uint64_t));
+            kb += ch.keys.size();
+            mb += ch.mins.size();
+            wbase += ch.words.size();
         }
-        for (KlKey kk : ch.keys) {
-            kk.woff += wbase;  // undefined-key entries carry no bitset; their woff is never read
-            keys.push_back(kk);
-        }
-        mins.insert(mins.end(), ch.mins.begin(), ch.mins.end());
-        words.insert(words.end(), ch.words.begin(), ch.words.end());
     }
     hipStream_t s = c->stream;
     if (n > 0) {
-        HIPCHK(c->d_l_req.upload(reqs, s));
-        HIPCHK(c->d_l_keys.upload(keys.empty() ? std::vector<KlKey>(1) : keys, s));
-        HIPCHK(c->d_l_mins.upload(mins.empty() ? std::vector<KlMinKey>(1) : mins, s));
-        HIPCHK(c->d_l_words.upload(words.empty() ? std::vector<uint64_t>(1) : words, s));
-        HIPCHK(c->d_l_rq.upload(rq, s));
+        auto up = [&](auto& dbuf, const auto* src, size_t count) -> hipError_t {
+            hipError_t e = dbuf.ensure(std::max<size_t>(count, 1));
+            if (e != hipSuccess || count == 0) return e;
+            return hipMemcpyAsync(dbuf.p, src, count * sizeof(*src), hipMemcpyHostToDevice, s);
+        };
+        HIPCHK(up(c->d_l_req, reqs, (size_t)n));
+        HIPCHK(up(c->d_l_keys, c->p_l_keys.p, nk));
+        HIPCHK(up(c->d_l_mins, c->p_l_mins.p, nm));
+        HIPCHK(up(c->d_l_words, c->p_l_words.p, nw));
+        HIPCHK(up(c->d_l_rq, rq, (size_t)n * R));
         HIPCHK(c->d_l_hdr.ensure((size_t)n * KL_HDR));
         HIPCHK(c->d_l_types.ensure((size_t)n * M));
         HIPCHK(c->d_l_over.ensure((size_t)n * M));
@@ -2829,50 +3113,79 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
     g.out_hdr = c->d_l_hdr.p;
     g.out_types = c->d_l_types.p;
     g.out_over = c->d_l_over.p;
+    const auto t_up = clk::now();
     HIPCHK(hipEventRecord(c->ev[0], s));
     HIPCHK(kp_launch_select_kernel(g, s));
     HIPCHK(hipEventRecord(c->ev[1], s));
-    std::vector<int32_t> hdr((size_t)n * KL_HDR), tys((size_t)n * M);
-    std::vector<uint64_t> ov((size_t)n * M);
+    HIPCHK(c->p_l_hdr.ensure((size_t)std::max(1, n) * KL_HDR));
+    HIPCHK(c->p_l_types.ensure((size_t)std::max(1, n) * M));
+    HIPCHK(c->p_l_over.ensure((size_t)std::max(1, n) * M));
+    const int32_t* const hdr = c->p_l_hdr.p;
+    const int32_t* const tys = c->p_l_types.p;
+    const uint64_t* const ov = c->p_l_over.p;
     if (n > 0) {
-        HIPCHK(hipMemcpyAsync(hdr.data(), c->d_l_hdr.p, hdr.size() * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(tys.data(), c->d_l_types.p, tys.size() * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(ov.data(), c->d_l_over.p, ov.size() * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(c->p_l_hdr.p, c->d_l_hdr.p, (size_t)n * KL_HDR * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(c->p_l_types.p, c->d_l_types.p, (size_t)n * M * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(c->p_l_over.p, c->d_l_over.p, (size_t)n * M * 8, hipMemcpyDeviceToHost, s));
     }
     HIPCHK(hipStreamSynchronize(s));
     float kms = 0.f;
     HIPCHK(hipEventElapsedTime(&kms, c->ev[0], c->ev[1]));
     c->launch_ms[0] = kms;
-    int tpos = 0, opos = 0;
-    bool short_buf = false;
+    const auto t_dl = clk::now();
+    // result rows: counts first (type_offset / override_offset are prefix sums), then the lists, per thread range
+    std::vector<int64_t> toff(n + 1, 0), ooff(n + 1, 0);
+    auto par = [&](auto fn) {  // fn(i0, i1) over nthr contiguous ranges (the ctx's worker threads)
+        if (nthr == 1 || n < 1024) {
+            fn(0, n);
+            return;
+        }
+        c->pool.run(nthr, [&](int ti) { fn((int)((int64_t)n * ti / nthr), (int)((int64_t)n * (ti + 1) / nthr)); });
+    };
+    par([&](int i0, int i1) {
+        for (int i = i0; i < i1; i++) {
+            const int nt = hdr[(size_t)i * KL_HDR + 3];
+            int64_t no = 0;
+            for (int k = 0; k < nt; k++) no += __builtin_popcountll(ov[(size_t)i * M + k]);
+            toff[i + 1] = nt;
+            ooff[i + 1] = no;
+        }
+    });
     for (int i = 0; i < n; i++) {
-        const int32_t* h = &hdr[(size_t)i * KL_HDR];
-        kp_launch_result& r = results[i];
-        r.status = h[0];
-        r.failed_filter = h[1];
-        r.capacity_type = h[2];
-        r.n_types = h[3];
-        r.n_options = h[5];
-        for (int f = 0; f < KP_N_FILTERS; f++) r.rejected[f] = h[8 + f];
-        r.type_offset = tpos;
-        r.override_offset = opos;
-        r.n_overrides = 0;
-        for (int k = 0; k < r.n_types; k++) {
-            const int32_t t = tys[(size_t)i * M + k];
-            if (type_ids && tpos < cap_type_ids) type_ids[tpos] = t;
-            else short_buf = true;
-            tpos++;
-            // override offerings of slot k: bit j = offering row off_begin[t] + j, ascending
-            for (uint64_t m = ov[(size_t)i * M + k]; m; m &= m - 1) {
-                if (override_offerings && opos < cap_overrides)
-                    override_offerings[opos] = c->l_off_begin[t] + __builtin_ctzll(m);
-                else short_buf = true;
-                opos++;
-                r.n_overrides++;
+        toff[i + 1] += toff[i];
+        ooff[i + 1] += ooff[i];
+    }
+    const bool short_buf = (n > 0 && toff[n] > 0 && (!type_ids || toff[n] > cap_type_ids)) ||
+                           (n > 0 && ooff[n] > 0 && (!override_offerings || ooff[n] > cap_overrides));
+    par([&](int i0, int i1) {
+        for (int i = i0; i < i1; i++) {
+            const int32_t* h = &hdr[(size_t)i * KL_HDR];
+            kp_launch_result& r = results[i];
+            r.status = h[0];
+            r.failed_filter = h[1];
+            r.capacity_type = h[2];
+            r.n_types = h[3];
+            r.n_options = h[5];
+            for (int f = 0; f < KP_N_FILTERS; f++) r.rejected[f] = h[8 + f];
+            r.type_offset = (int32_t)toff[i];
+            r.override_offset = (int32_t)ooff[i];
+            r.n_overrides = (int32_t)(ooff[i + 1] - ooff[i]);
+            int64_t tp = toff[i], op = ooff[i];
+            for (int k = 0; k < r.n_types; k++, tp++) {
+                const int32_t t = tys[(size_t)i * M + k];
+                if (type_ids && tp < cap_type_ids) type_ids[tp] = t;
+                // override offerings of slot k: bit j = offering row off_begin[t] + j, ascending
+                for (uint64_t m = ov[(size_t)i * M + k]; m; m &= m - 1, op++)
+                    if (override_offerings && op < cap_overrides) override_offerings[op] = c->l_off_begin[t] + __builtin_ctzll(m);
             }
         }
-    }
+    });
     c->launch_ms[1] = ns_since(t0) / 1e6;
+    auto ms_between = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    c->launch_ms[2] = ms_between(t0, t_enc);
+    c->launch_ms[3] = ms_between(t_enc, t_up);
+    c->launch_ms[4] = ms_between(t_up, t_dl);
+    c->launch_ms[5] = ms_between(t_dl, clk::now());
     if (short_buf) return fail(c, KP_E_BUFFER, "type_ids / override_offerings too small");
     return KP_OK;
 } catch (const std::exception& e) {
@@ -2935,6 +3248,6 @@ extern "C" kp_status kp_nodeclaim_labels(kp_ctx* ctx, int32_t type_index, int32_
 
 extern "C" kp_status kp_launch_stats(kp_ctx* ctx, double* ms, int32_t n) {
     if (!ctx || !ms) return KP_E_INVALID;
-    for (int i = 0; i < n && i < 2; i++) ms[i] = ctx->launch_ms[i];
+    for (int i = 0; i < n && i < 6; i++) ms[i] = ctx->launch_ms[i];
     return KP_OK;
 }

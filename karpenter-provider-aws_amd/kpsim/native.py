@@ -131,9 +131,10 @@ class Context:
         labels = dict(line.split("\t", 1) for line in buf.value.decode().splitlines() if line)
         return labels, cap, alloc
 
-    def launch_stats(self):
-        ms = (C.c_double * 2)()
-        self.check(self.L.kp_launch_stats(self.h, ms, 2), "kp_launch_stats")
+    def launch_stats(self, n=2):
+        """[kernel ms, whole call ms] (n=6 adds the host phases: encode, merge + upload, kernel + download, expand)."""
+        ms = (C.c_double * n)()
+        self.check(self.L.kp_launch_stats(self.h, ms, n), "kp_launch_stats")
         return list(ms)
 
     def prepare(self, input_view):

@@ -32,6 +32,9 @@ hipError_t hipGetDeviceProperties(hipDeviceProp_t* p, int d);
 const char* hipGetErrorString(hipError_t e);
 hipError_t hipMalloc(void** p, size_t bytes);
 hipError_t hipFree(void* p);
+#define hipHostMallocDefault 0x0
+hipError_t hipHostMalloc(void** p, size_t bytes, unsigned flags);
+hipError_t hipHostFree(void* p);
 hipError_t hipMemcpy(void* dst, const void* src, size_t bytes, hipMemcpyKind k);
 hipError_t hipMemcpyAsync(void* dst, const void* src, size_t bytes, hipMemcpyKind k, hipStream_t s);
 hipError_t hipMemsetAsync(void* dst, int v, size_t bytes, hipStream_t s);

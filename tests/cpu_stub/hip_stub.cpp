@@ -53,6 +53,8 @@ hipError_t hipFree(void* p) {
     free(p);
     return hipSuccess;
 }
+hipError_t hipHostMalloc(void** p, size_t bytes, unsigned) { return hipMalloc(p, bytes); }
+hipError_t hipHostFree(void* p) { return hipFree(p); }
 hipError_t hipMemcpy(void* dst, const void* src, size_t bytes, hipMemcpyKind) {
     if (bytes) memmove(dst, src, bytes);
     return hipSuccess;
