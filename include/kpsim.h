@@ -472,6 +472,139 @@ kp_status kp_nodeclaim_labels(kp_ctx* ctx, int32_t type_index, int32_t offering,
                               int64_t* capacity, int64_t* allocatable);
 
 /*
+ * Catalog ingestion — replaces instancetype.DefaultProvider.List's construction of the
+ * `[]*cloudprovider.InstanceType` (pkg/providers/instancetype/instancetype.go:123-165) from raw EC2 data:
+ *   NewInstanceType (pkg/providers/instancetype/types.go:123-155) = computeRequirements (:158-299),
+ *     computeCapacity (:320-338: cpu, memory − VM overhead, ephemeral storage from the block device mappings / AMI
+ *     family defaults, pods, pod-eni, GPUs, neuron, gaudi, efa), PrivateIPv4Address for Windows-compatible types
+ *     (:151-153), Overhead = kubeReservedResources (:493-530) + systemReservedResources (:487-491) +
+ *     evictionThreshold (:532-560, computeEvictionSignal :598-615); Allocatable = Capacity − Overhead.Total();
+ *     AMI family feature flags (pkg/providers/amifamily/resolver.go:102-119, bottlerocket.go:126-131,
+ *     windows.go:101-107) and default block devices (al2023.go:99-108, bottlerocket.go:95-112, windows.go:88-99,
+ *     custom.go:48-58, resolver.go:40-43);
+ *   offering.DefaultProvider.InjectOfferings / createOfferings (pkg/providers/instancetype/offering/offering.go:70-196):
+ *     one offering per (zone of all_zones, capacity type on-demand|spot of the type), Available = !ICE && hasPrice &&
+ *     zone ∈ the type's zones (:148), zone-id when the NodeClass maps the zone (:151-153); with the ReservedCapacity
+ *     gate, one reserved offering per capacity reservation of the type, price = on-demand / 1e7 (:176), Available =
+ *     count ≠ 0 && zone ok && not expiring (:187).
+ * The resulting kp_catalog is a host object; kp_catalog_get_view exposes it as a kp_catalog_view (resource axes in the
+ * order of kp_catalog_resource_name) that stays valid until kp_catalog_free, ready for kp_catalog_upload.  Go iterates
+ * the allZones set in map order (offering.go:135); here offerings follow all_zones order, types follow input order.
+ */
+enum { KP_AMI_AL2 = 0, KP_AMI_AL2023 = 1, KP_AMI_BOTTLEROCKET = 2, KP_AMI_WINDOWS2019 = 3, KP_AMI_WINDOWS2022 = 4,
+       KP_AMI_CUSTOM = 5 };
+#define KP_CATALOG_R 12                      /* resource axes of a built catalog */
+
+typedef struct kp_ec2_device {               /* GpuDeviceInfo / InferenceDeviceInfo / NeuronDeviceInfo */
+    const char* name;
+    const char* manufacturer;
+    int32_t count;
+    int32_t memory_mib;                      /* GPUs: MemoryInfo.SizeInMiB */
+    int32_t cores;                           /* neuron: CoreInfo.Count */
+} kp_ec2_device;
+
+/* ec2types.InstanceTypeInfo fields the provider reads, plus the per-name tables it joins
+   (zz_generated.vpclimits.go Limits, zz_generated.bandwidth.go InstanceTypeBandwidthMegabits). */
+typedef struct kp_ec2_instance_type {
+    const char* name;                        /* InstanceType */
+    int32_t default_vcpus;                   /* VCpuInfo.DefaultVCpus */
+    int64_t memory_mib;                      /* MemoryInfo.SizeInMiB */
+    int32_t n_architectures;                 /* ProcessorInfo.SupportedArchitectures ("x86_64", "arm64", ...) */
+    const char* const* architectures;
+    int32_t has_processor_info;              /* ProcessorInfo != nil */
+    const char* cpu_manufacturer;            /* ProcessorInfo.Manufacturer (NULL: nil) */
+    double sustained_clock_ghz;              /* ProcessorInfo.SustainedClockSpeedInGhz (NaN: nil) */
+    int32_t n_usage_classes;                 /* SupportedUsageClasses */
+    const char* const* usage_classes;
+    const char* hypervisor;                  /* Hypervisor (NULL: "") */
+    int32_t encryption_in_transit;           /* NetworkInfo.EncryptionInTransitSupported */
+    int32_t n_network_cards;                 /* NetworkInfo.NetworkCards[].MaximumNetworkInterfaces */
+    const int32_t* card_max_interfaces;
+    int32_t default_card;                    /* NetworkInfo.DefaultNetworkCardIndex */
+    int32_t max_network_interfaces;          /* used only when n_network_cards == 0 */
+    int32_t ipv4_per_interface;              /* NetworkInfo.Ipv4AddressesPerInterface */
+    int32_t efa_max;                         /* NetworkInfo.EfaInfo.MaximumEfaInterfaces (0: nil) */
+    int64_t instance_storage_gb;             /* InstanceStorageInfo.TotalSizeInGB (< 0: nil) */
+    const char* nvme_support;                /* InstanceStorageInfo.NvmeSupport (NULL: nil) */
+    int32_t n_gpus;                          /* GpuInfo.Gpus */
+    const kp_ec2_device* gpus;
+    int32_t n_accelerators;                  /* InferenceAcceleratorInfo.Accelerators (< 0: nil) */
+    const kp_ec2_device* accelerators;
+    int32_t n_neuron;                        /* NeuronInfo.NeuronDevices (< 0: NeuronInfo nil) */
+    const kp_ec2_device* neuron;
+    int64_t ebs_max_bandwidth_mbps;          /* EbsInfo.EbsOptimizedInfo.MaximumBandwidthInMbps (< 0: nil) */
+    const char* ebs_optimized_support;       /* EbsInfo.EbsOptimizedSupport */
+    int32_t has_vpc_limits;                  /* Limits[name] present */
+    int32_t vpc_trunking;                    /*   .IsTrunkingCompatible */
+    int32_t vpc_branch_interface;            /*   .BranchInterface */
+    int32_t vpc_ipv4_per_interface;          /*   .IPv4PerInterface */
+    int64_t network_bandwidth_mbps;          /* InstanceTypeBandwidthMegabits[name] (< 0: absent) */
+} kp_ec2_instance_type;
+
+typedef struct kp_string_pair { const char* key; const char* value; } kp_string_pair;   /* map[string]string entry */
+typedef struct kp_zone_info { const char* zone; const char* zone_id; } kp_zone_info;    /* v1.ZoneInfo */
+typedef struct kp_block_device_mapping {     /* v1.BlockDeviceMapping */
+    const char* device_name;
+    int32_t root_volume;
+    const char* volume_size;                 /* EBS.VolumeSize quantity ("100Gi"), NULL: nil */
+} kp_block_device_mapping;
+typedef struct kp_capacity_reservation {     /* v1.CapacityReservation (EC2NodeClass status) */
+    const char* id;
+    const char* instance_type;
+    const char* availability_zone;
+    const char* reservation_type;            /* "default" | "capacity-block" */
+    int32_t expiring;                        /* State == expiring */
+    int32_t available_count;                 /* capacityReservationProvider.GetAvailableInstanceCount(id) */
+} kp_capacity_reservation;
+
+/* The EC2NodeClass (resolved kubelet configuration included) and the provider options the catalog depends on. */
+typedef struct kp_nodeclass_view {
+    int32_t ami_family;                      /* KP_AMI_* (amifamily.GetAMIFamily) */
+    const char* region;
+    int32_t n_zones;                         /* nodeClass.ZoneInfo(): subnet zones and their zone ids */
+    const kp_zone_info* zones;
+    int32_t n_block_device_mappings;
+    const kp_block_device_mapping* block_device_mappings;
+    int32_t instance_store_raid0;            /* InstanceStorePolicy == RAID0 */
+    int32_t max_pods;                        /* kubelet maxPods (< 0: nil) */
+    int32_t pods_per_core;                   /* kubelet podsPerCore (<= 0: nil) */
+    int32_t n_kube_reserved;                 /* kubelet kubeReserved / systemReserved (resource → quantity) */
+    const kp_string_pair* kube_reserved;
+    int32_t n_system_reserved;
+    const kp_string_pair* system_reserved;
+    int32_t n_eviction_hard;                 /* kubelet evictionHard / evictionSoft (signal → quantity or "N%") */
+    const kp_string_pair* eviction_hard;
+    int32_t n_eviction_soft;
+    const kp_string_pair* eviction_soft;
+    int32_t n_capacity_reservations;         /* nodeClass.CapacityReservations() */
+    const kp_capacity_reservation* capacity_reservations;
+    double vm_memory_overhead_percent;       /* options.VMMemoryOverheadPercent (0.075) */
+    int32_t reserved_enis;                   /* options.ReservedENIs */
+    int32_t reserved_capacity;               /* feature gate ReservedCapacity */
+} kp_nodeclass_view;
+
+/* Prices and the ICE cache as createOfferings reads them (pricing.OnDemandPrice / SpotPrice, IsUnavailable). */
+typedef struct kp_offering_source {
+    int32_t n_zones;                         /* allZones: every zone with an instance-type offering */
+    const char* const* zones;
+    const char* const* type_zones;           /* [n_types] per type: its offering zones, '\n'-separated
+                                                (DescribeInstanceTypeOfferings) */
+    const double* od_price;                  /* [n_types] on-demand price, NaN: no price */
+    const double* spot_price;                /* [n_types * n_zones] spot price per zone, NaN: no price */
+    const uint8_t* unavailable;              /* [n_types * n_zones * 2] ICE (zone-major, then od/spot), NULL: none */
+} kp_offering_source;
+
+typedef struct kp_catalog kp_catalog;
+kp_status kp_catalog_build(int32_t n_types, const kp_ec2_instance_type* types, const kp_nodeclass_view* nodeclass,
+                           const kp_offering_source* offerings, kp_catalog** out);
+/* A view of the built catalog (borrowed from `cat`, valid until kp_catalog_free). */
+kp_status kp_catalog_get_view(const kp_catalog* cat, kp_catalog_view* view);
+/* Overhead.Total() of type t ([KP_CATALOG_R]) and the resource-axis names. */
+kp_status kp_catalog_overhead(const kp_catalog* cat, int32_t t, int64_t* overhead);
+const char* kp_catalog_resource_name(int32_t r);
+kp_status kp_catalog_free(kp_catalog* cat);
+
+/*
  * Requirements of NodeClaim `nc` from the last kp_solve on this ctx (hostname removed as in
  * FinalizeScheduling), one line per key, lines sorted:
  *   "key \t complement(0|1) \t gt|- \t lt|- \t minValues|- \t v1 \x1f v2 ..."   (values sorted)

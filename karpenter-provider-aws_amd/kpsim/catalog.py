@@ -106,7 +106,8 @@ def instance_resources(info, opts: TypeOptions, vpclimits=None):
     mem = mib * Mi
     mem -= int(math.ceil(float(mem) * opts.vm_memory_overhead_pct / 1024 / 1024)) * Mi
     cap[RIDX["memory"]] = mem * 1000
-    eph = 20 * Gi
+    # the AMI family's ephemeral block device default: 20Gi (resolver.go:40-43), Windows /dev/sda1 50Gi (windows.go:88-99)
+    eph = 50 * Gi if opts.ami_family.startswith("Windows") else 20 * Gi
     if opts.raid0 and info.get("instance_storage_gb") is not None:
         eph = int(info["instance_storage_gb"]) * 1000 ** 3
     cap[RIDX["ephemeral-storage"]] = eph * 1000

@@ -12,7 +12,8 @@ EXPORTS = [
     "kp_catalog_patch_price", "kp_solve", "kp_solve_prepare", "kp_solve_execute", "kp_solve_fetch",
     "kp_result_nodeclaim_requirements", "kp_last_kernel_times", "kp_consolidate_probe_count", "kp_consolidate",
     "kp_consolidate_stats", "kp_consolidate_prepare", "kp_consolidate_execute", "kp_launch_select", "kp_launch_stats",
-    "kp_nodeclaim_labels",
+    "kp_nodeclaim_labels", "kp_catalog_build", "kp_catalog_get_view", "kp_catalog_overhead", "kp_catalog_resource_name",
+    "kp_catalog_free",
 ]
 
 _lib = None
@@ -61,7 +62,7 @@ def load():
     L.kp_nodeclaim_labels.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_char_p, C.c_char_p, C.c_int32, C.c_char_p,
                                       C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     for f in EXPORTS:
-        if f not in ("kp_last_error", "kp_version"):
+        if f not in ("kp_last_error", "kp_version", "kp_catalog_resource_name"):
             getattr(L, f).restype = C.c_int32
     _lib = L
     return L

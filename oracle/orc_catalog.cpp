@@ -54,8 +54,9 @@ extern "C" void orc_instance_type_resources(const orc_ec2_info* info, const orc_
     double ovh = (double)mem_bytes * o->vm_memory_overhead_pct / 1024 / 1024;
     mem_bytes -= (int64_t)std::ceil(ovh) * Mi;
     cap[ORC_R_MEMORY] = mem_bytes * 1000;
-    // ephemeralStorage(): RAID0 with instance storage → "%dG"; otherwise the AMI's default 20Gi root volume
-    int64_t eph_bytes = 20 * Gi;
+    // ephemeralStorage(): RAID0 with instance storage → "%dG"; otherwise the AMI family's ephemeral block device default:
+    // 20Gi (DefaultEBS, amifamily/resolver.go:40-43), 50Gi for Windows' /dev/sda1 (amifamily/windows.go:88-99)
+    int64_t eph_bytes = o->ami_family == ORC_AMI_WINDOWS ? 50 * Gi : 20 * Gi;
     if (o->raid0 && info->instance_storage_gb >= 0) eph_bytes = info->instance_storage_gb * 1000000000LL;
     cap[ORC_R_EPHEMERAL] = eph_bytes * 1000;
     // pods()
