@@ -449,14 +449,15 @@ __device__ __forceinline__ bool topo_narrow(const KpDev& d, const ClassCache& CC
 // AllowUndefinedWellKnownLabels option when allow_wk, owner's tolerations); spread / affinity record a single-valued
 // domain, anti-affinity and inverse groups record every value (requirement.Values(), the excluded set of a complement).
 __device__ inline bool topo_filter_compatible(const KpDev& d, const ClassCache& CC, const WaveScratch& ws,
-                                              const ReqHdr* Ahdr, const uint64_t* Aw, int owner, bool allow_wk, int lane) {
+                                              const ReqHdr* Ahdr, const uint64_t* Aw, int owner, bool allow_wk, int lane,
+                                              bool exnode = false) {
     bool ok = true;
     for (int i = d.cls_xkoff[owner] + lane; i < d.cls_xkoff[owner + 1]; i += 64) {
         const int k = d.cls_xkeys[i];
         const ReqHdr B = d.cls_hdr[(size_t)owner * d.K + k];
         const uint64_t* bw = d.cls_words + (size_t)owner * d.DW + d.woff[k];
         const bool bno = op_notin_or_dne(req_op(B.flags, popc_words(bw, d.nw[k])));
-        if (k == d.key_host) {  // NodeClaim hostname In [placeholder]: only a complement without bounds admits it
+        if (k == d.key_host && !exnode) {  // NodeClaim hostname In [placeholder]: only a complement without bounds admits it
             if (!((B.flags & RF_CMP) && !(B.flags & (RF_GT | RF_LT)))) ok = false;
             continue;
         }
@@ -475,8 +476,9 @@ __device__ inline bool topo_filter_compatible(const KpDev& d, const ClassCache& 
     return ballot(!ok) == 0;
 }
 
+// exnode >= 0: the placement is on existing node exnode (its taints: ex_tol; its hostname is a real node name).
 __device__ __forceinline__ void topo_record(const KpDev& d, const ClassCache& CC, const WaveScratch& ws, const ReqHdr* Ahdr,
-                                         const uint64_t* Aw, int host, int tmpl, bool allow_wk, int lane) {
+                                         const uint64_t* Aw, int host, int tmpl, bool allow_wk, int lane, int exnode = -1) {
     for (int e = 0; e < CC.ntr; e++) {
         const int g = CC.tr[e], ki = CC.tr_ki[e];
         const int4 info = d.tg_info[g];
@@ -484,8 +486,12 @@ __device__ __forceinline__ void topo_record(const KpDev& d, const ClassCache& CC
         const bool inv = info.x & TG_INVERSE;
         if (!inv && type == 0) {  // TopologyNodeFilter.Matches
             const int pol = d.tg_pol[g], owner = d.tg_owner[g];
-            if ((pol & 2) && !((d.tol[owner] >> tmpl) & 1u)) continue;
-            if ((pol & 1) && owner != CC.cls && !topo_filter_compatible(d, CC, ws, Ahdr, Aw, owner, allow_wk, lane)) continue;
+            const bool tolerated = exnode >= 0 ? ((d.ex_tol[(size_t)owner * d.EW + (exnode >> 6)] >> (exnode & 63)) & 1ull) != 0
+                                               : ((d.tol[owner] >> tmpl) & 1u) != 0;
+            if ((pol & 2) && !tolerated) continue;
+            if ((pol & 1) && owner != CC.cls &&
+                !topo_filter_compatible(d, CC, ws, Ahdr, Aw, owner, allow_wk, lane, exnode >= 0))
+                continue;
         }
         if (info.x & TG_HOST) {
             if (lane == 0) {
@@ -504,6 +510,68 @@ __device__ __forceinline__ void topo_record(const KpDev& d, const ClassCache& CC
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
+// ExistingNode.Add ([core] scheduling/existingnode.go) for a pod of a topology class on existing node j, one wave,
+// after the caller found j tolerated, Compatible (XT) and with headroom: the requirement merge of the class's keys into
+// the node's requirements (no undefined-label allowance), then Topology.AddRequirements with the node's own domains
+// (hostname = the node's name: host row j).  On success ws holds the merged class keys.
+template <bool CONS>
+__device__ inline bool existing_topo_try(const KpDev& d, const ClassCache& CC, WaveScratch& ws, int j, int lane) {
+    const ReqHdr* nh = d.ex_hdr + (size_t)j * d.K;
+    const uint64_t* nwp = d.ex_words + (size_t)j * d.DW;
+    if (lane < CC.nck) {
+        const int k = CC.key[lane], n = CC.nw[lane];
+        const ReqHdr A = nh[k];
+        const uint64_t* aw = nwp + CC.woff[lane];
+        uint64_t* ow = ws.words + CC.wsoff[lane];
+        ReqHdr O;
+        if (((CC.kneutral >> lane) & 1u) || !(CC.hdr[lane].flags & RF_DEF)) {
+            O = A;  // the class does not constrain the key: the node's requirement stands
+            for (int i = 0; i < n; i++) ow[i] = (A.flags & RF_DEF) ? aw[i] : 0ull;
+        } else if (!(A.flags & RF_DEF)) {
+            O = CC.hdr[lane];  // undefined on the node: XT admitted it (NotIn / DoesNotExist)
+            for (int i = 0; i < n; i++) ow[i] = CC.words[CC.wsoff[lane] + i];
+        } else {
+            req_intersect(d, k, A, aw, CC.hdr[lane], CC.words + CC.wsoff[lane], O, ow);
+        }
+        ws.hdr[lane] = O;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (CONS) return topo_narrow(d, CC, ws, j, false, lane);
+    return true;
+}
+
+// Commit of existing_topo_try: the node's requirements become the merged ones; when they changed, node j's XT column is
+// recomputed for every class (as existing_merge does).
+__device__ inline void existing_topo_commit(const KpDev& d, const ClassCache& CC, const WaveScratch& ws, int j, int lane) {
+    ReqHdr* nh = d.ex_hdr + (size_t)j * d.K;
+    uint64_t* nwp = d.ex_words + (size_t)j * d.DW;
+    bool ch = false;
+    if (lane < CC.nck) {
+        const int k = CC.key[lane], n = CC.nw[lane];
+        const ReqHdr O = ws.hdr[lane];
+        const ReqHdr A = nh[k];
+        ch = O.flags != A.flags || O.gt != A.gt || O.lt != A.lt || O.minv != A.minv;
+        for (int i = 0; i < n; i++) {
+            const uint64_t x = ws.words[CC.wsoff[lane] + i];
+            const uint64_t y = (A.flags & RF_DEF) ? nwp[CC.woff[lane] + i] : 0ull;
+            ch |= x != y;
+            nwp[CC.woff[lane] + i] = x;
+        }
+        nh[k] = O;
+    }
+    if (!ballot(ch)) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");  // the merged requirements are visible to every lane
+    const int w = j >> 6;
+    const uint64_t bm = 1ull << (j & 63);
+    for (int cc = lane; cc < d.C; cc += 64) {
+        const bool ok = d.ex_static[j] && (d.ex_tol[(size_t)cc * d.EW + w] & bm) && node_compatible(d, nh, nwp, cc);
+        if (ok) atomicOr((unsigned long long*)&d.XT[(size_t)cc * d.EW + w], (unsigned long long)bm);
+        else atomicAnd((unsigned long long*)&d.XT[(size_t)cc * d.EW + w], (unsigned long long)~bm);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 #define EV_STAMP(slot)                                                           \
     do {                                                                         \
         if (a.prof) {                                                            \

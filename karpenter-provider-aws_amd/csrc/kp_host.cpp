@@ -1391,8 +1391,6 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     {
         const kp_status ts = topo_build(c, in, creq, th, err);
         if (ts != KP_OK) return fail(ctx, ts, err);
-        if (!th.g.empty() && in->n_existing > 0)
-            return fail(ctx, KP_E_UNSUPPORTED, "topology with existing nodes (device path pending)");
     }
     // existing nodes (ExistingNode, [core] scheduling/existingnode.go NewExistingNode): requirements =
     // NewLabelRequirements(node labels) + hostname In [name].  Only label keys some pod class constrains can
@@ -1803,6 +1801,8 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         std::vector<uint64_t> tknown0(G1, 0);
         std::vector<int32_t> tcoff(C + 1, 0), tcl, troff(C + 1, 0), trl;
         std::vector<uint8_t> vrank((size_t)K * 64, 0xFF);
+        const int HN = E + NCcap;
+        std::vector<int32_t> hc0((size_t)std::max(1, th.n_host) * HN, 0);
         if (G > 0) {
             auto hreq_has = [&](const HReq& q, int v) {
                 const bool in = std::binary_search(q.vals.begin(), q.vals.end(), v);
@@ -1876,11 +1876,58 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
                 tcoff[i + 1] = (int)tcl.size();
                 troff[i + 1] = (int)trl.size();
             }
-            if (in->n_bound > 0) return fail(ctx, KP_E_UNSUPPORTED, "bound pods with topology (device path pending)");
+            // countDomains over the pods bound to existing nodes (forward groups that select the pod's class; a spread
+            // group's node filter against the node's labels and taints) and updateInverseAffinities (the inverse
+            // anti-affinity groups of the bound pod's class record the node's domain) — [core] scheduling/topology.go,
+            // restated in oracle/orc_solve.cpp build_topology.  A node without the key's label is not counted.
+            auto node_val = [&](int j, int k) {
+                for (auto& e : exlab[j])
+                    if (e.first == k) return e.second;
+                return -1;
+            };
+            auto node_compatible_with = [&](int j, int owner) {  // Compatible(node labels, owner reqs), no wk allowance
+                for (auto& kv : creq[owner]) {
+                    const HReq& q = kv.second;
+                    const int v = node_val(j, kv.first);
+                    const bool qno = (q.complement && !q.vals.empty()) || (!q.complement && q.vals.empty());
+                    if (v < 0) {
+                        if (!qno) return false;
+                        continue;
+                    }
+                    if (!hreq_has(q, v)) return false;
+                }
+                return true;
+            };
+            auto node_tolerated_by = [&](int j, int owner) {
+                const kp_existing_node& en = in->existing[j];
+                for (int q = 0; q < en.n_taints; q++)
+                    if (!tolerates(en.taints[q], in->classes[owner].tolerations, in->classes[owner].n_tolerations)) return false;
+                return true;
+            };
+            for (int i = 0; i < in->n_bound; i++) {
+                const int j = in->bound_node[i], b = in->bound_class[i];
+                if (j < 0 || j >= E || b < 0 || b >= C) return fail(ctx, KP_E_INVALID, "bound pod index out of range");
+                for (int gi = 0; gi < G; gi++) {
+                    const HGroup& g = th.g[gi];
+                    if (g.inverse ? g.owner != b : !g.sel[b]) continue;
+                    if (!g.inverse && g.type == KP_TOPO_SPREAD) {
+                        if ((g.pol & 1) && !node_compatible_with(j, g.owner)) continue;
+                        if ((g.pol & 2) && !node_tolerated_by(j, g.owner)) continue;
+                    }
+                    if (g.host) {
+                        if (hc0[(size_t)g.hrow * HN + j]++ == 0) tpos0[gi]++;
+                    } else {
+                        const int v = node_val(j, g.key);
+                        if (v < 0) continue;
+                        if (v >= 64) return fail(ctx, KP_E_UNSUPPORTED, "topology key with more than 64 values");
+                        tcnt0[(size_t)gi * 64 + v]++;
+                        tknown0[gi] |= 1ull << v;
+                    }
+                }
+            }
         }
         if (tcl.empty()) tcl.push_back(0);
         if (trl.empty()) trl.push_back(0);
-        const int HN = E + NCcap;
         HIPCHK(c->d_tg_info.upload(tinfo, s));
         HIPCHK(c->d_tg_hrow.upload(thr_row, s));
         HIPCHK(c->d_tg_owner.upload(towner, s));
@@ -1891,7 +1938,6 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         HIPCHK(c->d_tg_known.ensure(tknown0.size()));
         HIPCHK(c->d_tg_pos0.upload(tpos0, s));
         HIPCHK(c->d_tg_pos.ensure(tpos0.size()));
-        std::vector<int32_t> hc0((size_t)std::max(1, th.n_host) * HN, 0);
         HIPCHK(c->d_tg_hcnt0.upload(hc0, s));
         HIPCHK(c->d_tg_hcnt.ensure(hc0.size()));
         HIPCHK(c->d_cls_tcoff.upload(tcoff, s));

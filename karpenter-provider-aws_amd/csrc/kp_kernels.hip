@@ -188,6 +188,7 @@ struct FfdShared {
     // topology prefilter of the current pod (topo_prefilter_setup): a NodeClaim whose own requirements admit no
     // domain a constraining group allows cannot accept the pod, and is skipped without an evaluation
     int tp_n, topo_pod, topo_quick;
+    int ex_placed;                 // the current topology pod went to this existing node (-1: none accepted it)
     int tp_k[KP_MAX_TOPO];         // value-keyed group: key; hostname group: -1 - row of tg_hcnt
     int tp_lo[KP_MAX_TOPO], tp_hi[KP_MAX_TOPO];  // hostname group: the host's count must lie in [lo, hi]
     int tp_cmp[KP_MAX_TOPO];       // value-keyed: a complement (NotIn) NodeClaim requirement is not prefiltered
@@ -736,8 +737,9 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                     prev_shape = shape;
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 }
-                // ExistingNode.Add on the existing nodes in order, before sort.Slice (no re-sort when one accepts)
-                if (d.E > 0 && xstart < d.E) {
+                // ExistingNode.Add on the existing nodes in order, before sort.Slice (no re-sort when one accepts); a
+                // pod of a topology class is placed on existing nodes by the block (domain counts, node requirements)
+                if (d.E > 0 && xstart < d.E && !(TOPO_ON && ctopo)) {
                     int jf = -1;
                     for (int base = xstart; base < d.E; base += 64) {
                         const int j = base + lane;
@@ -1103,6 +1105,70 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
         if (S.done) break;
         const long long c_slow = prof_clock(d);
         const int pod = S.cur_pod;
+        if (TOPO_ON && S.topo_pod && d.E > 0) {
+            // ================= a pod with topology terms: existing nodes first (wave 0) =================
+            // ExistingNode.Add in scheduling order: tolerations + Compatible (XT) and headroom, then the requirement
+            // merge and Topology.AddRequirements on the node's own domains; the first node that accepts takes the pod
+            // and Topology.Record counts it there.  Counts change with every placement, so nothing is memoised.
+            if (S.cls_fill) fill_class_cache(d, S.cur_cls, S.CC, tid, nthr);
+            __syncthreads();
+            if (wave == 0) {
+                const int c = S.cur_cls;
+                const bool cons = (d.cls_flags[c] & CF_TOPO_CONS) != 0;
+                int placed = -1;
+                for (int base = 0; base < d.E && placed < 0; base += 64) {
+                    const int j = base + lane;
+                    bool cand = false;
+                    if (j < d.E) {
+                        const uint64_t xw = __hip_atomic_load(&d.XT[(size_t)c * d.EW + (j >> 6)], __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT);
+                        cand = (xw >> (j & 63)) & 1ull;
+                        for (int ai = 0; ai < d.n_active && cand; ai++)
+                            cand = S.pod_req[d.active_axes[ai]] <= ld_req(&d.ex_head[(size_t)ai * d.E + j]);
+                    }
+                    uint64_t m = ballot(cand);
+                    while (m) {
+                        const int jj = base + __ffsll((unsigned long long)m) - 1;
+                        m &= m - 1;
+                        const bool ok = cons ? existing_topo_try<true>(d, S.CC, S.ws[0], jj, lane)
+                                             : existing_topo_try<false>(d, S.CC, S.ws[0], jj, lane);
+                        if (ok) {
+                            placed = jj;
+                            break;
+                        }
+                    }
+                }
+                if (placed >= 0) {
+                    existing_topo_commit(d, S.CC, S.ws[0], placed, lane);
+                    topo_record(d, S.CC, S.ws[0], d.ex_hdr + (size_t)placed * K, d.ex_words + (size_t)placed * d.DW,
+                                placed, 0, false, lane, placed);
+                    if (lane < d.n_active) {
+                        const int64_t x = S.pod_req[d.active_axes[lane]];
+                        if (x) atomicAdd((unsigned long long*)&d.ex_head[(size_t)lane * d.E + placed], (unsigned long long)(-x));
+                    }
+                    if (lane == 0) {
+                        d.pod_result[pod] = -2 - placed;
+                        d.pod_order[pod] = S.seq++;
+                        S.scan_start = 0;
+                        S.st[ST_EXIST_PLACED] += 1;
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                if (lane == 0) {
+                    S.ex_placed = placed;
+                    S.cls_fill = 0;
+                }
+            }
+            __syncthreads();
+            if (S.ex_placed >= 0) {
+                if (tid == 0) {
+                    S.tp_n = 0;
+                    S.topo_pod = 0;
+                }
+                __syncthreads();
+                continue;
+            }
+        }
         if (TOPO_ON && S.topo_pod) {
             // ================= a pod with topology terms (wave 0) =================
             // prefilter of this pod's groups, first surviving NodeClaim in slice order; quick accept when it has

@@ -254,3 +254,14 @@ def fuzz_consolidation(catalog, seed, n_nodes=40, n_pods=200, n_candidates=None,
         cands.append(model.Candidate(node=int(j), pods=np.nonzero(owner == i)[0].astype(np.int32), price=price,
                                      capacity_type=ct, instance_type=t, nodepool=npool, capacity=cap))
     return model.ConsolidationProblem(prob, cands, np.nonzero(owner < 0)[0].astype(np.int32), init)
+
+
+def fuzz_topology_existing_problem(catalog, seed, n_pods=200, n_classes=10, n_existing=24, n_bound=40):
+    """fuzz_topology_problem over a cluster: existing nodes (labels with zone / capacity-type / team, partial
+    headroom, taints) and pods of the classes already bound to them, whose topology terms count (countDomains) and
+    whose required anti-affinity blocks their nodes' domains (updateInverseAffinities)."""
+    prob = fuzz_problem(catalog, seed, n_pods=n_pods, n_classes=n_classes, n_existing=n_existing)
+    rng = np.random.Generator(np.random.PCG64(seed + 7))
+    prob = add_topology(rng, prob)
+    prob.bound = [(int(rng.integers(0, n_existing)), int(rng.integers(0, n_classes))) for _ in range(n_bound)]
+    return prob

@@ -129,3 +129,35 @@ def test_config3_full_digest(ctx, golden):
     prob = synth.config3(catalog=golden, n_pods=want["n_pods"])
     got = parity.result_digest(parity.run_device(ctx, prob))
     assert got == {k: v for k, v in want.items() if k != "n_pods"}
+
+
+def test_bound_pods_zonal_spread(ctx, golden):
+    """countDomains: two bound pods in test-zone-1a push the pending pods to 1b and 1c (test_topology_cpu's case)."""
+    r, q = same(ctx, TC._bound_zone_problem(golden, 4))
+    assert r.n_nodeclaims == 2 and list(r.nodeclaim_n_pods) == [2, 2]
+
+
+def test_existing_nodes_hostname_anti_affinity(ctx, golden):
+    """Existing nodes with room: a hostname self-anti-affinity deployment takes one pod per existing node (bound pods of
+    the class block their nodes), then one NodeClaim per remaining pod."""
+    lab = {"app": "spread-me"}
+    pc, pods = TC.deployment(8, lab, [model.TopologyTerm("anti", model.HOSTNAME, TC.sel(lab))])
+    it = golden[0]
+    nodes = []
+    for j in range(4):
+        labels = synth.node_labels(it, "test-zone-1%s" % "abc"[j % 3], "on-demand", "default")
+        nodes.append(model.ExistingNode("node-%d" % j, labels, np.array(it.allocatable, np.int64)))
+    prob = model.Problem(golden, [synth.default_nodepool()], [pc], pods, nodes, bound=[(1, 0)])
+    r, _ = same(ctx, prob)
+    assert sorted(int(x) for x in r.pod_result if x < -1) == [-5, -4, -2]   # nodes 0, 2, 3 (node 1 holds one already)
+    assert r.n_nodeclaims == 5
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_fuzz_topology_existing(ctx, golden, seed):
+    """Topology terms over a cluster: existing nodes (placement order, headroom, taints, team labels, hostname /
+    team requirements on the pods) and bound pods (countDomains, inverse anti-affinity), bit-exact with the oracle."""
+    rng = np.random.Generator(np.random.PCG64(seed + 1000))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=160, replace=False))]
+    same(ctx, fuzzgen.fuzz_topology_existing_problem(sub, seed, n_pods=int(rng.integers(50, 300)),
+                                                     n_existing=int(rng.integers(4, 40))))
