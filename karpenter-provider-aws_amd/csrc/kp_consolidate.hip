@@ -40,6 +40,12 @@ __device__ __forceinline__ int32_t ld32(const int32_t* p) {
 __device__ __forceinline__ uint64_t ld64u(const uint64_t* p) {
     return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Wave-uniform values read from LDS: the compiler cannot prove them uniform, and a branch on them would make the
+// pod loop's control flow divergent (exec-mask save/restore around every chunk test); readfirstlane keeps them scalar.
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+}
 __device__ __forceinline__ double wave_min_f64(double x) {
     for (int o = 32; o >= 1; o >>= 1) {
         const double y = __shfl_xor(x, o);
@@ -334,6 +340,15 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
         bool bad = false, stop = false;
         uint64_t nc_opts = 0;
         while (count > 0) {
+            // loop-carried wave-uniform state: re-asserted scalar each pod, so the chunk tests below branch on SGPRs
+            head = __builtin_amdgcn_readfirstlane(head);
+            count = __builtin_amdgcn_readfirstlane(count);
+            wbase = __builtin_amdgcn_readfirstlane(wbase);
+            xstart = __builtin_amdgcn_readfirstlane(xstart);
+            cbase = __builtin_amdgcn_readfirstlane(cbase);
+            ccls = __builtin_amdgcn_readfirstlane(ccls);
+            prev_shape = __builtin_amdgcn_readfirstlane(prev_shape);
+            cx = uni64(cx);
             if (head - wbase >= 64) win_load(head);
             const int off = head - wbase;
             const int ent = rl32(vpod, off);
@@ -360,7 +375,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             // placement stays in registers (effective headroom and this probe's added requests per lane)
             int jf = -1;
             const long long cs0 = prof ? __builtin_amdgcn_s_memtime() : 0;
-            for (int base = xstart & ~63; base < E; base += 64) {
+            for (int base = __builtin_amdgcn_readfirstlane(xstart & ~63); base < E; base += 64) {
                 const int w = base >> 6;
                 const int j = base + lane;
                 const uint64_t ge = xstart > base ? (~0ull << (xstart - base)) : ~0ull;
@@ -369,7 +384,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 if (base == cbase) {
                     st_hits++;
                     if (ccls != c) {
-                        cx = (d.C <= KP_CONS_XTC) ? xtc[c] : (d.XT[(size_t)c * EW + w] & ~excl[w]);
+                        cx = uni64((d.C <= KP_CONS_XTC) ? xtc[c] : (d.XT[(size_t)c * EW + w] & ~excl[w]));
                         ccls = c;
                     }
                     xw = cx;
@@ -379,13 +394,13 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                         dl[ai] = cd[ai];
                     }
                 } else {
-                    xw = d.XT[(size_t)c * EW + w] & ~excl[w];
+                    xw = uni64(d.XT[(size_t)c * EW + w] & ~excl[w]);
                     if (!(xw & ge)) {
                         st_nodes += 64;
                         continue;
                     }
                     st_loads++;
-                    const uint64_t mw = modb[w];
+                    const uint64_t mw = uni64(modb[w]);
                     if (mw & xw) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this probe's delta stores landed
                     const bool md = (mw >> lane) & 1ull;
 #pragma unroll
@@ -406,7 +421,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 st_nodes += 64;
                 const uint64_t m = ballot(cand);
                 if (m) {
-                    jf = base + __ffsll((unsigned long long)m) - 1;
+                    jf = __builtin_amdgcn_readfirstlane(base + __ffsll((unsigned long long)m) - 1);
                     if (base != cbase) {
                         // evict: this probe's requests on the old chunk go to the delta slab (read back past L1)
                         if (cbase >= 0 && ((modb[cbase >> 6] >> lane) & 1ull)) {
@@ -445,7 +460,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 xstart = jf;
                 st_placed++;
                 if (!pend) {
-                    if ((initb[jf >> 6] >> (jf & 63)) & 1ull) ok_np++;
+                    if ((uni64(initb[jf >> 6]) >> (jf & 63)) & 1ull) ok_np++;
                     else bad = true;  // SimulateScheduling: uninitialized-node placement is an error
                 }
                 continue;

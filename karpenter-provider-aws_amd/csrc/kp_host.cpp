@@ -2368,6 +2368,8 @@ static kp_status cons_prepare_one(kp_ctx* ctx, const kp_consolidate_input* in) t
     if (!c->pref.relax_next.empty())
         return fail(ctx, KP_E_UNSUPPORTED, "consolidation over pods with preferences to relax is not supported by this build");
     if (c->best_effort) return fail(ctx, KP_E_UNSUPPORTED, "consolidation with MIN_VALUES_POLICY=BestEffort is not supported by this build");
+    if (c->tg_G > 0)  // the probe kernel has no domain counters (each probe would need its own copy)
+        return fail(ctx, KP_E_UNSUPPORTED, "consolidation over pods with topology spread / pod (anti-)affinity is not supported by this build");
     const KpDev& d = c->dev;
     // minValues NodePools: the probe kernel counts distinct values of single-valued catalog keys only
     if (c->min_multi)
