@@ -32,6 +32,7 @@ struct ConsShared {
     Roles roles;
     int64_t nc_req[KP_MAX_R];
     int64_t st[CS_COUNT];
+    int32_t rcap[64];  // RESV: the probe's ReservationManager capacities (NewReservationManager per SimulateScheduling)
 };
 
 __device__ __forceinline__ int32_t ld32(const int32_t* p) {
@@ -75,9 +76,17 @@ __device__ inline uint64_t limit_filter_rem(const KpDev& d, int j, uint64_t o, c
     return out;
 }
 
-// Offerings.Available().WorstLaunchPrice(reqs) over the admissible slots m of type t: reserved (none in this build's
-// catalogs), then spot, then on-demand; the most expensive offering of the first capacity type present.
-__device__ inline double worst_launch_price(const KpDev& d, const KpCons& k, int t, uint64_t m) {
+// Offerings.Available().WorstLaunchPrice(reqs) over the admissible slots m and reserved offerings rm (ResvTab rows) of
+// type t: reserved, then spot, then on-demand; the most expensive offering of the first capacity type present.
+__device__ inline double worst_launch_price(const KpDev& d, const KpCons& k, int t, uint64_t m, uint64_t rm = 0) {
+    if (rm) {
+        double mx = 0.0;
+        for (uint64_t x = rm; x; x &= x - 1) {
+            const double p = d.ro_price[__ffsll((unsigned long long)x) - 1];
+            mx = p > mx ? p : mx;
+        }
+        return mx;
+    }
     const uint64_t ms = m & k.spot_slots;
     uint64_t mm = ms ? ms : (m & k.od_slots);
     if (!mm) return DBL_MAX;
@@ -136,9 +145,24 @@ __device__ inline bool min_values_ok(const KpDev& d, const ReqHdr* nch, int j, i
 
 }  // namespace
 
+// NodeClaim.Add's commit of offeringsToReserve (fallback mode): newly held IDs take one unit of capacity, IDs no longer
+// held are released (ReservationManager.Reserve / Release).  Returns the new held set.
+__device__ inline uint64_t commit_held(int32_t* rcap, uint64_t old, uint64_t nw, int lane) {
+    if (lane < 64) {
+        const uint64_t b = 1ull << lane;
+        if ((nw & b) && !(old & b)) rcap[lane]--;
+        if ((old & b) && !(nw & b)) rcap[lane]++;
+    }
+    return nw;
+}
+
 // FULL = false: the fast variant handles probes whose pods all fit existing nodes (no NodeClaim code, a small register
 // footprint); a probe that needs a NodeClaim is handed to the FULL variant through k.retry.
-template <bool FULL>
+// RESV (FULL only): the catalog has reserved offerings — NodeClaim.Add runs the reservation step in
+// ReservedOfferingModeFallback (SimulateScheduling never fails an Add for want of a reservation), the in-flight
+// NodeClaim's held IDs take / release the probe's capacities, FinalizeScheduling adds reservation-id In [held], and
+// OrderByPrice / WorstLaunchPrice see the reserved offerings.
+template <bool FULL, bool RESV = false>
 __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     ConsShared& S = *reinterpret_cast<ConsShared*>(smem);
@@ -183,10 +207,10 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             if (d.min_keys[(size_t)j * KP_MAX_CLASS_KEYS] >= 0) mmask |= 1u << j;
         Ev.min_tmpl_mask = mmask;
     }
-    Ev.ro = nullptr;       // catalogs with reserved offerings are rejected by kp_consolidate
-    Ev.type_ro = nullptr;
-    Ev.rcap = nullptr;
-    Ev.resv_on = 0;
+    Ev.ro = RESV ? d.ro : nullptr;
+    Ev.type_ro = RESV ? d.type_ro : nullptr;
+    Ev.rcap = RESV ? S.rcap : nullptr;
+    Ev.resv_on = RESV ? d.resv_on : 0;  // disruption simulations: ReservedOfferingModeFallback (STRICT = false below)
 
     for (int it = 0;; it++) {
         int probe = 0;
@@ -218,6 +242,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             modb[w] = 0;
         }
         for (int i = lane; i < NT * R; i += 64) rem[i] = d.remaining[i];
+        if (RESV) S.rcap[lane] = d.rcap0[lane];
         __syncthreads();
         for (int c = c0 + lane; c < c1; c += 64) {
             const int node = k.cand_i[c * 4 + 0];
@@ -339,6 +364,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
         for (int ai = 0; ai < KP_LDS_AXES; ai++) ch[ai] = cd[ai] = 0;
         bool bad = false, stop = false;
         uint64_t nc_opts = 0;
+        uint64_t nc_held = 0;  // RESV: reservation IDs the in-flight NodeClaim holds
         while (count > 0) {
             // loop-carried wave-uniform state: re-asserted scalar each pod, so the chunk tests below branch on SGPRs
             head = __builtin_amdgcn_readfirstlane(head);
@@ -486,9 +512,9 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 a.force_off = false;
                 a.prof = nullptr;
                 a.host = 0;
-                a.held = 0;
+                a.held = nc_held;
                 st_nc++;
-                if (eval_wave<false>(d, Ev, S.CC, a, S.ws, lane)) {
+                if (eval_wave<false, RESV, false>(d, Ev, S.CC, a, S.ws, lane)) {
                     if (lane < S.CC.nck) {
                         const int kk = S.CC.key[lane];
                         nch[kk] = S.ws.hdr[lane];
@@ -496,6 +522,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     }
                     if (lane < TW) nc_opts = S.ws.opts[lane];
                     if (lane < R) S.nc_req[lane] += preq[lane];
+                    if (RESV && d.resv_on) nc_held = commit_held(S.rcap, nc_held, S.ws.held, lane);
                     __syncthreads();
                     placed = true;
                 }
@@ -519,7 +546,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     a.host = 0;
                     a.held = 0;
                     st_tmpl++;
-                    if (!eval_wave<false>(d, Ev, S.CC, a, S.ws, lane)) continue;
+                    if (!eval_wave<false, RESV, false>(d, Ev, S.CC, a, S.ws, lane)) continue;
                     if (n_nc == 1) {  // a second NodeClaim: computeConsolidation returns NONE
                         stop = true;
                         break;
@@ -534,6 +561,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     }
                     nc_opts = lane < TW ? S.ws.opts[lane] : 0;
                     if (lane < R) S.nc_req[lane] = d.daemon[(size_t)j * R + lane] + preq[lane];
+                    if (RESV && d.resv_on) nc_held = commit_held(S.rcap, 0ull, S.ws.held, lane);
                     // subtractMax(remaining, nodeClaim.InstanceTypeOptions)
                     for (int r = 0; r < R; r++) {
                         if (!d.limit_set[(size_t)j * R + r]) continue;
@@ -598,6 +626,16 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             decision = KP_DECISION_DELETE;
             valid = 1;
         } else if (FULL && all) {
+            // FinalizeScheduling: a NodeClaim holding reservations gets reservation-id In [held IDs]
+            if (RESV && nc_held && d.key_resvid >= 0) {
+                if (lane == 0) {
+                    ReqHdr h{};
+                    h.flags = RF_DEF;
+                    nch[d.key_resvid] = h;
+                }
+                for (int i = lane; i < d.nw[d.key_resvid]; i += 64) ncw[d.woff[d.key_resvid] + i] = i == 0 ? nc_held : 0ull;
+                __syncthreads();
+            }
             // Offerings.Available().Compatible(NodeClaim requirements) over zone × capacity-type slots
             bool okslot = false;
             if (lane < d.n_slots) {
@@ -618,6 +656,32 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                          dneok(d.key_resvtype);
             }
             const uint64_t mzc = ballot(okslot);
+            // ... and over the reserved offerings (capacity-type In [reserved], zone, zone-id, reservation id / type)
+            uint64_t mro = 0;
+            if (RESV) {
+                bool ok = false;
+                if (lane < d.ro->n && ((d.ro->avail >> lane) & 1ull)) {
+                    auto adm = [&](int kk, int v) -> bool {
+                        if (kk < 0) return true;
+                        const ReqHdr h = nch[kk];
+                        if (!(h.flags & RF_DEF)) return true;
+                        return req_has(d, kk, v, h, ncw + d.woff[kk]);
+                    };
+                    const int zid = d.ro->zid[lane], rt = d.ro->rtype[lane];
+                    bool rtok;
+                    if (rt >= 0) {
+                        rtok = adm(d.key_resvtype, rt);
+                    } else {
+                        const int kk = d.key_resvtype;
+                        const ReqHdr h = kk >= 0 ? nch[kk] : ReqHdr{};
+                        rtok = kk < 0 || !(h.flags & RF_DEF) ||
+                               op_notin_or_dne(req_op(h.flags, popc_words(ncw + d.woff[kk], d.nw[kk])));
+                    }
+                    ok = adm(d.key_ct, d.ro->ctv) && adm(d.key_zone, d.ro->zone[lane]) && (zid < 0 || adm(d.key_zoneid, zid)) &&
+                         adm(d.key_resvid, d.ro->rid[lane]) && rtok;
+                }
+                mro = ballot(ok);
+            }
             // OrderByPrice(reqs) + Truncate(M): select the M cheapest options by (price, name)
             double pr[KP_TW_MAX];
             uint32_t rk[KP_TW_MAX];
@@ -640,6 +704,11 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                             const double sp = d.slot_price[(size_t)t * KP_MAX_SLOTS + s];
                             price = sp < price ? sp : price;
                         }
+                        if (RESV)
+                            for (uint64_t x = d.type_ro[t] & mro; x; x &= x - 1) {
+                                const double rp = d.ro_price[__ffsll((unsigned long long)x) - 1];
+                                price = rp < price ? rp : price;
+                            }
                         pr[w] = price;
                         rk[w] = d.name_rank[t];
                         present |= 1u << w;
@@ -693,6 +762,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             };
             const bool has_spot = ct_has(k.v_spot), has_od = ct_has(k.v_od);
             const uint64_t mt = my_t >= 0 ? d.avail_zc[my_t] & mzc : 0;
+            const uint64_t mr = (RESV && my_t >= 0) ? d.type_ro[my_t] & mro : 0ull;  // the option's reserved offerings
             bool keep = false, none = false, spot_only = false;
             if (!trunc_ok) {
                 // the dropped NodeClaim's pods get errors: if one of them is not pending, not all non-pending pods
@@ -719,7 +789,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     }
                 }
             } else {  // RemoveInstanceTypeOptionsByPriceAndMinValues
-                keep = my_t >= 0 && worst_launch_price(d, k, my_t, mt) < cprice;
+                keep = my_t >= 0 && worst_launch_price(d, k, my_t, mt, mr) < cprice;
                 const uint64_t km = ballot(keep);
                 if (!km || (has_min && !min_values_ok(d, nch, nc_tmpl, my_t, km, lane, nullptr))) none = true;
                 spot_only = has_spot && has_od;  // spot/on-demand flexible replacement narrowed to spot
@@ -729,8 +799,8 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 valid = 1;
             } else if (!none) {
                 decision = KP_DECISION_REPLACE;
-                const uint64_t mr = spot_only ? (mt & k.spot_slots) : mt;
-                const double wl = keep ? worst_launch_price(d, k, my_t, mr) : DBL_MAX;
+                const uint64_t ms = spot_only ? (mt & k.spot_slots) : mt;
+                const double wl = keep ? worst_launch_price(d, k, my_t, ms, spot_only ? 0ull : mr) : DBL_MAX;
                 if (!single) {  // filterOutSameInstanceType
                     double mp = DBL_MAX;
                     if (keep)
@@ -825,13 +895,19 @@ hipError_t kp_cons_set_attributes() {
     if (e == hipSuccess)
         e = hipFuncSetAttribute((const void*)consolidate_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 KP_LDS_BYTES);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void*)consolidate_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                KP_LDS_BYTES);
     return e;
 }
 
 hipError_t kp_launch_consolidate(const KpDev& d, const KpCons& k, int n_workers, hipStream_t s) {
     if (n_workers <= 0 || k.n_probes <= 0) return hipSuccess;
     if (k.no_fast != 1) hipLaunchKernelGGL(consolidate_kernel<false>, dim3(n_workers), dim3(64), (size_t)k.lds_bytes, s, d, k);
-    if (k.no_fast != 2) hipLaunchKernelGGL(consolidate_kernel<true>, dim3(n_workers), dim3(64), (size_t)k.lds_bytes, s, d, k);
+    if (k.no_fast != 2) {
+        if (d.ro) hipLaunchKernelGGL((consolidate_kernel<true, true>), dim3(n_workers), dim3(64), (size_t)k.lds_bytes, s, d, k);
+        else hipLaunchKernelGGL(consolidate_kernel<true>, dim3(n_workers), dim3(64), (size_t)k.lds_bytes, s, d, k);
+    }
     return hipGetLastError();
 }
 

@@ -106,7 +106,7 @@ struct EvalEnv {
     const ResvTab* ro;         // reserved offerings (null: none)
     const uint64_t* type_ro;   // [T] the type's reserved offerings (bits over ro index)
     const int32_t* rcap;       // ReservationManager capacity by reservation-id value id (FFD kernel LDS)
-    int resv_on;               // run the reservation step of NodeClaim.Add (ReservedOfferingModeStrict)
+    int resv_on;               // run the reservation step of NodeClaim.Add
 };
 
 // Cooperative fill by all threads of the block; contains two __syncthreads().
@@ -515,7 +515,7 @@ __device__ __forceinline__ void topo_record(const KpDev& d, const ClassCache& CC
 // the node's requirements (no undefined-label allowance), then Topology.AddRequirements with the node's own domains
 // (hostname = the node's name: host row j).  On success ws holds the merged class keys.
 template <bool CONS>
-__device__ inline bool existing_topo_try(const KpDev& d, const ClassCache& CC, WaveScratch& ws, int j, int lane) {
+__device__ __attribute__((noinline)) bool existing_topo_try(const KpDev& d, const ClassCache& CC, WaveScratch& ws, int j, int lane) {
     const ReqHdr* nh = d.ex_hdr + (size_t)j * d.K;
     const uint64_t* nwp = d.ex_words + (size_t)j * d.DW;
     if (lane < CC.nck) {
@@ -542,7 +542,7 @@ __device__ inline bool existing_topo_try(const KpDev& d, const ClassCache& CC, W
 
 // Commit of existing_topo_try: the node's requirements become the merged ones; when they changed, node j's XT column is
 // recomputed for every class (as existing_merge does).
-__device__ inline void existing_topo_commit(const KpDev& d, const ClassCache& CC, const WaveScratch& ws, int j, int lane) {
+__device__ __attribute__((noinline)) void existing_topo_commit(const KpDev& d, const ClassCache& CC, const WaveScratch& ws, int j, int lane) {
     ReqHdr* nh = d.ex_hdr + (size_t)j * d.K;
     uint64_t* nwp = d.ex_words + (size_t)j * d.DW;
     bool ch = false;
@@ -586,7 +586,9 @@ __device__ inline void existing_topo_commit(const KpDev& d, const ClassCache& CC
 // and the type sweep, and keys carried only for narrowing (kneutral) merge as the base requirement.  RESV: the catalog
 // has reserved offerings (offering compatibility over them, and the reservation step when E.resv_on).  The
 // instantiations keep the topology and reservation code out of the common path.
-template <bool TOPO, bool RESV = false>
+// STRICT: ReservedOfferingModeStrict (provisioning); false: Fallback (disruption simulations never fail an Add for want
+// of a reservation).
+template <bool TOPO, bool RESV = false, bool STRICT = true>
 __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, const ClassCache& CC, const EvalIn& a,
                                           WaveScratch& ws, int lane) {
     const int TW = d.TW, T = d.T;
@@ -808,7 +810,7 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         const int rid = lane < X.n ? X.rid[lane] : 0;
         const bool res = comp && (((a.held >> rid) & 1ull) || E.rcap[rid] > 0);
         const uint64_t cm = ballot(comp), rm = ballot(res);
-        if ((cm && !rm) || (a.held && !rm)) return false;
+        if (STRICT && ((cm && !rm) || (a.held && !rm))) return false;
         rlive = cm != 0;
         const uint64_t nh = wave_or64(res ? (1ull << rid) : 0ull);
         if (lane == 0) {

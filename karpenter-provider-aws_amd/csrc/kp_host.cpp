@@ -2337,8 +2337,8 @@ static kp_status cons_prepare_one(kp_ctx* ctx, const kp_consolidate_input* in) t
     if (!ctx || !in) return KP_E_INVALID;
     ctx->cons_prepared = false;
     ctx->cons_prep_valid = false;
-    if (ctx->has_reserved)
-        return fail(ctx, KP_E_UNSUPPORTED, "consolidation over a catalog with reserved offerings is not supported by this build");
+    if (ctx->has_reserved && !ctx->ro_ok)
+        return fail(ctx, KP_E_UNSUPPORTED, "consolidation over a catalog with more than 64 reserved offerings");
     if (!ctx->solve_unsupported.empty()) return fail(ctx, KP_E_UNSUPPORTED, "consolidation: " + ctx->solve_unsupported);
     if (in->mode != KP_CONSOLIDATE_SINGLE && in->mode != KP_CONSOLIDATE_MULTI)
         return fail(ctx, KP_E_INVALID, "unknown consolidation mode");

@@ -539,7 +539,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
     E.ro = sRo;
     E.type_ro = d.type_ro;
     E.rcap = sRcap;
-    E.resv_on = RESV ? d.resv_on : 0;
+    E.resv_on = RESV ? d.resv_on : 0;  // provisioning: ReservedOfferingModeStrict (eval_wave's STRICT default)
     {
         uint32_t mmask = 0;
         for (int j = 0; j < d.NT; j++)

@@ -140,3 +140,72 @@ def test_multi_device_state_errors(golden):
         assert e.value.status == abi.KP_E_STATE
     finally:
         multi.close()
+
+
+def _reserved_consolidation(golden, seed, full_cluster=False):
+    """fuzz_consolidation over a catalog with reserved offerings (config5_catalog on the subsample: ODCR default and
+    capacity-block reservations of capacity 1-20, some expiring) and NodePools that admit capacity-type reserved."""
+    rng = np.random.Generator(np.random.PCG64(1300 + seed))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(80, 240)), replace=False))]
+    cat = synth.config5_catalog(sub, n_default=min(44, len(sub) // 2), n_block=min(20, len(sub) // 6), seed=1300 + seed)
+    cp = fuzzgen.fuzz_consolidation(cat, 1300 + seed, n_nodes=int(rng.integers(4, 60)),
+                                    n_pods=int(rng.integers(20, 250)), all_spot=seed % 4 == 0, supported=True,
+                                    pending_frac=0.0 if full_cluster else 0.15)
+    for np_ in cp.cluster.nodepools:
+        for r in np_.requirements:
+            if r.key == model.CAPACITY_TYPE and r.op == "In" and rng.random() < 0.8:
+                r.values = sorted(set(r.values) | {"reserved"})
+    if full_cluster:  # no headroom anywhere: every probe's pods need a new NodeClaim (REPLACE / NONE decisions)
+        for n in cp.cluster.existing:
+            n.available = np.minimum(n.available, 0)
+    return cp
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_fuzz_consolidation_reserved(ctx, golden, seed):
+    """Reserved offerings in the probes (ReservedOfferingModeFallback): NodeClaim.Add reserves compatible reserved
+    offerings while the probe's capacities last but never fails for want of one, FinalizeScheduling's reservation-id
+    requirement, reserved prices in OrderByPrice and first in WorstLaunchPrice — against the oracle."""
+    cp = _reserved_consolidation(golden, seed, full_cluster=seed % 2 == 0)
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        s2s = seed % 2 == 1
+        assert_probes_equal(device_probes(ctx, cp, mode, s2s), pyoracle.consolidate(cp, mode, spot_to_spot=s2s))
+
+
+def _reserved_replace_case(golden, rcap, expiring=False, n_cands=1, ct="on-demand"):
+    """One NodePool admitting on-demand + reserved, a catalog whose reserved offerings have capacity rcap, candidates
+    each carrying one small pod on otherwise full nodes: the probe's NodeClaim reserves while capacity lasts."""
+    cat = synth.config5_catalog(golden[:120], n_default=60, n_block=0, seed=3, expiring_frac=1.0 if expiring else 0.0)
+    for it in cat:
+        for o in it.offerings:
+            if o.capacity_type == "reserved":
+                o.reservation_capacity = rcap
+                o.available = o.available and rcap != 0
+    np_ = synth.default_nodepool()
+    np_.requirements = [model.Requirement(model.CAPACITY_TYPE, "In", ["on-demand", "reserved"])]
+    pods = synth.pods_from_specs([(0, {"cpu": "100m", "memory": "128Mi"})] * n_cands)
+    nodes = []
+    for j in range(n_cands):
+        it = cat[j]
+        nodes.append(model.ExistingNode("node-%d" % j, synth.node_labels(it, "test-zone-1a", ct, "default"),
+                                        np.zeros(model.R, np.int64)))
+    prob = model.Problem(cat, [np_], [model.PodClass()], pods, nodes)
+    cands = [model.Candidate(node=j, pods=np.array([j], np.int32), price=5.0,
+                             capacity_type=abi.KP_CT_SPOT if ct == "spot" else abi.KP_CT_ON_DEMAND, instance_type=j,
+                             nodepool=0, capacity=None) for j in range(n_cands)]
+    return model.ConsolidationProblem(prob, cands, np.zeros(0, np.int32), np.ones(n_cands, np.uint8))
+
+
+@pytest.mark.parametrize("rcap,expiring", [(3, False), (1, False), (0, False), (5, True)])
+def test_reserved_replacement(ctx, golden, rcap, expiring):
+    """A REPLACE onto reserved capacity is priced at odPrice / 1e7 (offering.go:176) and is WorstLaunchPrice's first
+    choice; with no capacity (or expiring reservations) the probe falls back to on-demand."""
+    cp = _reserved_replace_case(golden, rcap, expiring, n_cands=3)
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        dev = device_probes(ctx, cp, mode)
+        assert_probes_equal(dev, pyoracle.consolidate(cp, mode))
+        assert (dev["decision"] == abi.KP_DECISION_REPLACE).all()
+        if rcap > 0 and not expiring:
+            assert (dev["replacement_price"] < 1e-6).all()
+        else:
+            assert (dev["replacement_price"] > 1e-6).all()

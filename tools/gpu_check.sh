@@ -8,7 +8,7 @@ rc=$?
 tail -3 gpurun_out/t.log
 [ $rc -ne 0 ] && { grep -E "Error|error|assert" gpurun_out/t.log | head -20; exit $rc; }
 timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/b.json 2> gpurun_out/b.err || exit $?
-KPSIM_PROFILE=1 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 1 --warmup 0 > gpurun_out/bp.json 2>&1 || exit $?
+KPSIM_PROFILE=1 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 1 --warmup 0 > gpurun_out/bp.json 2> gpurun_out/bp.err || exit $?
 python3 - <<'PY'
 import json
 for f in ["gpurun_out/b.json", "gpurun_out/bp.json"]:
