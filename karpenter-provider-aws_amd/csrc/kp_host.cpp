@@ -96,6 +96,20 @@ bool well_known(const std::string& k) {
     return false;
 }
 // karpv1.NormalizedLabels + topology.ebs.csi.aws.com/zone (pkg/operator/operator.go:71)
+// normalize without a std::string temporary (launch-request encoding)
+const char* normalize_c(const char* k) {
+    static const std::pair<const char*, const char*> m[] = {
+        {"failure-domain.beta.kubernetes.io/zone", "topology.kubernetes.io/zone"},
+        {"failure-domain.beta.kubernetes.io/region", "topology.kubernetes.io/region"},
+        {"beta.kubernetes.io/arch", "kubernetes.io/arch"},
+        {"beta.kubernetes.io/os", "kubernetes.io/os"},
+        {"beta.kubernetes.io/instance-type", "node.kubernetes.io/instance-type"},
+        {"topology.ebs.csi.aws.com/zone", "topology.kubernetes.io/zone"},
+    };
+    for (auto& p : m)
+        if (!strcmp(k, p.first)) return p.second;
+    return k;
+}
 std::string normalize(const char* k) {
     static const std::pair<const char*, const char*> m[] = {
         {"failure-domain.beta.kubernetes.io/zone", "topology.kubernetes.io/zone"},
@@ -171,6 +185,27 @@ struct Dicts {
     int find_key(const std::string& k) const {
         auto it = kid.find(k);
         return it == kid.end() ? -1 : it->second;
+    }
+    // FNV index over the key names for C-string lookups (launch-request encoding); rebuilt by freeze_keys()
+    std::vector<int32_t> kslots;
+    void freeze_keys() {
+        size_t cap = 16;
+        while (cap < keys.size() * 2) cap <<= 1;
+        kslots.assign(cap, -1);
+        for (int i = 0; i < (int)keys.size(); i++) {
+            size_t h = KeyDict::hash(keys[i].name.c_str()) & (cap - 1);
+            while (kslots[h] >= 0) h = (h + 1) & (cap - 1);
+            kslots[h] = i;
+        }
+    }
+    int find_key_fast(const char* k) const {
+        if (kslots.empty() || kslots.size() < keys.size() * 2) return find_key(k);
+        const size_t mask = kslots.size() - 1;
+        for (size_t h = KeyDict::hash(k) & mask;; h = (h + 1) & mask) {
+            const int i = kslots[h];
+            if (i < 0) return -1;
+            if (!strcmp(keys[i].name.c_str(), k)) return i;
+        }
     }
 };
 
@@ -876,6 +911,7 @@ static kp_status catalog_upload_one(kp_ctx* ctx, const kp_catalog_view* v, uint6
     HIPCHK(hipStreamSynchronize(s));
     c->epoch = epoch;
     for (auto& kd : c->cat.keys) kd.freeze();  // the catalog dictionaries are complete: index them for lookups
+    c->cat.freeze_keys();
     c->have_catalog = true;
     c->prepared = c->executed = false;
     c->cons_prepared = false;
@@ -2812,7 +2848,7 @@ SReq sreq_intersection(const SReq& a, const SReq& b) {
 // dictionary of key kc knows (sorted), `unk` the others (kept by name only — they decide whether a set is empty).
 struct IReq {
     int kc = -1;          // catalog key, -1 when no type or offering carries it
-    std::string name;     // normalised key
+    const char* name = "";  // normalised key (the request's string or a static alias target)
     bool comp = false;
     std::vector<int> ids;
     std::vector<std::string> unk;
@@ -2835,11 +2871,15 @@ bool ireq_within(const IReq& q, const std::string& v) {
     if (q.has_lt && q.lt <= x) return false;
     return true;
 }
-IReq ireq_new(const kp_ctx* c, const kp_requirement& r) {
-    IReq q;
-    q.name = normalize(r.key);
-    q.kc = c->cat.find_key(q.name);
+// fills q in place (its vectors keep their capacity across requests)
+void ireq_fill(const kp_ctx* c, const kp_requirement& r, IReq& q) {
+    q.name = normalize_c(r.key);
+    q.kc = c->cat.find_key_fast(q.name);
     q.comp = !(r.op == KP_OP_IN || r.op == KP_OP_DOES_NOT_EXIST);
+    q.ids.clear();
+    q.unk.clear();
+    q.has_gt = q.has_lt = false;
+    q.gt = q.lt = 0;
     if (r.op == KP_OP_IN || r.op == KP_OP_NOT_IN) {
         const KeyDict* kd = q.kc >= 0 ? &c->cat.keys[q.kc] : nullptr;
         q.ids.reserve(r.n_values);
@@ -2862,7 +2902,6 @@ IReq ireq_new(const kp_ctx* c, const kp_requirement& r) {
     }
     q.has_min = r.min_values >= 0;
     q.minv = r.min_values;
-    return q;
 }
 template <class V>
 V set_op(const V& a, const V& b, int how) {  // 0 union, 1 a \ b, 2 a ∩ b (sorted inputs)
@@ -2975,19 +3014,28 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
         if (lr.n_requirements < 0 || (lr.n_requirements > 0 && !lr.requirements)) return err(KP_E_INVALID, "bad request");
         // NewNodeSelectorRequirementsWithMinValues: Add = intersect per key, in catalog value-id space (values no type
         // or offering carries are kept by name only: they decide whether a set is empty)
-        std::vector<IReq>& m = ch.scratch;
-        m.clear();
+        // ch.scratch holds reusable IReq slots: the first nm are this request's merged requirements
+        std::vector<IReq>& slots = ch.scratch;
+        size_t nm = 0;
         for (int j = 0; j < lr.n_requirements; j++) {
             const kp_requirement& r = lr.requirements[j];
             if (!r.key || r.op < 0 || r.op > 5) return err(KP_E_INVALID, "bad requirement");
-            IReq q = ireq_new(c, r);
+            if (nm == slots.size()) slots.emplace_back();
+            IReq& q = slots[nm];
+            ireq_fill(c, r, q);
             IReq* hit = nullptr;
-            for (IReq& x : m)
-                if (x.kc == q.kc && (q.kc >= 0 || x.name == q.name)) hit = &x;
+            for (size_t x = 0; x < nm; x++)
+                if (slots[x].kc == q.kc && (q.kc >= 0 || !strcmp(slots[x].name, q.name))) hit = &slots[x];
             if (hit) *hit = ireq_intersection(c, q, *hit);
-            else m.push_back(std::move(q));
+            else nm++;
         }
-        std::sort(m.begin(), m.end(), [](const IReq& a, const IReq& b) { return a.name < b.name; });
+        std::sort(slots.begin(), slots.begin() + nm, [](const IReq& a, const IReq& b) { return strcmp(a.name, b.name) < 0; });
+        struct View {  // the merged requirements of this request
+            const IReq* b;
+            const IReq* e;
+            const IReq* begin() const { return b; }
+            const IReq* end() const { return e; }
+        } m{slots.data(), slots.data() + nm};
         if (lr.requests)
             for (int r = 0; r < R; r++) rq[(size_t)i * R + r] = lr.requests[r];
         KlReq& q = reqs[i];
@@ -3050,7 +3098,7 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
         }
         const IReq* ct = nullptr;
         for (const IReq& x : m)
-            if (x.name == "karpenter.sh/capacity-type") ct = &x;
+            if (c->key_ct >= 0 ? x.kc == c->key_ct : !strcmp(x.name, "karpenter.sh/capacity-type")) ct = &x;
         for (int x = 0; x < 3; x++) q.ct_has[x] = ct == nullptr ? 1 : (ireq_has(c, *ct, c->ct_vid[x], kCtNames[x]) ? 1 : 0);
         q.min_off = (int)mins.size();
         for (const IReq& sq : m) {
