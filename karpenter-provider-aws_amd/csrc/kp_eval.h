@@ -515,7 +515,7 @@ __device__ __forceinline__ void topo_record(const KpDev& d, const ClassCache& CC
 // the node's requirements (no undefined-label allowance), then Topology.AddRequirements with the node's own domains
 // (hostname = the node's name: host row j).  On success ws holds the merged class keys.
 template <bool CONS>
-__device__ __attribute__((noinline)) bool existing_topo_try(const KpDev& d, const ClassCache& CC, WaveScratch& ws, int j, int lane) {
+__device__ inline bool existing_topo_try(const KpDev& d, const ClassCache& CC, WaveScratch& ws, int j, int lane) {
     const ReqHdr* nh = d.ex_hdr + (size_t)j * d.K;
     const uint64_t* nwp = d.ex_words + (size_t)j * d.DW;
     if (lane < CC.nck) {
@@ -542,7 +542,7 @@ __device__ __attribute__((noinline)) bool existing_topo_try(const KpDev& d, cons
 
 // Commit of existing_topo_try: the node's requirements become the merged ones; when they changed, node j's XT column is
 // recomputed for every class (as existing_merge does).
-__device__ __attribute__((noinline)) void existing_topo_commit(const KpDev& d, const ClassCache& CC, const WaveScratch& ws, int j, int lane) {
+__device__ inline void existing_topo_commit(const KpDev& d, const ClassCache& CC, const WaveScratch& ws, int j, int lane) {
     ReqHdr* nh = d.ex_hdr + (size_t)j * d.K;
     uint64_t* nwp = d.ex_words + (size_t)j * d.DW;
     bool ch = false;
@@ -587,8 +587,8 @@ __device__ __attribute__((noinline)) void existing_topo_commit(const KpDev& d, c
 // has reserved offerings (offering compatibility over them, and the reservation step when E.resv_on).  The
 // instantiations keep the topology and reservation code out of the common path.
 // STRICT: ReservedOfferingModeStrict (provisioning); false: Fallback (disruption simulations never fail an Add for want
-// of a reservation).
-template <bool TOPO, bool RESV = false, bool STRICT = true>
+// of a reservation).  BE: the solve may run MIN_VALUES_POLICY=BestEffort (false compiles the relaxation bookkeeping out).
+template <bool TOPO, bool RESV = false, bool STRICT = true, bool BE = true>
 __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, const ClassCache& CC, const EvalIn& a,
                                           WaveScratch& ws, int lane) {
     const int TW = d.TW, T = d.T;
@@ -603,7 +603,7 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
     int kmul = -1;
     if (lane == 0) {
         ws.memo_ok = 1;
-        ws.n_minrel = 0;
+        if (BE) ws.n_minrel = 0;
     }
     // DoesNotExist-type elimination and the admissible value mask of a multi-valued key, from the merged requirement
     auto classify = [&](int k, const ReqHdr& O, const uint64_t* ow, int cnt) {
@@ -791,7 +791,7 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
                 for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
                 count = c;
             }
-            if (count < h.minv && !min_values_unmet(d, ws, k, count, lane)) return false;
+            if (count < h.minv && !(BE && min_values_unmet(d, ws, k, count, lane))) return false;
         }
     }
     // ---- reservations (NodeClaim.Add's offeringsToReserve, ReservedOfferingModeStrict) ----
@@ -839,10 +839,11 @@ __device__ __forceinline__ void commit_reqs(const KpDev& d, const ClassCache& CC
 // is idempotent (Intersection is idempotent and associative), and its label, DoesNotExist, multi-valued and
 // offering filters are already applied to the options, which only shrink.  What remains is
 // resources.Fits(requests + pod, Allocatable) over the options, then minValues.
+template <bool BE = true>
 __device__ __forceinline__ bool eval_fits_only(const KpDev& d, const EvalEnv& E, const EvalIn& a, WaveScratch& ws,
                                                int lane) {
     const int TW = d.TW, T = d.T;
-    if (lane == 0) ws.n_minrel = 0;
+    if (BE && lane == 0) ws.n_minrel = 0;
     int64_t tot[KP_LDS_AXES];
 #pragma unroll
     for (int ai = 0; ai < KP_LDS_AXES; ai++) {
@@ -912,7 +913,7 @@ __device__ __forceinline__ bool eval_fits_only(const KpDev& d, const EvalEnv& E,
                 for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
                 count = c;
             }
-            if (count < h.minv && !min_values_unmet(d, ws, k, count, lane)) return false;
+            if (count < h.minv && !(BE && min_values_unmet(d, ws, k, count, lane))) return false;
         }
     }
     if (lane < TW) ws.opts[lane] = newword;

@@ -440,7 +440,59 @@ __device__ __forceinline__ void commit_reservations(const KpDev& d, int32_t* rca
 // can resolve alone: a pod whose first non-rejected NodeClaim (slice order) has already absorbed the pod's class
 // and whose witness type still fits is placed without an evaluation (exact: see pick_witness).  Any other pod is
 // handed to all 8 waves (the slow path: NodeClaim.Add of up to 8 candidates at once, or the templates).
-template <bool RESV, bool TOPO>
+// ExistingNode.Add over the existing nodes for a pod of a topology class (wave 0; DESIGN.md §4 "Topology over a
+// cluster"): the first node in scheduling order that is tolerated, Compatible, has headroom and passes
+// Topology.AddRequirements takes the pod; its requirements, the domain counts and its headroom are updated.  Kept out
+// of line: it runs only for clusters, and inlined it would weigh on the topology instantiations' register plan.
+__device__ __attribute__((noinline)) int existing_topo_scan(const KpDev& d, FfdShared& S, int pod, int lane) {
+    const int K = d.K;
+    const int c = S.cur_cls;
+    const bool cons = (d.cls_flags[c] & CF_TOPO_CONS) != 0;
+    int placed = -1;
+    for (int base = 0; base < d.E && placed < 0; base += 64) {
+        const int j = base + lane;
+        bool cand = false;
+        if (j < d.E) {
+            const uint64_t xw = __hip_atomic_load(&d.XT[(size_t)c * d.EW + (j >> 6)], __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+            cand = (xw >> (j & 63)) & 1ull;
+            for (int ai = 0; ai < d.n_active && cand; ai++)
+                cand = S.pod_req[d.active_axes[ai]] <= ld_req(&d.ex_head[(size_t)ai * d.E + j]);
+        }
+        uint64_t m = ballot(cand);
+        while (m) {
+            const int jj = base + __ffsll((unsigned long long)m) - 1;
+            m &= m - 1;
+            const bool ok = cons ? existing_topo_try<true>(d, S.CC, S.ws[0], jj, lane)
+                                 : existing_topo_try<false>(d, S.CC, S.ws[0], jj, lane);
+            if (ok) {
+                placed = jj;
+                break;
+            }
+        }
+    }
+    if (placed >= 0) {
+        existing_topo_commit(d, S.CC, S.ws[0], placed, lane);
+        topo_record(d, S.CC, S.ws[0], d.ex_hdr + (size_t)placed * K, d.ex_words + (size_t)placed * d.DW,
+                    placed, 0, false, lane, placed);
+        if (lane < d.n_active) {
+            const int64_t x = S.pod_req[d.active_axes[lane]];
+            if (x) atomicAdd((unsigned long long*)&d.ex_head[(size_t)lane * d.E + placed], (unsigned long long)(-x));
+        }
+        if (lane == 0) {
+            d.pod_result[pod] = -2 - placed;
+            d.pod_order[pod] = S.seq++;
+            S.scan_start = 0;
+            S.st[ST_EXIST_PLACED] += 1;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    return placed;
+}
+
+// PREF: the solve relaxes preferences or runs MIN_VALUES_POLICY=BestEffort; false compiles that code out, so the
+// common instantiations keep the register plan they had without it.
+template <bool RESV, bool TOPO, bool PREF>
 __device__ __forceinline__ void ffd_solve(KpDev d) {
     constexpr bool TOPO_ON = KP_TOPO_ON && TOPO;  // the solve has topology groups
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -493,7 +545,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
         d.pod_result[p] = -1;
         d.pod_order[p] = -1;
     }
-    if (d.relax_next)  // a previous execute may have relaxed pods: every pod starts from its input class
+    if (PREF && d.relax_next)  // a previous execute may have relaxed pods: every pod starts from its input class
         for (int p = tid; p < P; p += nthr) {
             d.pod_cls[p] = d.pod_cls0[p];
             d.pod_shape[p] = d.pod_shape0[p];
@@ -577,7 +629,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
             int sstart = S.scan_start;  // every slice position < sstart has rejected the current shape
             int any_rej = S.any_rej;
             const int ep = S.epoch;
-            if (d.relax_next && S.relaxed) {
+            if (PREF && d.relax_next && S.relaxed) {
                 vlast = -1;  // Queue.Push(pod, relaxed): every lastLen read into the window is gone
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 if (lane == 0) S.relaxed = 0;
@@ -690,7 +742,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                         vp = d.qbuf[pos];
                         vc = d.pod_cls[vp];
                         vshape = d.pod_shape[vp];
-                        vlast = (d.last_ep && d.last_ep[vp] != ep) ? -1 : d.last_len[vp];
+                        vlast = (PREF && d.last_ep && d.last_ep[vp] != ep) ? -1 : d.last_len[vp];
                         vtol = (d.tol[vc] & 0x7FFFFFFFu) | ((d.cls_flags[vc] & 4u) ? 0x80000000u : 0u);
                         for (int r = 0; r < R; r++) S.qw_req[lane][r] = d.pod_req[(size_t)vp * R + r];
 #pragma unroll
@@ -1113,47 +1165,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
             if (S.cls_fill) fill_class_cache(d, S.cur_cls, S.CC, tid, nthr);
             __syncthreads();
             if (wave == 0) {
-                const int c = S.cur_cls;
-                const bool cons = (d.cls_flags[c] & CF_TOPO_CONS) != 0;
-                int placed = -1;
-                for (int base = 0; base < d.E && placed < 0; base += 64) {
-                    const int j = base + lane;
-                    bool cand = false;
-                    if (j < d.E) {
-                        const uint64_t xw = __hip_atomic_load(&d.XT[(size_t)c * d.EW + (j >> 6)], __ATOMIC_RELAXED,
-                                                              __HIP_MEMORY_SCOPE_AGENT);
-                        cand = (xw >> (j & 63)) & 1ull;
-                        for (int ai = 0; ai < d.n_active && cand; ai++)
-                            cand = S.pod_req[d.active_axes[ai]] <= ld_req(&d.ex_head[(size_t)ai * d.E + j]);
-                    }
-                    uint64_t m = ballot(cand);
-                    while (m) {
-                        const int jj = base + __ffsll((unsigned long long)m) - 1;
-                        m &= m - 1;
-                        const bool ok = cons ? existing_topo_try<true>(d, S.CC, S.ws[0], jj, lane)
-                                             : existing_topo_try<false>(d, S.CC, S.ws[0], jj, lane);
-                        if (ok) {
-                            placed = jj;
-                            break;
-                        }
-                    }
-                }
-                if (placed >= 0) {
-                    existing_topo_commit(d, S.CC, S.ws[0], placed, lane);
-                    topo_record(d, S.CC, S.ws[0], d.ex_hdr + (size_t)placed * K, d.ex_words + (size_t)placed * d.DW,
-                                placed, 0, false, lane, placed);
-                    if (lane < d.n_active) {
-                        const int64_t x = S.pod_req[d.active_axes[lane]];
-                        if (x) atomicAdd((unsigned long long*)&d.ex_head[(size_t)lane * d.E + placed], (unsigned long long)(-x));
-                    }
-                    if (lane == 0) {
-                        d.pod_result[pod] = -2 - placed;
-                        d.pod_order[pod] = S.seq++;
-                        S.scan_start = 0;
-                        S.st[ST_EXIST_PLACED] += 1;
-                    }
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
+                const int placed = existing_topo_scan(d, S, pod, lane);
                 if (lane == 0) {
                     S.ex_placed = placed;
                     S.cls_fill = 0;
@@ -1263,9 +1275,9 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 const bool fast = !(S.CC.flags & CF_TOPO) && !(RESV && d.resv_on && ld_i32(&d.nc_rlive[nc])) &&
                                   (slast[nc] == (uint16_t)S.cur_cls || ((S.CC.flags & CF_NOKEYS) && ((S.CC.tol >> a.tmpl) & 1u)));
                 if (fast && lane == 0) S.ws[wave].memo_ok = 1;
-                const bool ok = fast ? eval_fits_only(d, E, a, S.ws[wave], lane)
-                                : (TOPO_ON && (S.CC.flags & CF_TOPO_CONS)) ? eval_wave<true, RESV>(d, E, S.CC, a, S.ws[wave], lane)
-                                                              : eval_wave<false, RESV>(d, E, S.CC, a, S.ws[wave], lane);
+                const bool ok = fast ? eval_fits_only<PREF>(d, E, a, S.ws[wave], lane)
+                                : (TOPO_ON && (S.CC.flags & CF_TOPO_CONS)) ? eval_wave<true, RESV, true, PREF>(d, E, S.CC, a, S.ws[wave], lane)
+                                                              : eval_wave<false, RESV, true, PREF>(d, E, S.CC, a, S.ws[wave], lane);
                 if (d.trace && (pod == d.trace_pod || (S.cur_cls == -2 - d.trace_pod && pod <= d.trace_max)) && lane == 0) {
                     const int i = atomicAdd(&d.trace[0], 1);
                     {  // ring of the last KP_TRACE_N entries
@@ -1316,7 +1328,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                     commit_reqs(d, S.CC, S.ws[win], nc, lane);
                     if (RESV && d.resv_on && lane == 0) commit_reservations(d, sRcap, S.ws[win], nc, ld_u64(&d.nc_held[nc]), &S.rel_flag);
                 }
-                if (d.best_effort) {
+                if (PREF && d.best_effort) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // commit_reqs' header rows have landed
                     commit_min_relax(d, S.ws[win], nc, lane);
                 }
@@ -1375,8 +1387,8 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                         a.prof = nullptr;
                         a.host = d.E + S.N;  // NewNodeClaim's fresh hostname (no pod counted there yet)
                         a.held = 0;
-                        ok = (TOPO_ON && (S.CC.flags & CF_TOPO_CONS)) ? eval_wave<true, RESV>(d, E, S.CC, a, S.ws[wave], lane)
-                                                         : eval_wave<false, RESV>(d, E, S.CC, a, S.ws[wave], lane);
+                        ok = (TOPO_ON && (S.CC.flags & CF_TOPO_CONS)) ? eval_wave<true, RESV, true, PREF>(d, E, S.CC, a, S.ws[wave], lane)
+                                                         : eval_wave<false, RESV, true, PREF>(d, E, S.CC, a, S.ws[wave], lane);
                     }
                     if (d.trace && pod == d.trace_pod && lane == 0) {
                         const int i = atomicAdd(&d.trace[0], 1);
@@ -1413,7 +1425,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                             d.nc_words[(size_t)n * d.DW + i] = d.cls_words[(size_t)(d.C + jj) * d.DW + i];
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         commit_reqs(d, S.CC, S.ws[wave], n, lane);
-                        if (d.best_effort) {
+                        if (PREF && d.best_effort) {
                             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the header rows above have landed
                             commit_min_relax(d, S.ws[wave], n, lane);
                         }
@@ -1464,7 +1476,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                     const int tail = (S.qhead + S.qcount) % P;
                     d.qbuf[tail] = pod;
                     S.qcount++;
-                    const int nx = d.relax_next ? d.relax_next[S.cur_cls] : -1;
+                    const int nx = (PREF && d.relax_next) ? d.relax_next[S.cur_cls] : -1;
                     if (nx >= 0) {
                         // the pod takes its class's next relaxation stage (Topology.Update / updateCachedPodData) and
                         // lastLen is cleared: a new epoch
@@ -1474,7 +1486,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                         S.relaxed = 1;
                     } else {
                         d.last_len[pod] = S.qcount;
-                        if (d.last_ep) d.last_ep[pod] = S.epoch;
+                        if (PREF && d.last_ep) d.last_ep[pod] = S.epoch;
                     }
                 }
             }
@@ -1501,10 +1513,15 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
 
 // One named entry point per feature instantiation, so kernel traces (rocprofv3 --stats) report the common case
 // (ffd_kernel: no topology groups, no reserved offerings) separately from the topology / reservation variants.
-__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) { ffd_solve<false, false>(d); }
-__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_topo_kernel(KpDev d) { ffd_solve<false, true>(d); }
-__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_resv_kernel(KpDev d) { ffd_solve<true, false>(d); }
-__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_resv_topo_kernel(KpDev d) { ffd_solve<true, true>(d); }
+__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) { ffd_solve<false, false, false>(d); }
+__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_topo_kernel(KpDev d) { ffd_solve<false, true, false>(d); }
+__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_resv_kernel(KpDev d) { ffd_solve<true, false, false>(d); }
+__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_resv_topo_kernel(KpDev d) { ffd_solve<true, true, false>(d); }
+// preference relaxation / BestEffort minValues
+__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_pref_kernel(KpDev d) { ffd_solve<false, false, true>(d); }
+__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_pref_topo_kernel(KpDev d) { ffd_solve<false, true, true>(d); }
+__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_pref_resv_kernel(KpDev d) { ffd_solve<true, false, true>(d); }
+__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_pref_resv_topo_kernel(KpDev d) { ffd_solve<true, true, true>(d); }
 
 // ------------------------------------------------------------------------------------------------
 // FinalizeScheduling + Truncate(OrderByPrice, maxInstanceTypes) + SatisfiesMinValues
@@ -1754,8 +1771,9 @@ hipError_t kp_launch_template_init(const KpDev& d, hipStream_t s) {
 // Per-device kernel attributes: called by kp_ctx_create with the ctx's device current (every ctx, so a second ctx on
 // another device of the same process gets them too; the call is idempotent and needs no process-wide flag).
 hipError_t kp_ffd_set_attributes() {
-    const void* ks[4] = {(const void*)ffd_kernel, (const void*)ffd_topo_kernel, (const void*)ffd_resv_kernel,
-                         (const void*)ffd_resv_topo_kernel};
+    const void* ks[8] = {(const void*)ffd_kernel, (const void*)ffd_topo_kernel, (const void*)ffd_resv_kernel,
+                         (const void*)ffd_resv_topo_kernel, (const void*)ffd_pref_kernel, (const void*)ffd_pref_topo_kernel,
+                         (const void*)ffd_pref_resv_kernel, (const void*)ffd_pref_resv_topo_kernel};
     for (const void* k : ks) {
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, KP_LDS_BYTES);
         if (e != hipSuccess) return e;
@@ -1764,9 +1782,16 @@ hipError_t kp_ffd_set_attributes() {
 }
 hipError_t kp_launch_ffd(const KpDev& d, hipStream_t s) {
     const size_t bytes = (size_t)d.lds_bytes;
-    // instantiation by solve features: reserved offerings (RESV), topology groups (TOPO)
+    // instantiation by solve features: reserved offerings (RESV), topology groups (TOPO), preference relaxation or
+    // BestEffort minValues (PREF)
     const dim3 g(1), b(KP_NWAVES * 64);
-    if (d.ro && d.G > 0) hipLaunchKernelGGL(ffd_resv_topo_kernel, g, b, bytes, s, d);
+    const bool pref = d.relax_next || d.best_effort;
+    if (pref) {
+        if (d.ro && d.G > 0) hipLaunchKernelGGL(ffd_pref_resv_topo_kernel, g, b, bytes, s, d);
+        else if (d.ro) hipLaunchKernelGGL(ffd_pref_resv_kernel, g, b, bytes, s, d);
+        else if (d.G > 0) hipLaunchKernelGGL(ffd_pref_topo_kernel, g, b, bytes, s, d);
+        else hipLaunchKernelGGL(ffd_pref_kernel, g, b, bytes, s, d);
+    } else if (d.ro && d.G > 0) hipLaunchKernelGGL(ffd_resv_topo_kernel, g, b, bytes, s, d);
     else if (d.ro) hipLaunchKernelGGL(ffd_resv_kernel, g, b, bytes, s, d);
     else if (d.G > 0) hipLaunchKernelGGL(ffd_topo_kernel, g, b, bytes, s, d);
     else hipLaunchKernelGGL(ffd_kernel, g, b, bytes, s, d);
