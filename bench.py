@@ -71,16 +71,18 @@ def consolidation_leg(a, cat, local, rank, world, dist, barrier):
         ctx.upload_catalog(model.CatalogView(cat))
         ctx.consolidate_prepare(model.ConsolidateInputView(cp, abi.KP_CONSOLIDATE_SINGLE))
 
-    def probe_fn(c, mode, b0, b1):
-        return ctx.consolidate_execute(mode, n_s if mode == abi.KP_CONSOLIDATE_SINGLE else n_m, b0, b1)
-
     def step():
-        # the library's own sharding: one call per mode over the whole probe range (no torch.distributed collective)
-        cs = consolidation.compute_command(cp, abi.KP_CONSOLIDATE_SINGLE, probe_fn, distributed=False)
-        ms_s, cst_s = ctx.consolidate_stats()
-        cm = consolidation.compute_command(cp, abi.KP_CONSOLIDATE_MULTI, probe_fn, distributed=False)
-        ms_m, cst_m = ctx.consolidate_stats()
-        return cs, cm, (ms_s, cst_s), (ms_m, cst_m)
+        # one pass over both probe lists (KP_CONSOLIDATE_BOTH: one launch per device, the longest multi-node prefixes
+        # first, the single-node probes on the remaining compute units); the library shards it over its devices itself
+        # (no torch.distributed collective).  The decisions replay MultiNodeConsolidation's binary search and
+        # SingleNodeConsolidation's first-valid scan over the two slices.
+        res = ctx.consolidate_execute(abi.KP_CONSOLIDATE_BOTH, n_m + n_s)
+        st = ctx.consolidate_stats()
+        part = {abi.KP_CONSOLIDATE_MULTI: res[:n_m], abi.KP_CONSOLIDATE_SINGLE: res[n_m:]}
+        fn = lambda c, mode, b0, b1: part[mode]  # noqa: E731 (whole ranges: distributed=False)
+        cs = consolidation.compute_command(cp, abi.KP_CONSOLIDATE_SINGLE, fn, distributed=False)
+        cm = consolidation.compute_command(cp, abi.KP_CONSOLIDATE_MULTI, fn, distributed=False)
+        return cs, cm, st
 
     if rank == 0:
         for _ in range(max(1, a.warmup)):
@@ -91,9 +93,9 @@ def consolidation_leg(a, cat, local, rank, world, dist, barrier):
     cs = cm = None
     if rank == 0:
         for _ in range(a.steps):
-            cs, cm, st_s, st_m = step()
-            kms.append([st_s[0][0], st_s[0][1], st_m[0][0], st_m[0][1]])
-            kcs.append(np.array(st_s[1]) + np.array(st_m[1]))
+            cs, cm, st = step()
+            kms.append([st[0][0], st[0][1]])
+            kcs.append(np.array(st[1]))
     elapsed = time.perf_counter() - t0
     barrier()
     if dist is not None:
@@ -107,7 +109,7 @@ def consolidation_leg(a, cat, local, rank, world, dist, barrier):
     cst = np.array(kcs).mean(axis=0)
     A = int(np.any(cp.cluster.pods.requests != 0, axis=0).sum())  # active axes (no daemon overhead in config4)
     B = consolidation_bytes(cst, A)
-    kern_s = (km[1] + km[3]) / 1e3
+    kern_s = km[1] / 1e3
     achieved = B / kern_s / 1e9 if kern_s > 0 else 0.0
     out = {
         "metric": "consolidation cands/sec",
@@ -121,16 +123,14 @@ def consolidation_leg(a, cat, local, rank, world, dist, barrier):
                                                                                     cp.cluster.pods.n, n_s, n_m),
                    "parallelism": "probe shards x%d (one multi-device ctx, in-library gather)" % world},
         "decisions": {"single": [cs.decision, cs.candidates[:1]], "multi": [cm.decision, len(cm.candidates)]},
-        "kernel_ms_rank0": {"single_prep": km[0], "single_probes": km[1], "multi_prep": km[2], "multi_probes": km[3]},
+        "kernel_ms_rank0": {"prep": km[0], "probes": km[1]},
         "counters_per_step": dict(zip(["pods_popped", "existing_slots", "nodeclaim_evals", "template_evals", "probes",
                                        "bitmap_words", "placed_existing", "new_nodeclaims", "chunk_loads", "chunk_hits",
                                        "cyc_build", "cyc_scan", "cyc_nodeclaim", "cyc_decide", "cyc_total"],
                                       [int(x) for x in cst])),
-        "counters_multi": dict(zip(["pods_popped", "existing_slots", "chunk_loads", "chunk_hits", "cyc_build",
-                                    "cyc_scan", "cyc_total"], [int(st_m[1][i]) for i in (0, 1, 8, 9, 10, 11, 14)])),
         "roofline": {"bound": "hbm", "kernel": "consolidate_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes": int(B),
-                     "kernel_ms": float(km[1] + km[3]),
+                     "kernel_ms": float(km[1]),
                      "traffic_per_launch": pmc_traffic("consolidate")},
         "cpu_baseline": None,
     }

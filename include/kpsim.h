@@ -345,7 +345,10 @@ kp_status kp_last_kernel_times(kp_ctx* ctx, double* ms, int32_t n);
  * cluster.existing must be in NewScheduler's order (initialized nodes first, then by name); probes keep that order
  * with the candidates removed.  Candidate prices must be >= 0 (getCandidatePrices fails otherwise).
  */
-enum { KP_CONSOLIDATE_SINGLE = 0, KP_CONSOLIDATE_MULTI = 1 };
+enum { KP_CONSOLIDATE_SINGLE = 0, KP_CONSOLIDATE_MULTI = 1,
+       KP_CONSOLIDATE_BOTH = 2 };  /* both probe lists in one pass: the multi-node probes, then the single-node probes
+                                      (one device launch; the longest multi-node prefixes are started first, the
+                                      single-node probes fill the remaining compute units) */
 enum { KP_DECISION_NONE = 0, KP_DECISION_DELETE = 1, KP_DECISION_REPLACE = 2 };
 enum { KP_CT_ON_DEMAND = 0, KP_CT_SPOT = 1, KP_CT_RESERVED = 2 };
 

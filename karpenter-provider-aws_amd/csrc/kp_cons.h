@@ -17,9 +17,11 @@ enum { CS_POPS = 0, CS_EX_NODES, CS_NC_EVALS, CS_TMPL_EVALS, CS_PROBES, CS_BITMA
 #define KP_CONS_XTC 1024  // pod classes whose XT column of the cached node chunk is kept in LDS
 
 struct KpCons {
-    int32_t n_probes;           // probes of this call: global probe ids probe0 .. probe0 + n_probes - 1
-    int32_t probe0;
+    int32_t n_probes;           // probes of this call (out[0 .. n_probes))
+    int32_t probe0;             // first probe of the call (multi-node part for KP_CONSOLIDATE_BOTH)
     int32_t mode;               // KP_CONSOLIDATE_*
+    int32_t n_multi;            // BOTH: out[0, n_multi) are multi-node probes probe0.., the rest single-node sprobe0..
+    int32_t sprobe0;
     int32_t n_cand;
     int32_t spot_to_spot;
     int32_t v_spot, v_od;       // capacity-type value ids in the solve dictionary, -1 when absent

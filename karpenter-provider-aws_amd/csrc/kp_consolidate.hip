@@ -228,8 +228,12 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             probe = __builtin_amdgcn_readfirstlane(__shfl(probe, 0));
         }
         if (probe >= k.n_probes) break;
-        const int gp = k.probe0 + probe;
-        const bool single = k.mode == KP_CONSOLIDATE_SINGLE;
+        // work slot → probe: multi-node prefixes are taken longest first (the pass waits for its longest probe, so it
+        // must start first); with KP_CONSOLIDATE_BOTH the single-node probes follow them in the same launch
+        const int nmul = k.mode == KP_CONSOLIDATE_MULTI ? k.n_probes : (k.mode == KP_CONSOLIDATE_BOTH ? k.n_multi : 0);
+        const bool single = probe >= nmul;
+        const int oi = single ? probe : nmul - 1 - probe;  // output index
+        const int gp = single ? (k.mode == KP_CONSOLIDATE_BOTH ? k.sprobe0 + probe - nmul : k.probe0 + probe) : k.probe0 + oi;
         const int c0 = single ? gp : 0, c1 = single ? gp + 1 : gp + 2;
         int64_t st_pops = 0, st_nodes = 0, st_nc = 0, st_tmpl = 0, st_words = 0, st_placed = 0, st_loads = 0, st_hits = 0;
         long long cy_build = 0, cy_scan = 0, cy_nc = 0, cy_dec = 0;
@@ -826,7 +830,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             o.n_pods = n;
             o.candidate_price = cprice;
             o.replacement_price = rprice;
-            k.out[probe] = o;
+            k.out[oi] = o;
             // counters stay in LDS until the worker exits (per-probe global atomics on 16 words serialise in L2)
             S.st[CS_POPS] += st_pops;
             S.st[CS_EX_NODES] += st_nodes;

@@ -2363,10 +2363,12 @@ extern "C" kp_status kp_result_nodeclaim_requirements(kp_ctx* ctx, int32_t nc, c
 extern "C" int32_t kp_consolidate_probe_count(const kp_consolidate_input* in) {
     if (!in) return 0;
     const int n = in->n_candidates;
-    if (in->mode == KP_CONSOLIDATE_SINGLE) return n > 0 ? n : 0;
-    if (n < 2) return 0;
+    const int ns = n > 0 ? n : 0;
     const int mx = in->max_candidates > 0 ? in->max_candidates : 100;
-    return n <= mx ? n - 1 : mx;  // firstNConsolidationOption: mid in [1, max], prefix candidates[0 : mid+1]
+    const int nm = n < 2 ? 0 : (n <= mx ? n - 1 : mx);  // firstNConsolidationOption: mid in [1, max], candidates[0 : mid+1]
+    if (in->mode == KP_CONSOLIDATE_SINGLE) return ns;
+    if (in->mode == KP_CONSOLIDATE_MULTI) return nm;
+    return nm + ns;  // KP_CONSOLIDATE_BOTH
 }
 
 static kp_status cons_prepare_one(kp_ctx* ctx, const kp_consolidate_input* in) try {
@@ -2489,19 +2491,25 @@ extern "C" kp_status kp_consolidate_prepare(kp_ctx* ctx, const kp_consolidate_in
     return fail(ctx, KP_E_INVALID, "kp_consolidate_prepare: host error");
 }
 
+// probes of a prepared pass: multi-node (firstNConsolidationOption's prefixes), single-node, or both (multi first)
+static int cons_probes(const kp_ctx* c, int mode) {
+    const int NC = c->cons.n_cand;
+    const int nm = NC < 2 ? 0 : (NC <= c->cons_max_candidates ? NC - 1 : c->cons_max_candidates);
+    return mode == KP_CONSOLIDATE_SINGLE ? NC : mode == KP_CONSOLIDATE_MULTI ? nm : nm + NC;
+}
+
 static kp_status cons_execute_one(kp_ctx* ctx, int32_t mode, int32_t probe_begin, int32_t probe_end,
                                   kp_probe_result* results, int32_t cap_results) try {
     if (!ctx) return KP_E_INVALID;
     if (!ctx->cons_prepared || !ctx->have_catalog)
         return fail(ctx, KP_E_STATE, "kp_consolidate_execute before kp_consolidate_prepare");
-    if (mode != KP_CONSOLIDATE_SINGLE && mode != KP_CONSOLIDATE_MULTI) return fail(ctx, KP_E_INVALID, "unknown consolidation mode");
+    if (mode != KP_CONSOLIDATE_SINGLE && mode != KP_CONSOLIDATE_MULTI && mode != KP_CONSOLIDATE_BOTH)
+        return fail(ctx, KP_E_INVALID, "unknown consolidation mode");
     kp_ctx* c = ctx;
     HIPCHK(hipSetDevice(c->device));
     KpCons k = c->cons;
     const int NC = k.n_cand;
-    int np;
-    if (mode == KP_CONSOLIDATE_SINGLE) np = NC;
-    else np = NC < 2 ? 0 : (NC <= c->cons_max_candidates ? NC - 1 : c->cons_max_candidates);
+    const int np = cons_probes(c, mode);
     const int b0 = probe_begin > 0 ? probe_begin : 0;
     const int b1 = probe_end > 0 && probe_end < np ? probe_end : np;
     if (b0 > b1) return fail(ctx, KP_E_INVALID, "probe range outside the probe list");
@@ -2515,15 +2523,23 @@ static kp_status cons_execute_one(kp_ctx* ctx, int32_t mode, int32_t probe_begin
     d.profile = 0;
     hipStream_t s = c->stream;
     const std::vector<int32_t>& coff = c->cons_off;
-    int maxp = 0;  // ring capacity: pods of the largest probe
-    if (mode == KP_CONSOLIDATE_SINGLE) {
-        for (int i = b0; i < b1; i++) maxp = std::max(maxp, coff[i + 1] - coff[i]);
-    } else {
-        maxp = coff[std::min(NC, b1 + 1)];
+    // the range as a multi-node part [m0, m1) and a single-node part [s0, s1) (BOTH: multi probes come first)
+    const int nm_all = cons_probes(c, KP_CONSOLIDATE_MULTI);
+    int m0 = 0, m1 = 0, s0 = 0, s1 = 0;
+    if (mode == KP_CONSOLIDATE_MULTI) m0 = b0, m1 = b1;
+    else if (mode == KP_CONSOLIDATE_SINGLE) s0 = b0, s1 = b1;
+    else {
+        m0 = std::min(b0, nm_all), m1 = std::min(b1, nm_all);
+        s0 = std::max(b0, nm_all) - nm_all, s1 = std::max(b1, nm_all) - nm_all;
     }
+    int maxp = 0;  // ring capacity: pods of the largest probe
+    for (int i = s0; i < s1; i++) maxp = std::max(maxp, coff[i + 1] - coff[i]);
+    if (m1 > m0) maxp = std::max(maxp, coff[std::min(NC, m1 + 1)]);
     k.mode = mode;
     k.n_probes = nprobe;
-    k.probe0 = b0;
+    k.probe0 = mode == KP_CONSOLIDATE_SINGLE ? s0 : m0;
+    k.n_multi = m1 - m0;
+    k.sprobe0 = s0;
     k.ring_cap = std::max(1, c->cons_n_pending + maxp);
     if (!kp_cons_plan_lds(d, k, KP_LDS_BYTES)) return fail(ctx, KP_E_UNSUPPORTED, "consolidation LDS plan exceeds 160 KB");
     const int occ = std::max(1, std::min(8, KP_LDS_BYTES / std::max(k.lds_bytes, 1)));
@@ -2613,9 +2629,9 @@ extern "C" kp_status kp_consolidate_execute(kp_ctx* ctx, int32_t mode, int32_t p
     for (kp_ctx* p : ctx->peers)
         if (!p->cons_prepared || !p->have_catalog)
             return fail(ctx, KP_E_STATE, "kp_consolidate_execute: a peer device has no prepared pass");
-    if (mode != KP_CONSOLIDATE_SINGLE && mode != KP_CONSOLIDATE_MULTI) return fail(ctx, KP_E_INVALID, "unknown consolidation mode");
-    const int NC = ctx->cons.n_cand;
-    const int np = mode == KP_CONSOLIDATE_SINGLE ? NC : (NC < 2 ? 0 : (NC <= ctx->cons_max_candidates ? NC - 1 : ctx->cons_max_candidates));
+    if (mode != KP_CONSOLIDATE_SINGLE && mode != KP_CONSOLIDATE_MULTI && mode != KP_CONSOLIDATE_BOTH)
+        return fail(ctx, KP_E_INVALID, "unknown consolidation mode");
+    const int np = cons_probes(ctx, mode);
     const int b0 = probe_begin > 0 ? probe_begin : 0;
     const int b1 = probe_end > 0 && probe_end < np ? probe_end : np;
     if (b0 > b1) return fail(ctx, KP_E_INVALID, "probe range outside the probe list");

@@ -126,7 +126,7 @@ class kp_solve_output(C.Structure):
                 ("pod_order", c_int32_p), ("stats", kp_solve_stats)]
 
 
-KP_CONSOLIDATE_SINGLE, KP_CONSOLIDATE_MULTI = 0, 1
+KP_CONSOLIDATE_SINGLE, KP_CONSOLIDATE_MULTI, KP_CONSOLIDATE_BOTH = 0, 1, 2
 KP_DECISION_NONE, KP_DECISION_DELETE, KP_DECISION_REPLACE = 0, 1, 2
 KP_CT_ON_DEMAND, KP_CT_SPOT, KP_CT_RESERVED = 0, 1, 2
 

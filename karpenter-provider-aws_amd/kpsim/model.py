@@ -207,12 +207,11 @@ class ConsolidationProblem:
 
 
 def consolidation_probe_count(n_candidates, mode, max_candidates=100):
-    """Same numbering as kp_consolidate_probe_count (include/kpsim.h)."""
+    """Same numbering as kp_consolidate_probe_count (include/kpsim.h); KP_CONSOLIDATE_BOTH: multi then single."""
     if mode == abi.KP_CONSOLIDATE_SINGLE:
         return n_candidates
-    if n_candidates < 2:
-        return 0
-    return n_candidates - 1 if n_candidates <= max_candidates else max_candidates
+    nm = 0 if n_candidates < 2 else (n_candidates - 1 if n_candidates <= max_candidates else max_candidates)
+    return nm + n_candidates if mode == abi.KP_CONSOLIDATE_BOTH else nm
 
 
 # ------------------------------------------------------------------------------------------------

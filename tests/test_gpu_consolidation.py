@@ -209,3 +209,26 @@ def test_reserved_replacement(ctx, golden, rcap, expiring):
             assert (dev["replacement_price"] < 1e-6).all()
         else:
             assert (dev["replacement_price"] > 1e-6).all()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_both_modes_one_pass(ctx, golden, seed):
+    """KP_CONSOLIDATE_BOTH: one pass returns the multi-node probes then the single-node probes, each equal to its own
+    mode's pass (and shards of the combined list concatenate to it)."""
+    rng = np.random.Generator(np.random.PCG64(700 + seed))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 300)), replace=False))]
+    cp = fuzzgen.fuzz_consolidation(sub, 700 + seed, n_nodes=int(rng.integers(4, 80)), n_pods=int(rng.integers(20, 300)),
+                                    supported=True)
+    ctx.upload_catalog(model.CatalogView(cp.cluster.catalog))
+    ctx.consolidate_prepare(model.ConsolidateInputView(cp, abi.KP_CONSOLIDATE_SINGLE))
+    nc = len(cp.candidates)
+    n_s = model.consolidation_probe_count(nc, abi.KP_CONSOLIDATE_SINGLE)
+    n_m = model.consolidation_probe_count(nc, abi.KP_CONSOLIDATE_MULTI)
+    both = ctx.consolidate_execute(abi.KP_CONSOLIDATE_BOTH, n_m + n_s)
+    assert_probes_equal(both[:n_m], ctx.consolidate_execute(abi.KP_CONSOLIDATE_MULTI, n_m))
+    assert_probes_equal(both[n_m:], ctx.consolidate_execute(abi.KP_CONSOLIDATE_SINGLE, n_s))
+    assert_probes_equal(both[:n_m], pyoracle.consolidate(cp, abi.KP_CONSOLIDATE_MULTI))
+    cut = (n_m + n_s) // 3
+    parts = [ctx.consolidate_execute(abi.KP_CONSOLIDATE_BOTH, n_m + n_s, b, e)
+             for b, e in ((0, cut), (cut, 2 * cut), (2 * cut, n_m + n_s))]
+    assert_probes_equal(np.concatenate(parts), both)
