@@ -480,6 +480,12 @@ extern "C" kp_status kp_catalog_build(int32_t n_types, const kp_ec2_instance_typ
     if (nc->ami_family < KP_AMI_AL2 || nc->ami_family > KP_AMI_CUSTOM) return KP_E_INVALID;
     if (os->n_zones < 0 || (os->n_zones > 0 && !os->zones) || (n_types > 0 && (!os->type_zones || !os->od_price)))
         return KP_E_INVALID;
+    auto bad_array = [](int32_t n, const void* p) { return n < 0 || (n > 0 && !p); };
+    if (bad_array(nc->n_zones, nc->zones) || bad_array(nc->n_block_device_mappings, nc->block_device_mappings) ||
+        bad_array(nc->n_kube_reserved, nc->kube_reserved) || bad_array(nc->n_system_reserved, nc->system_reserved) ||
+        (nc->eviction_hard && nc->n_eviction_hard < 0) || (nc->eviction_soft && nc->n_eviction_soft < 0) ||
+        bad_array(nc->n_capacity_reservations, nc->capacity_reservations))
+        return KP_E_INVALID;
     try {
         kp_catalog* c = new kp_catalog();
         const int Z = os->n_zones;
