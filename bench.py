@@ -190,10 +190,11 @@ def launch_leg(a, golden, local, rank, world, dist, barrier):
     phases = []
     for _ in range(a.steps):
         res = ctx.launch_select(batch, 60)
-        st6 = ctx.launch_stats(6)
-        kms.append(st6[0])
-        cms.append(st6[1])
-        phases.append(st6[2:])
+        st7 = ctx.launch_stats(7)
+        kms.append(st7[0])
+        cms.append(st7[1])
+        phases.append(st7[2:6])
+        nsub = int(st7[6])
     elapsed = time.perf_counter() - t0
     barrier()
     kern = float(np.mean(kms))
@@ -214,7 +215,10 @@ def launch_leg(a, golden, local, rank, world, dist, barrier):
         "steps": a.steps,
         "kernel_ms": kern,
         "call_ms": float(np.mean(cms)),
-        "call_phases_ms": dict(zip(["encode", "merge_upload", "kernel_download", "expand"],
+        # the call pipelines nsub sub-batches: host encoding / expansion of one overlaps the kernel of another, so the
+        # phases below are host-side sums (wait_download = time the host waited for a sub-batch's kernel + download)
+        "sub_batches": nsub,
+        "call_phases_ms": dict(zip(["encode", "merge_upload", "wait_download", "expand"],
                                    [float(x) for x in np.mean(phases, axis=0)])),
         "call_rate_pcie_inclusive": a.launch_batch * a.steps / elapsed,
         "scaling": "strong",
@@ -223,9 +227,10 @@ def launch_leg(a, golden, local, rank, world, dist, barrier):
             "parallelism": "batch slices x%d" % world},
         "outcomes": {"ok": int((st == abi.KP_OK).sum()), "ice": int((st == abi.KP_E_INSUFFICIENT_CAPACITY).sum()),
                      "reserved": int((res.rows["capacity_type"] == abi.KP_CT_RESERVED).sum())},
+        # per launch: algorithmic bytes B / nsub over the mean launch duration kern / nsub (the same ratio)
         "roofline": {"bound": "hbm", "kernel": "launch_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes": int(B),
-                     "traffic": pmc_traffic("launch")},
+                     "launches_per_step": nsub, "algorithmic_bytes_per_launch": int(B / nsub), "traffic": pmc_traffic("launch")},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -452,8 +452,10 @@ typedef struct kp_launch_result {
 kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_request* requests, int32_t max_instance_types,
                            kp_launch_result* results, int32_t* type_ids, int32_t cap_type_ids,
                            int32_t* override_offerings, int32_t cap_overrides);
-/* Of the last kp_launch_select: ms[0] = launch kernel (HIP events on the ctx stream), ms[1] = whole call; host phases
- * ms[2] = request encoding, ms[3] = table merge + upload, ms[4] = kernel + result download, ms[5] = result expansion. */
+/* Of the last kp_launch_select: ms[0] = launch kernel time (HIP events on the ctx stream, summed over the call's
+ * sub-batches), ms[1] = whole call; host phases ms[2] = request encoding, ms[3] = table merge + upload, ms[4] = waits
+ * for kernel + result download, ms[5] = result expansion; ms[6] = number of sub-batches.  A batch of >= 4096 requests
+ * is cut into up to 4 sub-batches so that encoding and expansion on the host overlap the kernel. */
 kp_status kp_launch_stats(kp_ctx* ctx, double* ms, int32_t n);
 
 /*

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <chrono>
 #include <cstdint>
@@ -262,12 +263,14 @@ struct PrefExpansion {
 
 // Persistent worker threads of a ctx for the host-side batch work of kp_launch_select (request encoding, result
 // expansion): run(k, fn) calls fn(0..k-1) across the workers and the calling thread and returns when all are done.
+// A pipelined call issues several runs within a millisecond, so an idle worker spins on the generation counter for a
+// while before it sleeps on the condition variable (a futex wake-up of 15 threads costs ~0.3 ms per run).
 class WorkerPool {
   public:
     ~WorkerPool() {
         {
             std::lock_guard<std::mutex> g(mu_);
-            stop_ = true;
+            stop_.store(true);
         }
         cv_.notify_all();
         for (auto& t : th_) t.join();
@@ -281,55 +284,63 @@ class WorkerPool {
             for (int i = 0; i < k; i++) fn(i);
             return;
         }
+        const uint32_t g = (gen_.load(std::memory_order_relaxed) + 1) & kGenMask;
+        fn_ = &fn;  // published by the release store of claim_ (a claim acquires it)
+        left_.store(k, std::memory_order_relaxed);
+        claim_.store(((uint64_t)g << 40) | ((uint64_t)k << 20), std::memory_order_release);
         {
-            std::lock_guard<std::mutex> g(mu_);
-            fn_ = &fn;
-            next_ = 0;
-            tasks_ = k;
-            left_ = k;
-            gen_++;
+            std::lock_guard<std::mutex> lk(mu_);  // a worker about to sleep re-checks gen_ under the lock
+            gen_.store(g, std::memory_order_release);
         }
         cv_.notify_all();
-        work();
-        std::unique_lock<std::mutex> g(mu_);
-        done_.wait(g, [this] { return left_ == 0; });
-        fn_ = nullptr;
+        work(g);
+        while (left_.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
     }
 
   private:
-    void work() {
+    static constexpr uint32_t kGenMask = (1u << 24) - 1;
+    // claim_ = generation << 40 | tasks << 20 | next task: a worker still inside an older generation cannot claim
+    void work(uint32_t g) {
+        uint64_t v = claim_.load(std::memory_order_acquire);
         for (;;) {
-            int i;
-            const std::function<void(int)>* f;
-            {
-                std::lock_guard<std::mutex> g(mu_);
-                if (!fn_ || next_ >= tasks_) return;
-                i = next_++;
-                f = fn_;
-            }
-            (*f)(i);
-            std::lock_guard<std::mutex> g(mu_);
-            if (--left_ == 0) done_.notify_all();
+            if ((uint32_t)(v >> 40) != g) return;
+            const int tasks = (int)((v >> 20) & 0xFFFFF), i = (int)(v & 0xFFFFF);
+            if (i >= tasks) return;
+            if (!claim_.compare_exchange_weak(v, v + 1, std::memory_order_acq_rel, std::memory_order_acquire)) continue;
+            (*fn_)(i);
+            left_.fetch_sub(1, std::memory_order_release);
+            v = claim_.load(std::memory_order_acquire);
         }
     }
     void loop() {
-        int seen = 0;
+        uint32_t seen = gen_.load(std::memory_order_acquire);
         for (;;) {
-            {
-                std::unique_lock<std::mutex> g(mu_);
-                cv_.wait(g, [&] { return stop_ || gen_ != seen; });
-                if (stop_) return;
-                seen = gen_;
+            uint32_t g = seen;
+            const auto t0 = std::chrono::steady_clock::now();
+            for (int spins = 1; !stop_.load(std::memory_order_relaxed); spins++) {
+                g = gen_.load(std::memory_order_acquire);
+                if (g != seen) break;
+                __builtin_ia32_pause();
+                if ((spins & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
             }
-            work();
+            if (g == seen) {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_.load() || gen_.load(std::memory_order_acquire) != seen; });
+                g = gen_.load(std::memory_order_acquire);
+            }
+            if (stop_.load()) return;
+            seen = g;
+            work(g);
         }
     }
     std::vector<std::thread> th_;
     std::mutex mu_;
-    std::condition_variable cv_, done_;
+    std::condition_variable cv_;
     const std::function<void(int)>* fn_ = nullptr;
-    int next_ = 0, tasks_ = 0, left_ = 0, gen_ = 0;
-    bool stop_ = false;
+    std::atomic<uint64_t> claim_{0};
+    std::atomic<int> left_{0};
+    std::atomic<uint32_t> gen_{0};
+    std::atomic<bool> stop_{false};
 };
 
 // Pinned host staging buffer, grow-only (launch-request tables: DMA without the pageable-copy staging).
@@ -468,19 +479,21 @@ struct kp_ctx {
     DBuf<double> d_l_price;
     DBuf<uint8_t> d_l_avail, d_l_exotic;
     DBuf<KlReq> d_l_req;
-    DBuf<KlKey> d_l_keys;
-    DBuf<KlMinKey> d_l_mins;
-    DBuf<uint64_t> d_l_words;
+    DBuf<KlKey> d_l_keys[2];                 // two staging sets: sub-batch b uses set b & 1 (kp_launch_select)
+    DBuf<KlMinKey> d_l_mins[2];
+    DBuf<uint64_t> d_l_words[2];
     DBuf<int64_t> d_l_rq;
     PinBuf<KlReq> p_l_req;                   // pinned staging of the launch tables and results
     PinBuf<int64_t> p_l_rq;
-    PinBuf<KlKey> p_l_keys;
-    PinBuf<KlMinKey> p_l_mins;
-    PinBuf<uint64_t> p_l_words, p_l_over;
+    PinBuf<KlKey> p_l_keys[2];
+    PinBuf<KlMinKey> p_l_mins[2];
+    PinBuf<uint64_t> p_l_words[2], p_l_over;
     PinBuf<int32_t> p_l_hdr, p_l_types;
     WorkerPool pool;                         // host threads of kp_launch_select's batch work
-    double launch_ms[6] = {};                // launch kernel, whole call; host phases: encode, merge + upload,
-                                             // kernel + download, result expansion
+    double launch_ms[6] = {};                // Σ launch kernel, whole call; host phases: encode, merge + upload,
+                                             // waits for the downloads, result expansion
+    int launch_nsub = 0;                     // sub-batches of the last call
+    hipEvent_t lev[3 * KL_MAX_SUB] = {};     // per sub-batch: kernel start, kernel end, download landed
     // topology (kp_solve_prepare encodes the groups; execute resets the counts from the *0 copies)
     int tg_G = 0, tg_HG = 0;
     DBuf<int4> d_tg_info;
@@ -592,6 +605,8 @@ extern "C" kp_status kp_ctx_destroy(kp_ctx* ctx) {
     hipSetDevice(ctx->device);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
     for (auto& e : ctx->ev)
+        if (e) hipEventDestroy(e);
+    for (auto& e : ctx->lev)
         if (e) hipEventDestroy(e);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;  // every DBuf member frees its device memory (on the device set above)
@@ -3138,166 +3153,212 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
         q.n_min = (int)mins.size() - q.min_off;
         return true;
     };
-    auto run_chunk = [&](int ti) {
-        const int i0 = (int)((int64_t)n * ti / nthr), i1 = (int)((int64_t)n * (ti + 1) / nthr);
-        for (int i = i0; i < i1; i++)
-            if (!encode_one(i, chunks[ti])) return;
-    };
-    c->pool.grow(nthr);
-    c->pool.run(nthr, run_chunk);
-    const auto t_enc = clk::now();
-    // chunk tables concatenated straight into pinned staging, offsets rebased per chunk
-    size_t nk = 0, nm = 0, nw = 0;
-    for (int ti = 0; ti < nthr; ti++) {
-        if (chunks[ti].st != KP_OK) return fail(c, chunks[ti].st, chunks[ti].msg);
-        nk += chunks[ti].keys.size();
-        nm += chunks[ti].mins.size();
-        nw += chunks[ti].words.size();
-    }
-    HIPCHK(c->p_l_keys.ensure(std::max<size_t>(nk, 1)));
-    HIPCHK(c->p_l_mins.ensure(std::max<size_t>(nm, 1)));
-    HIPCHK(c->p_l_words.ensure(std::max<size_t>(nw, 1)));
-    {
-        size_t kb = 0, mb = 0, wbase = 0;
-        for (int ti = 0; ti < nthr; ti++) {
-            Chunk& ch = chunks[ti];
-            const int i0 = (int)((int64_t)n * ti / nthr), i1 = (int)((int64_t)n * (ti + 1) / nthr);
-            for (int i = i0; i < i1; i++) {
-                KlReq& q = reqs[i];
-                q.key_off += (int)kb;
-                q.und_off += (int)kb;
-                q.min_off += (int)mb;
-                for (int r = 0; r < KL_ROLES; r++)
-                    if (q.role[r].mode == KLR_CONSTRAINED) q.role[r].woff += (int)wbase;
-            }
-            KlKey* kd = c->p_l_keys.p + kb;
-            for (size_t j = 0; j < ch.keys.size(); j++) {
-                kd[j] = ch.keys[j];
-                kd[j].woff += (int)wbase;  // undefined-key entries carry no bitset; their woff is never read
-            }
-            if (!ch.mins.empty()) memcpy(c->p_l_mins.p + mb, ch.mins.data(), ch.mins.size() * sizeof(KlMinKey));
-            if (!ch.words.empty()) memcpy(c->p_l_words.p + wbase, ch.words.data(), ch.words.size() * sizeof(uint64_t));
-            kb += ch.keys.size();
-            mb += ch.mins.size();
-            wbase += ch.words.size();
-        }
-    }
+    // Pipeline over sub-batches: sub-batch b is encoded on the host threads while the kernel of b-1 runs, and the
+    // results of b-1 are expanded once its download has landed.  The request rows (KlReq, requests) and the result
+    // rows live at their batch positions; the key / minValues / word tables of sub-batch b go to staging set b & 1,
+    // which is free again because sub-batch b-2's download (queued behind its kernel) was waited for before b is
+    // encoded.
+    int nsub = n >= 4096 ? std::min(KL_MAX_SUB, n / 2048) : 1;
+    if (const char* e = getenv("KPSIM_LAUNCH_SUB")) nsub = std::max(1, std::min({KL_MAX_SUB, atoi(e), std::max(1, n)}));
+    const auto sub_begin = [&](int b) { return (int)((int64_t)n * b / nsub); };
     hipStream_t s = c->stream;
     if (n > 0) {
-        auto up = [&](auto& dbuf, const auto* src, size_t count) -> hipError_t {
-            hipError_t e = dbuf.ensure(std::max<size_t>(count, 1));
-            if (e != hipSuccess || count == 0) return e;
-            return hipMemcpyAsync(dbuf.p, src, count * sizeof(*src), hipMemcpyHostToDevice, s);
-        };
-        HIPCHK(up(c->d_l_req, reqs, (size_t)n));
-        HIPCHK(up(c->d_l_keys, c->p_l_keys.p, nk));
-        HIPCHK(up(c->d_l_mins, c->p_l_mins.p, nm));
-        HIPCHK(up(c->d_l_words, c->p_l_words.p, nw));
-        HIPCHK(up(c->d_l_rq, rq, (size_t)n * R));
+        HIPCHK(c->d_l_req.ensure((size_t)n));
+        HIPCHK(c->d_l_rq.ensure((size_t)n * R));
         HIPCHK(c->d_l_hdr.ensure((size_t)n * KL_HDR));
         HIPCHK(c->d_l_types.ensure((size_t)n * M));
         HIPCHK(c->d_l_over.ensure((size_t)n * M));
     }
-    KpLaunch g{};
-    g.T = T;
-    g.TW = c->TW;
-    g.R = R;
-    g.M = M;
-    g.type_val = c->d_type_val.p;
-    g.multi_mask = c->d_multi_mask.p;
-    g.dne_mask = c->d_dne_mask.p;
-    g.alloc = c->d_alloc.p;
-    g.name_rank = c->d_name_rank.p;
-    g.exotic = c->d_l_exotic.p;
-    g.off_begin = c->d_l_off_begin.p;
-    g.off_val = c->d_l_off_val.p;
-    g.ct_code = c->d_l_ct.p;
-    g.rt_code = c->d_l_rt.p;
-    g.off_price = c->d_l_price.p;
-    g.off_avail = c->d_l_avail.p;
-    g.off_rcap = c->d_l_rcap.p;
-    g.L = n;
-    g.req = c->d_l_req.p;
-    g.keys = c->d_l_keys.p;
-    g.mins = c->d_l_mins.p;
-    g.words = c->d_l_words.p;
-    g.requests = c->d_l_rq.p;
-    g.out_hdr = c->d_l_hdr.p;
-    g.out_types = c->d_l_types.p;
-    g.out_over = c->d_l_over.p;
-    const auto t_up = clk::now();
-    HIPCHK(hipEventRecord(c->ev[0], s));
-    HIPCHK(kp_launch_select_kernel(g, s));
-    HIPCHK(hipEventRecord(c->ev[1], s));
     HIPCHK(c->p_l_hdr.ensure((size_t)std::max(1, n) * KL_HDR));
     HIPCHK(c->p_l_types.ensure((size_t)std::max(1, n) * M));
     HIPCHK(c->p_l_over.ensure((size_t)std::max(1, n) * M));
+    for (auto& e : c->lev)
+        if (!e) HIPCHK(hipEventCreate(&e));
+    KpLaunch g0{};
+    g0.T = T;
+    g0.TW = c->TW;
+    g0.R = R;
+    g0.M = M;
+    g0.type_val = c->d_type_val.p;
+    g0.multi_mask = c->d_multi_mask.p;
+    g0.dne_mask = c->d_dne_mask.p;
+    g0.alloc = c->d_alloc.p;
+    g0.name_rank = c->d_name_rank.p;
+    g0.exotic = c->d_l_exotic.p;
+    g0.off_begin = c->d_l_off_begin.p;
+    g0.off_val = c->d_l_off_val.p;
+    g0.ct_code = c->d_l_ct.p;
+    g0.rt_code = c->d_l_rt.p;
+    g0.off_price = c->d_l_price.p;
+    g0.off_avail = c->d_l_avail.p;
+    g0.off_rcap = c->d_l_rcap.p;
     const int32_t* const hdr = c->p_l_hdr.p;
     const int32_t* const tys = c->p_l_types.p;
     const uint64_t* const ov = c->p_l_over.p;
-    if (n > 0) {
-        HIPCHK(hipMemcpyAsync(c->p_l_hdr.p, c->d_l_hdr.p, (size_t)n * KL_HDR * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(c->p_l_types.p, c->d_l_types.p, (size_t)n * M * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(c->p_l_over.p, c->d_l_over.p, (size_t)n * M * 8, hipMemcpyDeviceToHost, s));
-    }
-    HIPCHK(hipStreamSynchronize(s));
-    float kms = 0.f;
-    HIPCHK(hipEventElapsedTime(&kms, c->ev[0], c->ev[1]));
-    c->launch_ms[0] = kms;
-    const auto t_dl = clk::now();
     // result rows: counts first (type_offset / override_offset are prefix sums), then the lists, per thread range
     std::vector<int64_t> toff(n + 1, 0), ooff(n + 1, 0);
-    auto par = [&](auto fn) {  // fn(i0, i1) over nthr contiguous ranges (the ctx's worker threads)
-        if (nthr == 1 || n < 1024) {
-            fn(0, n);
+    auto par = [&](int i0, int i1, auto fn) {  // fn(a, b) over contiguous ranges of [i0, i1) (the ctx's worker threads)
+        const int k = std::max(1, std::min(nthr, (i1 - i0) / 256));
+        if (k == 1) {
+            fn(i0, i1);
             return;
         }
-        c->pool.run(nthr, [&](int ti) { fn((int)((int64_t)n * ti / nthr), (int)((int64_t)n * (ti + 1) / nthr)); });
+        c->pool.run(k, [&](int ti) { fn(i0 + (int)((int64_t)(i1 - i0) * ti / k), i0 + (int)((int64_t)(i1 - i0) * (ti + 1) / k)); });
     };
-    par([&](int i0, int i1) {
-        for (int i = i0; i < i1; i++) {
-            const int nt = hdr[(size_t)i * KL_HDR + 3];
-            int64_t no = 0;
-            for (int k = 0; k < nt; k++) no += __builtin_popcountll(ov[(size_t)i * M + k]);
-            toff[i + 1] = nt;
-            ooff[i + 1] = no;
+    double ms_enc = 0, ms_up = 0, ms_wait = 0, ms_exp = 0;
+    float kms_sum = 0.f;
+    auto ms_between = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    auto expand = [&](int b) -> hipError_t {
+        const auto tw = clk::now();
+        hipError_t he = hipEventSynchronize(c->lev[3 * b + 2]);
+        float k = 0.f;
+        if (he == hipSuccess) he = hipEventElapsedTime(&k, c->lev[3 * b], c->lev[3 * b + 1]);
+        if (he != hipSuccess) return he;
+        kms_sum += k;
+        const auto tx = clk::now();
+        ms_wait += ms_between(tw, tx);
+        const int s0 = sub_begin(b), s1 = sub_begin(b + 1);
+        par(s0, s1, [&](int i0, int i1) {
+            for (int i = i0; i < i1; i++) {
+                const int nt = hdr[(size_t)i * KL_HDR + 3];
+                int64_t no = 0;
+                for (int k = 0; k < nt; k++) no += __builtin_popcountll(ov[(size_t)i * M + k]);
+                toff[i + 1] = nt;
+                ooff[i + 1] = no;
+            }
+        });
+        for (int i = s0; i < s1; i++) {
+            toff[i + 1] += toff[i];
+            ooff[i + 1] += ooff[i];
         }
-    });
-    for (int i = 0; i < n; i++) {
-        toff[i + 1] += toff[i];
-        ooff[i + 1] += ooff[i];
-    }
-    const bool short_buf = (n > 0 && toff[n] > 0 && (!type_ids || toff[n] > cap_type_ids)) ||
-                           (n > 0 && ooff[n] > 0 && (!override_offerings || ooff[n] > cap_overrides));
-    par([&](int i0, int i1) {
-        for (int i = i0; i < i1; i++) {
-            const int32_t* h = &hdr[(size_t)i * KL_HDR];
-            kp_launch_result& r = results[i];
-            r.status = h[0];
-            r.failed_filter = h[1];
-            r.capacity_type = h[2];
-            r.n_types = h[3];
-            r.n_options = h[5];
-            for (int f = 0; f < KP_N_FILTERS; f++) r.rejected[f] = h[8 + f];
-            r.type_offset = (int32_t)toff[i];
-            r.override_offset = (int32_t)ooff[i];
-            r.n_overrides = (int32_t)(ooff[i + 1] - ooff[i]);
-            int64_t tp = toff[i], op = ooff[i];
-            for (int k = 0; k < r.n_types; k++, tp++) {
-                const int32_t t = tys[(size_t)i * M + k];
-                if (type_ids && tp < cap_type_ids) type_ids[tp] = t;
-                // override offerings of slot k: bit j = offering row off_begin[t] + j, ascending
-                for (uint64_t m = ov[(size_t)i * M + k]; m; m &= m - 1, op++)
-                    if (override_offerings && op < cap_overrides) override_offerings[op] = c->l_off_begin[t] + __builtin_ctzll(m);
+        par(s0, s1, [&](int i0, int i1) {
+            for (int i = i0; i < i1; i++) {
+                const int32_t* h = &hdr[(size_t)i * KL_HDR];
+                kp_launch_result& r = results[i];
+                r.status = h[0];
+                r.failed_filter = h[1];
+                r.capacity_type = h[2];
+                r.n_types = h[3];
+                r.n_options = h[5];
+                for (int f = 0; f < KP_N_FILTERS; f++) r.rejected[f] = h[8 + f];
+                r.type_offset = (int32_t)toff[i];
+                r.override_offset = (int32_t)ooff[i];
+                r.n_overrides = (int32_t)(ooff[i + 1] - ooff[i]);
+                int64_t tp = toff[i], op = ooff[i];
+                for (int k = 0; k < r.n_types; k++, tp++) {
+                    const int32_t t = tys[(size_t)i * M + k];
+                    if (type_ids && tp < cap_type_ids) type_ids[tp] = t;
+                    // override offerings of slot k: bit j = offering row off_begin[t] + j, ascending
+                    for (uint64_t m = ov[(size_t)i * M + k]; m; m &= m - 1, op++)
+                        if (override_offerings && op < cap_overrides) override_offerings[op] = c->l_off_begin[t] + __builtin_ctzll(m);
+                }
+            }
+        });
+        ms_exp += ms_between(tx, clk::now());
+        return hipSuccess;
+    };
+    c->pool.grow(nthr);
+    for (int b = 0; b < nsub; b++) {
+        const int s0 = sub_begin(b), s1 = sub_begin(b + 1), ns = s1 - s0;
+        const int nt = std::max(1, std::min(nthr, (ns + 255) / 256));
+        const auto te0 = clk::now();
+        for (auto& ch : chunks) {
+            ch.keys.clear();
+            ch.mins.clear();
+            ch.words.clear();
+        }
+        c->pool.run(nt, [&](int ti) {
+            const int i0 = s0 + (int)((int64_t)ns * ti / nt), i1 = s0 + (int)((int64_t)ns * (ti + 1) / nt);
+            for (int i = i0; i < i1; i++)
+                if (!encode_one(i, chunks[ti])) return;
+        });
+        const auto te1 = clk::now();
+        ms_enc += ms_between(te0, te1);
+        // chunk tables concatenated straight into pinned staging, offsets rebased per chunk
+        size_t nk = 0, nm = 0, nw = 0;
+        for (int ti = 0; ti < nt; ti++) {
+            if (chunks[ti].st != KP_OK) {
+                hipStreamSynchronize(s);  // no copy may still read the staging when the caller sees the error
+                return fail(c, chunks[ti].st, chunks[ti].msg);
+            }
+            nk += chunks[ti].keys.size();
+            nm += chunks[ti].mins.size();
+            nw += chunks[ti].words.size();
+        }
+        const int set = b & 1;
+        HIPCHK(c->p_l_keys[set].ensure(std::max<size_t>(nk, 1)));
+        HIPCHK(c->p_l_mins[set].ensure(std::max<size_t>(nm, 1)));
+        HIPCHK(c->p_l_words[set].ensure(std::max<size_t>(nw, 1)));
+        {
+            size_t kb = 0, mb = 0, wbase = 0;
+            for (int ti = 0; ti < nt; ti++) {
+                Chunk& ch = chunks[ti];
+                const int i0 = s0 + (int)((int64_t)ns * ti / nt), i1 = s0 + (int)((int64_t)ns * (ti + 1) / nt);
+                for (int i = i0; i < i1; i++) {
+                    KlReq& q = reqs[i];
+                    q.key_off += (int)kb;
+                    q.und_off += (int)kb;
+                    q.min_off += (int)mb;
+                    for (int r = 0; r < KL_ROLES; r++)
+                        if (q.role[r].mode == KLR_CONSTRAINED) q.role[r].woff += (int)wbase;
+                }
+                KlKey* kd = c->p_l_keys[set].p + kb;
+                for (size_t j = 0; j < ch.keys.size(); j++) {
+                    kd[j] = ch.keys[j];
+                    kd[j].woff += (int)wbase;  // undefined-key entries carry no bitset; their woff is never read
+                }
+                if (!ch.mins.empty()) memcpy(c->p_l_mins[set].p + mb, ch.mins.data(), ch.mins.size() * sizeof(KlMinKey));
+                if (!ch.words.empty()) memcpy(c->p_l_words[set].p + wbase, ch.words.data(), ch.words.size() * sizeof(uint64_t));
+                kb += ch.keys.size();
+                mb += ch.mins.size();
+                wbase += ch.words.size();
             }
         }
-    });
+        KpLaunch g = g0;
+        g.L = ns;
+        if (ns > 0) {
+            auto up = [&](auto& dbuf, const auto* src, size_t count) -> hipError_t {
+                hipError_t e = dbuf.ensure(std::max<size_t>(count, 1));
+                if (e != hipSuccess || count == 0) return e;
+                return hipMemcpyAsync(dbuf.p, src, count * sizeof(*src), hipMemcpyHostToDevice, s);
+            };
+            HIPCHK(hipMemcpyAsync(c->d_l_req.p + s0, reqs + s0, (size_t)ns * sizeof(KlReq), hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(c->d_l_rq.p + (size_t)s0 * R, rq + (size_t)s0 * R, (size_t)ns * R * sizeof(int64_t),
+                                  hipMemcpyHostToDevice, s));
+            HIPCHK(up(c->d_l_keys[set], c->p_l_keys[set].p, nk));
+            HIPCHK(up(c->d_l_mins[set], c->p_l_mins[set].p, nm));
+            HIPCHK(up(c->d_l_words[set], c->p_l_words[set].p, nw));
+            g.req = c->d_l_req.p + s0;
+            g.keys = c->d_l_keys[set].p;
+            g.mins = c->d_l_mins[set].p;
+            g.words = c->d_l_words[set].p;
+            g.requests = c->d_l_rq.p + (size_t)s0 * R;
+            g.out_hdr = c->d_l_hdr.p + (size_t)s0 * KL_HDR;
+            g.out_types = c->d_l_types.p + (size_t)s0 * M;
+            g.out_over = c->d_l_over.p + (size_t)s0 * M;
+        }
+        HIPCHK(hipEventRecord(c->lev[3 * b], s));
+        if (ns > 0) HIPCHK(kp_launch_select_kernel(g, s));
+        HIPCHK(hipEventRecord(c->lev[3 * b + 1], s));
+        if (ns > 0) {
+            HIPCHK(hipMemcpyAsync(c->p_l_hdr.p + (size_t)s0 * KL_HDR, g.out_hdr, (size_t)ns * KL_HDR * 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(c->p_l_types.p + (size_t)s0 * M, g.out_types, (size_t)ns * M * 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(c->p_l_over.p + (size_t)s0 * M, g.out_over, (size_t)ns * M * 8, hipMemcpyDeviceToHost, s));
+        }
+        HIPCHK(hipEventRecord(c->lev[3 * b + 2], s));
+        ms_up += ms_between(te1, clk::now());
+        if (b > 0) HIPCHK(expand(b - 1));
+    }
+    HIPCHK(expand(nsub - 1));
+    const bool short_buf = (n > 0 && toff[n] > 0 && (!type_ids || toff[n] > cap_type_ids)) ||
+                           (n > 0 && ooff[n] > 0 && (!override_offerings || ooff[n] > cap_overrides));
+    c->launch_ms[0] = kms_sum;  // Σ kernel time over the sub-batches
     c->launch_ms[1] = ns_since(t0) / 1e6;
-    auto ms_between = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-    c->launch_ms[2] = ms_between(t0, t_enc);
-    c->launch_ms[3] = ms_between(t_enc, t_up);
-    c->launch_ms[4] = ms_between(t_up, t_dl);
-    c->launch_ms[5] = ms_between(t_dl, clk::now());
+    c->launch_ms[2] = ms_enc;
+    c->launch_ms[3] = ms_up;
+    c->launch_ms[4] = ms_wait;
+    c->launch_ms[5] = ms_exp;
+    c->launch_nsub = nsub;
     if (short_buf) return fail(c, KP_E_BUFFER, "type_ids / override_offerings too small");
     return KP_OK;
 } catch (const std::exception& e) {
@@ -3361,5 +3422,6 @@ extern "C" kp_status kp_nodeclaim_labels(kp_ctx* ctx, int32_t type_index, int32_
 extern "C" kp_status kp_launch_stats(kp_ctx* ctx, double* ms, int32_t n) {
     if (!ctx || !ms) return KP_E_INVALID;
     for (int i = 0; i < n && i < 6; i++) ms[i] = ctx->launch_ms[i];
+    if (n > 6) ms[6] = ctx->launch_nsub;
     return KP_OK;
 }

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #define KL_MAX_OFF 64        // offerings per instance type (u64 masks)
+#define KL_MAX_SUB 4         // sub-batches of one kp_launch_select call (host / device pipeline)
 #define KL_ROLES 5           // offering requirement keys: zone, capacity-type, zone-id, reservation-id, reservation-type
 #define KL_ROLE_ZONE 0
 #define KL_ROLE_CT 1

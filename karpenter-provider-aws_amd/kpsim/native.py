@@ -133,7 +133,8 @@ class Context:
         return labels, cap, alloc
 
     def launch_stats(self, n=2):
-        """[kernel ms, whole call ms] (n=6 adds the host phases: encode, merge + upload, kernel + download, expand)."""
+        """[kernel ms, whole call ms] (n=6 adds the host phases: encode, merge + upload, download waits, expand;
+        n=7 the number of sub-batches the call was pipelined over)."""
         ms = (C.c_double * n)()
         self.check(self.L.kp_launch_stats(self.h, ms, n), "kp_launch_stats")
         return list(ms)

@@ -87,6 +87,7 @@ hipError_t hipEventRecord(hipEvent_t e, hipStream_t) {
     e->ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
     return hipSuccess;
 }
+hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
 hipError_t hipEventElapsedTime(float* ms, hipEvent_t a, hipEvent_t b) {
     *ms = (float)((b->ns - a->ns) * 1e-6);
     return hipSuccess;

@@ -229,6 +229,14 @@ int worker(const Catalog& cat, const Problem& pb, int id, int iters, std::vector
         int32_t tids[60], ovr[256];
         const kp_status ls = kp_launch_select(ctx, 1, &lr, 60, res, tids, 60, ovr, 256);
         CHECK(ls == KP_OK);
+        if (it == 0) {  // a batch large enough to be pipelined over sub-batches on the ctx's worker pool
+            std::vector<kp_launch_request> big(4500, lr);
+            std::vector<kp_launch_result> bres(big.size());
+            CHECK(kp_launch_select(ctx, (int32_t)big.size(), big.data(), 60, bres.data(), tids, 60, ovr, 256) == KP_OK);
+            double st[7];
+            CHECK(kp_launch_stats(ctx, st, 7) == KP_OK && st[6] == 2);
+            for (const auto& r : bres) CHECK(r.n_types == 0 && r.type_offset == 0);
+        }
         if (it == 0) *sig = so.pres;
         else CHECK(*sig == so.pres);
     }

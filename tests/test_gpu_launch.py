@@ -46,6 +46,35 @@ def test_config5_batch_parity(ctx, golden, seed):
     assert (dev.rows["status"] == abi.KP_E_INSUFFICIENT_CAPACITY).sum() > 0
 
 
+def test_pipelined_batch_parity(ctx, golden):
+    """A batch of >= 4096 requests is evaluated as sub-batches (host encoding and expansion overlap the kernel): equal
+    to the oracle, and to the same requests selected in small single-launch calls (offsets rebased per call)."""
+    cat = synth.config5_catalog(golden, seed=synth.SEED + 5)
+    reqs = synth.launch_requests(cat, n=6200, seed=synth.SEED + 5)
+    cv = model.CatalogView(cat)
+    ctx.upload_catalog(cv)
+    dev = ctx.launch_select(model.LaunchBatchView(reqs), 60)
+    assert ctx.launch_stats(7)[6] == 3
+    st, orc = pyoracle.launch_select(cv, model.LaunchBatchView(reqs[:2500]), 60)
+    assert st == abi.KP_OK
+    for i in range(2500):  # the first sub-batch boundary (2066) lies inside
+        for f in ("status", "failed_filter", "n_types", "n_options", "n_overrides"):
+            assert int(dev.rows[i][f]) == int(orc.rows[i][f]), (i, f)
+        assert list(dev.rows[i]["rejected"]) == list(orc.rows[i]["rejected"]), i
+        if int(dev.rows[i]["status"]) == abi.KP_OK:
+            assert int(dev.rows[i]["capacity_type"]) == int(orc.rows[i]["capacity_type"]), i
+        assert list(dev.types(i)) == list(orc.types(i)), i
+        assert list(dev.offerings(i)) == list(orc.offerings(i)), i
+    for b0 in range(0, len(reqs), 1000):
+        part = ctx.launch_select(model.LaunchBatchView(reqs[b0:b0 + 1000]), 60)
+        assert ctx.launch_stats(7)[6] == 1
+        for i in range(len(part.rows)):
+            for f in ("status", "failed_filter", "n_types", "n_options", "n_overrides", "capacity_type"):
+                assert int(part.rows[i][f]) == int(dev.rows[b0 + i][f]), (b0 + i, f)
+            assert list(part.types(i)) == list(dev.types(b0 + i)), b0 + i
+            assert list(part.offerings(i)) == list(dev.offerings(b0 + i)), b0 + i
+
+
 def test_patches_reach_launch(ctx, golden):
     """ICE marks and price refreshes (kp_catalog_patch_avail / _price) change the launch result like a re-List."""
     cat = synth.config5_catalog(golden)
