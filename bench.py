@@ -187,14 +187,15 @@ def launch_leg(a, golden, local, rank, world, dist, barrier):
     barrier()
     kms, cms = [], []
     t0 = time.perf_counter()
-    phases = []
+    phases, busy = [], []
     for _ in range(a.steps):
         res = ctx.launch_select(batch, 60)
-        st7 = ctx.launch_stats(7)
-        kms.append(st7[0])
-        cms.append(st7[1])
-        phases.append(st7[2:6])
-        nsub = int(st7[6])
+        st8 = ctx.launch_stats(8)
+        kms.append(st8[0])
+        cms.append(st8[1])
+        phases.append(st8[2:6])
+        nsub = int(st8[6])
+        busy.append(st8[7])
     elapsed = time.perf_counter() - t0
     barrier()
     kern = float(np.mean(kms))
@@ -213,7 +214,8 @@ def launch_leg(a, golden, local, rank, world, dist, barrier):
         "unit": "nodeclaims/s",
         "n_gpus": world,
         "steps": a.steps,
-        "kernel_ms": kern,
+        "kernel_ms": kern,  # Σ launch_kernel durations of the call's sub-batches (≥ the device busy time below)
+        "device_busy_ms": float(np.mean(busy)),
         "call_ms": float(np.mean(cms)),
         # the call pipelines nsub sub-batches: host encoding / expansion of one overlaps the kernel of another, so the
         # phases below are host-side sums (wait_download = time the host waited for a sub-batch's kernel + download)

@@ -454,8 +454,9 @@ kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_request* requ
                            int32_t* override_offerings, int32_t cap_overrides);
 /* Of the last kp_launch_select: ms[0] = launch kernel time (HIP events on the ctx stream, summed over the call's
  * sub-batches), ms[1] = whole call; host phases ms[2] = request encoding, ms[3] = table merge + upload, ms[4] = waits
- * for kernel + result download, ms[5] = result expansion; ms[6] = number of sub-batches.  A batch of >= 4096 requests
- * is cut into up to 4 sub-batches so that encoding and expansion on the host overlap the kernel. */
+ * for kernel + result download, ms[5] = result expansion; ms[6] = number of sub-batches, ms[7] = device busy time (union
+ * of the sub-batch kernels, which overlap on two streams).  A batch of >= 4096 requests is cut into up to 4 sub-batches
+ * so that encoding and expansion on the host overlap the kernels. */
 kp_status kp_launch_stats(kp_ctx* ctx, double* ms, int32_t n);
 
 /*

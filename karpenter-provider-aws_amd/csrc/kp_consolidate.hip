@@ -363,6 +363,9 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
         bool aborted = false;
         int cbase = -1, ccls = -1;  // cached node chunk (wave-uniform)
         uint64_t cx = 0;
+        // the cached chunk's words of the modified-node bitmap (written back to LDS when the chunk is evicted) and of
+        // the initialized-node bitmap: the per-pod commit touches no LDS
+        uint64_t cmod = 0, cinit = 0;
         int64_t ch[KP_LDS_AXES], cd[KP_LDS_AXES];
 #pragma unroll
         for (int ai = 0; ai < KP_LDS_AXES; ai++) ch[ai] = cd[ai] = 0;
@@ -379,6 +382,8 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             ccls = __builtin_amdgcn_readfirstlane(ccls);
             prev_shape = __builtin_amdgcn_readfirstlane(prev_shape);
             cx = uni64(cx);
+            cmod = uni64(cmod);
+            cinit = uni64(cinit);
             if (head - wbase >= 64) win_load(head);
             const int off = head - wbase;
             const int ent = rl32(vpod, off);
@@ -409,7 +414,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 const int w = base >> 6;
                 const int j = base + lane;
                 const uint64_t ge = xstart > base ? (~0ull << (xstart - base)) : ~0ull;
-                uint64_t xw;
+                uint64_t xw, mw = 0;
                 int64_t h[KP_LDS_AXES], dl[KP_LDS_AXES];
                 if (base == cbase) {
                     st_hits++;
@@ -430,7 +435,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                         continue;
                     }
                     st_loads++;
-                    const uint64_t mw = uni64(modb[w]);
+                    mw = uni64(modb[w]);  // not the cached chunk's word: LDS is current
                     if (mw & xw) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this probe's delta stores landed
                     const bool md = (mw >> lane) & 1ull;
 #pragma unroll
@@ -454,7 +459,8 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     jf = __builtin_amdgcn_readfirstlane(base + __ffsll((unsigned long long)m) - 1);
                     if (base != cbase) {
                         // evict: this probe's requests on the old chunk go to the delta slab (read back past L1)
-                        if (cbase >= 0 && ((modb[cbase >> 6] >> lane) & 1ull)) {
+                        if (cbase >= 0 && lane == 0) modb[cbase >> 6] = cmod;
+                        if (cbase >= 0 && ((cmod >> lane) & 1ull)) {
 #pragma unroll
                             for (int ai = 0; ai < KP_LDS_AXES; ai++)
                                 if (ai < A)
@@ -466,6 +472,8 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                         cbase = base;
                         cx = xw;
                         ccls = c;
+                        cmod = mw;
+                        cinit = uni64(initb[w]);
 #pragma unroll
                         for (int ai = 0; ai < KP_LDS_AXES; ai++) {
                             ch[ai] = h[ai];
@@ -486,11 +494,11 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                         }
                     }
                 }
-                if (lane == 0) modb[jf >> 6] |= 1ull << (jf & 63);
+                cmod |= 1ull << (jf & 63);  // jf lies in the cached chunk
                 xstart = jf;
                 st_placed++;
                 if (!pend) {
-                    if ((uni64(initb[jf >> 6]) >> (jf & 63)) & 1ull) ok_np++;
+                    if ((cinit >> (jf & 63)) & 1ull) ok_np++;
                     else bad = true;  // SimulateScheduling: uninitialized-node placement is an error
                 }
                 continue;

@@ -263,14 +263,12 @@ struct PrefExpansion {
 
 // Persistent worker threads of a ctx for the host-side batch work of kp_launch_select (request encoding, result
 // expansion): run(k, fn) calls fn(0..k-1) across the workers and the calling thread and returns when all are done.
-// A pipelined call issues several runs within a millisecond, so an idle worker spins on the generation counter for a
-// while before it sleeps on the condition variable (a futex wake-up of 15 threads costs ~0.3 ms per run).
 class WorkerPool {
   public:
     ~WorkerPool() {
         {
             std::lock_guard<std::mutex> g(mu_);
-            stop_.store(true);
+            stop_ = true;
         }
         cv_.notify_all();
         for (auto& t : th_) t.join();
@@ -284,63 +282,55 @@ class WorkerPool {
             for (int i = 0; i < k; i++) fn(i);
             return;
         }
-        const uint32_t g = (gen_.load(std::memory_order_relaxed) + 1) & kGenMask;
-        fn_ = &fn;  // published by the release store of claim_ (a claim acquires it)
-        left_.store(k, std::memory_order_relaxed);
-        claim_.store(((uint64_t)g << 40) | ((uint64_t)k << 20), std::memory_order_release);
         {
-            std::lock_guard<std::mutex> lk(mu_);  // a worker about to sleep re-checks gen_ under the lock
-            gen_.store(g, std::memory_order_release);
+            std::lock_guard<std::mutex> g(mu_);
+            fn_ = &fn;
+            next_ = 0;
+            tasks_ = k;
+            left_ = k;
+            gen_++;
         }
         cv_.notify_all();
-        work(g);
-        while (left_.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
+        work();
+        std::unique_lock<std::mutex> g(mu_);
+        done_.wait(g, [this] { return left_ == 0; });
+        fn_ = nullptr;
     }
 
   private:
-    static constexpr uint32_t kGenMask = (1u << 24) - 1;
-    // claim_ = generation << 40 | tasks << 20 | next task: a worker still inside an older generation cannot claim
-    void work(uint32_t g) {
-        uint64_t v = claim_.load(std::memory_order_acquire);
+    void work() {
         for (;;) {
-            if ((uint32_t)(v >> 40) != g) return;
-            const int tasks = (int)((v >> 20) & 0xFFFFF), i = (int)(v & 0xFFFFF);
-            if (i >= tasks) return;
-            if (!claim_.compare_exchange_weak(v, v + 1, std::memory_order_acq_rel, std::memory_order_acquire)) continue;
-            (*fn_)(i);
-            left_.fetch_sub(1, std::memory_order_release);
-            v = claim_.load(std::memory_order_acquire);
+            int i;
+            const std::function<void(int)>* f;
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                if (!fn_ || next_ >= tasks_) return;
+                i = next_++;
+                f = fn_;
+            }
+            (*f)(i);
+            std::lock_guard<std::mutex> g(mu_);
+            if (--left_ == 0) done_.notify_all();
         }
     }
     void loop() {
-        uint32_t seen = gen_.load(std::memory_order_acquire);
+        int seen = 0;
         for (;;) {
-            uint32_t g = seen;
-            const auto t0 = std::chrono::steady_clock::now();
-            for (int spins = 1; !stop_.load(std::memory_order_relaxed); spins++) {
-                g = gen_.load(std::memory_order_acquire);
-                if (g != seen) break;
-                __builtin_ia32_pause();
-                if ((spins & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
             }
-            if (g == seen) {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return stop_.load() || gen_.load(std::memory_order_acquire) != seen; });
-                g = gen_.load(std::memory_order_acquire);
-            }
-            if (stop_.load()) return;
-            seen = g;
-            work(g);
+            work();
         }
     }
     std::vector<std::thread> th_;
     std::mutex mu_;
-    std::condition_variable cv_;
+    std::condition_variable cv_, done_;
     const std::function<void(int)>* fn_ = nullptr;
-    std::atomic<uint64_t> claim_{0};
-    std::atomic<int> left_{0};
-    std::atomic<uint32_t> gen_{0};
-    std::atomic<bool> stop_{false};
+    int next_ = 0, tasks_ = 0, left_ = 0, gen_ = 0;
+    bool stop_ = false;
 };
 
 // Pinned host staging buffer, grow-only (launch-request tables: DMA without the pageable-copy staging).
@@ -374,6 +364,7 @@ struct PinBuf {
 struct kp_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t lstream2 = nullptr;          // kp_launch_select: odd sub-batches (their kernels overlap the even ones' tails)
     // kp_device_opts.devices[1..n): one ctx per further device (own stream, own copies of the catalog and of the
     // prepared consolidation pass).  Catalog uploads / patches and kp_consolidate_prepare run on every device (one host
     // thread each); kp_consolidate_execute splits the probe range into one contiguous shard per device and gathers the
@@ -493,6 +484,7 @@ struct kp_ctx {
     double launch_ms[6] = {};                // Σ launch kernel, whole call; host phases: encode, merge + upload,
                                              // waits for the downloads, result expansion
     int launch_nsub = 0;                     // sub-batches of the last call
+    double launch_busy_ms = 0;               // union of the call's kernel intervals (overlapping sub-batch kernels)
     hipEvent_t lev[3 * KL_MAX_SUB] = {};     // per sub-batch: kernel start, kernel end, download landed
     // topology (kp_solve_prepare encodes the groups; execute resets the counts from the *0 copies)
     int tg_G = 0, tg_HG = 0;
@@ -608,6 +600,10 @@ extern "C" kp_status kp_ctx_destroy(kp_ctx* ctx) {
         if (e) hipEventDestroy(e);
     for (auto& e : ctx->lev)
         if (e) hipEventDestroy(e);
+    if (ctx->lstream2) {
+        hipStreamSynchronize(ctx->lstream2);
+        hipStreamDestroy(ctx->lstream2);
+    }
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;  // every DBuf member frees its device memory (on the device set above)
     return KP_OK;
@@ -3157,10 +3153,14 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
     // results of b-1 are expanded once its download has landed.  The request rows (KlReq, requests) and the result
     // rows live at their batch positions; the key / minValues / word tables of sub-batch b go to staging set b & 1,
     // which is free again because sub-batch b-2's download (queued behind its kernel) was waited for before b is
-    // encoded.
-    int nsub = n >= 4096 ? std::min(KL_MAX_SUB, n / 2048) : 1;
+    // encoded.  Sub-batch b runs on stream b & 1, so a kernel's start overlaps the previous kernel's tail of long
+    // workgroups.
+    // two halves measured best on MI355X for the 10k config-5 batch (call 4.3 -> 3.1 ms; each extra launch costs ~0.17 ms
+    // of kernel ramp and tail, and the host encoding of a half outlasts the kernel of the other)
+    int nsub = n >= 4096 ? 2 : 1;
     if (const char* e = getenv("KPSIM_LAUNCH_SUB")) nsub = std::max(1, std::min({KL_MAX_SUB, atoi(e), std::max(1, n)}));
     const auto sub_begin = [&](int b) { return (int)((int64_t)n * b / nsub); };
+    if (nsub > 1 && !c->lstream2) HIPCHK(hipStreamCreateWithFlags(&c->lstream2, hipStreamNonBlocking));
     hipStream_t s = c->stream;
     if (n > 0) {
         HIPCHK(c->d_l_req.ensure((size_t)n));
@@ -3207,14 +3207,18 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
     };
     double ms_enc = 0, ms_up = 0, ms_wait = 0, ms_exp = 0;
     float kms_sum = 0.f;
+    std::pair<float, float> span[KL_MAX_SUB];  // kernel intervals after the first kernel's start (device busy time)
     auto ms_between = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     auto expand = [&](int b) -> hipError_t {
         const auto tw = clk::now();
         hipError_t he = hipEventSynchronize(c->lev[3 * b + 2]);
         float k = 0.f;
         if (he == hipSuccess) he = hipEventElapsedTime(&k, c->lev[3 * b], c->lev[3 * b + 1]);
+        float k0 = 0.f;
+        if (he == hipSuccess && b > 0) he = hipEventElapsedTime(&k0, c->lev[0], c->lev[3 * b]);
         if (he != hipSuccess) return he;
         kms_sum += k;
+        span[b] = {k0, k0 + k};
         const auto tx = clk::now();
         ms_wait += ms_between(tw, tx);
         const int s0 = sub_begin(b), s1 = sub_begin(b + 1);
@@ -3261,6 +3265,7 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
     for (int b = 0; b < nsub; b++) {
         const int s0 = sub_begin(b), s1 = sub_begin(b + 1), ns = s1 - s0;
         const int nt = std::max(1, std::min(nthr, (ns + 255) / 256));
+        s = (b & 1) ? c->lstream2 : c->stream;
         const auto te0 = clk::now();
         for (auto& ch : chunks) {
             ch.keys.clear();
@@ -3278,7 +3283,8 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
         size_t nk = 0, nm = 0, nw = 0;
         for (int ti = 0; ti < nt; ti++) {
             if (chunks[ti].st != KP_OK) {
-                hipStreamSynchronize(s);  // no copy may still read the staging when the caller sees the error
+                hipStreamSynchronize(c->stream);  // no copy may still read the staging when the caller sees the error
+                if (c->lstream2) hipStreamSynchronize(c->lstream2);
                 return fail(c, chunks[ti].st, chunks[ti].msg);
             }
             nk += chunks[ti].keys.size();
@@ -3353,6 +3359,16 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
     const bool short_buf = (n > 0 && toff[n] > 0 && (!type_ids || toff[n] > cap_type_ids)) ||
                            (n > 0 && ooff[n] > 0 && (!override_offerings || ooff[n] > cap_overrides));
     c->launch_ms[0] = kms_sum;  // Σ kernel time over the sub-batches
+    {
+        std::sort(span, span + nsub);
+        double busy = 0, hi = -1;
+        for (int b = 0; b < nsub; b++) {
+            const double lo = std::max<double>(span[b].first, hi);
+            if (span[b].second > lo) busy += span[b].second - lo;
+            hi = std::max<double>(hi, span[b].second);
+        }
+        c->launch_busy_ms = busy;
+    }
     c->launch_ms[1] = ns_since(t0) / 1e6;
     c->launch_ms[2] = ms_enc;
     c->launch_ms[3] = ms_up;
@@ -3423,5 +3439,6 @@ extern "C" kp_status kp_launch_stats(kp_ctx* ctx, double* ms, int32_t n) {
     if (!ctx || !ms) return KP_E_INVALID;
     for (int i = 0; i < n && i < 6; i++) ms[i] = ctx->launch_ms[i];
     if (n > 6) ms[6] = ctx->launch_nsub;
+    if (n > 7) ms[7] = ctx->launch_busy_ms;
     return KP_OK;
 }

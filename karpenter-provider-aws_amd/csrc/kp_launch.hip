@@ -27,17 +27,37 @@ namespace {
 constexpr int NT = 256;
 constexpr int NWV = NT / 64;
 
-struct LShared {
-    uint64_t lv[KP_MAX_TYPES], cmn[KP_MAX_TYPES], ctok[KP_MAX_TYPES], am[KP_MAX_TYPES], tmp[KP_MAX_TYPES];
-    double key[KP_MAX_TYPES];
-    uint8_t keep[KP_MAX_TYPES];
-    uint8_t aux[KP_MAX_TYPES];
-    int16_t pos[KP_MAX_TYPES];
-    uint64_t minbits[KP_MAX_MIN_WORDS];
+struct LShared {  // reductions (static LDS)
     double redd[NWV];
     int redi[NWV];
     int ncomp;
 };
+
+// Per-type LDS arrays, sized by the catalog's T at launch (launch_lds_bytes): ≈32 KB at T = 918, i.e. 5 workgroups
+// per CU.  ctok doubles as the Truncate stage's order keys once every type's mask is in registers; key holds the
+// CapacityBlockFilter / Truncate prices, the ReservedOfferingFilter winners (win) and, after Truncate, the
+// SatisfiesMinValues bitset (minbits).
+struct LTypes {
+    uint64_t *lv, *ac, *ctok, *win, *minbits;  // live offerings, Available ∧ Compatible w/o capacity type, ct-compatible
+    double* key;
+    uint8_t *keep, *aux;
+    int8_t* pos;  // CapacityBlockFilter offering, then Truncate rank (< M <= 64)
+};
+__host__ __device__ inline int ltypes_key_len(int T) { return T > KP_MAX_MIN_WORDS ? T : KP_MAX_MIN_WORDS; }
+__device__ __forceinline__ LTypes ltypes(char* p, int T) {
+    LTypes L;
+    L.lv = reinterpret_cast<uint64_t*>(p);
+    L.ac = L.lv + T;
+    L.ctok = L.ac + T;
+    L.key = reinterpret_cast<double*>(L.ctok + T);
+    L.win = reinterpret_cast<uint64_t*>(L.key);
+    L.minbits = reinterpret_cast<uint64_t*>(L.key);
+    L.keep = reinterpret_cast<uint8_t*>(L.key + ltypes_key_len(T));
+    L.aux = L.keep + T;
+    L.pos = reinterpret_cast<int8_t*>(L.aux + T);
+    return L;
+}
+inline size_t launch_lds_bytes(int T) { return (size_t)(3 * T + ltypes_key_len(T)) * 8 + 3 * (size_t)T; }
 
 __device__ __forceinline__ bool wbit(const uint64_t* w, int off, int v) { return (w[off + (v >> 6)] >> (v & 63)) & 1ull; }
 
@@ -126,7 +146,9 @@ __device__ __forceinline__ uint64_t ct_mask(const KpLaunch& g, int o0, uint64_t 
 
 __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
     __shared__ LShared S;
+    extern __shared__ __attribute__((aligned(16))) char ldyn[];
     const int i = blockIdx.x, tid = threadIdx.x, T = g.T, M = g.M;
+    const LTypes L = ltypes(ldyn, T);
     const KlReq q = g.req[i];
     const int64_t* rq = g.requests + (size_t)i * g.R;
     int32_t* hdr = g.out_hdr + (size_t)i * KL_HDR;
@@ -148,16 +170,15 @@ __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
             if (g.off_avail[o]) am |= 1ull << j;
         }
         const uint64_t lv = no >= 64 ? ~0ull : ((1ull << no) - 1);
-        S.lv[t] = lv;
-        S.cmn[t] = cmn;
-        S.ctok[t] = ctok;
-        S.am[t] = am;
+        L.lv[t] = lv;
+        L.ac[t] = am & cmn;
+        L.ctok[t] = ctok;
         bool keep = (lv & cmn & ctok & am) != 0;
         if (keep) {
             for (int r = 0; r < g.R && keep; r++) keep = !(rq[r] != 0 && rq[r] > g.alloc[(size_t)r * T + t]);
         }
         keep = keep && type_compat(g, q, t);
-        S.keep[t] = keep;
+        L.keep[t] = keep;
         n += keep;
     }
     n = bsum(n, S);
@@ -170,9 +191,9 @@ __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
         double c0 = DBL_MAX, c1 = DBL_MAX;
         for (int t = tid; t < T; t += NT) {
             uint8_t mem = 0;
-            if (S.keep[t]) {
+            if (L.keep[t]) {
                 const int o0 = g.off_begin[t];
-                uint64_t m = S.lv[t] & S.am[t] & S.cmn[t] & S.ctok[t];
+                uint64_t m = L.lv[t] & L.ac[t] & L.ctok[t];
                 while (m) {
                     const int j = __ffsll((unsigned long long)m) - 1;
                     m &= m - 1;
@@ -189,28 +210,28 @@ __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
                     }
                 }
             }
-            S.aux[t] = mem;
+            L.aux[t] = mem;
         }
         c0 = bmin_d(c0, S);
         c1 = bmin_d(c1, S);
         const int sel = (c1 < c0) ? 1 : 0;  // lo.MinBy: cheaper partition, ties to default (priority 0)
         int cnt = 0;
-        for (int t = tid; t < T; t += NT) cnt += S.keep[t] && ((S.aux[t] >> sel) & 1);
+        for (int t = tid; t < T; t += NT) cnt += L.keep[t] && ((L.aux[t] >> sel) & 1);
         cnt = bsum(cnt, S);
         if (cnt > 0) {
             for (int t = tid; t < T; t += NT) {
-                if (!S.keep[t]) continue;
-                if ((S.aux[t] >> sel) & 1) {
+                if (!L.keep[t]) continue;
+                if ((L.aux[t] >> sel) & 1) {
                     const int o0 = g.off_begin[t];
-                    uint64_t m = S.lv[t], nl = 0;
+                    uint64_t m = L.lv[t], nl = 0;
                     while (m) {
                         const int j = __ffsll((unsigned long long)m) - 1;
                         m &= m - 1;
                         if (g.ct_code[o0 + j] == KP_CT_RESERVED && g.rt_code[o0 + j] == sel) nl |= 1ull << j;
                     }
-                    S.lv[t] = nl;
+                    L.lv[t] = nl;
                 } else {
-                    S.keep[t] = 0;
+                    L.keep[t] = 0;
                 }
             }
             rejected[1] = n - cnt;
@@ -224,9 +245,9 @@ __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
         int first = INT32_MAX;
         for (int t = tid; t < T; t += NT) {
             uint8_t code = 0;
-            if (S.keep[t]) {
+            if (L.keep[t]) {
                 const int o0 = g.off_begin[t];
-                uint64_t m = S.lv[t];
+                uint64_t m = L.lv[t];
                 while (m) {
                     const int j = __ffsll((unsigned long long)m) - 1;
                     m &= m - 1;
@@ -236,18 +257,18 @@ __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
                     }
                 }
             }
-            S.aux[t] = code;
+            L.aux[t] = code;
             if (code) first = min(first, t);
         }
         first = bmin_i(first, S);
-        if (first != INT32_MAX && S.aux[first] == 2) {
+        if (first != INT32_MAX && L.aux[first] == 2) {
             double best = DBL_MAX;
             for (int t = tid; t < T; t += NT) {
-                S.key[t] = DBL_MAX;
-                S.pos[t] = -1;
-                if (!S.keep[t]) continue;
+                L.key[t] = DBL_MAX;
+                L.pos[t] = -1;
+                if (!L.keep[t]) continue;
                 const int o0 = g.off_begin[t];
-                uint64_t m = S.lv[t];
+                uint64_t m = L.lv[t];
                 int sj = -1;
                 double sp = 0.0;
                 while (m) {
@@ -261,19 +282,19 @@ __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
                     }
                 }
                 if (sj >= 0) {
-                    S.key[t] = sp;
-                    S.pos[t] = (int16_t)sj;
+                    L.key[t] = sp;
+                    L.pos[t] = (int8_t)sj;
                     best = sp < best ? sp : best;
                 }
             }
             best = bmin_d(best, S);
             int win = INT32_MAX;
             for (int t = tid; t < T; t += NT)
-                if (S.pos[t] >= 0 && S.key[t] == best) win = min(win, t);
+                if (L.pos[t] >= 0 && L.key[t] == best) win = min(win, t);
             win = bmin_i(win, S);
             for (int t = tid; t < T; t += NT) {
-                if (t == win) S.lv[t] = 1ull << S.pos[t];
-                else S.keep[t] = 0;
+                if (t == win) L.lv[t] = 1ull << L.pos[t];
+                else L.keep[t] = 0;
             }
             rejected[2] = n - 1;
             n = 1;
@@ -284,10 +305,10 @@ __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
     if (failed < 0 && reserved) {
         int cnt = 0;
         for (int t = tid; t < T; t += NT) {
-            S.tmp[t] = 0;
-            if (!S.keep[t]) continue;
+            L.win[t] = 0;
+            if (!L.keep[t]) continue;
             const int o0 = g.off_begin[t];
-            uint64_t cand = S.lv[t] & S.am[t] & S.cmn[t] & S.ctok[t] & ct_mask(g, o0, S.lv[t], KP_CT_RESERVED);
+            uint64_t cand = L.lv[t] & L.ac[t] & L.ctok[t] & ct_mask(g, o0, L.lv[t], KP_CT_RESERVED);
             uint64_t m = cand, win = 0;
             while (m) {  // per zone: the first offering with the greatest ReservationCapacity
                 const int j = __ffsll((unsigned long long)m) - 1;
@@ -305,15 +326,15 @@ __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
                 }
                 if (best) win |= 1ull << j;
             }
-            S.tmp[t] = win;
+            L.win[t] = win;
             cnt += win != 0;
         }
         cnt = bsum(cnt, S);
         if (cnt > 0) {
             for (int t = tid; t < T; t += NT) {
-                if (!S.keep[t]) continue;
-                if (S.tmp[t]) S.lv[t] = S.tmp[t];
-                else S.keep[t] = 0;
+                if (!L.keep[t]) continue;
+                if (L.win[t]) L.lv[t] = L.win[t];
+                else L.keep[t] = 0;
             }
             rejected[3] = n - cnt;
             n = cnt;
@@ -323,11 +344,11 @@ __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
     // ---- ExoticInstanceTypeFilter (filter.go:289-318) ----
     if (failed < 0 && !q.has_min) {
         int cnt = 0;
-        for (int t = tid; t < T; t += NT) cnt += S.keep[t] && !g.exotic[t];
+        for (int t = tid; t < T; t += NT) cnt += L.keep[t] && !g.exotic[t];
         cnt = bsum(cnt, S);
         if (cnt > 0) {
             for (int t = tid; t < T; t += NT)
-                if (g.exotic[t]) S.keep[t] = 0;
+                if (g.exotic[t]) L.keep[t] = 0;
             rejected[4] = n - cnt;
             n = cnt;
         }
@@ -338,9 +359,9 @@ __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
         double cod = DBL_MAX;
         int has_od = 0, has_spot = 0;
         for (int t = tid; t < T; t += NT) {
-            if (!S.keep[t]) continue;
+            if (!L.keep[t]) continue;
             const int o0 = g.off_begin[t];
-            uint64_t m = S.lv[t] & S.am[t] & S.cmn[t] & S.ctok[t];
+            uint64_t m = L.lv[t] & L.ac[t] & L.ctok[t];
             while (m) {
                 const int j = __ffsll((unsigned long long)m) - 1;
                 m &= m - 1;
@@ -359,9 +380,9 @@ __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
         if (has_od && has_spot) {
             int cnt = 0;
             for (int t = tid; t < T; t += NT) {
-                if (!S.keep[t]) continue;
+                if (!L.keep[t]) continue;
                 const int o0 = g.off_begin[t];
-                uint64_t m = S.lv[t] & S.am[t] & S.cmn[t] & S.ctok[t];
+                uint64_t m = L.lv[t] & L.ac[t] & L.ctok[t];
                 bool keep = true, spot = false, cheap = false, resv = false;
                 while (m) {
                     const int j = __ffsll((unsigned long long)m) - 1;
@@ -374,7 +395,7 @@ __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
                     }
                 }
                 keep = resv || cheap || !spot;
-                S.keep[t] = keep;
+                L.keep[t] = keep;
                 cnt += keep;
             }
             cnt = bsum(cnt, S);
@@ -388,27 +409,38 @@ __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
     int status = failed >= 0 ? KP_E_INSUFFICIENT_CAPACITY : KP_OK;
     int ct_sel = KP_CT_ON_DEMAND, n_types = 0, n_over = 0;
     if (failed < 0) {
-        // compact the kept types: S.key[u] = cheapest compatible available price, S.tmp[u] = name_rank << 32 | t
+        // compact the kept types: L.key[u] = cheapest compatible available price, ordk[u] = name_rank << 32 | t
         // (order of u is irrelevant: the rank below is a pure count over the (price, name, index) order)
+        constexpr int PER = (KP_MAX_TYPES + NT - 1) / NT;
         if (tid == 0) S.ncomp = 0;
-        __syncthreads();
-        for (int t = tid; t < T; t += NT) {
-            if (!S.keep[t]) continue;
+        double pk[PER];
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const int t = tid + k * NT;
+            pk[k] = -1.0;  // not kept
+            if (t >= T || !L.keep[t]) continue;
             const int o0 = g.off_begin[t];
-            uint64_t m = S.lv[t] & S.am[t] & S.cmn[t] & S.ctok[t];
+            uint64_t m = L.lv[t] & L.ac[t] & L.ctok[t];
             double p = DBL_MAX;
             while (m) {
                 const int j = __ffsll((unsigned long long)m) - 1;
                 m &= m - 1;
                 p = g.off_price[o0 + j] < p ? g.off_price[o0 + j] : p;
             }
+            pk[k] = p;
+        }
+        __syncthreads();  // every ctok read is done: ctok becomes the order keys
+        uint64_t* const ordk = L.ctok;
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const int t = tid + k * NT;
+            if (pk[k] < 0.0) continue;
             const int u = atomicAdd(&S.ncomp, 1);
-            S.key[u] = p;
-            S.tmp[u] = ((uint64_t)g.name_rank[t] << 32) | (uint32_t)t;
+            L.key[u] = pk[k];
+            ordk[u] = ((uint64_t)g.name_rank[t] << 32) | (uint32_t)t;
         }
         __syncthreads();
         const int nc = S.ncomp;
-        constexpr int PER = (KP_MAX_TYPES + NT - 1) / NT;
         int my_t[PER], my_r[PER];
 #pragma unroll
         for (int k = 0; k < PER; k++) {
@@ -416,22 +448,22 @@ __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
             my_r[k] = M;
             const int u = tid + k * NT;
             if (u >= nc) continue;
-            const double kt = S.key[u];
-            const uint64_t pt = S.tmp[u];
+            const double kt = L.key[u];
+            const uint64_t pt = ordk[u];
             int rank = 0;
             for (int v = 0; v < nc && rank < M; v++) {
-                const double kv = S.key[v];
-                rank += (kv < kt) || (kv == kt && S.tmp[v] < pt);
+                const double kv = L.key[v];
+                rank += (kv < kt) || (kv == kt && ordk[v] < pt);
             }
             my_t[k] = (int)(uint32_t)pt;
             my_r[k] = rank;
         }
-        for (int t = tid; t < T; t += NT) S.pos[t] = -1;
+        for (int t = tid; t < T; t += NT) L.pos[t] = -1;
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < PER; k++)
             if (my_t[k] >= 0 && my_r[k] < M) {
-                S.pos[my_t[k]] = (int16_t)my_r[k];
+                L.pos[my_t[k]] = (int8_t)my_r[k];
                 g.out_types[(size_t)i * M + my_r[k]] = my_t[k];
             }
         n_types = n < M ? n : M;
@@ -439,22 +471,22 @@ __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
         // SatisfiesMinValues over the truncated list (monotone in the prefix, so the full list decides)
         for (int mk = 0; mk < q.n_min && status == KP_OK; mk++) {
             const KlMinKey mkey = g.mins[q.min_off + mk];
-            for (int w = tid; w < KP_MAX_MIN_WORDS; w += NT) S.minbits[w] = 0;
+            for (int w = tid; w < KP_MAX_MIN_WORDS; w += NT) L.minbits[w] = 0;
             __syncthreads();
             for (int t = tid; t < T; t += NT) {
-                if (S.pos[t] < 0) continue;
+                if (L.pos[t] < 0) continue;
                 if (mkey.mi >= 0) {
                     const uint64_t mm = g.multi_mask[(size_t)mkey.mi * T + t];
-                    if (mm) atomicOr((unsigned long long*)&S.minbits[0], (unsigned long long)mm);
+                    if (mm) atomicOr((unsigned long long*)&L.minbits[0], (unsigned long long)mm);
                 } else {
                     const uint32_t v = g.type_val[(size_t)mkey.k * T + t];
                     if (v != VAL_ABSENT && v != VAL_DNE)
-                        atomicOr((unsigned long long*)&S.minbits[v >> 6], 1ull << (v & 63));
+                        atomicOr((unsigned long long*)&L.minbits[v >> 6], 1ull << (v & 63));
                 }
             }
             __syncthreads();
             int c = 0;
-            for (int w = tid; w < KP_MAX_MIN_WORDS; w += NT) c += __popcll(S.minbits[w]);
+            for (int w = tid; w < KP_MAX_MIN_WORDS; w += NT) c += __popcll(L.minbits[w]);
             c = bsum(c, S);
             if (c < mkey.minv) status = KP_E_CREATE;
         }
@@ -466,9 +498,9 @@ __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
                 if (!q.ct_has[ct]) continue;
                 int any = 0;
                 for (int t = tid; t < T; t += NT) {
-                    if (S.pos[t] < 0) continue;
+                    if (L.pos[t] < 0) continue;
                     const int o0 = g.off_begin[t];
-                    any |= (S.lv[t] & S.am[t] & S.cmn[t] & ct_mask(g, o0, S.lv[t], ct)) != 0;
+                    any |= (L.lv[t] & L.ac[t] & ct_mask(g, o0, L.lv[t], ct)) != 0;
                 }
                 any = bsum(any, S);
                 if (any) {
@@ -478,10 +510,10 @@ __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
             }
             // getOverrides: Available ∧ Compatible(reqs with capacity-type := In[ct_sel]), per kept type in price order
             for (int t = tid; t < T; t += NT) {
-                if (S.pos[t] < 0) continue;
+                if (L.pos[t] < 0) continue;
                 const int o0 = g.off_begin[t];
-                uint64_t m = S.lv[t] & S.am[t] & S.cmn[t] & ct_mask(g, o0, S.lv[t], ct_sel);
-                g.out_over[(size_t)i * M + S.pos[t]] = m;  // the host expands bit j to offering row o0 + j
+                uint64_t m = L.lv[t] & L.ac[t] & ct_mask(g, o0, L.lv[t], ct_sel);
+                g.out_over[(size_t)i * M + L.pos[t]] = m;  // the host expands bit j to offering row o0 + j
                 n_over += __popcll(m);
             }
             n_over = bsum(n_over, S);
@@ -503,6 +535,6 @@ __global__ __launch_bounds__(NT) void launch_kernel(KpLaunch g) {
 
 hipError_t kp_launch_select_kernel(const KpLaunch& g, hipStream_t s) {
     if (g.L <= 0) return hipSuccess;
-    hipLaunchKernelGGL(launch_kernel, dim3(g.L), dim3(NT), 0, s, g);
+    hipLaunchKernelGGL(launch_kernel, dim3(g.L), dim3(NT), launch_lds_bytes(g.T), s, g);
     return hipGetLastError();
 }
