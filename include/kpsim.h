@@ -344,6 +344,14 @@ kp_status kp_last_kernel_times(kp_ctx* ctx, double* ms, int32_t n);
  * every probe the sequential search would visit has been evaluated.
  * cluster.existing must be in NewScheduler's order (initialized nodes first, then by name); probes keep that order
  * with the candidates removed.  Candidate prices must be >= 0 (getCandidatePrices fails otherwise).
+ *
+ * Caller-side, outside this entry point (website/content/en/preview/concepts/disruption.md):
+ *   - Empty Node Consolidation (:94-97) deletes nodes with no reschedulable pods without any simulation, so empty
+ *     nodes need no probe;
+ *   - NodePool disruption budgets (:274-285) cap how many candidates may be disrupted.  The caller drops candidates
+ *     whose NodePool has no allowed disruptions left before building `candidates`, as the disruption controller does
+ *     when it lists them;
+ *   - consolidationPolicy / consolidateAfter decide which nodes are candidates at all.
  */
 enum { KP_CONSOLIDATE_SINGLE = 0, KP_CONSOLIDATE_MULTI = 1,
        KP_CONSOLIDATE_BOTH = 2 };  /* both probe lists in one pass: the multi-node probes, then the single-node probes
