@@ -2916,8 +2916,8 @@ void ireq_fill(const kp_ctx* c, const kp_requirement& r, IReq& q) {
             if (id >= 0) q.ids.push_back(id);
             else q.unk.emplace_back(v);
         }
-        std::sort(q.ids.begin(), q.ids.end());
-        q.ids.erase(std::unique(q.ids.begin(), q.ids.end()), q.ids.end());
+        // ids stay in request order (duplicates allowed): the bitset build ORs them; ireq_norm sorts them for the set
+        // algebra of a repeated key
         std::sort(q.unk.begin(), q.unk.end());
         q.unk.erase(std::unique(q.unk.begin(), q.unk.end()), q.unk.end());
     }
@@ -2929,6 +2929,10 @@ void ireq_fill(const kp_ctx* c, const kp_requirement& r, IReq& q) {
     }
     q.has_min = r.min_values >= 0;
     q.minv = r.min_values;
+}
+void ireq_norm(IReq& q) {
+    std::sort(q.ids.begin(), q.ids.end());
+    q.ids.erase(std::unique(q.ids.begin(), q.ids.end()), q.ids.end());
 }
 template <class V>
 V set_op(const V& a, const V& b, int how) {  // 0 union, 1 a \ b, 2 a ∩ b (sorted inputs)
@@ -2986,7 +2990,7 @@ IReq ireq_intersection(const kp_ctx* c, const IReq& a, const IReq& b) {
 // Requirement.Has for a value given by id (or by name when the dictionary does not know it, id < 0)
 bool ireq_has(const kp_ctx* c, const IReq& q, int id, const char* name) {
     bool in;
-    if (id >= 0) in = std::binary_search(q.ids.begin(), q.ids.end(), id);
+    if (id >= 0) in = std::find(q.ids.begin(), q.ids.end(), id) != q.ids.end();
     else in = std::binary_search(q.unk.begin(), q.unk.end(), std::string(name));
     return (q.comp ? !in : in) && ireq_within(q, name);
 }
@@ -3024,7 +3028,16 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
     for (int x = 0; x < 3; x++) c->ct_vid[x] = c->key_ct >= 0 ? c->cat.keys[c->key_ct].find(kCtNames[x]) : -1;
     int nthr = std::max(1, std::min<int>({16, (int)std::thread::hardware_concurrency(), (n + 255) / 256}));
     if (const char* e = getenv("KPSIM_LAUNCH_THREADS")) nthr = std::max(1, std::min(nthr, atoi(e)));  // diagnostics
-    std::vector<Chunk> chunks(nthr);
+    // per calling thread, reused across calls: the chunk tables and requirement slots keep their capacity, so the
+    // encoding threads do not contend in malloc
+    // (a named reference: the worker threads must reach the calling thread's instance, not their own)
+    static thread_local std::vector<Chunk> tl_chunks;
+    std::vector<Chunk>& chunks = tl_chunks;
+    if ((int)chunks.size() < nthr) chunks.resize(nthr);
+    for (auto& ch : chunks) {
+        ch.st = KP_OK;
+        ch.msg.clear();
+    }
     // catalog keys that are well-known labels (undefined on a request: no constraint), computed once per call
     std::vector<uint8_t> wk(Kc, 0);
     for (int kc = 0; kc < Kc; kc++) wk[kc] = well_known(c->cat.keys[kc].name) ? 1 : 0;
@@ -3053,7 +3066,11 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
             IReq* hit = nullptr;
             for (size_t x = 0; x < nm; x++)
                 if (slots[x].kc == q.kc && (q.kc >= 0 || !strcmp(slots[x].name, q.name))) hit = &slots[x];
-            if (hit) *hit = ireq_intersection(c, q, *hit);
+            if (hit) {
+                ireq_norm(q);
+                ireq_norm(*hit);
+                *hit = ireq_intersection(c, q, *hit);
+            }
             else nm++;
         }
         std::sort(slots.begin(), slots.begin() + nm, [](const IReq& a, const IReq& b) { return strcmp(a.name, b.name) < 0; });
