@@ -875,7 +875,9 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                                 auto mv = [&](auto& x) {
                                     using X = std::remove_reference_t<decltype(x)>;
                                     const int xf = rl32((int)x, fl);
-                                    const int nx = __shfl_down((int)x, 1);
+                                    // lane i ← lane i+1 with a DPP wavefront shift (wave_shl:1) instead of an LDS
+                                    // permute; lane 63's result is unused (sh requires lane < el - 1 <= 63)
+                                    const int nx = __builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xF, 0xF, false);
                                     x = sh ? (X)nx : (last ? (X)xf : x);
                                 };
                                 mv(wk);
