@@ -179,16 +179,49 @@ __device__ __forceinline__ int64_t ld_req(const int64_t* p) {
     return __hip_atomic_load(const_cast<int64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Full-wave reductions without LDS permutes: DPP inside each 16-lane row (quad xor 1, quad xor 2, half-row mirror, row
+// mirror leave every lane of a row holding the row's value), then the four row values combined through readlane.  The
+// result is wave-uniform.  Callers run with the whole wave active.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t x) {
+    return ((uint64_t)dpp32<CTRL>((uint32_t)(x >> 32)) << 32) | dpp32<CTRL>((uint32_t)x);
+}
+__device__ __forceinline__ uint64_t rlane64(uint64_t x, int l) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+}
+constexpr int kDppQuadXor1 = 0xB1, kDppQuadXor2 = 0x4E, kDppRowHalfMirror = 0x141, kDppRowMirror = 0x140;
+template <class F>
+__device__ __forceinline__ uint32_t wave_reduce32(uint32_t x, F f) {
+    x = f(x, dpp32<kDppQuadXor1>(x));
+    x = f(x, dpp32<kDppQuadXor2>(x));
+    x = f(x, dpp32<kDppRowHalfMirror>(x));
+    x = f(x, dpp32<kDppRowMirror>(x));
+    uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)x, 0);
+    r = f(r, (uint32_t)__builtin_amdgcn_readlane((int)x, 16));
+    r = f(r, (uint32_t)__builtin_amdgcn_readlane((int)x, 32));
+    return f(r, (uint32_t)__builtin_amdgcn_readlane((int)x, 48));
+}
+template <class F>
+__device__ __forceinline__ uint64_t wave_reduce64(uint64_t x, F f) {
+    x = f(x, dpp64<kDppQuadXor1>(x));
+    x = f(x, dpp64<kDppQuadXor2>(x));
+    x = f(x, dpp64<kDppRowHalfMirror>(x));
+    x = f(x, dpp64<kDppRowMirror>(x));
+    uint64_t r = rlane64(x, 0);
+    r = f(r, rlane64(x, 16));
+    r = f(r, rlane64(x, 32));
+    return f(r, rlane64(x, 48));
+}
 __device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
-    for (int o = 32; o >= 1; o >>= 1) x |= __shfl_xor(x, o);
-    return x;
+    return wave_reduce64(x, [](uint64_t a, uint64_t b) { return a | b; });
 }
 __device__ __forceinline__ int64_t wave_max64(int64_t x) {
-    for (int o = 32; o >= 1; o >>= 1) {
-        const int64_t y = __shfl_xor(x, o);
-        x = y > x ? y : x;
-    }
-    return x;
+    return (int64_t)wave_reduce64((uint64_t)x, [](uint64_t a, uint64_t b) { return (int64_t)b > (int64_t)a ? b : a; });
 }
 
 // Has(merged, v) for an offering-role key r: merged = scratch (class constrains the key) or the base digest.
@@ -280,13 +313,31 @@ struct WitnessAcc {
             if (lane < A) ws.hr[lane] = -1;
             return;
         }
-        for (int o = 32; o >= 1; o >>= 1) {
-            const float ob = __shfl_xor(best, o);
-            const int ot = __shfl_xor(bt, o);
+        // arg-best over the wave ((score desc, type asc) is a total order, so the reduction tree does not matter)
+        auto take = [&](float ob, int ot) {
             if (ob > best || (ob == best && ot < bt)) {
                 best = ob;
                 bt = ot;
             }
+        };
+        take(__uint_as_float(dpp32<kDppQuadXor1>(__float_as_uint(best))), (int)dpp32<kDppQuadXor1>((uint32_t)bt));
+        take(__uint_as_float(dpp32<kDppQuadXor2>(__float_as_uint(best))), (int)dpp32<kDppQuadXor2>((uint32_t)bt));
+        take(__uint_as_float(dpp32<kDppRowHalfMirror>(__float_as_uint(best))), (int)dpp32<kDppRowHalfMirror>((uint32_t)bt));
+        take(__uint_as_float(dpp32<kDppRowMirror>(__float_as_uint(best))), (int)dpp32<kDppRowMirror>((uint32_t)bt));
+        {
+            const float b0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(best), 0));
+            const int t0 = __builtin_amdgcn_readlane(bt, 0);
+            const float b1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(best), 16));
+            const int t1 = __builtin_amdgcn_readlane(bt, 16);
+            const float b2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(best), 32));
+            const int t2 = __builtin_amdgcn_readlane(bt, 32);
+            const float b3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(best), 48));
+            const int t3 = __builtin_amdgcn_readlane(bt, 48);
+            best = b0;
+            bt = t0;
+            take(b1, t1);
+            take(b2, t2);
+            take(b3, t3);
         }
         int64_t my = 0;
 #pragma unroll
@@ -320,18 +371,10 @@ __device__ __forceinline__ uint64_t ld_u64(const uint64_t* p) {
     return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
-    for (int o = 32; o >= 1; o >>= 1) {
-        const uint32_t y = __shfl_xor(x, o);
-        x = y < x ? y : x;
-    }
-    return x;
+    return wave_reduce32(x, [](uint32_t a, uint32_t b) { return b < a ? b : a; });
 }
 __device__ __forceinline__ int wave_min_i32(int x) {
-    for (int o = 32; o >= 1; o >>= 1) {
-        const int y = __shfl_xor(x, o);
-        x = y < x ? y : x;
-    }
-    return x;
+    return (int)wave_reduce32((uint32_t)x, [](uint32_t a, uint32_t b) { return (int)b < (int)a ? b : a; });
 }
 
 // Topology.AddRequirements ([core] scheduling/topology.go) for one candidate, after the requirement merge: every group
