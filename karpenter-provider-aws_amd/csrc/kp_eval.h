@@ -20,6 +20,7 @@
 //     admissible slot mask;
 //   * Fits compares the request totals with LDS-staged allocatable columns of the active resource axes.
 #pragma once
+#include "kp_wave.h"
 #include "kp_device.h"
 
 // Per-wave LDS scratch: merged requirements of the class's keys, resulting options, minValues bitset.
@@ -179,44 +180,6 @@ __device__ __forceinline__ int64_t ld_req(const int64_t* p) {
     return __hip_atomic_load(const_cast<int64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Full-wave reductions without LDS permutes: DPP inside each 16-lane row (quad xor 1, quad xor 2, half-row mirror, row
-// mirror leave every lane of a row holding the row's value), then the four row values combined through readlane.  The
-// result is wave-uniform.  Callers run with the whole wave active.
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp32(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
-}
-template <int CTRL>
-__device__ __forceinline__ uint64_t dpp64(uint64_t x) {
-    return ((uint64_t)dpp32<CTRL>((uint32_t)(x >> 32)) << 32) | dpp32<CTRL>((uint32_t)x);
-}
-__device__ __forceinline__ uint64_t rlane64(uint64_t x, int l) {
-    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l) << 32) |
-           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
-}
-constexpr int kDppQuadXor1 = 0xB1, kDppQuadXor2 = 0x4E, kDppRowHalfMirror = 0x141, kDppRowMirror = 0x140;
-template <class F>
-__device__ __forceinline__ uint32_t wave_reduce32(uint32_t x, F f) {
-    x = f(x, dpp32<kDppQuadXor1>(x));
-    x = f(x, dpp32<kDppQuadXor2>(x));
-    x = f(x, dpp32<kDppRowHalfMirror>(x));
-    x = f(x, dpp32<kDppRowMirror>(x));
-    uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)x, 0);
-    r = f(r, (uint32_t)__builtin_amdgcn_readlane((int)x, 16));
-    r = f(r, (uint32_t)__builtin_amdgcn_readlane((int)x, 32));
-    return f(r, (uint32_t)__builtin_amdgcn_readlane((int)x, 48));
-}
-template <class F>
-__device__ __forceinline__ uint64_t wave_reduce64(uint64_t x, F f) {
-    x = f(x, dpp64<kDppQuadXor1>(x));
-    x = f(x, dpp64<kDppQuadXor2>(x));
-    x = f(x, dpp64<kDppRowHalfMirror>(x));
-    x = f(x, dpp64<kDppRowMirror>(x));
-    uint64_t r = rlane64(x, 0);
-    r = f(r, rlane64(x, 16));
-    r = f(r, rlane64(x, 32));
-    return f(r, rlane64(x, 48));
-}
 __device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
     return wave_reduce64(x, [](uint64_t a, uint64_t b) { return a | b; });
 }

@@ -21,6 +21,7 @@
 #include "../../include/kpsim.h"
 #include "kp_launch.h"
 #include "kp_layout.h"
+#include "kp_wave.h"
 
 namespace {
 
@@ -62,7 +63,7 @@ inline size_t launch_lds_bytes(int T) { return (size_t)(3 * T + ltypes_key_len(T
 __device__ __forceinline__ bool wbit(const uint64_t* w, int off, int v) { return (w[off + (v >> 6)] >> (v & 63)) & 1ull; }
 
 __device__ int bsum(int x, LShared& S) {
-    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+    x = (int)wave_reduce32((uint32_t)x, [](uint32_t a, uint32_t b) { return a + b; });
     if ((threadIdx.x & 63) == 0) S.redi[threadIdx.x >> 6] = x;
     __syncthreads();
     int r = 0;
@@ -71,7 +72,7 @@ __device__ int bsum(int x, LShared& S) {
     return r;
 }
 __device__ int bmin_i(int x, LShared& S) {
-    for (int o = 32; o >= 1; o >>= 1) x = min(x, __shfl_xor(x, o));
+    x = (int)wave_reduce32((uint32_t)x, [](uint32_t a, uint32_t b) { return (int)b < (int)a ? b : a; });
     if ((threadIdx.x & 63) == 0) S.redi[threadIdx.x >> 6] = x;
     __syncthreads();
     int r = S.redi[0];
@@ -80,10 +81,9 @@ __device__ int bmin_i(int x, LShared& S) {
     return r;
 }
 __device__ double bmin_d(double x, LShared& S) {
-    for (int o = 32; o >= 1; o >>= 1) {
-        const double y = __shfl_xor(x, o);
-        x = y < x ? y : x;
-    }
+    x = __longlong_as_double((long long)wave_reduce64((uint64_t)__double_as_longlong(x), [](uint64_t a, uint64_t b) {
+        return __longlong_as_double((long long)b) < __longlong_as_double((long long)a) ? b : a;
+    }));
     if ((threadIdx.x & 63) == 0) S.redd[threadIdx.x >> 6] = x;
     __syncthreads();
     double r = S.redd[0];
