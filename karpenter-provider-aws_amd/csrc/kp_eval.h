@@ -442,8 +442,8 @@ __device__ __forceinline__ bool topo_narrow(const KpDev& d, const ClassCache& CC
             }
         }
     }
-    fail = __shfl(fail ? 1 : 0, 0) != 0;
-    changed = __shfl(changed ? 1 : 0, 0) != 0;
+    fail = __builtin_amdgcn_readlane(fail ? 1 : 0, 0) != 0;  // lane 0's verdict, whole wave active here
+    changed = __builtin_amdgcn_readlane(changed ? 1 : 0, 0) != 0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     if (changed || fail) ws.memo_ok = 0;
     return !fail;
