@@ -409,6 +409,45 @@ kp_status kp_consolidate(kp_ctx* ctx, const kp_consolidate_input* in, kp_probe_r
 kp_status kp_consolidate_prepare(kp_ctx* ctx, const kp_consolidate_input* in);
 kp_status kp_consolidate_execute(kp_ctx* ctx, int32_t mode, int32_t probe_begin, int32_t probe_end,
                                  kp_probe_result* results, int32_t cap_results);
+/*
+ * The consolidation command of a prepared pass — replaces the decision loops of [core] disruption
+ * (SingleNodeConsolidation.ComputeCommand, singlenodeconsolidation.go: the first candidate in disruption-cost order whose
+ * computeConsolidation is not a no-op; MultiNodeConsolidation.firstNConsolidationOption, multinodeconsolidation.go: the
+ * binary search over the prefix length, a prefix kept when DELETE or a REPLACE with options left after
+ * filterOutSameInstanceType) and their Command (consolidation.go computeConsolidation: delete set + replacement
+ * NodeClaim).  One call evaluates every probe the loop could visit (one device pass, sharded over a multi-device ctx),
+ * replays the loop over the results on the host, then re-runs the chosen probe on the primary device to read back its
+ * replacement NodeClaim — the NodeClaim CloudProvider.Create (pkg/cloudprovider/cloudprovider.go:90-137) is later called
+ * with:
+ *   type_ids      its InstanceTypeOptions after RemoveInstanceTypeOptionsByPriceAndMinValues (or the spot-to-spot cut
+ *                 to max(15, minNeeded) cheapest) and, for multi-node, filterOutSameInstanceType; OrderByPrice order;
+ *   requirements  its Requirements (FinalizeScheduling's reservation-id In [held IDs] included; capacity-type narrowed to
+ *                 spot when the replacement was priced as spot), kp_result_nodeclaim_requirements' text format.
+ * mode: KP_CONSOLIDATE_SINGLE, _MULTI, or _BOTH = the disruption controller's method order (multi-node, then single-node
+ * when the multi-node search finds no command), evaluated in one pass.
+ */
+typedef struct kp_consolidation_command {
+    /* caller-set buffers */
+    int32_t cap_type_ids;
+    int32_t* type_ids;               /* [cap_type_ids] catalog rows */
+    int64_t cap_requirements;
+    char* requirements;              /* [cap_requirements] bytes incl. NUL */
+    /* results */
+    int32_t decision;                /* KP_DECISION_*; NONE: no command */
+    int32_t mode;                    /* KP_CONSOLIDATE_SINGLE / _MULTI: the method that produced the command */
+    int32_t probe;                   /* index of the chosen probe in that method's probe list, -1 */
+    int32_t first_candidate;         /* delete set: candidates[first_candidate, first_candidate + n_candidates) */
+    int32_t n_candidates;
+    int32_t nodepool;                /* REPLACE: the replacement's NodePool (index into cluster.nodepools), else -1 */
+    int32_t n_type_ids;              /* REPLACE: number of options (written up to cap_type_ids) */
+    int32_t n_reserved;              /* REPLACE: reservation IDs the replacement holds */
+    int64_t requirements_needed;     /* REPLACE: bytes incl. NUL of the requirements text */
+    kp_probe_result result;          /* the chosen probe's row */
+} kp_consolidation_command;
+
+/* KP_E_BUFFER (with n_type_ids / requirements_needed set) when a replacement does not fit the caller's buffers. */
+kp_status kp_consolidate_command(kp_ctx* ctx, int32_t mode, kp_consolidation_command* out);
+
 /* Diagnostics of the last kp_consolidate: ms[3] = {device prep (queue sort, masks), probe kernel, whole call};
  * counters[16] = {pods popped, existing-node slots examined, NodeClaim evaluations, template evaluations, probes,
  * queue-bitmap words scanned, existing-node placements, new NodeClaims, node chunks loaded, cached-chunk hits, then
@@ -463,8 +502,10 @@ kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_request* requ
 /* Of the last kp_launch_select: ms[0] = launch kernel time (HIP events on the ctx stream, summed over the call's
  * sub-batches), ms[1] = whole call; host phases ms[2] = request encoding, ms[3] = table merge + upload, ms[4] = waits
  * for kernel + result download, ms[5] = result expansion; ms[6] = number of sub-batches, ms[7] = device busy time (union
- * of the sub-batch kernels, which overlap on two streams).  A batch of >= 4096 requests is cut into up to 4 sub-batches
- * so that encoding and expansion on the host overlap the kernels. */
+ * of the sub-batch kernels, which overlap on two streams).  A batch of >= 4096 requests is cut into 2 sub-batches on two
+ * streams (even sub-batches on the ctx stream, odd ones on a second stream) so that encoding and expansion on the host
+ * overlap the kernels; the KPSIM_LAUNCH_SUB environment variable overrides the count (diagnostics, capped at
+ * KL_MAX_SUB). */
 kp_status kp_launch_stats(kp_ctx* ctx, double* ms, int32_t n);
 
 /*

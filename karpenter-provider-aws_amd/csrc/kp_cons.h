@@ -49,6 +49,12 @@ struct KpCons {
     int32_t* retry;             // [n_probes] probes the fast variant handed over
     kp_probe_result* out;       // [n_probes]
     int64_t* stats;             // [CS_COUNT]
+    // kp_consolidate_command's read-back of one REPLACE probe (FULL variant, one probe per launch), else null:
+    // rec_i = {decision, template, spot-narrowed, n options, options in price order [64], held IDs}, the NodeClaim's
+    // requirements digest after FinalizeScheduling (rec_hdr [K], rec_words [DW]) and its held reservation IDs
+    int32_t* rec_i;
+    ReqHdr* rec_hdr;
+    uint64_t* rec_words;
     int32_t profile;            // s_memtime stage cycles (KPSIM_PROFILE)
     int32_t no_fast;            // diagnostics: every probe on the FULL variant (KPSIM_CONS_NOFAST)
     // dynamic LDS plan (kp_cons_plan_lds)

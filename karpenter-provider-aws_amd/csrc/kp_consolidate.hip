@@ -825,8 +825,20 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 valid = km != 0;
                 nrep = __popcll(km);
                 rprice = nrep ? wave_min_f64(keep ? wl : DBL_MAX) : 0.0;
+                if (FULL && k.rec_i) {  // kp_consolidate_command: the replacement NodeClaim of this probe
+                    if (keep) k.rec_i[4 + __popcll(km & ((1ull << lane) - 1))] = my_t;
+                    if (lane == 0) {
+                        k.rec_i[1] = nc_tmpl;
+                        k.rec_i[2] = spot_only ? 1 : 0;
+                        k.rec_i[3] = nrep;
+                        k.rec_i[4 + 64] = __popcll(nc_held);
+                    }
+                    for (int kk = lane; kk < K; kk += 64) k.rec_hdr[kk] = nch[kk];
+                    for (int i = lane; i < d.DW; i += 64) k.rec_words[i] = ncw[i];
+                }
             }
         }
+        if (FULL && k.rec_i && lane == 0) k.rec_i[0] = decision;
         if (prof) cy_dec = __builtin_amdgcn_s_memtime() - cd0;
         if (lane == 0) {
             kp_probe_result o;

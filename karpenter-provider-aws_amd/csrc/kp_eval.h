@@ -276,6 +276,7 @@ struct WitnessAcc {
             if (lane < A) ws.hr[lane] = -1;
             return;
         }
+        KP_ASSERT_FULL_WAVE();
         // arg-best over the wave ((score desc, type asc) is a total order, so the reduction tree does not matter)
         auto take = [&](float ob, int ot) {
             if (ob > best || (ob == best && ot < bt)) {

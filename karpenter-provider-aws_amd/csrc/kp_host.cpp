@@ -277,10 +277,16 @@ class WorkerPool {
     void grow(int n) {  // at most n - 1 workers (the caller is the n-th)
         while ((int)th_.size() < n - 1) th_.emplace_back([this] { loop(); });
     }
-    void run(int k, const std::function<void(int)>& fn) {
+    // false when a task threw (the exception is contained in its worker: one escaping a std::thread would
+    // std::terminate the caller's process); the caller reports it as a KP_E_* status
+    bool run(int k, const std::function<void(int)>& fn) {
         if (k <= 1 || th_.empty()) {
-            for (int i = 0; i < k; i++) fn(i);
-            return;
+            try {
+                for (int i = 0; i < k; i++) fn(i);
+            } catch (...) {
+                return false;
+            }
+            return true;
         }
         {
             std::lock_guard<std::mutex> g(mu_);
@@ -288,6 +294,7 @@ class WorkerPool {
             next_ = 0;
             tasks_ = k;
             left_ = k;
+            failed_ = false;
             gen_++;
         }
         cv_.notify_all();
@@ -295,6 +302,7 @@ class WorkerPool {
         std::unique_lock<std::mutex> g(mu_);
         done_.wait(g, [this] { return left_ == 0; });
         fn_ = nullptr;
+        return !failed_;
     }
 
   private:
@@ -308,8 +316,14 @@ class WorkerPool {
                 i = next_++;
                 f = fn_;
             }
-            (*f)(i);
+            bool ok = true;
+            try {
+                (*f)(i);
+            } catch (...) {
+                ok = false;
+            }
             std::lock_guard<std::mutex> g(mu_);
+            if (!ok) failed_ = true;
             if (--left_ == 0) done_.notify_all();
         }
     }
@@ -330,7 +344,7 @@ class WorkerPool {
     std::condition_variable cv_, done_;
     const std::function<void(int)>* fn_ = nullptr;
     int next_ = 0, tasks_ = 0, left_ = 0, gen_ = 0;
-    bool stop_ = false;
+    bool stop_ = false, failed_ = false;
 };
 
 // Pinned host staging buffer, grow-only (launch-request tables: DMA without the pageable-copy staging).
@@ -433,7 +447,10 @@ struct kp_ctx {
     DBuf<uint64_t> d_pend_bits, d_pbits;
     DBuf<uint64_t> d_init;
     DBuf<kp_probe_result> d_probe_out;
-    KpCons cons{};                           // prepared consolidation pass (device pointers set per execute)
+    DBuf<int32_t> d_rec_i;                   // kp_consolidate_command's read-back of the chosen REPLACE probe
+    DBuf<ReqHdr> d_rec_hdr;
+    DBuf<uint64_t> d_rec_words;
+    KpCons cons{};                         // prepared consolidation pass (device pointers set per execute)
     bool cons_prepared = false;
     // device prep of the prepared cluster (queue sort, ranks, pending bits, class / template / existing-node masks)
     // is reused by later kp_consolidate_execute calls until any entry point that rewrites device tables runs
@@ -521,7 +538,14 @@ static kp_status fan_out(kp_ctx* ctx, F f) {
     std::vector<kp_status> st(G, KP_OK);
     std::vector<std::thread> th;
     th.reserve(G);
-    for (size_t i = 0; i < G; i++) th.emplace_back([&st, &f, ctx, i] { st[i] = f(ctx->peers[i]); });
+    for (size_t i = 0; i < G; i++)
+        th.emplace_back([&st, &f, ctx, i] {
+            try {
+                st[i] = f(ctx->peers[i]);
+            } catch (...) {  // an exception may not leave the thread (std::terminate)
+                st[i] = fail(ctx->peers[i], KP_E_INVALID, "host error");
+            }
+        });
     const kp_status s0 = f(ctx);
     for (auto& t : th) t.join();
     if (s0 != KP_OK) return s0;
@@ -2327,6 +2351,8 @@ extern "C" kp_status kp_solve(kp_ctx* ctx, const kp_solve_input* in, kp_solve_ou
     return kp_solve_fetch(ctx, out);
 }
 
+static std::string reqs_text(const kp_ctx* ctx, const ReqHdr* h, const uint64_t* w);
+
 extern "C" kp_status kp_result_nodeclaim_requirements(kp_ctx* ctx, int32_t nc, char* buf, int64_t cap, int64_t* needed) {
     if (!ctx) return KP_E_INVALID;
     if (!ctx->executed) return fail(ctx, KP_E_STATE, "no solve result");
@@ -2337,6 +2363,17 @@ extern "C" kp_status kp_result_nodeclaim_requirements(kp_ctx* ctx, int32_t nc, c
     std::vector<uint64_t> w(DW);
     HIPCHK(hipMemcpy(h.data(), ctx->d_nc_hdr.p + (size_t)nc * K, K * sizeof(ReqHdr), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(w.data(), ctx->d_nc_words.p + (size_t)nc * DW, DW * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    const std::string s = reqs_text(ctx, h.data(), w.data());
+    if (needed) *needed = (int64_t)s.size() + 1;
+    if ((int64_t)s.size() + 1 > cap || !buf) return KP_E_BUFFER;
+    memcpy(buf, s.c_str(), s.size() + 1);
+    return KP_OK;
+}
+
+// A requirements digest (one ReqHdr per solve key, value bitsets at the keys' word offsets) as the text of
+// kp_result_nodeclaim_requirements: "key \t complement \t gt \t lt \t minValues \t sorted values" lines, sorted.
+static std::string reqs_text(const kp_ctx* ctx, const ReqHdr* h, const uint64_t* w) {
+    const int K = ctx->K;
     std::vector<std::string> lines;
     int off = 0;
     for (int k = 0; k < K; k++) {
@@ -2362,10 +2399,7 @@ extern "C" kp_status kp_result_nodeclaim_requirements(kp_ctx* ctx, int32_t nc, c
     std::sort(lines.begin(), lines.end());
     std::string s;
     for (auto& l : lines) s += l + "\n";
-    if (needed) *needed = (int64_t)s.size() + 1;
-    if ((int64_t)s.size() + 1 > cap || !buf) return KP_E_BUFFER;
-    memcpy(buf, s.c_str(), s.size() + 1);
-    return KP_OK;
+    return s;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2509,24 +2543,23 @@ static int cons_probes(const kp_ctx* c, int mode) {
     return mode == KP_CONSOLIDATE_SINGLE ? NC : mode == KP_CONSOLIDATE_MULTI ? nm : nm + NC;
 }
 
-static kp_status cons_execute_one(kp_ctx* ctx, int32_t mode, int32_t probe_begin, int32_t probe_end,
-                                  kp_probe_result* results, int32_t cap_results) try {
+// One device's share of a pass: multi-node probes [m0, m1) and single-node probes [s0, s1) of the prepared pass in one
+// launch (the multi-node prefixes first, longest first), results into out_multi[m1 - m0] / out_single[s1 - s0].
+// record: kp_consolidate_command's read-back run of one probe (FULL variant only; the replacement NodeClaim lands in
+// d_rec_*).
+static kp_status cons_run(kp_ctx* ctx, int m0, int m1, int s0, int s1, kp_probe_result* out_multi,
+                          kp_probe_result* out_single, bool record = false) try {
     if (!ctx) return KP_E_INVALID;
     if (!ctx->cons_prepared || !ctx->have_catalog)
         return fail(ctx, KP_E_STATE, "kp_consolidate_execute before kp_consolidate_prepare");
-    if (mode != KP_CONSOLIDATE_SINGLE && mode != KP_CONSOLIDATE_MULTI && mode != KP_CONSOLIDATE_BOTH)
-        return fail(ctx, KP_E_INVALID, "unknown consolidation mode");
     kp_ctx* c = ctx;
     HIPCHK(hipSetDevice(c->device));
     KpCons k = c->cons;
     const int NC = k.n_cand;
-    const int np = cons_probes(c, mode);
-    const int b0 = probe_begin > 0 ? probe_begin : 0;
-    const int b1 = probe_end > 0 && probe_end < np ? probe_end : np;
-    if (b0 > b1) return fail(ctx, KP_E_INVALID, "probe range outside the probe list");
-    const int nprobe = b1 - b0;
-    if (nprobe > cap_results || (nprobe > 0 && !results)) return fail(ctx, KP_E_BUFFER, "probe results buffer too small");
+    const int nmp = std::max(0, m1 - m0), nsp = std::max(0, s1 - s0);
+    const int nprobe = nmp + nsp;
     if (nprobe == 0) return KP_OK;
+    const int mode = nmp && nsp ? KP_CONSOLIDATE_BOTH : nmp ? KP_CONSOLIDATE_MULTI : KP_CONSOLIDATE_SINGLE;
     KpDev d = c->dev;
     const int P = d.P, E = d.E, A = d.n_active;
     d.lds_A = 0;  // no quick-accept witness in probes
@@ -2534,15 +2567,6 @@ static kp_status cons_execute_one(kp_ctx* ctx, int32_t mode, int32_t probe_begin
     d.profile = 0;
     hipStream_t s = c->stream;
     const std::vector<int32_t>& coff = c->cons_off;
-    // the range as a multi-node part [m0, m1) and a single-node part [s0, s1) (BOTH: multi probes come first)
-    const int nm_all = cons_probes(c, KP_CONSOLIDATE_MULTI);
-    int m0 = 0, m1 = 0, s0 = 0, s1 = 0;
-    if (mode == KP_CONSOLIDATE_MULTI) m0 = b0, m1 = b1;
-    else if (mode == KP_CONSOLIDATE_SINGLE) s0 = b0, s1 = b1;
-    else {
-        m0 = std::min(b0, nm_all), m1 = std::min(b1, nm_all);
-        s0 = std::max(b0, nm_all) - nm_all, s1 = std::max(b1, nm_all) - nm_all;
-    }
     int maxp = 0;  // ring capacity: pods of the largest probe
     for (int i = s0; i < s1; i++) maxp = std::max(maxp, coff[i + 1] - coff[i]);
     if (m1 > m0) maxp = std::max(maxp, coff[std::min(NC, m1 + 1)]);
@@ -2610,9 +2634,26 @@ static kp_status cons_execute_one(kp_ctx* ctx, int32_t mode, int32_t probe_begin
     k.stats = c->d_cons_stats.p;
     k.profile = getenv("KPSIM_PROFILE") ? 1 : 0;
     k.no_fast = getenv("KPSIM_CONS_NOFAST") ? atoi(getenv("KPSIM_CONS_NOFAST")) : 0;  // 1: FULL only, 2: fast only
+    k.rec_i = nullptr;
+    k.rec_hdr = nullptr;
+    k.rec_words = nullptr;
+    if (record) {
+        HIPCHK(c->d_rec_i.ensure(4 + 64 + 1));
+        HIPCHK(c->d_rec_hdr.ensure(std::max(d.K, 1)));
+        HIPCHK(c->d_rec_words.ensure(std::max(d.DW, 1)));
+        HIPCHK(hipMemsetAsync(c->d_rec_i.p, 0xff, (4 + 64 + 1) * sizeof(int32_t), s));
+        k.rec_i = c->d_rec_i.p;
+        k.rec_hdr = c->d_rec_hdr.p;
+        k.rec_words = c->d_rec_words.p;
+        k.no_fast = 1;
+    }
     HIPCHK(kp_launch_consolidate(d, k, workers, s));
     HIPCHK(hipEventRecord(c->ev[2], s));
-    HIPCHK(hipMemcpyAsync(results, c->d_probe_out.p, (size_t)nprobe * sizeof(kp_probe_result), hipMemcpyDeviceToHost, s));
+    if (nmp)
+        HIPCHK(hipMemcpyAsync(out_multi, c->d_probe_out.p, (size_t)nmp * sizeof(kp_probe_result), hipMemcpyDeviceToHost, s));
+    if (nsp)
+        HIPCHK(hipMemcpyAsync(out_single, c->d_probe_out.p + nmp, (size_t)nsp * sizeof(kp_probe_result),
+                              hipMemcpyDeviceToHost, s));
     int64_t cst[CS_COUNT];
     HIPCHK(hipMemcpyAsync(cst, c->d_cons_stats.p, sizeof cst, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -2628,13 +2669,14 @@ static kp_status cons_execute_one(kp_ctx* ctx, int32_t mode, int32_t probe_begin
     return fail(ctx, KP_E_INVALID, e.what());
 }
 
-// Multi-device: probes [b0, b1) split into one contiguous shard per device (equal probe counts), each evaluated on its
-// device by its own host thread into its slice of `results`; counters are summed, device times are the max over
-// devices.  Probes are independent, so the gathered vector equals a single-device evaluation of the whole range.
+// Probes [b0, b1) of `mode` as a multi-node part [m0, m1) and a single-node part [s0, s1) (BOTH: the multi-node probes
+// come first in the caller's numbering).  Multi-device: each part is split into one contiguous shard per device (so the
+// long multi-node prefixes spread over the devices instead of all landing on the first), each device runs its two
+// shards in one launch from its own host thread, writing into its slices of `results`; counters are summed, device
+// times are the max over devices.  Probes are independent, so the gathered vector equals a single-device evaluation.
 extern "C" kp_status kp_consolidate_execute(kp_ctx* ctx, int32_t mode, int32_t probe_begin, int32_t probe_end,
                                             kp_probe_result* results, int32_t cap_results) try {
     if (!ctx) return KP_E_INVALID;
-    if (ctx->peers.empty()) return cons_execute_one(ctx, mode, probe_begin, probe_end, results, cap_results);
     if (!ctx->cons_prepared || !ctx->have_catalog)
         return fail(ctx, KP_E_STATE, "kp_consolidate_execute before kp_consolidate_prepare");
     for (kp_ctx* p : ctx->peers)
@@ -2649,18 +2691,37 @@ extern "C" kp_status kp_consolidate_execute(kp_ctx* ctx, int32_t mode, int32_t p
     const int nprobe = b1 - b0;
     if (nprobe > cap_results || (nprobe > 0 && !results)) return fail(ctx, KP_E_BUFFER, "probe results buffer too small");
     if (nprobe == 0) return KP_OK;
+    const int nm_all = cons_probes(ctx, KP_CONSOLIDATE_MULTI);
+    int m0 = 0, m1 = 0, s0 = 0, s1 = 0;
+    if (mode == KP_CONSOLIDATE_MULTI) {
+        m0 = b0, m1 = b1;
+    } else if (mode == KP_CONSOLIDATE_SINGLE) {
+        s0 = b0, s1 = b1;
+    } else {
+        m0 = std::min(b0, nm_all), m1 = std::min(b1, nm_all);
+        s0 = std::max(b0, nm_all) - nm_all, s1 = std::max(b1, nm_all) - nm_all;
+    }
+    kp_probe_result* rm = results;
+    kp_probe_result* rs = results + (m1 - m0);
+    if (ctx->peers.empty()) return cons_run(ctx, m0, m1, s0, s1, rm, rs);
     const auto t0 = clk::now();
     const int G = 1 + (int)ctx->peers.size();
     std::vector<kp_ctx*> dev(1, ctx);
     dev.insert(dev.end(), ctx->peers.begin(), ctx->peers.end());
-    std::vector<int> lo(G), hi(G);
+    std::vector<int> ml(G), mh(G), sl(G), sh(G);
     for (int g = 0; g < G; g++) {
-        lo[g] = b0 + (int)((int64_t)nprobe * g / G);
-        hi[g] = b0 + (int)((int64_t)nprobe * (g + 1) / G);
+        ml[g] = m0 + (int)((int64_t)(m1 - m0) * g / G);
+        mh[g] = m0 + (int)((int64_t)(m1 - m0) * (g + 1) / G);
+        sl[g] = s0 + (int)((int64_t)(s1 - s0) * g / G);
+        sh[g] = s0 + (int)((int64_t)(s1 - s0) * (g + 1) / G);
     }
     std::vector<kp_status> st(G, KP_OK);
     auto run = [&](int g) {
-        if (hi[g] > lo[g]) st[g] = cons_execute_one(dev[g], mode, lo[g], hi[g], results + (lo[g] - b0), hi[g] - lo[g]);
+        try {
+            st[g] = cons_run(dev[g], ml[g], mh[g], sl[g], sh[g], rm + (ml[g] - m0), rs + (sl[g] - s0));
+        } catch (...) {
+            st[g] = fail(dev[g], KP_E_INVALID, "consolidation shard: host error");
+        }
     };
     std::vector<std::thread> th;
     th.reserve(G - 1);
@@ -2673,7 +2734,7 @@ extern "C" kp_status kp_consolidate_execute(kp_ctx* ctx, int32_t mode, int32_t p
     int64_t sum[CS_COUNT] = {};
     double ms0 = 0, ms1 = 0;
     for (int g = 0; g < G; g++) {
-        if (hi[g] <= lo[g]) continue;
+        if (mh[g] <= ml[g] && sh[g] <= sl[g]) continue;
         for (int i = 0; i < CS_COUNT; i++) sum[i] += dev[g]->cons_stats[i];
         ms0 = std::max(ms0, dev[g]->cons_ms[0]);
         ms1 = std::max(ms1, dev[g]->cons_ms[1]);
@@ -2699,6 +2760,131 @@ extern "C" kp_status kp_consolidate(kp_ctx* ctx, const kp_consolidate_input* in,
     if (st != KP_OK) return st;
     if (b1 == b0) return KP_OK;
     return kp_consolidate_execute(ctx, in->mode, b0, b1, results, cap_results);
+}
+
+// firstNConsolidationOption's binary search over the multi-node probe rows (row i = the prefix of i + 2 candidates):
+// the largest prefix whose command is DELETE or a REPLACE with options left (row.valid).  Returns the row or -1.
+static int replay_multi(const kp_probe_result* r, int n_cand, int max_cand) {
+    if (n_cand < 2) return -1;
+    int lo = 1, hi = max_cand;
+    if (n_cand <= hi) hi = n_cand - 1;
+    int best = -1;
+    while (lo <= hi) {
+        const int mid = (lo + hi) / 2;
+        if (r[mid - 1].valid) {
+            best = mid - 1;
+            lo = mid + 1;
+        } else {
+            hi = mid - 1;
+        }
+    }
+    return best;
+}
+
+extern "C" kp_status kp_consolidate_command(kp_ctx* ctx, int32_t mode, kp_consolidation_command* out) try {
+    if (!ctx || !out) return KP_E_INVALID;
+    if (mode != KP_CONSOLIDATE_SINGLE && mode != KP_CONSOLIDATE_MULTI && mode != KP_CONSOLIDATE_BOTH)
+        return fail(ctx, KP_E_INVALID, "unknown consolidation mode");
+    if (!ctx->cons_prepared || !ctx->have_catalog)
+        return fail(ctx, KP_E_STATE, "kp_consolidate_command before kp_consolidate_prepare");
+    out->decision = KP_DECISION_NONE;
+    out->mode = -1;
+    out->probe = -1;
+    out->first_candidate = 0;
+    out->n_candidates = 0;
+    out->nodepool = -1;
+    out->n_type_ids = 0;
+    out->n_reserved = 0;
+    out->requirements_needed = 0;
+    out->result = kp_probe_result{};
+    if (out->requirements && out->cap_requirements > 0) out->requirements[0] = 0;
+    const int NC = ctx->cons.n_cand, mx = ctx->cons_max_candidates;
+    const int nm = cons_probes(ctx, KP_CONSOLIDATE_MULTI), np = cons_probes(ctx, mode);
+    std::vector<kp_probe_result> res(std::max(np, 1));
+    if (np > 0) {
+        const kp_status st = kp_consolidate_execute(ctx, mode, 0, np, res.data(), np);
+        if (st != KP_OK) return st;
+    }
+    // the disruption controller's method order: multi-node (binary search), then single-node (first non-no-op)
+    int chosen = -1, probe = -1;
+    const kp_probe_result* rows = res.data();
+    if (mode != KP_CONSOLIDATE_SINGLE) {
+        probe = replay_multi(res.data(), NC, mx);
+        if (probe >= 0) chosen = KP_CONSOLIDATE_MULTI;
+    }
+    if (chosen < 0 && mode != KP_CONSOLIDATE_MULTI) {
+        rows = res.data() + (mode == KP_CONSOLIDATE_BOTH ? nm : 0);
+        for (int i = 0; i < NC; i++)
+            if (rows[i].decision != KP_DECISION_NONE) {
+                probe = i;
+                chosen = KP_CONSOLIDATE_SINGLE;
+                break;
+            }
+    }
+    if (chosen < 0) return KP_OK;
+    const kp_probe_result row = rows[probe];
+    out->mode = chosen;
+    out->probe = probe;
+    out->first_candidate = chosen == KP_CONSOLIDATE_SINGLE ? probe : 0;
+    out->n_candidates = chosen == KP_CONSOLIDATE_SINGLE ? 1 : probe + 2;
+    out->result = row;
+    out->decision = row.decision;
+    if (row.decision != KP_DECISION_REPLACE) return KP_OK;
+    // the replacement NodeClaim: re-run the chosen probe on the primary device with the read-back on (the pass's
+    // timings and counters stay those of the pass)
+    double ms_keep[3];
+    int64_t st_keep[CS_COUNT];
+    memcpy(ms_keep, ctx->cons_ms, sizeof ms_keep);
+    memcpy(st_keep, ctx->cons_stats, sizeof st_keep);
+    kp_probe_result again{};
+    const bool multi = chosen == KP_CONSOLIDATE_MULTI;
+    const kp_status st = multi ? cons_run(ctx, probe, probe + 1, 0, 0, &again, nullptr, true)
+                               : cons_run(ctx, 0, 0, probe, probe + 1, nullptr, &again, true);
+    memcpy(ctx->cons_ms, ms_keep, sizeof ms_keep);
+    memcpy(ctx->cons_stats, st_keep, sizeof st_keep);
+    if (st != KP_OK) return st;
+    const int K = ctx->K, DW = ctx->DW;
+    int32_t ri[4 + 64 + 1];
+    std::vector<ReqHdr> h(std::max(K, 1));
+    std::vector<uint64_t> w(std::max(DW, 1));
+    HIPCHK(hipMemcpy(ri, ctx->d_rec_i.p, sizeof ri, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(h.data(), ctx->d_rec_hdr.p, (size_t)K * sizeof(ReqHdr), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(w.data(), ctx->d_rec_words.p, (size_t)DW * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    if (ri[0] != KP_DECISION_REPLACE || again.decision != row.decision || again.n_replacement_types != row.n_replacement_types ||
+        ri[3] != row.n_replacement_types || ri[1] < 0 || ri[1] >= (int)ctx->tmpl_np.size())
+        return fail(ctx, KP_E_DEVICE, "kp_consolidate_command: the read-back run disagrees with the pass");
+    out->nodepool = ctx->tmpl_np[ri[1]];
+    out->n_reserved = ri[4 + 64];
+    // the replacement was priced as spot: Requirements.Add(capacity-type In [spot]) (consolidation.go)
+    if (ri[2] && ctx->key_ct >= 0) {
+        const int kct = ctx->key_ct;
+        int wo = 0;
+        for (int k = 0; k < kct; k++) wo += std::max(1, ((int)ctx->sol.keys[k].vals.size() + 63) / 64);
+        const int nwk = std::max(1, ((int)ctx->sol.keys[kct].vals.size() + 63) / 64);
+        const int vs = ctx->sol.keys[kct].find("spot");
+        ReqHdr& hc = h[kct];
+        const uint32_t keep_min = hc.flags & RF_MIN;
+        hc.flags = RF_DEF | keep_min;
+        hc.gt = hc.lt = 0;
+        for (int i = 0; i < nwk; i++) w[wo + i] = 0;
+        if (vs >= 0) w[wo + vs / 64] |= 1ull << (vs % 64);
+    }
+    const int n = ri[3];
+    out->n_type_ids = n;
+    const std::string txt = reqs_text(ctx, h.data(), w.data());
+    out->requirements_needed = (int64_t)txt.size() + 1;
+    bool small = false;
+    for (int i = 0; i < n; i++) {
+        if (i < out->cap_type_ids && out->type_ids) out->type_ids[i] = ri[4 + i];
+        else small = true;
+    }
+    if (out->requirements && out->cap_requirements >= (int64_t)txt.size() + 1)
+        memcpy(out->requirements, txt.c_str(), txt.size() + 1);
+    else
+        small = true;
+    return small ? fail(ctx, KP_E_BUFFER, "kp_consolidate_command: replacement buffers too small") : KP_OK;
+} catch (const std::exception& e) {
+    return fail(ctx, KP_E_INVALID, e.what());
 }
 
 extern "C" kp_status kp_consolidate_stats(kp_ctx* ctx, double* ms, int64_t* counters, int32_t n_counters) {
@@ -3214,13 +3400,15 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
     const uint64_t* const ov = c->p_l_over.p;
     // result rows: counts first (type_offset / override_offset are prefix sums), then the lists, per thread range
     std::vector<int64_t> toff(n + 1, 0), ooff(n + 1, 0);
+    bool host_err = false;  // a worker task threw (reported as KP_E_INVALID once the streams are idle)
     auto par = [&](int i0, int i1, auto fn) {  // fn(a, b) over contiguous ranges of [i0, i1) (the ctx's worker threads)
         const int k = std::max(1, std::min(nthr, (i1 - i0) / 256));
         if (k == 1) {
             fn(i0, i1);
             return;
         }
-        c->pool.run(k, [&](int ti) { fn(i0 + (int)((int64_t)(i1 - i0) * ti / k), i0 + (int)((int64_t)(i1 - i0) * (ti + 1) / k)); });
+        if (!c->pool.run(k, [&](int ti) { fn(i0 + (int)((int64_t)(i1 - i0) * ti / k), i0 + (int)((int64_t)(i1 - i0) * (ti + 1) / k)); }))
+            host_err = true;
     };
     double ms_enc = 0, ms_up = 0, ms_wait = 0, ms_exp = 0;
     float kms_sum = 0.f;
@@ -3289,11 +3477,17 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
             ch.mins.clear();
             ch.words.clear();
         }
-        c->pool.run(nt, [&](int ti) {
-            const int i0 = s0 + (int)((int64_t)ns * ti / nt), i1 = s0 + (int)((int64_t)ns * (ti + 1) / nt);
-            for (int i = i0; i < i1; i++)
-                if (!encode_one(i, chunks[ti])) return;
-        });
+        if (!c->pool.run(nt, [&](int ti) {
+                const int i0 = s0 + (int)((int64_t)ns * ti / nt), i1 = s0 + (int)((int64_t)ns * (ti + 1) / nt);
+                for (int i = i0; i < i1; i++)
+                    if (!encode_one(i, chunks[ti])) return;
+            }))
+            host_err = true;
+        if (host_err) {
+            hipStreamSynchronize(c->stream);  // no copy may still read the staging when the caller sees the error
+            if (c->lstream2) hipStreamSynchronize(c->lstream2);
+            return fail(c, KP_E_INVALID, "kp_launch_select: host error in a worker thread");
+        }
         const auto te1 = clk::now();
         ms_enc += ms_between(te0, te1);
         // chunk tables concatenated straight into pinned staging, offsets rebased per chunk
@@ -3373,6 +3567,7 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
         if (b > 0) HIPCHK(expand(b - 1));
     }
     HIPCHK(expand(nsub - 1));
+    if (host_err) return fail(c, KP_E_INVALID, "kp_launch_select: host error in a worker thread");
     const bool short_buf = (n > 0 && toff[n] > 0 && (!type_ids || toff[n] > cap_type_ids)) ||
                            (n > 0 && ooff[n] > 0 && (!override_offerings || ooff[n] > cap_overrides));
     c->launch_ms[0] = kms_sum;  // Σ kernel time over the sub-batches

@@ -15,6 +15,7 @@
 #include <cstdint>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <set>
 #include <string>
 #include <vector>
@@ -487,7 +488,8 @@ extern "C" kp_status kp_catalog_build(int32_t n_types, const kp_ec2_instance_typ
         bad_array(nc->n_capacity_reservations, nc->capacity_reservations))
         return KP_E_INVALID;
     try {
-        kp_catalog* c = new kp_catalog();
+        auto owned = std::make_unique<kp_catalog>();  // freed if building any type throws
+        kp_catalog* c = owned.get();
         const int Z = os->n_zones;
         std::map<std::string, std::string> zone_id;  // subnetZonesToZoneIDs (offering.go:75-77): the last subnet wins
         for (int i = 0; i < nc->n_zones; i++)
@@ -589,7 +591,7 @@ extern "C" kp_status kp_catalog_build(int32_t n_types, const kp_ec2_instance_typ
         for (const auto& v : c->values) c->value_ptrs.push_back(v.c_str());
         for (const auto& v : c->o_vals) c->o_val_ptrs.push_back(v.c_str());
         for (int q = 0; q < 5; q++) c->o_key_ptrs.push_back(kOfferingKeys[q]);
-        *out = c;
+        *out = owned.release();
         return KP_OK;
     } catch (const Err&) {
         return KP_E_INVALID;

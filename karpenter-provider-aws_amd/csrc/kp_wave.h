@@ -7,6 +7,15 @@
 // Full-wave reductions without LDS permutes: DPP inside each 16-lane row (quad xor 1, quad xor 2, half-row mirror, row
 // mirror leave every lane of a row holding the row's value), then the four row values combined through readlane.  The
 // result is wave-uniform.  Callers run with the whole wave active.
+// Debug builds (-DKPSIM_DEVICE_DEBUG) check the whole-wave precondition: with an inactive lane, update_dpp's bound
+// lanes read 0 and a readlane of an inactive row would return a stale value, so a divergent call site fails loudly.
+#ifdef KPSIM_DEVICE_DEBUG
+#include <cassert>
+#define KP_ASSERT_FULL_WAVE() assert(__builtin_amdgcn_read_exec() == ~0ull)
+#else
+#define KP_ASSERT_FULL_WAVE() ((void)0)
+#endif
+
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp32(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
@@ -22,6 +31,7 @@ __device__ __forceinline__ uint64_t rlane64(uint64_t x, int l) {
 constexpr int kDppQuadXor1 = 0xB1, kDppQuadXor2 = 0x4E, kDppRowHalfMirror = 0x141, kDppRowMirror = 0x140;
 template <class F>
 __device__ __forceinline__ uint32_t wave_reduce32(uint32_t x, F f) {
+    KP_ASSERT_FULL_WAVE();
     x = f(x, dpp32<kDppQuadXor1>(x));
     x = f(x, dpp32<kDppQuadXor2>(x));
     x = f(x, dpp32<kDppRowHalfMirror>(x));
@@ -33,6 +43,7 @@ __device__ __forceinline__ uint32_t wave_reduce32(uint32_t x, F f) {
 }
 template <class F>
 __device__ __forceinline__ uint64_t wave_reduce64(uint64_t x, F f) {
+    KP_ASSERT_FULL_WAVE();
     x = f(x, dpp64<kDppQuadXor1>(x));
     x = f(x, dpp64<kDppQuadXor2>(x));
     x = f(x, dpp64<kDppRowHalfMirror>(x));

@@ -150,6 +150,14 @@ class kp_probe_result(C.Structure):
                 ("candidate_price", C.c_double), ("replacement_price", C.c_double)]
 
 
+class kp_consolidation_command(C.Structure):
+    _fields_ = [("cap_type_ids", C.c_int32), ("type_ids", c_int32_p), ("cap_requirements", C.c_int64),
+                ("requirements", C.c_char_p), ("decision", C.c_int32), ("mode", C.c_int32), ("probe", C.c_int32),
+                ("first_candidate", C.c_int32), ("n_candidates", C.c_int32), ("nodepool", C.c_int32),
+                ("n_type_ids", C.c_int32), ("n_reserved", C.c_int32), ("requirements_needed", C.c_int64),
+                ("result", kp_probe_result)]
+
+
 PROBE_DTYPE = np.dtype([("decision", np.int32), ("valid", np.int32), ("all_scheduled", np.int32),
                         ("n_new_nodeclaims", np.int32), ("n_replacement_types", np.int32), ("n_pods", np.int32),
                         ("candidate_price", np.float64), ("replacement_price", np.float64)])

@@ -10,7 +10,7 @@ wave per probe; one shard of probes per GPU) and the loops are replayed over the
 the sequential code would reach.  Across ranks the only exchange is the result vector: an all-reduce MIN of the first
 valid single-node index, or an all-gather of the multi-node prefix results.
 """
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Optional
 
 import numpy as np
@@ -25,9 +25,45 @@ class Command:
     n_replacement_types: int = 0
     candidate_price: float = 0.0
     replacement_price: float = 0.0
+    # kp_consolidate_command only: the method that produced it, its probe, and the replacement NodeClaim
+    mode: int = -1
+    probe: int = -1
+    nodepool: int = -1
+    type_ids: list = field(default_factory=list)  # catalog rows, OrderByPrice order
+    requirements: str = ""                         # kp_result_nodeclaim_requirements text
+    n_reserved: int = 0
 
 
 NO_OP = Command(abi.KP_DECISION_NONE, [])
+
+
+def command_call(fn, cap_types=1024, cap_req=1 << 16):
+    """Call fn(kp_consolidation_command) (kp_consolidate_command or the oracle's) with output buffers, growing them on
+    KP_E_BUFFER -> (status, Command)."""
+    import ctypes as C
+    for _ in range(2):
+        types = np.zeros(cap_types, np.int32)
+        req = C.create_string_buffer(int(cap_req))
+        cc = abi.kp_consolidation_command()
+        cc.cap_type_ids = cap_types
+        cc.type_ids = types.ctypes.data_as(C.POINTER(C.c_int32))
+        cc.cap_requirements = cap_req
+        cc.requirements = C.cast(req, C.c_char_p)
+        st = fn(cc)
+        if st == abi.KP_E_BUFFER:
+            cap_types = max(cap_types, cc.n_type_ids)
+            cap_req = max(cap_req, cc.requirements_needed)
+            continue
+        break
+    if st != abi.KP_OK:
+        return st, None
+    r = cc.result
+    cands = list(range(cc.first_candidate, cc.first_candidate + cc.n_candidates))
+    cmd = Command(int(cc.decision), cands, int(r.n_replacement_types), float(r.candidate_price),
+                  float(r.replacement_price), int(cc.mode), int(cc.probe), int(cc.nodepool),
+                  [int(x) for x in types[:cc.n_type_ids]], req.value.decode() if cc.decision == abi.KP_DECISION_REPLACE
+                  else "", int(cc.n_reserved))
+    return st, cmd
 
 
 def first_valid_single(results: np.ndarray, probe0: int = 0) -> int:

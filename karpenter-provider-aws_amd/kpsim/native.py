@@ -13,7 +13,7 @@ EXPORTS = [
     "kp_result_nodeclaim_requirements", "kp_last_kernel_times", "kp_consolidate_probe_count", "kp_consolidate",
     "kp_consolidate_stats", "kp_consolidate_prepare", "kp_consolidate_execute", "kp_launch_select", "kp_launch_stats",
     "kp_nodeclaim_labels", "kp_catalog_build", "kp_catalog_get_view", "kp_catalog_overhead", "kp_catalog_resource_name",
-    "kp_catalog_free",
+    "kp_catalog_free", "kp_consolidate_command",
 ]
 
 _lib = None
@@ -55,6 +55,7 @@ def load():
     L.kp_consolidate_execute.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(abi.kp_probe_result),
                                          C.c_int32]
     L.kp_consolidate_stats.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.c_int32]
+    L.kp_consolidate_command.argtypes = [C.c_void_p, C.c_int32, C.POINTER(abi.kp_consolidation_command)]
     L.kp_launch_select.argtypes = [C.c_void_p, C.c_int32, C.POINTER(abi.kp_launch_request), C.c_int32,
                                    C.POINTER(abi.kp_launch_result), C.POINTER(C.c_int32), C.c_int32,
                                    C.POINTER(C.c_int32), C.c_int32]
@@ -199,6 +200,13 @@ class Context:
                                                  out.ctypes.data_as(C.POINTER(abi.kp_probe_result)), len(out)),
                    "kp_consolidate_execute")
         return out[:max(0, b1 - begin)]
+
+    def consolidate_command(self, mode):
+        """kp_consolidate_command over the prepared pass -> kpsim.consolidation.Command (with the replacement)."""
+        from kpsim import consolidation
+        st, cmd = consolidation.command_call(lambda cc: self.L.kp_consolidate_command(self.h, mode, C.byref(cc)))
+        self.check(st, "kp_consolidate_command")
+        return cmd
 
     def consolidate_stats(self):
         """(ms[prep, probe kernel, call], counters[16]) of the last kp_consolidate (kpsim.h kp_consolidate_stats)."""

@@ -1273,8 +1273,16 @@ static int consolidate_probe_count(const kp_consolidate_input* in) {
     return n <= mx ? n - 1 : mx;  // firstNConsolidationOption: mid in [1, max], prefix candidates[0 : mid+1]
 }
 
+// The replacement NodeClaim of a REPLACE probe (computeConsolidation's Command.Replacements[0]).
+struct Replacement {
+    int nodepool = -1;
+    int n_held = 0;
+    std::vector<int> opts;  // catalog rows, OrderByPrice order
+    Reqs reqs;
+};
+
 // One SimulateScheduling + computeConsolidation (+ the multi-node filterOutSameInstanceType test).
-static void run_probe(const ConsCtx& X, int probe, kp_probe_result& pr) {
+static void run_probe(const ConsCtx& X, int probe, kp_probe_result& pr, Replacement* rep = nullptr) {
     const kp_consolidate_input* in = X.in;
     const Solver& b = *X.base;
     const int c0 = in->mode == KP_CONSOLIDATE_SINGLE ? probe : 0;
@@ -1394,6 +1402,12 @@ static void run_probe(const ConsCtx& X, int probe, kp_probe_result& pr) {
         if (i == 0 || w < best) best = w;
     }
     pr.replacement_price = best;
+    if (rep) {
+        rep->nodepool = s.tmpls[nc.tmpl].np_index;
+        rep->n_held = (int)nc.held.size();
+        rep->opts = opts;
+        rep->reqs = reqs;
+    }
 }
 
 }  // namespace orc
@@ -1404,13 +1418,20 @@ extern "C" int32_t orc_consolidate_probe_count(const kp_consolidate_input* in) {
 
 static std::atomic<double> g_last_probe_seconds{0.0};
 
-extern "C" kp_status orc_consolidate(const kp_catalog_view* cat, const kp_consolidate_input* in,
-                                     kp_probe_result* results, int32_t cap_results, int32_t n_threads) {
+static std::string reqs_text(const orc::Dict& D, const orc::Reqs& reqs);
+
+// Parsed cluster of a consolidation pass, shared read-only by its probes.
+struct ConsEnv {
+    Dict D;
+    Solver base{D};
+    ConsCtx X;
+};
+
+static kp_status cons_setup(const kp_catalog_view* cat, const kp_consolidate_input* in, ConsEnv& env) {
     if (!cat || !in) return KP_E_INVALID;
     if (in->cluster.min_values_policy != KP_MIN_VALUES_STRICT) return KP_E_UNSUPPORTED;
-    if (in->mode != KP_CONSOLIDATE_SINGLE && in->mode != KP_CONSOLIDATE_MULTI) return KP_E_INVALID;
-    Dict D;
-    Solver base(D);
+    Dict& D = env.D;
+    Solver& base = env.base;
     base.resv_on = true;        // ReservedCapacity gate on; disruption simulations use ReservedOfferingModeFallback
     base.resv_strict = false;
     kp_status st = parse_into(base, cat, &in->cluster, KP_PREFERENCE_RESPECT);
@@ -1428,11 +1449,7 @@ extern "C" kp_status orc_consolidate(const kp_catalog_view* cat, const kp_consol
         for (int i = 0; i < cd.n_pods; i++)
             if (cd.pods[i] < 0 || cd.pods[i] >= P) return KP_E_INVALID;
     }
-    const int np = consolidate_probe_count(in);
-    const int b0 = in->probe_begin > 0 ? in->probe_begin : 0;
-    const int b1 = in->probe_end > 0 && in->probe_end < np ? in->probe_end : np;
-    if (b1 - b0 > cap_results) return KP_E_BUFFER;
-    ConsCtx X;
+    ConsCtx& X = env.X;
     X.base = &base;
     X.in = in;
     X.ct_key = D.key("karpenter.sh/capacity-type");
@@ -1442,9 +1459,11 @@ extern "C" kp_status orc_consolidate(const kp_catalog_view* cat, const kp_consol
     X.spot_req = new_req(D, X.ct_key, OP_IN, {"spot"}, false, 0);
     X.v_spot = D.value(X.ct_key, "spot");
     X.v_od = D.value(X.ct_key, "on-demand");
-    // the dictionary is frozen from here on: probes only read it
-    const int nt = n_threads > 1 ? n_threads : 1;
-    const auto tp0 = std::chrono::steady_clock::now();
+    return KP_OK;  // the dictionary is frozen from here on: probes only read it
+}
+
+// probes [b0, b1) of X.in's mode over nt threads
+static void run_probes(const ConsCtx& X, int b0, int b1, kp_probe_result* results, int nt) {
     std::atomic<int> next{b0};
     auto worker = [&]() {
         for (;;) {
@@ -1457,21 +1476,117 @@ extern "C" kp_status orc_consolidate(const kp_catalog_view* cat, const kp_consol
     for (int t = 1; t < nt; t++) th.emplace_back(worker);
     worker();
     for (auto& t : th) t.join();
+}
+
+extern "C" kp_status orc_consolidate(const kp_catalog_view* cat, const kp_consolidate_input* in,
+                                     kp_probe_result* results, int32_t cap_results, int32_t n_threads) {
+    if (!cat || !in) return KP_E_INVALID;
+    if (in->mode != KP_CONSOLIDATE_SINGLE && in->mode != KP_CONSOLIDATE_MULTI) return KP_E_INVALID;
+    auto env = std::make_unique<ConsEnv>();
+    kp_status st = cons_setup(cat, in, *env);
+    if (st != KP_OK) return st;
+    const int np = consolidate_probe_count(in);
+    const int b0 = in->probe_begin > 0 ? in->probe_begin : 0;
+    const int b1 = in->probe_end > 0 && in->probe_end < np ? in->probe_end : np;
+    if (b1 - b0 > cap_results) return KP_E_BUFFER;
+    const auto tp0 = std::chrono::steady_clock::now();
+    run_probes(env->X, b0, b1, results, n_threads > 1 ? n_threads : 1);
     g_last_probe_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - tp0).count();
     return KP_OK;
+}
+
+// The consolidation command (kp_consolidate_command's restatement): MultiNodeConsolidation.firstNConsolidationOption's
+// binary search (multinodeconsolidation.go), then SingleNodeConsolidation's first non-no-op candidate
+// (singlenodeconsolidation.go), in the disruption controller's method order for KP_CONSOLIDATE_BOTH; a REPLACE carries
+// its replacement NodeClaim (options after the price filter / spot-to-spot cut / filterOutSameInstanceType, requirements
+// with capacity-type narrowed to spot when priced as spot).
+extern "C" kp_status orc_consolidate_command(const kp_catalog_view* cat, const kp_consolidate_input* in, int32_t mode,
+                                             kp_consolidation_command* out, int32_t n_threads) {
+    if (!cat || !in || !out) return KP_E_INVALID;
+    if (mode != KP_CONSOLIDATE_SINGLE && mode != KP_CONSOLIDATE_MULTI && mode != KP_CONSOLIDATE_BOTH) return KP_E_INVALID;
+    auto env = std::make_unique<ConsEnv>();
+    kp_status st = cons_setup(cat, in, *env);
+    if (st != KP_OK) return st;
+    out->decision = KP_DECISION_NONE;
+    out->mode = out->probe = out->nodepool = -1;
+    out->first_candidate = out->n_candidates = out->n_type_ids = out->n_reserved = 0;
+    out->requirements_needed = 0;
+    out->result = kp_probe_result{};
+    const int nt = n_threads > 1 ? n_threads : 1;
+    kp_consolidate_input im = *in;
+    int chosen = -1, probe = -1;
+    std::vector<kp_probe_result> rows;
+    if (mode != KP_CONSOLIDATE_SINGLE) {
+        im.mode = KP_CONSOLIDATE_MULTI;
+        env->X.in = &im;
+        const int n = consolidate_probe_count(&im);
+        rows.assign(std::max(n, 1), kp_probe_result{});
+        run_probes(env->X, 0, n, rows.data(), nt);
+        // firstNConsolidationOption: mid in [1, max], the prefix candidates[0 : mid+1] is row mid - 1
+        if (in->n_candidates >= 2) {
+            int lo = 1, hi = in->max_candidates > 0 ? in->max_candidates : 100;
+            if (in->n_candidates <= hi) hi = in->n_candidates - 1;
+            while (lo <= hi) {
+                const int mid = (lo + hi) / 2;
+                if (rows[mid - 1].valid) {
+                    probe = mid - 1;
+                    lo = mid + 1;
+                } else {
+                    hi = mid - 1;
+                }
+            }
+        }
+        if (probe >= 0) chosen = KP_CONSOLIDATE_MULTI;
+    }
+    if (chosen < 0 && mode != KP_CONSOLIDATE_MULTI) {
+        im.mode = KP_CONSOLIDATE_SINGLE;
+        env->X.in = &im;
+        rows.assign(std::max(in->n_candidates, 1), kp_probe_result{});
+        run_probes(env->X, 0, in->n_candidates, rows.data(), nt);
+        for (int i = 0; i < in->n_candidates && chosen < 0; i++)
+            if (rows[i].decision != KP_DECISION_NONE) {
+                chosen = KP_CONSOLIDATE_SINGLE;
+                probe = i;
+            }
+    }
+    if (chosen < 0) return KP_OK;
+    out->mode = chosen;
+    out->probe = probe;
+    out->first_candidate = chosen == KP_CONSOLIDATE_SINGLE ? probe : 0;
+    out->n_candidates = chosen == KP_CONSOLIDATE_SINGLE ? 1 : probe + 2;
+    out->result = rows[probe];
+    out->decision = rows[probe].decision;
+    if (out->decision != KP_DECISION_REPLACE) return KP_OK;
+    im.mode = chosen;
+    env->X.in = &im;
+    Replacement rep;
+    kp_probe_result again{};
+    run_probe(env->X, probe, again, &rep);
+    out->nodepool = rep.nodepool;
+    out->n_reserved = rep.n_held;
+    out->n_type_ids = (int)rep.opts.size();
+    const std::string txt = reqs_text(env->D, rep.reqs);
+    out->requirements_needed = (int64_t)txt.size() + 1;
+    bool small = false;
+    for (int i = 0; i < out->n_type_ids; i++) {
+        if (i < out->cap_type_ids && out->type_ids) out->type_ids[i] = rep.opts[i];
+        else small = true;
+    }
+    if (out->requirements && out->cap_requirements >= (int64_t)txt.size() + 1)
+        memcpy(out->requirements, txt.c_str(), txt.size() + 1);
+    else
+        small = true;
+    return small ? KP_E_BUFFER : KP_OK;
 }
 
 // Wall time of the probe phase of the last orc_consolidate (input parsing excluded): bench.py's CPU baseline.
 extern "C" double orc_consolidate_last_probe_seconds(void) { return g_last_probe_seconds; }
 
-extern "C" kp_status orc_result_nodeclaim_requirements(const orc_result* res, int32_t nc, char* buf, int64_t cap,
-                                                       int64_t* needed) {
-    if (!res || nc < 0 || nc >= (int)res->ncs.size()) return KP_E_INVALID;
+// canonical serialization: "key\tcomplement\tgt\tlt\tmin\tv1\x1fv2..." values sorted as strings, keys sorted
+static std::string reqs_text(const orc::Dict& D, const orc::Reqs& reqs) {
     std::string s;
-    const Dict& D = res->D;
-    // canonical serialization: "key\tcomplement\tgt\tlt\tmin\tv1\x1fv2..." values sorted as strings, keys sorted
     std::vector<std::string> lines;
-    for (auto& kv : res->ncs[nc].reqs.m) {
+    for (auto& kv : reqs.m) {
         const Req& r = kv.second;
         std::string l = D.keys[kv.first] + "\t" + (r.complement ? "1" : "0") + "\t" +
                         (r.has_gt ? std::to_string(r.gt) : "-") + "\t" + (r.has_lt ? std::to_string(r.lt) : "-") +
@@ -1487,6 +1602,13 @@ extern "C" kp_status orc_result_nodeclaim_requirements(const orc_result* res, in
     }
     std::sort(lines.begin(), lines.end());
     for (auto& l : lines) s += l + "\n";
+    return s;
+}
+
+extern "C" kp_status orc_result_nodeclaim_requirements(const orc_result* res, int32_t nc, char* buf, int64_t cap,
+                                                       int64_t* needed) {
+    if (!res || nc < 0 || nc >= (int)res->ncs.size()) return KP_E_INVALID;
+    const std::string s = reqs_text(res->D, res->ncs[nc].reqs);
     if (needed) *needed = (int64_t)s.size() + 1;
     if ((int64_t)s.size() + 1 > cap) return KP_E_BUFFER;
     memcpy(buf, s.c_str(), s.size() + 1);

@@ -43,6 +43,9 @@ def lib():
         _lib.orc_consolidate.argtypes = [C.POINTER(abi.kp_catalog_view), C.POINTER(abi.kp_consolidate_input),
                                          C.POINTER(abi.kp_probe_result), C.c_int32, C.c_int32]
         _lib.orc_consolidate.restype = C.c_int32
+        _lib.orc_consolidate_command.argtypes = [C.POINTER(abi.kp_catalog_view), C.POINTER(abi.kp_consolidate_input),
+                                                 C.c_int32, C.POINTER(abi.kp_consolidation_command), C.c_int32]
+        _lib.orc_consolidate_command.restype = C.c_int32
         _lib.orc_launch_select.argtypes = [C.POINTER(abi.kp_catalog_view), C.c_int32, C.POINTER(abi.kp_launch_request),
                                            C.c_int32, C.POINTER(abi.kp_launch_result), C.POINTER(C.c_int32), C.c_int32,
                                            C.POINTER(C.c_int32), C.c_int32]
@@ -159,6 +162,19 @@ def consolidate(cp, mode, probe_begin=0, probe_end=0, spot_to_spot=False, max_ca
     if st != 0:
         raise RuntimeError("orc_consolidate failed: %d" % st)
     return out[:max(0, b1 - b0)]
+
+
+def consolidate_command(cp, mode, spot_to_spot=False, max_candidates=100, n_threads=1, catalog_view=None):
+    """CPU oracle consolidation command (orc_consolidate_command) -> kpsim.consolidation.Command."""
+    from kpsim import consolidation, model
+    L = lib()
+    cv = catalog_view or model.CatalogView(cp.cluster.catalog)
+    iv = model.ConsolidateInputView(cp, mode, 0, 0, spot_to_spot, max_candidates)
+    st, cmd = consolidation.command_call(
+        lambda cc: L.orc_consolidate_command(C.byref(cv.view), C.byref(iv.view), mode, C.byref(cc), n_threads))
+    if st != 0:
+        raise RuntimeError("orc_consolidate_command failed: %d" % st)
+    return cmd
 
 
 def last_consolidate_seconds():

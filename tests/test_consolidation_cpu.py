@@ -237,3 +237,40 @@ def test_sharded_command_equals_single_rank_gloo():
     for p in procs:
         p.join(60)
     assert got[0] == want and got[1] == want
+
+
+# ------------------------------------------------------------------------------------------------
+# the command (orc_consolidate_command, the restatement kp_consolidate_command is checked against)
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", sorted(__import__("cons_cases").SCENARIOS))
+@pytest.mark.parametrize("mode", [abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_BOTH])
+def test_command_reference_scenarios(golden, name, mode):
+    """The reference's e2e consolidation outcomes (tests/cons_cases.py) from the oracle's command."""
+    import cons_cases
+    cp, expect = cons_cases.SCENARIOS[name](golden)
+    cmd = pyoracle.consolidate_command(cp, mode)
+    cons_cases.check_expect(cmd, cp, expect)
+    assert cmd.mode == abi.KP_CONSOLIDATE_SINGLE and cmd.candidates == [0]
+
+
+def _both(cp, fn, s2s):
+    m = consolidation.compute_command(cp, abi.KP_CONSOLIDATE_MULTI, fn)
+    return m if m.decision != abi.KP_DECISION_NONE else consolidation.compute_command(cp, abi.KP_CONSOLIDATE_SINGLE, fn)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_command_equals_probe_replay(seed):
+    """orc_consolidate_command = the Python replay (first valid single / firstNConsolidationOption) over the oracle's
+    probe rows; BOTH = multi-node, else single-node (the disruption controller's method order)."""
+    cp = _fuzz_cp(40 + seed)
+    s2s = seed % 2 == 0
+    fn = lambda c, m, b0, b1: pyoracle.consolidate(c, m, b0, b1, spot_to_spot=s2s)  # noqa: E731
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI, abi.KP_CONSOLIDATE_BOTH):
+        want = _both(cp, fn, s2s) if mode == abi.KP_CONSOLIDATE_BOTH else consolidation.compute_command(cp, mode, fn)
+        got = pyoracle.consolidate_command(cp, mode, spot_to_spot=s2s)
+        assert (got.decision, got.candidates, got.n_replacement_types, got.candidate_price, got.replacement_price) == \
+            (want.decision, want.candidates, want.n_replacement_types, want.candidate_price, want.replacement_price)
+        if got.decision == abi.KP_DECISION_REPLACE:
+            assert len(got.type_ids) == got.n_replacement_types and got.nodepool >= 0 and got.requirements
+        else:
+            assert got.type_ids == [] and got.nodepool == -1

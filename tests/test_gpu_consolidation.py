@@ -116,6 +116,21 @@ def test_multi_device_ctx(golden, devices):
             assert cst[4] == len(want)  # probes evaluated, summed over the devices
             n = len(want)
             assert_probes_equal(device_probes(multi, cp, mode, begin=n // 3, end=n - 2), want[n // 3:n - 2])
+        # KP_CONSOLIDATE_BOTH (the pass bench.py times): the multi-node and single-node parts are sharded separately;
+        # the full range and sub-ranges inside / straddling the multi-node part, against the one-device pass and the
+        # oracle
+        n_s = model.consolidation_probe_count(len(cp.candidates), abi.KP_CONSOLIDATE_SINGLE)
+        n_m = model.consolidation_probe_count(len(cp.candidates), abi.KP_CONSOLIDATE_MULTI)
+        for c in (one, multi):
+            c.upload_catalog(model.CatalogView(cp.cluster.catalog))
+            c.consolidate_prepare(model.ConsolidateInputView(cp, abi.KP_CONSOLIDATE_SINGLE))
+        want = one.consolidate_execute(abi.KP_CONSOLIDATE_BOTH, n_m + n_s)
+        assert_probes_equal(multi.consolidate_execute(abi.KP_CONSOLIDATE_BOTH, n_m + n_s), want)
+        assert multi.consolidate_stats()[1][4] == n_m + n_s
+        for b, e in ((n_m // 2, n_m + 37), (3, n_m - 5), (n_m + 11, n_m + n_s - 9)):
+            assert_probes_equal(multi.consolidate_execute(abi.KP_CONSOLIDATE_BOTH, n_m + n_s, b, e), want[b:e])
+        assert_probes_equal(want[:n_m], pyoracle.consolidate(cp, abi.KP_CONSOLIDATE_MULTI, n_threads=8))
+        assert_probes_equal(want[n_m:], pyoracle.consolidate(cp, abi.KP_CONSOLIDATE_SINGLE, n_threads=8))
         # split form: prepare once (every device), execute twice
         multi.consolidate_prepare(model.ConsolidateInputView(cp, abi.KP_CONSOLIDATE_SINGLE))
         n_s = model.consolidation_probe_count(len(cp.candidates), abi.KP_CONSOLIDATE_SINGLE)
@@ -232,3 +247,76 @@ def test_both_modes_one_pass(ctx, golden, seed):
     parts = [ctx.consolidate_execute(abi.KP_CONSOLIDATE_BOTH, n_m + n_s, b, e)
              for b, e in ((0, cut), (cut, 2 * cut), (2 * cut, n_m + n_s))]
     assert_probes_equal(np.concatenate(parts), both)
+
+
+# ------------------------------------------------------------------------------------------------
+# kp_consolidate_command: the decision loops replayed in the library + the replacement NodeClaim read-back
+# ------------------------------------------------------------------------------------------------
+CMD_FIELDS = ("decision", "mode", "probe", "candidates", "n_replacement_types", "candidate_price", "replacement_price",
+              "nodepool", "type_ids", "requirements", "n_reserved")
+
+
+def device_command(ctx, cp, mode, spot_to_spot=False):
+    ctx.upload_catalog(model.CatalogView(cp.cluster.catalog))
+    ctx.consolidate_prepare(model.ConsolidateInputView(cp, abi.KP_CONSOLIDATE_SINGLE, spot_to_spot=spot_to_spot))
+    return ctx.consolidate_command(mode)
+
+
+def assert_commands_equal(dev, orc):
+    for f in CMD_FIELDS:
+        assert getattr(dev, f) == getattr(orc, f), (f, dev, orc)
+
+
+def _command_cases(golden):
+    """(cp, spot_to_spot) over the fuzz generators: plain, minValues, reserved (REPLACE-heavy full clusters)."""
+    out = []
+    for seed in range(8):
+        rng = np.random.Generator(np.random.PCG64(2500 + seed))
+        sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 300)), replace=False))]
+        cp = fuzzgen.fuzz_consolidation(sub, 2500 + seed, n_nodes=int(rng.integers(4, 60)),
+                                        n_pods=int(rng.integers(20, 250)), all_spot=seed % 4 == 0, supported=True,
+                                        with_min=seed % 3 == 0)
+        out.append((cp, seed % 2 == 0))
+    for seed in range(8):
+        out.append((_reserved_consolidation(golden, 40 + seed, full_cluster=seed % 2 == 0), seed % 2 == 1))
+    return out
+
+
+def test_command_parity(ctx, golden):
+    """kp_consolidate_command = orc_consolidate_command for SINGLE / MULTI / BOTH: the chosen method, probe and
+    delete set, the probe row, and for a REPLACE the replacement's NodePool, price-ordered options, requirements text
+    (capacity-type narrowed to spot, reservation-id of the held reservations) and held-reservation count."""
+    n_replace = 0
+    for cp, s2s in _command_cases(golden):
+        for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI, abi.KP_CONSOLIDATE_BOTH):
+            dev = device_command(ctx, cp, mode, s2s)
+            assert_commands_equal(dev, pyoracle.consolidate_command(cp, mode, spot_to_spot=s2s))
+            n_replace += dev.decision == abi.KP_DECISION_REPLACE and len(dev.type_ids) > 1
+    assert n_replace >= 4
+
+
+@pytest.mark.parametrize("name", ["reserved_into", "reserved_between"])
+def test_command_reference_scenarios(ctx, golden, name):
+    """test/suites/consolidation/suite_test.go:915-1001 through the library: the on-demand m5.large is replaced by the
+    m5.xlarge in the new reservation; the m5.xlarge reserved node moves to the m5.large reservation."""
+    import cons_cases
+    cp, expect = cons_cases.SCENARIOS[name](golden)
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_BOTH):
+        cmd = device_command(ctx, cp, mode)
+        cons_cases.check_expect(cmd, cp, expect)
+        assert_commands_equal(cmd, pyoracle.consolidate_command(cp, mode))
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_command_multi_device(golden, devices):
+    """The command over a multi-device ctx (probes sharded, the read-back on the primary) equals one device's."""
+    from kpsim import native
+    one = native.Context(0)
+    multi = native.Context(devices=devices)
+    try:
+        for cp, s2s in _command_cases(golden)[::3]:
+            for mode in (abi.KP_CONSOLIDATE_MULTI, abi.KP_CONSOLIDATE_BOTH):
+                assert_commands_equal(device_command(multi, cp, mode, s2s), device_command(one, cp, mode, s2s))
+    finally:
+        multi.close()
+        one.close()
