@@ -2450,7 +2450,11 @@ static kp_status cons_prepare_one(kp_ctx* ctx, const kp_consolidate_input* in) t
     kp_ctx* c = ctx;
     if (!c->pref.relax_next.empty())
         return fail(ctx, KP_E_UNSUPPORTED, "consolidation over pods with preferences to relax is not supported by this build");
-    if (c->best_effort) return fail(ctx, KP_E_UNSUPPORTED, "consolidation with MIN_VALUES_POLICY=BestEffort is not supported by this build");
+    // BestEffort differs from Strict only where a minValues requirement cannot be met: without minValues the probes are
+    // the same simulation under either policy
+    if (c->best_effort && c->any_min_values)
+        return fail(ctx, KP_E_UNSUPPORTED, "consolidation with MIN_VALUES_POLICY=BestEffort over minValues NodePools is not "
+                                           "supported by this build");
     if (c->tg_G > 0)  // the probe kernel has no domain counters (each probe would need its own copy)
         return fail(ctx, KP_E_UNSUPPORTED, "consolidation over pods with topology spread / pod (anti-)affinity is not supported by this build");
     const KpDev& d = c->dev;

@@ -216,6 +216,7 @@ struct Solver {
     Req host_req;                     // hostname In [placeholder] of a new NodeClaim (no pod can select it)
     int next_host = 0;                // NewNodeClaim's hostname-placeholder counter (value id -2 - n)
     std::vector<TopoGroup> groups;    // Topology.topologyGroups ∪ inverseTopologyGroups
+    std::vector<TopoGroup> groups_dg; // ... as buildDomainGroups left them, before countDomains
     std::vector<std::vector<int>> t_cons, t_rec;  // per class: groups that constrain / count its pods
     kp_solve_stats stats{};
     // ReservationManager ([core] scheduling/reservationmanager.go): capacity per reservation ID, the least
@@ -727,6 +728,7 @@ struct orc_result {
 // Input views → NewScheduler state (catalog rows, classes, pods, NodeClaimTemplates in weight order, existing nodes),
 // then NewTopology (domain groups, topology groups, counts of the bound pods).
 static kp_status build_topology(Solver& s, const kp_solve_input* in, const std::vector<PoolDomains>& pools);
+static void count_bound_pod(Solver& s, int j, int b);
 
 static kp_status parse_into(Solver& s, const kp_catalog_view* cat, const kp_solve_input* in, int pref_policy) {
     Dict& D = s.D;
@@ -1127,32 +1129,38 @@ static kp_status build_topology(Solver& s, const kp_solve_input* in, const std::
             }
         }
     }
+    s.groups_dg = s.groups;  // the domain groups before any pod is counted (consolidation probes recount)
     // bound pods: countDomains (forward groups; node filter against the node's labels and taints) and the inverse
     // anti-affinity of bound pods (recorded at their node's domain)
     const int E = (int)s.own_existing.size();
     for (int i = 0; i < in->n_bound; i++) {
         const int j = in->bound_node[i], b = in->bound_class[i];
         if (j < 0 || j >= E || b < 0 || b >= C) return KP_E_INVALID;
-        const ExistingNode& n = s.own_existing[j];
-        for (TopoGroup& g : s.groups) {
-            if (g.inverse ? g.owner != b : !g.sel[b]) continue;
-            if (!g.inverse && g.type == KP_TOPO_SPREAD) {
-                const PodClass& fc = s.own_classes[g.owner];
-                if (g.aff_pol == KP_POLICY_HONOR && !reqs_compatible(D, n.reqs, fc.reqs, false)) continue;
-                if (g.taint_pol == KP_POLICY_HONOR && !tolerates_all(n.taints, fc.tols)) continue;
-            }
-            int dom;
-            if (g.host) {
-                dom = n.host;
-            } else {
-                auto it = n.reqs.m.find(g.key);
-                if (it == n.reqs.m.end() || it->second.complement || it->second.values.size() != 1) continue;  // unlabeled
-                dom = it->second.values[0];
-            }
-            g.cnt[dom]++;
-        }
+        count_bound_pod(s, j, b);
     }
     return KP_OK;
+}
+
+// countDomains / updateInverseAffinities for one pod of class b bound to existing node j.
+static void count_bound_pod(Solver& s, int j, int b) {
+    const ExistingNode& n = (*s.ex_base)[j];
+    for (TopoGroup& g : s.groups) {
+        if (g.inverse ? g.owner != b : !g.sel[b]) continue;
+        if (!g.inverse && g.type == KP_TOPO_SPREAD) {
+            const PodClass& fc = (*s.cp)[g.owner];
+            if (g.aff_pol == KP_POLICY_HONOR && !reqs_compatible(s.D, n.reqs, fc.reqs, false)) continue;
+            if (g.taint_pol == KP_POLICY_HONOR && !tolerates_all(n.taints, fc.tols)) continue;
+        }
+        int dom;
+        if (g.host) {
+            dom = n.host;
+        } else {
+            auto it = n.reqs.m.find(g.key);
+            if (it == n.reqs.m.end() || it->second.complement || it->second.values.size() != 1) continue;  // unlabeled
+            dom = it->second.values[0];
+        }
+        g.cnt[dom]++;
+    }
 }
 
 extern "C" kp_status orc_solve_opts(const kp_catalog_view* cat, const kp_solve_input* in, const kp_device_opts* opts,
@@ -1322,6 +1330,20 @@ static void run_probe(const ConsCtx& X, int probe, kp_probe_result& pr, Replacem
     }
     for (int j = 0; j < (int)b.own_existing.size(); j++)
         if (!excluded[j]) s.ex_idx.push_back(j);
+    // NewTopology of the simulation: the domain groups, then countDomains over the pods bound in the cluster except
+    // the ones this simulation schedules (excludedPods = its candidates' reschedulable pods): the pods of
+    // cluster.bound and every other candidate's reschedulable pods on that candidate's node
+    if (!b.groups.empty()) {
+        s.groups = b.groups_dg;
+        s.t_cons = b.t_cons;
+        s.t_rec = b.t_rec;
+        for (int i = 0; i < in->cluster.n_bound; i++) count_bound_pod(s, in->cluster.bound_node[i], in->cluster.bound_class[i]);
+        for (int c = 0; c < in->n_candidates; c++) {
+            if (c >= c0 && c < c1) continue;
+            const kp_candidate& cd = in->candidates[c];
+            for (int i = 0; i < cd.n_pods; i++) count_bound_pod(s, cd.node, b.own_pods[cd.pods[i]].cls);
+        }
+    }
     // pods = pending + candidates' reschedulable pods
     for (int i = 0; i < in->n_pending; i++) s.plist.push_back(in->pending[i]);
     const int n_pending = (int)s.plist.size();
@@ -1429,7 +1451,11 @@ struct ConsEnv {
 
 static kp_status cons_setup(const kp_catalog_view* cat, const kp_consolidate_input* in, ConsEnv& env) {
     if (!cat || !in) return KP_E_INVALID;
-    if (in->cluster.min_values_policy != KP_MIN_VALUES_STRICT) return KP_E_UNSUPPORTED;
+    // MIN_VALUES_POLICY=BestEffort: the same simulation as Strict unless a NodePool carries minValues
+    if (in->cluster.min_values_policy != KP_MIN_VALUES_STRICT)
+        for (int i = 0; i < in->cluster.n_nodepools; i++)
+            for (int q = 0; q < in->cluster.nodepools[i].n_requirements; q++)
+                if (in->cluster.nodepools[i].requirements[q].min_values >= 0) return KP_E_UNSUPPORTED;
     Dict& D = env.D;
     Solver& base = env.base;
     base.resv_on = true;        // ReservedCapacity gate on; disruption simulations use ReservedOfferingModeFallback
@@ -1437,9 +1463,6 @@ static kp_status cons_setup(const kp_catalog_view* cat, const kp_consolidate_inp
     kp_status st = parse_into(base, cat, &in->cluster, KP_PREFERENCE_RESPECT);
     if (st != KP_OK) return st;
     if (!base.relax_next.empty()) return KP_E_UNSUPPORTED;  // preference relaxation inside probes: not restated
-    // consolidation over topology-constrained pods (topology counts of the remaining cluster, excluded candidate pods)
-    // is not restated yet
-    if (!base.groups.empty()) return KP_E_UNSUPPORTED;
     const int E = (int)base.own_existing.size(), P = (int)base.own_pods.size();
     for (int i = 0; i < in->n_pending; i++)
         if (in->pending[i] < 0 || in->pending[i] >= P) return KP_E_INVALID;

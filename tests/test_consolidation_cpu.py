@@ -274,3 +274,50 @@ def test_command_equals_probe_replay(seed):
             assert len(got.type_ids) == got.n_replacement_types and got.nodepool >= 0 and got.requirements
         else:
             assert got.type_ids == [] and got.nodepool == -1
+
+
+# ------------------------------------------------------------------------------------------------
+# the reference's e2e disruption scenarios on the cluster emulator, oracle backend (tests/e2e_cases.py)
+# ------------------------------------------------------------------------------------------------
+def _oracle_backend():
+    import cluster_sim
+    return cluster_sim.OracleBackend()
+
+
+@pytest.mark.parametrize("spot", [False, True])
+def test_e2e_replace_hostname_spread(golden, spot):
+    import e2e_cases
+    sim = e2e_cases.replace_hostname_spread(golden, _oracle_backend(), spot)
+    assert [c.decision for c in sim.commands] == [abi.KP_DECISION_REPLACE] * 3 + [abi.KP_DECISION_NONE]
+
+
+def test_e2e_od_to_spot(golden):
+    import e2e_cases
+    e2e_cases.od_to_spot(golden, _oracle_backend())
+
+
+@pytest.mark.parametrize("spot", [False, True])
+def test_e2e_delete_utilization(golden, spot):
+    import e2e_cases
+    e2e_cases.delete_utilization(golden, _oracle_backend(), spot)
+
+
+def test_e2e_anti_affinity_replace(golden):
+    import e2e_cases
+    e2e_cases.anti_affinity_replace(golden, _oracle_backend(), n_nodes=8)
+
+
+def test_e2e_multi_delete(golden):
+    import e2e_cases
+    sim = e2e_cases.multi_delete(golden, _oracle_backend(), n_nodes=50)
+    assert sim.commands[0].mode == abi.KP_CONSOLIDATE_MULTI
+
+
+@pytest.mark.parametrize("name", ["reserved_into", "reserved_between"])
+def test_command_reference_scenarios_best_effort(golden, name):
+    """suite_test.go's reserved scenarios run under MIN_VALUES_POLICY BestEffort too (the Describe's Entries,
+    :1002-1004): without minValues the simulation is the Strict one."""
+    import cons_cases
+    cp, expect = cons_cases.SCENARIOS[name](golden)
+    cp.cluster.min_values_policy = 1
+    cons_cases.check_expect(pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH), cp, expect)
