@@ -55,8 +55,20 @@ struct KpCons {
     int32_t* rec_i;
     ReqHdr* rec_hdr;
     uint64_t* rec_words;
+    // topology (consolidate_kernel<..., TOPO>): per-worker probe counts (ProbeTopo, kp_eval.h) and the probes' starting
+    // decrements — the value-keyed counts of the pods each probe reschedules, one row of 64 counts per group:
+    // single-node probe c: rows [dec_soff[c], dec_soff[c + 1]); multi-node probe i: rows [dec_moff[i], dec_moff[i + 1])
+    int32_t G, HG;
+    int32_t* pt_cnt;            // [workers][G][64]
+    uint64_t* pt_known;         // [workers][G]
+    int32_t* pt_hd;             // [workers][HG][E + 1]
+    const uint64_t* pt_dgk;     // [G]
+    const int32_t* dec_soff;
+    const int32_t* dec_moff;
+    const int32_t* dec_g;       // [rows] group of the row
+    const int32_t* dec_v;       // [rows][64]
     int32_t profile;            // s_memtime stage cycles (KPSIM_PROFILE)
     int32_t no_fast;            // diagnostics: every probe on the FULL variant (KPSIM_CONS_NOFAST)
     // dynamic LDS plan (kp_cons_plan_lds)
-    int32_t off_hdr, off_words, off_rem, off_excl, off_mod, off_init, off_xtc, lds_bytes;
+    int32_t off_hdr, off_words, off_rem, off_excl, off_mod, off_init, off_xtc, off_touch, off_hmod, lds_bytes;
 };

@@ -162,7 +162,12 @@ __device__ inline uint64_t commit_held(int32_t* rcap, uint64_t old, uint64_t nw,
 // ReservedOfferingModeFallback (SimulateScheduling never fails an Add for want of a reservation), the in-flight
 // NodeClaim's held IDs take / release the probe's capacities, FinalizeScheduling adds reservation-id In [held], and
 // OrderByPrice / WorstLaunchPrice see the reserved offerings.
-template <bool FULL, bool RESV = false>
+// TOPO: the cluster's pods carry topology terms — each probe keeps its own domain counts (ProbeTopo: the prepared base of
+// every bound pod minus the pods it reschedules); pods of constrained classes run ExistingNode.Add's
+// Topology.AddRequirements on each candidate node (first-fit over the nodes that pass, never memoised: counts move) and
+// NodeClaim.Add's on the in-flight NodeClaim (hostname row E) and on templates (a fresh hostname, count 0); every
+// placement of a counted class is recorded.
+template <bool FULL, bool RESV = false, bool TOPO = false>
 __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     ConsShared& S = *reinterpret_cast<ConsShared*>(smem);
@@ -174,6 +179,17 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
     uint64_t* initb = reinterpret_cast<uint64_t*>(smem + k.off_init);
     uint64_t* xtc = reinterpret_cast<uint64_t*>(smem + k.off_xtc);  // XT column of the cached chunk, by class
     const int lane = threadIdx.x;
+    ProbeTopo P{};
+    if (TOPO) {
+        P.cnt = k.pt_cnt + (size_t)blockIdx.x * k.G * 64;
+        P.known = k.pt_known + (size_t)blockIdx.x * k.G;
+        P.touched = reinterpret_cast<uint64_t*>(smem + k.off_touch);
+        P.hd = k.pt_hd + (size_t)blockIdx.x * k.HG * (d.E + 1);
+        P.hmod = reinterpret_cast<uint64_t*>(smem + k.off_hmod);
+        P.dgk = k.pt_dgk;
+        P.E = d.E;
+        P.HG = k.HG;
+    }
     const int wid = blockIdx.x;
     const int E = d.E, EW = d.EW, A = d.n_active, R = d.R, K = d.K, TW = d.TW, T = d.T, NT = d.NT;
     const int cap = k.ring_cap;
@@ -211,6 +227,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
     Ev.type_ro = RESV ? d.type_ro : nullptr;
     Ev.rcap = RESV ? S.rcap : nullptr;
     Ev.resv_on = RESV ? d.resv_on : 0;  // disruption simulations: ReservedOfferingModeFallback (STRICT = false below)
+    Ev.pt = TOPO ? &P : nullptr;
 
     for (int it = 0;; it++) {
         int probe = 0;
@@ -251,6 +268,15 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
         for (int c = c0 + lane; c < c1; c += 64) {
             const int node = k.cand_i[c * 4 + 0];
             atomicOr((unsigned long long*)&excl[node >> 6], 1ull << (node & 63));
+        }
+        if (TOPO) {
+            // this probe's NewTopology: no row copied yet, no node column of its own; then the pods it reschedules come
+            // off the base counts
+            for (int w = lane; w < ((k.G + 63) >> 6); w += 64) P.touched[w] = 0;
+            for (int w = lane; w < EW; w += 64) P.hmod[w] = 0;
+            __syncthreads();
+            const int r0 = single ? k.dec_soff[gp] : k.dec_moff[gp], r1 = single ? k.dec_soff[gp + 1] : k.dec_moff[gp + 1];
+            for (int r = r0; r < r1; r++) pt_init_row(d, P, k.dec_g[r], k.dec_v + (size_t)r * 64, lane);
         }
         double cprice = 0.0;
         bool all_spot = true;
@@ -406,14 +432,23 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 prev_shape = shape;
                 xstart = 0;
             }
+            // TOPO: a class counted by some group records each placement; a constrained class's node rejections depend
+            // on counts (scan from the first node, no resume)
+            uint32_t cflags = 0;
+            if (TOPO) {
+                cflags = __builtin_amdgcn_readfirstlane(d.cls_flags[c]);
+                if ((cflags & CF_TOPO) && S.CC.cls != c) fill_class_cache(d, c, S.CC, lane, 64);
+            }
+            const bool tcons = TOPO && (cflags & CF_TOPO_CONS);
+            const int xs = tcons ? 0 : xstart;
             // ExistingNode.Add in scheduling order (candidates excluded), 64-node aligned chunks; the chunk of the last
             // placement stays in registers (effective headroom and this probe's added requests per lane)
             int jf = -1;
             const long long cs0 = prof ? __builtin_amdgcn_s_memtime() : 0;
-            for (int base = __builtin_amdgcn_readfirstlane(xstart & ~63); base < E; base += 64) {
+            for (int base = __builtin_amdgcn_readfirstlane(xs & ~63); base < E; base += 64) {
                 const int w = base >> 6;
                 const int j = base + lane;
-                const uint64_t ge = xstart > base ? (~0ull << (xstart - base)) : ~0ull;
+                const uint64_t ge = xs > base ? (~0ull << (xs - base)) : ~0ull;
                 uint64_t xw, mw = 0;
                 int64_t h[KP_LDS_AXES], dl[KP_LDS_AXES];
                 if (base == cbase) {
@@ -454,7 +489,15 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 for (int ai = 0; ai < KP_LDS_AXES; ai++)
                     if (ai < A) cand &= q[ai] <= h[ai];
                 st_nodes += 64;
-                const uint64_t m = ballot(cand);
+                uint64_t m = ballot(cand);
+                if (tcons) {  // ExistingNode.Add's topology step on each fitting node, in order
+                    while (m) {
+                        const int jj = __builtin_amdgcn_readfirstlane(base + __ffsll((unsigned long long)m) - 1);
+                        if (existing_topo_try<true, true>(d, S.CC, S.ws, jj, lane, &P)) break;
+                        m &= m - 1;
+                    }
+                    m = uni64(m);
+                }
                 if (m) {
                     jf = __builtin_amdgcn_readfirstlane(base + __ffsll((unsigned long long)m) - 1);
                     if (base != cbase) {
@@ -495,7 +538,12 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     }
                 }
                 cmod |= 1ull << (jf & 63);  // jf lies in the cached chunk
-                xstart = jf;
+                if (!tcons) xstart = jf;
+                if (TOPO && (cflags & CF_TOPO)) {  // Topology.Record with the node's merged requirements and taints
+                    if (!tcons) existing_topo_try<false, true>(d, S.CC, S.ws, jf, lane, &P);
+                    topo_record<true>(d, S.CC, S.ws, d.ex_hdr + (size_t)jf * K, d.ex_words + (size_t)jf * d.DW, jf, -1,
+                                      false, lane, jf, &P);
+                }
                 st_placed++;
                 if (!pend) {
                     if ((cinit >> (jf & 63)) & 1ull) ok_np++;
@@ -503,7 +551,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 }
                 continue;
             }
-            xstart = E;
+            if (!tcons) xstart = E;
             if constexpr (!FULL) {
                 aborted = true;  // needs a NodeClaim: the FULL variant redoes this probe
                 break;
@@ -523,10 +571,11 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 a.compat = true;
                 a.force_off = false;
                 a.prof = nullptr;
-                a.host = 0;
+                a.host = E;  // the in-flight NodeClaim's hostname row
                 a.held = nc_held;
                 st_nc++;
-                if (eval_wave<false, RESV, false>(d, Ev, S.CC, a, S.ws, lane)) {
+                if (tcons ? eval_wave<true, RESV, false, true, true>(d, Ev, S.CC, a, S.ws, lane)
+                          : eval_wave<false, RESV, false>(d, Ev, S.CC, a, S.ws, lane)) {
                     if (lane < S.CC.nck) {
                         const int kk = S.CC.key[lane];
                         nch[kk] = S.ws.hdr[lane];
@@ -536,6 +585,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     if (lane < R) S.nc_req[lane] += preq[lane];
                     if (RESV && d.resv_on) nc_held = commit_held(S.rcap, nc_held, S.ws.held, lane);
                     __syncthreads();
+                    if (TOPO && (cflags & CF_TOPO)) topo_record<true>(d, S.CC, S.ws, nch, ncw, E, nc_tmpl, true, lane, -1, &P);
                     placed = true;
                 }
             }
@@ -555,10 +605,12 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     a.compat = true;
                     a.force_off = false;
                     a.prof = nullptr;
-                    a.host = 0;
+                    a.host = E + 1;  // a new NodeClaim's hostname: no pod counted there yet
                     a.held = 0;
                     st_tmpl++;
-                    if (!eval_wave<false, RESV, false>(d, Ev, S.CC, a, S.ws, lane)) continue;
+                    if (!(tcons ? eval_wave<true, RESV, false, true, true>(d, Ev, S.CC, a, S.ws, lane)
+                                : eval_wave<false, RESV, false>(d, Ev, S.CC, a, S.ws, lane)))
+                        continue;
                     if (n_nc == 1) {  // a second NodeClaim: computeConsolidation returns NONE
                         stop = true;
                         break;
@@ -592,6 +644,12 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     n_nc = 1;
                     placed = true;
                     __syncthreads();
+                    if (TOPO) {  // the NodeClaim's hostname row starts empty; Record the pod
+                        for (int r = lane; r < k.HG; r += 64)
+                            __hip_atomic_store(&P.hd[(size_t)r * (E + 1) + E], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        if (cflags & CF_TOPO) topo_record<true>(d, S.CC, S.ws, nch, ncw, E, j, true, lane, -1, &P);
+                    }
                     break;
                 }
             }
@@ -908,29 +966,41 @@ bool kp_cons_plan_lds(const KpDev& d, KpCons& k, int max_bytes) {
     off = al(off + 8 * (size_t)(d.EW > 0 ? d.EW : 1));
     k.off_xtc = (int)off;
     off = al(off + 8 * (size_t)(d.C < KP_CONS_XTC ? (d.C > 0 ? d.C : 1) : KP_CONS_XTC));
+    k.off_touch = (int)off;  // TOPO: the probe's copied count rows and node host-count columns
+    off = al(off + (k.G > 0 ? 8 * (size_t)((k.G + 63) / 64) : 0));
+    k.off_hmod = (int)off;
+    off = al(off + (k.G > 0 ? 8 * (size_t)(d.EW > 0 ? d.EW : 1) : 0));
     k.lds_bytes = (int)off;
     return (int)off <= max_bytes;
 }
 
 // Per-device kernel attributes, set by kp_ctx_create with the ctx's device current (see kp_ffd_set_attributes).
 hipError_t kp_cons_set_attributes() {
-    hipError_t e = hipFuncSetAttribute((const void*)consolidate_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       KP_LDS_BYTES);
-    if (e == hipSuccess)
-        e = hipFuncSetAttribute((const void*)consolidate_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                KP_LDS_BYTES);
-    if (e == hipSuccess)
-        e = hipFuncSetAttribute((const void*)consolidate_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                KP_LDS_BYTES);
-    return e;
+    const void* fns[] = {(const void*)consolidate_kernel<false>, (const void*)consolidate_kernel<true>,
+                         (const void*)consolidate_kernel<true, true>, (const void*)consolidate_kernel<false, false, true>,
+                         (const void*)consolidate_kernel<true, false, true>, (const void*)consolidate_kernel<true, true, true>};
+    for (const void* f : fns) {
+        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, KP_LDS_BYTES);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t kp_launch_consolidate(const KpDev& d, const KpCons& k, int n_workers, hipStream_t s) {
     if (n_workers <= 0 || k.n_probes <= 0) return hipSuccess;
-    if (k.no_fast != 1) hipLaunchKernelGGL(consolidate_kernel<false>, dim3(n_workers), dim3(64), (size_t)k.lds_bytes, s, d, k);
+    const size_t lds = (size_t)k.lds_bytes;
+    if (k.G > 0) {
+        if (k.no_fast != 1) hipLaunchKernelGGL((consolidate_kernel<false, false, true>), dim3(n_workers), dim3(64), lds, s, d, k);
+        if (k.no_fast != 2) {
+            if (d.ro) hipLaunchKernelGGL((consolidate_kernel<true, true, true>), dim3(n_workers), dim3(64), lds, s, d, k);
+            else hipLaunchKernelGGL((consolidate_kernel<true, false, true>), dim3(n_workers), dim3(64), lds, s, d, k);
+        }
+        return hipGetLastError();
+    }
+    if (k.no_fast != 1) hipLaunchKernelGGL(consolidate_kernel<false>, dim3(n_workers), dim3(64), lds, s, d, k);
     if (k.no_fast != 2) {
-        if (d.ro) hipLaunchKernelGGL((consolidate_kernel<true, true>), dim3(n_workers), dim3(64), (size_t)k.lds_bytes, s, d, k);
-        else hipLaunchKernelGGL(consolidate_kernel<true>, dim3(n_workers), dim3(64), (size_t)k.lds_bytes, s, d, k);
+        if (d.ro) hipLaunchKernelGGL((consolidate_kernel<true, true>), dim3(n_workers), dim3(64), lds, s, d, k);
+        else hipLaunchKernelGGL(consolidate_kernel<true>, dim3(n_workers), dim3(64), lds, s, d, k);
     }
     return hipGetLastError();
 }

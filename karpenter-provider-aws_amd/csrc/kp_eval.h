@@ -93,6 +93,22 @@ struct Roles {
     int nw[5];
 };
 
+// Topology counts of one consolidation probe (SimulateScheduling builds its own Topology: the domain groups, then
+// countDomains over the bound pods minus the ones it reschedules).  The prepared pass holds the base counts of every bound
+// pod (d.tg_cnt / d.tg_hcnt, read-only in probes); a probe keeps its own value-keyed rows (copied from the base on first
+// use, the probe's candidates' pods subtracted at probe start) and hostname-count deltas per node column (valid once the
+// node's hmod bit is set; column E is the probe's in-flight NodeClaim).  Hostname pod affinity (whose bootstrap counts
+// domains) is refused on the host.
+struct ProbeTopo {
+    int32_t* cnt;          // [G][64] value-keyed counts (row g valid when touched bit g is set)
+    uint64_t* known;       // [G] registered domains of row g
+    uint64_t* touched;     // LDS [ceil(G / 64)]
+    int32_t* hd;           // [HG][E + 1] hostname-count deltas
+    uint64_t* hmod;        // LDS [EW]: node column valid
+    const uint64_t* dgk;   // [G] domains of buildDomainGroups (registered before any pod is counted)
+    int E, HG;
+};
+
 // Tables shared by every evaluation of a kernel (LDS in ffd_kernel).
 struct EvalEnv {
     const int64_t* alloc;      // [lds_nstage][astride] staged allocatable of the first active axes
@@ -108,6 +124,7 @@ struct EvalEnv {
     const uint64_t* type_ro;   // [T] the type's reserved offerings (bits over ro index)
     const int32_t* rcap;       // ReservationManager capacity by reservation-id value id (FFD kernel LDS)
     int resv_on;               // run the reservation step of NodeClaim.Add
+    const ProbeTopo* pt;       // consolidation probe topology counts (eval_wave<..., CT = true>)
 };
 
 // Cooperative fill by all threads of the block; contains two __syncthreads().
@@ -341,6 +358,44 @@ __device__ __forceinline__ int wave_min_i32(int x) {
     return (int)wave_reduce32((uint32_t)x, [](uint32_t a, uint32_t b) { return (int)b < (int)a ? b : a; });
 }
 
+// ---- probe topology counts (ProbeTopo) ----
+// Row g of the probe's value-keyed counts: base - dec (the probe's candidates' pods, at probe start) or the base (first
+// use); its registered domains are buildDomainGroups' plus every domain with a positive count.  Hostname rows: column
+// j < E is node j, column E the probe's in-flight NodeClaim, E + 1 a NodeClaim being created (no pods yet).
+__device__ inline void pt_init_row(const KpDev& d, const ProbeTopo& P, int g, const int32_t* dec, int lane) {
+    const int32_t v = d.tg_cnt[(size_t)g * 64 + lane] - (dec ? dec[lane] : 0);
+    __hip_atomic_store(&P.cnt[(size_t)g * 64 + lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t kn = P.dgk[g] | ballot(v > 0);
+    if (lane == 0) {
+        __hip_atomic_store(&P.known[g], kn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        P.touched[g >> 6] |= 1ull << (g & 63);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void pt_row(const KpDev& d, const ProbeTopo& P, int g, int lane) {
+    const uint64_t t = __builtin_amdgcn_readfirstlane((int)(uint32_t)(P.touched[g >> 6] >> (g & 63))) & 1;
+    if (!t) pt_init_row(d, P, g, nullptr, lane);
+}
+__device__ __forceinline__ int pt_hcnt(const KpDev& d, const ProbeTopo& P, int hrow, int host) {
+    int32_t* col = P.hd + (size_t)hrow * (P.E + 1);
+    if (host > P.E) return 0;  // a NodeClaim not created yet
+    if (host == P.E) return ld_i32(col + P.E);
+    int c = d.tg_hcnt[(size_t)hrow * d.HN + host];
+    if ((P.hmod[host >> 6] >> (host & 63)) & 1ull) c += ld_i32(col + host);
+    return c;
+}
+// one more pod counted in hostname row hrow at `host` (whole wave)
+__device__ inline void pt_hadd(const ProbeTopo& P, int hrow, int host, int lane) {
+    if (host < P.E && !((P.hmod[host >> 6] >> (host & 63)) & 1ull)) {
+        for (int r = lane; r < P.HG; r += 64)
+            __hip_atomic_store(&P.hd[(size_t)r * (P.E + 1) + host], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) P.hmod[host >> 6] |= 1ull << (host & 63);
+    }
+    if (lane == 0) atomicAdd(&P.hd[(size_t)hrow * (P.E + 1) + host], 1);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+
 // Topology.AddRequirements ([core] scheduling/topology.go) for one candidate, after the requirement merge: every group
 // that constrains the pod's class yields its allowed domains (TopologyGroup.Get: nextDomainTopologySpread /
 // nextDomainAffinity / nextDomainAntiAffinity), all computed from the same merged requirements (nodeDomains) and
@@ -349,8 +404,10 @@ __device__ __forceinline__ int wave_min_i32(int x) {
 // iteration order; the smallest value name (vrank) is the canonical choice (oracle/orc_solve.cpp topo_get).
 // Hostname groups: the candidate's own host is the only domain its requirements allow (hostname In [host]).
 // ws.memo_ok is cleared when the outcome depends on counts (a count check failed or a key was narrowed).
+// CT: the counts are a consolidation probe's (pt).
+template <bool CT = false>
 __device__ __forceinline__ bool topo_narrow(const KpDev& d, const ClassCache& CC, WaveScratch& ws, int host, bool allow_wk,
-                                         int lane) {
+                                         int lane, const ProbeTopo* pt = nullptr) {
     int nk = 0;
     int kidx[KP_MAX_TOPO];
     uint64_t kmask[KP_MAX_TOPO];
@@ -359,11 +416,11 @@ __device__ __forceinline__ bool topo_narrow(const KpDev& d, const ClassCache& CC
         const int4 info = d.tg_info[g];
         const int type = info.x & TG_TYPE;
         if (info.x & TG_HOST) {
-            const int cnt = ld_i32(&d.tg_hcnt[(size_t)d.tg_hrow[g] * d.HN + host]);
+            const int cnt = CT ? pt_hcnt(d, *pt, d.tg_hrow[g], host) : ld_i32(&d.tg_hcnt[(size_t)d.tg_hrow[g] * d.HN + host]);
             bool ok;
             if (type == 0) ok = cnt + self <= info.z;             // spread: hostname domainMinCount is 0
             else if (type == 2) ok = cnt == 0;                    // anti-affinity: an empty domain
-            else ok = cnt > 0 || (self && ld_i32(&d.tg_pos[g]) == 0);  // affinity (self-selecting bootstrap)
+            else ok = cnt > 0 || (!CT && self && ld_i32(&d.tg_pos[g]) == 0);  // affinity (self-selecting bootstrap)
             if (!ok) {
                 ws.memo_ok = 0;
                 return false;
@@ -372,9 +429,10 @@ __device__ __forceinline__ bool topo_narrow(const KpDev& d, const ClassCache& CC
         }
         const int k = info.y;
         const bool valid = lane < CC.nval[ki];
-        const uint64_t known = ld_u64(&d.tg_known[g]);
+        if (CT) pt_row(d, *pt, g, lane);
+        const uint64_t known = ld_u64(CT ? &pt->known[g] : &d.tg_known[g]);
         const bool kn = valid && ((known >> lane) & 1ull);
-        const int cnt = kn ? ld_i32(&d.tg_cnt[(size_t)g * 64 + lane]) : 0;
+        const int cnt = kn ? ld_i32(CT ? &pt->cnt[(size_t)g * 64 + lane] : &d.tg_cnt[(size_t)g * 64 + lane]) : 0;
         const bool pod_has = valid && req_has(d, k, lane, CC.hdr[ki], CC.words + CC.wsoff[ki]);
         const ReqHdr nh = ws.hdr[ki];
         const bool node_has = valid && (!(nh.flags & RF_DEF) || req_has(d, k, lane, nh, ws.words + CC.wsoff[ki]));
@@ -484,8 +542,10 @@ __device__ inline bool topo_filter_compatible(const KpDev& d, const ClassCache& 
 }
 
 // exnode >= 0: the placement is on existing node exnode (its taints: ex_tol; its hostname is a real node name).
+template <bool CT = false>
 __device__ __forceinline__ void topo_record(const KpDev& d, const ClassCache& CC, const WaveScratch& ws, const ReqHdr* Ahdr,
-                                         const uint64_t* Aw, int host, int tmpl, bool allow_wk, int lane, int exnode = -1) {
+                                         const uint64_t* Aw, int host, int tmpl, bool allow_wk, int lane, int exnode = -1,
+                                         const ProbeTopo* pt = nullptr) {
     for (int e = 0; e < CC.ntr; e++) {
         const int g = CC.tr[e], ki = CC.tr_ki[e];
         const int4 info = d.tg_info[g];
@@ -501,7 +561,9 @@ __device__ __forceinline__ void topo_record(const KpDev& d, const ClassCache& CC
                 continue;
         }
         if (info.x & TG_HOST) {
-            if (lane == 0) {
+            if (CT) {
+                pt_hadd(*pt, d.tg_hrow[g], host, lane);
+            } else if (lane == 0) {
                 const int old = atomicAdd(&d.tg_hcnt[(size_t)d.tg_hrow[g] * d.HN + host], 1);
                 if (old == 0) atomicAdd(&d.tg_pos[g], 1);
             }
@@ -512,8 +574,11 @@ __device__ __forceinline__ void topo_record(const KpDev& d, const ClassCache& CC
         const uint64_t w = ki >= 0 ? ws.words[CC.wsoff[ki]] : ld_u64(Aw + d.woff[k]);
         if (!(h.flags & RF_DEF)) continue;  // Get() of an undefined key is Exists: no values
         if (!inv && type != 2 && ((h.flags & RF_CMP) || __popcll(w) != 1)) continue;
-        if ((w >> lane) & 1ull) atomicAdd(&d.tg_cnt[(size_t)g * 64 + lane], 1);
-        if (lane == 0 && w) atomicOr((unsigned long long*)&d.tg_known[g], (unsigned long long)w);
+        if (CT) pt_row(d, *pt, g, lane);
+        int32_t* cnt = CT ? pt->cnt : d.tg_cnt;
+        uint64_t* known = CT ? pt->known : d.tg_known;
+        if ((w >> lane) & 1ull) atomicAdd(&cnt[(size_t)g * 64 + lane], 1);
+        if (lane == 0 && w) atomicOr((unsigned long long*)&known[g], (unsigned long long)w);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -521,8 +586,9 @@ __device__ __forceinline__ void topo_record(const KpDev& d, const ClassCache& CC
 // after the caller found j tolerated, Compatible (XT) and with headroom: the requirement merge of the class's keys into
 // the node's requirements (no undefined-label allowance), then Topology.AddRequirements with the node's own domains
 // (hostname = the node's name: host row j).  On success ws holds the merged class keys.
-template <bool CONS>
-__device__ inline bool existing_topo_try(const KpDev& d, const ClassCache& CC, WaveScratch& ws, int j, int lane) {
+template <bool CONS, bool CT = false>
+__device__ inline bool existing_topo_try(const KpDev& d, const ClassCache& CC, WaveScratch& ws, int j, int lane,
+                                         const ProbeTopo* pt = nullptr) {
     const ReqHdr* nh = d.ex_hdr + (size_t)j * d.K;
     const uint64_t* nwp = d.ex_words + (size_t)j * d.DW;
     if (lane < CC.nck) {
@@ -543,7 +609,7 @@ __device__ inline bool existing_topo_try(const KpDev& d, const ClassCache& CC, W
         ws.hdr[lane] = O;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    if (CONS) return topo_narrow(d, CC, ws, j, false, lane);
+    if (CONS) return topo_narrow<CT>(d, CC, ws, j, false, lane, pt);
     return true;
 }
 
@@ -595,7 +661,7 @@ __device__ inline void existing_topo_commit(const KpDev& d, const ClassCache& CC
 // instantiations keep the topology and reservation code out of the common path.
 // STRICT: ReservedOfferingModeStrict (provisioning); false: Fallback (disruption simulations never fail an Add for want
 // of a reservation).  BE: the solve may run MIN_VALUES_POLICY=BestEffort (false compiles the relaxation bookkeeping out).
-template <bool TOPO, bool RESV = false, bool STRICT = true, bool BE = true>
+template <bool TOPO, bool RESV = false, bool STRICT = true, bool BE = true, bool CT = false>
 __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, const ClassCache& CC, const EvalIn& a,
                                           WaveScratch& ws, int lane) {
     const int TW = d.TW, T = d.T;
@@ -659,7 +725,7 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
     if (ballot(fail)) return false;
     if (TOPO) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        if (!topo_narrow(d, CC, ws, a.host, a.compat, lane)) return false;
+        if (!topo_narrow<CT>(d, CC, ws, a.host, a.compat, lane, E.pt)) return false;
         if (lane < nck) {
             const ReqHdr O = ws.hdr[lane];
             const uint64_t* ow = ws.words + CC.wsoff[lane];

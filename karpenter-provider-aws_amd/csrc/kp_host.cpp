@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cfloat>
 #include <chrono>
@@ -440,6 +441,7 @@ struct kp_ctx {
     bool any_min_values = false;             // some template requirement carries minValues
     bool min_multi = false;                  // ... on a multi-valued catalog key (zone, capacity type, ...)
     bool cons_mayfix = false;                // a pod's NotIn/DoesNotExist merge can change a later Compatible
+    std::string cons_mayfix_key;
     // consolidation probes
     DBuf<int32_t> d_retry, d_rank, d_cand_i, d_cand_off, d_cand_pods, d_pending, d_ring, d_ring_last, d_next;
     DBuf<double> d_cand_price;
@@ -510,6 +512,15 @@ struct kp_ctx {
         d_cls_tcoff, d_cls_tc, d_cls_troff, d_cls_tr;
     DBuf<uint64_t> d_tg_known0, d_tg_known;
     DBuf<uint8_t> d_cls_kneutral, d_vrank;
+    // consolidation over topology (kp_consolidate_prepare sets cons_extra before kp_solve_prepare): the candidates'
+    // reschedulable pods (node, pod, candidate) join the base counts; cons_dec[candidate][group] = its value-keyed counts
+    std::vector<std::array<int, 3>> cons_extra;
+    int cons_extra_ncand = 0;
+    std::vector<std::map<int, std::vector<int32_t>>> cons_dec;
+    std::vector<uint64_t> h_tknown_dg;       // [G] buildDomainGroups' domains (before any pod is counted)
+    DBuf<int32_t> d_dec_soff, d_dec_moff, d_dec_g, d_dec_v, d_pt_cnt, d_pt_hd;
+    DBuf<uint64_t> d_pt_known, d_pt_dgk;
+    std::vector<uint8_t> tg_host_aff;        // [G] hostname pod-affinity group (not in consolidation probes)
     // preference relaxation stages of the prepared solve (expand_preferences) and MIN_VALUES_POLICY
     PrefExpansion pref;
     bool best_effort = false;
@@ -1502,7 +1513,10 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         }
         c->cons_mayfix = false;
         for (int k = 0; k < K; k++)
-            if (neg[k] && pos[k] && undef[k]) c->cons_mayfix = true;
+            if (neg[k] && pos[k] && undef[k]) {
+                c->cons_mayfix = true;
+                c->cons_mayfix_key = c->sol.keys[k].name;
+            }
     }
     // ---- key layout ----
     std::vector<uint32_t> kflags(K, 0);
@@ -1865,6 +1879,10 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     const int G = (int)th.g.size();
     c->tg_G = G;
     c->tg_HG = th.n_host;
+    c->tg_host_aff.assign(std::max(G, 1), 0);
+    for (int gi = 0; gi < G; gi++)
+        c->tg_host_aff[gi] = th.g[gi].host && th.g[gi].type == KP_TOPO_AFFINITY && !th.g[gi].inverse;
+    c->cons_dec.assign(c->cons_extra_ncand, {});
     {
         const int G1 = std::max(G, 1);
         std::vector<int4> tinfo(G1);
@@ -1975,9 +1993,10 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
                     if (!tolerates(en.taints[q], in->classes[owner].tolerations, in->classes[owner].n_tolerations)) return false;
                 return true;
             };
-            for (int i = 0; i < in->n_bound; i++) {
-                const int j = in->bound_node[i], b = in->bound_class[i];
-                if (j < 0 || j >= E || b < 0 || b >= C) return fail(ctx, KP_E_INVALID, "bound pod index out of range");
+            c->h_tknown_dg.assign(tknown0.begin(), tknown0.end());  // buildDomainGroups only (consolidation probes)
+            // one bound pod of class b on node j; cand >= 0: a consolidation candidate's reschedulable pod, whose
+            // value-keyed contributions are also kept per candidate (a probe takes off the pods it reschedules)
+            auto count_pod = [&](int j, int b, int cand) -> bool {
                 for (int gi = 0; gi < G; gi++) {
                     const HGroup& g = th.g[gi];
                     if (g.inverse ? g.owner != b : !g.sel[b]) continue;
@@ -1990,12 +2009,28 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
                     } else {
                         const int v = node_val(j, g.key);
                         if (v < 0) continue;
-                        if (v >= 64) return fail(ctx, KP_E_UNSUPPORTED, "topology key with more than 64 values");
+                        if (v >= 64) return false;
                         tcnt0[(size_t)gi * 64 + v]++;
                         tknown0[gi] |= 1ull << v;
+                        if (cand >= 0) {
+                            auto& row = c->cons_dec[cand][gi];
+                            if (row.empty()) row.assign(64, 0);
+                            row[v]++;
+                        }
                     }
                 }
+                return true;
+            };
+            for (int i = 0; i < in->n_bound; i++) {
+                const int j = in->bound_node[i], b = in->bound_class[i];
+                if (j < 0 || j >= E || b < 0 || b >= C) return fail(ctx, KP_E_INVALID, "bound pod index out of range");
+                if (!count_pod(j, b, -1)) return fail(ctx, KP_E_UNSUPPORTED, "topology key with more than 64 values");
             }
+            // kp_consolidate_prepare: each candidate's reschedulable pods are bound to its node in the cluster
+            c->cons_dec.assign(c->cons_extra_ncand, {});
+            for (auto& e : c->cons_extra)
+                if (!count_pod(e[0], in->pods.class_id[e[1]], e[2]))
+                    return fail(ctx, KP_E_UNSUPPORTED, "topology key with more than 64 values");
         }
         if (tcl.empty()) tcl.push_back(0);
         if (trl.empty()) trl.push_back(0);
@@ -2445,7 +2480,16 @@ static kp_status cons_prepare_one(kp_ctx* ctx, const kp_consolidate_input* in) t
             }
         }
     }
+    // topology: every candidate's reschedulable pods are bound to its node in the cluster (base counts); kp_solve_prepare
+    // also keeps each candidate's value-keyed contributions (cons_dec) so that a probe takes off the pods it reschedules
+    ctx->cons_extra.clear();
+    ctx->cons_extra_ncand = NC;
+    for (int ci = 0; ci < NC; ci++)
+        for (int q = 0; q < in->candidates[ci].n_pods; q++)
+            ctx->cons_extra.push_back({in->candidates[ci].node, in->candidates[ci].pods[q], ci});
     kp_status st = kp_solve_prepare(ctx, &cl);
+    ctx->cons_extra.clear();
+    ctx->cons_extra_ncand = 0;
     if (st != KP_OK) return st;
     kp_ctx* c = ctx;
     if (!c->pref.relax_next.empty())
@@ -2455,15 +2499,18 @@ static kp_status cons_prepare_one(kp_ctx* ctx, const kp_consolidate_input* in) t
     if (c->best_effort && c->any_min_values)
         return fail(ctx, KP_E_UNSUPPORTED, "consolidation with MIN_VALUES_POLICY=BestEffort over minValues NodePools is not "
                                            "supported by this build");
-    if (c->tg_G > 0)  // the probe kernel has no domain counters (each probe would need its own copy)
-        return fail(ctx, KP_E_UNSUPPORTED, "consolidation over pods with topology spread / pod (anti-)affinity is not supported by this build");
+    for (int gi = 0; gi < c->tg_G; gi++)
+        if (c->tg_host_aff[gi])  // its bootstrap counts the hostname domains holding pods, which probes do not track
+            return fail(ctx, KP_E_UNSUPPORTED, "consolidation over pods with required hostname pod affinity is not supported by "
+                                               "this build");
     const KpDev& d = c->dev;
     // minValues NodePools: the probe kernel counts distinct values of single-valued catalog keys only
     if (c->min_multi)
         return fail(ctx, KP_E_UNSUPPORTED, "consolidation with minValues on a multi-valued label is not supported by this build");
     if (c->cons_mayfix)
         return fail(ctx, KP_E_UNSUPPORTED, "consolidation with NotIn/DoesNotExist pod requirements on keys some node lacks "
-                                           "and other pods select positively is not supported by this build");
+                                           "and other pods select positively is not supported by this build (" +
+                                               c->cons_mayfix_key + ")");
     if (d.n_active > KP_LDS_AXES) return fail(ctx, KP_E_UNSUPPORTED, "more than 6 requested resource axes");
     if (d.M <= 0 || d.M > 64) return fail(ctx, KP_E_UNSUPPORTED, "consolidation needs max_instance_types in 1..64");
     const int T = c->T, TW = c->TW, R = c->R, A = d.n_active;
@@ -2522,6 +2569,49 @@ static kp_status cons_prepare_one(kp_ctx* ctx, const kp_consolidate_input* in) t
     HIPCHK(c->d_cand_cap.upload(ccap, s));
     HIPCHK(c->d_init.upload(init, s));
     HIPCHK(c->d_alloc_act.upload(act, s));
+    // topology: the starting decrements of every probe — single-node probe ci: candidate ci's rows; multi-node probe i:
+    // the sum over candidates [0, i + 2) — one row of 64 value counts per group
+    k.G = c->tg_G;
+    k.HG = c->tg_HG;
+    if (k.G > 0) {
+        std::vector<int32_t> soff(NC + 1, 0), dg, dv;
+        for (int ci = 0; ci < NC; ci++) {
+            for (auto& kv : c->cons_dec[ci]) {
+                dg.push_back(kv.first);
+                dv.insert(dv.end(), kv.second.begin(), kv.second.end());
+            }
+            soff[ci + 1] = (int32_t)dg.size();
+        }
+        const int mx = c->cons_max_candidates;
+        const int nm = NC < 2 ? 0 : (NC <= mx ? NC - 1 : mx);
+        std::vector<int32_t> moff(nm + 1, (int32_t)dg.size());
+        std::map<int, std::vector<int32_t>> acc;
+        auto add = [&](int ci) {
+            for (auto& kv : c->cons_dec[ci]) {
+                auto& row = acc[kv.first];
+                if (row.empty()) row.assign(64, 0);
+                for (int v = 0; v < 64; v++) row[v] += kv.second[v];
+            }
+        };
+        for (int i = 0; i < nm; i++) {
+            if (i == 0) add(0);
+            add(i + 1);
+            for (auto& kv : acc) {
+                dg.push_back(kv.first);
+                dv.insert(dv.end(), kv.second.begin(), kv.second.end());
+            }
+            moff[i + 1] = (int32_t)dg.size();
+        }
+        if (dg.empty()) {
+            dg.push_back(0);
+            dv.assign(64, 0);
+        }
+        HIPCHK(c->d_dec_soff.upload(soff, s));
+        HIPCHK(c->d_dec_moff.upload(moff, s));
+        HIPCHK(c->d_dec_g.upload(dg, s));
+        HIPCHK(c->d_dec_v.upload(dv, s));
+        HIPCHK(c->d_pt_dgk.upload(c->h_tknown_dg, s));
+    }
     HIPCHK(c->d_next.ensure(3));
     HIPCHK(c->d_rank.ensure(std::max(P, 1)));
     HIPCHK(c->d_pend_bits.ensure(k.PW));
@@ -2583,6 +2673,21 @@ static kp_status cons_run(kp_ctx* ctx, int m0, int m1, int s0, int s1, kp_probe_
     if (!kp_cons_plan_lds(d, k, KP_LDS_BYTES)) return fail(ctx, KP_E_UNSUPPORTED, "consolidation LDS plan exceeds 160 KB");
     const int occ = std::max(1, std::min(8, KP_LDS_BYTES / std::max(k.lds_bytes, 1)));
     const int workers = std::min(nprobe, 256 * occ);
+    if (k.G > 0) {  // per-worker probe topology counts (ProbeTopo); the base counts are read-only in probes
+        HIPCHK(c->d_pt_cnt.ensure((size_t)workers * k.G * 64));
+        HIPCHK(c->d_pt_known.ensure((size_t)workers * k.G));
+        HIPCHK(c->d_pt_hd.ensure((size_t)workers * std::max(k.HG, 1) * (E + 1)));
+        k.pt_cnt = c->d_pt_cnt.p;
+        k.pt_known = c->d_pt_known.p;
+        k.pt_hd = c->d_pt_hd.p;
+        k.pt_dgk = c->d_pt_dgk.p;
+        k.dec_soff = c->d_dec_soff.p;
+        k.dec_moff = c->d_dec_moff.p;
+        k.dec_g = c->d_dec_g.p;
+        k.dec_v = c->d_dec_v.p;
+        d.tg_cnt = c->d_tg_cnt0.p;
+        d.tg_hcnt = c->d_tg_hcnt0.p;
+    }
     const auto t0 = clk::now();
     HIPCHK(c->d_ring.ensure((size_t)workers * k.ring_cap));
     HIPCHK(c->d_ring_last.ensure((size_t)workers * k.ring_cap));

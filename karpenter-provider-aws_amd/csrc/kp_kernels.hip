@@ -122,6 +122,7 @@ __global__ __launch_bounds__(64) void template_init_kernel(KpDev d) {
     }
     __syncthreads();
     EvalEnv E;
+    E.pt = nullptr;
     E.alloc = nullptr;  // no requests: Fits({}, alloc) only needs non-negative allocatable (tmpl rows ∧ nonneg)
     E.astride = 0;
     E.avail = d.avail_zc;
@@ -580,6 +581,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
     }
     __syncthreads();
     EvalEnv E;
+    E.pt = nullptr;
     E.alloc = sAlloc;
     E.astride = TP;
     E.avail = sAvail;

@@ -206,6 +206,10 @@ def drop_mutating_requirements(prob):
     """Remove NotIn/DoesNotExist pod requirements that could change a node's requirements in a way a later pod sees
     (a key some node lacks that another class selects positively): consolidation probes keep nodes immutable and the
     library rejects such inputs (KP_E_UNSUPPORTED)."""
+    def empty_in(pc, key):  # In requirements on one key with no common value: the merged requirement is In [] = DNE
+        ins = [set(r.values) for r in pc.requirements if r.key == key and r.op == "In"]
+        return len(ins) > 1 and not set.intersection(*ins)
+
     keys = set()
     for pc in prob.classes:
         keys |= {r.key for r in pc.requirements}
@@ -213,7 +217,8 @@ def drop_mutating_requirements(prob):
     undef = {k for k in keys if k != HOSTNAME and any(k not in n.labels for n in prob.existing)}
     bad = pos & undef
     for pc in prob.classes:
-        pc.requirements = [r for r in pc.requirements if not (_negative(r) and r.key in bad)]
+        pc.requirements = [r for r in pc.requirements
+                           if not ((_negative(r) or empty_in(pc, r.key)) and r.key in bad)]
     return prob
 
 
@@ -265,3 +270,19 @@ def fuzz_topology_existing_problem(catalog, seed, n_pods=200, n_classes=10, n_ex
     prob = add_topology(rng, prob)
     prob.bound = [(int(rng.integers(0, n_existing)), int(rng.integers(0, n_classes))) for _ in range(n_bound)]
     return prob
+
+
+def fuzz_topology_consolidation(catalog, seed, n_nodes=30, n_pods=160, n_bound=40, all_spot=False):
+    """fuzz_consolidation over pods with topology terms (add_topology: zonal / hostname / capacity-type spread,
+    anti-affinity, zonal affinity; hostname pod affinity is refused by the library and turned into anti-affinity here)
+    plus non-reschedulable pods bound to random nodes (cluster.bound)."""
+    cp = fuzz_consolidation(catalog, seed, n_nodes=n_nodes, n_pods=n_pods, all_spot=all_spot, supported=True)
+    rng = np.random.Generator(np.random.PCG64(seed + 123))
+    prob = add_topology(rng, cp.cluster, p_term=0.4)
+    for pc in prob.classes:
+        for t in pc.topology:
+            if t.kind == "affinity" and t.key == HOSTNAME:
+                t.kind = "anti"
+    E = len(prob.existing)
+    prob.bound = [(int(rng.integers(0, E)), int(rng.integers(0, len(prob.classes)))) for _ in range(n_bound)]
+    return cp

@@ -320,3 +320,83 @@ def test_command_multi_device(golden, devices):
     finally:
         multi.close()
         one.close()
+
+
+# ------------------------------------------------------------------------------------------------
+# consolidation over topology-constrained clusters (per-probe domain counts)
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("seed", range(24))
+def test_fuzz_consolidation_topology(ctx, golden, seed):
+    """Probes over pods with zonal / hostname / capacity-type spread, anti-affinity and zonal affinity, bound pods
+    counted: every probe's counts = the cluster's bound pods minus the pods it reschedules, against the oracle's
+    recount; and the command."""
+    rng = np.random.Generator(np.random.PCG64(3100 + seed))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 300)), replace=False))]
+    cp = fuzzgen.fuzz_topology_consolidation(sub, 3100 + seed, n_nodes=int(rng.integers(4, 60)),
+                                             n_pods=int(rng.integers(20, 250)), all_spot=seed % 4 == 0)
+    s2s = seed % 2 == 0
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        assert_probes_equal(device_probes(ctx, cp, mode, s2s), pyoracle.consolidate(cp, mode, spot_to_spot=s2s))
+    assert_commands_equal(device_command(ctx, cp, abi.KP_CONSOLIDATE_BOTH, s2s),
+                          pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH, spot_to_spot=s2s))
+
+
+def test_consolidation_refuses_hostname_affinity(ctx, golden):
+    from kpsim import native
+    cp = fuzzgen.fuzz_topology_consolidation(golden[:100], 11, n_nodes=10, n_pods=40)
+    cp.cluster.classes[0].topology = [model.TopologyTerm("affinity", model.HOSTNAME, [model.Requirement("app", "Exists")])]
+    with pytest.raises(native.KpError) as e:
+        device_probes(ctx, cp, abi.KP_CONSOLIDATE_SINGLE)
+    assert e.value.status == abi.KP_E_UNSUPPORTED
+
+
+# ------------------------------------------------------------------------------------------------
+# the reference's e2e disruption scenarios (tests/e2e_cases.py) driven through the library: Solve for provisioning,
+# kp_consolidate_command for disruption; the reference's end state, and the same command trajectory as the oracle
+# ------------------------------------------------------------------------------------------------
+def _trajectory(sim):
+    return [(c.decision, c.mode, c.candidates, c.type_ids, c.requirements, c.nodepool) for c in sim.commands]
+
+
+def _e2e(ctx, golden, fn, **kw):
+    import cluster_sim
+    dev = fn(golden, cluster_sim.DeviceBackend(ctx), **kw)
+    orc = fn(golden, cluster_sim.OracleBackend(), **kw)
+    assert _trajectory(dev) == _trajectory(orc)
+    return dev
+
+
+@pytest.mark.parametrize("spot", [False, True])
+def test_e2e_replace_hostname_spread(ctx, golden, spot):
+    """suite_test.go:574-729: 3 x 2xlarge (hostname spread) -> 3 x .large, one single-node REPLACE at a time."""
+    import e2e_cases
+    sim = _e2e(ctx, golden, e2e_cases.replace_hostname_spread, spot=spot)
+    assert [c.decision for c in sim.commands] == [abi.KP_DECISION_REPLACE] * 3 + [abi.KP_DECISION_NONE]
+
+
+def test_e2e_od_to_spot(ctx, golden):
+    """suite_test.go:730-860: on-demand nodes replaced by spot (replacement requirements narrowed to spot)."""
+    import e2e_cases
+    sim = _e2e(ctx, golden, e2e_cases.od_to_spot)
+    assert all("karpenter.sh/capacity-type\t0\t-\t-\t-\tspot\n" in c.requirements for c in sim.commands[:-1])
+
+
+@pytest.mark.parametrize("spot", [False, True])
+def test_e2e_delete_utilization(ctx, golden, spot):
+    """suite_test.go:491-573: 100 pods scaled to 40, consolidation deletes nodes until utilisation > 0.6."""
+    import e2e_cases
+    _e2e(ctx, golden, e2e_cases.delete_utilization, spot=spot)
+
+
+def test_e2e_anti_affinity_replace(ctx, golden):
+    """deprovisioning_test.go:454-523: 20 nodes with hostname anti-affinity, each replaced once the size requirement
+    goes (20 deleted, 20 remain)."""
+    import e2e_cases
+    _e2e(ctx, golden, e2e_cases.anti_affinity_replace, n_nodes=20)
+
+
+def test_e2e_multi_delete(ctx, golden):
+    """deprovisioning_test.go:399-453: 200 nodes at 20 pods, scaled to 20%: 160 deleted by multi-node consolidation."""
+    import e2e_cases
+    sim = _e2e(ctx, golden, e2e_cases.multi_delete, n_nodes=200)
+    assert sim.commands[0].mode == abi.KP_CONSOLIDATE_MULTI and len(sim.nodes) == 40
