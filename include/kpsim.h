@@ -492,6 +492,11 @@ typedef struct kp_launch_result {
     int32_t override_offset;                 /* into override_offerings */
     int32_t n_options;                       /* types left by the filter chain, before Truncate */
     int32_t rejected[KP_N_FILTERS];          /* types each filter rejected */
+    int32_t fleet_pick;                      /* the override offering row a lowest-price CreateFleet launches (SURVEY §8f
+                                                row 4, the kwok fake EC2: kwok/ec2/ec2.go:432-461 lo.MinBy over the
+                                                overrides in order, scored by kwok/strategy/strategy.go:45-60 — the spot
+                                                price of (type, zone) for a spot launch, else the type's on-demand price;
+                                                a missing price scores MaxFloat64, a zero score never wins); -1 on error */
 } kp_launch_result;
 
 /* Evaluates n requests on the ctx's device.  type_ids / override_offerings receive the concatenated lists

@@ -3563,13 +3563,35 @@ extern "C" kp_status kp_launch_select(kp_ctx* ctx, int32_t n, const kp_launch_re
                 r.override_offset = (int32_t)ooff[i];
                 r.n_overrides = (int32_t)(ooff[i + 1] - ooff[i]);
                 int64_t tp = toff[i], op = ooff[i];
+                // kwok CreateFleet's lowest-price pick (kpsim.h kp_launch_result.fleet_pick): lo.MinBy over the overrides
+                // in order; score = the spot price of (type, zone) for a spot fleet, else the type's on-demand price
+                const bool spot = r.capacity_type == KP_CT_SPOT;
+                int32_t pick = -1;
+                double best = 0.0;
                 for (int k = 0; k < r.n_types; k++, tp++) {
                     const int32_t t = tys[(size_t)i * M + k];
                     if (type_ids && tp < cap_type_ids) type_ids[tp] = t;
                     // override offerings of slot k: bit j = offering row off_begin[t] + j, ascending
-                    for (uint64_t m = ov[(size_t)i * M + k]; m; m &= m - 1, op++)
-                        if (override_offerings && op < cap_overrides) override_offerings[op] = c->l_off_begin[t] + __builtin_ctzll(m);
+                    for (uint64_t m = ov[(size_t)i * M + k]; m; m &= m - 1, op++) {
+                        const int32_t row = c->l_off_begin[t] + __builtin_ctzll(m);
+                        if (override_offerings && op < cap_overrides) override_offerings[op] = row;
+                        double sc = DBL_MAX;
+                        const int nO = (int)c->l_ct.size();
+                        for (int f = c->l_off_begin[t]; f < c->l_off_begin[t + 1]; f++) {
+                            if (spot ? (c->l_ct[f] == KP_CT_SPOT &&
+                                        c->l_off_val[(size_t)KL_ROLE_ZONE * nO + f] == c->l_off_val[(size_t)KL_ROLE_ZONE * nO + row])
+                                     : c->l_ct[f] == KP_CT_ON_DEMAND) {
+                                sc = c->l_price[f];
+                                break;
+                            }
+                        }
+                        if (pick < 0 || best == 0.0 || (sc != 0.0 && sc < best)) {
+                            pick = row;
+                            best = sc;
+                        }
+                    }
                 }
+                r.fleet_pick = r.status == KP_OK ? pick : -1;
             }
         });
         ms_exp += ms_between(tx, clk::now());

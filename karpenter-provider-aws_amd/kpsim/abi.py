@@ -179,12 +179,14 @@ class kp_launch_request(C.Structure):
 class kp_launch_result(C.Structure):
     _fields_ = [("status", C.c_int32), ("failed_filter", C.c_int32), ("capacity_type", C.c_int32),
                 ("n_types", C.c_int32), ("type_offset", C.c_int32), ("n_overrides", C.c_int32),
-                ("override_offset", C.c_int32), ("n_options", C.c_int32), ("rejected", C.c_int32 * KP_N_FILTERS)]
+                ("override_offset", C.c_int32), ("n_options", C.c_int32), ("rejected", C.c_int32 * KP_N_FILTERS),
+                ("fleet_pick", C.c_int32)]
 
 
 LAUNCH_DTYPE = np.dtype([("status", np.int32), ("failed_filter", np.int32), ("capacity_type", np.int32),
                          ("n_types", np.int32), ("type_offset", np.int32), ("n_overrides", np.int32),
-                         ("override_offset", np.int32), ("n_options", np.int32), ("rejected", np.int32, KP_N_FILTERS)])
+                         ("override_offset", np.int32), ("n_options", np.int32), ("rejected", np.int32, KP_N_FILTERS),
+                         ("fleet_pick", np.int32)])
 assert LAUNCH_DTYPE.itemsize == C.sizeof(kp_launch_result)
 
 

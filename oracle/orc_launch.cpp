@@ -369,6 +369,21 @@ extern "C" kp_status orc_launch_select(const kp_catalog_view* cat, int32_t n, co
             }
         }
         res.capacity_type = ct;
+        // kwok CreateFleet (kwok/ec2/ec2.go:432-461, kwok/strategy/strategy.go:45-60): lo.MinBy over the overrides in
+        // order, score = SpotPrice(type, zone) for a spot fleet else OnDemandPrice(type), MaxFloat64 without a price;
+        // MinBy's comparison holds when the running minimum's score is 0 (lo.IsEmpty) or item < minimum with item != 0
+        res.fleet_pick = -1;
+        double best_score = 0;
+        auto fleet_score = [&](const Off& o, const IT& it) {
+            for (auto& f : it.offs) {
+                if (ct == KP_CT_SPOT) {
+                    if (X.ct(f) == "spot" && X.zone(f) == X.zone(o)) return f.price;
+                } else if (X.ct(f) == "on-demand") {
+                    return f.price;
+                }
+            }
+            return DBL_MAX;
+        };
         Reqs r3 = reqs;
         r3.m[X.kct] = new_req(D, X.kct, OP_IN, {names[ct]}, false, 0);
         res.n_types = (int)key.size();
@@ -377,6 +392,11 @@ extern "C" kp_status orc_launch_select(const kp_catalog_view* cat, int32_t n, co
             else short_buf = true;
             tpos++;
             for (auto* o : X.avail_compat(its[k.second].offs, r3)) {
+                const double sc = fleet_score(*o, *its[k.second].it);
+                if (res.fleet_pick < 0 || best_score == 0.0 || (sc != 0.0 && sc < best_score)) {
+                    res.fleet_pick = o->row;
+                    best_score = sc;
+                }
                 if (override_offerings && opos < cap_overrides) override_offerings[opos] = o->row;
                 else short_buf = true;
                 opos++;

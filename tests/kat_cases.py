@@ -583,6 +583,97 @@ def min_values_multiple_keys(fx):
                launch_check)
 
 
+# ----------------------------------------------------------------------------------------------------------------------
+# test/suites/scheduling/suite_test.go — provisioning end to end (Solve → CreateFleet overrides → kwok's lowest-price
+# override pick), over the golden catalog (test-zone-1a/1b/1c = zone ids use1-az1 / use1-az2 / use1-az4)
+# ----------------------------------------------------------------------------------------------------------------------
+def _env_default_pool(*replace):
+    """env.DefaultNodePool (test/pkg/environment/common/environment.go:133-177) + test.ReplaceRequirements."""
+    reqs = [Requirement("kubernetes.io/os", "In", ["linux"]), Requirement(CAPACITY_TYPE, "In", ["on-demand"]),
+            Requirement(AWS + "instance-category", "In", ["c", "m", "r"]),
+            Requirement(AWS + "instance-generation", "Gt", ["4"]), Requirement(AWS + "instance-family", "NotIn", ["a1"])]
+    keys = {r.key for r in replace}
+    return model.NodePool("default", requirements=[r for r in reqs if r.key not in keys] + list(replace))
+
+
+def picked(cat, lres, i):
+    """(type name, offering) of kwok CreateFleet's pick for launch row i."""
+    row = int(lres.rows[i]["fleet_pick"])  # kp_launch_result.fleet_pick (device) / its oracle restatement
+    t, o = flat_offerings(cat)[row]
+    return cat[t].name, o
+
+
+@case
+def e2e_nodepool_weight(fx):
+    """A pod against NodePools of weight 10 (instance-type In [t3.nano]) and 100 (In [c5.large]): one node, a c5.large
+    from the high-priority pool."""
+    cat = catalog.golden_catalog(fx=fx)
+    low = model.NodePool("low", weight=10, requirements=[Requirement("kubernetes.io/os", "In", ["linux"]),
+                                                         Requirement(INSTANCE_TYPE, "In", ["t3.nano"])])
+    high = model.NodePool("high", weight=100, requirements=[Requirement("kubernetes.io/os", "In", ["linux"]),
+                                                            Requirement(INSTANCE_TYPE, "In", ["c5.large"])])
+    prob = problem(cat, [low, high], [PodClass()], [(0, {})])
+
+    def check(prob, res, reqs):
+        assert res.n_nodeclaims == 1 and (res.pod_result == 0).all()
+        assert prob.nodepools[int(res.nodeclaim_nodepool[0])].name == "high"
+
+    def launch_check(cat, lreqs, lres):
+        assert picked(cat, lres, 0)[0] == "c5.large"
+    return Kat("e2e_nodepool_weight", "test/suites/scheduling/suite_test.go:471-538", prob, check, launch_check)
+
+
+@case
+def e2e_flex_node(fx):
+    """env.DefaultNodePool with instance-capacity-flex In [true]: the pod's node is a flex instance type."""
+    cat = catalog.golden_catalog(fx=fx)
+    prob = problem(cat, [_env_default_pool(Requirement(AWS + "instance-capacity-flex", "In", ["true"]))], [PodClass()],
+                   [(0, {})])
+
+    def launch_check(cat, lreqs, lres):
+        assert "flex" in picked(cat, lres, 0)[0]
+    return Kat("e2e_flex_node", "test/suites/scheduling/suite_test.go:539-553", prob, _all_scheduled, launch_check)
+
+
+@case
+def e2e_zone_and_zone_id_overlap(fx):
+    """zone In [1a, 1b] and zone-id In [az2, az4]: only test-zone-1b / use1-az2 satisfies both — the node lands
+    there (offering-level joint compatibility, not per-label)."""
+    cat = catalog.golden_catalog(fx=fx)
+    cls = PodClass(requirements=[Requirement(ZONE, "In", ["test-zone-1a", "test-zone-1b"]),
+                                 Requirement(model.ZONE_ID, "In", ["use1-az2", "use1-az4"])])
+    prob = problem(cat, [_env_default_pool()], [cls], [(0, {})])
+
+    def launch_check(cat, lreqs, lres):
+        _, o = picked(cat, lres, 0)
+        assert (o.zone, o.zone_id) == ("test-zone-1b", "use1-az2")
+        assert {(z, c) for _, z, c, _ in overrides(cat, lres, 0)} == {("test-zone-1b", "on-demand")}
+    return Kat("e2e_zone_and_zone_id_overlap", "test/suites/scheduling/suite_test.go:692-718", prob, _all_scheduled,
+               launch_check)
+
+
+@case
+def e2e_zone_id_correct_zone(fx):
+    """A NodePool requiring expected-zone-label Exists; one pod per zone with expected-zone-label In [zone] and
+    zone-id In [that zone's id]: three nodes, each in the zone its label names."""
+    cat = catalog.golden_catalog(fx=fx)
+    zid = {"test-zone-1a": "use1-az1", "test-zone-1b": "use1-az2", "test-zone-1c": "use1-az4"}
+    classes = [PodClass(requirements=[Requirement("expected-zone-label", "In", [z]),
+                                      Requirement(model.ZONE_ID, "In", [zid[z]])]) for z in sorted(zid)]
+    prob = problem(cat, [_env_default_pool(Requirement("expected-zone-label", "Exists"))], classes,
+                   [(i, {}) for i in range(3)])
+
+    def check(prob, res, reqs):
+        assert res.n_nodeclaims == 3 and (res.pod_result >= 0).all()
+
+    def launch_check(cat, lreqs, lres):
+        for i, lr in enumerate(lreqs):
+            want = next(r.values[0] for r in lr.requirements if r.key == "expected-zone-label")
+            _, o = picked(cat, lres, i)
+            assert (o.zone, o.zone_id) == (want, zid[want])
+    return Kat("e2e_zone_id_correct_zone", "test/suites/scheduling/suite_test.go:719-768", prob, check, launch_check)
+
+
 def build(fx, mk):
     return mk(fx)
 

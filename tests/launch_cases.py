@@ -342,3 +342,4 @@ def assert_same(a, b):
             assert int(ra["capacity_type"]) == int(rb["capacity_type"]), (i, ra, rb)
             assert list(a.types(i)) == list(b.types(i)), i
             assert list(a.offerings(i)) == list(b.offerings(i)), i
+            assert int(ra["fleet_pick"]) == int(rb["fleet_pick"]), (i, ra, rb)

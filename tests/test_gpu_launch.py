@@ -43,6 +43,11 @@ def test_config5_batch_parity(ctx, golden, seed):
     dev, orc = _both(ctx, cat, reqs)
     LC.assert_same(dev, orc)
     assert (dev.rows["capacity_type"] == abi.KP_CT_RESERVED).sum() > 0
+    # fleet emulation folded into the launch result: kwok's CreateFleet pick per request
+    from kpsim import launch
+    for i in range(len(reqs)):
+        want = launch.fleet_pick(cat, dev, i)
+        assert int(dev.rows[i]["fleet_pick"]) == (want[1] if want else -1), i
     assert (dev.rows["status"] == abi.KP_E_INSUFFICIENT_CAPACITY).sum() > 0
 
 

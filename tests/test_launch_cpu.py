@@ -118,6 +118,8 @@ def test_fleet_pick_config5(golden):
         k = rows.index(row)
         assert scores[k] == min(scores)
         assert all(s != scores[k] for s in scores[:k])
+        # the oracle's restatement inside orc_launch_select (kp_launch_result.fleet_pick) agrees
+        assert int(res.rows[i]["fleet_pick"]) == row
     assert n_ok > 0
 
 
