@@ -23,6 +23,12 @@ import numpy as np  # noqa: E402
 
 T_START = time.perf_counter()
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+# ctx.ffd_cycles(): FFD kernel counters (the cyc_* stage cycles only under KPSIM_PROFILE=1)
+FFD_COUNTERS = ["cyc_fast_loop", "cyc_sort", "cyc_slow_eval", "cyc_templates", "-", "cyc_sort_full", "ev_req", "ev_mask",
+                "ev_off", "ev_types", "ev_min", "ev_calls", "quick_accepts", "slow_pods", "witness_misses", "cyc_q_pop",
+                "cyc_q_scan", "cyc_q_check", "cyc_q_commit", "n_noinv", "n_winmove", "n_ldssort", "n_pivot", "n_winload",
+                "n_flush", "n_shape", "n_lds_append", "n_lds_nowin", "n_lds_outside", "n_batches", "topo_quick",
+                "cyc_topo_setup", "cyc_topo_scan"]
 
 
 def log(msg):
@@ -49,20 +55,24 @@ def consolidation_bytes(cst, A, R=12):
     """Algorithmic bytes of the probe kernel: every existing-node slot examined reads its headroom on
     the A active axes and one compatibility bit; every pod popped reads its requests, class and shape (S_pod); every
     NodeClaim / template evaluation reads one NodeClaim row (S_nc = ceil(T/8) + 8R + 64, T = 918); the queue
-    bitmap scan reads and clears 8 B per word."""
+    bitmap scan reads and clears 8 B per word; a chunk the headroom summary rules out costs its summary row and one
+    compatibility word (8A + 8 B) instead of its 64 node slots."""
     s_nc = (918 + 7) // 8 + 8 * R + 64
     s_pod = 8 * R + 64
-    return (cst[1] * (8 * A + 1 / 8) + cst[0] * s_pod + (cst[2] + cst[3]) * s_nc + cst[5] * 16)
+    return (cst[1] * (8 * A + 1 / 8) + cst[0] * s_pod + (cst[2] + cst[3]) * s_nc + cst[5] * 16 + cst[15] * (8 * A + 8))
 
 
-def consolidation_leg(a, cat, local, rank, world, dist, barrier):
+def consolidation_leg(a, cat, local, rank, world, dist, barrier, headroom=None):
     """BASELINE configs[3]: single-node consolidation over every candidate of a 5k-node / ~100k-pod cluster plus the
-    multi-node prefix probes (first 100 by disruption cost).  With N GPUs the library shards the probes itself: rank 0
+    multi-node prefix probes (first 100 by disruption cost).  headroom=None: nodes at 40-60% utilisation (the probes'
+    pods all fit the other nodes: DELETE decisions, existing-node first-fit only); headroom=0.02: every node's free
+    cpu / memory capped at 2% of allocatable, so the probes scan the whole cluster, run NodeClaim.Add and the templates
+    and mostly decide REPLACE (the "config4-replace" leg: the NodeClaim path timed at scale).  With N GPUs the library shards the probes itself: rank 0
     opens one multi-device ctx over devices 0..N-1 (kp_device_opts.devices), which evaluates one
     contiguous probe shard per device on its own host thread and gathers the results in-process; the other ranks only
     join the barriers.  The decision (kpsim.consolidation.compute_command) replays over the gathered vector."""
     from kpsim import abi, consolidation, model, native, synth
-    cp = synth.config4(n_nodes=a.nodes, catalog=cat)
+    cp = synth.config4(n_nodes=a.nodes, catalog=cat, headroom=headroom)
     n_s = model.consolidation_probe_count(len(cp.candidates), abi.KP_CONSOLIDATE_SINGLE)
     n_m = model.consolidation_probe_count(len(cp.candidates), abi.KP_CONSOLIDATE_MULTI)
     ctx = None
@@ -82,7 +92,7 @@ def consolidation_leg(a, cat, local, rank, world, dist, barrier):
         fn = lambda c, mode, b0, b1: part[mode]  # noqa: E731 (whole ranges: distributed=False)
         cs = consolidation.compute_command(cp, abi.KP_CONSOLIDATE_SINGLE, fn, distributed=False)
         cm = consolidation.compute_command(cp, abi.KP_CONSOLIDATE_MULTI, fn, distributed=False)
-        return cs, cm, st
+        return cs, cm, st, res
 
     if rank == 0:
         for _ in range(max(1, a.warmup)):
@@ -93,7 +103,7 @@ def consolidation_leg(a, cat, local, rank, world, dist, barrier):
     cs = cm = None
     if rank == 0:
         for _ in range(a.steps):
-            cs, cm, st = step()
+            cs, cm, st, res = step()
             kms.append([st[0][0], st[0][1]])
             kcs.append(np.array(st[1]))
     elapsed = time.perf_counter() - t0
@@ -118,15 +128,19 @@ def consolidation_leg(a, cat, local, rank, world, dist, barrier):
         "n_gpus": world,
         "ms_per_step": elapsed / a.steps * 1e3,
         "scaling": "strong",
-        "config": {"workload": "config4: %d existing nodes, %d bound pods (config2 classes), single-node probes over "
-                               "all %d candidates + %d multi-node prefix probes" % (len(cp.cluster.existing),
-                                                                                    cp.cluster.pods.n, n_s, n_m),
+        "config": {"workload": "config4%s: %d existing nodes, %d bound pods (config2 classes), single-node probes over "
+                               "all %d candidates + %d multi-node prefix probes" % (
+                                   "" if headroom is None else "-replace (node headroom %g)" % headroom,
+                                   len(cp.cluster.existing), cp.cluster.pods.n, n_s, n_m),
                    "parallelism": "probe shards x%d (one multi-device ctx, in-library gather)" % world},
         "decisions": {"single": [cs.decision, cs.candidates[:1]], "multi": [cm.decision, len(cm.candidates)]},
+        "probe_decisions": {"none": int((res["decision"] == abi.KP_DECISION_NONE).sum()),
+                            "delete": int((res["decision"] == abi.KP_DECISION_DELETE).sum()),
+                            "replace": int((res["decision"] == abi.KP_DECISION_REPLACE).sum())},
         "kernel_ms_rank0": {"prep": km[0], "probes": km[1]},
         "counters_per_step": dict(zip(["pods_popped", "existing_slots", "nodeclaim_evals", "template_evals", "probes",
                                        "bitmap_words", "placed_existing", "new_nodeclaims", "chunk_loads", "chunk_hits",
-                                       "cyc_build", "cyc_scan", "cyc_nodeclaim", "cyc_decide", "cyc_total"],
+                                       "cyc_build", "cyc_scan", "cyc_nodeclaim", "cyc_decide", "cyc_total", "chunk_skips"],
                                       [int(x) for x in cst])),
         "roofline": {"bound": "hbm", "kernel": "consolidate_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes": int(B),
@@ -309,6 +323,7 @@ def solve_leg(a, cat, prob, metric, workload, cpu_sample, local, rank, world, di
         "roofline": {"bound": "hbm", "kernel": "ffd_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes": int(B), "kernel_ms": float(kt[3])},
         "solve_stats": {k: v for k, v in res.stats.items() if not k.startswith("ns_")},
+        "ffd_counters": dict(zip(FFD_COUNTERS, ctx.ffd_cycles())),
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -363,6 +378,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=0, help="pods in the CPU-baseline sample (0 = the full workload)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-consolidation", action="store_true")
+    ap.add_argument("--no-consolidation-replace", action="store_true")
     ap.add_argument("--nodes", type=int, default=5000, help="config4 cluster size (consolidation leg)")
     ap.add_argument("--launch-batch", type=int, default=10_000, help="config5 launch batch (NodeClaims)")
     ap.add_argument("--no-launch", action="store_true")
@@ -448,6 +464,9 @@ def main():
     log("config2 solve leg done: %.1f ms/step" % (elapsed / a.steps * 1e3))
     cons = None if a.no_consolidation else consolidation_leg(a, cat, local, rank, world, dist, barrier)
     log("consolidation leg done")
+    cons_r = None if (a.no_consolidation or a.no_consolidation_replace) else consolidation_leg(
+        a, cat, local, rank, world, dist, barrier, headroom=0.02)
+    log("consolidation replace leg done")
     launch = None if a.no_launch else launch_leg(a, cat, local, rank, world, dist, barrier)
     log("launch leg done")
     topo = None if a.no_topology else topology_leg(a, cat, local, rank, world, dist, barrier)
@@ -504,15 +523,12 @@ def main():
                           "ffd": float(kt[3]), "finalize": float(kt[4])},
             "end_to_end_ms": e2e_ms,
             "solve_call_warm": solve_call,
-            "ffd_counters": dict(zip(["cyc_fast_loop", "cyc_sort", "cyc_slow_eval", "cyc_templates", "-",
-                                      "cyc_sort_full", "ev_req", "ev_mask", "ev_off", "ev_types", "ev_min", "ev_calls",
-                                      "quick_accepts", "slow_pods", "witness_misses", "cyc_q_pop", "cyc_q_scan",
-                                      "cyc_q_check", "cyc_q_commit", "n_noinv", "n_winmove", "n_ldssort", "n_pivot",
-                                      "n_winload", "n_flush", "n_shape", "n_lds_append", "n_lds_nowin", "n_lds_outside", "n_batches"], cyc)),
+            "ffd_counters": dict(zip(FFD_COUNTERS, cyc)),
             "nodeclaims": res.n_nodeclaims,
             "unschedulable": int((res.pod_result == -1).sum()),
             "solve_stats": {k: v for k, v in res.stats.items() if not k.startswith("ns_")},
             "consolidation": cons,
+            "consolidation_replace": cons_r,
             "launch": launch,
             "topology": topo,
             "reserved": resv,

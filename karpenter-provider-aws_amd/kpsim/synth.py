@@ -249,14 +249,18 @@ def _selector_ok(req: Requirement, labels):
 
 
 def config4(n_nodes=5000, pods_per_node=(10, 30), n_classes=250, catalog=None, seed=SEED, n_pending=0,
-            util=(0.4, 0.6)) -> ConsolidationProblem:
+            util=(0.4, 0.6), headroom=None) -> ConsolidationProblem:
     """5k existing nodes with ~100k bound pods of config-2 classes at 40-60% utilisation (BASELINE configs[3]).
 
     Each node: a NodePool (80% default spot/on-demand, 20% the tainted on-demand pool), a zone, a capacity type, then
     the smallest catalog type (non-GPU, with an offering in that zone / capacity type) whose cpu and memory put the
     node's pods at the drawn utilisation; its pods are drawn from the classes the node satisfies (selectors,
     tolerations).  available = allocatable - bound pod requests.  Candidates = every node in disruption-cost order
-    (fewer pods first, then name); multi-node consolidation takes the first 100.  All nodes initialized."""
+    (fewer pods first, then name); multi-node consolidation takes the first 100.  All nodes initialized.
+
+    headroom = f caps each node's available cpu and memory at f x allocatable (capacity held by pods that are not
+    rescheduled, e.g. DaemonSets): with a small f the candidates' pods no longer fit the other nodes and the probes run
+    NodeClaim.Add and the templates (REPLACE decisions; the "config4-replace" bench leg)."""
     rng = np.random.Generator(np.random.PCG64(seed + 4))
     catalog = catalog if catalog is not None else golden_catalog(seed=seed)
     taint_key = "example.com/dedicated"
@@ -313,6 +317,9 @@ def config4(n_nodes=5000, pods_per_node=(10, 30), n_classes=250, catalog=None, s
                 cls[q] = int(rng.choice(ok, p=okw))
         used = creq_vec[cls].sum(axis=0)
         avail = np.array(it.allocatable, np.int64) - used
+        if headroom is not None:
+            for r in (RIDX["cpu"], RIDX["memory"]):
+                avail[r] = min(avail[r], int(it.allocatable[r] * headroom))
         name = "node-%05d" % j
         nodes.append(ExistingNode(name=name, labels=labels, available=avail, requests=np.zeros(R, np.int64),
                                   taints=list(pool.taints)))

@@ -98,6 +98,18 @@ def test_config4_full_size_properties(ctx, golden):
     assert_probes_equal(multi, pyoracle.consolidate(cp, abi.KP_CONSOLIDATE_MULTI, n_threads=8))
 
 
+@pytest.mark.parametrize("n_nodes", [600, 5000])
+def test_config4_replace_parity(ctx, golden, n_nodes):
+    """config4 with 2% node headroom (synth.config4(headroom=0.02), the bench's replace leg): the candidates' pods mostly
+    miss the other nodes, so the probes scan the whole cluster, then run NodeClaim.Add / the templates and produce
+    REPLACE decisions.  Every probe of both modes against the oracle, and the mix of decisions the leg exists for."""
+    cp = synth.config4(n_nodes=n_nodes, catalog=golden, headroom=0.02)
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        dev = device_probes(ctx, cp, mode)
+        assert_probes_equal(dev, pyoracle.consolidate(cp, mode, n_threads=8))
+        assert (dev["decision"] == abi.KP_DECISION_REPLACE).sum() > len(dev) // 3
+
+
 @pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
 def test_multi_device_ctx(golden, devices):
     """kp_device_opts.devices: one ctx over several device streams (the same ordinal repeated on a
