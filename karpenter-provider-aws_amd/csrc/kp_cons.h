@@ -12,9 +12,10 @@
 
 enum { CS_POPS = 0, CS_EX_NODES, CS_NC_EVALS, CS_TMPL_EVALS, CS_PROBES, CS_BITMAP_WORDS, CS_PLACED_EXISTING,
        CS_NEW_NC, CS_CHUNK_LOADS, CS_CACHE_HITS, CS_CYC_BUILD, CS_CYC_SCAN, CS_CYC_NODECLAIM, CS_CYC_DECIDE,
-       CS_CYC_TOTAL, CS_COUNT = 16 };
+       CS_CYC_TOTAL, CS_CHUNK_SKIPS, CS_COUNT = 16 };
 
 #define KP_CONS_XTC 1024  // pod classes whose XT column of the cached node chunk is kept in LDS
+#define KP_CONS_STORE 8   // node chunks the fast probe variant keeps in its LDS headroom store
 
 struct KpCons {
     int32_t n_probes;           // probes of this call (out[0 .. n_probes))
@@ -67,8 +68,17 @@ struct KpCons {
     const int32_t* dec_moff;
     const int32_t* dec_g;       // [rows] group of the row
     const int32_t* dec_v;       // [rows][64]
+    // chunk headroom summary: cmax0[w][ai] = the largest headroom on active axis ai over the nodes of 64-node chunk w
+    // (kp_launch_cons_chunk_max, after the existing-node tables); each probe copies it to LDS and lowers a chunk's entry
+    // to its true maximum whenever it has the chunk's headroom in hand, so the entries stay upper bounds and a pod whose
+    // request exceeds one on some axis skips the chunk without loading it (use_cmax: the LDS plan has room)
+    const int64_t* cmax0;       // [EW][KP_LDS_AXES]
+    int32_t use_cmax;
     int32_t profile;            // s_memtime stage cycles (KPSIM_PROFILE)
+    int64_t* prof_probe;        // KPSIM_PROFILE: [n_probes][4] cycles of build, existing-node placement, total; pods
     int32_t no_fast;            // diagnostics: every probe on the FULL variant (KPSIM_CONS_NOFAST)
     // dynamic LDS plan (kp_cons_plan_lds)
-    int32_t off_hdr, off_words, off_rem, off_excl, off_mod, off_init, off_xtc, off_touch, off_hmod, lds_bytes;
+    int32_t n_store;            // chunks in the fast variant's LDS headroom store (kp_cons_plan_lds)
+    int32_t off_hdr, off_words, off_rem, off_excl, off_mod, off_init, off_xtc, off_touch, off_hmod, off_cmax, off_hs;
+    int32_t lds_bytes;
 };

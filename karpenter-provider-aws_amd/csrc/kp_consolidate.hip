@@ -178,6 +178,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
     uint64_t* modb = reinterpret_cast<uint64_t*>(smem + k.off_mod);
     uint64_t* initb = reinterpret_cast<uint64_t*>(smem + k.off_init);
     uint64_t* xtc = reinterpret_cast<uint64_t*>(smem + k.off_xtc);  // XT column of the cached chunk, by class
+    int64_t* cmax = reinterpret_cast<int64_t*>(smem + k.off_cmax);  // [EW][KP_LDS_AXES] chunk headroom upper bounds
     const int lane = threadIdx.x;
     ProbeTopo P{};
     if (TOPO) {
@@ -253,6 +254,8 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
         const int gp = single ? (k.mode == KP_CONSOLIDATE_BOTH ? k.sprobe0 + probe - nmul : k.probe0 + probe) : k.probe0 + oi;
         const int c0 = single ? gp : 0, c1 = single ? gp + 1 : gp + 2;
         int64_t st_pops = 0, st_nodes = 0, st_nc = 0, st_tmpl = 0, st_words = 0, st_placed = 0, st_loads = 0, st_hits = 0;
+        int64_t st_skips = 0;
+        long long pf_load = 0, pf_prep = 0, pf_nodes = 0, pf_visits = 0;  // KPSIM_PROFILE: fast-path stages
         long long cy_build = 0, cy_scan = 0, cy_nc = 0, cy_dec = 0;
         const bool prof = k.profile != 0;
         const long long cy0 = prof ? __builtin_amdgcn_s_memtime() : 0;
@@ -263,6 +266,8 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             modb[w] = 0;
         }
         for (int i = lane; i < NT * R; i += 64) rem[i] = d.remaining[i];
+        if (k.use_cmax)
+            for (int i = lane; i < EW * KP_LDS_AXES; i += 64) cmax[i] = k.cmax0[i];
         if (RESV) S.rcap[lane] = d.rcap0[lane];
         __syncthreads();
         for (int c = c0 + lane; c < c1; c += 64) {
@@ -278,30 +283,34 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             const int r0 = single ? k.dec_soff[gp] : k.dec_moff[gp], r1 = single ? k.dec_soff[gp + 1] : k.dec_moff[gp + 1];
             for (int r = r0; r < r1; r++) pt_init_row(d, P, k.dec_g[r], k.dec_v + (size_t)r * 64, lane);
         }
+        // the probe's candidates are [c0, c1) and their pods one contiguous run of cand_pods (CSR in candidate order)
+        const int po0 = k.cand_off[c0], po1 = k.cand_off[c1];
+        const int n_np = po1 - po0;
+        // getCandidatePrices (Σ in candidate order, as Go adds them), the all-spot test, and the candidates' capacity
+        // back into their NodePools' remaining limits; candidates 64 at a time, one per lane, so the probe pays one load
+        // latency per 64 candidates, not one per candidate
         double cprice = 0.0;
         bool all_spot = true;
-        int n_np = 0;
-        for (int c = c0; c < c1; c++) {  // getCandidatePrices: Σ in candidate order
-            cprice += k.cand_price[c];
-            all_spot &= k.cand_i[c * 4 + 1] == KP_CT_SPOT;
-            n_np += k.cand_off[c + 1] - k.cand_off[c];
-            const int j = k.cand_i[c * 4 + 3];
-            if (j >= 0 && lane < R && d.limit_set[(size_t)j * R + lane])
-                rem[j * R + lane] += k.cand_cap[(size_t)c * R + lane];
+        for (int cb = c0; cb < c1; cb += 64) {
+            const int c = cb + lane;
+            const bool v = c < c1;
+            const double pr = v ? k.cand_price[c] : 0.0;
+            const int4 cit = v ? reinterpret_cast<const int4*>(k.cand_i)[c] : make_int4(0, KP_CT_SPOT, 0, -1);
+            if (ballot(cit.y != KP_CT_SPOT)) all_spot = false;
+            const int nv = c1 - cb < 64 ? c1 - cb : 64;
+            const uint32_t plo = (uint32_t)__double2loint(pr), phi = (uint32_t)__double2hiint(pr);
+            for (int i = 0; i < nv; i++)
+                cprice += __hiloint2double(__builtin_amdgcn_readlane((int)phi, i), __builtin_amdgcn_readlane((int)plo, i));
+            if (cit.w >= 0)
+                for (int r = 0; r < R; r++)
+                    if (d.limit_set[(size_t)cit.w * R + r])
+                        atomicAdd((unsigned long long*)&rem[cit.w * R + r], (unsigned long long)k.cand_cap[(size_t)c * R + r]);
         }
         // ---- the probe's pods in queue order ----
         int n = 0;
         if (k.n_pending == 0 && n_np <= 64) {
             // at most one pod per lane: bitonic sort of (queue position, pod) across the wave
-            int myp = -1;
-            {
-                int i = lane;
-                for (int c = c0; c < c1 && myp < 0; c++) {
-                    const int cnt = k.cand_off[c + 1] - k.cand_off[c];
-                    if (i < cnt) myp = k.cand_pods[k.cand_off[c] + i];
-                    else i -= cnt;
-                }
-            }
+            const int myp = lane < n_np ? k.cand_pods[po0 + lane] : -1;
             uint64_t key = myp >= 0 ? ((uint64_t)(uint32_t)k.rank[myp] << 32) | (uint32_t)myp : ~0ull;
             for (int kk = 2; kk <= 64; kk <<= 1)
                 for (int j = kk >> 1; j > 0; j >>= 1) {
@@ -317,31 +326,32 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             }
             n = n_np;
         } else {
-        // mark queue positions, then scan the bitmap with the pending pods
-        for (int c = c0; c < c1; c++) {
-            const int o0 = k.cand_off[c], o1 = k.cand_off[c + 1];
-            for (int i = o0 + lane; i < o1; i += 64) {
-                const int r = k.rank[k.cand_pods[i]];
-                __hip_atomic_fetch_or(&pbits[r >> 6], 1ull << (r & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+        // mark queue positions, then scan the bitmap with the pending pods (the next 64 words' loads issued before the
+        // current ones are expanded)
+        for (int i = po0 + lane; i < po1; i += 64) {
+            const int r = k.rank[k.cand_pods[i]];
+            __hip_atomic_fetch_or(&pbits[r >> 6], 1ull << (r & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        uint64_t nmine = 0, npend = 0;
+        if (lane < k.PW) {
+            nmine = ld64u(&pbits[lane]);
+            npend = k.n_pending ? k.pend_bits[lane] : 0ull;
+        }
         for (int wb = 0; wb < k.PW; wb += 64) {
             const int w = wb + lane;
-            uint64_t mine = 0, pend = 0;
-            if (w < k.PW) {
-                mine = ld64u(&pbits[w]);
-                pend = k.pend_bits[w];
+            const uint64_t mine = nmine, pend = npend;
+            nmine = npend = 0;
+            if (w + 64 < k.PW) {
+                nmine = ld64u(&pbits[w + 64]);
+                npend = k.n_pending ? k.pend_bits[w + 64] : 0ull;
             }
             uint64_t x = mine | pend;
+            if (!ballot(x != 0)) continue;
             const int cnt = __popcll(x);
-            int v = cnt;
-            for (int o = 1; o < 64; o <<= 1) {
-                const int y = __shfl_up(v, o);
-                if (lane >= o) v += y;
-            }
-            const int total = __shfl(v, 63);
+            const int v = (int)wave_scan_add32((uint32_t)cnt);
+            const int total = __builtin_amdgcn_readlane(v, 63);
             int pos = n + v - cnt;
             while (x) {
                 const int b = __ffsll((unsigned long long)x) - 1;
@@ -398,6 +408,326 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
         bool bad = false, stop = false;
         uint64_t nc_opts = 0;
         uint64_t nc_held = 0;  // RESV: reservation IDs the in-flight NodeClaim holds
+        // Largest headroom of the cached chunk's nodes that are not candidates (lanes past E hold 0): the chunk's entry
+        // of the headroom summary when the chunk leaves the registers.
+        auto chunk_max = [&](int base, const int64_t (&h)[KP_LDS_AXES], int ai) -> int64_t {
+            const bool in = base + lane < E && !((excl[base >> 6] >> lane) & 1ull);
+            return wave_max64(in ? h[ai] : INT64_MIN);
+        };
+        // ExistingNode.Add in scheduling order from node xs (candidates excluded) for a pod of class c requesting q on
+        // the active axes: the first node that takes it, or -1.  64-node aligned chunks; the chunk of the last placement
+        // stays in registers (effective headroom and this probe's added requests per lane) and becomes the chunk of the
+        // returned node.  Other chunks are first filtered 64 at a time (one lane per chunk) by the pod's compatible
+        // nodes and the headroom summary, so a pod that fits nowhere skips the cluster without loading it.
+        auto scan_nodes = [&](int c, const int64_t (&q)[KP_LDS_AXES], int xs, bool tcons) -> int {
+            int jf = -1;
+            uint64_t fmask = 0;
+            int fgrp = -1;
+            for (int base = __builtin_amdgcn_readfirstlane(xs & ~63); base < E; base += 64) {
+                const int w = base >> 6;
+                const int j = base + lane;
+                if (base != cbase && k.use_cmax) {
+                    if ((w >> 6) != fgrp) {
+                        fgrp = w >> 6;
+                        const int wl = (fgrp << 6) + lane;
+                        bool pc = false;
+                        if (wl < EW) {
+                            pc = (d.XT[(size_t)c * EW + wl] & ~excl[wl]) != 0;
+#pragma unroll
+                            for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                                if (ai < A) pc = pc && q[ai] <= cmax[wl * KP_LDS_AXES + ai];
+                        }
+                        fmask = ballot(pc);
+                    }
+                    if (!((fmask >> (w & 63)) & 1ull)) {  // no node of the chunk can take the pod
+                        const uint64_t rest = fmask & ~((2ull << (w & 63)) - 1ull);
+                        const int nxt = rest ? (fgrp << 6) + __ffsll((unsigned long long)rest) - 1 : (fgrp + 1) << 6;
+                        st_skips += nxt - w;
+                        base = __builtin_amdgcn_readfirstlane((nxt << 6) - 64);
+                        continue;
+                    }
+                }
+                const uint64_t ge = xs > base ? (~0ull << (xs - base)) : ~0ull;
+                uint64_t xw, mw = 0;
+                int64_t h[KP_LDS_AXES], dl[KP_LDS_AXES];
+                bool fresh = false;
+                if (base == cbase) {
+                    st_hits++;
+                    if (ccls != c) {
+                        cx = uni64((d.C <= KP_CONS_XTC) ? xtc[c] : (d.XT[(size_t)c * EW + w] & ~excl[w]));
+                        ccls = c;
+                    }
+                    xw = cx;
+#pragma unroll
+                    for (int ai = 0; ai < KP_LDS_AXES; ai++) {
+                        h[ai] = ch[ai];
+                        dl[ai] = cd[ai];
+                    }
+                } else {
+                    xw = uni64(d.XT[(size_t)c * EW + w] & ~excl[w]);
+                    if (!(xw & ge)) {
+                        st_nodes += 64;
+                        continue;
+                    }
+                    st_loads++;
+                    fresh = true;
+                    mw = uni64(modb[w]);  // not the cached chunk's word: LDS is current
+                    if (mw & xw) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this probe's delta stores landed
+                    const bool md = (mw >> lane) & 1ull;
+#pragma unroll
+                    for (int ai = 0; ai < KP_LDS_AXES; ai++) {
+                        h[ai] = 0;
+                        dl[ai] = 0;
+                        if (ai < A && j < E) {
+                            h[ai] = d.ex_head[(size_t)ai * E + j];
+                            if (md) dl[ai] = ld_req(&delta[(size_t)ai * E + j]);
+                            h[ai] -= dl[ai];
+                        }
+                    }
+                }
+                bool cand = (xw & ge) >> lane & 1ull;
+#pragma unroll
+                for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                    if (ai < A) cand &= q[ai] <= h[ai];
+                st_nodes += 64;
+                uint64_t m = ballot(cand);
+                if (TOPO && tcons) {  // ExistingNode.Add's topology step on each fitting node, in order
+                    while (m) {
+                        const int jj = __builtin_amdgcn_readfirstlane(base + __ffsll((unsigned long long)m) - 1);
+                        if (existing_topo_try<true, true>(d, S.CC, S.ws, jj, lane, &P)) break;
+                        m &= m - 1;
+                    }
+                    m = uni64(m);
+                }
+                if (m) {
+                    jf = __builtin_amdgcn_readfirstlane(base + __ffsll((unsigned long long)m) - 1);
+                    if (base != cbase) {
+                        // evict: this probe's requests on the old chunk go to the delta slab (read back past L1), its
+                        // headroom maximum to the summary
+                        if (cbase >= 0) {
+                            if (lane == 0) modb[cbase >> 6] = cmod;
+                            if (k.use_cmax)
+#pragma unroll
+                                for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                                    if (ai < A) {
+                                        const int64_t mx = chunk_max(cbase, ch, ai);
+                                        if (lane == 0) cmax[(cbase >> 6) * KP_LDS_AXES + ai] = mx;
+                                    }
+                        }
+                        if (cbase >= 0 && ((cmod >> lane) & 1ull)) {
+#pragma unroll
+                            for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                                if (ai < A)
+                                    __hip_atomic_store(&delta[(size_t)ai * E + cbase + lane], cd[ai], __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                        if (d.C <= KP_CONS_XTC)
+                            for (int cc = lane; cc < d.C; cc += 64) xtc[cc] = d.XT[(size_t)cc * EW + w] & ~excl[w];
+                        cbase = base;
+                        cx = xw;
+                        ccls = c;
+                        cmod = mw;
+                        cinit = uni64(initb[w]);
+#pragma unroll
+                        for (int ai = 0; ai < KP_LDS_AXES; ai++) {
+                            ch[ai] = h[ai];
+                            cd[ai] = dl[ai];
+                        }
+                    }
+                    break;
+                }
+                if (fresh && k.use_cmax)  // the loaded chunk cannot take the pod: its summary entry drops to its maximum
+#pragma unroll
+                    for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                        if (ai < A) {
+                            const int64_t mx = chunk_max(base, h, ai);
+                            if (lane == 0) cmax[w * KP_LDS_AXES + ai] = mx;
+                        }
+            }
+            return jf;
+        };
+        if constexpr (!FULL && !TOPO) {
+            // ---- fast variant: the probe's pods in windows of 64, one pod per lane ----
+            // Every pod here lands on an existing node or the probe goes to the FULL variant, so the queue is one pass
+            // in order and the probe is plain first fit: each pod takes the first node in scheduling order that is
+            // compatible, not a candidate, and has headroom for it.  First fit is computed node-major: node j, in order,
+            // takes from the window's pods not yet placed, in queue order, each one that still fits it (a pod that first
+            // fits node j under pod-major first fit is exactly one node j takes here: by induction over j, the pods an
+            // earlier node took before pod i are the same in both orders).  Per node the intake is greedy in queue
+            // order over the pods that fit it on their own: when there are many, one round of inclusive prefix sums
+            // takes the prefix up to the first running-total overflow, and a scalar pass over the few later pods that
+            // still fit what is left finishes it.  The first KS chunks live in an LDS store for the probe (hs: headroom
+            // per axis and node, loaded on first touch, updated in place); a pod that fits no store node takes the serial
+            // scan over the later chunks, in queue order.
+            const int KS = k.n_store;
+            const int SE = KS * 64 < E ? KS * 64 : E;  // nodes [0, SE) are in the store
+            int64_t* hs = reinterpret_cast<int64_t*>(smem + k.off_hs);  // [KS][A][64]
+            uint64_t loaded = 0;  // store chunks in LDS
+            const long long cf0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+            for (int wb = 0; wb < n && !aborted; wb += 64) {
+                const long long cw0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+                const int wn = __builtin_amdgcn_readfirstlane(n - wb < 64 ? n - wb : 64);
+                const bool live = lane < wn;
+                const int went = live ? ld32(&ring[wb + lane]) : 0;
+                const int wp = went & 0x7fffffff;
+                const bool wpend = went < 0;
+                const int wc = live ? d.pod_cls[wp] : 0;
+                int64_t wq[KP_LDS_AXES];
+#pragma unroll
+                for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                    wq[ai] = (live && ai < A) ? d.pod_req[(size_t)wp * R + d.active_axes[ai]] : 0;
+                st_pops += wn;
+                const uint64_t pendm = ballot(live && wpend);
+                if (prof) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    pf_load += __builtin_amdgcn_s_memtime() - cw0;
+                }
+                uint64_t U = ballot(live);  // pods of the window not placed yet
+                for (int w = 0; w < KS && U; w++) {
+                    const long long cc0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+                    const bool inU = (U >> lane) & 1ull;
+                    const uint64_t xw = inU ? (d.XT[(size_t)wc * EW + w] & ~excl[w]) : 0ull;  // this pod's nodes
+                    const uint64_t anyc = uni64(wave_or64(xw));
+                    if (!anyc) continue;
+                    if (!((loaded >> w) & 1ull)) {  // first touch: the chunk's headroom into the store
+                        const int j = w * 64 + lane;
+#pragma unroll
+                        for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                            if (ai < A) hs[(w * A + ai) * 64 + lane] = j < E ? d.ex_head[(size_t)ai * E + j] : -1;
+                        loaded |= 1ull << w;
+                        st_loads++;
+                    }
+                    // a node below the smallest remaining request on some axis takes none of them
+                    bool pot = (anyc >> lane) & 1ull;
+                    int64_t hl[KP_LDS_AXES];
+#pragma unroll
+                    for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                        if (ai < A) {
+                            hl[ai] = hs[(w * A + ai) * 64 + lane];
+                            const int64_t mq = (int64_t)wave_reduce64(inU ? (uint64_t)wq[ai] : (uint64_t)INT64_MAX,
+                                                                      [](uint64_t a, uint64_t b) { return (int64_t)b < (int64_t)a ? b : a; });
+                            pot = pot && hl[ai] >= mq;
+                        }
+                    st_nodes += 64;
+                    const uint64_t iw = uni64(initb[w]);
+                    uint64_t touched = 0;
+                    const long long cn0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+                    if (prof) pf_prep += cn0 - cc0;
+                    for (uint64_t m = ballot(pot); m && U; m &= m - 1) {
+                        const int jn = __ffsll((unsigned long long)m) - 1;
+                        pf_visits++;
+                        int64_t hj[KP_LDS_AXES];
+#pragma unroll
+                        for (int ai = 0; ai < KP_LDS_AXES; ai++) hj[ai] = ai < A ? (int64_t)rl64((uint64_t)hl[ai], jn) : 0;
+                        // the pods that fit the node on their own; a pod outside this set never fits it later
+                        bool e = ((U >> lane) & 1ull) && ((xw >> jn) & 1ull);
+#pragma unroll
+                        for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                            if (ai < A) e = e && wq[ai] <= hj[ai];
+                        uint64_t em = ballot(e);
+                        if (!em) continue;
+                        uint64_t took = 0;
+                        if (__popcll(em) > 4) {
+                            // many: the prefix up to the first running-total overflow is taken in one round of prefix sums
+                            bool over = false;
+                            int64_t pv[KP_LDS_AXES];
+#pragma unroll
+                            for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                                if (ai < A) {
+                                    pv[ai] = (int64_t)wave_scan_add64(e ? (uint64_t)wq[ai] : 0ull);
+                                    over = over || pv[ai] > hj[ai];
+                                }
+                            const uint64_t ov = ballot(e && over);
+                            const int fo = ov ? __ffsll((unsigned long long)ov) - 1 : 64;
+                            took = em & (fo >= 64 ? ~0ull : ((1ull << fo) - 1ull));
+                            if (took) {
+                                const int last = 63 - __clzll((long long)took);
+#pragma unroll
+                                for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                                    if (ai < A) hj[ai] -= (int64_t)rl64((uint64_t)pv[ai], last);
+                            }
+                            // the rest: the pods after the overflowing one that still fit what is left
+                            bool e2 = e && lane > fo;
+#pragma unroll
+                            for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                                if (ai < A) e2 = e2 && wq[ai] <= hj[ai];
+                            em = fo >= 64 ? 0ull : ballot(e2);
+                        }
+                        // few: greedily in queue order with scalar running totals
+                        for (; em; em &= em - 1) {
+                            const int t = __ffsll((unsigned long long)em) - 1;
+                            int64_t qt[KP_LDS_AXES];
+                            bool ok = true;
+#pragma unroll
+                            for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                                if (ai < A) {
+                                    qt[ai] = (int64_t)rl64((uint64_t)wq[ai], t);
+                                    ok = ok && qt[ai] <= hj[ai];
+                                }
+                            if (!ok) continue;
+#pragma unroll
+                            for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                                if (ai < A) hj[ai] -= qt[ai];
+                            took |= 1ull << t;
+                        }
+                        if (!took) continue;
+                        U &= ~took;
+                        touched |= 1ull << jn;
+#pragma unroll
+                        for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                            if (ai < A && lane == jn) hl[ai] = hj[ai];
+                        const int ntk = __popcll(took);
+                        st_placed += ntk;
+                        st_hits += ntk;
+                        // SimulateScheduling: a non-pending pod placed on an uninitialized node is an error
+                        const uint64_t npl = took & ~pendm;
+                        if ((iw >> jn) & 1ull) ok_np += __popcll(npl);
+                        else if (npl) bad = true;
+                    }
+                    if ((touched >> lane) & 1ull) {  // each lane writes back its own node
+#pragma unroll
+                        for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                            if (ai < A) hs[(w * A + ai) * 64 + lane] = hl[ai];
+                    }
+                    if (prof) pf_nodes += __builtin_amdgcn_s_memtime() - cn0;
+                }
+                // the pods no store node takes: the chunks after the store, serially in queue order
+                for (uint64_t m = U; m && !aborted; m &= m - 1) {
+                    const int i = __ffsll((unsigned long long)m) - 1;
+                    const int c = rl32(wc, i);
+                    const int shape = d.pod_shape[rl32(wp, i)];
+                    const bool pend = (pendm >> i) & 1ull;
+                    int64_t q[KP_LDS_AXES];
+#pragma unroll
+                    for (int ai = 0; ai < KP_LDS_AXES; ai++) q[ai] = (int64_t)rl64((uint64_t)wq[ai], i);
+                    if (shape != prev_shape) {
+                        prev_shape = shape;
+                        xstart = 0;
+                    }
+                    const int jf = SE < E ? scan_nodes(c, q, xstart > SE ? xstart : SE, false) : -1;
+                    if (jf < 0) {
+                        aborted = true;  // needs a NodeClaim: the FULL variant redoes this probe
+                        break;
+                    }
+                    if (lane == jf - cbase) {
+#pragma unroll
+                        for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                            if (ai < A) {
+                                ch[ai] -= q[ai];
+                                cd[ai] += q[ai];
+                            }
+                    }
+                    cmod |= 1ull << (jf & 63);
+                    xstart = jf;
+                    st_placed++;
+                    if (!pend) {
+                        if ((cinit >> (jf & 63)) & 1ull) ok_np++;
+                        else bad = true;
+                    }
+                }
+            }
+            if (prof) cy_scan = __builtin_amdgcn_s_memtime() - cf0;
+        } else
         while (count > 0) {
             // loop-carried wave-uniform state: re-asserted scalar each pod, so the chunk tests below branch on SGPRs
             head = __builtin_amdgcn_readfirstlane(head);
@@ -441,91 +771,8 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             }
             const bool tcons = TOPO && (cflags & CF_TOPO_CONS);
             const int xs = tcons ? 0 : xstart;
-            // ExistingNode.Add in scheduling order (candidates excluded), 64-node aligned chunks; the chunk of the last
-            // placement stays in registers (effective headroom and this probe's added requests per lane)
-            int jf = -1;
             const long long cs0 = prof ? __builtin_amdgcn_s_memtime() : 0;
-            for (int base = __builtin_amdgcn_readfirstlane(xs & ~63); base < E; base += 64) {
-                const int w = base >> 6;
-                const int j = base + lane;
-                const uint64_t ge = xs > base ? (~0ull << (xs - base)) : ~0ull;
-                uint64_t xw, mw = 0;
-                int64_t h[KP_LDS_AXES], dl[KP_LDS_AXES];
-                if (base == cbase) {
-                    st_hits++;
-                    if (ccls != c) {
-                        cx = uni64((d.C <= KP_CONS_XTC) ? xtc[c] : (d.XT[(size_t)c * EW + w] & ~excl[w]));
-                        ccls = c;
-                    }
-                    xw = cx;
-#pragma unroll
-                    for (int ai = 0; ai < KP_LDS_AXES; ai++) {
-                        h[ai] = ch[ai];
-                        dl[ai] = cd[ai];
-                    }
-                } else {
-                    xw = uni64(d.XT[(size_t)c * EW + w] & ~excl[w]);
-                    if (!(xw & ge)) {
-                        st_nodes += 64;
-                        continue;
-                    }
-                    st_loads++;
-                    mw = uni64(modb[w]);  // not the cached chunk's word: LDS is current
-                    if (mw & xw) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this probe's delta stores landed
-                    const bool md = (mw >> lane) & 1ull;
-#pragma unroll
-                    for (int ai = 0; ai < KP_LDS_AXES; ai++) {
-                        h[ai] = 0;
-                        dl[ai] = 0;
-                        if (ai < A && j < E) {
-                            h[ai] = d.ex_head[(size_t)ai * E + j];
-                            if (md) dl[ai] = ld_req(&delta[(size_t)ai * E + j]);
-                            h[ai] -= dl[ai];
-                        }
-                    }
-                }
-                bool cand = (xw & ge) >> lane & 1ull;
-#pragma unroll
-                for (int ai = 0; ai < KP_LDS_AXES; ai++)
-                    if (ai < A) cand &= q[ai] <= h[ai];
-                st_nodes += 64;
-                uint64_t m = ballot(cand);
-                if (tcons) {  // ExistingNode.Add's topology step on each fitting node, in order
-                    while (m) {
-                        const int jj = __builtin_amdgcn_readfirstlane(base + __ffsll((unsigned long long)m) - 1);
-                        if (existing_topo_try<true, true>(d, S.CC, S.ws, jj, lane, &P)) break;
-                        m &= m - 1;
-                    }
-                    m = uni64(m);
-                }
-                if (m) {
-                    jf = __builtin_amdgcn_readfirstlane(base + __ffsll((unsigned long long)m) - 1);
-                    if (base != cbase) {
-                        // evict: this probe's requests on the old chunk go to the delta slab (read back past L1)
-                        if (cbase >= 0 && lane == 0) modb[cbase >> 6] = cmod;
-                        if (cbase >= 0 && ((cmod >> lane) & 1ull)) {
-#pragma unroll
-                            for (int ai = 0; ai < KP_LDS_AXES; ai++)
-                                if (ai < A)
-                                    __hip_atomic_store(&delta[(size_t)ai * E + cbase + lane], cd[ai], __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-                        }
-                        if (d.C <= KP_CONS_XTC)
-                            for (int cc = lane; cc < d.C; cc += 64) xtc[cc] = d.XT[(size_t)cc * EW + w] & ~excl[w];
-                        cbase = base;
-                        cx = xw;
-                        ccls = c;
-                        cmod = mw;
-                        cinit = uni64(initb[w]);
-#pragma unroll
-                        for (int ai = 0; ai < KP_LDS_AXES; ai++) {
-                            ch[ai] = h[ai];
-                            cd[ai] = dl[ai];
-                        }
-                    }
-                    break;
-                }
-            }
+            const int jf = scan_nodes(c, q, xs, tcons);
             if (prof) cy_scan += __builtin_amdgcn_s_memtime() - cs0;
             if (jf >= 0) {
                 if (lane == jf - cbase) {
@@ -920,7 +1167,19 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             S.st[CS_NEW_NC] += o.n_new_nodeclaims;
             S.st[CS_CHUNK_LOADS] += st_loads;
             S.st[CS_CACHE_HITS] += st_hits;
+            S.st[CS_CHUNK_SKIPS] += st_skips;
             if (prof) {
+                if (k.prof_probe) {
+                    int64_t* pp = k.prof_probe + (size_t)oi * 8;
+                    pp[0] = cy_build;
+                    pp[1] = cy_scan;
+                    pp[2] = __builtin_amdgcn_s_memtime() - cy0;
+                    pp[3] = n;
+                    pp[4] = pf_load;
+                    pp[5] = pf_prep;
+                    pp[6] = pf_nodes;
+                    pp[7] = pf_visits;
+                }
                 S.st[CS_CYC_BUILD] += cy_build;
                 S.st[CS_CYC_SCAN] += cy_scan;
                 S.st[CS_CYC_NODECLAIM] += cy_nc;
@@ -932,6 +1191,24 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
         __syncthreads();
     }
     if (lane < CS_COUNT && S.st[lane]) atomicAdd((unsigned long long*)&k.stats[lane], (unsigned long long)S.st[lane]);
+}
+
+// cmax0[w][ai]: the largest headroom on active axis ai over the nodes of chunk w (one wave per chunk; lanes past E and
+// axes past n_active hold INT64_MIN)
+__global__ __launch_bounds__(64) void chunk_max_kernel(const int64_t* __restrict__ ex_head, int E, int A,
+                                                        int64_t* __restrict__ cmax0) {
+    const int w = blockIdx.x, j = w * 64 + threadIdx.x;
+#pragma unroll
+    for (int ai = 0; ai < KP_LDS_AXES; ai++) {
+        const int64_t h = (ai < A && j < E) ? ex_head[(size_t)ai * E + j] : INT64_MIN;
+        const int64_t mx = wave_max64(h);
+        if (threadIdx.x == 0) cmax0[(size_t)w * KP_LDS_AXES + ai] = mx;
+    }
+}
+
+hipError_t kp_launch_cons_chunk_max(const KpDev& d, int64_t* cmax0, hipStream_t s) {
+    if (d.E > 0) hipLaunchKernelGGL(chunk_max_kernel, dim3(d.EW), dim3(64), 0, s, d.ex_head, d.E, d.n_active, cmax0);
+    return hipGetLastError();
 }
 
 // queue position of each pod: rank[queue0[i]] = i
@@ -970,6 +1247,21 @@ bool kp_cons_plan_lds(const KpDev& d, KpCons& k, int max_bytes) {
     off = al(off + (k.G > 0 ? 8 * (size_t)((k.G + 63) / 64) : 0));
     k.off_hmod = (int)off;
     off = al(off + (k.G > 0 ? 8 * (size_t)(d.EW > 0 ? d.EW : 1) : 0));
+    // the fast variant's store of the first chunks' headroom ([n_store][n_active][64] i64): up to KP_CONS_STORE chunks,
+    // fewer when the cluster is smaller
+    {
+        const int A = d.n_active > 0 ? d.n_active : 1;
+        int ns = d.EW < KP_CONS_STORE ? d.EW : KP_CONS_STORE;
+        if (ns < 1) ns = 1;
+        k.n_store = ns;
+        k.off_hs = (int)off;
+        off = al(off + (size_t)ns * A * 64 * 8);
+    }
+    // the chunk headroom summary, when it fits beside the rest (it is an accelerator, not needed for the result)
+    k.off_cmax = (int)off;
+    const size_t cm = 8 * (size_t)(d.EW > 0 ? d.EW : 1) * KP_LDS_AXES;
+    k.use_cmax = (k.cmax0 != nullptr && d.E > 0 && off + cm <= (size_t)max_bytes) ? 1 : 0;
+    if (k.use_cmax) off = al(off + cm);
     k.lds_bytes = (int)off;
     return (int)off <= max_bytes;
 }

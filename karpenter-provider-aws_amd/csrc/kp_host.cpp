@@ -41,6 +41,7 @@ hipError_t kp_launch_finalize(const KpDev& d, int n_nodeclaims, hipStream_t s);
 bool kp_cons_plan_lds(const KpDev& d, KpCons& k, int max_bytes);
 hipError_t kp_launch_select_kernel(const KpLaunch& g, hipStream_t s);
 hipError_t kp_launch_consolidate(const KpDev& d, const KpCons& k, int n_workers, hipStream_t s);
+hipError_t kp_launch_cons_chunk_max(const KpDev& d, int64_t* cmax0, hipStream_t s);
 hipError_t kp_launch_cons_prep(const int32_t* queue0, int P, int32_t* rank, const int32_t* pending, int n_pending,
                                uint64_t* pend_bits, hipStream_t s);
 hipError_t kp_queue_sort(const int64_t* fields, int n, int32_t* perm_a, int32_t* perm_b, uint64_t* keys_a,
@@ -445,11 +446,12 @@ struct kp_ctx {
     // consolidation probes
     DBuf<int32_t> d_retry, d_rank, d_cand_i, d_cand_off, d_cand_pods, d_pending, d_ring, d_ring_last, d_next;
     DBuf<double> d_cand_price;
-    DBuf<int64_t> d_cand_cap, d_delta, d_alloc_act, d_cons_stats;
+    DBuf<int64_t> d_cand_cap, d_delta, d_alloc_act, d_cons_stats, d_cmax0;
     DBuf<uint64_t> d_pend_bits, d_pbits;
     DBuf<uint64_t> d_init;
     DBuf<kp_probe_result> d_probe_out;
     DBuf<int32_t> d_rec_i;                   // kp_consolidate_command's read-back of the chosen REPLACE probe
+    DBuf<int64_t> d_prof_probe;              // KPSIM_PROFILE: per-probe cycles
     DBuf<ReqHdr> d_rec_hdr;
     DBuf<uint64_t> d_rec_words;
     KpCons cons{};                         // prepared consolidation pass (device pointers set per execute)
@@ -2670,6 +2672,8 @@ static kp_status cons_run(kp_ctx* ctx, int m0, int m1, int s0, int s1, kp_probe_
     k.n_multi = m1 - m0;
     k.sprobe0 = s0;
     k.ring_cap = std::max(1, c->cons_n_pending + maxp);
+    HIPCHK(c->d_cmax0.ensure((size_t)std::max(d.EW, 1) * KP_LDS_AXES));
+    k.cmax0 = getenv("KPSIM_CONS_NOSUMMARY") ? nullptr : c->d_cmax0.p;  // diagnostics: no chunk summary
     if (!kp_cons_plan_lds(d, k, KP_LDS_BYTES)) return fail(ctx, KP_E_UNSUPPORTED, "consolidation LDS plan exceeds 160 KB");
     const int occ = std::max(1, std::min(8, KP_LDS_BYTES / std::max(k.lds_bytes, 1)));
     const int workers = std::min(nprobe, 256 * occ);
@@ -2718,6 +2722,7 @@ static kp_status cons_run(kp_ctx* ctx, int m0, int m1, int s0, int s1, kp_probe_
         HIPCHK(kp_launch_class_mask(d, s));
         HIPCHK(kp_launch_template_init(d, s));
         HIPCHK(kp_launch_existing(d, s));
+        HIPCHK(kp_launch_cons_chunk_max(d, c->d_cmax0.p, s));
         c->cons_q0 = q0;
         c->cons_prep_valid = true;
     }
@@ -2743,6 +2748,12 @@ static kp_status cons_run(kp_ctx* ctx, int m0, int m1, int s0, int s1, kp_probe_
     k.stats = c->d_cons_stats.p;
     k.profile = getenv("KPSIM_PROFILE") ? 1 : 0;
     k.no_fast = getenv("KPSIM_CONS_NOFAST") ? atoi(getenv("KPSIM_CONS_NOFAST")) : 0;  // 1: FULL only, 2: fast only
+    k.prof_probe = nullptr;
+    if (k.profile) {
+        HIPCHK(c->d_prof_probe.ensure((size_t)nprobe * 8));
+        HIPCHK(hipMemsetAsync(c->d_prof_probe.p, 0, (size_t)nprobe * 8 * sizeof(int64_t), s));
+        k.prof_probe = c->d_prof_probe.p;
+    }
     k.rec_i = nullptr;
     k.rec_hdr = nullptr;
     k.rec_words = nullptr;
@@ -2773,6 +2784,23 @@ static kp_status cons_run(kp_ctx* ctx, int m0, int m1, int s0, int s1, kp_probe_
     c->cons_ms[1] = ms;
     c->cons_ms[2] = ns_since(t0) * 1e-6;
     for (int i = 0; i < CS_COUNT; i++) c->cons_stats[i] = cst[i];
+    if (k.prof_probe) {  // diagnostics: the probes that bound the pass
+        std::vector<int64_t> pp((size_t)nprobe * 8);
+        HIPCHK(hipMemcpy(pp.data(), k.prof_probe, pp.size() * sizeof(int64_t), hipMemcpyDeviceToHost));
+        for (int part = 0; part < 2; part++) {
+            const int b = part == 0 ? 0 : nmp, e = part == 0 ? nmp : nprobe;
+            int arg = -1;
+            for (int i = b; i < e; i++)
+                if (arg < 0 || pp[(size_t)i * 8 + 2] > pp[(size_t)arg * 8 + 2]) arg = i;
+            if (arg >= 0) {
+                const int64_t* q = &pp[(size_t)arg * 8];
+                fprintf(stderr, "[kpsim] %s probes %d: longest #%d: %lld cycles (build %lld, placement %lld: window loads %lld, "
+                        "chunk prep %lld, node intake %lld over %lld node visits), %lld pods\n",
+                        part == 0 ? "multi-node" : "single-node", e - b, arg - b, (long long)q[2], (long long)q[0],
+                        (long long)q[1], (long long)q[4], (long long)q[5], (long long)q[6], (long long)q[7], (long long)q[3]);
+            }
+        }
+    }
     return KP_OK;
 } catch (const std::exception& e) {
     return fail(ctx, KP_E_INVALID, e.what());

@@ -41,6 +41,37 @@ __device__ __forceinline__ uint32_t wave_reduce32(uint32_t x, F f) {
     r = f(r, (uint32_t)__builtin_amdgcn_readlane((int)x, 32));
     return f(r, (uint32_t)__builtin_amdgcn_readlane((int)x, 48));
 }
+// Inclusive prefix sum over the 64 lanes (lane i gets x_0 + .. + x_i), all DPP: a Hillis-Steele scan inside each row
+// (row_shr 1, 2, 4, 8; lanes shifted out of the row read 0), then row_bcast:15 adds the last lane of rows 0 / 2 to rows
+// 1 / 3 and row_bcast:31 adds lane 31 to rows 2 and 3 (the GFX9 broadcast controls; gfx950 keeps them).
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp32z(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xF, true);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint64_t dpp64z(uint64_t x) {
+    return ((uint64_t)dpp32z<CTRL, ROWS>((uint32_t)(x >> 32)) << 32) | dpp32z<CTRL, ROWS>((uint32_t)x);
+}
+__device__ __forceinline__ uint32_t wave_scan_add32(uint32_t x) {
+    KP_ASSERT_FULL_WAVE();
+    x += dpp32z<0x111, 0xF>(x);
+    x += dpp32z<0x112, 0xF>(x);
+    x += dpp32z<0x114, 0xF>(x);
+    x += dpp32z<0x118, 0xF>(x);
+    x += dpp32z<0x142, 0xA>(x);
+    x += dpp32z<0x143, 0xC>(x);
+    return x;
+}
+__device__ __forceinline__ uint64_t wave_scan_add64(uint64_t x) {
+    KP_ASSERT_FULL_WAVE();
+    x += dpp64z<0x111, 0xF>(x);
+    x += dpp64z<0x112, 0xF>(x);
+    x += dpp64z<0x114, 0xF>(x);
+    x += dpp64z<0x118, 0xF>(x);
+    x += dpp64z<0x142, 0xA>(x);
+    x += dpp64z<0x143, 0xC>(x);
+    return x;
+}
 template <class F>
 __device__ __forceinline__ uint64_t wave_reduce64(uint64_t x, F f) {
     KP_ASSERT_FULL_WAVE();

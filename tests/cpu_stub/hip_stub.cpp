@@ -139,6 +139,7 @@ hipError_t kp_launch_consolidate(const KpDev&, const KpCons& k, int, hipStream_t
 hipError_t kp_launch_cons_prep(const int32_t*, int, int32_t*, const int32_t*, int, uint64_t*, hipStream_t) {
     return hipSuccess;
 }
+hipError_t kp_launch_cons_chunk_max(const KpDev&, int64_t*, hipStream_t) { return hipSuccess; }
 hipError_t kp_queue_sort(const int64_t* fields, int n, int32_t* perm_a, int32_t*, uint64_t*, uint64_t*, void*,
                          size_t* temp_bytes, hipStream_t, int32_t** result) {
     if (!fields) {
