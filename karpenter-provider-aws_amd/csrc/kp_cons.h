@@ -44,6 +44,7 @@ struct KpCons {
     int32_t ring_cap;           // >= pods of any probe
     int32_t* ring;              // [workers][ring_cap] queue entries: pod | pending << 31
     int32_t* ring_last;         // [workers][ring_cap] Queue.lastLen of the entry (-1: never pushed)
+    int32_t* pnode;             // [workers][ring_cap] FULL variant: 0 = an existing node took the pod, -1 = none does
     int64_t* delta;             // [workers][n_active][E] requests added to node j by this probe (valid: mod bit)
     uint64_t* pbits;            // [workers][PW] probe pods by queue position (all zero between probes)
     int32_t* next_probe;        // [3] work counters: fast variant, full variant, probes handed to the full variant

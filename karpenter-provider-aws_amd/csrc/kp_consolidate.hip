@@ -167,7 +167,10 @@ __device__ inline uint64_t commit_held(int32_t* rcap, uint64_t old, uint64_t nw,
 // Topology.AddRequirements on each candidate node (first-fit over the nodes that pass, never memoised: counts move) and
 // NodeClaim.Add's on the in-flight NodeClaim (hostname row E) and on templates (a fresh hostname, count 0); every
 // placement of a counted class is recorded.
-template <bool FULL, bool RESV = false, bool TOPO = false>
+// NA (fast variant only): the number of active axes, fixed at compile time so that the window intake's per-axis tests
+// and prefix sums unroll without runtime guards (0: read from d.n_active).
+#define AXL(ai) _Pragma("unroll") for (int ai = 0; ai < (NA > 0 ? NA : KP_LDS_AXES); ai++) if (NA > 0 || ai < A)
+template <bool FULL, bool RESV = false, bool TOPO = false, int NA = 0>
 __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     ConsShared& S = *reinterpret_cast<ConsShared*>(smem);
@@ -372,7 +375,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
         if (prof) cy_build = __builtin_amdgcn_s_memtime() - cy0;
         // ---- Solve: queue with lastLen termination; existing nodes, the in-flight NodeClaim, the templates ----
         int head = 0, count = n, wbase = -64;
-        int vpod = -1, vlast = -1, vc = 0, vshape = -1;
+        int vpod = -1, vlast = -1, vc = 0, vshape = -1, vpn = -1;
         int64_t vq[KP_LDS_AXES];
 #pragma unroll
         for (int ai = 0; ai < KP_LDS_AXES; ai++) vq[ai] = 0;
@@ -387,6 +390,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 const int slot = pos % cap;
                 vpod = ld32(&ring[slot]);
                 vlast = ld32(&rlast[slot]);
+                if (FULL && !TOPO) vpn = ld32(&k.pnode[(size_t)wid * cap + slot]);
                 const int p = vpod & 0x7fffffff;
                 vc = d.pod_cls[p];
                 vshape = d.pod_shape[p];
@@ -546,11 +550,15 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             }
             return jf;
         };
-        if constexpr (!FULL && !TOPO) {
-            // ---- fast variant: the probe's pods in windows of 64, one pod per lane ----
-            // Every pod here lands on an existing node or the probe goes to the FULL variant, so the queue is one pass
-            // in order and the probe is plain first fit: each pod takes the first node in scheduling order that is
-            // compatible, not a candidate, and has headroom for it.  First fit is computed node-major: node j, in order,
+        if constexpr (!TOPO) {
+            // ---- existing nodes: the probe's pods in windows of 64, one pod per lane ----
+            // Fast variant: every pod here lands on an existing node or the probe goes to the FULL variant, so the queue
+            // is one pass in order and the probe is plain first fit: each pod takes the first node in scheduling order
+            // that is compatible, not a candidate, and has headroom for it.  FULL variant: the same pass runs first and
+            // records which pods no existing node takes (k.pnode); ExistingNode.Add is independent of the in-flight
+            // NodeClaim, existing nodes only lose headroom, and a pod is first popped in queue order, so these are the
+            // placements the serial queue below would make, and a pod refused once (or re-pushed later) is refused by
+            // every node again: the queue then runs NodeClaim.Add / the templates for those pods only.  First fit is computed node-major: node j, in order,
             // takes from the window's pods not yet placed, in queue order, each one that still fits it (a pod that first
             // fits node j under pod-major first fit is exactly one node j takes here: by induction over j, the pods an
             // earlier node took before pod i are the same in both orders).  Per node the intake is greedy in queue
@@ -560,10 +568,12 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             // per axis and node, loaded on first touch, updated in place); a pod that fits no store node takes the serial
             // scan over the later chunks, in queue order.
             const int KS = k.n_store;
+            const int AA = NA > 0 ? NA : A;  // active axes (compile-time in the NA instantiations)
             const int SE = KS * 64 < E ? KS * 64 : E;  // nodes [0, SE) are in the store
             int64_t* hs = reinterpret_cast<int64_t*>(smem + k.off_hs);  // [KS][A][64]
             uint64_t loaded = 0;  // store chunks in LDS
             const long long cf0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+            int32_t* pnode = FULL ? k.pnode + (size_t)wid * cap : nullptr;
             for (int wb = 0; wb < n && !aborted; wb += 64) {
                 const long long cw0 = prof ? __builtin_amdgcn_s_memtime() : 0;
                 const int wn = __builtin_amdgcn_readfirstlane(n - wb < 64 ? n - wb : 64);
@@ -591,19 +601,15 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     if (!anyc) continue;
                     if (!((loaded >> w) & 1ull)) {  // first touch: the chunk's headroom into the store
                         const int j = w * 64 + lane;
-#pragma unroll
-                        for (int ai = 0; ai < KP_LDS_AXES; ai++)
-                            if (ai < A) hs[(w * A + ai) * 64 + lane] = j < E ? d.ex_head[(size_t)ai * E + j] : -1;
+                        AXL(ai) hs[(w * AA + ai) * 64 + lane] = j < E ? d.ex_head[(size_t)ai * E + j] : -1;
                         loaded |= 1ull << w;
                         st_loads++;
                     }
                     // a node below the smallest remaining request on some axis takes none of them
                     bool pot = (anyc >> lane) & 1ull;
                     int64_t hl[KP_LDS_AXES];
-#pragma unroll
-                    for (int ai = 0; ai < KP_LDS_AXES; ai++)
-                        if (ai < A) {
-                            hl[ai] = hs[(w * A + ai) * 64 + lane];
+                    AXL(ai) {
+                            hl[ai] = hs[(w * AA + ai) * 64 + lane];
                             const int64_t mq = (int64_t)wave_reduce64(inU ? (uint64_t)wq[ai] : (uint64_t)INT64_MAX,
                                                                       [](uint64_t a, uint64_t b) { return (int64_t)b < (int64_t)a ? b : a; });
                             pot = pot && hl[ai] >= mq;
@@ -621,9 +627,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                         for (int ai = 0; ai < KP_LDS_AXES; ai++) hj[ai] = ai < A ? (int64_t)rl64((uint64_t)hl[ai], jn) : 0;
                         // the pods that fit the node on their own; a pod outside this set never fits it later
                         bool e = ((U >> lane) & 1ull) && ((xw >> jn) & 1ull);
-#pragma unroll
-                        for (int ai = 0; ai < KP_LDS_AXES; ai++)
-                            if (ai < A) e = e && wq[ai] <= hj[ai];
+                        AXL(ai) e = e && wq[ai] <= hj[ai];
                         uint64_t em = ballot(e);
                         if (!em) continue;
                         uint64_t took = 0;
@@ -631,9 +635,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                             // many: the prefix up to the first running-total overflow is taken in one round of prefix sums
                             bool over = false;
                             int64_t pv[KP_LDS_AXES];
-#pragma unroll
-                            for (int ai = 0; ai < KP_LDS_AXES; ai++)
-                                if (ai < A) {
+                            AXL(ai) {
                                     pv[ai] = (int64_t)wave_scan_add64(e ? (uint64_t)wq[ai] : 0ull);
                                     over = over || pv[ai] > hj[ai];
                                 }
@@ -642,15 +644,11 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                             took = em & (fo >= 64 ? ~0ull : ((1ull << fo) - 1ull));
                             if (took) {
                                 const int last = 63 - __clzll((long long)took);
-#pragma unroll
-                                for (int ai = 0; ai < KP_LDS_AXES; ai++)
-                                    if (ai < A) hj[ai] -= (int64_t)rl64((uint64_t)pv[ai], last);
+                                AXL(ai) hj[ai] -= (int64_t)rl64((uint64_t)pv[ai], last);
                             }
                             // the rest: the pods after the overflowing one that still fit what is left
                             bool e2 = e && lane > fo;
-#pragma unroll
-                            for (int ai = 0; ai < KP_LDS_AXES; ai++)
-                                if (ai < A) e2 = e2 && wq[ai] <= hj[ai];
+                            AXL(ai) e2 = e2 && wq[ai] <= hj[ai];
                             em = fo >= 64 ? 0ull : ballot(e2);
                         }
                         // few: greedily in queue order with scalar running totals
@@ -658,24 +656,18 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                             const int t = __ffsll((unsigned long long)em) - 1;
                             int64_t qt[KP_LDS_AXES];
                             bool ok = true;
-#pragma unroll
-                            for (int ai = 0; ai < KP_LDS_AXES; ai++)
-                                if (ai < A) {
+                            AXL(ai) {
                                     qt[ai] = (int64_t)rl64((uint64_t)wq[ai], t);
                                     ok = ok && qt[ai] <= hj[ai];
                                 }
                             if (!ok) continue;
-#pragma unroll
-                            for (int ai = 0; ai < KP_LDS_AXES; ai++)
-                                if (ai < A) hj[ai] -= qt[ai];
+                            AXL(ai) hj[ai] -= qt[ai];
                             took |= 1ull << t;
                         }
                         if (!took) continue;
                         U &= ~took;
                         touched |= 1ull << jn;
-#pragma unroll
-                        for (int ai = 0; ai < KP_LDS_AXES; ai++)
-                            if (ai < A && lane == jn) hl[ai] = hj[ai];
+                        AXL(ai) if (lane == jn) hl[ai] = hj[ai];
                         const int ntk = __popcll(took);
                         st_placed += ntk;
                         st_hits += ntk;
@@ -685,9 +677,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                         else if (npl) bad = true;
                     }
                     if ((touched >> lane) & 1ull) {  // each lane writes back its own node
-#pragma unroll
-                        for (int ai = 0; ai < KP_LDS_AXES; ai++)
-                            if (ai < A) hs[(w * A + ai) * 64 + lane] = hl[ai];
+                        AXL(ai) hs[(w * AA + ai) * 64 + lane] = hl[ai];
                     }
                     if (prof) pf_nodes += __builtin_amdgcn_s_memtime() - cn0;
                 }
@@ -706,13 +696,17 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     }
                     const int jf = SE < E ? scan_nodes(c, q, xstart > SE ? xstart : SE, false) : -1;
                     if (jf < 0) {
-                        aborted = true;  // needs a NodeClaim: the FULL variant redoes this probe
-                        break;
+                        if constexpr (!FULL) {
+                            aborted = true;  // needs a NodeClaim: the FULL variant redoes this probe
+                            break;
+                        } else {
+                            xstart = E;  // every node refuses this shape from now on
+                            continue;
+                        }
                     }
+                    U &= ~(1ull << i);
                     if (lane == jf - cbase) {
-#pragma unroll
-                        for (int ai = 0; ai < KP_LDS_AXES; ai++)
-                            if (ai < A) {
+                        AXL(ai) {
                                 ch[ai] -= q[ai];
                                 cd[ai] += q[ai];
                             }
@@ -725,10 +719,12 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                         else bad = true;
                     }
                 }
+                if (FULL && live) pnode[wb + lane] = ((U >> lane) & 1ull) ? -1 : 0;
             }
+            if (FULL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (prof) cy_scan = __builtin_amdgcn_s_memtime() - cf0;
-        } else
-        while (count > 0) {
+        }
+        if constexpr (FULL || TOPO) while (count > 0) {
             // loop-carried wave-uniform state: re-asserted scalar each pod, so the chunk tests below branch on SGPRs
             head = __builtin_amdgcn_readfirstlane(head);
             count = __builtin_amdgcn_readfirstlane(count);
@@ -743,9 +739,13 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             if (head - wbase >= 64) win_load(head);
             const int off = head - wbase;
             const int ent = rl32(vpod, off);
-            if (rl32(vlast, off) == count) break;  // Queue.Pop: cycled through the queue without progress
+            const int elast = rl32(vlast, off);
+            if (elast == count) break;  // Queue.Pop: cycled through the queue without progress
             head++;
             count--;
+            // FULL, no topology: the window pass above placed this pod on an existing node (first pop), or every node
+            // refuses it
+            if (FULL && !TOPO && elast < 0 && rl32(vpn, off) >= 0) continue;
             st_pops++;
             const bool pend = ent < 0;
             const int p = ent & 0x7fffffff;
@@ -772,7 +772,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             const bool tcons = TOPO && (cflags & CF_TOPO_CONS);
             const int xs = tcons ? 0 : xstart;
             const long long cs0 = prof ? __builtin_amdgcn_s_memtime() : 0;
-            const int jf = scan_nodes(c, q, xs, tcons);
+            const int jf = (FULL && !TOPO) ? -1 : scan_nodes(c, q, xs, tcons);
             if (prof) cy_scan += __builtin_amdgcn_s_memtime() - cs0;
             if (jf >= 0) {
                 if (lane == jf - cbase) {
@@ -1269,6 +1269,12 @@ bool kp_cons_plan_lds(const KpDev& d, KpCons& k, int max_bytes) {
 // Per-device kernel attributes, set by kp_ctx_create with the ctx's device current (see kp_ffd_set_attributes).
 hipError_t kp_cons_set_attributes() {
     const void* fns[] = {(const void*)consolidate_kernel<false>, (const void*)consolidate_kernel<true>,
+                         (const void*)consolidate_kernel<false, false, false, 1>,
+                         (const void*)consolidate_kernel<false, false, false, 2>,
+                         (const void*)consolidate_kernel<false, false, false, 3>,
+                         (const void*)consolidate_kernel<false, false, false, 4>,
+                         (const void*)consolidate_kernel<false, false, false, 5>,
+                         (const void*)consolidate_kernel<false, false, false, 6>,
                          (const void*)consolidate_kernel<true, true>, (const void*)consolidate_kernel<false, false, true>,
                          (const void*)consolidate_kernel<true, false, true>, (const void*)consolidate_kernel<true, true, true>};
     for (const void* f : fns) {
@@ -1289,7 +1295,18 @@ hipError_t kp_launch_consolidate(const KpDev& d, const KpCons& k, int n_workers,
         }
         return hipGetLastError();
     }
-    if (k.no_fast != 1) hipLaunchKernelGGL(consolidate_kernel<false>, dim3(n_workers), dim3(64), lds, s, d, k);
+    if (k.no_fast != 1) {
+        const dim3 g(n_workers), b(64);
+        switch (d.n_active) {
+            case 1: hipLaunchKernelGGL((consolidate_kernel<false, false, false, 1>), g, b, lds, s, d, k); break;
+            case 2: hipLaunchKernelGGL((consolidate_kernel<false, false, false, 2>), g, b, lds, s, d, k); break;
+            case 3: hipLaunchKernelGGL((consolidate_kernel<false, false, false, 3>), g, b, lds, s, d, k); break;
+            case 4: hipLaunchKernelGGL((consolidate_kernel<false, false, false, 4>), g, b, lds, s, d, k); break;
+            case 5: hipLaunchKernelGGL((consolidate_kernel<false, false, false, 5>), g, b, lds, s, d, k); break;
+            case 6: hipLaunchKernelGGL((consolidate_kernel<false, false, false, 6>), g, b, lds, s, d, k); break;
+            default: hipLaunchKernelGGL(consolidate_kernel<false>, g, b, lds, s, d, k); break;
+        }
+    }
     if (k.no_fast != 2) {
         if (d.ro) hipLaunchKernelGGL((consolidate_kernel<true, true>), dim3(n_workers), dim3(64), lds, s, d, k);
         else hipLaunchKernelGGL(consolidate_kernel<true>, dim3(n_workers), dim3(64), lds, s, d, k);

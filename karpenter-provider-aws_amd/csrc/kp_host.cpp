@@ -444,7 +444,7 @@ struct kp_ctx {
     bool cons_mayfix = false;                // a pod's NotIn/DoesNotExist merge can change a later Compatible
     std::string cons_mayfix_key;
     // consolidation probes
-    DBuf<int32_t> d_retry, d_rank, d_cand_i, d_cand_off, d_cand_pods, d_pending, d_ring, d_ring_last, d_next;
+    DBuf<int32_t> d_retry, d_rank, d_cand_i, d_cand_off, d_cand_pods, d_pending, d_ring, d_ring_last, d_next, d_pnode;
     DBuf<double> d_cand_price;
     DBuf<int64_t> d_cand_cap, d_delta, d_alloc_act, d_cons_stats, d_cmax0;
     DBuf<uint64_t> d_pend_bits, d_pbits;
@@ -2695,6 +2695,7 @@ static kp_status cons_run(kp_ctx* ctx, int m0, int m1, int s0, int s1, kp_probe_
     const auto t0 = clk::now();
     HIPCHK(c->d_ring.ensure((size_t)workers * k.ring_cap));
     HIPCHK(c->d_ring_last.ensure((size_t)workers * k.ring_cap));
+    HIPCHK(c->d_pnode.ensure((size_t)workers * k.ring_cap));
     HIPCHK(c->d_delta.ensure((size_t)workers * std::max(A, 1) * std::max(E, 1)));
     const size_t pb = (size_t)workers * k.PW;
     if (c->d_pbits.n < pb) {  // kept all-zero between probes by the kernel
@@ -2740,6 +2741,7 @@ static kp_status cons_run(kp_ctx* ctx, int m0, int m1, int s0, int s1, kp_probe_
     k.alloc_act = c->d_alloc_act.p;
     k.ring = c->d_ring.p;
     k.ring_last = c->d_ring_last.p;
+    k.pnode = c->d_pnode.p;
     k.delta = c->d_delta.p;
     k.pbits = c->d_pbits.p;
     k.next_probe = c->d_next.p;
