@@ -28,7 +28,7 @@ FFD_COUNTERS = ["cyc_fast_loop", "cyc_sort", "cyc_slow_eval", "cyc_templates", "
                 "ev_off", "ev_types", "ev_min", "ev_calls", "quick_accepts", "slow_pods", "witness_misses", "cyc_q_pop",
                 "cyc_q_scan", "cyc_q_check", "cyc_q_commit", "n_noinv", "n_winmove", "n_ldssort", "n_pivot", "n_winload",
                 "n_flush", "n_shape", "n_lds_append", "n_lds_nowin", "n_lds_outside", "n_batches", "topo_quick",
-                "cyc_topo_setup", "cyc_topo_scan"]
+                "cyc_topo_setup", "cyc_topo_scan", "rej_requirements", "rej_topology", "rej_types", "rej_min_values"]
 
 
 def log(msg):

@@ -323,7 +323,9 @@ kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out);
  * [5..10]: wave-0 fast loop, its sort.Slice share, slow-path NodeClaim.Add rounds, new-NodeClaim templates, -,
  * full-pdqsort share; [11..16] per-stage evaluation cycles; then event counts [17] quick accepts, [18] slow-path
  * pods, [19] witness misses (slow-path evaluations of a NodeClaim whose class repeats), [20..23] fast-loop
- * cycles: pop, scan, quick check, quick commit. */
+ * cycles: pop, scan, quick check, quick commit; [24..34] fast-loop event counts; [35] topology quick accepts, [36..37]
+ * topology prefilter setup / scan cycles; [38..41] failed NodeClaim.Add evaluations by stage: requirement merge,
+ * topology narrowing, no instance type left, minValues (n up to 42). */
 kp_status kp_last_kernel_times(kp_ctx* ctx, double* ms, int32_t n);
 
 /*

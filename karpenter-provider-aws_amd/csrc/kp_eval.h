@@ -667,7 +667,10 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
     const int TW = d.TW, T = d.T;
     long long _t0 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
     if (a.prof && lane == 0) atomicAdd((unsigned long long*)&a.prof[ST_EV_CALLS - ST_EV_REQ], 1ull);
-    if (a.compat && !((CC.tol >> a.tmpl) & 1u)) return false;
+    if (a.compat && !((CC.tol >> a.tmpl) & 1u)) {
+        if (lane == 0) ws.memo_ok = 1;  // taints are fixed: the rejection holds for the shape
+        return false;
+    }
     const int nck = CC.nck;
 
     // ---- requirements: Compatible + Add (lane = class key) ----
@@ -722,10 +725,20 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         ws.hdr[lane] = O;
         if (!TOPO) classify(k, O, ow, cnt);
     }
-    if (ballot(fail)) return false;
+#define EV_REJ(slot) \
+    do { \
+        if (a.prof && lane == 0) atomicAdd((unsigned long long*)&a.prof[(slot) - ST_EV_REQ], 1ull); \
+    } while (0)
+    if (ballot(fail)) {
+        EV_REJ(ST_REJ_REQ);
+        return false;
+    }
     if (TOPO) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        if (!topo_narrow<CT>(d, CC, ws, a.host, a.compat, lane, E.pt)) return false;
+        if (!topo_narrow<CT>(d, CC, ws, a.host, a.compat, lane, E.pt)) {
+            EV_REJ(ST_REJ_TOPO);
+            return false;
+        }
         if (lane < nck) {
             const ReqHdr O = ws.hdr[lane];
             const uint64_t* ow = ws.words + CC.wsoff[lane];
@@ -822,7 +835,10 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         anyw |= nb;
     }
     EV_STAMP(3);
-    if (anyw == 0) return false;
+    if (anyw == 0) {
+        EV_REJ(ST_REJ_TYPES);
+        return false;
+    }
 
     // ---- minValues (Strict): distinct values per key over the remaining options ----
     if (a.tmpl >= 0 && ((E.min_tmpl_mask >> a.tmpl) & 1u)) {
@@ -864,7 +880,10 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
                 for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
                 count = c;
             }
-            if (count < h.minv && !(BE && min_values_unmet(d, ws, k, count, lane))) return false;
+            if (count < h.minv && !(BE && min_values_unmet(d, ws, k, count, lane))) {
+                EV_REJ(ST_REJ_MIN);
+                return false;
+            }
         }
     }
     // ---- reservations (NodeClaim.Add's offeringsToReserve, ReservedOfferingModeStrict) ----

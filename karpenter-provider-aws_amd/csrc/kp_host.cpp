@@ -438,7 +438,7 @@ struct kp_ctx {
     double ns_prep = 0, ns_exec = 0, ns_fin = 0;
     hipEvent_t ev[6] = {};
     double kernel_ms[5] = {};
-    int64_t cycles[33] = {};  // FFD phases (s_memtime): pop, sort, scan+eval, templates, commit, full pdqsort
+    int64_t cycles[37] = {};  // FFD phases (s_memtime): pop, sort, scan+eval, templates, commit, full pdqsort
     bool any_min_values = false;             // some template requirement carries minValues
     bool min_multi = false;                  // ... on a multi-valued catalog key (zone, capacity type, ...)
     bool cons_mayfix = false;                // a pod's NotIn/DoesNotExist merge can change a later Compatible
@@ -2163,6 +2163,8 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.stats = c->d_stats.p;
     d.err = c->d_err.p;
     d.profile = getenv("KPSIM_PROFILE") ? 1 : 0;
+    // topology pods: candidates per block round (KPSIM_TOPO_CANDS, diagnostics)
+    d.topo_cands = getenv("KPSIM_TOPO_CANDS") ? std::max(1, std::min(KP_NWAVES, atoi(getenv("KPSIM_TOPO_CANDS")))) : KP_NWAVES;
     // KPSIM_TRACE_POD=p traces pod p; KPSIM_TRACE_CLASS=c traces every slow-path pod of class c (trace_pod = -2 - c)
     d.trace_pod = getenv("KPSIM_TRACE_POD") ? atoi(getenv("KPSIM_TRACE_POD"))
                   : getenv("KPSIM_TRACE_CLASS") ? -2 - atoi(getenv("KPSIM_TRACE_CLASS")) : -1;
@@ -2344,6 +2346,7 @@ extern "C" kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out) {
     for (int i = 0; i < 7; i++) c->cycles[12 + i] = st[ST_QUICK + i];
     for (int i = 0; i < 11; i++) c->cycles[19 + i] = st[ST_N_NOINV + i];
     for (int i = 0; i < 3; i++) c->cycles[30 + i] = st[ST_TOPO_QUICK + i];
+    for (int i = 0; i < 4; i++) c->cycles[33 + i] = st[ST_REJ_REQ + i];
     so.ns_host_prep = c->ns_prep;
     so.ns_device_solve = c->ns_exec;
     if (N > out->cap_nodeclaims || n_ids > out->cap_type_ids) return fail(ctx, KP_E_BUFFER, "output buffers too small");
@@ -2376,7 +2379,7 @@ extern "C" kp_status kp_last_kernel_times(kp_ctx* ctx, double* ms, int32_t n) {
     if (!ctx || !ms) return KP_E_INVALID;
     if (!ctx->executed) return fail(ctx, KP_E_STATE, "no execute yet");
     for (int i = 0; i < n && i < 5; i++) ms[i] = ctx->kernel_ms[i];
-    for (int i = 5; i < n && i < 38; i++) ms[i] = (double)ctx->cycles[i - 5];
+    for (int i = 5; i < n && i < 42; i++) ms[i] = (double)ctx->cycles[i - 5];
     return KP_OK;
 }
 

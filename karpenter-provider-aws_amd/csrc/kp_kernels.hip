@@ -268,8 +268,8 @@ __device__ __forceinline__ bool topo_prefilter_pass(const KpDev& d, const FfdSha
 
 // wave 0: the first slice position in [start, N) that has not rejected the shape and passes the topology prefilter
 // (N if none).  Four 64-position chunks per round so the prefilter's global loads of 256 NodeClaims overlap.
-__device__ inline int topo_scan(const KpDev& d, const FfdShared& S, const uint32_t* skey, const uint16_t* sord, int N,
-                                int start, int lane) {
+__device__ inline int topo_scan(const KpDev& d, const FfdShared& S, const uint32_t* skey, const uint16_t* sord,
+                                const uint8_t* stmpl, int N, int start, int lane) {
     for (int base = start; base < N; base += 256) {
         bool ok[4];
         int nc[4];
@@ -278,6 +278,7 @@ __device__ inline int topo_scan(const KpDev& d, const FfdShared& S, const uint32
             const int p = base + u * 64 + lane;
             ok[u] = p < N && !(skey[p] >> 31);
             nc[u] = ok[u] ? (int)sord[p] : 0;
+            ok[u] = ok[u] && ((S.cur_tol >> stmpl[nc[u]]) & 1u);  // NodeClaim.Add's toleration check
         }
         for (int e = 0; e < S.tp_n; e++) {
             const int k = S.tp_k[e];
@@ -359,15 +360,21 @@ __device__ inline void topo_record_quick(const KpDev& d, int c, int nc, int tmpl
 
 // wave 0: collect up to KP_NWAVES slice positions >= start whose NodeClaim has not rejected the current shape (and
 // passes the topology prefilter of the current pod)
-__device__ inline void collect_candidates(const KpDev& d, FfdShared& S, const uint32_t* key, const uint16_t* ord, int N,
-                                          int start, int buf, int lane) {
+__device__ inline void collect_candidates(const KpDev& d, FfdShared& S, const uint32_t* key, const uint16_t* ord,
+                                          const uint8_t* stmpl, uint32_t tol, int N, int start, int buf, int lane) {
     int cnt = 0, pos = start, next = N;
+    // topology pods: at most d.topo_cands candidates per round (the first prefilter survivor usually accepts; fewer waves
+    // evaluating leaves each its own SIMD)
+    const int L = S.tp_n ? d.topo_cands : KP_NWAVES;
     while (pos < N) {
         const int p = pos + lane;
         bool c = p < N && !(key[p] >> 31);
+        // NodeClaim.Add's first check (the pod tolerates the NodeClaim's template taints) is decided here: a candidate
+        // that fails it would be rejected before any other stage
+        if (c) c = (tol >> stmpl[ord[p]]) & 1u;
         if (S.tp_n && c) c = topo_prefilter_pass(d, S, ord[p]);
         const uint64_t m0 = __ballot(c);
-        if (S.tp_n && m0 && cnt + __popcll(m0) < KP_NWAVES) {
+        if (S.tp_n && m0 && cnt + __popcll(m0) < L) {
             // topology pods: the first prefilter survivor usually accepts; end the round with this window rather than
             // paying the prefilter's loads for up to 8 candidates (the next round continues after it)
             const int rank = cnt + __popcll(m0 & ((1ull << lane) - 1ull));
@@ -383,12 +390,12 @@ __device__ inline void collect_candidates(const KpDev& d, FfdShared& S, const ui
         }
         const uint64_t m = __ballot(c);
         const int rank = cnt + __popcll(m & ((1ull << lane) - 1ull));
-        if (c && rank < KP_NWAVES) S.cand_pos[buf][rank] = p;
+        if (c && rank < L) S.cand_pos[buf][rank] = p;
         const int tot = cnt + __popcll(m);
-        if (tot >= KP_NWAVES) {
-            const uint64_t last = __ballot(c && rank == KP_NWAVES - 1);
+        if (tot >= L) {
+            const uint64_t last = __ballot(c && rank == L - 1);
             next = pos + __ffsll((unsigned long long)last);  // position after the last collected candidate
-            cnt = KP_NWAVES;
+            cnt = L;
             break;
         }
         cnt = tot;
@@ -396,8 +403,8 @@ __device__ inline void collect_candidates(const KpDev& d, FfdShared& S, const ui
     }
     if (lane == 0) {
         S.n_cand[buf] = cnt;
-        S.scan_next[buf] = cnt == KP_NWAVES ? next : N;
-        S.scan_done[buf] = (cnt < KP_NWAVES) || next >= N;
+        S.scan_next[buf] = cnt == L ? next : N;
+        S.scan_done[buf] = (cnt < L) || next >= N;
     }
 }
 
@@ -1101,7 +1108,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                     S.cls_fill = S.CC.cls != c;  // decided before the barrier: fill_class_cache rewrites CC.cls
                     S.topo_pod = 0;
                 }
-                collect_candidates(d, S, skey, sord, N, f, 0, lane);
+                collect_candidates(d, S, skey, sord, stmpl, tl, N, f, 0, lane);
                 break;
             }
             win_flush();
@@ -1198,7 +1205,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 if (cfl & CF_TOPO_CONS) topo_prefilter_setup(d, S, c, lane);
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 const long long t1 = prof_clock(d);
-                const int f = topo_scan(d, S, skey, sord, N, S.scan_start, lane);
+                const int f = topo_scan(d, S, skey, sord, stmpl, N, S.scan_start, lane);
                 const long long t2 = prof_clock(d);
                 bool quick = false;
                 if (f < N && (cfl & CF_TOPO_QREC) && A > 0) {
@@ -1224,7 +1231,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     }
                 }
-                if (!quick) collect_candidates(d, S, skey, sord, N, f, 0, lane);
+                if (!quick) collect_candidates(d, S, skey, sord, stmpl, S.cur_tol, N, f, 0, lane);
                 if (lane == 0) {
                     S.topo_quick = quick;
                     if (d.profile) {
@@ -1316,7 +1323,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 }
             if (tid == 0) S.st[ST_NC_EVALS] += nc_;
             if (win >= 0 || S.scan_done[b]) break;
-            if (wave == 0) collect_candidates(d, S, skey, sord, S.N, S.scan_next[b], b ^ 1, lane);
+            if (wave == 0) collect_candidates(d, S, skey, sord, stmpl, S.cur_tol, S.N, S.scan_next[b], b ^ 1, lane);
             __syncthreads();
             round++;
         }

@@ -180,6 +180,7 @@ struct KpDev {
     int64_t* stats;                  // [16]
     int32_t* err;                    // [1] device-side error code (capacity overflow etc.)
     int32_t profile;                 // accumulate per-stage evaluation cycles (diagnostics)
+    int32_t topo_cands;              // NodeClaims evaluated per block round for a topology pod (<= KP_NWAVES)
     int32_t trace_pod;               // diagnostics (KPSIM_TRACE_POD): the slow path logs this pod's evaluations
     int32_t trace_max;               //   KPSIM_TRACE_CLASS: only pods with index <= KPSIM_TRACE_MAXPOD
     int32_t* trace;                  //   [1 + 6 * KP_TRACE_N]: count, then {round, nodeclaim (-1-j: template j), ok, flags, held lo/hi}
@@ -251,5 +252,7 @@ enum {
     ST_EV_REQ = 16, ST_EV_MASK, ST_EV_OFF, ST_EV_TYPES, ST_EV_MIN, ST_EV_CALLS,
     ST_QUICK = 24, ST_SLOW, ST_WITNESS_MISS, ST_CYC_QPOP, ST_CYC_QSCAN, ST_CYC_QCHECK, ST_CYC_QCOMMIT,
     ST_N_NOINV = 32, ST_N_WINMOVE, ST_N_LDSSORT, ST_N_PIVOT, ST_N_WINLOAD, ST_N_FLUSH, ST_N_SHAPE, ST_EXIST_PLACED = 44,
-    ST_TOPO_QUICK = 45, ST_CYC_TSETUP, ST_CYC_TSCAN, ST_COUNT = 48
+    ST_TOPO_QUICK = 45, ST_CYC_TSETUP, ST_CYC_TSCAN,
+    // KPSIM_PROFILE: why evaluations fail (requirement merge, topology narrowing, no type left, minValues, other)
+    ST_REJ_REQ = 48, ST_REJ_TOPO, ST_REJ_TYPES, ST_REJ_MIN, ST_COUNT = 52
 };

@@ -172,8 +172,8 @@ class Context:
         """FFD-kernel counters of the last fetched solve (kpsim.h kp_last_kernel_times [5..19]): s_memtime cycles
         (with KPSIM_PROFILE=1) of the fast loop, sort, slow-path rounds, templates, -, full sort, six evaluation
         stages; then quick accepts, slow-path pods, witness misses, quick-path cycles (pop, scan, check, commit)."""
-        a = (C.c_double * 38)()
-        self.check(self.L.kp_last_kernel_times(self.h, a, 38), "kp_last_kernel_times")
+        a = (C.c_double * 42)()
+        self.check(self.L.kp_last_kernel_times(self.h, a, 42), "kp_last_kernel_times")
         return list(a)[5:]
 
     def consolidate(self, cons_view):
