@@ -232,6 +232,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
     Ev.rcap = RESV ? S.rcap : nullptr;
     Ev.resv_on = RESV ? d.resv_on : 0;  // disruption simulations: ReservedOfferingModeFallback (STRICT = false below)
     Ev.pt = TOPO ? &P : nullptr;
+    Ev.snap = nullptr;
 
     for (int it = 0;; it++) {
         int probe = 0;

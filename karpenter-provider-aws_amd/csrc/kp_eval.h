@@ -109,6 +109,16 @@ struct ProbeTopo {
     int E, HG;
 };
 
+// Per-pod snapshot of the value-keyed topology groups that constrain the current pod's class (FFD kernel, LDS; filled by
+// topo_prefilter_setup in CC.tc order): counts only change when a pod commits, so every candidate evaluation of the pod
+// reads them here instead of from the global counters.
+struct TopoSnap {
+    int32_t cnt[KP_MAX_TOPO][64];   // domain counts (0 where the domain is not registered)
+    uint8_t rk[KP_MAX_TOPO][64];    // value-name rank of each domain (tie-break)
+    uint64_t known[KP_MAX_TOPO];    // registered domains
+    uint64_t podhas[KP_MAX_TOPO];   // domains the pod's own requirement for the key admits
+};
+
 // Tables shared by every evaluation of a kernel (LDS in ffd_kernel).
 struct EvalEnv {
     const int64_t* alloc;      // [lds_nstage][astride] staged allocatable of the first active axes
@@ -125,6 +135,7 @@ struct EvalEnv {
     const int32_t* rcap;       // ReservationManager capacity by reservation-id value id (FFD kernel LDS)
     int resv_on;               // run the reservation step of NodeClaim.Add
     const ProbeTopo* pt;       // consolidation probe topology counts (eval_wave<..., CT = true>)
+    const TopoSnap* snap;      // FFD kernel: the current pod's topology snapshot (null: read the global counters)
 };
 
 // Cooperative fill by all threads of the block; contains two __syncthreads().
@@ -407,7 +418,7 @@ __device__ inline void pt_hadd(const ProbeTopo& P, int hrow, int host, int lane)
 // CT: the counts are a consolidation probe's (pt).
 template <bool CT = false>
 __device__ __forceinline__ bool topo_narrow(const KpDev& d, const ClassCache& CC, WaveScratch& ws, int host, bool allow_wk,
-                                         int lane, const ProbeTopo* pt = nullptr) {
+                                         int lane, const ProbeTopo* pt = nullptr, const TopoSnap* snap = nullptr) {
     int nk = 0;
     int kidx[KP_MAX_TOPO];
     uint64_t kmask[KP_MAX_TOPO];
@@ -429,14 +440,24 @@ __device__ __forceinline__ bool topo_narrow(const KpDev& d, const ClassCache& CC
         }
         const int k = info.y;
         const bool valid = lane < CC.nval[ki];
-        if (CT) pt_row(d, *pt, g, lane);
-        const uint64_t known = ld_u64(CT ? &pt->known[g] : &d.tg_known[g]);
-        const bool kn = valid && ((known >> lane) & 1ull);
-        const int cnt = kn ? ld_i32(CT ? &pt->cnt[(size_t)g * 64 + lane] : &d.tg_cnt[(size_t)g * 64 + lane]) : 0;
-        const bool pod_has = valid && req_has(d, k, lane, CC.hdr[ki], CC.words + CC.wsoff[ki]);
+        bool kn, pod_has;
+        int cnt;
+        uint32_t rk;
+        if (!CT && snap) {
+            kn = valid && ((snap->known[e] >> lane) & 1ull);
+            cnt = kn ? snap->cnt[e][lane] : 0;
+            pod_has = valid && ((snap->podhas[e] >> lane) & 1ull);
+            rk = valid ? snap->rk[e][lane] : 0xFFu;
+        } else {
+            if (CT) pt_row(d, *pt, g, lane);
+            const uint64_t known = ld_u64(CT ? &pt->known[g] : &d.tg_known[g]);
+            kn = valid && ((known >> lane) & 1ull);
+            cnt = kn ? ld_i32(CT ? &pt->cnt[(size_t)g * 64 + lane] : &d.tg_cnt[(size_t)g * 64 + lane]) : 0;
+            pod_has = valid && req_has(d, k, lane, CC.hdr[ki], CC.words + CC.wsoff[ki]);
+            rk = valid ? d.vrank[(size_t)k * 64 + lane] : 0xFFu;
+        }
         const ReqHdr nh = ws.hdr[ki];
         const bool node_has = valid && (!(nh.flags & RF_DEF) || req_has(d, k, lane, nh, ws.words + CC.wsoff[ki]));
-        const uint32_t rk = valid ? d.vrank[(size_t)k * 64 + lane] : 0xFFu;
         uint64_t mask = 0;
         if (type == 0) {  // nextDomainTopologySpread: min count over the pod's domains, then the least-loaded node domain
             const uint64_t sup = ballot(kn && pod_has);
@@ -688,10 +709,15 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         if (kf & (KF_CAT_SINGLE | KF_CAT_MULTI)) kill = !op_notin_or_dne(req_op(O.flags, cnt));
         if (kf & KF_CAT_MULTI) {
             kmul = CC.kmulti[lane];
-            adm = 0;
             const int nv = CC.nval[lane] < 64 ? CC.nval[lane] : 64;
-            for (int v = 0; v < nv; v++)
-                if (req_has(d, k, v, O, ow)) adm |= 1ull << v;
+            const uint64_t vm = nv >= 64 ? ~0ull : ((1ull << nv) - 1ull);
+            if (!(O.flags & (RF_GT | RF_LT))) {  // Has(v) is the bit (complement: its absence)
+                adm = ((O.flags & RF_CMP) ? ~ow[0] : ow[0]) & vm;
+            } else {
+                adm = 0;
+                for (int v = 0; v < nv; v++)
+                    if (req_has(d, k, v, O, ow)) adm |= 1ull << v;
+            }
         }
     };
     if (lane < nck) {
@@ -735,7 +761,7 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
     }
     if (TOPO) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        if (!topo_narrow<CT>(d, CC, ws, a.host, a.compat, lane, E.pt)) {
+        if (!topo_narrow<CT>(d, CC, ws, a.host, a.compat, lane, E.pt, E.snap)) {
             EV_REJ(ST_REJ_TOPO);
             return false;
         }

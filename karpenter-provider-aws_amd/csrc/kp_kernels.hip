@@ -123,6 +123,7 @@ __global__ __launch_bounds__(64) void template_init_kernel(KpDev d) {
     __syncthreads();
     EvalEnv E;
     E.pt = nullptr;
+    E.snap = nullptr;
     E.alloc = nullptr;  // no requests: Fits({}, alloc) only needs non-negative allocatable (tmpl rows ∧ nonneg)
     E.astride = 0;
     E.avail = d.avail_zc;
@@ -194,6 +195,7 @@ struct FfdShared {
     int tp_lo[KP_MAX_TOPO], tp_hi[KP_MAX_TOPO];  // hostname group: the host's count must lie in [lo, hi]
     int tp_cmp[KP_MAX_TOPO];       // value-keyed: a complement (NotIn) NodeClaim requirement is not prefiltered
     uint64_t tp_elig[KP_MAX_TOPO]; // value-keyed: allowed domains ∩ the pod's domains
+    TopoSnap tsnap;                // the pod's value-keyed group counts for topo_narrow (EvalEnv.snap)
 };
 
 // wave 0, once per pod of a class with constraining topology groups: the per-group conditions topo_narrow applies,
@@ -217,10 +219,19 @@ __device__ inline void topo_prefilter_setup(const KpDev& d, FfdShared& S, int c,
             // the pod's domains: its requirement for the key, or every value when it does not constrain it
             const ReqHdr ph = d.cls_hdr[(size_t)c * d.K + k];
             const bool valid = lane < d.nval[k];
-            const bool pod_has =
-                valid && (!(ph.flags & RF_DEF) || req_has(d, k, lane, ph, d.cls_words + (size_t)c * d.DW + d.woff[k]));
-            const bool kn = valid && ((ld_u64(&d.tg_known[g]) >> lane) & 1ull);
+            const bool ph_has = valid && req_has(d, k, lane, ph, d.cls_words + (size_t)c * d.DW + d.woff[k]);
+            const bool pod_has = valid && (!(ph.flags & RF_DEF) || ph_has);
+            const uint64_t known = ld_u64(&d.tg_known[g]);
+            const bool kn = valid && ((known >> lane) & 1ull);
             const int cnt = kn ? ld_i32(&d.tg_cnt[(size_t)g * 64 + lane]) : 0;
+            // topo_narrow's view of the group for every candidate of this pod (TopoSnap)
+            S.tsnap.cnt[e][lane] = cnt;
+            S.tsnap.rk[e][lane] = valid ? d.vrank[(size_t)k * 64 + lane] : 0xFFu;
+            const uint64_t phm = ballot(ph_has);
+            if (lane == 0) {
+                S.tsnap.known[e] = known;
+                S.tsnap.podhas[e] = phm;
+            }
             if (type == 0) {
                 const uint64_t sup = ballot(kn && pod_has);
                 int mn = wave_min_i32((kn && pod_has) ? cnt : INT32_MAX);
@@ -589,6 +600,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
     __syncthreads();
     EvalEnv E;
     E.pt = nullptr;
+    E.snap = &S.tsnap;  // filled per pod by topo_prefilter_setup before any topology evaluation of it
     E.alloc = sAlloc;
     E.astride = TP;
     E.avail = sAvail;
