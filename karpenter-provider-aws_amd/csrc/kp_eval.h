@@ -688,10 +688,7 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
     const int TW = d.TW, T = d.T;
     long long _t0 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
     if (a.prof && lane == 0) atomicAdd((unsigned long long*)&a.prof[ST_EV_CALLS - ST_EV_REQ], 1ull);
-    if (a.compat && !((CC.tol >> a.tmpl) & 1u)) {
-        if (lane == 0) ws.memo_ok = 1;  // taints are fixed: the rejection holds for the shape
-        return false;
-    }
+    if (a.compat && !((CC.tol >> a.tmpl) & 1u)) return false;
     const int nck = CC.nck;
 
     // ---- requirements: Compatible + Add (lane = class key) ----

@@ -195,7 +195,8 @@ struct FfdShared {
     int tp_lo[KP_MAX_TOPO], tp_hi[KP_MAX_TOPO];  // hostname group: the host's count must lie in [lo, hi]
     int tp_cmp[KP_MAX_TOPO];       // value-keyed: a complement (NotIn) NodeClaim requirement is not prefiltered
     uint64_t tp_elig[KP_MAX_TOPO]; // value-keyed: allowed domains ∩ the pod's domains
-    TopoSnap tsnap;                // the pod's value-keyed group counts for topo_narrow (EvalEnv.snap)
+    TopoSnap* tsnap;               // topology solves: the pod's value-keyed group counts for topo_narrow (dynamic LDS,
+                                   // EvalEnv.snap); null otherwise, so other solves keep that LDS for quick-accept rows
 };
 
 // wave 0, once per pod of a class with constraining topology groups: the per-group conditions topo_narrow applies,
@@ -225,12 +226,13 @@ __device__ inline void topo_prefilter_setup(const KpDev& d, FfdShared& S, int c,
             const bool kn = valid && ((known >> lane) & 1ull);
             const int cnt = kn ? ld_i32(&d.tg_cnt[(size_t)g * 64 + lane]) : 0;
             // topo_narrow's view of the group for every candidate of this pod (TopoSnap)
-            S.tsnap.cnt[e][lane] = cnt;
-            S.tsnap.rk[e][lane] = valid ? d.vrank[(size_t)k * 64 + lane] : 0xFFu;
+            TopoSnap& Z = *S.tsnap;
+            Z.cnt[e][lane] = cnt;
+            Z.rk[e][lane] = valid ? d.vrank[(size_t)k * 64 + lane] : 0xFFu;
             const uint64_t phm = ballot(ph_has);
             if (lane == 0) {
-                S.tsnap.known[e] = known;
-                S.tsnap.podhas[e] = phm;
+                Z.known[e] = known;
+                Z.podhas[e] = phm;
             }
             if (type == 0) {
                 const uint64_t sup = ballot(kn && pod_has);
@@ -279,8 +281,8 @@ __device__ __forceinline__ bool topo_prefilter_pass(const KpDev& d, const FfdSha
 
 // wave 0: the first slice position in [start, N) that has not rejected the shape and passes the topology prefilter
 // (N if none).  Four 64-position chunks per round so the prefilter's global loads of 256 NodeClaims overlap.
-__device__ inline int topo_scan(const KpDev& d, const FfdShared& S, const uint32_t* skey, const uint16_t* sord,
-                                const uint8_t* stmpl, int N, int start, int lane) {
+__device__ inline int topo_scan(const KpDev& d, const FfdShared& S, const uint32_t* skey, const uint16_t* sord, int N,
+                                int start, int lane) {
     for (int base = start; base < N; base += 256) {
         bool ok[4];
         int nc[4];
@@ -289,7 +291,6 @@ __device__ inline int topo_scan(const KpDev& d, const FfdShared& S, const uint32
             const int p = base + u * 64 + lane;
             ok[u] = p < N && !(skey[p] >> 31);
             nc[u] = ok[u] ? (int)sord[p] : 0;
-            ok[u] = ok[u] && ((S.cur_tol >> stmpl[nc[u]]) & 1u);  // NodeClaim.Add's toleration check
         }
         for (int e = 0; e < S.tp_n; e++) {
             const int k = S.tp_k[e];
@@ -371,8 +372,8 @@ __device__ inline void topo_record_quick(const KpDev& d, int c, int nc, int tmpl
 
 // wave 0: collect up to KP_NWAVES slice positions >= start whose NodeClaim has not rejected the current shape (and
 // passes the topology prefilter of the current pod)
-__device__ inline void collect_candidates(const KpDev& d, FfdShared& S, const uint32_t* key, const uint16_t* ord,
-                                          const uint8_t* stmpl, uint32_t tol, int N, int start, int buf, int lane) {
+__device__ inline void collect_candidates(const KpDev& d, FfdShared& S, const uint32_t* key, const uint16_t* ord, int N,
+                                          int start, int buf, int lane) {
     int cnt = 0, pos = start, next = N;
     // topology pods: at most d.topo_cands candidates per round (the first prefilter survivor usually accepts; fewer waves
     // evaluating leaves each its own SIMD)
@@ -380,9 +381,6 @@ __device__ inline void collect_candidates(const KpDev& d, FfdShared& S, const ui
     while (pos < N) {
         const int p = pos + lane;
         bool c = p < N && !(key[p] >> 31);
-        // NodeClaim.Add's first check (the pod tolerates the NodeClaim's template taints) is decided here: a candidate
-        // that fails it would be rejected before any other stage
-        if (c) c = (tol >> stmpl[ord[p]]) & 1u;
         if (S.tp_n && c) c = topo_prefilter_pass(d, S, ord[p]);
         const uint64_t m0 = __ballot(c);
         if (S.tp_n && m0 && cnt + __popcll(m0) < L) {
@@ -573,6 +571,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
     if (tid == 0) {
         S.N = 0;
         S.tp_n = 0;
+        S.tsnap = d.G > 0 ? reinterpret_cast<TopoSnap*>(smem + d.off_tsnap) : nullptr;
         S.topo_pod = 0;
         S.topo_quick = 0;
         S.qhead = 0;
@@ -600,7 +599,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
     __syncthreads();
     EvalEnv E;
     E.pt = nullptr;
-    E.snap = &S.tsnap;  // filled per pod by topo_prefilter_setup before any topology evaluation of it
+    E.snap = d.G > 0 ? reinterpret_cast<TopoSnap*>(smem + d.off_tsnap) : nullptr;  // filled per pod by topo_prefilter_setup
     E.alloc = sAlloc;
     E.astride = TP;
     E.avail = sAvail;
@@ -1120,7 +1119,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                     S.cls_fill = S.CC.cls != c;  // decided before the barrier: fill_class_cache rewrites CC.cls
                     S.topo_pod = 0;
                 }
-                collect_candidates(d, S, skey, sord, stmpl, tl, N, f, 0, lane);
+                collect_candidates(d, S, skey, sord, N, f, 0, lane);
                 break;
             }
             win_flush();
@@ -1217,7 +1216,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 if (cfl & CF_TOPO_CONS) topo_prefilter_setup(d, S, c, lane);
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 const long long t1 = prof_clock(d);
-                const int f = topo_scan(d, S, skey, sord, stmpl, N, S.scan_start, lane);
+                const int f = topo_scan(d, S, skey, sord, N, S.scan_start, lane);
                 const long long t2 = prof_clock(d);
                 bool quick = false;
                 if (f < N && (cfl & CF_TOPO_QREC) && A > 0) {
@@ -1243,7 +1242,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     }
                 }
-                if (!quick) collect_candidates(d, S, skey, sord, stmpl, S.cur_tol, N, f, 0, lane);
+                if (!quick) collect_candidates(d, S, skey, sord, N, f, 0, lane);
                 if (lane == 0) {
                     S.topo_quick = quick;
                     if (d.profile) {
@@ -1335,7 +1334,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 }
             if (tid == 0) S.st[ST_NC_EVALS] += nc_;
             if (win >= 0 || S.scan_done[b]) break;
-            if (wave == 0) collect_candidates(d, S, skey, sord, stmpl, S.cur_tol, S.N, S.scan_next[b], b ^ 1, lane);
+            if (wave == 0) collect_candidates(d, S, skey, sord, S.N, S.scan_next[b], b ^ 1, lane);
             __syncthreads();
             round++;
         }
@@ -1760,6 +1759,8 @@ bool kp_ffd_plan_lds(KpDev& d, int max_bytes) {
     if (d.multi16) off = al(off + 2 * (size_t)d.n_multi * tp);
     d.off_ro = (int)off;
     if (d.ro) off = al(off + sizeof(ResvTab) + 4 * 64);
+    d.off_tsnap = (int)off;
+    if (d.G > 0) off = al(off + sizeof(TopoSnap));
     d.off_hr = (int)off;
     if ((int)off > max_bytes) return false;
     d.lds_A = d.n_active <= KP_LDS_AXES ? d.n_active : 0;

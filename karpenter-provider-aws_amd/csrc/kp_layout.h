@@ -231,7 +231,7 @@ struct KpDev {
     int32_t lds_nstage;              // allocatable axes staged in LDS
     int32_t lds_A;                   // quick-accept axes (= n_active when n_active <= KP_LDS_AXES, else 0)
     int32_t lds_nq;                  // NodeClaims with a quick-accept headroom row (ids < lds_nq)
-    int32_t off_key, off_ord, off_last, off_tmpl, off_alloc, off_avail, off_multi, off_ro, off_hr;
+    int32_t off_key, off_ord, off_last, off_tmpl, off_alloc, off_avail, off_multi, off_ro, off_tsnap, off_hr;
     int32_t lds_bytes;
     int32_t qshift[KP_LDS_AXES];     // headroom scale per quick axis: value >> qshift fits 30 bits
 
