@@ -446,7 +446,9 @@ struct kp_ctx {
     // consolidation probes
     DBuf<int32_t> d_retry, d_rank, d_cand_i, d_cand_off, d_cand_pods, d_pending, d_ring, d_ring_last, d_next, d_pnode;
     DBuf<double> d_cand_price;
-    DBuf<int64_t> d_cand_cap, d_delta, d_alloc_act, d_cons_stats, d_cmax0;
+    DBuf<int64_t> d_cand_cap, d_delta, d_alloc_act, d_cons_stats, d_cmax0, d_alloc_stage;
+    int nc_cap = KP_NC_FIRST;                // in-flight NodeClaim capacity of the next solve prepare (grown by kp_solve)
+    bool nc_overflow = false;                // the last fetch found the solve out of in-flight NodeClaim capacity
     DBuf<uint64_t> d_pend_bits, d_pbits;
     DBuf<uint64_t> d_init;
     DBuf<kp_probe_result> d_probe_out;
@@ -1851,7 +1853,8 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     HIPCHK(c->d_sort_fields.upload(fields, s));
     HIPCHK(c->d_empty_hdr.upload(empty_hdr, s));
     HIPCHK(c->d_empty_words.upload(empty_words, s));
-    const int NCcap = std::min(KP_MAX_NC, std::max(P, 1));
+    // in-flight NodeClaim capacity: KP_NC_FIRST, or up to KP_MAX_NC after a solve of this ctx overflowed it (kp_solve)
+    const int NCcap = std::min(std::min(c->nc_cap, KP_MAX_NC), std::max(P, 1));
     HIPCHK(c->d_nc_hdr.ensure((size_t)NCcap * K));
     HIPCHK(c->d_nc_words.ensure((size_t)NCcap * DW));
     HIPCHK(c->d_nc_opts.ensure((size_t)NCcap * TW));
@@ -1892,7 +1895,9 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         std::vector<uint64_t> tknown0(G1, 0);
         std::vector<int32_t> tcoff(C + 1, 0), tcl, troff(C + 1, 0), trl;
         std::vector<uint8_t> vrank((size_t)K * 64, 0xFF);
-        const int HN = E + NCcap;
+        // hostname rows: existing nodes, then NodeClaim ids 0 .. NCcap, the last a spare that stays 0 (a template
+        // evaluation for a NodeClaim at capacity reads it; the capacity check then reports the overflow)
+        const int HN = E + NCcap + 1;
         std::vector<int32_t> hc0((size_t)std::max(1, th.n_host) * HN, 0);
         if (G > 0) {
             auto hreq_has = [&](const HReq& q, int v) {
@@ -2207,6 +2212,15 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.rcap0 = c->d_rcap0.p;
     d.nc_held = c->d_nc_held.p;
     d.nc_rlive = c->d_nc_rlive.p;
+    d.alloc_act = nullptr;
+    if (NCcap > KP_NC_FIRST) {  // large slice plan: the staged axes' allocatable table in HBM ([axes][TP], TP = 64-padded T)
+        const int TP = (T + 63) / 64 * 64, ns = std::min(d.n_active, KP_LDS_AXES);
+        std::vector<int64_t> act((size_t)std::max(ns, 1) * TP, 0);
+        for (int ai = 0; ai < ns; ai++)
+            for (int t = 0; t < T; t++) act[(size_t)ai * TP + t] = c->alloc_rt[(size_t)d.active_axes[ai] * T + t];
+        HIPCHK(c->d_alloc_stage.upload(act, s));
+        d.alloc_act = c->d_alloc_stage.p;
+    }
     if (!kp_ffd_plan_lds(d, KP_LDS_BYTES)) return fail(ctx, KP_E_UNSUPPORTED, "FFD kernel LDS plan exceeds 160 KB");
     c->P = P;
     c->C = C;
@@ -2308,7 +2322,8 @@ extern "C" kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out) {
     HIPCHK(hipMemcpyAsync(&err, c->d_err.p, sizeof err, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(st, c->d_stats.p, sizeof st, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    if (err == 1) return fail(ctx, KP_E_UNSUPPORTED, "in-flight NodeClaim capacity (KP_MAX_NC) exceeded");
+    c->nc_overflow = err == 1;
+    if (err == 1) return fail(ctx, KP_E_UNSUPPORTED, "in-flight NodeClaim capacity exceeded");
     if (err) return fail(ctx, KP_E_STATE, "device solve loop exceeded its pop bound (internal error)");
     const int P = c->P, M = c->M;
     std::vector<int32_t> npods(N), spos(N), nopts(N), valid(N), ntypes(N), tmpl(N), types((size_t)N * M), pres(P), pord(P);
@@ -2384,11 +2399,21 @@ extern "C" kp_status kp_last_kernel_times(kp_ctx* ctx, double* ms, int32_t n) {
 }
 
 extern "C" kp_status kp_solve(kp_ctx* ctx, const kp_solve_input* in, kp_solve_output* out) {
-    kp_status st = kp_solve_prepare(ctx, in);
-    if (st != KP_OK) return st;
-    st = kp_solve_execute(ctx);
-    if (st != KP_OK) return st;
-    return kp_solve_fetch(ctx, out);
+    for (;;) {
+        kp_status st = kp_solve_prepare(ctx, in);
+        if (st != KP_OK) return st;
+        st = kp_solve_execute(ctx);
+        if (st != KP_OK) return st;
+        st = kp_solve_fetch(ctx, out);
+        // more in-flight NodeClaims than the first plan holds (e.g. a large hostname anti-affinity Deployment): prepare
+        // again with room for up to KP_MAX_NC (the ctx keeps the larger capacity for its later solves)
+        const int want = std::min(KP_MAX_NC, std::max(in->pods.n_pods, 1));
+        if (st == KP_E_UNSUPPORTED && ctx->nc_overflow && ctx->nc_cap < want) {
+            ctx->nc_cap = want;
+            continue;
+        }
+        return st;
+    }
 }
 
 static std::string reqs_text(const kp_ctx* ctx, const ReqHdr* h, const uint64_t* w);

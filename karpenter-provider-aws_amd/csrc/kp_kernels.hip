@@ -529,7 +529,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
     const int T = d.T, TW = d.TW, K = d.K, R = d.R, P = d.P;
     const int TP = d.lds_tpad, NQ = d.lds_nq, A = d.lds_A, NCMAX = d.lds_ncmax;
     // ---- stage the type tables in LDS ----
-    for (int i = tid; i < d.lds_nstage * TP; i += nthr) {
+    for (int i = tid; i < (d.alloc_global ? 0 : d.lds_nstage * TP); i += nthr) {
         const int ai = i / TP, t = i % TP;
         sAlloc[i] = t < T ? d.alloc[(size_t)act_axis(d, ai) * T + t] : 0;
     }
@@ -600,7 +600,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
     EvalEnv E;
     E.pt = nullptr;
     E.snap = d.G > 0 ? reinterpret_cast<TopoSnap*>(smem + d.off_tsnap) : nullptr;  // filled per pod by topo_prefilter_setup
-    E.alloc = sAlloc;
+    E.alloc = d.alloc_global ? d.alloc_act : sAlloc;
     E.astride = TP;
     E.avail = sAvail;
     E.multi16 = d.multi16 ? sMulti : nullptr;
@@ -1738,7 +1738,20 @@ size_t kp_ffd_shared_bytes() { return sizeof(FfdShared); }
 bool kp_ffd_plan_lds(KpDev& d, int max_bytes) {
     auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
     size_t off = al(sizeof(FfdShared));
-    const int ncmax = d.NCcap < KP_MAX_NC ? d.NCcap : KP_MAX_NC;
+    // a solve is planned for KP_NC_FIRST in-flight NodeClaims with the allocatable table staged in LDS and the rest of
+    // LDS as quick-accept rows; a solve that overflowed that is re-planned (NCcap above KP_NC_FIRST) with the table read
+    // from HBM and as many slice entries as LDS holds (9 B per NodeClaim)
+    int ncmax = d.NCcap < KP_MAX_NC ? d.NCcap : KP_MAX_NC;
+    d.alloc_global = ncmax > KP_NC_FIRST && d.alloc_act != nullptr;
+    if (d.alloc_global) {
+        const int tp0 = (d.T + 63) / 64 * 64;
+        const int nst = d.n_active < KP_LDS_AXES ? d.n_active : KP_LDS_AXES;
+        size_t fixed = off + 8 * (size_t)tp0 + (d.multi16 ? 2 * (size_t)d.n_multi * tp0 : 0) +
+                       (d.ro ? sizeof(ResvTab) + 4 * 64 : 0) + (d.G > 0 ? sizeof(TopoSnap) : 0) + 256;
+        (void)nst;
+        const long room = ((long)max_bytes - (long)fixed) / 9;
+        if (room < ncmax) ncmax = room > 0 ? (int)room : 0;
+    }
     d.lds_ncmax = ncmax;
     d.off_key = (int)off;
     off = al(off + 4 * (size_t)ncmax);
@@ -1752,7 +1765,7 @@ bool kp_ffd_plan_lds(KpDev& d, int max_bytes) {
     d.lds_tpad = tp;
     d.lds_nstage = d.n_active < KP_LDS_AXES ? d.n_active : KP_LDS_AXES;
     d.off_alloc = (int)off;
-    off = al(off + 8 * (size_t)d.lds_nstage * tp);
+    if (!d.alloc_global) off = al(off + 8 * (size_t)d.lds_nstage * tp);
     d.off_avail = (int)off;
     off = al(off + 8 * (size_t)tp);
     d.off_multi = (int)off;

@@ -16,7 +16,8 @@
 
 #define KP_MAX_TYPES 1024            // TW <= 16
 #define KP_TW_MAX (KP_MAX_TYPES / 64)
-#define KP_MAX_NC 4096               // in-flight NodeClaims per solve (LDS order/key arrays)
+#define KP_MAX_NC 65535              // in-flight NodeClaims per solve (u16 ids in the LDS slice arrays)
+#define KP_NC_FIRST 4096             // slice capacity a solve is first planned with (kp_solve grows it on overflow)
 #define KP_MAX_KEYS 96               // label keys per solve
 #define KP_MAX_CLASS_KEYS 32         // label keys constrained by one pod class / template
 #define KP_MAX_SLOTS 64              // zone slots × capacity-type slots
@@ -231,6 +232,8 @@ struct KpDev {
     int32_t lds_nstage;              // allocatable axes staged in LDS
     int32_t lds_A;                   // quick-accept axes (= n_active when n_active <= KP_LDS_AXES, else 0)
     int32_t lds_nq;                  // NodeClaims with a quick-accept headroom row (ids < lds_nq)
+    int32_t alloc_global;            // large slice plans: allocatable read from alloc_act in HBM, not staged in LDS
+    const int64_t* alloc_act;        // [lds_nstage][lds_tpad] allocatable of the staged axes (alloc_global)
     int32_t off_key, off_ord, off_last, off_tmpl, off_alloc, off_avail, off_multi, off_ro, off_tsnap, off_hr;
     int32_t lds_bytes;
     int32_t qshift[KP_LDS_AXES];     // headroom scale per quick axis: value >> qshift fits 30 bits

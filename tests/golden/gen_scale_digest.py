@@ -18,10 +18,16 @@ sys.path[:0] = [os.path.join(ROOT, "karpenter-provider-aws_amd"), os.path.join(R
 from kpsim import catalog, synth  # noqa: E402
 import parity  # noqa: E402
 
+def node_dense(cat, n_pods):
+    import test_topology_cpu as TC
+    return TC.node_dense(cat, n_pods)
+
+
 CASES = {
     "config2_200k": ("config2", dict(n_pods=200_000)),  # BASELINE configs[4]'s pod count over the config-2 pod mix
     "config3_50k": ("config3", dict(n_pods=50_000)),    # BASELINE configs[2]: topology + five weighted NodePools
     "config5_200k": ("config5", dict(n_pods=200_000)),  # BASELINE configs[4]: reserved offerings, ODCR-first NodePools
+    "node_dense_10k": (node_dense, dict(n_pods=10_000)),  # 10k in-flight NodeClaims
 }
 
 
@@ -34,7 +40,10 @@ def main():
             out = json.load(f)
     for name in sys.argv[1:] or list(CASES):
         gen, kw = CASES[name]
-        prob = synth.config5(golden=cat, **kw) if gen == "config5" else getattr(synth, gen)(catalog=cat, **kw)
+        if callable(gen):
+            prob = gen(cat, **kw)
+        else:
+            prob = synth.config5(golden=cat, **kw) if gen == "config5" else getattr(synth, gen)(catalog=cat, **kw)
         t = time.time()
         out[name] = dict(kw, **parity.result_digest(parity.run_oracle(prob)))
         print(name, "%.1f s" % (time.time() - t), out[name]["n_nodeclaims"])

@@ -161,3 +161,19 @@ def test_fuzz_topology_existing(ctx, golden, seed):
     sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=160, replace=False))]
     same(ctx, fuzzgen.fuzz_topology_existing_problem(sub, seed, n_pods=int(rng.integers(50, 300)),
                                                      n_existing=int(rng.integers(4, 40))))
+
+
+def test_node_dense_10k_beyond_first_slice_plan(golden):
+    """10,000-pod node-dense Deployment (hostname anti-affinity): 10,000 in-flight NodeClaims, beyond the first slice
+    plan (KP_NC_FIRST = 4096).  kp_solve re-plans with room for them (allocatable read from HBM); every output field
+    equals the oracle's committed digest (tests/golden/gen_scale_digest.py node_dense_10k; ~1 min of oracle time)."""
+    from kpsim import native
+    with open(os.path.join(os.path.dirname(__file__), "golden", "scale_digests.json")) as f:
+        want = json.load(f)["node_dense_10k"]
+    c = native.Context(0)  # its own ctx: the grown capacity stays with it
+    try:
+        dev = parity.run_device(c, TC.node_dense(golden, want["n_pods"]))
+        assert dev[0].n_nodeclaims == 10_000 and (dev[0].nodeclaim_n_pods == 1).all()
+        assert parity.result_digest(dev) == {k: v for k, v in want.items() if k != "n_pods"}
+    finally:
+        c.close()

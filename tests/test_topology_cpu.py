@@ -196,3 +196,12 @@ def test_config3_small_runs(golden):
         placed = np.nonzero((cls == c) & (r.pod_result >= 0))[0]
         if any(t.key == HOSTNAME for t in pc.topology):
             assert len(set(r.pod_result[placed].tolist())) == len(placed)
+
+
+def node_dense(cat, n_pods):
+    """The scale suite's node-dense Deployment (test/suites/scale/provisioning_test.go:76-136: hostname anti-affinity on
+    its own label) at n_pods: one NodeClaim per pod.  At 10k it exceeds the FFD kernel's first slice plan (KP_NC_FIRST);
+    tests/golden/gen_scale_digest.py node_dense_10k holds the oracle's digest of it."""
+    lab = {"app": "node-dense"}
+    pc, pods = deployment(n_pods, lab, [model.TopologyTerm("anti", model.HOSTNAME, sel(lab))])
+    return model.Problem(cat, [e2e_nodepool(None)], [pc], pods)
