@@ -246,6 +246,11 @@ struct DBuf {  // device buffer, grow-only; freed by its destructor (the owning 
         if (e != hipSuccess || v.empty()) return e;
         return hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
     }
+    hipError_t upload(const T* v, size_t count, hipStream_t s) {
+        hipError_t e = ensure(count);
+        if (e != hipSuccess || count == 0) return e;
+        return hipMemcpyAsync(p, v, count * sizeof(T), hipMemcpyHostToDevice, s);
+    }
     void release() {
         if (p) hipFree(p);
         p = nullptr;
@@ -447,6 +452,9 @@ struct kp_ctx {
     DBuf<int32_t> d_retry, d_rank, d_cand_i, d_cand_off, d_cand_pods, d_pending, d_ring, d_ring_last, d_next, d_pnode;
     DBuf<double> d_cand_price;
     DBuf<int64_t> d_cand_cap, d_delta, d_alloc_act, d_cons_stats, d_cmax0, d_alloc_stage;
+    // kp_solve_prepare's per-pod host arrays, kept across calls
+    std::vector<int32_t> h_uid_p;
+    std::vector<uint64_t> h_uid_k;
     int nc_cap = KP_NC_FIRST;                // in-flight NodeClaim capacity of the next solve prepare (grown by kp_solve)
     bool nc_overflow = false;                // the last fetch found the solve out of in-flight NodeClaim capacity
     DBuf<uint64_t> d_pend_bits, d_pbits;
@@ -503,6 +511,8 @@ struct kp_ctx {
     PinBuf<KlMinKey> p_l_mins[2];
     PinBuf<uint64_t> p_l_words[2], p_l_over;
     PinBuf<int32_t> p_l_hdr, p_l_types;
+    PinBuf<int32_t> p_pcls, p_pshape;        // kp_solve_prepare's per-pod arrays (pinned: DMA uploads)
+    PinBuf<int64_t> p_preq, p_fields;
     WorkerPool pool;                         // host threads of kp_launch_select's batch work
     double launch_ms[6] = {};                // Σ launch kernel, whole call; host phases: encode, merge + upload,
                                              // waits for the downloads, result expansion
@@ -1421,7 +1431,18 @@ static kp_status topo_build(kp_ctx* c, const kp_solve_input* in, const std::vect
     return KP_OK;
 }
 
+// KPSIM_PREP_TIMES (diagnostics): host prepare phase times to stderr
+static thread_local std::chrono::steady_clock::time_point g_prep_t;
+#define PREP_MARK(i)                                                                                          \
+    do {                                                                                                      \
+        if (getenv("KPSIM_PREP_TIMES")) {                                                                     \
+            const auto _n = std::chrono::steady_clock::now();                                                 \
+            fprintf(stderr, "[prep] mark %d: %.3f ms\n", i, std::chrono::duration<double>(_n - g_prep_t).count() * 1e3); \
+            g_prep_t = _n;                                                                                    \
+        }                                                                                                     \
+    } while (0)
 extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try {
+    g_prep_t = std::chrono::steady_clock::now();
     if (!ctx || !in) return KP_E_INVALID;
     ctx->cons_prep_valid = false;
     if (!ctx->have_catalog) return fail(ctx, KP_E_STATE, "kp_solve before kp_catalog_upload");
@@ -1449,6 +1470,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     }
     in = &c->pref.in;  // from here on: the expanded classes (stage 0 of input class i is class i)
     const int T = c->T, TW = c->TW, R = c->R, P = in->pods.n_pods, C = in->n_classes;
+    PREP_MARK(0);
     // ---- dictionaries: catalog ∪ solve strings ----
     c->sol = c->cat;
     std::vector<std::map<int, HReq>> creq(C);
@@ -1557,6 +1579,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
             return fail(ctx, KP_E_UNSUPPORTED, "topology key " + c->sol.keys[g.key].name +
                                                    ": single-valued instance-type labels or > 64 values are not supported");
     }
+    PREP_MARK(1);
     // ---- class digests: pod classes then templates ----
     const int CT = C + NT;
     std::vector<ReqHdr> chdr((size_t)CT * K);
@@ -1698,9 +1721,19 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
             if (all) extol[(size_t)i * EW + j / 64] |= 1ull << (j % 64);
         }
     }
+    PREP_MARK(2);
     // ---- pods ----
-    std::vector<int32_t> pcls(P), pshape(P);
-    std::vector<int64_t> preq((size_t)P * R), fields((size_t)P * 4);
+    // per-pod arrays: pinned ctx buffers kept across calls (no allocation or page faults per solve, DMA uploads); the
+    // previous solve's uploads from them have finished before they are rewritten
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(c->p_pcls.ensure(std::max(P, 1)));
+    HIPCHK(c->p_pshape.ensure(std::max(P, 1)));
+    HIPCHK(c->p_preq.ensure((size_t)std::max(P, 1) * R));
+    HIPCHK(c->p_fields.ensure((size_t)std::max(P, 1) * 4));
+    int32_t* const pcls = c->p_pcls.p;
+    int32_t* const pshape = c->p_pshape.p;
+    int64_t* const preq = c->p_preq.p;
+    int64_t* const fields = c->p_fields.p;
     int cpu_axis = -1, mem_axis = -1;
     for (int r = 0; r < R; r++) {
         if (c->resource_names[r] == "cpu") cpu_axis = r;
@@ -1717,25 +1750,43 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         bool operator<(const ShapeKey& o) const { return cls != o.cls ? cls < o.cls : req < o.req; }
     };
     std::map<ShapeKey, int> shapes;
-    std::unordered_map<uint64_t, int> uidseen;
-    uidseen.reserve((size_t)P * 2);
+    // NewQueue's UID tie-break enters as the UID's first 8 bytes; distinct UIDs sharing them are detected with an
+    // open-addressing table over those prefixes (ctx scratch, cleared per call)
+    size_t HT = 1024;
+    while (HT < (size_t)P * 2) HT <<= 1;
+    std::vector<uint64_t>& uid_k = c->h_uid_k;
+    std::vector<int32_t>& uid_p = c->h_uid_p;
+    if (uid_k.size() < HT) {
+        uid_k.resize(HT);
+        uid_p.resize(HT);
+    }
+    std::fill(uid_p.begin(), uid_p.begin() + HT, -1);
     bool uid_collision = false;
     const kp_pods_view& pv = in->pods;
     // kp_pods_view.uids is optional (NULL, or NULL entries): a missing UID is the empty string
     auto uid_of = [&](int p) -> const char* { return pv.uids && pv.uids[p] ? pv.uids[p] : ""; };
+    int prev_shape = -1;
     for (int p = 0; p < P; p++) {
         const int cl = pv.class_id[p];
         if (cl < 0 || cl >= C) return fail(ctx, KP_E_INVALID, "pod class out of range");
         pcls[p] = cl;
-        ShapeKey sk{cl, std::vector<int64_t>(pv.requests + (size_t)p * R, pv.requests + (size_t)(p + 1) * R)};
+        const int64_t* rq = pv.requests + (size_t)p * R;
+        int64_t* dst = &preq[(size_t)p * R];
         for (int r = 0; r < R; r++) {
-            preq[(size_t)p * R + r] = sk.req[r];
-            if (sk.req[r] != 0) active[r] = 1;
-            if (sk.req[r] < 0) return fail(ctx, KP_E_INVALID, "negative request");
+            dst[r] = rq[r];
+            if (rq[r] != 0) active[r] = 1;
+            if (rq[r] < 0) return fail(ctx, KP_E_INVALID, "negative request");
         }
-        auto it = shapes.find(sk);
-        if (it == shapes.end()) it = shapes.emplace(std::move(sk), (int)shapes.size()).first;
-        pshape[p] = it->second;
+        // shapes are numbered in order of first appearance; a pod with the previous pod's class and requests (the pods
+        // of one Deployment, typically) reuses its shape without a lookup
+        if (p > 0 && cl == pcls[p - 1] && memcmp(dst, dst - R, sizeof(int64_t) * R) == 0) {
+            pshape[p] = prev_shape;
+        } else {
+            ShapeKey sk{cl, std::vector<int64_t>(rq, rq + R)};
+            auto it = shapes.find(sk);
+            if (it == shapes.end()) it = shapes.emplace(std::move(sk), (int)shapes.size()).first;
+            pshape[p] = prev_shape = it->second;
+        }
         // NewQueue key: cpu desc, memory desc, creation asc, UID asc.  The UID enters as its first 8 bytes
         // (big-endian, order-preserving); if two distinct UIDs share that prefix, exact string ranks are used.
         const char* u = uid_of(p);
@@ -1745,12 +1796,24 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
             uk <<= 8;
             if (*q) uk |= (uint8_t)*q++;
         }
-        fields[(size_t)p * 4 + 0] = preq[(size_t)p * R + cpu_axis];
-        fields[(size_t)p * 4 + 1] = preq[(size_t)p * R + mem_axis];
+        fields[(size_t)p * 4 + 0] = dst[cpu_axis];
+        fields[(size_t)p * 4 + 1] = dst[mem_axis];
         fields[(size_t)p * 4 + 2] = pv.creation_ns ? pv.creation_ns[p] : 0;
         fields[(size_t)p * 4 + 3] = (int64_t)(uk ^ 0x8000000000000000ull);
-        auto ins = uidseen.emplace(uk, p);
-        if (!ins.second && strcmp(uid_of(ins.first->second), u) != 0) uid_collision = true;
+        if (!uid_collision) {
+            size_t h = (size_t)((uk * 0x9E3779B97F4A7C15ull) >> 20) & (HT - 1);
+            for (;; h = (h + 1) & (HT - 1)) {
+                if (uid_p[h] < 0) {
+                    uid_k[h] = uk;
+                    uid_p[h] = p;
+                    break;
+                }
+                if (uid_k[h] == uk) {
+                    if (strcmp(uid_of(uid_p[h]), u) != 0) uid_collision = true;
+                    break;
+                }
+            }
+        }
     }
     if (uid_collision) {
         std::vector<int> idx(P);
@@ -1762,6 +1825,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
             fields[(size_t)idx[i] * 4 + 3] = (int64_t)((uint64_t)rank ^ 0x8000000000000000ull);
         }
     }
+    PREP_MARK(3);
     // relaxation stages of every shape: shape_next[s] = the shape of (relax_next[class of s], the same requests)
     std::vector<int32_t> shape_next;
     if (!c->pref.relax_next.empty()) {
@@ -1787,6 +1851,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.n_active = 0;
     for (int r = 0; r < R; r++)
         if (active[r]) d.active_axes[d.n_active++] = r;
+    PREP_MARK(4);
     // ---- device buffers ----
     hipStream_t s = c->stream;
     std::vector<ReqHdr> empty_hdr(K);
@@ -1840,17 +1905,17 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     HIPCHK(c->d_ex_static.ensure(std::max(E, 1)));
     HIPCHK(c->d_ex_tol.upload(extol, s));
     HIPCHK(c->d_XT.ensure(extol.size()));
-    HIPCHK(c->d_pod_cls.upload(pcls, s));
-    HIPCHK(c->d_pod_shape.upload(pshape, s));
+    HIPCHK(c->d_pod_cls.upload(pcls, P, s));
+    HIPCHK(c->d_pod_shape.upload(pshape, P, s));
     if (!shape_next.empty()) {
-        HIPCHK(c->d_pod_cls0.upload(pcls, s));
-        HIPCHK(c->d_pod_shape0.upload(pshape, s));
+        HIPCHK(c->d_pod_cls0.upload(pcls, P, s));
+        HIPCHK(c->d_pod_shape0.upload(pshape, P, s));
         HIPCHK(c->d_relax_next.upload(c->pref.relax_next, s));
         HIPCHK(c->d_shape_next.upload(shape_next, s));
         HIPCHK(c->d_last_ep.ensure(std::max(P, 1)));
     }
-    HIPCHK(c->d_pod_req.upload(preq, s));
-    HIPCHK(c->d_sort_fields.upload(fields, s));
+    HIPCHK(c->d_pod_req.upload(preq, (size_t)P * R, s));
+    HIPCHK(c->d_sort_fields.upload(fields, (size_t)P * 4, s));
     HIPCHK(c->d_empty_hdr.upload(empty_hdr, s));
     HIPCHK(c->d_empty_words.upload(empty_words, s));
     // in-flight NodeClaim capacity: KP_NC_FIRST, or up to KP_MAX_NC after a solve of this ctx overflowed it (kp_solve)
