@@ -306,6 +306,10 @@ kp_status kp_catalog_patch_avail(kp_ctx* ctx, const uint8_t* available, int32_t 
 /* price delta: price of offering rows idx[i] becomes price[i]. */
 kp_status kp_catalog_patch_price(kp_ctx* ctx, const int32_t* idx, const double* price, int32_t n, uint64_t epoch);
 
+/* Solve = kp_solve_prepare + kp_solve_execute + kp_solve_fetch.  A solve whose in-flight NodeClaims outgrow the first
+ * device plan (4096) is prepared and run again with room for up to 65,535; the ctx keeps that capacity for its later
+ * solves.  With the split calls the overflow surfaces as KP_E_UNSUPPORTED from kp_solve_fetch (the next prepare of that
+ * ctx uses the larger plan only after a kp_solve grew it). */
 kp_status kp_solve(kp_ctx* ctx, const kp_solve_input* in, kp_solve_output* out);
 
 /* kp_solve split into its phases (kp_solve == prepare + execute + fetch):
