@@ -329,13 +329,15 @@ def solve_leg(a, cat, prob, metric, workload, cpu_sample, local, rank, world, di
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         import parity
         import pyoracle
-        sample = synth.subsample(prob, min(P, cpu_sample))
+        full = cpu_sample >= P
+        sample = prob if full else synth.subsample(prob, cpu_sample)
         log("cpu baseline: oracle on %d pods" % sample.pods.n)
         orc = pyoracle.solve(sample)
         cpu_s = oracle_solve_seconds(orc)
+        what = "the full %d-pod workload" % sample.pods.n if full else "a seeded %d-pod subsample" % sample.pods.n
         line["cpu_baseline"] = {"value": sample.pods.n / cpu_s, "unit": "pods/s", "cores": 1, "kind": "port",
-                                "sample": "oracle (1 thread) on a seeded %d-pod subsample: %.2f s of Solve + Truncate "
-                                          "(input parsing excluded)" % (sample.pods.n, cpu_s)}
+                                "sample": "oracle (1 thread) on %s: %.2f s of Solve + Truncate "
+                                          "(input parsing excluded)" % (what, cpu_s)}
         try:
             parity.assert_same(parity.run_device(ctx, sample),
                                (orc.results, [model.parse_requirements_blob(orc.requirements(i))
@@ -383,10 +385,12 @@ def main():
     ap.add_argument("--launch-batch", type=int, default=10_000, help="config5 launch batch (NodeClaims)")
     ap.add_argument("--no-launch", action="store_true")
     ap.add_argument("--no-topology", action="store_true")
-    ap.add_argument("--topo-cpu-sample", type=int, default=12_000, help="pods in config3's CPU-baseline sample")
+    ap.add_argument("--topo-cpu-sample", type=int, default=50_000,
+                    help="pods in config3's CPU-baseline sample (default: the full workload, ~30 s of oracle time)")
     ap.add_argument("--no-reserved", action="store_true")
     ap.add_argument("--resv-pods", type=int, default=200_000, help="config5 Solve pods")
-    ap.add_argument("--resv-cpu-sample", type=int, default=40_000, help="pods in config5's CPU-baseline sample")
+    ap.add_argument("--resv-cpu-sample", type=int, default=200_000,
+                    help="pods in config5's CPU-baseline sample (default: the full workload, ~15 s of oracle time)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
