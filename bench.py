@@ -389,8 +389,9 @@ def main():
                     help="pods in config3's CPU-baseline sample (default: the full workload, ~30 s of oracle time)")
     ap.add_argument("--no-reserved", action="store_true")
     ap.add_argument("--resv-pods", type=int, default=200_000, help="config5 Solve pods")
-    ap.add_argument("--resv-cpu-sample", type=int, default=200_000,
-                    help="pods in config5's CPU-baseline sample (default: the full workload, ~15 s of oracle time)")
+    ap.add_argument("--resv-cpu-sample", type=int, default=40_000,
+                    help="pods in config5's CPU-baseline sample (the full 200k takes the oracle ~9 min: its reservation "
+                         "bookkeeping grows with NodeClaims x pods; DESIGN.md §6)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
