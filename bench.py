@@ -140,7 +140,8 @@ def consolidation_leg(a, cat, local, rank, world, dist, barrier, headroom=None):
         "kernel_ms_rank0": {"prep": km[0], "probes": km[1]},
         "counters_per_step": dict(zip(["pods_popped", "existing_slots", "nodeclaim_evals", "template_evals", "probes",
                                        "bitmap_words", "placed_existing", "new_nodeclaims", "chunk_loads", "chunk_hits",
-                                       "cyc_build", "cyc_scan", "cyc_nodeclaim", "cyc_decide", "cyc_total", "chunk_skips"],
+                                       "cyc_build", "cyc_scan", "cyc_nodeclaim", "cyc_decide", "cyc_total", "chunk_skips",
+                                       "relaxed"],
                                       [int(x) for x in cst])),
         "roofline": {"bound": "hbm", "kernel": "consolidate_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes": int(B),

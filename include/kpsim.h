@@ -455,10 +455,10 @@ typedef struct kp_consolidation_command {
 kp_status kp_consolidate_command(kp_ctx* ctx, int32_t mode, kp_consolidation_command* out);
 
 /* Diagnostics of the last kp_consolidate: ms[3] = {device prep (queue sort, masks), probe kernel, whole call};
- * counters[16] = {pods popped, existing-node slots examined, NodeClaim evaluations, template evaluations, probes,
+ * counters[17] = {pods popped, existing-node slots examined, NodeClaim evaluations, template evaluations, probes,
  * queue-bitmap words scanned, existing-node placements, new NodeClaims, node chunks loaded, cached-chunk hits, then
  * with KPSIM_PROFILE set: s_memtime cycles of queue build, existing-node scans, NodeClaim/template evaluation,
- * decision, whole probe (summed over probes)}. */
+ * decision, whole probe (summed over probes); then chunks the headroom summary skipped, preference relaxations}. */
 kp_status kp_consolidate_stats(kp_ctx* ctx, double* ms, int64_t* counters, int32_t n_counters);
 
 /*

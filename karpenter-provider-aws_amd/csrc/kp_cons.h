@@ -12,7 +12,7 @@
 
 enum { CS_POPS = 0, CS_EX_NODES, CS_NC_EVALS, CS_TMPL_EVALS, CS_PROBES, CS_BITMAP_WORDS, CS_PLACED_EXISTING,
        CS_NEW_NC, CS_CHUNK_LOADS, CS_CACHE_HITS, CS_CYC_BUILD, CS_CYC_SCAN, CS_CYC_NODECLAIM, CS_CYC_DECIDE,
-       CS_CYC_TOTAL, CS_CHUNK_SKIPS, CS_COUNT = 16 };
+       CS_CYC_TOTAL, CS_CHUNK_SKIPS, CS_RELAXED, CS_COUNT = 17 };
 
 #define KP_CONS_XTC 1024  // pod classes whose XT column of the cached node chunk is kept in LDS
 #define KP_CONS_STORE 8   // node chunks the fast probe variant keeps in its LDS headroom store
@@ -42,7 +42,12 @@ struct KpCons {
     int32_t astride;
     // per-worker scratch
     int32_t ring_cap;           // >= pods of any probe
-    int32_t* ring;              // [workers][ring_cap] queue entries: pod | pending << 31
+    int32_t* ring;              // [workers][ring_cap] queue entries: pod | relaxed << 30 | pending << 31
+    // preference relaxation (relax != 0, d.relax_next): an entry with the relaxed bit carries its class (| fresh << 31:
+    // not yet offered to the existing nodes) and shape here; other entries use the pod's input class / shape
+    int32_t relax;
+    int32_t* ring_cls;          // [workers][ring_cap]
+    int32_t* ring_shape;        // [workers][ring_cap]
     int32_t* ring_last;         // [workers][ring_cap] Queue.lastLen of the entry (-1: never pushed)
     int32_t* pnode;             // [workers][ring_cap] FULL variant: 0 = an existing node took the pod, -1 = none does
     int64_t* delta;             // [workers][n_active][E] requests added to node j by this probe (valid: mod bit)
@@ -69,6 +74,12 @@ struct KpCons {
     const int32_t* dec_moff;
     const int32_t* dec_g;       // [rows] group of the row
     const int32_t* dec_v;       // [rows][64]
+    // hostname pod affinity (a self-selecting pod bootstraps a domain only when no hostname domain holds a selected
+    // pod): per probe, the positive-domain count of each such group after its candidates' pods come off —
+    // hpos0[(single ? candidate : n_cand + prefix) * n_ha + ga]; tg_ha[g] = ga or -1
+    int32_t n_ha;
+    const int32_t* hpos0;
+    const int32_t* tg_ha;
     // chunk headroom summary: cmax0[w][ai] = the largest headroom on active axis ai over the nodes of 64-node chunk w
     // (kp_launch_cons_chunk_max, after the existing-node tables); each probe copies it to LDS and lowers a chunk's entry
     // to its true maximum whenever it has the chunk's headroom in hand, so the entries stay upper bounds and a pod whose
@@ -80,6 +91,6 @@ struct KpCons {
     int32_t no_fast;            // diagnostics: every probe on the FULL variant (KPSIM_CONS_NOFAST)
     // dynamic LDS plan (kp_cons_plan_lds)
     int32_t n_store;            // chunks in the fast variant's LDS headroom store (kp_cons_plan_lds)
-    int32_t off_hdr, off_words, off_rem, off_excl, off_mod, off_init, off_xtc, off_touch, off_hmod, off_cmax, off_hs;
+    int32_t off_hdr, off_words, off_rem, off_excl, off_mod, off_init, off_xtc, off_touch, off_hmod, off_cmax, off_hs, off_hpos;
     int32_t lds_bytes;
 };

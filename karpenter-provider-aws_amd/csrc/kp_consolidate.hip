@@ -120,6 +120,19 @@ __device__ inline uint64_t first_values(const KpDev& d, int k, int my_t, uint64_
     return ballot(first);
 }
 
+// The same for a multi-valued catalog key (zone, capacity-type, ...: <= 64 values, one mask per type): lane i gets the
+// number of distinct values over the kept lanes <= i (an inclusive prefix OR of the masks).
+__device__ inline int multi_values_upto(const KpDev& d, int k, int my_t, uint64_t m, int lane) {
+    uint64_t v = (((m >> lane) & 1ull) && my_t >= 0) ? d.multi_mask[(size_t)d.kmulti[k] * d.T + my_t] : 0ull;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(v >> 32), o) << 32) |
+                           (uint32_t)__shfl_up((int)(uint32_t)v, o);
+        if (lane >= o) v |= y;
+    }
+    return __popcll(v);
+}
+
 // InstanceTypes.SatisfiesMinValues over the kept lanes m of NodeClaim template j's minValues keys (header nch):
 // *need = minNeededInstanceTypes, the shortest kept prefix that satisfies every key.
 __device__ inline bool min_values_ok(const KpDev& d, const ReqHdr* nch, int j, int my_t, uint64_t m, int lane, int* need) {
@@ -130,17 +143,31 @@ __device__ inline bool min_values_ok(const KpDev& d, const ReqHdr* nch, int j, i
         if (k < 0) break;
         const ReqHdr h = nch[k];
         if (!(h.flags & RF_MIN) || h.minv <= 0) continue;
-        const uint64_t f = first_values(d, k, my_t, m, lane);
-        if (__popcll(f) < h.minv) return false;
-        // the kept lane at which the count reaches minv, as a position in the kept list
-        uint64_t x = f;
-        for (int i = 1; i < h.minv; i++) x &= x - 1;
-        const int L = __ffsll((unsigned long long)x) - 1;
+        int L;
+        if (d.kmulti[k] >= 0) {
+            const int upto = multi_values_upto(d, k, my_t, m, lane);
+            const uint64_t reach = ballot(upto >= h.minv);
+            if (!reach) return false;
+            L = __ffsll((unsigned long long)reach) - 1;
+        } else {
+            const uint64_t f = first_values(d, k, my_t, m, lane);
+            if (__popcll(f) < h.minv) return false;
+            // the kept lane at which the count reaches minv, as a position in the kept list
+            uint64_t x = f;
+            for (int i = 1; i < h.minv; i++) x &= x - 1;
+            L = __ffsll((unsigned long long)x) - 1;
+        }
         const int pos = __popcll(m & ((L >= 63) ? ~0ull : ((2ull << L) - 1)));
         nd = pos > nd ? pos : nd;
     }
     if (need) *need = nd;
     return true;
+}
+
+// MIN_VALUES_POLICY=BestEffort: the Add's relaxed minValues into the probe's NodeClaim digest (after its class keys).
+__device__ inline void commit_min_relax_lds(ReqHdr* nch, const WaveScratch& ws, int lane) {
+    if (lane < ws.n_minrel) nch[ws.minrel_k[lane]].minv = ws.minrel_v[lane];
+    __syncthreads();
 }
 
 }  // namespace
@@ -191,14 +218,21 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
         P.hd = k.pt_hd + (size_t)blockIdx.x * k.HG * (d.E + 1);
         P.hmod = reinterpret_cast<uint64_t*>(smem + k.off_hmod);
         P.dgk = k.pt_dgk;
+        P.hpos = reinterpret_cast<int32_t*>(smem + k.off_hpos);
+        P.ha = k.tg_ha;
         P.E = d.E;
         P.HG = k.HG;
     }
+    // input classes / shapes of the pods (pod_cls0 when preferences can relax: a Solve execute rewrites pod_cls)
+    const int32_t* const pcls = d.pod_cls0 ? d.pod_cls0 : d.pod_cls;
+    const int32_t* const pshape = d.pod_shape0 ? d.pod_shape0 : d.pod_shape;
     const int wid = blockIdx.x;
     const int E = d.E, EW = d.EW, A = d.n_active, R = d.R, K = d.K, TW = d.TW, T = d.T, NT = d.NT;
     const int cap = k.ring_cap;
     int32_t* ring = k.ring + (size_t)wid * cap;
     int32_t* rlast = k.ring_last + (size_t)wid * cap;
+    int32_t* rcls = k.relax ? k.ring_cls + (size_t)wid * cap : nullptr;
+    int32_t* rshape = k.relax ? k.ring_shape + (size_t)wid * cap : nullptr;
     int64_t* delta = k.delta + (size_t)wid * A * (E > 0 ? E : 1);
     uint64_t* pbits = k.pbits + (size_t)wid * k.PW;
 
@@ -258,7 +292,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
         const int gp = single ? (k.mode == KP_CONSOLIDATE_BOTH ? k.sprobe0 + probe - nmul : k.probe0 + probe) : k.probe0 + oi;
         const int c0 = single ? gp : 0, c1 = single ? gp + 1 : gp + 2;
         int64_t st_pops = 0, st_nodes = 0, st_nc = 0, st_tmpl = 0, st_words = 0, st_placed = 0, st_loads = 0, st_hits = 0;
-        int64_t st_skips = 0;
+        int64_t st_skips = 0, st_relax = 0;
         long long pf_load = 0, pf_prep = 0, pf_nodes = 0, pf_visits = 0;  // KPSIM_PROFILE: fast-path stages
         long long cy_build = 0, cy_scan = 0, cy_nc = 0, cy_dec = 0;
         const bool prof = k.profile != 0;
@@ -286,6 +320,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             __syncthreads();
             const int r0 = single ? k.dec_soff[gp] : k.dec_moff[gp], r1 = single ? k.dec_soff[gp + 1] : k.dec_moff[gp + 1];
             for (int r = r0; r < r1; r++) pt_init_row(d, P, k.dec_g[r], k.dec_v + (size_t)r * 64, lane);
+            for (int ga = lane; ga < k.n_ha; ga += 64) P.hpos[ga] = k.hpos0[(size_t)(single ? gp : k.n_cand + gp) * k.n_ha + ga];
         }
         // the probe's candidates are [c0, c1) and their pods one contiguous run of cand_pods (CSR in candidate order)
         const int po0 = k.cand_off[c0], po1 = k.cand_off[c1];
@@ -392,15 +427,21 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 vpod = ld32(&ring[slot]);
                 vlast = ld32(&rlast[slot]);
                 if (FULL && !TOPO) vpn = ld32(&k.pnode[(size_t)wid * cap + slot]);
-                const int p = vpod & 0x7fffffff;
-                vc = d.pod_cls[p];
-                vshape = d.pod_shape[p];
+                const int p = vpod & 0x3fffffff;
+                if (vpod & 0x40000000) {  // a relaxed entry: its class (| fresh << 31) and shape
+                    vc = ld32(&rcls[slot]);
+                    vshape = ld32(&rshape[slot]);
+                } else {
+                    vc = pcls[p];
+                    vshape = pshape[p];
+                }
 #pragma unroll
                 for (int ai = 0; ai < KP_LDS_AXES; ai++)
                     vq[ai] = ai < A ? d.pod_req[(size_t)p * R + d.active_axes[ai]] : 0;
             }
         };
         int n_nc = 0, nc_tmpl = -1, prev_shape = -1, xstart = 0, ok_np = 0, nc_nonpend = 0;
+        int relax_at = -1;  // queue position of the last Queue.Push(pod, relaxed): every lastLen pushed before is gone
         bool aborted = false;
         int cbase = -1, ccls = -1;  // cached node chunk (wave-uniform)
         uint64_t cx = 0;
@@ -582,7 +623,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 const int went = live ? ld32(&ring[wb + lane]) : 0;
                 const int wp = went & 0x7fffffff;
                 const bool wpend = went < 0;
-                const int wc = live ? d.pod_cls[wp] : 0;
+                const int wc = live ? pcls[wp] : 0;
                 int64_t wq[KP_LDS_AXES];
 #pragma unroll
                 for (int ai = 0; ai < KP_LDS_AXES; ai++)
@@ -686,7 +727,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 for (uint64_t m = U; m && !aborted; m &= m - 1) {
                     const int i = __ffsll((unsigned long long)m) - 1;
                     const int c = rl32(wc, i);
-                    const int shape = d.pod_shape[rl32(wp, i)];
+                    const int shape = pshape[rl32(wp, i)];
                     const bool pend = (pendm >> i) & 1ull;
                     int64_t q[KP_LDS_AXES];
 #pragma unroll
@@ -722,6 +763,19 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 }
                 if (FULL && live) pnode[wb + lane] = ((U >> lane) & 1ull) ? -1 : 0;
             }
+            if (FULL && k.relax) {
+                // a relaxed pod is offered to the existing nodes again by scan_nodes, which reads headroom as ex_head
+                // minus this probe's delta slab: the store chunks' headroom goes there
+                for (int w = 0; w < KS; w++) {
+                    if (!((loaded >> w) & 1ull)) continue;
+                    const int j = w * 64 + lane;
+                    if (j < E)
+                        AXL(ai) __hip_atomic_store(&delta[(size_t)ai * E + j], d.ex_head[(size_t)ai * E + j] - hs[(w * AA + ai) * 64 + lane],
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (lane == 0) modb[w] = ~0ull;
+                }
+                __syncthreads();
+            }
             if (FULL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (prof) cy_scan = __builtin_amdgcn_s_memtime() - cf0;
         }
@@ -737,20 +791,24 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             cx = uni64(cx);
             cmod = uni64(cmod);
             cinit = uni64(cinit);
+            relax_at = __builtin_amdgcn_readfirstlane(relax_at);
             if (head - wbase >= 64) win_load(head);
             const int off = head - wbase;
+            const int pos0 = head;
             const int ent = rl32(vpod, off);
-            const int elast = rl32(vlast, off);
+            const int elast = pos0 <= relax_at ? -1 : rl32(vlast, off);
             if (elast == count) break;  // Queue.Pop: cycled through the queue without progress
             head++;
             count--;
             // FULL, no topology: the window pass above placed this pod on an existing node (first pop), or every node
             // refuses it
-            if (FULL && !TOPO && elast < 0 && rl32(vpn, off) >= 0) continue;
+            if (FULL && !TOPO && pos0 < n && rl32(vpn, off) >= 0) continue;
             st_pops++;
             const bool pend = ent < 0;
-            const int p = ent & 0x7fffffff;
-            const int c = rl32(vc, off);
+            const int p = ent & 0x3fffffff;
+            const int cf = rl32(vc, off);
+            const int c = cf & 0x7fffffff;
+            const bool fresh = cf < 0;  // a relaxed class the existing nodes have not been offered yet
             const int shape = rl32(vshape, off);
             int64_t q[KP_LDS_AXES];
 #pragma unroll
@@ -773,7 +831,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             const bool tcons = TOPO && (cflags & CF_TOPO_CONS);
             const int xs = tcons ? 0 : xstart;
             const long long cs0 = prof ? __builtin_amdgcn_s_memtime() : 0;
-            const int jf = (FULL && !TOPO) ? -1 : scan_nodes(c, q, xs, tcons);
+            const int jf = (FULL && !TOPO && !fresh) ? -1 : scan_nodes(c, q, xs, tcons);
             if (prof) cy_scan += __builtin_amdgcn_s_memtime() - cs0;
             if (jf >= 0) {
                 if (lane == jf - cbase) {
@@ -833,6 +891,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     if (lane < R) S.nc_req[lane] += preq[lane];
                     if (RESV && d.resv_on) nc_held = commit_held(S.rcap, nc_held, S.ws.held, lane);
                     __syncthreads();
+                    if (d.best_effort) commit_min_relax_lds(nch, S.ws, lane);
                     if (TOPO && (cflags & CF_TOPO)) topo_record<true>(d, S.CC, S.ws, nch, ncw, E, nc_tmpl, true, lane, -1, &P);
                     placed = true;
                 }
@@ -892,6 +951,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     n_nc = 1;
                     placed = true;
                     __syncthreads();
+                    if (d.best_effort) commit_min_relax_lds(nch, S.ws, lane);
                     if (TOPO) {  // the NodeClaim's hostname row starts empty; Record the pod
                         for (int r = lane; r < k.HG; r += 64)
                             __hip_atomic_store(&P.hd[(size_t)r * (E + 1) + E], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -910,17 +970,31 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 }
                 continue;
             }
-            // Queue.Push(pod, relaxed=false): lastLen = len after the append
+            // preferences.Relax, then Queue.Push(pod, relaxed): a relaxed pod takes its class's next stage (fresh: the
+            // existing nodes see it again) and clears every lastLen; otherwise lastLen = len after the append
             const int tail = head + count;
+            const int nx = k.relax ? d.relax_next[c] : -1;
+            const int nent = k.relax ? (ent | 0x40000000) : ent;
+            const int ncls = nx >= 0 ? (nx | (int)0x80000000) : c;
+            const int nshape = nx >= 0 ? d.shape_next[shape] : shape;
+            const int nlast = nx >= 0 ? -1 : count + 1;
+            if (nx >= 0) {
+                relax_at = tail;
+                st_relax++;
+            }
             if (lane == 0) {
-                ring[tail % cap] = ent;
-                rlast[tail % cap] = count + 1;
+                ring[tail % cap] = nent;
+                rlast[tail % cap] = nlast;
+                if (k.relax) {
+                    rcls[tail % cap] = ncls;
+                    rshape[tail % cap] = nshape;
+                }
             }
             if (tail - wbase < 64 && lane == tail - wbase) {
-                vpod = ent;
-                vlast = count + 1;
-                vc = c;
-                vshape = shape;
+                vpod = nent;
+                vlast = nlast;
+                vc = ncls;
+                vshape = nshape;
 #pragma unroll
                 for (int ai = 0; ai < KP_LDS_AXES; ai++) vq[ai] = q[ai];
             }
@@ -1169,6 +1243,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             S.st[CS_CHUNK_LOADS] += st_loads;
             S.st[CS_CACHE_HITS] += st_hits;
             S.st[CS_CHUNK_SKIPS] += st_skips;
+            S.st[CS_RELAXED] += st_relax;
             if (prof) {
                 if (k.prof_probe) {
                     int64_t* pp = k.prof_probe + (size_t)oi * 8;
@@ -1248,6 +1323,8 @@ bool kp_cons_plan_lds(const KpDev& d, KpCons& k, int max_bytes) {
     off = al(off + (k.G > 0 ? 8 * (size_t)((k.G + 63) / 64) : 0));
     k.off_hmod = (int)off;
     off = al(off + (k.G > 0 ? 8 * (size_t)(d.EW > 0 ? d.EW : 1) : 0));
+    k.off_hpos = (int)off;  // TOPO: positive hostname domains per hostname-affinity group
+    off = al(off + 4 * (size_t)(k.n_ha > 0 ? k.n_ha : 1));
     // the fast variant's store of the first chunks' headroom ([n_store][n_active][64] i64): up to KP_CONS_STORE chunks,
     // fewer when the cluster is smaller
     {

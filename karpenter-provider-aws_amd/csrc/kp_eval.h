@@ -98,7 +98,7 @@ struct Roles {
 // pod (d.tg_cnt / d.tg_hcnt, read-only in probes); a probe keeps its own value-keyed rows (copied from the base on first
 // use, the probe's candidates' pods subtracted at probe start) and hostname-count deltas per node column (valid once the
 // node's hmod bit is set; column E is the probe's in-flight NodeClaim).  Hostname pod affinity (whose bootstrap counts
-// domains) is refused on the host.
+// domains) keeps the probe's positive-domain count per group (hpos).
 struct ProbeTopo {
     int32_t* cnt;          // [G][64] value-keyed counts (row g valid when touched bit g is set)
     uint64_t* known;       // [G] registered domains of row g
@@ -106,6 +106,8 @@ struct ProbeTopo {
     int32_t* hd;           // [HG][E + 1] hostname-count deltas
     uint64_t* hmod;        // LDS [EW]: node column valid
     const uint64_t* dgk;   // [G] domains of buildDomainGroups (registered before any pod is counted)
+    int32_t* hpos;         // LDS [n_ha]: hostname domains holding a selected pod, per hostname-affinity group
+    const int32_t* ha;     // [G] hostname-affinity group index into hpos, or -1
     int E, HG;
 };
 
@@ -431,7 +433,7 @@ __device__ __forceinline__ bool topo_narrow(const KpDev& d, const ClassCache& CC
             bool ok;
             if (type == 0) ok = cnt + self <= info.z;             // spread: hostname domainMinCount is 0
             else if (type == 2) ok = cnt == 0;                    // anti-affinity: an empty domain
-            else ok = cnt > 0 || (!CT && self && ld_i32(&d.tg_pos[g]) == 0);  // affinity (self-selecting bootstrap)
+            else ok = cnt > 0 || (self && (CT ? pt->hpos[pt->ha[g]] : ld_i32(&d.tg_pos[g])) == 0);  // affinity (self-selecting bootstrap)
             if (!ok) {
                 ws.memo_ok = 0;
                 return false;
@@ -583,6 +585,9 @@ __device__ __forceinline__ void topo_record(const KpDev& d, const ClassCache& CC
         }
         if (info.x & TG_HOST) {
             if (CT) {
+                // a hostname-affinity group's domain becomes positive: one more domain holds a selected pod
+                if (!inv && type == 1 && pt->ha[g] >= 0 && pt_hcnt(d, *pt, d.tg_hrow[g], host) == 0 && lane == 0)
+                    pt->hpos[pt->ha[g]]++;
                 pt_hadd(*pt, d.tg_hrow[g], host, lane);
             } else if (lane == 0) {
                 const int old = atomicAdd(&d.tg_hcnt[(size_t)d.tg_hrow[g] * d.HN + host], 1);

@@ -531,6 +531,13 @@ struct kp_ctx {
     std::vector<std::array<int, 3>> cons_extra;
     int cons_extra_ncand = 0;
     std::vector<std::map<int, std::vector<int32_t>>> cons_dec;
+    // hostname pod affinity: per candidate, the hostname-affinity groups whose domain on its node holds a selected pod
+    // only through the candidate's reschedulable pods (a probe of the candidate has one positive domain less); h_tpos0 =
+    // positive domains per group over every bound pod
+    std::vector<std::map<int, int>> cons_hdec;
+    std::vector<std::vector<int>> cons_hlost;
+    std::vector<int32_t> h_tpos0;
+    DBuf<int32_t> d_hpos0, d_tg_ha, d_ring_cls, d_ring_shape;
     std::vector<uint64_t> h_tknown_dg;       // [G] buildDomainGroups' domains (before any pod is counted)
     DBuf<int32_t> d_dec_soff, d_dec_moff, d_dec_g, d_dec_v, d_pt_cnt, d_pt_hd;
     DBuf<uint64_t> d_pt_known, d_pt_dgk;
@@ -1953,6 +1960,9 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     for (int gi = 0; gi < G; gi++)
         c->tg_host_aff[gi] = th.g[gi].host && th.g[gi].type == KP_TOPO_AFFINITY && !th.g[gi].inverse;
     c->cons_dec.assign(c->cons_extra_ncand, {});
+    c->cons_hdec.assign(c->cons_extra_ncand, {});
+    c->cons_hlost.assign(c->cons_extra_ncand, {});
+    c->h_tpos0.clear();
     {
         const int G1 = std::max(G, 1);
         std::vector<int4> tinfo(G1);
@@ -2078,6 +2088,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
                     }
                     if (g.host) {
                         if (hc0[(size_t)g.hrow * HN + j]++ == 0) tpos0[gi]++;
+                        if (cand >= 0 && c->tg_host_aff[gi]) c->cons_hdec[cand][gi]++;
                     } else {
                         const int v = node_val(j, g.key);
                         if (v < 0) continue;
@@ -2100,9 +2111,18 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
             }
             // kp_consolidate_prepare: each candidate's reschedulable pods are bound to its node in the cluster
             c->cons_dec.assign(c->cons_extra_ncand, {});
-            for (auto& e : c->cons_extra)
+            c->cons_hdec.assign(c->cons_extra_ncand, {});
+            c->cons_hlost.assign(c->cons_extra_ncand, {});
+            std::vector<int> cand_node(c->cons_extra_ncand, -1);
+            for (auto& e : c->cons_extra) {
                 if (!count_pod(e[0], in->pods.class_id[e[1]], e[2]))
                     return fail(ctx, KP_E_UNSUPPORTED, "topology key with more than 64 values");
+                cand_node[e[2]] = e[0];
+            }
+            for (int ci = 0; ci < c->cons_extra_ncand; ci++)
+                for (auto& kv : c->cons_hdec[ci])
+                    if (hc0[(size_t)th.g[kv.first].hrow * HN + cand_node[ci]] == kv.second) c->cons_hlost[ci].push_back(kv.first);
+            c->h_tpos0.assign(tpos0.begin(), tpos0.end());
         }
         if (tcl.empty()) tcl.push_back(0);
         if (trl.empty()) trl.push_back(0);
@@ -2587,21 +2607,10 @@ static kp_status cons_prepare_one(kp_ctx* ctx, const kp_consolidate_input* in) t
     ctx->cons_extra_ncand = 0;
     if (st != KP_OK) return st;
     kp_ctx* c = ctx;
-    if (!c->pref.relax_next.empty())
-        return fail(ctx, KP_E_UNSUPPORTED, "consolidation over pods with preferences to relax is not supported by this build");
-    // BestEffort differs from Strict only where a minValues requirement cannot be met: without minValues the probes are
-    // the same simulation under either policy
-    if (c->best_effort && c->any_min_values)
-        return fail(ctx, KP_E_UNSUPPORTED, "consolidation with MIN_VALUES_POLICY=BestEffort over minValues NodePools is not "
-                                           "supported by this build");
-    for (int gi = 0; gi < c->tg_G; gi++)
-        if (c->tg_host_aff[gi])  // its bootstrap counts the hostname domains holding pods, which probes do not track
-            return fail(ctx, KP_E_UNSUPPORTED, "consolidation over pods with required hostname pod affinity is not supported by "
-                                               "this build");
+    // preference relaxation (PREFERENCE_POLICY=Respect), MIN_VALUES_POLICY=BestEffort, hostname pod affinity and minValues
+    // on multi-valued labels run inside the probes as in the Solve (consolidate_kernel: relaxed queue entries, the Add's
+    // relaxed minValues, per-probe positive hostname domains, prefix-OR distinct counts)
     const KpDev& d = c->dev;
-    // minValues NodePools: the probe kernel counts distinct values of single-valued catalog keys only
-    if (c->min_multi)
-        return fail(ctx, KP_E_UNSUPPORTED, "consolidation with minValues on a multi-valued label is not supported by this build");
     if (c->cons_mayfix)
         return fail(ctx, KP_E_UNSUPPORTED, "consolidation with NotIn/DoesNotExist pod requirements on keys some node lacks "
                                            "and other pods select positively is not supported by this build (" +
@@ -2706,6 +2715,30 @@ static kp_status cons_prepare_one(kp_ctx* ctx, const kp_consolidate_input* in) t
         HIPCHK(c->d_dec_g.upload(dg, s));
         HIPCHK(c->d_dec_v.upload(dv, s));
         HIPCHK(c->d_pt_dgk.upload(c->h_tknown_dg, s));
+        // hostname pod affinity: each probe's positive-domain count per group (the base minus the domains only its
+        // candidates' pods held)
+        std::vector<int32_t> ha(k.G, -1), hg;
+        for (int gi = 0; gi < k.G; gi++)
+            if (c->tg_host_aff[gi]) {
+                ha[gi] = (int)hg.size();
+                hg.push_back(gi);
+            }
+        k.n_ha = (int)hg.size();
+        std::vector<int32_t> hp((size_t)std::max(1, (NC + nm) * k.n_ha), 0);
+        if (k.n_ha > 0) {
+            std::vector<int32_t> acc(k.n_ha, 0);
+            for (int ci = 0; ci < NC; ci++) {
+                for (int ga = 0; ga < k.n_ha; ga++) hp[(size_t)ci * k.n_ha + ga] = c->h_tpos0[hg[ga]];
+                for (int g : c->cons_hlost[ci]) hp[(size_t)ci * k.n_ha + ha[g]]--;
+            }
+            for (int i = 0; i < nm; i++) {  // multi-node probe i: candidates [0, i + 2)
+                for (int cc = i == 0 ? 0 : i + 1; cc < i + 2; cc++)
+                    for (int g : c->cons_hlost[cc]) acc[ha[g]]++;
+                for (int ga = 0; ga < k.n_ha; ga++) hp[(size_t)(NC + i) * k.n_ha + ga] = c->h_tpos0[hg[ga]] - acc[ga];
+            }
+        }
+        HIPCHK(c->d_tg_ha.upload(ha, s));
+        HIPCHK(c->d_hpos0.upload(hp, s));
     }
     HIPCHK(c->d_next.ensure(3));
     HIPCHK(c->d_rank.ensure(std::max(P, 1)));
@@ -2782,12 +2815,21 @@ static kp_status cons_run(kp_ctx* ctx, int m0, int m1, int s0, int s1, kp_probe_
         k.dec_moff = c->d_dec_moff.p;
         k.dec_g = c->d_dec_g.p;
         k.dec_v = c->d_dec_v.p;
+        k.tg_ha = c->d_tg_ha.p;
+        k.hpos0 = c->d_hpos0.p;
         d.tg_cnt = c->d_tg_cnt0.p;
         d.tg_hcnt = c->d_tg_hcnt0.p;
     }
     const auto t0 = clk::now();
     HIPCHK(c->d_ring.ensure((size_t)workers * k.ring_cap));
     HIPCHK(c->d_ring_last.ensure((size_t)workers * k.ring_cap));
+    k.relax = d.relax_next ? 1 : 0;  // preference relaxation: relaxed queue entries carry their class and shape
+    if (k.relax) {
+        HIPCHK(c->d_ring_cls.ensure((size_t)workers * k.ring_cap));
+        HIPCHK(c->d_ring_shape.ensure((size_t)workers * k.ring_cap));
+        k.ring_cls = c->d_ring_cls.p;
+        k.ring_shape = c->d_ring_shape.p;
+    }
     HIPCHK(c->d_pnode.ensure((size_t)workers * k.ring_cap));
     HIPCHK(c->d_delta.ensure((size_t)workers * std::max(A, 1) * std::max(E, 1)));
     const size_t pb = (size_t)workers * k.PW;

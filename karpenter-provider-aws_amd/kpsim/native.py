@@ -209,10 +209,10 @@ class Context:
         return cmd
 
     def consolidate_stats(self):
-        """(ms[prep, probe kernel, call], counters[16]) of the last kp_consolidate (kpsim.h kp_consolidate_stats)."""
+        """(ms[prep, probe kernel, call], counters[17]) of the last kp_consolidate (kpsim.h kp_consolidate_stats)."""
         ms = (C.c_double * 3)()
-        ct = (C.c_int64 * 16)()
-        self.check(self.L.kp_consolidate_stats(self.h, ms, ct, 16), "kp_consolidate_stats")
+        ct = (C.c_int64 * 17)()
+        self.check(self.L.kp_consolidate_stats(self.h, ms, ct, 17), "kp_consolidate_stats")
         return list(ms), list(ct)
 
     def close(self):

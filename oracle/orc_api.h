@@ -26,10 +26,16 @@ void orc_result_free(orc_result* res);
 int32_t orc_consolidate_probe_count(const kp_consolidate_input* in);
 kp_status orc_consolidate(const kp_catalog_view* cat, const kp_consolidate_input* in, kp_probe_result* results,
                           int32_t cap_results, int32_t n_threads);
+/* ... with the context's solver parameters (kp_device_opts.preference_policy; the cluster's min_values_policy) */
+kp_status orc_consolidate_opts(const kp_catalog_view* cat, const kp_consolidate_input* in, const kp_device_opts* opts,
+                               kp_probe_result* results, int32_t cap_results, int32_t n_threads);
 double orc_consolidate_last_probe_seconds(void);
 /* kp_consolidate_command's restatement: the decision loops replayed over every probe, the replacement of a REPLACE. */
 kp_status orc_consolidate_command(const kp_catalog_view* cat, const kp_consolidate_input* in, int32_t mode,
                                   kp_consolidation_command* out, int32_t n_threads);
+kp_status orc_consolidate_command_opts(const kp_catalog_view* cat, const kp_consolidate_input* in,
+                                       const kp_device_opts* opts, int32_t mode, kp_consolidation_command* out,
+                                       int32_t n_threads);
 
 /* Launch-time selection (filter.go chain + Truncate + getCapacityType + getOverrides' offering side), same
  * contract as kp_launch_select. */

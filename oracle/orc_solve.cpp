@@ -1307,6 +1307,10 @@ static void run_probe(const ConsCtx& X, int probe, kp_probe_result& pr, Replacem
     s.resv_key = b.resv_key;
     s.resv_on = b.resv_on;
     s.resv_strict = b.resv_strict;
+    // the simulation's scheduler relaxes preferences and minValues as provisioning does (PREFERENCE_POLICY /
+    // MIN_VALUES_POLICY are controller-wide options; scheduling.md:217-219 "when determining if a pod can be shifted")
+    s.relax_next = b.relax_next;
+    s.best_effort = b.best_effort;
     s.tp = &b.own_types;
     s.cp = &b.own_classes;
     s.pp = &b.own_pods;
@@ -1449,20 +1453,18 @@ struct ConsEnv {
     ConsCtx X;
 };
 
-static kp_status cons_setup(const kp_catalog_view* cat, const kp_consolidate_input* in, ConsEnv& env) {
+static kp_status cons_setup(const kp_catalog_view* cat, const kp_consolidate_input* in, const kp_device_opts* opts,
+                            ConsEnv& env) {
     if (!cat || !in) return KP_E_INVALID;
-    // MIN_VALUES_POLICY=BestEffort: the same simulation as Strict unless a NodePool carries minValues
-    if (in->cluster.min_values_policy != KP_MIN_VALUES_STRICT)
-        for (int i = 0; i < in->cluster.n_nodepools; i++)
-            for (int q = 0; q < in->cluster.nodepools[i].n_requirements; q++)
-                if (in->cluster.nodepools[i].requirements[q].min_values >= 0) return KP_E_UNSUPPORTED;
+    if (in->cluster.min_values_policy != KP_MIN_VALUES_STRICT && in->cluster.min_values_policy != KP_MIN_VALUES_BEST_EFFORT)
+        return KP_E_INVALID;
     Dict& D = env.D;
     Solver& base = env.base;
     base.resv_on = true;        // ReservedCapacity gate on; disruption simulations use ReservedOfferingModeFallback
     base.resv_strict = false;
-    kp_status st = parse_into(base, cat, &in->cluster, KP_PREFERENCE_RESPECT);
+    base.best_effort = in->cluster.min_values_policy == KP_MIN_VALUES_BEST_EFFORT;
+    kp_status st = parse_into(base, cat, &in->cluster, opts ? opts->preference_policy : KP_PREFERENCE_RESPECT);
     if (st != KP_OK) return st;
-    if (!base.relax_next.empty()) return KP_E_UNSUPPORTED;  // preference relaxation inside probes: not restated
     const int E = (int)base.own_existing.size(), P = (int)base.own_pods.size();
     for (int i = 0; i < in->n_pending; i++)
         if (in->pending[i] < 0 || in->pending[i] >= P) return KP_E_INVALID;
@@ -1501,12 +1503,13 @@ static void run_probes(const ConsCtx& X, int b0, int b1, kp_probe_result* result
     for (auto& t : th) t.join();
 }
 
-extern "C" kp_status orc_consolidate(const kp_catalog_view* cat, const kp_consolidate_input* in,
-                                     kp_probe_result* results, int32_t cap_results, int32_t n_threads) {
+extern "C" kp_status orc_consolidate_opts(const kp_catalog_view* cat, const kp_consolidate_input* in,
+                                          const kp_device_opts* opts, kp_probe_result* results, int32_t cap_results,
+                                          int32_t n_threads) {
     if (!cat || !in) return KP_E_INVALID;
     if (in->mode != KP_CONSOLIDATE_SINGLE && in->mode != KP_CONSOLIDATE_MULTI) return KP_E_INVALID;
     auto env = std::make_unique<ConsEnv>();
-    kp_status st = cons_setup(cat, in, *env);
+    kp_status st = cons_setup(cat, in, opts, *env);
     if (st != KP_OK) return st;
     const int np = consolidate_probe_count(in);
     const int b0 = in->probe_begin > 0 ? in->probe_begin : 0;
@@ -1523,12 +1526,18 @@ extern "C" kp_status orc_consolidate(const kp_catalog_view* cat, const kp_consol
 // (singlenodeconsolidation.go), in the disruption controller's method order for KP_CONSOLIDATE_BOTH; a REPLACE carries
 // its replacement NodeClaim (options after the price filter / spot-to-spot cut / filterOutSameInstanceType, requirements
 // with capacity-type narrowed to spot when priced as spot).
-extern "C" kp_status orc_consolidate_command(const kp_catalog_view* cat, const kp_consolidate_input* in, int32_t mode,
-                                             kp_consolidation_command* out, int32_t n_threads) {
+extern "C" kp_status orc_consolidate(const kp_catalog_view* cat, const kp_consolidate_input* in,
+                                     kp_probe_result* results, int32_t cap_results, int32_t n_threads) {
+    return orc_consolidate_opts(cat, in, nullptr, results, cap_results, n_threads);
+}
+
+extern "C" kp_status orc_consolidate_command_opts(const kp_catalog_view* cat, const kp_consolidate_input* in,
+                                                  const kp_device_opts* opts, int32_t mode, kp_consolidation_command* out,
+                                                  int32_t n_threads) {
     if (!cat || !in || !out) return KP_E_INVALID;
     if (mode != KP_CONSOLIDATE_SINGLE && mode != KP_CONSOLIDATE_MULTI && mode != KP_CONSOLIDATE_BOTH) return KP_E_INVALID;
     auto env = std::make_unique<ConsEnv>();
-    kp_status st = cons_setup(cat, in, *env);
+    kp_status st = cons_setup(cat, in, opts, *env);
     if (st != KP_OK) return st;
     out->decision = KP_DECISION_NONE;
     out->mode = out->probe = out->nodepool = -1;
@@ -1600,6 +1609,11 @@ extern "C" kp_status orc_consolidate_command(const kp_catalog_view* cat, const k
     else
         small = true;
     return small ? KP_E_BUFFER : KP_OK;
+}
+
+extern "C" kp_status orc_consolidate_command(const kp_catalog_view* cat, const kp_consolidate_input* in, int32_t mode,
+                                             kp_consolidation_command* out, int32_t n_threads) {
+    return orc_consolidate_command_opts(cat, in, nullptr, mode, out, n_threads);
 }
 
 // Wall time of the probe phase of the last orc_consolidate (input parsing excluded): bench.py's CPU baseline.

@@ -46,6 +46,14 @@ def lib():
         _lib.orc_consolidate_command.argtypes = [C.POINTER(abi.kp_catalog_view), C.POINTER(abi.kp_consolidate_input),
                                                  C.c_int32, C.POINTER(abi.kp_consolidation_command), C.c_int32]
         _lib.orc_consolidate_command.restype = C.c_int32
+        _lib.orc_consolidate_opts.argtypes = [C.POINTER(abi.kp_catalog_view), C.POINTER(abi.kp_consolidate_input),
+                                              C.POINTER(abi.kp_device_opts), C.POINTER(abi.kp_probe_result), C.c_int32,
+                                              C.c_int32]
+        _lib.orc_consolidate_opts.restype = C.c_int32
+        _lib.orc_consolidate_command_opts.argtypes = [C.POINTER(abi.kp_catalog_view), C.POINTER(abi.kp_consolidate_input),
+                                                      C.POINTER(abi.kp_device_opts), C.c_int32,
+                                                      C.POINTER(abi.kp_consolidation_command), C.c_int32]
+        _lib.orc_consolidate_command_opts.restype = C.c_int32
         _lib.orc_launch_select.argtypes = [C.POINTER(abi.kp_catalog_view), C.c_int32, C.POINTER(abi.kp_launch_request),
                                            C.c_int32, C.POINTER(abi.kp_launch_result), C.POINTER(C.c_int32), C.c_int32,
                                            C.POINTER(C.c_int32), C.c_int32]
@@ -147,31 +155,35 @@ def solve(problem, catalog_view=None, preference_policy=0, reserved_capacity=1):
 
 
 def consolidate(cp, mode, probe_begin=0, probe_end=0, spot_to_spot=False, max_candidates=100, n_threads=1,
-                catalog_view=None):
+                catalog_view=None, preference_policy=0):
     """CPU oracle consolidation probes for a kpsim.model.ConsolidationProblem -> numpy array of abi.PROBE_DTYPE."""
     from kpsim import abi, model
     L = lib()
+    opts = abi.kp_device_opts(preference_policy=preference_policy)
     cv = catalog_view or model.CatalogView(cp.cluster.catalog)
     iv = model.ConsolidateInputView(cp, mode, probe_begin, probe_end, spot_to_spot, max_candidates)
     n = L.orc_consolidate_probe_count(C.byref(iv.view))
     b0 = max(0, probe_begin)
     b1 = probe_end if 0 < probe_end < n else n
     out = np.zeros(max(1, b1 - b0), abi.PROBE_DTYPE)
-    st = L.orc_consolidate(C.byref(cv.view), C.byref(iv.view), out.ctypes.data_as(C.POINTER(abi.kp_probe_result)),
-                           len(out), n_threads)
+    st = L.orc_consolidate_opts(C.byref(cv.view), C.byref(iv.view), C.byref(opts),
+                                out.ctypes.data_as(C.POINTER(abi.kp_probe_result)), len(out), n_threads)
     if st != 0:
         raise RuntimeError("orc_consolidate failed: %d" % st)
     return out[:max(0, b1 - b0)]
 
 
-def consolidate_command(cp, mode, spot_to_spot=False, max_candidates=100, n_threads=1, catalog_view=None):
+def consolidate_command(cp, mode, spot_to_spot=False, max_candidates=100, n_threads=1, catalog_view=None,
+                        preference_policy=0):
     """CPU oracle consolidation command (orc_consolidate_command) -> kpsim.consolidation.Command."""
-    from kpsim import consolidation, model
+    from kpsim import abi, consolidation, model
     L = lib()
+    opts = abi.kp_device_opts(preference_policy=preference_policy)
     cv = catalog_view or model.CatalogView(cp.cluster.catalog)
     iv = model.ConsolidateInputView(cp, mode, 0, 0, spot_to_spot, max_candidates)
     st, cmd = consolidation.command_call(
-        lambda cc: L.orc_consolidate_command(C.byref(cv.view), C.byref(iv.view), mode, C.byref(cc), n_threads))
+        lambda cc: L.orc_consolidate_command_opts(C.byref(cv.view), C.byref(iv.view), C.byref(opts), mode, C.byref(cc),
+                                                  n_threads))
     if st != 0:
         raise RuntimeError("orc_consolidate_command failed: %d" % st)
     return cmd

@@ -45,15 +45,18 @@ def _req_dict(text):
 
 
 class OracleBackend:
+    def __init__(self, preference_policy=0):
+        self.preference_policy = preference_policy  # PREFERENCE_POLICY (the device backend's ctx carries its own)
+
     def solve(self, prob):
         import pyoracle
-        o = pyoracle.solve(prob)
+        o = pyoracle.solve(prob, preference_policy=self.preference_policy)
         r = o.results
         return r, [o.requirements(i) for i in range(r.n_nodeclaims)]
 
     def command(self, cp, mode, spot_to_spot=False):
         import pyoracle
-        return pyoracle.consolidate_command(cp, mode, spot_to_spot=spot_to_spot)
+        return pyoracle.consolidate_command(cp, mode, spot_to_spot=spot_to_spot, preference_policy=self.preference_policy)
 
 
 class DeviceBackend:

@@ -7,6 +7,15 @@ allocatable) come from the golden catalog.
   delete_utilization       test/suites/consolidation/suite_test.go:491-573  "should consolidate nodes (delete)"
   anti_affinity_replace    test/suites/scale/deprovisioning_test.go:454-523 "single consolidation replace"
   multi_delete             test/suites/scale/deprovisioning_test.go:399-453 "multi-consolidation delete"
+
+Preference scenarios (website/content/en/preview/concepts/scheduling.md:217-219: preferences are treated as requirements
+"when determining if a pod can be shifted to a new node", relaxed one at a time when they cannot be met; PREFERENCE_POLICY,
+reference/settings.md:40):
+  preferred_anti_affinity_replace  anti_affinity_replace with a preferred (weight 50) hostname anti-affinity: under
+                                   Respect every pod keeps a node of its own through consolidation; under Ignore the
+                                   Deployment packs onto one node
+  preferred_affinity_delete        delete_utilization with pods preferring an instance category no NodePool offers: every
+                                   probe relaxes the preference before the pods fit the remaining nodes
 """
 import copy
 
@@ -150,4 +159,46 @@ def multi_delete(golden, backend, n_nodes=200, per_node=20):
     sim.consolidate()
     assert len(sim.nodes) == n_nodes // 5, len(sim.nodes)
     assert sum(len(n.pods) for n in sim.nodes) == len(keep)
+    return sim
+
+
+def preferred_anti_affinity_replace(golden, backend, n_nodes=10, respect=True):
+    pool = _nitro_pool("2xlarge")
+    cls = model.PodClass(labels={"app": "dep"}, topology=[model.TopologyTerm(
+        "anti", HOSTNAME, selector=[model.Requirement("app", "In", ["dep"])], weight=50)])
+    sim = SimCluster(golden, [pool], [cls], backend)
+    sim.add_pods(0, n_nodes, {"cpu": "10m", "memory": "50Mi"})
+    sim.provision()
+    first = {n.name for n in sim.nodes}
+    assert len(first) == (n_nodes if respect else 1), len(first)
+    pool.requirements = [r for r in pool.requirements if r.key != SIZE]
+    sim.consolidate()
+    if respect:  # each node replaced by a cheaper one, one pod per node throughout
+        assert len(sim.nodes) == n_nodes and not first & {n.name for n in sim.nodes}
+        assert all(len(n.pods) == 1 for n in sim.nodes)
+    else:
+        assert len(sim.nodes) == 1 and not first & {n.name for n in sim.nodes}
+    return sim
+
+
+def preferred_affinity_delete(golden, backend, n_pods=60):
+    pool = model.NodePool("default", requirements=[
+        model.Requirement(CAPACITY_TYPE, "In", ["on-demand"]), model.Requirement(SIZE, "In", ["medium", "large", "xlarge"]),
+        model.Requirement("karpenter.k8s.aws/instance-category", "In", ["c", "m"]),
+        model.Requirement(FAMILY, "NotIn", EXCLUDED_FAMILIES)])
+    cls = model.PodClass(labels={"app": "dep"}, preferred_terms=[
+        (10, [model.Requirement("karpenter.k8s.aws/instance-category", "In", ["r"])])])
+    sim = SimCluster(golden, [pool], [cls], backend)
+    pods = sim.add_pods(0, n_pods, {"cpu": "1"})
+    sim.provision()
+    keep = int(n_pods * 0.4)
+    drop = []
+    while len(pods) - len(drop) > keep:
+        n = max(sim.nodes, key=lambda x: (len([p for p in x.pods if p not in drop]), x.name))
+        drop.append([p for p in n.pods if p not in drop][-1])
+    sim.delete_pods(drop)
+    assert sim.utilization() < 0.5
+    sim.consolidate()
+    assert sim.utilization() > 0.6, sim.utilization()
+    assert sum(c.decision == 1 for c in sim.commands) >= 1  # DELETE commands: the relaxed pods fit the other nodes
     return sim

@@ -272,17 +272,77 @@ def fuzz_topology_existing_problem(catalog, seed, n_pods=200, n_classes=10, n_ex
     return prob
 
 
-def fuzz_topology_consolidation(catalog, seed, n_nodes=30, n_pods=160, n_bound=40, all_spot=False):
+def fuzz_topology_consolidation(catalog, seed, n_nodes=30, n_pods=160, n_bound=40, all_spot=False, host_affinity=False):
     """fuzz_consolidation over pods with topology terms (add_topology: zonal / hostname / capacity-type spread,
-    anti-affinity, zonal affinity; hostname pod affinity is refused by the library and turned into anti-affinity here)
-    plus non-reschedulable pods bound to random nodes (cluster.bound)."""
+    anti-affinity, zonal affinity; hostname pod affinity turned into anti-affinity unless host_affinity) plus
+    non-reschedulable pods bound to random nodes (cluster.bound)."""
     cp = fuzz_consolidation(catalog, seed, n_nodes=n_nodes, n_pods=n_pods, all_spot=all_spot, supported=True)
     rng = np.random.Generator(np.random.PCG64(seed + 123))
     prob = add_topology(rng, cp.cluster, p_term=0.4)
     for pc in prob.classes:
         for t in pc.topology:
-            if t.kind == "affinity" and t.key == HOSTNAME:
+            if t.kind == "affinity" and t.key == HOSTNAME and not host_affinity:
                 t.kind = "anti"
     E = len(prob.existing)
     prob.bound = [(int(rng.integers(0, E)), int(rng.integers(0, len(prob.classes)))) for _ in range(n_bound)]
+    return cp
+
+
+def add_preferences(rng, prob, p_node=0.45, p_topo=0.6):
+    """Preferences on a problem's classes, as the Solve's preference suites draw them: preferred node-affinity terms
+    (weights 1-100) and ORed required node-affinity terms over instance-category / arch, ScheduleAnyway spreads (zonal or
+    hostname), preferred pod anti-affinity (hostname) and preferred pod affinity (zonal or hostname); a handful of
+    classes per selector."""
+    cats = ["c", "m", "r", "t", "g", "i"]
+    for ci, pc in enumerate(prob.classes):
+        app = "p%d" % (ci % 5)
+        pc.labels = dict(pc.labels)
+        pc.labels["app"] = app
+        sel = [Requirement("app", "In", [app])]
+        u = rng.random()
+        if u < p_node * 0.65:
+            pc.preferred_terms = [(int(rng.integers(1, 100)),
+                                   [Requirement(AWS + "instance-category", "In",
+                                                [str(x) for x in rng.choice(cats, size=int(rng.integers(1, 3)), replace=False)])])
+                                  for _ in range(int(rng.integers(1, 4)))]
+        elif u < p_node:
+            pc.required_terms = [[Requirement(AWS + "instance-category", "In", [str(rng.choice(cats))])],
+                                 [Requirement(ARCH, "In", [str(rng.choice(["amd64", "arm64"]))])]]
+        v = rng.random()
+        if v < p_topo * 0.4:
+            pc.topology = [model.TopologyTerm("spread", HOSTNAME if rng.random() < 0.5 else ZONE, selector=sel,
+                                              max_skew=int(rng.integers(1, 3)), when_unsatisfiable="ScheduleAnyway",
+                                              node_affinity_policy="Ignore")]
+        elif v < p_topo * 0.75:
+            pc.topology = [model.TopologyTerm("anti", HOSTNAME, selector=sel, weight=int(rng.integers(1, 100)))]
+        elif v < p_topo:
+            pc.topology = [model.TopologyTerm("affinity", ZONE if rng.random() < 0.6 else HOSTNAME, selector=sel,
+                                              weight=int(rng.integers(1, 100)))]
+    return prob
+
+
+def fuzz_preference_consolidation(catalog, seed, n_nodes=30, n_pods=160, n_bound=30, all_spot=False, best_effort=False,
+                                  zone_min=False):
+    """fuzz_consolidation over pods with preferences to relax (add_preferences), pods of those classes bound to random
+    nodes (their selectors count), sometimes a PreferNoSchedule taint on a pool; best_effort: MIN_VALUES_POLICY=BestEffort
+    with minValues on instance-family that a NodeClaim may not meet; zone_min: minValues on the zone label."""
+    from kpsim import abi
+    cp = fuzz_consolidation(catalog, seed, n_nodes=n_nodes, n_pods=n_pods, all_spot=all_spot, supported=True,
+                            with_min=best_effort)
+    rng = np.random.Generator(np.random.PCG64(seed + 321))
+    prob = add_preferences(rng, cp.cluster)
+    E = len(prob.existing)
+    prob.bound = [(int(rng.integers(0, E)), int(rng.integers(0, len(prob.classes)))) for _ in range(n_bound)]
+    if seed % 3 == 0:
+        prob.nodepools[0].taints = list(prob.nodepools[0].taints) + [Taint("example.com/soft", "", "PreferNoSchedule")]
+    if best_effort:
+        prob.min_values_policy = abi.KP_MIN_VALUES_BEST_EFFORT
+        for np_ in prob.nodepools:
+            if rng.random() < 0.7:
+                np_.requirements = list(np_.requirements) + [
+                    Requirement(AWS + "instance-family", "Exists", [], int(rng.choice([2, 5, 20, 60, 150])))]
+    if zone_min:
+        for np_ in prob.nodepools:
+            np_.requirements = [r for r in np_.requirements if r.key != ZONE] + [
+                Requirement(ZONE, "Exists", [], int(rng.choice([1, 2, 3])))]
     return cp

@@ -321,3 +321,15 @@ def test_command_reference_scenarios_best_effort(golden, name):
     cp, expect = cons_cases.SCENARIOS[name](golden)
     cp.cluster.min_values_policy = 1
     cons_cases.check_expect(pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH), cp, expect)
+
+
+@pytest.mark.parametrize("policy", [0, 1])
+def test_e2e_preferred_anti_affinity_replace(golden, policy):
+    import cluster_sim
+    import e2e_cases
+    e2e_cases.preferred_anti_affinity_replace(golden, cluster_sim.OracleBackend(policy), n_nodes=6, respect=policy == 0)
+
+
+def test_e2e_preferred_affinity_delete(golden):
+    import e2e_cases
+    e2e_cases.preferred_affinity_delete(golden, _oracle_backend())

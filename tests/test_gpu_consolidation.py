@@ -353,13 +353,102 @@ def test_fuzz_consolidation_topology(ctx, golden, seed):
                           pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH, spot_to_spot=s2s))
 
 
-def test_consolidation_refuses_hostname_affinity(ctx, golden):
-    from kpsim import native
+def test_consolidation_hostname_affinity_case(ctx, golden):
+    """Required hostname pod affinity in the probes: a self-selecting class bootstraps a hostname domain only while no
+    domain holds a selected pod, counted per probe (the candidates' pods come off)."""
     cp = fuzzgen.fuzz_topology_consolidation(golden[:100], 11, n_nodes=10, n_pods=40)
     cp.cluster.classes[0].topology = [model.TopologyTerm("affinity", model.HOSTNAME, [model.Requirement("app", "Exists")])]
-    with pytest.raises(native.KpError) as e:
-        device_probes(ctx, cp, abi.KP_CONSOLIDATE_SINGLE)
-    assert e.value.status == abi.KP_E_UNSUPPORTED
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        assert_probes_equal(device_probes(ctx, cp, mode), pyoracle.consolidate(cp, mode))
+    assert_commands_equal(device_command(ctx, cp, abi.KP_CONSOLIDATE_BOTH),
+                          pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH))
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_fuzz_consolidation_hostname_affinity(ctx, golden, seed):
+    """fuzz_topology_consolidation with hostname pod affinity kept (self-selecting and cross-class selectors, bound pods
+    holding some domains): probes of both modes and the command against the oracle."""
+    rng = np.random.Generator(np.random.PCG64(3700 + seed))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 300)), replace=False))]
+    cp = fuzzgen.fuzz_topology_consolidation(sub, 3700 + seed, n_nodes=int(rng.integers(4, 60)),
+                                             n_pods=int(rng.integers(20, 250)), all_spot=seed % 4 == 0, host_affinity=True,
+                                             n_bound=int(rng.integers(0, 40)))
+    s2s = seed % 2 == 0
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        assert_probes_equal(device_probes(ctx, cp, mode, s2s), pyoracle.consolidate(cp, mode, spot_to_spot=s2s))
+    assert_commands_equal(device_command(ctx, cp, abi.KP_CONSOLIDATE_BOTH, s2s),
+                          pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH, spot_to_spot=s2s))
+
+
+# ------------------------------------------------------------------------------------------------
+# consolidation over pods with preferences (PREFERENCE_POLICY Respect / Ignore) and MIN_VALUES_POLICY=BestEffort
+# ------------------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def pctx():
+    from kpsim import native
+    cs = {p: native.Context(0, preference_policy=p) for p in (abi.KP_PREFERENCE_RESPECT, abi.KP_PREFERENCE_IGNORE)}
+    yield cs
+    for c in cs.values():
+        c.close()
+
+
+@pytest.mark.parametrize("seed", range(16))
+@pytest.mark.parametrize("policy", ["respect", "ignore"])
+def test_fuzz_consolidation_preferences(pctx, golden, seed, policy):
+    """Probes whose pods carry preferred node affinity, ORed required terms, ScheduleAnyway spreads and preferred pod
+    (anti-)affinity (fuzzgen.add_preferences), some under MIN_VALUES_POLICY=BestEffort with minValues a NodeClaim can
+    miss, some with minValues on the zone label: each probe relaxes a failing pod's preferences one at a time and
+    re-queues it (Queue.Push(pod, relaxed) clears lastLen), as the Solve does.  Probes of both modes and the command."""
+    pol = abi.KP_PREFERENCE_RESPECT if policy == "respect" else abi.KP_PREFERENCE_IGNORE
+    ctx = pctx[pol]
+    rng = np.random.Generator(np.random.PCG64(4100 + seed))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 300)), replace=False))]
+    cp = fuzzgen.fuzz_preference_consolidation(sub, 4100 + seed, n_nodes=int(rng.integers(4, 60)),
+                                               n_pods=int(rng.integers(20, 250)), all_spot=seed % 4 == 0,
+                                               best_effort=seed % 3 == 1, zone_min=seed % 4 == 2)
+    s2s = seed % 2 == 1
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        assert_probes_equal(device_probes(ctx, cp, mode, s2s),
+                            pyoracle.consolidate(cp, mode, spot_to_spot=s2s, preference_policy=pol))
+    assert_commands_equal(device_command(ctx, cp, abi.KP_CONSOLIDATE_BOTH, s2s),
+                          pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH, spot_to_spot=s2s, preference_policy=pol))
+
+
+def test_preference_relaxations_in_probes(pctx, golden):
+    """The fuzz above relaxes preferences inside the probes (kp_consolidate_stats counter 16): under Respect every
+    preference kind; under Ignore only the ORed required node-affinity terms (removeRequiredNodeAffinityTerm)."""
+    tot = {}
+    for pol in (abi.KP_PREFERENCE_RESPECT, abi.KP_PREFERENCE_IGNORE):
+        tot[pol] = 0
+        for seed in range(6):
+            rng = np.random.Generator(np.random.PCG64(4100 + seed))
+            sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 300)), replace=False))]
+            cp = fuzzgen.fuzz_preference_consolidation(sub, 4100 + seed, n_nodes=int(rng.integers(4, 60)),
+                                                       n_pods=int(rng.integers(20, 250)), all_spot=seed % 4 == 0,
+                                                       best_effort=seed % 3 == 1, zone_min=seed % 4 == 2)
+            device_probes(pctx[pol], cp, abi.KP_CONSOLIDATE_SINGLE)
+            tot[pol] += pctx[pol].consolidate_stats()[1][16]
+    assert tot[abi.KP_PREFERENCE_RESPECT] > tot[abi.KP_PREFERENCE_IGNORE], tot
+
+
+@pytest.mark.parametrize("policy", ["respect", "ignore"])
+def test_e2e_preferred_anti_affinity_replace(pctx, golden, policy):
+    """Preferred hostname anti-affinity through Solve + consolidation: under Respect each node is replaced and every pod
+    keeps a node of its own; under Ignore the Deployment packs onto one node.  Same trajectory as the oracle."""
+    import cluster_sim
+    import e2e_cases
+    pol = abi.KP_PREFERENCE_RESPECT if policy == "respect" else abi.KP_PREFERENCE_IGNORE
+    kw = dict(n_nodes=8, respect=policy == "respect")
+    dev = e2e_cases.preferred_anti_affinity_replace(golden, cluster_sim.DeviceBackend(pctx[pol]), **kw)
+    orc = e2e_cases.preferred_anti_affinity_replace(golden, cluster_sim.OracleBackend(pol), **kw)
+    assert _trajectory(dev) == _trajectory(orc)
+
+
+def test_e2e_preferred_affinity_delete(ctx, golden):
+    """Pods preferring an instance category no NodePool offers: the probes relax the preference, then the pods fit the
+    remaining nodes (DELETE), until utilisation > 0.6; same trajectory as the oracle."""
+    import e2e_cases
+    _e2e(ctx, golden, e2e_cases.preferred_affinity_delete)
 
 
 # ------------------------------------------------------------------------------------------------
