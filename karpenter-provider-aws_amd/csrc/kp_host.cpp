@@ -538,6 +538,7 @@ struct kp_ctx {
     std::vector<std::vector<int>> cons_hlost;
     std::vector<int32_t> h_tpos0;
     DBuf<int32_t> d_hpos0, d_tg_ha, d_ring_cls, d_ring_shape;
+    DBuf<KpDev> d_self;  // device copy of dev for out-of-line kernel helpers (KpDev::self)
     std::vector<uint64_t> h_tknown_dg;       // [G] buildDomainGroups' domains (before any pod is counted)
     DBuf<int32_t> d_dec_soff, d_dec_moff, d_dec_g, d_dec_v, d_pt_cnt, d_pt_hd;
     DBuf<uint64_t> d_pt_known, d_pt_dgk;
@@ -2361,6 +2362,9 @@ extern "C" kp_status kp_solve_execute(kp_ctx* ctx) {
     HIPCHK(kp_launch_template_init(d, s));
     HIPCHK(kp_launch_existing(d, s));
     HIPCHK(hipEventRecord(c->ev[3], s));
+    HIPCHK(c->d_self.ensure(1));
+    d.self = c->d_self.p;
+    HIPCHK(hipMemcpyAsync(c->d_self.p, &d, sizeof(KpDev), hipMemcpyHostToDevice, s));
     HIPCHK(kp_launch_ffd(d, s));
     HIPCHK(hipEventRecord(c->ev[4], s));
     HIPCHK(kp_launch_finalize(d, d.NCcap, s));

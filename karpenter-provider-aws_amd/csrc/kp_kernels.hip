@@ -461,7 +461,8 @@ __device__ __forceinline__ void commit_reservations(const KpDev& d, int32_t* rca
 // cluster"): the first node in scheduling order that is tolerated, Compatible, has headroom and passes
 // Topology.AddRequirements takes the pod; its requirements, the domain counts and its headroom are updated.  Kept out
 // of line: it runs only for clusters, and inlined it would weigh on the topology instantiations' register plan.
-__device__ __attribute__((noinline)) int existing_topo_scan(const KpDev& d, FfdShared& S, int pod, int lane) {
+__device__ __attribute__((noinline)) int existing_topo_scan(const KpDev* __restrict__ dp, FfdShared& S, int pod, int lane) {
+    const KpDev& d = *dp;
     const int K = d.K;
     const int c = S.cur_cls;
     const bool cons = (d.cls_flags[c] & CF_TOPO_CONS) != 0;
@@ -1187,7 +1188,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
             if (S.cls_fill) fill_class_cache(d, S.cur_cls, S.CC, tid, nthr);
             __syncthreads();
             if (wave == 0) {
-                const int placed = existing_topo_scan(d, S, pod, lane);
+                const int placed = existing_topo_scan(d.self, S, pod, lane);
                 if (lane == 0) {
                     S.ex_placed = placed;
                     S.cls_fill = 0;

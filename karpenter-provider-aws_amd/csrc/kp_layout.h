@@ -246,6 +246,10 @@ struct KpDev {
     const int32_t* rcap0;            // [64] ReservationManager capacity per reservation-id value id (least over offerings)
     uint64_t* nc_held;               // [NCcap] reservation IDs a NodeClaim holds (NodeClaim.reservedOfferings' IDs)
     int32_t* nc_rlive;               // [NCcap] the NodeClaim's options keep a compatible available reserved offering
+
+    // a device copy of this struct (uploaded before each FFD launch): out-of-line device functions take it instead of
+    // the kernel argument, whose address would otherwise escape and put every field read of the kernel in scratch
+    const KpDev* self;
 };
 
 // stats slots

@@ -7,8 +7,9 @@ NodeClaim becomes a node of its cheapest option at the cheapest available offeri
 lowest-price, kwok/strategy/strategy.go:45-60); evicted / pending pods are scheduled by a Solve over the remaining nodes
 (the provisioner); candidates are every node in disruption-cost order (fewer pods first, then name).
 """
+import math
 from dataclasses import dataclass, field
-from typing import List
+from typing import Dict, List, Optional
 
 import numpy as np
 
@@ -25,6 +26,7 @@ class Node:
     nodepool: int
     reservation: str = ""
     pods: List[int] = field(default_factory=list)
+    labels: Dict[str, str] = field(default_factory=dict)  # single-valued custom requirements of its NodeClaim
 
 
 def _admits(reqs, key, value):
@@ -79,8 +81,11 @@ class DeviceBackend:
 
 
 class SimCluster:
-    def __init__(self, catalog, nodepools, classes, backend, spot_to_spot=False, min_values_policy=0):
+    def __init__(self, catalog, nodepools, classes, backend, spot_to_spot=False, min_values_policy=0, budgets=None):
         self.catalog = catalog
+        # NodePool disruption budgets (karpv1.Budget.Nodes: "40%", "3", ...) by NodePool index; None: no budgets (the
+        # consolidation pass runs both methods over every candidate in one call)
+        self.budgets: Optional[Dict[int, List[str]]] = budgets
         self.nodepools = nodepools
         self.classes = classes
         self.backend = backend
@@ -117,6 +122,7 @@ class SimCluster:
         if n.reservation:
             lab[RESERVATION_ID] = n.reservation
             lab[RESERVATION_TYPE] = "default"
+        lab.update(n.labels)
         return lab
 
     def _existing(self, nodes):
@@ -180,6 +186,12 @@ class SimCluster:
         _, t, o = best
         self.n_launched += 1
         n = Node("node-%04d" % self.n_launched, t, o.zone, o.capacity_type, nodepool, o.reservation_id or "")
+        # NodeClaim labels from single-valued requirements on keys the instance type does not label (e.g. a custom
+        # partition key the pod selected)
+        known = set(synth.node_labels(self.catalog[t], o.zone, o.capacity_type, self.nodepools[nodepool].name))
+        for key, (cmp_, vals) in reqs.items():
+            if not cmp_ and len(vals) == 1 and key not in known and key != RESERVATION_ID:
+                n.labels[key] = vals[0]
         if o.reservation_id:
             o.reservation_capacity -= 1
             o.available = o.reservation_capacity != 0
@@ -187,7 +199,8 @@ class SimCluster:
         return n
 
     # ---- consolidation ----
-    def consolidation_problem(self):
+    def consolidation_problem(self, keep=None):
+        """keep(node) -> bool: the candidates offered (disruption budgets); every node stays in the cluster."""
         nodes = self._sorted_nodes()
         pods = [p for n in nodes for p in n.pods]
         pos = {p: i for i, p in enumerate(pods)}
@@ -202,15 +215,27 @@ class SimCluster:
                 price=synth.candidate_price(it, self._labels(n)), capacity_type=ct, instance_type=n.type_row,
                 nodepool=n.nodepool, capacity=np.array(it.capacity, np.int64))))
         cands.sort(key=lambda c: (c[0], c[1]))
+        if keep is not None:
+            cands = [c for c in cands if keep(nodes[c[2].node])]
         cp = model.ConsolidationProblem(prob, [c[2] for c in cands], np.zeros(0, np.int32),
                                         np.ones(len(nodes), np.uint8))
         return cp, nodes
 
-    def consolidate_once(self, mode=abi.KP_CONSOLIDATE_BOTH):
-        """One disruption pass: compute the command, then execute it (replacement launched, candidates deleted, their
-        pods rescheduled).  Returns the command."""
-        cp, nodes = self.consolidation_problem()
-        cmd = self.backend.command(cp, mode, self.spot_to_spot)
+    def allowed_disruptions(self):
+        """NodePool → allowed disruptions: the least over its budgets, a percentage of its nodes rounded up
+        (Budget.GetAllowedDisruptions, intstr.GetScaledValueFromIntOrPercent(..., roundUp=true)); no disruption is in
+        flight between the emulator's synchronous commands."""
+        out = {}
+        for j in range(len(self.nodepools)):
+            specs = (self.budgets or {}).get(j)
+            if not specs:
+                out[j] = 1 << 30
+                continue
+            n = sum(1 for x in self.nodes if x.nodepool == j)
+            out[j] = min(math.ceil(n * int(b[:-1]) / 100) if b.endswith("%") else int(b) for b in specs)
+        return out
+
+    def _execute(self, cp, nodes, cmd):
         self.commands.append(cmd)
         if cmd.decision == abi.KP_DECISION_NONE:
             return cmd
@@ -228,6 +253,50 @@ class SimCluster:
         self.provision()
         assert not self.pending, "pods left pending after executing a consolidation command"
         return cmd
+
+    def consolidate_once_budgeted(self):
+        """The disruption controller's methods in order under NodePool budgets, candidates filtered caller-side as the
+        controller does (kpsim.h: budgets are outside kp_consolidate): Emptiness deletes empty candidates while their
+        NodePool allows (no simulation), then MultiNodeConsolidation over the candidates taken in order while their
+        NodePool allows (each taken one counts), then SingleNodeConsolidation over the candidates of NodePools with any
+        disruption allowed."""
+        from kpsim.consolidation import Command
+        allowed = self.allowed_disruptions()
+        cp, nodes = self.consolidation_problem()
+        left = dict(allowed)
+        empty = []
+        for ci, c in enumerate(cp.candidates):
+            n = nodes[c.node]
+            if not n.pods and left[n.nodepool] > 0:
+                left[n.nodepool] -= 1
+                empty.append(ci)
+        if empty:
+            return self._execute(cp, nodes, Command(abi.KP_DECISION_DELETE, empty, mode=-1))
+        left = dict(allowed)
+
+        def take(n):
+            if left[n.nodepool] <= 0:
+                return False
+            left[n.nodepool] -= 1
+            return True
+
+        cp, nodes = self.consolidation_problem(keep=take)
+        if cp.candidates:
+            cmd = self.backend.command(cp, abi.KP_CONSOLIDATE_MULTI, self.spot_to_spot)
+            if cmd.decision != abi.KP_DECISION_NONE:
+                return self._execute(cp, nodes, cmd)
+        cp, nodes = self.consolidation_problem(keep=lambda n: allowed[n.nodepool] > 0)
+        if not cp.candidates:
+            return self._execute(cp, nodes, Command(abi.KP_DECISION_NONE, []))
+        return self._execute(cp, nodes, self.backend.command(cp, abi.KP_CONSOLIDATE_SINGLE, self.spot_to_spot))
+
+    def consolidate_once(self, mode=abi.KP_CONSOLIDATE_BOTH):
+        """One disruption pass: compute the command, then execute it (replacement launched, candidates deleted, their
+        pods rescheduled).  Returns the command."""
+        if self.budgets is not None:
+            return self.consolidate_once_budgeted()
+        cp, nodes = self.consolidation_problem()
+        return self._execute(cp, nodes, self.backend.command(cp, mode, self.spot_to_spot))
 
     def consolidate(self, max_rounds=100, mode=abi.KP_CONSOLIDATE_BOTH):
         for _ in range(max_rounds):

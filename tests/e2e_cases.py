@@ -16,6 +16,14 @@ reference/settings.md:40):
                                    Deployment packs onto one node
   preferred_affinity_delete        delete_utilization with pods preferring an instance category no NodePool offers: every
                                    probe relaxes the preference before the pods fit the remaining nodes
+
+NodePool disruption budgets (test/suites/consolidation/suite_test.go:188-453; budgets filter the candidates caller-side,
+cluster_sim.SimCluster.consolidate_once_budgeted; the emulator executes commands synchronously, so "nodes disrupting at
+once" is the size of one command):
+  budget_empty_delete     :211-247 "should respect budgets for empty delete consolidation" (40%: at most 2 at once)
+  budget_nonempty_delete  :248-306 "should respect budgets for non-empty delete consolidation" (50% of 3: at most 2)
+  budget_replace          :307-409 "should respect budgets for non-empty replace consolidation" ("3"; 5 replaced)
+  budget_blocking         :410-436 "should not allow consolidation if the budget is fully blocking" ("0")
 """
 import copy
 
@@ -201,4 +209,86 @@ def preferred_affinity_delete(golden, backend, n_pods=60):
     sim.consolidate()
     assert sim.utilization() > 0.6, sim.utilization()
     assert sum(c.decision == 1 for c in sim.commands) >= 1  # DELETE commands: the relaxed pods fit the other nodes
+    return sim
+
+
+def _default_pool(name="default"):
+    """env.DefaultNodePool (test/pkg/environment/common/environment.go:133-177)."""
+    return model.NodePool(name, requirements=[
+        model.Requirement(OS, "In", ["linux"]), model.Requirement(CAPACITY_TYPE, "In", ["on-demand"]),
+        model.Requirement("karpenter.k8s.aws/instance-category", "In", ["c", "m", "r"]),
+        model.Requirement("karpenter.k8s.aws/instance-generation", "Gt", ["4"]), model.Requirement(FAMILY, "NotIn", ["a1"])])
+
+
+def _anti_class(app):
+    return model.PodClass(labels={"app": app}, topology=[model.TopologyTerm(
+        "anti", HOSTNAME, selector=[model.Requirement("app", "In", [app])])])
+
+
+def _budget_commands_within(sim, limit):
+    for c in sim.commands:
+        assert len(c.candidates) <= limit, (len(c.candidates), limit)
+
+
+def budget_empty_delete(golden, backend):
+    sim = SimCluster(golden, [_default_pool()], [_anti_class("regular-app")], backend, budgets={0: ["40%"]})
+    pods = sim.add_pods(0, 5, {"cpu": "1"})
+    sim.provision()
+    assert len(sim.nodes) == 5
+    sim.delete_pods(pods[1:])  # replicas 5 -> 1: four empty nodes
+    sim.consolidate()
+    _budget_commands_within(sim, 2)  # ConsistentlyExpectDisruptionsUntilNoneLeft(5, 2, ...)
+    assert [len(c.candidates) for c in sim.commands if c.decision == 1] == [2, 2]
+    assert len(sim.nodes) == 1
+    return sim
+
+
+def budget_nonempty_delete(golden, backend):
+    pool = _default_pool()
+    _replace(pool, model.Requirement(SIZE, "In", ["2xlarge"]))
+    sim = SimCluster(golden, [pool], [model.PodClass(labels={"app": "large-app"})], backend, budgets={0: ["50%"]})
+    pods = sim.add_pods(0, 9, {"cpu": "2100m"})
+    sim.provision()
+    assert len(sim.nodes) == 3
+    keep = {n.pods[0] for n in sim.nodes}  # replicas 9 -> 3, ForcePodsToSpread: one per node
+    sim.delete_pods([p for p in pods if p not in keep])
+    sim.consolidate()
+    _budget_commands_within(sim, 2)  # ConsistentlyExpectDisruptionsUntilNoneLeft(3, 2, ...)
+    assert sim.commands[0].decision == 1 and len(sim.commands[0].candidates) == 2
+    assert len(sim.nodes) == 1
+    return sim
+
+
+def budget_replace(golden, backend):
+    pool = _default_pool()
+    _replace(pool, model.Requirement(SIZE, "In", ["xlarge", "2xlarge"]), model.Requirement("test-partition", "Exists"))
+    pool.labels = {"app": "large-app"}
+    ds = np.zeros(model.R, np.int64)
+    ds[model.RIDX["cpu"]] = 3000  # the 3-cpu daemonset
+    pool.daemon_overhead = ds
+    classes = [model.PodClass(labels={"app": "large-app"},
+                              requirements=[model.Requirement("test-partition", "In", [str(i)])]) for i in range(5)]
+    sim = SimCluster(golden, [pool], classes, backend, budgets={0: ["3"]})
+    for i in range(5):
+        sim.add_pods(i, 1, {"cpu": "3"})
+    sim.provision()
+    first = {n.name for n in sim.nodes}
+    assert len(first) == 5 and all(golden[n.type_row].name.endswith(".2xlarge") for n in sim.nodes)
+    pool.daemon_overhead = np.zeros(model.R, np.int64)  # the daemonset is deleted
+    sim.consolidate()
+    _budget_commands_within(sim, 3)  # ConsistentlyExpectDisruptionsUntilNoneLeft(5, 3, ...)
+    assert [c.decision for c in sim.commands] == [2] * 5 + [0]
+    assert len(sim.nodes) == 5 and not first & {n.name for n in sim.nodes}  # ExpectNodeCount("==", 5), all rolled
+    assert all(golden[n.type_row].name.endswith(".xlarge") for n in sim.nodes)
+    return sim
+
+
+def budget_blocking(golden, backend):
+    sim = SimCluster(golden, [_default_pool()], [_anti_class("regular-app")], backend, budgets={0: ["0"]})
+    pods = sim.add_pods(0, 5, {"cpu": "1"})
+    sim.provision()
+    sim.delete_pods(pods[1:])
+    sim.consolidate()
+    assert [c.decision for c in sim.commands] == [0]  # ConsistentlyExpectNoDisruptions(5, ...)
+    assert len(sim.nodes) == 5
     return sim

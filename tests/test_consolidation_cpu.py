@@ -333,3 +333,11 @@ def test_e2e_preferred_anti_affinity_replace(golden, policy):
 def test_e2e_preferred_affinity_delete(golden):
     import e2e_cases
     e2e_cases.preferred_affinity_delete(golden, _oracle_backend())
+
+
+@pytest.mark.parametrize("name", ["budget_empty_delete", "budget_nonempty_delete", "budget_replace", "budget_blocking"])
+def test_e2e_budgets(golden, name):
+    """test/suites/consolidation/suite_test.go:188-453 (NodePool disruption budgets, filtered caller-side) on the
+    emulator, oracle backend: the reference's per-step disruption bound and end state."""
+    import e2e_cases
+    getattr(e2e_cases, name)(golden, _oracle_backend())

@@ -501,3 +501,12 @@ def test_e2e_multi_delete(ctx, golden):
     import e2e_cases
     sim = _e2e(ctx, golden, e2e_cases.multi_delete, n_nodes=200)
     assert sim.commands[0].mode == abi.KP_CONSOLIDATE_MULTI and len(sim.nodes) == 40
+
+
+@pytest.mark.parametrize("name", ["budget_empty_delete", "budget_nonempty_delete", "budget_replace", "budget_blocking"])
+def test_e2e_budgets(ctx, golden, name):
+    """test/suites/consolidation/suite_test.go:188-453: NodePool disruption budgets filter the candidates caller-side
+    (Emptiness, then MultiNodeConsolidation over the budget-capped prefix, then SingleNodeConsolidation); the device
+    command trajectory equals the oracle's and meets the reference's per-step bound and end state."""
+    import e2e_cases
+    _e2e(ctx, golden, getattr(e2e_cases, name))
