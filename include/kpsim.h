@@ -306,10 +306,12 @@ kp_status kp_catalog_patch_avail(kp_ctx* ctx, const uint8_t* available, int32_t 
 /* price delta: price of offering rows idx[i] becomes price[i]. */
 kp_status kp_catalog_patch_price(kp_ctx* ctx, const int32_t* idx, const double* price, int32_t n, uint64_t epoch);
 
-/* Solve = kp_solve_prepare + kp_solve_execute + kp_solve_fetch.  A solve whose in-flight NodeClaims outgrow the first
- * device plan (4096) is prepared and run again with room for up to 65,535; the ctx keeps that capacity for its later
- * solves.  With the split calls the overflow surfaces as KP_E_UNSUPPORTED from kp_solve_fetch (the next prepare of that
- * ctx uses the larger plan only after a kp_solve grew it). */
+/* Solve = kp_solve_prepare + kp_solve_execute + kp_solve_fetch.  In-flight NodeClaims per solve: up to 65,535 (u16 ids).
+ * The prepare plans for 4096, or from the start for more when the pods' self-selecting hostname anti-affinity / spread
+ * terms need more (one NodeClaim per pod / per maxSkew pods): such node-dense solves run one execute, with the slice
+ * arrays in HBM once they outgrow LDS (~11k NodeClaims).  A solve that still overflows its plan surfaces as
+ * KP_E_UNSUPPORTED from kp_solve_fetch; the next prepare of that ctx (only that one) then plans for every pod, and
+ * kp_solve does that one re-run itself.  Later solves on the ctx start from the first plan again. */
 kp_status kp_solve(kp_ctx* ctx, const kp_solve_input* in, kp_solve_output* out);
 
 /* kp_solve split into its phases (kp_solve == prepare + execute + fetch):

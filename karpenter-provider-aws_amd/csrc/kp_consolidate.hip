@@ -256,9 +256,9 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
     Ev.slot_zoneid = d.slot_zoneid;
     Ev.roles = &S.roles;
     {
-        uint32_t mmask = 0;  // templates whose requirements carry minValues (single-valued keys, kp_consolidate_prepare)
+        uint64_t mmask = 0;  // templates whose requirements carry minValues
         for (int j = 0; j < d.NT; j++)
-            if (d.min_keys[(size_t)j * KP_MAX_CLASS_KEYS] >= 0) mmask |= 1u << j;
+            if (d.min_keys[(size_t)j * KP_MAX_CLASS_KEYS] >= 0) mmask |= 1ull << j;
         Ev.min_tmpl_mask = mmask;
     }
     Ev.ro = RESV ? d.ro : nullptr;
@@ -465,7 +465,11 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
         // stays in registers (effective headroom and this probe's added requests per lane) and becomes the chunk of the
         // returned node.  Other chunks are first filtered 64 at a time (one lane per chunk) by the pod's compatible
         // nodes and the headroom summary, so a pod that fits nowhere skips the cluster without loading it.
-        auto scan_nodes = [&](int c, const int64_t (&q)[KP_LDS_AXES], int xs, bool tcons) -> int {
+        // wide: more requested resource axes than the registers hold (A > KP_LDS_AXES): the axes past KP_LDS_AXES are
+        // checked per candidate node from HBM (ex_head minus this probe's delta slab, which holds them as soon as a
+        // node takes a pod), and the probe runs the serial queue only (no window pass; the fast variant is not used)
+        const bool wide = A > KP_LDS_AXES;
+        auto scan_nodes = [&](int c, const int64_t (&q)[KP_LDS_AXES], int xs, bool tcons, const int64_t* pr) -> int {
             int jf = -1;
             uint64_t fmask = 0;
             int fgrp = -1;
@@ -535,6 +539,14 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
 #pragma unroll
                 for (int ai = 0; ai < KP_LDS_AXES; ai++)
                     if (ai < A) cand &= q[ai] <= h[ai];
+                if (wide && ballot(cand)) {
+                    const bool md = (((base == cbase) ? cmod : mw) >> lane) & 1ull;
+                    for (int ai = KP_LDS_AXES; ai < A && cand; ai++) {
+                        int64_t hx = d.ex_head[(size_t)ai * E + j];
+                        if (md) hx -= ld_req(&delta[(size_t)ai * E + j]);
+                        cand = pr[d.active_axes[ai]] <= hx;
+                    }
+                }
                 st_nodes += 64;
                 uint64_t m = ballot(cand);
                 if (TOPO && tcons) {  // ExistingNode.Add's topology step on each fitting node, in order
@@ -592,7 +604,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             }
             return jf;
         };
-        if constexpr (!TOPO) {
+        if (!TOPO && !wide) {
             // ---- existing nodes: the probe's pods in windows of 64, one pod per lane ----
             // Fast variant: every pod here lands on an existing node or the probe goes to the FULL variant, so the queue
             // is one pass in order and the probe is plain first fit: each pod takes the first node in scheduling order
@@ -736,7 +748,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                         prev_shape = shape;
                         xstart = 0;
                     }
-                    const int jf = SE < E ? scan_nodes(c, q, xstart > SE ? xstart : SE, false) : -1;
+                    const int jf = SE < E ? scan_nodes(c, q, xstart > SE ? xstart : SE, false, nullptr) : -1;
                     if (jf < 0) {
                         if constexpr (!FULL) {
                             aborted = true;  // needs a NodeClaim: the FULL variant redoes this probe
@@ -802,7 +814,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             count--;
             // FULL, no topology: the window pass above placed this pod on an existing node (first pop), or every node
             // refuses it
-            if (FULL && !TOPO && pos0 < n && rl32(vpn, off) >= 0) continue;
+            if (FULL && !TOPO && !wide && pos0 < n && rl32(vpn, off) >= 0) continue;
             st_pops++;
             const bool pend = ent < 0;
             const int p = ent & 0x3fffffff;
@@ -831,9 +843,17 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             const bool tcons = TOPO && (cflags & CF_TOPO_CONS);
             const int xs = tcons ? 0 : xstart;
             const long long cs0 = prof ? __builtin_amdgcn_s_memtime() : 0;
-            const int jf = (FULL && !TOPO && !fresh) ? -1 : scan_nodes(c, q, xs, tcons);
+            const int jf = (FULL && !TOPO && !fresh && !wide) ? -1 : scan_nodes(c, q, xs, tcons, d.pod_req + (size_t)p * R);
             if (prof) cy_scan += __builtin_amdgcn_s_memtime() - cs0;
             if (jf >= 0) {
+                if (wide && lane == 0) {  // the axes past the registers: this probe's delta slab, valid from the first pod
+                    const bool was = (cmod >> (jf & 63)) & 1ull;
+                    for (int ai = KP_LDS_AXES; ai < A; ai++) {
+                        int64_t* dp = &delta[(size_t)ai * E + jf];
+                        __hip_atomic_store(dp, (was ? ld_req(dp) : 0) + d.pod_req[(size_t)p * R + d.active_axes[ai]],
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
                 if (lane == jf - cbase) {
 #pragma unroll
                     for (int ai = 0; ai < KP_LDS_AXES; ai++) {
@@ -1108,7 +1128,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 }
             }
             const int nsel = n_opt < d.M ? n_opt : d.M;
-            const bool has_min = (Ev.min_tmpl_mask >> nc_tmpl) & 1u;
+            const bool has_min = (Ev.min_tmpl_mask >> nc_tmpl) & 1ull;
             int my_t = -1;
             for (int i = 0; i < nsel; i++) {
                 double bp = DBL_MAX;

@@ -62,7 +62,7 @@ __device__ __forceinline__ void commit_min_relax(const KpDev& d, const WaveScrat
 struct ClassCache {
     int cls;
     int nck;
-    uint32_t tol;
+    uint64_t tol;
     uint32_t flags;
     int role[5];  // class-key index of zone, capacity-type, zone-id, reservation-id, reservation-type (or -1)
     int key[KP_MAX_CLASS_KEYS];
@@ -131,7 +131,7 @@ struct EvalEnv {
     const int* slot_ct;
     const int* slot_zoneid;
     const Roles* roles;
-    uint32_t min_tmpl_mask;    // templates whose requirements carry minValues
+    uint64_t min_tmpl_mask;    // templates whose requirements carry minValues
     const ResvTab* ro;         // reserved offerings (null: none)
     const uint64_t* type_ro;   // [T] the type's reserved offerings (bits over ro index)
     const int32_t* rcap;       // ReservationManager capacity by reservation-id value id (FFD kernel LDS)
@@ -168,7 +168,7 @@ __device__ inline void fill_class_cache(const KpDev& d, int c, ClassCache& CC, i
     if (tid == 0) {
         CC.cls = c;
         CC.nck = nck;
-        CC.tol = c < d.C ? d.tol[c] : 0xFFFFFFFFu;
+        CC.tol = c < d.C ? d.tol[c] : ~0ull;
         CC.flags = d.cls_flags[c];
         uint32_t kn = 0;
         if (d.cls_kneutral)
@@ -298,22 +298,16 @@ struct WitnessAcc {
             bt = t;
         }
     }
-    __device__ __forceinline__ void finish(const KpDev& d, const EvalEnv& E, const int64_t* tot, bool minv,
-                                           WaveScratch& ws, int lane) {
-        const int A = d.lds_A;
-        if (A == 0) return;
-        if (!on || minv) {
-            if (lane < A) ws.hr[lane] = -1;
-            return;
+    __device__ __forceinline__ void take(float ob, int ot) {
+        if (ob > best || (ob == best && ot < bt)) {
+            best = ob;
+            bt = ot;
         }
+    }
+    // arg-best over the wave ((score desc, type asc) is a total order, so the reduction tree does not matter); every
+    // lane ends with the wave's best
+    __device__ __forceinline__ void reduce_wave() {
         KP_ASSERT_FULL_WAVE();
-        // arg-best over the wave ((score desc, type asc) is a total order, so the reduction tree does not matter)
-        auto take = [&](float ob, int ot) {
-            if (ob > best || (ob == best && ot < bt)) {
-                best = ob;
-                bt = ot;
-            }
-        };
         take(__uint_as_float(dpp32<kDppQuadXor1>(__float_as_uint(best))), (int)dpp32<kDppQuadXor1>((uint32_t)bt));
         take(__uint_as_float(dpp32<kDppQuadXor2>(__float_as_uint(best))), (int)dpp32<kDppQuadXor2>((uint32_t)bt));
         take(__uint_as_float(dpp32<kDppRowHalfMirror>(__float_as_uint(best))), (int)dpp32<kDppRowHalfMirror>((uint32_t)bt));
@@ -333,6 +327,17 @@ struct WitnessAcc {
             take(b2, t2);
             take(b3, t3);
         }
+    }
+    // ws.hr from the arg-best (reduced: already wave- or team-reduced)
+    __device__ __forceinline__ void finish(const KpDev& d, const EvalEnv& E, const int64_t* tot, bool minv,
+                                           WaveScratch& ws, int lane, bool reduced = false) {
+        const int A = d.lds_A;
+        if (A == 0) return;
+        if (!on || minv) {
+            if (lane < A) ws.hr[lane] = -1;
+            return;
+        }
+        if (!reduced) reduce_wave();
         int64_t my = 0;
 #pragma unroll
         for (int ai = 0; ai < KP_LDS_AXES; ai++)
@@ -342,6 +347,15 @@ struct WitnessAcc {
             ws.hr[lane] = h < 0 ? -1 : (int32_t)(h >> qshift_of(d, lane));
         }
     }
+};
+
+// One evaluation shared by every wave of the block (TEAM): each wave sweeps the option words w ≡ rank (mod n); the
+// partial results meet here (double-buffered by evaluation parity, so one barrier per evaluation suffices).
+struct TeamBuf {
+    uint64_t nw[KP_TW_MAX];    // remaining options, by word (written by the word's wave)
+    uint64_t any[KP_NWAVES];   // per wave: OR of its words
+    float best[KP_NWAVES];     // per wave: witness arg-best (score, type)
+    int bt[KP_NWAVES];
 };
 
 struct EvalIn {
@@ -577,7 +591,7 @@ __device__ __forceinline__ void topo_record(const KpDev& d, const ClassCache& CC
         if (!inv && type == 0) {  // TopologyNodeFilter.Matches
             const int pol = d.tg_pol[g], owner = d.tg_owner[g];
             const bool tolerated = exnode >= 0 ? ((d.ex_tol[(size_t)owner * d.EW + (exnode >> 6)] >> (exnode & 63)) & 1ull) != 0
-                                               : ((d.tol[owner] >> tmpl) & 1u) != 0;
+                                               : ((d.tol[owner] >> tmpl) & 1ull) != 0;
             if ((pol & 2) && !tolerated) continue;
             if ((pol & 1) && owner != CC.cls &&
                 !topo_filter_compatible(d, CC, ws, Ahdr, Aw, owner, allow_wk, lane, exnode >= 0))
@@ -687,14 +701,28 @@ __device__ inline void existing_topo_commit(const KpDev& d, const ClassCache& CC
 // instantiations keep the topology and reservation code out of the common path.
 // STRICT: ReservedOfferingModeStrict (provisioning); false: Fallback (disruption simulations never fail an Add for want
 // of a reservation).  BE: the solve may run MIN_VALUES_POLICY=BestEffort (false compiles the relaxation bookkeeping out).
-template <bool TOPO, bool RESV = false, bool STRICT = true, bool BE = true, bool CT = false>
+// TEAM: every wave of the block evaluates the same candidate (tb: this evaluation's TeamBuf, rank = wave, n waves):
+// the requirement, topology and offering steps run in each wave alike, the type sweep is split over the waves by word,
+// and one block barrier joins the partial sweeps; every wave ends with the same result in its ws.
+template <bool TOPO, bool RESV = false, bool STRICT = true, bool BE = true, bool CT = false, bool TEAM = false>
 __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, const ClassCache& CC, const EvalIn& a,
-                                          WaveScratch& ws, int lane) {
+                                          WaveScratch& ws, int lane, TeamBuf* tb = nullptr, int trank = 0, int tn = 1) {
     const int TW = d.TW, T = d.T;
     long long _t0 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
     if (a.prof && lane == 0) atomicAdd((unsigned long long*)&a.prof[ST_EV_CALLS - ST_EV_REQ], 1ull);
-    if (a.compat && !((CC.tol >> a.tmpl) & 1u)) return false;
+    if (a.compat && !((CC.tol >> a.tmpl) & 1ull)) return false;
     const int nck = CC.nck;
+    // request totals over the active axes (the first KP_LDS_AXES live in registers): the candidate's totals are read
+    // past L1 here, so their latency overlaps the requirement merge
+    int64_t tot[KP_LDS_AXES];
+#pragma unroll
+    for (int ai = 0; ai < KP_LDS_AXES; ai++) {
+        tot[ai] = 0;
+        if (ai < d.n_active) {
+            const int r = d.active_axes[ai];
+            tot[ai] = (a.base_req ? ld_req(a.base_req + r) : 0) + (a.pod_req ? a.pod_req[r] : 0);
+        }
+    }
 
     // ---- requirements: Compatible + Add (lane = class key) ----
     bool fail = false, kill = false;
@@ -761,6 +789,9 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         EV_REJ(ST_REJ_REQ);
         return false;
     }
+#ifdef KP_DIAG_SPLIT
+    EV_STAMP(0);
+#endif
     if (TOPO) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         if (!topo_narrow<CT>(d, CC, ws, a.host, a.compat, lane, E.pt, E.snap)) {
@@ -773,7 +804,11 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
             classify(CC.key[lane], O, ow, popc_words(ow, CC.nw[lane]));
         }
     }
+#ifdef KP_DIAG_SPLIT
+    EV_STAMP(1);
+#else
     EV_STAMP(0);
+#endif
 
     // ---- options ∧ V[class] ∧ ¬DoesNotExist-types of keys whose merged operator is In/Exists ----
     uint64_t myopt = 0;
@@ -806,23 +841,16 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         (RESV && E.ro && E.ro->n > 0 && (need_off || E.resv_on)) ? resv_adm(d, E, CC, ws, a.Ahdr, a.Aw, lane) : 0ull;
     EV_STAMP(2);
 
-    // ---- request totals over the active axes (the first KP_LDS_AXES live in registers) ----
-    int64_t tot[KP_LDS_AXES];
-#pragma unroll
-    for (int ai = 0; ai < KP_LDS_AXES; ai++) {
-        tot[ai] = 0;
-        if (ai < d.n_active) {
-            const int r = d.active_axes[ai];
-            tot[ai] = (a.base_req ? ld_req(a.base_req + r) : 0) + (a.pod_req ? a.pod_req[r] : 0);
-        }
-    }
     const int n_extra = d.n_active > KP_LDS_AXES ? d.n_active - KP_LDS_AXES : 0;
+#ifdef KP_DIAG_SPLIT
+    EV_STAMP(2);
+#endif
 
     // ---- per type: Fits ∧ multi-valued labels ∧ offerings (64 types per ballot) ----
     WitnessAcc wit;
     wit.init(d, E, a.pod_req);
     uint64_t anyw = 0, newword = 0;
-    for (int w = 0; w < TW; w++) {
+    for (int w = TEAM ? trank : 0; w < TW; w += TEAM ? tn : 1) {
         const uint64_t cw = rl64(myopt, w);
         if (cw == 0) continue;
         const int t = w * 64 + lane;
@@ -862,14 +890,39 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         if (lane == w) newword = nb;
         anyw |= nb;
     }
+#ifdef KP_DIAG_SPLIT
     EV_STAMP(3);
+#endif
+    if (TEAM) {
+        // join the partial sweeps: every wave reads back all words, the OR and the team's witness arg-best
+        if (wit.on) wit.reduce_wave();
+        for (int w = trank; w < TW; w += tn)
+            if (lane == w) tb->nw[w] = newword;
+        if (lane == 0) {
+            tb->any[trank] = anyw;
+            tb->best[trank] = wit.best;
+            tb->bt[trank] = wit.bt;
+        }
+        __syncthreads();
+        newword = lane < TW ? tb->nw[lane] : 0ull;
+        anyw = 0;
+        for (int r = 0; r < tn; r++) {
+            anyw |= tb->any[r];
+            wit.take(tb->best[r], tb->bt[r]);
+        }
+    }
+#ifdef KP_DIAG_SPLIT
+    EV_STAMP(4);
+#else
+    EV_STAMP(3);
+#endif
     if (anyw == 0) {
         EV_REJ(ST_REJ_TYPES);
         return false;
     }
 
     // ---- minValues (Strict): distinct values per key over the remaining options ----
-    if (a.tmpl >= 0 && ((E.min_tmpl_mask >> a.tmpl) & 1u)) {
+    if (a.tmpl >= 0 && ((E.min_tmpl_mask >> a.tmpl) & 1ull)) {
         const int* mk = d.min_keys + (size_t)a.tmpl * KP_MAX_CLASS_KEYS;
         for (int q = 0; q < KP_MAX_CLASS_KEYS; q++) {
             const int k = mk[q];
@@ -940,7 +993,7 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
     }
     if (lane < TW) ws.opts[lane] = newword;
     // a NodeClaim that keeps reserved offerings is never quick-accepted (hr = -1): every Add recomputes its reservations
-    wit.finish(d, E, tot, rlive || (a.tmpl >= 0 && ((E.min_tmpl_mask >> a.tmpl) & 1u)), ws, lane);
+    wit.finish(d, E, tot, rlive || (a.tmpl >= 0 && ((E.min_tmpl_mask >> a.tmpl) & 1ull)), ws, lane, TEAM);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     EV_STAMP(4);
     return true;
@@ -999,7 +1052,7 @@ __device__ __forceinline__ bool eval_fits_only(const KpDev& d, const EvalEnv& E,
         anyw |= nb;
     }
     if (anyw == 0) return false;
-    if ((E.min_tmpl_mask >> a.tmpl) & 1u) {
+    if ((E.min_tmpl_mask >> a.tmpl) & 1ull) {
         const int* mk = d.min_keys + (size_t)a.tmpl * KP_MAX_CLASS_KEYS;
         for (int q = 0; q < KP_MAX_CLASS_KEYS; q++) {
             const int k = mk[q];
@@ -1037,7 +1090,7 @@ __device__ __forceinline__ bool eval_fits_only(const KpDev& d, const EvalEnv& E,
         }
     }
     if (lane < TW) ws.opts[lane] = newword;
-    wit.finish(d, E, tot, (E.min_tmpl_mask >> a.tmpl) & 1u, ws, lane);
+    wit.finish(d, E, tot, (E.min_tmpl_mask >> a.tmpl) & 1ull, ws, lane);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     return true;
 }

@@ -425,7 +425,8 @@ struct kp_ctx {
     int P = 0, C = 0, NT = 0, K = 0, DW = 0;
     std::vector<int> tmpl_np;                // template → input nodepool index
     std::vector<int64_t> h_remaining;        // NodePool limits at solve start (re-applied by every execute)
-    DBuf<uint32_t> d_kflags, d_cls_flags, d_tol;
+    DBuf<uint32_t> d_kflags, d_cls_flags;
+    DBuf<uint64_t> d_tol;
     DBuf<ReqHdr> d_ex_hdr0, d_ex_hdr;
     DBuf<uint64_t> d_ex_words0, d_ex_words, d_ex_tol, d_XT;
     DBuf<int64_t> d_ex_avail, d_ex_req, d_ex_head;
@@ -455,7 +456,8 @@ struct kp_ctx {
     // kp_solve_prepare's per-pod host arrays, kept across calls
     std::vector<int32_t> h_uid_p;
     std::vector<uint64_t> h_uid_k;
-    int nc_cap = KP_NC_FIRST;                // in-flight NodeClaim capacity of the next solve prepare (grown by kp_solve)
+    int nc_cap_once = 0;                     // > 0: the next prepare plans for this many NodeClaims (after an overflow)
+    int last_plan_nc = 0;                    // in-flight NodeClaim capacity of the last prepare
     bool nc_overflow = false;                // the last fetch found the solve out of in-flight NodeClaim capacity
     DBuf<uint64_t> d_pend_bits, d_pbits;
     DBuf<uint64_t> d_init;
@@ -538,6 +540,10 @@ struct kp_ctx {
     std::vector<std::vector<int>> cons_hlost;
     std::vector<int32_t> h_tpos0;
     DBuf<int32_t> d_hpos0, d_tg_ha, d_ring_cls, d_ring_shape;
+    DBuf<uint64_t> d_nc_cls;  // [NCcap][CWc] absorbed classes per NodeClaim (KpDev::nc_cls)
+    DBuf<uint32_t> d_g_key;  // HBM slice arrays of node-dense plans (KpDev::g_key ...)
+    DBuf<uint16_t> d_g_ord, d_g_last;
+    DBuf<uint8_t> d_g_tmpl;
     DBuf<KpDev> d_self;  // device copy of dev for out-of-line kernel helpers (KpDev::self)
     std::vector<uint64_t> h_tknown_dg;       // [G] buildDomainGroups' domains (before any pod is counted)
     DBuf<int32_t> d_dec_soff, d_dec_moff, d_dec_g, d_dec_v, d_pt_cnt, d_pt_hd;
@@ -1493,7 +1499,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         return strcmp(in->nodepools[a].name, in->nodepools[b].name) < 0;
     });
     const int NT = (int)npo.size();
-    if (NT > 31) return fail(ctx, KP_E_UNSUPPORTED, "more than 31 NodePools");
+    if (NT > KP_MAX_NP) return fail(ctx, KP_E_UNSUPPORTED, "more than 63 NodePools");
     if (C + NT >= 65535) return fail(ctx, KP_E_UNSUPPORTED, "too many pod classes");
     std::vector<std::map<int, HReq>> treq(NT);
     for (int j = 0; j < NT; j++) {
@@ -1673,7 +1679,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
             }
     }
     // ---- templates: taints, daemon overhead, limits, instance-type rows ----
-    std::vector<uint32_t> tol(std::max(C, 1), 0);
+    std::vector<uint64_t> tol(std::max(C, 1), 0);
     std::vector<int64_t> daemon((size_t)NT * R, 0), remaining((size_t)NT * R, 0);
     std::vector<uint8_t> limit_set((size_t)NT * R, 0);
     std::vector<uint64_t> rows((size_t)NT * TW, 0);
@@ -1684,7 +1690,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
             bool all = true;
             for (int q = 0; q < np.n_taints && all; q++)
                 all = tolerates(np.taints[q], in->classes[i].tolerations, in->classes[i].n_tolerations);
-            if (all) tol[i] |= 1u << j;
+            if (all) tol[i] |= 1ull << j;
         }
         for (int r = 0; r < R; r++) {
             if (np.daemon_overhead) daemon[(size_t)j * R + r] = np.daemon_overhead[r];
@@ -1926,13 +1932,33 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     HIPCHK(c->d_sort_fields.upload(fields, (size_t)P * 4, s));
     HIPCHK(c->d_empty_hdr.upload(empty_hdr, s));
     HIPCHK(c->d_empty_words.upload(empty_words, s));
-    // in-flight NodeClaim capacity: KP_NC_FIRST, or up to KP_MAX_NC after a solve of this ctx overflowed it (kp_solve)
-    const int NCcap = std::min(std::min(c->nc_cap, KP_MAX_NC), std::max(P, 1));
+    // in-flight NodeClaim capacity.  A self-selecting hostname anti-affinity (required, or preferred under Respect: each
+    // pod takes a new NodeClaim before anything is relaxed) puts every pod of its class on a host of its own, a
+    // self-selecting hostname spread at most maxSkew per host: when that lower bound exceeds the first plan
+    // (KP_NC_FIRST), the solve is planned for it from the start, so a node-dense Deployment runs one execute.  A solve
+    // that still overflows (kp_solve_fetch) makes the next prepare of this ctx, and only that one, plan for every pod.
+    int64_t dense = 0;
+    {
+        std::vector<int64_t> ccount(std::max(C, 1), 0);
+        for (int p = 0; p < P; p++) ccount[in->pods.class_id[p]]++;
+        for (const HGroup& g : th.g)
+            if (!g.inverse && g.host && g.owner >= 0 && g.owner < C && g.sel[g.owner]) {
+                if (g.type == KP_TOPO_ANTI_AFFINITY) dense += ccount[g.owner];
+                else if (g.type == KP_TOPO_SPREAD && g.skew > 0) dense += (ccount[g.owner] + g.skew - 1) / g.skew;
+            }
+    }
+    int64_t plan = c->nc_cap_once > 0 ? c->nc_cap_once : KP_NC_FIRST;
+    c->nc_cap_once = 0;
+    if (dense + dense / 8 + 64 > plan) plan = dense + dense / 8 + 64;
+    const int NCcap = (int)std::min<int64_t>(std::min<int64_t>(plan, KP_MAX_NC), std::max(P, 1));
+    c->last_plan_nc = NCcap;
     HIPCHK(c->d_nc_hdr.ensure((size_t)NCcap * K));
     HIPCHK(c->d_nc_words.ensure((size_t)NCcap * DW));
     HIPCHK(c->d_nc_opts.ensure((size_t)NCcap * TW));
     HIPCHK(c->d_nc_req.ensure((size_t)NCcap * R));
     HIPCHK(c->d_nc_tmpl.ensure(NCcap));
+    const int CWc = std::max(1, (C + 63) / 64);
+    HIPCHK(c->d_nc_cls.ensure((size_t)NCcap * CWc));
     HIPCHK(c->d_nc_held.ensure(NCcap));
     HIPCHK(c->d_nc_rlive.ensure(NCcap));
     HIPCHK(c->d_qbuf.ensure(std::max(P, 1)));
@@ -2237,6 +2263,8 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.nc_opts = c->d_nc_opts.p;
     d.nc_req = c->d_nc_req.p;
     d.nc_tmpl = c->d_nc_tmpl.p;
+    d.nc_cls = c->d_nc_cls.p;
+    d.CWc = CWc;
     d.empty_hdr = c->d_empty_hdr.p;
     d.empty_words = c->d_empty_words.p;
     d.qbuf = c->d_qbuf.p;
@@ -2256,6 +2284,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.profile = getenv("KPSIM_PROFILE") ? 1 : 0;
     // topology pods: candidates per block round (KPSIM_TOPO_CANDS, diagnostics)
     d.topo_cands = getenv("KPSIM_TOPO_CANDS") ? std::max(1, std::min(KP_NWAVES, atoi(getenv("KPSIM_TOPO_CANDS")))) : KP_NWAVES;
+    d.team_eval = getenv("KPSIM_NO_TEAM") ? 0 : 1;  // diagnostics: KPSIM_NO_TEAM=1 evaluates topology candidates one per wave
     // KPSIM_TRACE_POD=p traces pod p; KPSIM_TRACE_CLASS=c traces every slow-path pod of class c (trace_pod = -2 - c)
     d.trace_pod = getenv("KPSIM_TRACE_POD") ? atoi(getenv("KPSIM_TRACE_POD"))
                   : getenv("KPSIM_TRACE_CLASS") ? -2 - atoi(getenv("KPSIM_TRACE_CLASS")) : -1;
@@ -2306,6 +2335,15 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
             for (int t = 0; t < T; t++) act[(size_t)ai * TP + t] = c->alloc_rt[(size_t)d.active_axes[ai] * T + t];
         HIPCHK(c->d_alloc_stage.upload(act, s));
         d.alloc_act = c->d_alloc_stage.p;
+        // HBM slice arrays, used when the plan holds more NodeClaims than LDS (kp_ffd_plan_lds)
+        HIPCHK(c->d_g_key.ensure(NCcap));
+        HIPCHK(c->d_g_ord.ensure(NCcap));
+        HIPCHK(c->d_g_last.ensure(NCcap));
+        HIPCHK(c->d_g_tmpl.ensure(NCcap));
+        d.g_key = c->d_g_key.p;
+        d.g_ord = c->d_g_ord.p;
+        d.g_last = c->d_g_last.p;
+        d.g_tmpl = c->d_g_tmpl.p;
     }
     if (!kp_ffd_plan_lds(d, KP_LDS_BYTES)) return fail(ctx, KP_E_UNSUPPORTED, "FFD kernel LDS plan exceeds 160 KB");
     c->P = P;
@@ -2412,7 +2450,10 @@ extern "C" kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out) {
     HIPCHK(hipMemcpyAsync(st, c->d_stats.p, sizeof st, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     c->nc_overflow = err == 1;
-    if (err == 1) return fail(ctx, KP_E_UNSUPPORTED, "in-flight NodeClaim capacity exceeded");
+    if (err == 1) {
+        c->nc_cap_once = std::min(KP_MAX_NC, std::max(c->P, 1));  // the next prepare plans for every pod, once
+        return fail(ctx, KP_E_UNSUPPORTED, "in-flight NodeClaim capacity exceeded");
+    }
     if (err) return fail(ctx, KP_E_STATE, "device solve loop exceeded its pop bound (internal error)");
     const int P = c->P, M = c->M;
     std::vector<int32_t> npods(N), spos(N), nopts(N), valid(N), ntypes(N), tmpl(N), types((size_t)N * M), pres(P), pord(P);
@@ -2451,6 +2492,11 @@ extern "C" kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out) {
     for (int i = 0; i < 11; i++) c->cycles[19 + i] = st[ST_N_NOINV + i];
     for (int i = 0; i < 3; i++) c->cycles[30 + i] = st[ST_TOPO_QUICK + i];
     for (int i = 0; i < 4; i++) c->cycles[33 + i] = st[ST_REJ_REQ + i];
+    if (getenv("KPSIM_PROFILE") && st[ST_TQ_WHY] + st[ST_TQ_WHY + 1] + st[ST_TQ_WHY + 2] + st[ST_TQ_WHY + 3] + st[ST_TQ_WHY + 4])
+        fprintf(stderr, "[kpsim] topology pods past the prefilter: no survivor %lld, not QREC %lld, no quick row %lld, class not "
+                        "absorbed %lld, quick row %lld (witness fits %lld); NQ %d of %d NodeClaims\n",
+                (long long)st[ST_TQ_WHY], (long long)st[ST_TQ_WHY + 1], (long long)st[ST_TQ_WHY + 2], (long long)st[ST_TQ_WHY + 3],
+                (long long)st[ST_TQ_WHY + 4], (long long)st[ST_TQ_WHY + 5], c->dev.lds_nq, N);
     so.ns_host_prep = c->ns_prep;
     so.ns_device_solve = c->ns_exec;
     if (N > out->cap_nodeclaims || n_ids > out->cap_type_ids) return fail(ctx, KP_E_BUFFER, "output buffers too small");
@@ -2488,19 +2534,17 @@ extern "C" kp_status kp_last_kernel_times(kp_ctx* ctx, double* ms, int32_t n) {
 }
 
 extern "C" kp_status kp_solve(kp_ctx* ctx, const kp_solve_input* in, kp_solve_output* out) {
-    for (;;) {
+    for (int attempt = 0;; attempt++) {
         kp_status st = kp_solve_prepare(ctx, in);
         if (st != KP_OK) return st;
         st = kp_solve_execute(ctx);
         if (st != KP_OK) return st;
         st = kp_solve_fetch(ctx, out);
-        // more in-flight NodeClaims than the first plan holds (e.g. a large hostname anti-affinity Deployment): prepare
-        // again with room for up to KP_MAX_NC (the ctx keeps the larger capacity for its later solves)
+        // more in-flight NodeClaims than the plan holds (the prepare's node-dense estimate missed): one more run planned
+        // for every pod (kp_solve_fetch set it up for the next prepare only; later solves start from the first plan)
         const int want = std::min(KP_MAX_NC, std::max(in->pods.n_pods, 1));
-        if (st == KP_E_UNSUPPORTED && ctx->nc_overflow && ctx->nc_cap < want) {
-            ctx->nc_cap = want;
-            continue;
-        }
+        if (st == KP_E_UNSUPPORTED && ctx->nc_overflow && attempt == 0 && ctx->last_plan_nc < want) continue;
+        ctx->nc_cap_once = 0;
         return st;
     }
 }
@@ -2619,7 +2663,6 @@ static kp_status cons_prepare_one(kp_ctx* ctx, const kp_consolidate_input* in) t
         return fail(ctx, KP_E_UNSUPPORTED, "consolidation with NotIn/DoesNotExist pod requirements on keys some node lacks "
                                            "and other pods select positively is not supported by this build (" +
                                                c->cons_mayfix_key + ")");
-    if (d.n_active > KP_LDS_AXES) return fail(ctx, KP_E_UNSUPPORTED, "more than 6 requested resource axes");
     if (d.M <= 0 || d.M > 64) return fail(ctx, KP_E_UNSUPPORTED, "consolidation needs max_instance_types in 1..64");
     const int T = c->T, TW = c->TW, R = c->R, A = d.n_active;
     hipStream_t s = c->stream;
@@ -2889,6 +2932,7 @@ static kp_status cons_run(kp_ctx* ctx, int m0, int m1, int s0, int s1, kp_probe_
     k.stats = c->d_cons_stats.p;
     k.profile = getenv("KPSIM_PROFILE") ? 1 : 0;
     k.no_fast = getenv("KPSIM_CONS_NOFAST") ? atoi(getenv("KPSIM_CONS_NOFAST")) : 0;  // 1: FULL only, 2: fast only
+    if (A > KP_LDS_AXES) k.no_fast = 1;  // more requested axes than the probe registers hold: the FULL variant's serial path
     k.prof_probe = nullptr;
     if (k.profile) {
         HIPCHK(c->d_prof_probe.ensure((size_t)nprobe * 8));

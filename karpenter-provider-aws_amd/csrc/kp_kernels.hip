@@ -132,7 +132,7 @@ __global__ __launch_bounds__(64) void template_init_kernel(KpDev d) {
     E.slot_ct = d.slot_ct;
     E.slot_zoneid = d.slot_zoneid;
     E.roles = &roles;
-    E.min_tmpl_mask = d.min_keys[(size_t)j * KP_MAX_CLASS_KEYS] >= 0 ? (1u << j) : 0u;
+    E.min_tmpl_mask = d.min_keys[(size_t)j * KP_MAX_CLASS_KEYS] >= 0 ? (1ull << j) : 0ull;
     E.ro = d.ro;
     E.type_ro = d.type_ro;
     E.rcap = nullptr;
@@ -164,6 +164,7 @@ struct FfdShared {
     int64_t qw_req[64][KP_MAX_R];  // requests of the queue window's pods
     int fastp[2][KP_NWAVES];
     WaveScratch ws[KP_NWAVES];
+    TeamBuf team[2];               // topology pods: the block evaluates one candidate at a time (eval_wave TEAM)
     ClassCache CC;
     Roles roles;
     int slot_zone[KP_MAX_SLOTS], slot_ct[KP_MAX_SLOTS], slot_zoneid[KP_MAX_SLOTS];
@@ -183,7 +184,7 @@ struct FfdShared {
     int epoch;                     // lastLen generation: Queue.Push(pod, relaxed = true) clears lastLen
     int relaxed;                   // a pod relaxed since wave 0 last loaded its queue window (its lastLens are stale)
     int xstart;                    // every existing node < xstart has rejected the current shape
-    uint32_t cur_tol;              // tolerations word of the current shape's class (bit 31: no requirement keys)
+    uint64_t cur_tol;              // tolerations word of the current shape's class (bit 63: no requirement keys)
     int32_t cur_pq[KP_LDS_AXES];   // scaled quick-accept requests of the current shape
     int64_t shape_req[KP_MAX_R];   // requests of the current shape (pending-total flush)
     long long st[ST_COUNT];
@@ -279,10 +280,11 @@ __device__ __forceinline__ bool topo_prefilter_pass(const KpDev& d, const FfdSha
     return ok;
 }
 
-// wave 0: the first slice position in [start, N) that has not rejected the shape and passes the topology prefilter
-// (N if none).  Four 64-position chunks per round so the prefilter's global loads of 256 NodeClaims overlap.
-__device__ inline int topo_scan(const KpDev& d, const FfdShared& S, const uint32_t* skey, const uint16_t* sord, int N,
-                                int start, int lane) {
+// wave 0: the first slice position in [start, N) that has not rejected the shape, whose template's taints the class
+// tolerates (tol: bit j = template j) and that passes the topology prefilter (N if none).  Four 64-position chunks per
+// round so the prefilter's global loads of 256 NodeClaims overlap.
+__device__ inline int topo_scan(const KpDev& d, const FfdShared& S, const uint32_t* skey, const uint16_t* sord,
+                                const uint8_t* stmpl, uint64_t tol, int N, int start, int lane) {
     for (int base = start; base < N; base += 256) {
         bool ok[4];
         int nc[4];
@@ -291,6 +293,7 @@ __device__ inline int topo_scan(const KpDev& d, const FfdShared& S, const uint32
             const int p = base + u * 64 + lane;
             ok[u] = p < N && !(skey[p] >> 31);
             nc[u] = ok[u] ? (int)sord[p] : 0;
+            ok[u] = ok[u] && ((tol >> stmpl[nc[u]]) & 1ull);
         }
         for (int e = 0; e < S.tp_n; e++) {
             const int k = S.tp_k[e];
@@ -351,7 +354,7 @@ __device__ inline void topo_record_quick(const KpDev& d, int c, int nc, int tmpl
         const int4 info = d.tg_info[g];
         const int type = info.x & TG_TYPE;
         const bool inv = info.x & TG_INVERSE;
-        if (!inv && type == 0 && (d.tg_pol[g] & 2) && !((d.tol[d.tg_owner[g]] >> tmpl) & 1u)) continue;
+        if (!inv && type == 0 && (d.tg_pol[g] & 2) && !((d.tol[d.tg_owner[g]] >> tmpl) & 1ull)) continue;
         if (info.x & TG_HOST) {
             if (lane == 0) {
                 const int old = atomicAdd(&d.tg_hcnt[(size_t)d.tg_hrow[g] * d.HN + d.E + nc], 1);
@@ -370,10 +373,11 @@ __device__ inline void topo_record_quick(const KpDev& d, int c, int nc, int tmpl
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// wave 0: collect up to KP_NWAVES slice positions >= start whose NodeClaim has not rejected the current shape (and
-// passes the topology prefilter of the current pod)
-__device__ inline void collect_candidates(const KpDev& d, FfdShared& S, const uint32_t* key, const uint16_t* ord, int N,
-                                          int start, int buf, int lane) {
+// wave 0: collect up to KP_NWAVES slice positions >= start whose NodeClaim has not rejected the current shape, whose
+// template's taints the pod's class tolerates (NodeClaim.Add's first test; tol bit j = template j) and that passes the
+// topology prefilter of the current pod
+__device__ inline void collect_candidates(const KpDev& d, FfdShared& S, const uint32_t* key, const uint16_t* ord,
+                                          const uint8_t* stmpl, uint64_t tol, int N, int start, int buf, int lane) {
     int cnt = 0, pos = start, next = N;
     // topology pods: at most d.topo_cands candidates per round (the first prefilter survivor usually accepts; fewer waves
     // evaluating leaves each its own SIMD)
@@ -381,6 +385,7 @@ __device__ inline void collect_candidates(const KpDev& d, FfdShared& S, const ui
     while (pos < N) {
         const int p = pos + lane;
         bool c = p < N && !(key[p] >> 31);
+        if (c) c = (tol >> stmpl[ord[p]]) & 1ull;
         if (S.tp_n && c) c = topo_prefilter_pass(d, S, ord[p]);
         const uint64_t m0 = __ballot(c);
         if (S.tp_n && m0 && cnt + __popcll(m0) < L) {
@@ -440,6 +445,13 @@ __device__ inline uint64_t limit_filter(const KpDev& d, int j, uint64_t o, int l
 }
 
 __device__ __forceinline__ long long prof_clock(const KpDev& d) { return d.profile ? __builtin_amdgcn_s_memtime() : 0; }
+
+// NodeClaim nc has absorbed a pod of class c at some point (d.nc_cls): its requirements are a subset of c's, so the
+// requirement merge of another pod of c leaves them unchanged (Intersection is idempotent) and every option stays
+// compatible with c — the premise of the quick accepts, which before only looked at the last absorbed class.
+__device__ __forceinline__ bool nc_absorbed(const KpDev& d, int nc, int c) {
+    return (ld_u64(&d.nc_cls[(size_t)nc * d.CWc + (c >> 6)]) >> (c & 63)) & 1ull;
+}
 
 // The winner's reservations (one lane): ReservationManager.Reserve for the IDs newly held, Release for the IDs the
 // Add no longer holds (NodeClaim.Add's reservedOfferings update), then the NodeClaim's held set and liveness.
@@ -510,15 +522,18 @@ __device__ __attribute__((noinline)) int existing_topo_scan(const KpDev* __restr
 
 // PREF: the solve relaxes preferences or runs MIN_VALUES_POLICY=BestEffort; false compiles that code out, so the
 // common instantiations keep the register plan they had without it.
-template <bool RESV, bool TOPO, bool PREF>
+// HBM: the slice arrays (9 B per in-flight NodeClaim) live in HBM (d.g_key ...) because the solve is planned for more
+// NodeClaims than LDS holds beside the fixed tables (kp_ffd_plan_lds sets d.slice_hbm); other instantiations keep them
+// in LDS and address them with ds instructions.
+template <bool RESV, bool TOPO, bool PREF, bool HBM = false>
 __device__ __forceinline__ void ffd_solve(KpDev d) {
     constexpr bool TOPO_ON = KP_TOPO_ON && TOPO;  // the solve has topology groups
     extern __shared__ __attribute__((aligned(16))) char smem[];
     FfdShared& S = *reinterpret_cast<FfdShared*>(smem);
-    uint32_t* const skey = reinterpret_cast<uint32_t*>(smem + d.off_key);   // len(Pods) by slice position
-    uint16_t* const sord = reinterpret_cast<uint16_t*>(smem + d.off_ord);   // NodeClaim id by slice position
-    uint16_t* const slast = reinterpret_cast<uint16_t*>(smem + d.off_last); // last absorbed class by NodeClaim id
-    uint8_t* const stmpl = reinterpret_cast<uint8_t*>(smem + d.off_tmpl);   // template by NodeClaim id
+    uint32_t* const skey = HBM ? d.g_key : reinterpret_cast<uint32_t*>(smem + d.off_key);    // len(Pods) by slice position
+    uint16_t* const sord = HBM ? d.g_ord : reinterpret_cast<uint16_t*>(smem + d.off_ord);    // NodeClaim id by slice position
+    uint16_t* const slast = HBM ? d.g_last : reinterpret_cast<uint16_t*>(smem + d.off_last); // last absorbed class by NodeClaim id
+    uint8_t* const stmpl = HBM ? d.g_tmpl : reinterpret_cast<uint8_t*>(smem + d.off_tmpl);   // template by NodeClaim id
     int64_t* const sAlloc = reinterpret_cast<int64_t*>(smem + d.off_alloc);
     uint64_t* const sAvail = reinterpret_cast<uint64_t*>(smem + d.off_avail);
     uint16_t* const sMulti = reinterpret_cast<uint16_t*>(smem + d.off_multi);
@@ -614,9 +629,9 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
     E.rcap = sRcap;
     E.resv_on = RESV ? d.resv_on : 0;  // provisioning: ReservedOfferingModeStrict (eval_wave's STRICT default)
     {
-        uint32_t mmask = 0;
+        uint64_t mmask = 0;
         for (int j = 0; j < d.NT; j++)
-            if (d.min_keys[(size_t)j * KP_MAX_CLASS_KEYS] >= 0) mmask |= 1u << j;
+            if (d.min_keys[(size_t)j * KP_MAX_CLASS_KEYS] >= 0) mmask |= 1ull << j;
         E.min_tmpl_mask = mmask;
     }
     SortSlice sl{skey, sord};
@@ -635,7 +650,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
     //     vq[a] = ceil(request[axis a] >> qshift[a]) for the quick-accept axes (clamped to int32).
     int qw_n = 0, qw_used = 0;
     int vp = 0, vc = 0, vshape = 0, vlast = 0;
-    uint32_t vtol = 0;
+    uint64_t vtol = 0;
     int32_t vq[KP_LDS_AXES];
 #pragma unroll
     for (int ai = 0; ai < KP_LDS_AXES; ai++) vq[ai] = 0;
@@ -685,7 +700,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
             int c = S.cur_cls;
             // the current shape's class carries topology (CF_TOPO): such pods are handled by the block
             bool ctopo = TOPO_ON && c >= 0 && (d.cls_flags[c] & CF_TOPO);
-            uint32_t tl = S.cur_tol;
+            uint64_t tl = S.cur_tol;
             int pq[KP_LDS_AXES];
 #pragma unroll
             for (int ai = 0; ai < KP_LDS_AXES; ai++) pq[ai] = S.cur_pq[ai];
@@ -703,7 +718,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
 #pragma unroll
             for (int ai = 0; ai < KP_LDS_AXES; ai++) wh[ai] = -1;
             auto absorbed = [&](uint32_t m) -> bool {
-                return (int)(m & 0xFFFFu) == c || ((tl >> 31) && ((tl >> (m >> 16)) & 1u));
+                return (int)(m & 0xFFFFu) == c || ((tl >> 63) && ((tl >> (m >> 16)) & 1ull));
             };
             // write the window back to LDS and the pending request totals to HBM (same-shape requests are identical)
             auto win_flush = [&]() {
@@ -764,7 +779,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                         vc = d.pod_cls[vp];
                         vshape = d.pod_shape[vp];
                         vlast = (PREF && d.last_ep && d.last_ep[vp] != ep) ? -1 : d.last_len[vp];
-                        vtol = (d.tol[vc] & 0x7FFFFFFFu) | ((d.cls_flags[vc] & 4u) ? 0x80000000u : 0u);
+                        vtol = (d.tol[vc] & ~(1ull << 63)) | ((d.cls_flags[vc] & 4u) ? (1ull << 63) : 0ull);
                         for (int r = 0; r < R; r++) S.qw_req[lane][r] = d.pod_req[(size_t)vp * R + r];
 #pragma unroll
                         for (int ai = 0; ai < KP_LDS_AXES; ai++) {
@@ -801,7 +816,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                     }
                     c = rl32(vc, off);
                     ctopo = TOPO_ON && (d.cls_flags[c] & CF_TOPO) != 0;
-                    tl = (uint32_t)rl32((int)vtol, off);
+                    tl = rl64(vtol, off);
 #pragma unroll
                     for (int ai = 0; ai < KP_LDS_AXES; ai++) pq[ai] = rl32(vq[ai], off);
                     if (lane < R) S.shape_req[lane] = S.qw_req[off][lane];
@@ -1120,7 +1135,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                     S.cls_fill = S.CC.cls != c;  // decided before the barrier: fill_class_cache rewrites CC.cls
                     S.topo_pod = 0;
                 }
-                collect_candidates(d, S, skey, sord, N, f, 0, lane);
+                collect_candidates(d, S, skey, sord, stmpl, ~0ull, N, f, 0, lane);
                 break;
             }
             win_flush();
@@ -1217,13 +1232,23 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 if (cfl & CF_TOPO_CONS) topo_prefilter_setup(d, S, c, lane);
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 const long long t1 = prof_clock(d);
-                const int f = topo_scan(d, S, skey, sord, N, S.scan_start, lane);
+                const uint64_t ctol = d.tol[c];
+                const int f = topo_scan(d, S, skey, sord, stmpl, ctol, N, S.scan_start, lane);
                 const long long t2 = prof_clock(d);
                 bool quick = false;
+                if (d.profile && lane == 0) {  // KPSIM_PROFILE: why the topology quick accept does not apply
+                    const int nc = f < N ? sord[f] : 0;
+                    const int why = f >= N ? 0 : !(cfl & CF_TOPO_QREC) ? 1 : nc >= NQ ? 2
+                                  : !(slast[nc] == (uint16_t)c || nc_absorbed(d, nc, c) ||
+                                      ((cfl & CF_NOKEYS) && ((d.tol[c] >> stmpl[nc]) & 1ull))) ? 3 : 4;
+                    S.st[ST_TQ_WHY + why]++;
+                }
                 if (f < N && (cfl & CF_TOPO_QREC) && A > 0) {
                     const int nc = sord[f], tm = stmpl[nc];
-                    bool ok = nc < NQ && (slast[nc] == (uint16_t)c || ((cfl & CF_NOKEYS) && ((d.tol[c] >> tm) & 1u)));
+                    bool ok = nc < NQ && (slast[nc] == (uint16_t)c || ((cfl & CF_NOKEYS) && ((d.tol[c] >> tm) & 1ull)) ||
+                                          nc_absorbed(d, nc, c));
                     for (int ai = 0; ai < A && ok; ai++) ok = S.cur_pq[ai] <= shr[ai * NQ + nc];
+                    if (d.profile && lane == 0 && nc < NQ && ok) S.st[ST_TQ_WHY + 5]++;  // witness fits
                     quick = ok && topo_pinned(d, S, nc);
                     if (quick) {
                         if (lane < A) shr[lane * NQ + nc] -= S.cur_pq[lane];
@@ -1243,7 +1268,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     }
                 }
-                if (!quick) collect_candidates(d, S, skey, sord, N, f, 0, lane);
+                if (!quick) collect_candidates(d, S, skey, sord, stmpl, ctol, N, f, 0, lane);
                 if (lane == 0) {
                     S.topo_quick = quick;
                     if (d.profile) {
@@ -1266,6 +1291,9 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
 
         // ================= in-flight NodeClaims in slice order: first whose Add succeeds =================
         int round = 0, win = -1;
+        // a pod with topology terms: its candidates one at a time, each evaluated by the whole block (the type sweep
+        // split over the waves; the first candidate that passes the prefilter usually accepts), in slice order
+        const bool team = TOPO_ON && S.topo_pod && d.team_eval;
         if (d.trace && pod == d.trace_pod && wave == 0) {  // diagnostics: the slice as the slow path sees it
             int* sl = d.trace + 1 + 6 * KP_TRACE_N;
             if (lane == 0) {
@@ -1278,7 +1306,50 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 sl[4 + 2 * i] = (int)skey[i];
             }
         }
-        for (;;) {
+        for (int ti = 0; team;) {
+            const int b = round & 1;
+            const int n = S.n_cand[b];
+            for (int i = 0; i < n; i++, ti++) {
+                const int nc = sord[S.cand_pos[b][i]];
+                EvalIn a;
+                a.Ahdr = d.nc_hdr + (size_t)nc * K;
+                a.Aw = d.nc_words + (size_t)nc * d.DW;
+                a.opts = lane < TW ? d.nc_opts[(size_t)nc * TW + lane] : 0;
+                a.base_req = d.nc_req + (size_t)nc * R;
+                a.pod_req = S.pod_req;
+                a.tmpl = d.nc_tmpl[nc];
+                a.compat = true;
+                a.force_off = false;
+                a.prof = (d.profile && wave == 0) ? &S.st[ST_EV_REQ] : nullptr;
+                a.host = d.E + nc;
+                a.held = (RESV && d.resv_on) ? ld_u64(&d.nc_held[nc]) : 0ull;
+                const bool ok = (S.CC.flags & CF_TOPO_CONS)
+                                    ? eval_wave<true, RESV, true, PREF, false, true>(d, E, S.CC, a, S.ws[wave], lane, &S.team[ti & 1],
+                                                                                     wave, KP_NWAVES)
+                                    : eval_wave<false, RESV, true, PREF, false, true>(d, E, S.CC, a, S.ws[wave], lane,
+                                                                                      &S.team[ti & 1], wave, KP_NWAVES);
+                if (wave == 0 && lane == 0) {
+                    S.fastp[b][i] = 0;
+                    S.acc[b][i] = ok;
+                    if (!ok && S.ws[0].memo_ok) {  // as below: rejected this shape for good
+                        skey[S.cand_pos[b][i]] |= 0x80000000u;
+                        S.any_rej = 1;
+                    }
+                    if (!ok && !S.ws[0].memo_ok) S.rej_volatile = 1;
+                    S.st[ST_NC_EVALS]++;
+                }
+                if (ok) {
+                    win = i;
+                    break;
+                }
+            }
+            if (win >= 0 || S.scan_done[b]) break;
+            if (wave == 0)
+                collect_candidates(d, S, skey, sord, stmpl, S.topo_pod ? d.tol[S.cur_cls] : ~0ull, S.N, S.scan_next[b], b ^ 1, lane);
+            __syncthreads();
+            round++;
+        }
+        for (; !team;) {
             const int b = round & 1;
             if (wave < S.n_cand[b]) {
                 const int nc = sord[S.cand_pos[b][wave]];
@@ -1296,7 +1367,8 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 a.held = (RESV && d.resv_on) ? ld_u64(&d.nc_held[nc]) : 0ull;
                 // a NodeClaim that keeps reserved offerings re-runs the whole Add (its reservations are recomputed)
                 const bool fast = !(S.CC.flags & CF_TOPO) && !(RESV && d.resv_on && ld_i32(&d.nc_rlive[nc])) &&
-                                  (slast[nc] == (uint16_t)S.cur_cls || ((S.CC.flags & CF_NOKEYS) && ((S.CC.tol >> a.tmpl) & 1u)));
+                                  (slast[nc] == (uint16_t)S.cur_cls || ((S.CC.flags & CF_NOKEYS) && ((S.CC.tol >> a.tmpl) & 1ull)) ||
+                                   nc_absorbed(d, nc, S.cur_cls));
                 if (fast && lane == 0) S.ws[wave].memo_ok = 1;
                 const bool ok = fast ? eval_fits_only<PREF>(d, E, a, S.ws[wave], lane)
                                 : (TOPO_ON && (S.CC.flags & CF_TOPO_CONS)) ? eval_wave<true, RESV, true, PREF>(d, E, S.CC, a, S.ws[wave], lane)
@@ -1335,7 +1407,8 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 }
             if (tid == 0) S.st[ST_NC_EVALS] += nc_;
             if (win >= 0 || S.scan_done[b]) break;
-            if (wave == 0) collect_candidates(d, S, skey, sord, S.N, S.scan_next[b], b ^ 1, lane);
+            if (wave == 0)
+                collect_candidates(d, S, skey, sord, stmpl, S.topo_pod ? d.tol[S.cur_cls] : ~0ull, S.N, S.scan_next[b], b ^ 1, lane);
             __syncthreads();
             round++;
         }
@@ -1344,26 +1417,28 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
             S.st[ST_CYC_SCAN] += t1 - c_slow;
         }
         if (win >= 0) {
-            if (wave == win) {
+            const int cw = team ? 0 : win;  // the wave whose scratch holds the accepted Add (team: every wave's does)
+            if (wave == cw) {
                 const int pos = S.cand_pos[round & 1][win];
                 const int nc = sord[pos];
                 if (!S.fastp[round & 1][win]) {
-                    commit_reqs(d, S.CC, S.ws[win], nc, lane);
-                    if (RESV && d.resv_on && lane == 0) commit_reservations(d, sRcap, S.ws[win], nc, ld_u64(&d.nc_held[nc]), &S.rel_flag);
+                    commit_reqs(d, S.CC, S.ws[cw], nc, lane);
+                    if (RESV && d.resv_on && lane == 0) commit_reservations(d, sRcap, S.ws[cw], nc, ld_u64(&d.nc_held[nc]), &S.rel_flag);
                 }
                 if (PREF && d.best_effort) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // commit_reqs' header rows have landed
-                    commit_min_relax(d, S.ws[win], nc, lane);
+                    commit_min_relax(d, S.ws[cw], nc, lane);
                 }
                 if (TOPO_ON && (S.CC.flags & CF_TOPO))
-                    topo_record(d, S.CC, S.ws[win], d.nc_hdr + (size_t)nc * K, d.nc_words + (size_t)nc * d.DW,
+                    topo_record(d, S.CC, S.ws[cw], d.nc_hdr + (size_t)nc * K, d.nc_words + (size_t)nc * d.DW,
                                 d.E + nc, d.nc_tmpl[nc], true, lane);
-                if (lane < TW) d.nc_opts[(size_t)nc * TW + lane] = S.ws[win].opts[lane];
+                if (lane < TW) d.nc_opts[(size_t)nc * TW + lane] = S.ws[cw].opts[lane];
                 if (lane < R && S.pod_req[lane])
                     atomicAdd((unsigned long long*)&d.nc_req[(size_t)nc * R + lane], (unsigned long long)S.pod_req[lane]);
-                if (lane < A && nc < NQ) shr[lane * NQ + nc] = S.ws[win].hr[lane];
+                if (lane < A && nc < NQ) shr[lane * NQ + nc] = S.ws[cw].hr[lane];
                 if (lane == 0) {
                     slast[nc] = (uint16_t)S.cur_cls;
+                    atomicOr((unsigned long long*)&d.nc_cls[(size_t)nc * d.CWc + (S.cur_cls >> 6)], 1ull << (S.cur_cls & 63));
                     skey[pos]++;
                     S.dirty_kind = 1;
                     S.dirty_pos = pos;
@@ -1442,6 +1517,10 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                     if (wave == twin) {
                         const int jj = tb + wave;
                         const int n = S.N;
+                        // absorbed classes of the new NodeClaim: the pod's
+                        for (int i = lane; i < d.CWc; i += 64)
+                            __hip_atomic_store(&d.nc_cls[(size_t)n * d.CWc + i], i == (S.cur_cls >> 6) ? 1ull << (S.cur_cls & 63) : 0ull,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         // NewNodeClaim(template): requirements = template requirements, then the Add's merge
                         for (int k = lane; k < K; k += 64) d.nc_hdr[(size_t)n * K + k] = d.cls_hdr[(size_t)(d.C + jj) * K + k];
                         for (int i = lane; i < d.DW; i += 64)
@@ -1545,6 +1624,15 @@ __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_pref_kernel(KpDev d) { ffd
 __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_pref_topo_kernel(KpDev d) { ffd_solve<false, true, true>(d); }
 __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_pref_resv_kernel(KpDev d) { ffd_solve<true, false, true>(d); }
 __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_pref_resv_topo_kernel(KpDev d) { ffd_solve<true, true, true>(d); }
+// node-dense solves (more in-flight NodeClaims than the LDS slice holds): the slice arrays in HBM
+__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_hbm_kernel(KpDev d) { ffd_solve<false, false, false, true>(d); }
+__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_topo_hbm_kernel(KpDev d) { ffd_solve<false, true, false, true>(d); }
+__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_resv_hbm_kernel(KpDev d) { ffd_solve<true, false, false, true>(d); }
+__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_resv_topo_hbm_kernel(KpDev d) { ffd_solve<true, true, false, true>(d); }
+__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_pref_hbm_kernel(KpDev d) { ffd_solve<false, false, true, true>(d); }
+__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_pref_topo_hbm_kernel(KpDev d) { ffd_solve<false, true, true, true>(d); }
+__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_pref_resv_hbm_kernel(KpDev d) { ffd_solve<true, false, true, true>(d); }
+__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_pref_resv_topo_hbm_kernel(KpDev d) { ffd_solve<true, true, true, true>(d); }
 
 // ------------------------------------------------------------------------------------------------
 // FinalizeScheduling + Truncate(OrderByPrice, maxInstanceTypes) + SatisfiesMinValues
@@ -1744,24 +1832,26 @@ bool kp_ffd_plan_lds(KpDev& d, int max_bytes) {
     // from HBM and as many slice entries as LDS holds (9 B per NodeClaim)
     int ncmax = d.NCcap < KP_MAX_NC ? d.NCcap : KP_MAX_NC;
     d.alloc_global = ncmax > KP_NC_FIRST && d.alloc_act != nullptr;
+    d.slice_hbm = 0;
     if (d.alloc_global) {
         const int tp0 = (d.T + 63) / 64 * 64;
-        const int nst = d.n_active < KP_LDS_AXES ? d.n_active : KP_LDS_AXES;
         size_t fixed = off + 8 * (size_t)tp0 + (d.multi16 ? 2 * (size_t)d.n_multi * tp0 : 0) +
                        (d.ro ? sizeof(ResvTab) + 4 * 64 : 0) + (d.G > 0 ? sizeof(TopoSnap) : 0) + 256;
-        (void)nst;
         const long room = ((long)max_bytes - (long)fixed) / 9;
-        if (room < ncmax) ncmax = room > 0 ? (int)room : 0;
+        // more NodeClaims than LDS holds beside the fixed tables: the slice arrays go to HBM (the HBM instantiations)
+        if (room < ncmax) d.slice_hbm = d.g_key != nullptr;
+        if (room < ncmax && !d.slice_hbm) ncmax = room > 0 ? (int)room : 0;
     }
     d.lds_ncmax = ncmax;
+    const size_t nsl = d.slice_hbm ? 0 : (size_t)ncmax;  // slice entries in LDS
     d.off_key = (int)off;
-    off = al(off + 4 * (size_t)ncmax);
+    off = al(off + 4 * nsl);
     d.off_ord = (int)off;
-    off = al(off + 2 * (size_t)ncmax);
+    off = al(off + 2 * nsl);
     d.off_last = (int)off;
-    off = al(off + 2 * (size_t)ncmax);
+    off = al(off + 2 * nsl);
     d.off_tmpl = (int)off;
-    off = al(off + (size_t)ncmax);
+    off = al(off + nsl);
     const int tp = (d.T + 63) / 64 * 64;
     d.lds_tpad = tp;
     d.lds_nstage = d.n_active < KP_LDS_AXES ? d.n_active : KP_LDS_AXES;
@@ -1809,9 +1899,13 @@ hipError_t kp_launch_template_init(const KpDev& d, hipStream_t s) {
 // Per-device kernel attributes: called by kp_ctx_create with the ctx's device current (every ctx, so a second ctx on
 // another device of the same process gets them too; the call is idempotent and needs no process-wide flag).
 hipError_t kp_ffd_set_attributes() {
-    const void* ks[8] = {(const void*)ffd_kernel, (const void*)ffd_topo_kernel, (const void*)ffd_resv_kernel,
-                         (const void*)ffd_resv_topo_kernel, (const void*)ffd_pref_kernel, (const void*)ffd_pref_topo_kernel,
-                         (const void*)ffd_pref_resv_kernel, (const void*)ffd_pref_resv_topo_kernel};
+    const void* ks[16] = {(const void*)ffd_kernel, (const void*)ffd_topo_kernel, (const void*)ffd_resv_kernel,
+                          (const void*)ffd_resv_topo_kernel, (const void*)ffd_pref_kernel, (const void*)ffd_pref_topo_kernel,
+                          (const void*)ffd_pref_resv_kernel, (const void*)ffd_pref_resv_topo_kernel,
+                          (const void*)ffd_hbm_kernel, (const void*)ffd_topo_hbm_kernel, (const void*)ffd_resv_hbm_kernel,
+                          (const void*)ffd_resv_topo_hbm_kernel, (const void*)ffd_pref_hbm_kernel,
+                          (const void*)ffd_pref_topo_hbm_kernel, (const void*)ffd_pref_resv_hbm_kernel,
+                          (const void*)ffd_pref_resv_topo_hbm_kernel};
     for (const void* k : ks) {
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, KP_LDS_BYTES);
         if (e != hipSuccess) return e;
@@ -1824,7 +1918,13 @@ hipError_t kp_launch_ffd(const KpDev& d, hipStream_t s) {
     // BestEffort minValues (PREF)
     const dim3 g(1), b(KP_NWAVES * 64);
     const bool pref = d.relax_next || d.best_effort;
-    if (pref) {
+    if (d.slice_hbm) {
+        void (*k)(KpDev) = pref ? (d.ro ? (d.G > 0 ? ffd_pref_resv_topo_hbm_kernel : ffd_pref_resv_hbm_kernel)
+                                        : (d.G > 0 ? ffd_pref_topo_hbm_kernel : ffd_pref_hbm_kernel))
+                                : (d.ro ? (d.G > 0 ? ffd_resv_topo_hbm_kernel : ffd_resv_hbm_kernel)
+                                        : (d.G > 0 ? ffd_topo_hbm_kernel : ffd_hbm_kernel));
+        hipLaunchKernelGGL(k, g, b, bytes, s, d);
+    } else if (pref) {
         if (d.ro && d.G > 0) hipLaunchKernelGGL(ffd_pref_resv_topo_kernel, g, b, bytes, s, d);
         else if (d.ro) hipLaunchKernelGGL(ffd_pref_resv_kernel, g, b, bytes, s, d);
         else if (d.G > 0) hipLaunchKernelGGL(ffd_pref_topo_kernel, g, b, bytes, s, d);

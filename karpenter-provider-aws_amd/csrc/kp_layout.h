@@ -21,6 +21,7 @@
 #define KP_MAX_KEYS 96               // label keys per solve
 #define KP_MAX_CLASS_KEYS 32         // label keys constrained by one pod class / template
 #define KP_MAX_SLOTS 64              // zone slots × capacity-type slots
+#define KP_MAX_NP 63                 // NodePools (templates) per solve: template bitmasks are u64, bit 63 a flag
 #define KP_MAX_R 16                  // resource axes
 #ifndef KP_NWAVES
 #define KP_NWAVES 8                  // waves in the single-workgroup FFD kernel
@@ -133,7 +134,7 @@ struct KpDev {
     const uint64_t* tmpl_rows;       // [NT][TW] GetInstanceTypes(nodepool) rows
     uint64_t* tmpl_opts;             // [NT][TW] NodeClaimTemplate.InstanceTypeOptions (template_init kernel)
     int32_t* tmpl_ok;                // [NT]
-    const uint32_t* tol;             // [C] bit j: class tolerates template j's taints
+    const uint64_t* tol;             // [C] bit j: class tolerates template j's taints (templates <= KP_MAX_NP)
     const int64_t* daemon;           // [NT][R]
     const uint8_t* limit_set;        // [NT][R]
     int64_t* remaining;              // [NT][R] (mutated by the FFD kernel)
@@ -162,6 +163,8 @@ struct KpDev {
     uint64_t* nc_opts;               // [NCcap][TW]
     int64_t* nc_req;                 // [NCcap][R]
     int32_t* nc_tmpl;                // [NCcap]
+    uint64_t* nc_cls;                // [NCcap][CWc] classes the NodeClaim has absorbed (bit per class)
+    int32_t CWc;                     // words of an nc_cls row: ceil(C / 64)
     const ReqHdr* empty_hdr;         // [K] all-undefined digest (template init)
     const uint64_t* empty_words;     // [DW]
     int32_t* qbuf;                   // [P] queue ring
@@ -182,6 +185,7 @@ struct KpDev {
     int32_t* err;                    // [1] device-side error code (capacity overflow etc.)
     int32_t profile;                 // accumulate per-stage evaluation cycles (diagnostics)
     int32_t topo_cands;              // NodeClaims evaluated per block round for a topology pod (<= KP_NWAVES)
+    int32_t team_eval;               // topology pods: one candidate at a time, evaluated by the whole block (eval_wave TEAM)
     int32_t trace_pod;               // diagnostics (KPSIM_TRACE_POD): the slow path logs this pod's evaluations
     int32_t trace_max;               //   KPSIM_TRACE_CLASS: only pods with index <= KPSIM_TRACE_MAXPOD
     int32_t* trace;                  //   [1 + 6 * KP_TRACE_N]: count, then {round, nodeclaim (-1-j: template j), ok, flags, held lo/hi}
@@ -228,6 +232,11 @@ struct KpDev {
     // Dynamic LDS after the fixed FfdShared block: slice arrays sized by lds_ncmax, the staged type tables
     // sized by lds_tpad, and the quick-accept headroom table hr[lds_A][lds_nq].
     int32_t lds_ncmax;               // in-flight NodeClaim capacity of the kernel (<= KP_MAX_NC, <= NCcap)
+    int32_t slice_hbm;               // the slice arrays are in HBM (g_key ...): more NodeClaims than LDS holds
+    uint32_t* g_key;                 // [NCcap] HBM slice arrays (allocated for plans above KP_NC_FIRST)
+    uint16_t* g_ord;
+    uint16_t* g_last;
+    uint8_t* g_tmpl;
     int32_t lds_tpad;                // staged-table row stride (T rounded up to 64)
     int32_t lds_nstage;              // allocatable axes staged in LDS
     int32_t lds_A;                   // quick-accept axes (= n_active when n_active <= KP_LDS_AXES, else 0)
@@ -261,5 +270,8 @@ enum {
     ST_N_NOINV = 32, ST_N_WINMOVE, ST_N_LDSSORT, ST_N_PIVOT, ST_N_WINLOAD, ST_N_FLUSH, ST_N_SHAPE, ST_EXIST_PLACED = 44,
     ST_TOPO_QUICK = 45, ST_CYC_TSETUP, ST_CYC_TSCAN,
     // KPSIM_PROFILE: why evaluations fail (requirement merge, topology narrowing, no type left, minValues, other)
-    ST_REJ_REQ = 48, ST_REJ_TOPO, ST_REJ_TYPES, ST_REJ_MIN, ST_COUNT = 52
+    ST_REJ_REQ = 48, ST_REJ_TOPO, ST_REJ_TYPES, ST_REJ_MIN,
+    // KPSIM_PROFILE: topology pods past the prefilter — no surviving NodeClaim, class records through another class's
+    // node filter (not QREC), NodeClaim without a quick row, class not absorbed, quick row present; witness fits
+    ST_TQ_WHY = 52, ST_COUNT = 58
 };

@@ -223,12 +223,12 @@ def drop_mutating_requirements(prob):
 
 
 def fuzz_consolidation(catalog, seed, n_nodes=40, n_pods=200, n_candidates=None, with_min=False, pending_frac=0.15,
-                       all_spot=False, supported=False):
+                       all_spot=False, supported=False, n_pools=3):
     """A consolidation pass over random state: fuzz_problem's classes / pools / existing nodes, NewScheduler node order
     (initialized first, then name), candidates with their bound pods, pending pods, candidate prices around their
     offering price (so REPLACE, price-filtered NONE and DELETE all occur)."""
     from kpsim import abi, synth
-    prob = fuzz_problem(catalog, seed, n_pods=n_pods, n_classes=12, with_min=with_min, n_existing=n_nodes)
+    prob = fuzz_problem(catalog, seed, n_pods=n_pods, n_classes=12, with_min=with_min, n_existing=n_nodes, n_pools=n_pools)
     if supported:
         drop_mutating_requirements(prob)
     rng = np.random.Generator(np.random.PCG64(seed + 7))
@@ -346,3 +346,23 @@ def fuzz_preference_consolidation(catalog, seed, n_nodes=30, n_pods=160, n_bound
             np_.requirements = [r for r in np_.requirements if r.key != ZONE] + [
                 Requirement(ZONE, "Exists", [], int(rng.choice([1, 2, 3])))]
     return cp
+
+
+WIDE_RESOURCES = ["vpc.amazonaws.com/pod-eni", "vpc.amazonaws.com/efa", "nvidia.com/gpu", "aws.amazon.com/neuron",
+                  "amd.com/gpu", "habana.ai/gaudi"]
+
+
+def add_extra_resources(rng, prob, n_extra=None):
+    """Requests of further resources on some classes' pods (pod ENIs, EFA, accelerators), so that more resource axes are
+    active than the consolidation probes keep in registers (cpu, memory, pods + these: 7-9 axes)."""
+    n_extra = int(n_extra or rng.integers(4, len(WIDE_RESOURCES) + 1))
+    req = prob.pods.requests.copy()
+    for res in WIDE_RESOURCES[:n_extra]:
+        c = int(rng.integers(0, len(prob.classes)))
+        req[prob.pods.class_id == c, model.RIDX[res]] = 1000 * int(rng.integers(1, 3))
+        for n in prob.existing:  # most nodes carry some of it (device-plugin resources of the cluster's nodes)
+            if rng.random() < 0.8:
+                n.available = np.array(n.available, np.int64).copy()
+                n.available[model.RIDX[res]] = 1000 * int(rng.integers(1, 9))
+    prob.pods.requests = req
+    return prob

@@ -28,6 +28,7 @@ CASES = {
     "config3_50k": ("config3", dict(n_pods=50_000)),    # BASELINE configs[2]: topology + five weighted NodePools
     "config5_200k": ("config5", dict(n_pods=200_000)),  # BASELINE configs[4]: reserved offerings, ODCR-first NodePools
     "node_dense_10k": (node_dense, dict(n_pods=10_000)),  # 10k in-flight NodeClaims
+    "node_dense_20k": (node_dense, dict(n_pods=20_000)),  # 20k: beyond the LDS slice (HBM slice arrays), one execute
 }
 
 

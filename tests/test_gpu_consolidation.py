@@ -510,3 +510,32 @@ def test_e2e_budgets(ctx, golden, name):
     command trajectory equals the oracle's and meets the reference's per-step bound and end state."""
     import e2e_cases
     _e2e(ctx, golden, getattr(e2e_cases, name))
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_consolidation_many_nodepools(ctx, golden, seed):
+    """40-60 NodePools: candidates' capacity back into their own pool's limits, replacements from any pool."""
+    rng = np.random.Generator(np.random.PCG64(5300 + seed))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=200, replace=False))]
+    cp = fuzzgen.fuzz_consolidation(sub, 5300 + seed, n_nodes=40, n_pods=200, supported=True,
+                                    n_pools=int(rng.integers(40, 61)))
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        assert_probes_equal(device_probes(ctx, cp, mode), pyoracle.consolidate(cp, mode))
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_consolidation_wide_axes(ctx, golden, seed):
+    """Pods requesting 7-9 resource axes (pod ENIs, EFA, GPUs, Neuron, Gaudi besides cpu / memory / pods): the probes
+    check the axes past their registers per candidate node from HBM; probes of both modes and the command vs the
+    oracle."""
+    rng = np.random.Generator(np.random.PCG64(5500 + seed))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(100, 300)), replace=False))]
+    cp = fuzzgen.fuzz_consolidation(sub, 5500 + seed, n_nodes=int(rng.integers(10, 80)),
+                                    n_pods=int(rng.integers(50, 300)), supported=True, all_spot=seed % 4 == 0)
+    fuzzgen.add_extra_resources(rng, cp.cluster)
+    active = (cp.cluster.pods.requests != 0).any(0).sum()
+    assert active > 6, active
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        assert_probes_equal(device_probes(ctx, cp, mode), pyoracle.consolidate(cp, mode))
+    assert_commands_equal(device_command(ctx, cp, abi.KP_CONSOLIDATE_BOTH),
+                          pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH))

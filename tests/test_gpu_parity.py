@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 import fuzzgen
+from kpsim import abi
 import parity
 from kpsim import catalog as cat
 from kpsim import model, synth
@@ -77,6 +78,26 @@ def test_fuzz_requirements(ctx, golden, seed):
     sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=160, replace=False))]
     prob = fuzzgen.fuzz_problem(sub, seed, n_pods=int(rng.integers(50, 400)))
     parity.assert_same(parity.run_device(ctx, prob), parity.run_oracle(prob))
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_fuzz_many_nodepools(ctx, golden, seed):
+    """32-63 NodePools (template bitmasks are 64-bit): weights, taints, limits, minValues, requirements as fuzz_problem
+    draws them for each pool."""
+    rng = np.random.Generator(np.random.PCG64(5100 + seed))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=200, replace=False))]
+    prob = fuzzgen.fuzz_problem(sub, 5100 + seed, n_pods=int(rng.integers(100, 500)), n_classes=20,
+                                n_pools=int(rng.integers(32, 64)))
+    assert len(prob.nodepools) > 31
+    parity.assert_same(parity.run_device(ctx, prob), parity.run_oracle(prob))
+
+
+def test_too_many_nodepools_refused(ctx, golden):
+    from kpsim import native
+    prob = fuzzgen.fuzz_problem(golden[:100], 5199, n_pods=50, n_pools=64)
+    with pytest.raises(native.KpError) as e:
+        parity.run_device(ctx, prob)
+    assert e.value.status == abi.KP_E_UNSUPPORTED
 
 
 @pytest.mark.parametrize("seed", range(6))

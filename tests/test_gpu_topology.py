@@ -165,8 +165,9 @@ def test_fuzz_topology_existing(ctx, golden, seed):
 
 def test_node_dense_10k_beyond_first_slice_plan(golden):
     """10,000-pod node-dense Deployment (hostname anti-affinity): 10,000 in-flight NodeClaims, beyond the first slice
-    plan (KP_NC_FIRST = 4096).  kp_solve re-plans with room for them (allocatable read from HBM); every output field
-    equals the oracle's committed digest (tests/golden/gen_scale_digest.py node_dense_10k; ~1 min of oracle time)."""
+    plan (KP_NC_FIRST = 4096).  The prepare plans for them from the pods' self-selecting anti-affinity (allocatable read
+    from HBM); every output field equals the oracle's committed digest (tests/golden/gen_scale_digest.py node_dense_10k;
+    ~1 min of oracle time)."""
     from kpsim import native
     with open(os.path.join(os.path.dirname(__file__), "golden", "scale_digests.json")) as f:
         want = json.load(f)["node_dense_10k"]
@@ -175,5 +176,69 @@ def test_node_dense_10k_beyond_first_slice_plan(golden):
         dev = parity.run_device(c, TC.node_dense(golden, want["n_pods"]))
         assert dev[0].n_nodeclaims == 10_000 and (dev[0].nodeclaim_n_pods == 1).all()
         assert parity.result_digest(dev) == {k: v for k, v in want.items() if k != "n_pods"}
+    finally:
+        c.close()
+
+
+def _split_solve(ctx, prob):
+    """prepare + execute + fetch (one execute: an overflow would surface as KP_E_UNSUPPORTED from fetch)."""
+    cv = model.CatalogView(prob.catalog)
+    ctx.upload_catalog(cv)
+    ctx.prepare(model.SolveInputView(prob))
+    ctx.execute()
+    cap_nc = max(16, prob.pods.n + 1)
+    out = model.OutputBuffers(prob.pods.n, cap_nc, cap_nc * prob.max_instance_types)
+    ctx.fetch(out)
+    r = out.results()
+    return r, [model.parse_requirements_blob(ctx.nodeclaim_requirements(i)) for i in range(r.n_nodeclaims)]
+
+
+def test_node_dense_20k_one_execute(golden):
+    """20,000-pod node-dense Deployment: planned for 20k NodeClaims at prepare (no overflow re-run: the split calls
+    succeed), slice arrays in HBM beyond the LDS slice; equal to the oracle's committed digest (node_dense_20k)."""
+    from kpsim import native
+    with open(os.path.join(os.path.dirname(__file__), "golden", "scale_digests.json")) as f:
+        want = json.load(f)["node_dense_20k"]
+    c = native.Context(0)
+    try:
+        dev = _split_solve(c, TC.node_dense(golden, want["n_pods"]))
+        assert dev[0].n_nodeclaims == 20_000 and (dev[0].nodeclaim_n_pods == 1).all()
+        assert parity.result_digest(dev) == {k: v for k, v in want.items() if k != "n_pods"}
+    finally:
+        c.close()
+
+
+def test_node_dense_does_not_stick_to_ctx(golden):
+    """A node-dense solve does not leave its large plan on the ctx: a config-2 solve after it on the same
+    ctx takes the same quick-accept path (counters) and result as on a fresh ctx."""
+    from kpsim import native
+    prob = synth.subsample(synth.config2(catalog=golden), 4000)
+    fresh = native.Context(0)
+    used = native.Context(0)
+    try:
+        want = parity.run_device(fresh, prob)
+        qa_want = fresh.ffd_cycles()[12]
+        parity.run_device(used, TC.node_dense(golden, 6000))
+        got = parity.run_device(used, prob)
+        parity.assert_same(got, want)
+        assert used.ffd_cycles()[12] == qa_want  # quick accepts
+    finally:
+        fresh.close()
+        used.close()
+
+
+def test_overflow_rerun_once(golden):
+    """In-flight NodeClaims the prepare cannot foresee (pods that each need most of a node, no topology terms): the first
+    plan overflows, kp_solve re-runs once planned for every pod, and the result equals the oracle."""
+    big = [it for it in golden if it.name.startswith("m5.") or it.name.startswith("m6i.")]
+    pc = model.PodClass(requirements=[model.Requirement("node.kubernetes.io/instance-type", "In", ["m5.large"])])
+    pods = synth.pods_from_specs([(0, {"cpu": "1500m", "memory": "1Gi"})] * 4500)
+    prob = model.Problem(big, [synth.default_nodepool()], [pc], pods)
+    from kpsim import native
+    c = native.Context(0)
+    try:
+        dev = parity.run_device(c, prob)
+        assert dev[0].n_nodeclaims == 4500
+        parity.assert_same(dev, parity.run_oracle(prob))
     finally:
         c.close()
