@@ -77,7 +77,7 @@ struct ClassCache {
     ReqHdr hdr[KP_MAX_CLASS_KEYS];
     uint64_t words[KP_MAX_SCR_WORDS];
     uint64_t V[KP_TW_MAX];
-    uint64_t dne[KP_MAX_CLASS_KEYS][KP_TW_MAX];
+    uint64_t dne[KP_MAX_CLASS_KEYS][KP_DNE_TW];
     uint32_t kneutral;          // class keys present only for topology narrowing (bit per class-key index)
     int ntc, ntr;               // topology groups constraining / recording the class
     int tc[KP_MAX_TOPO];        // group | self << 30
@@ -162,7 +162,7 @@ __device__ inline void fill_class_cache(const KpDev& d, int c, ClassCache& CC, i
         }
         CC.nbB[i] = nb;
         const int kc = d.kcat[k];
-        for (int w = 0; w < d.TW; w++) CC.dne[i][w] = kc >= 0 ? d.dne_mask[(size_t)kc * d.TW + w] : 0ull;
+        for (int w = 0; w < d.TW && w < KP_DNE_TW; w++) CC.dne[i][w] = kc >= 0 ? d.dne_mask[(size_t)kc * d.TW + w] : 0ull;
     }
     for (int w = tid; w < d.TW; w += nthr) CC.V[w] = d.V[(size_t)c * d.TW + w];
     if (tid == 0) {
@@ -817,7 +817,9 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
     while (km) {
         const int i = __ffsll((unsigned long long)km) - 1;
         km &= km - 1;
-        if (lane < TW) myopt &= ~CC.dne[i][lane];
+        if (lane < TW)
+            myopt &= ~(lane < KP_DNE_TW ? CC.dne[i][lane]
+                                        : (CC.kcat[i] >= 0 ? d.dne_mask[(size_t)CC.kcat[i] * TW + lane] : 0ull));
     }
     const uint64_t mm = ballot(kmul >= 0);
     EV_STAMP(1);

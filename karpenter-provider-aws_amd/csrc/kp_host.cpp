@@ -540,7 +540,6 @@ struct kp_ctx {
     std::vector<std::vector<int>> cons_hlost;
     std::vector<int32_t> h_tpos0;
     DBuf<int32_t> d_hpos0, d_tg_ha, d_ring_cls, d_ring_shape;
-    DBuf<uint64_t> d_nc_cls;  // [NCcap][CWc] absorbed classes per NodeClaim (KpDev::nc_cls)
     DBuf<uint32_t> d_g_key;  // HBM slice arrays of node-dense plans (KpDev::g_key ...)
     DBuf<uint16_t> d_g_ord, d_g_last;
     DBuf<uint8_t> d_g_tmpl;
@@ -1937,14 +1936,16 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     // self-selecting hostname spread at most maxSkew per host: when that lower bound exceeds the first plan
     // (KP_NC_FIRST), the solve is planned for it from the start, so a node-dense Deployment runs one execute.  A solve
     // that still overflows (kp_solve_fetch) makes the next prepare of this ctx, and only that one, plan for every pod.
-    int64_t dense = 0;
+    int64_t dense = 0;  // a lower bound of the NodeClaims: the largest such class, less the existing nodes
     {
         std::vector<int64_t> ccount(std::max(C, 1), 0);
         for (int p = 0; p < P; p++) ccount[in->pods.class_id[p]]++;
         for (const HGroup& g : th.g)
             if (!g.inverse && g.host && g.owner >= 0 && g.owner < C && g.sel[g.owner]) {
-                if (g.type == KP_TOPO_ANTI_AFFINITY) dense += ccount[g.owner];
-                else if (g.type == KP_TOPO_SPREAD && g.skew > 0) dense += (ccount[g.owner] + g.skew - 1) / g.skew;
+                int64_t n = 0;
+                if (g.type == KP_TOPO_ANTI_AFFINITY) n = ccount[g.owner];
+                else if (g.type == KP_TOPO_SPREAD && g.skew > 0) n = (ccount[g.owner] + g.skew - 1) / g.skew;
+                dense = std::max(dense, n - E);
             }
     }
     int64_t plan = c->nc_cap_once > 0 ? c->nc_cap_once : KP_NC_FIRST;
@@ -1957,8 +1958,6 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     HIPCHK(c->d_nc_opts.ensure((size_t)NCcap * TW));
     HIPCHK(c->d_nc_req.ensure((size_t)NCcap * R));
     HIPCHK(c->d_nc_tmpl.ensure(NCcap));
-    const int CWc = std::max(1, (C + 63) / 64);
-    HIPCHK(c->d_nc_cls.ensure((size_t)NCcap * CWc));
     HIPCHK(c->d_nc_held.ensure(NCcap));
     HIPCHK(c->d_nc_rlive.ensure(NCcap));
     HIPCHK(c->d_qbuf.ensure(std::max(P, 1)));
@@ -2263,8 +2262,6 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.nc_opts = c->d_nc_opts.p;
     d.nc_req = c->d_nc_req.p;
     d.nc_tmpl = c->d_nc_tmpl.p;
-    d.nc_cls = c->d_nc_cls.p;
-    d.CWc = CWc;
     d.empty_hdr = c->d_empty_hdr.p;
     d.empty_words = c->d_empty_words.p;
     d.qbuf = c->d_qbuf.p;
@@ -2328,7 +2325,8 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.nc_held = c->d_nc_held.p;
     d.nc_rlive = c->d_nc_rlive.p;
     d.alloc_act = nullptr;
-    if (NCcap > KP_NC_FIRST) {  // large slice plan: the staged axes' allocatable table in HBM ([axes][TP], TP = 64-padded T)
+    if (NCcap > KP_NC_FIRST || T > 1024) {  // node-dense plan or large catalog: the staged axes' allocatable table in HBM
+                                            // ([axes][TP], TP = 64-padded T) when LDS cannot hold it
         const int TP = (T + 63) / 64 * 64, ns = std::min(d.n_active, KP_LDS_AXES);
         std::vector<int64_t> act((size_t)std::max(ns, 1) * TP, 0);
         for (int ai = 0; ai < ns; ai++)

@@ -446,12 +446,6 @@ __device__ inline uint64_t limit_filter(const KpDev& d, int j, uint64_t o, int l
 
 __device__ __forceinline__ long long prof_clock(const KpDev& d) { return d.profile ? __builtin_amdgcn_s_memtime() : 0; }
 
-// NodeClaim nc has absorbed a pod of class c at some point (d.nc_cls): its requirements are a subset of c's, so the
-// requirement merge of another pod of c leaves them unchanged (Intersection is idempotent) and every option stays
-// compatible with c — the premise of the quick accepts, which before only looked at the last absorbed class.
-__device__ __forceinline__ bool nc_absorbed(const KpDev& d, int nc, int c) {
-    return (ld_u64(&d.nc_cls[(size_t)nc * d.CWc + (c >> 6)]) >> (c & 63)) & 1ull;
-}
 
 // The winner's reservations (one lane): ReservationManager.Reserve for the IDs newly held, Release for the IDs the
 // Add no longer holds (NodeClaim.Add's reservedOfferings update), then the NodeClaim's held set and liveness.
@@ -1239,14 +1233,12 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 if (d.profile && lane == 0) {  // KPSIM_PROFILE: why the topology quick accept does not apply
                     const int nc = f < N ? sord[f] : 0;
                     const int why = f >= N ? 0 : !(cfl & CF_TOPO_QREC) ? 1 : nc >= NQ ? 2
-                                  : !(slast[nc] == (uint16_t)c || nc_absorbed(d, nc, c) ||
-                                      ((cfl & CF_NOKEYS) && ((d.tol[c] >> stmpl[nc]) & 1ull))) ? 3 : 4;
+                                  : !(slast[nc] == (uint16_t)c || ((cfl & CF_NOKEYS) && ((d.tol[c] >> stmpl[nc]) & 1ull))) ? 3 : 4;
                     S.st[ST_TQ_WHY + why]++;
                 }
                 if (f < N && (cfl & CF_TOPO_QREC) && A > 0) {
                     const int nc = sord[f], tm = stmpl[nc];
-                    bool ok = nc < NQ && (slast[nc] == (uint16_t)c || ((cfl & CF_NOKEYS) && ((d.tol[c] >> tm) & 1ull)) ||
-                                          nc_absorbed(d, nc, c));
+                    bool ok = nc < NQ && (slast[nc] == (uint16_t)c || ((cfl & CF_NOKEYS) && ((d.tol[c] >> tm) & 1ull)));
                     for (int ai = 0; ai < A && ok; ai++) ok = S.cur_pq[ai] <= shr[ai * NQ + nc];
                     if (d.profile && lane == 0 && nc < NQ && ok) S.st[ST_TQ_WHY + 5]++;  // witness fits
                     quick = ok && topo_pinned(d, S, nc);
@@ -1367,8 +1359,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 a.held = (RESV && d.resv_on) ? ld_u64(&d.nc_held[nc]) : 0ull;
                 // a NodeClaim that keeps reserved offerings re-runs the whole Add (its reservations are recomputed)
                 const bool fast = !(S.CC.flags & CF_TOPO) && !(RESV && d.resv_on && ld_i32(&d.nc_rlive[nc])) &&
-                                  (slast[nc] == (uint16_t)S.cur_cls || ((S.CC.flags & CF_NOKEYS) && ((S.CC.tol >> a.tmpl) & 1ull)) ||
-                                   nc_absorbed(d, nc, S.cur_cls));
+                                  (slast[nc] == (uint16_t)S.cur_cls || ((S.CC.flags & CF_NOKEYS) && ((S.CC.tol >> a.tmpl) & 1ull)));
                 if (fast && lane == 0) S.ws[wave].memo_ok = 1;
                 const bool ok = fast ? eval_fits_only<PREF>(d, E, a, S.ws[wave], lane)
                                 : (TOPO_ON && (S.CC.flags & CF_TOPO_CONS)) ? eval_wave<true, RESV, true, PREF>(d, E, S.CC, a, S.ws[wave], lane)
@@ -1438,7 +1429,6 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 if (lane < A && nc < NQ) shr[lane * NQ + nc] = S.ws[cw].hr[lane];
                 if (lane == 0) {
                     slast[nc] = (uint16_t)S.cur_cls;
-                    atomicOr((unsigned long long*)&d.nc_cls[(size_t)nc * d.CWc + (S.cur_cls >> 6)], 1ull << (S.cur_cls & 63));
                     skey[pos]++;
                     S.dirty_kind = 1;
                     S.dirty_pos = pos;
@@ -1517,10 +1507,6 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                     if (wave == twin) {
                         const int jj = tb + wave;
                         const int n = S.N;
-                        // absorbed classes of the new NodeClaim: the pod's
-                        for (int i = lane; i < d.CWc; i += 64)
-                            __hip_atomic_store(&d.nc_cls[(size_t)n * d.CWc + i], i == (S.cur_cls >> 6) ? 1ull << (S.cur_cls & 63) : 0ull,
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         // NewNodeClaim(template): requirements = template requirements, then the Add's merge
                         for (int k = lane; k < K; k += 64) d.nc_hdr[(size_t)n * K + k] = d.cls_hdr[(size_t)(d.C + jj) * K + k];
                         for (int i = lane; i < d.DW; i += 64)
@@ -1824,14 +1810,21 @@ size_t kp_ffd_shared_bytes() { return sizeof(FfdShared); }
 
 // Lay out the FFD kernel's dynamic LDS for this solve (fills d.off_*, d.lds_*).  Returns false if even the
 // quick-accept-free layout exceeds max_bytes.
+static bool kp_ffd_plan_lds_tables(KpDev& d, int max_bytes);
+
+// A solve is planned for KP_NC_FIRST in-flight NodeClaims with the allocatable table staged in LDS and the rest of LDS as
+// quick-accept rows; a node-dense plan (NCcap above KP_NC_FIRST) reads the table from HBM and keeps as many slice entries
+// in LDS as it holds (9 B per NodeClaim), or all of them in HBM.  Catalogs too large for the staged tables read the
+// allocatable table, then the multi-valued label masks, from HBM.
 bool kp_ffd_plan_lds(KpDev& d, int max_bytes) {
+    d.alloc_global = d.NCcap > KP_NC_FIRST && d.alloc_act != nullptr;
+    return kp_ffd_plan_lds_tables(d, max_bytes);
+}
+
+static bool kp_ffd_plan_lds_tables(KpDev& d, int max_bytes) {
     auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
     size_t off = al(sizeof(FfdShared));
-    // a solve is planned for KP_NC_FIRST in-flight NodeClaims with the allocatable table staged in LDS and the rest of
-    // LDS as quick-accept rows; a solve that overflowed that is re-planned (NCcap above KP_NC_FIRST) with the table read
-    // from HBM and as many slice entries as LDS holds (9 B per NodeClaim)
     int ncmax = d.NCcap < KP_MAX_NC ? d.NCcap : KP_MAX_NC;
-    d.alloc_global = ncmax > KP_NC_FIRST && d.alloc_act != nullptr;
     d.slice_hbm = 0;
     if (d.alloc_global) {
         const int tp0 = (d.T + 63) / 64 * 64;
@@ -1866,7 +1859,18 @@ bool kp_ffd_plan_lds(KpDev& d, int max_bytes) {
     d.off_tsnap = (int)off;
     if (d.G > 0) off = al(off + sizeof(TopoSnap));
     d.off_hr = (int)off;
-    if ((int)off > max_bytes) return false;
+    if ((int)off > max_bytes) {
+        // large catalogs: the staged allocatable, then the multi-valued label masks, are read from HBM instead
+        if (!d.alloc_global && d.alloc_act) {
+            d.alloc_global = 1;
+            return kp_ffd_plan_lds_tables(d, max_bytes);
+        }
+        if (d.multi16) {
+            d.multi16 = nullptr;
+            return kp_ffd_plan_lds_tables(d, max_bytes);
+        }
+        return false;
+    }
     d.lds_A = d.n_active <= KP_LDS_AXES ? d.n_active : 0;
     int nq = 0;
     if (d.lds_A > 0) {

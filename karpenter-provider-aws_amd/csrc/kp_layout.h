@@ -14,8 +14,10 @@
 #pragma once
 #include <stdint.h>
 
-#define KP_MAX_TYPES 1024            // TW <= 16
+#define KP_MAX_TYPES 2048            // TW <= 32
 #define KP_TW_MAX (KP_MAX_TYPES / 64)
+#define KP_DNE_TW 16                 // DoesNotExist-type words of a class key kept in the class cache (LDS); the words of
+                                     // larger catalogs are read from HBM (dne_mask)
 #define KP_MAX_NC 65535              // in-flight NodeClaims per solve (u16 ids in the LDS slice arrays)
 #define KP_NC_FIRST 4096             // slice capacity a solve is first planned with (kp_solve grows it on overflow)
 #define KP_MAX_KEYS 96               // label keys per solve
@@ -163,8 +165,6 @@ struct KpDev {
     uint64_t* nc_opts;               // [NCcap][TW]
     int64_t* nc_req;                 // [NCcap][R]
     int32_t* nc_tmpl;                // [NCcap]
-    uint64_t* nc_cls;                // [NCcap][CWc] classes the NodeClaim has absorbed (bit per class)
-    int32_t CWc;                     // words of an nc_cls row: ceil(C / 64)
     const ReqHdr* empty_hdr;         // [K] all-undefined digest (template init)
     const uint64_t* empty_words;     // [DW]
     int32_t* qbuf;                   // [P] queue ring

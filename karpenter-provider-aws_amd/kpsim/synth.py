@@ -440,3 +440,30 @@ def launch_requests(catalog, n=1000, seed=SEED, with_min_values=True):
             rq[5] = int(rng.choice([1, 2, 4, 8])) * 1000
         out.append(model.LaunchRequest(reqs, rq))
     return out
+
+
+def widen_catalog(catalog, n_types, seed=SEED):
+    """A catalog of n_types rows: the given one plus renamed copies of its types ("<family>w<k>.<size>", the family
+    label renamed alike, prices scaled by a seeded factor), standing in for a region whose price table lists more types
+    than the golden catalog (the library's limit is KP_MAX_TYPES = 2048)."""
+    import copy
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = list(catalog)
+    fam_key = "karpenter.k8s.aws/instance-family"
+    k = 0
+    while len(out) < n_types:
+        base = catalog[len(out) % len(catalog)]
+        k += 1 if len(out) % len(catalog) == 0 else 0
+        it = copy.deepcopy(base)
+        fam, _, size = base.name.partition(".")
+        it.name = "%sw%d.%s" % (fam, k, size)
+        labels = dict(it.labels)
+        labels["node.kubernetes.io/instance-type"] = [it.name]
+        if labels.get(fam_key):
+            labels[fam_key] = ["%sw%d" % (labels[fam_key][0], k)]
+        it.labels = labels
+        f = float(rng.uniform(0.8, 1.25))
+        for o in it.offerings:
+            o.price = round(o.price * f, 6)
+        out.append(it)
+    return out

@@ -539,3 +539,12 @@ def test_consolidation_wide_axes(ctx, golden, seed):
         assert_probes_equal(device_probes(ctx, cp, mode), pyoracle.consolidate(cp, mode))
     assert_commands_equal(device_command(ctx, cp, abi.KP_CONSOLIDATE_BOTH),
                           pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH))
+
+
+def test_consolidation_wide_catalog(ctx, golden):
+    """Probes over a 1,300-type catalog (32 option words; OrderByPrice / Truncate over the wider option set)."""
+    cat = synth.widen_catalog(golden, 1300)
+    for seed in range(2):
+        cp = fuzzgen.fuzz_consolidation(cat, 5700 + seed, n_nodes=40, n_pods=200, supported=True, all_spot=seed == 1)
+        for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+            assert_probes_equal(device_probes(ctx, cp, mode), pyoracle.consolidate(cp, mode))

@@ -121,3 +121,11 @@ def test_empty_batch(ctx, golden):
     ctx.upload_catalog(model.CatalogView(golden))
     res = ctx.launch_select(model.LaunchBatchView([]), 60)
     assert len(res.rows) == 0
+
+
+def test_wide_catalog_launch(ctx, golden):
+    """Launch selection over a 1,800-type catalog with reserved offerings (Truncate ranks up to 2048 types)."""
+    cat = synth.config5_catalog(synth.widen_catalog(golden, 1800), seed=synth.SEED + 9)
+    reqs = synth.launch_requests(cat, n=400, seed=synth.SEED + 9)
+    dev, orc = _both(ctx, cat, reqs)
+    LC.assert_same(dev, orc)

@@ -80,6 +80,29 @@ def test_fuzz_requirements(ctx, golden, seed):
     parity.assert_same(parity.run_device(ctx, prob), parity.run_oracle(prob))
 
 
+@pytest.mark.parametrize("n_types", [1200, 2048])
+def test_wide_catalog_solve(ctx, golden, n_types):
+    """Catalogs past 1024 types (KP_MAX_TYPES = 2048; synth.widen_catalog): 32 option words, the staged allocatable table
+    read from HBM when LDS cannot hold it; config-2 pods bit-exact with the oracle."""
+    cat = synth.widen_catalog(golden, n_types)
+    prob = synth.subsample(synth.config2(catalog=cat), 2500)
+    parity.assert_same(parity.run_device(ctx, prob), parity.run_oracle(prob))
+
+
+def test_wide_catalog_topology(ctx, golden):
+    cat = synth.widen_catalog(golden, 1500)
+    prob = synth.subsample(synth.config3(catalog=cat), 2000)
+    parity.assert_same(parity.run_device(ctx, prob), parity.run_oracle(prob))
+
+
+def test_too_many_types_refused(ctx, golden):
+    from kpsim import native
+    cat = synth.widen_catalog(golden, 2049)
+    with pytest.raises(native.KpError) as e:
+        ctx.upload_catalog(model.CatalogView(cat))
+    assert e.value.status == abi.KP_E_UNSUPPORTED
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_fuzz_many_nodepools(ctx, golden, seed):
     """32-63 NodePools (template bitmasks are 64-bit): weights, taints, limits, minValues, requirements as fuzz_problem

@@ -13,6 +13,6 @@ python3 - <<'PY'
 import json
 for f in ["gpurun_out/bp.json", "gpurun_out/b.json"]:
     c = json.load(open(f))["consolidation"]
-    print(f, "cands/s %.0f ms/step %.3f" % (c["value"], c["ms_per_step"]), c["kernel_ms_rank0"])
+    print(f, "cands/s %.0f ms/step %.3f" % (c["candidates_per_s"], c["ms_per_step"]), c["kernel_ms_rank0"])
     print("  ", {k: v for k, v in c["counters_per_step"].items() if v}, c.get("counters_multi"))
 PY

@@ -14,7 +14,7 @@ for f in ("gpurun_out/bcq.json", "gpurun_out/bcp.json"):
     d = json.load(open(f))
     for leg in ("consolidation", "consolidation_replace"):
         c = d[leg]
-        print(f, leg, "cands/s %.0f ms %.3f" % (c["value"], c["ms_per_step"]), c["kernel_ms_rank0"], "parity",
+        print(f, leg, "cands/s %.0f ms %.3f" % (c["candidates_per_s"], c["ms_per_step"]), c["kernel_ms_rank0"], "parity",
               c.get("parity_vs_cpu_baseline"), c.get("probe_decisions"))
         print("   ", {k: v for k, v in c["counters_per_step"].items() if v})
 PY

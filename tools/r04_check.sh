@@ -4,7 +4,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_topology.py tests/test_gpu_preferences.py tests/test_gpu_consolidation.py tests/test_gpu_reserved.py -x -q --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/rc.log 2>&1 || { tail -30 gpurun_out/rc.log; exit 1; }
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/rc.log 2>&1 || { tail -30 gpurun_out/rc.log; exit 1; }
 tail -2 gpurun_out/rc.log
 timeout -k 10 300 python bench.py --no-cpu-baseline --no-consolidation --no-launch --no-reserved --steps 5 --warmup 1 > gpurun_out/bfq.json 2> gpurun_out/bfq.err || { tail -5 gpurun_out/bfq.err; exit 1; }
 python3 -c "
