@@ -2492,9 +2492,9 @@ extern "C" kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out) {
     for (int i = 0; i < 4; i++) c->cycles[33 + i] = st[ST_REJ_REQ + i];
     if (getenv("KPSIM_PROFILE") && st[ST_TQ_WHY] + st[ST_TQ_WHY + 1] + st[ST_TQ_WHY + 2] + st[ST_TQ_WHY + 3] + st[ST_TQ_WHY + 4])
         fprintf(stderr, "[kpsim] topology pods past the prefilter: no survivor %lld, not QREC %lld, no quick row %lld, class not "
-                        "absorbed %lld, quick row %lld (witness fits %lld); NQ %d of %d NodeClaims\n",
+                        "absorbed %lld, quick row %lld (witness fits %lld, merge no-op %lld); NQ %d of %d NodeClaims\n",
                 (long long)st[ST_TQ_WHY], (long long)st[ST_TQ_WHY + 1], (long long)st[ST_TQ_WHY + 2], (long long)st[ST_TQ_WHY + 3],
-                (long long)st[ST_TQ_WHY + 4], (long long)st[ST_TQ_WHY + 5], c->dev.lds_nq, N);
+                (long long)st[ST_TQ_WHY + 4], (long long)st[ST_TQ_WHY + 5], (long long)st[ST_TQ_WHY + 6], c->dev.lds_nq, N);
     so.ns_host_prep = c->ns_prep;
     so.ns_device_solve = c->ns_exec;
     if (N > out->cap_nodeclaims || n_ids > out->cap_type_ids) return fail(ctx, KP_E_BUFFER, "output buffers too small");

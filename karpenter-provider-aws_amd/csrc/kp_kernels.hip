@@ -345,6 +345,36 @@ __device__ inline bool topo_pinned(const KpDev& d, const FfdShared& S, int nc) {
     return true;
 }
 
+// The requirement merge of NodeClaim.Add(pod of class c) on NodeClaim nc is a no-op: for every key the class constrains
+// (keys carried only for topology narrowing aside), the NodeClaim has the key and Requirement.Intersection leaves it as it
+// is (header and values), and the pair passes Compatible.  Then the Add keeps the NodeClaim's requirements, so its options
+// stay compatible and its offerings the same: the topology quick accept applies as for a NodeClaim that absorbed the
+// class (wave 0; ws.words is free scratch here).
+__device__ inline bool merge_noop(const KpDev& d, WaveScratch& ws, int nc, int c, int lane) {
+    const int k0 = d.cls_koff[c], nck = d.cls_koff[c + 1] - k0;
+    bool ok = true;
+    if (lane < nck && !(d.cls_kneutral && d.cls_kneutral[k0 + lane])) {
+        const int k = d.cls_keys[k0 + lane], n = d.nw[k];
+        const ReqHdr A = d.nc_hdr[(size_t)nc * d.K + k];
+        const uint64_t* aw = d.nc_words + (size_t)nc * d.DW + d.woff[k];
+        if (!(A.flags & RF_DEF)) {
+            ok = false;  // the merge adds the key
+        } else {
+            const ReqHdr B = d.cls_hdr[(size_t)c * d.K + k];
+            const uint64_t* bw = d.cls_words + (size_t)c * d.DW + d.woff[k];
+            uint64_t* ow = ws.words + d.cls_wsoff[k0 + lane];
+            ReqHdr O;
+            const int cnt = req_intersect(d, k, A, aw, B, bw, O, ow);
+            ok = O.flags == A.flags && O.gt == A.gt && O.lt == A.lt && O.minv == A.minv;
+            for (int i = 0; i < n && ok; i++) ok = ow[i] == aw[i];
+            if (!(O.flags & RF_CMP) && cnt == 0 &&
+                !(op_notin_or_dne(req_op(B.flags, popc_words(bw, n))) && op_notin_or_dne(req_op(A.flags, popc_words(aw, n)))))
+                ok = false;
+        }
+    }
+    return ballot(!ok) == 0;
+}
+
 // Topology.Record of a quick accept onto NodeClaim nc (template tmpl): its requirements are unchanged by the Add, so
 // every recorded domain comes from its digest (hostname groups: its host E + nc).  CF_TOPO_QREC guarantees that no
 // recording group needs the node-affinity filter of another class.
@@ -1238,10 +1268,16 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 }
                 if (f < N && (cfl & CF_TOPO_QREC) && A > 0) {
                     const int nc = sord[f], tm = stmpl[nc];
-                    bool ok = nc < NQ && (slast[nc] == (uint16_t)c || ((cfl & CF_NOKEYS) && ((d.tol[c] >> tm) & 1ull)));
+                    const bool absd = slast[nc] == (uint16_t)c || ((cfl & CF_NOKEYS) && ((d.tol[c] >> tm) & 1ull));
+                    bool ok = nc < NQ;
                     for (int ai = 0; ai < A && ok; ai++) ok = S.cur_pq[ai] <= shr[ai * NQ + nc];
                     if (d.profile && lane == 0 && nc < NQ && ok) S.st[ST_TQ_WHY + 5]++;  // witness fits
-                    quick = ok && topo_pinned(d, S, nc);
+                    ok = ok && topo_pinned(d, S, nc);
+                    // a NodeClaim that has not absorbed the class: quick when the Add's merge changes nothing
+                    const bool noop = ok && !absd && merge_noop(d, S.ws[0], nc, c, lane);
+                    if (d.profile && lane == 0 && noop) S.st[ST_TQ_WHY + 6]++;
+                    quick = ok && (absd || noop);
+                    if (noop && lane == 0) slast[nc] = (uint16_t)c;  // its requirements are a subset of the class's
                     if (quick) {
                         if (lane < A) shr[lane * NQ + nc] -= S.cur_pq[lane];
                         if (lane < R && S.pod_req[lane])

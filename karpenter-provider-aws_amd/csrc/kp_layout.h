@@ -273,5 +273,5 @@ enum {
     ST_REJ_REQ = 48, ST_REJ_TOPO, ST_REJ_TYPES, ST_REJ_MIN,
     // KPSIM_PROFILE: topology pods past the prefilter — no surviving NodeClaim, class records through another class's
     // node filter (not QREC), NodeClaim without a quick row, class not absorbed, quick row present; witness fits
-    ST_TQ_WHY = 52, ST_COUNT = 58
+    ST_TQ_WHY = 52, ST_COUNT = 59
 };
