@@ -647,10 +647,19 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     pf_load += __builtin_amdgcn_s_memtime() - cw0;
                 }
                 uint64_t U = ballot(live);  // pods of the window not placed yet
+                // this pod's compatible-node words, one chunk ahead (the next chunk's load is in flight while this one is
+                // taken)
+                uint64_t xnext = (live && KS > 0) ? d.XT[(size_t)wc * EW] : 0ull;
+                // smallest request per axis over the window's pods not placed yet (recomputed when U changes)
+                int64_t mq[KP_LDS_AXES];
+                uint64_t mqU = 0;
+#pragma unroll
+                for (int ai = 0; ai < KP_LDS_AXES; ai++) mq[ai] = 0;
                 for (int w = 0; w < KS && U; w++) {
                     const long long cc0 = prof ? __builtin_amdgcn_s_memtime() : 0;
                     const bool inU = (U >> lane) & 1ull;
-                    const uint64_t xw = inU ? (d.XT[(size_t)wc * EW + w] & ~excl[w]) : 0ull;  // this pod's nodes
+                    const uint64_t xw = inU ? (xnext & ~excl[w]) : 0ull;  // this pod's nodes
+                    xnext = (live && w + 1 < KS) ? d.XT[(size_t)wc * EW + w + 1] : 0ull;
                     const uint64_t anyc = uni64(wave_or64(xw));
                     if (!anyc) continue;
                     if (!((loaded >> w) & 1ull)) {  // first touch: the chunk's headroom into the store
@@ -660,13 +669,16 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                         st_loads++;
                     }
                     // a node below the smallest remaining request on some axis takes none of them
+                    if (U != mqU) {
+                        mqU = U;
+                        AXL(ai) mq[ai] = (int64_t)wave_reduce64(inU ? (uint64_t)wq[ai] : (uint64_t)INT64_MAX,
+                                                                [](uint64_t a, uint64_t b) { return (int64_t)b < (int64_t)a ? b : a; });
+                    }
                     bool pot = (anyc >> lane) & 1ull;
                     int64_t hl[KP_LDS_AXES];
                     AXL(ai) {
                             hl[ai] = hs[(w * AA + ai) * 64 + lane];
-                            const int64_t mq = (int64_t)wave_reduce64(inU ? (uint64_t)wq[ai] : (uint64_t)INT64_MAX,
-                                                                      [](uint64_t a, uint64_t b) { return (int64_t)b < (int64_t)a ? b : a; });
-                            pot = pot && hl[ai] >= mq;
+                            pot = pot && hl[ai] >= mq[ai];
                         }
                     st_nodes += 64;
                     const uint64_t iw = uni64(initb[w]);

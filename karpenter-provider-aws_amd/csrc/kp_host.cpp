@@ -2282,6 +2282,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     // topology pods: candidates per block round (KPSIM_TOPO_CANDS, diagnostics)
     d.topo_cands = getenv("KPSIM_TOPO_CANDS") ? std::max(1, std::min(KP_NWAVES, atoi(getenv("KPSIM_TOPO_CANDS")))) : KP_NWAVES;
     d.team_eval = getenv("KPSIM_NO_TEAM") ? 0 : 1;  // diagnostics: KPSIM_NO_TEAM=1 evaluates topology candidates one per wave
+    d.noop_quick = getenv("KPSIM_NO_NOOP") ? 0 : 1;  // diagnostics: KPSIM_NO_NOOP=1 disables the no-op merge quick accept
     // KPSIM_TRACE_POD=p traces pod p; KPSIM_TRACE_CLASS=c traces every slow-path pod of class c (trace_pod = -2 - c)
     d.trace_pod = getenv("KPSIM_TRACE_POD") ? atoi(getenv("KPSIM_TRACE_POD"))
                   : getenv("KPSIM_TRACE_CLASS") ? -2 - atoi(getenv("KPSIM_TRACE_CLASS")) : -1;
@@ -2397,10 +2398,10 @@ extern "C" kp_status kp_solve_execute(kp_ctx* ctx) {
     HIPCHK(hipEventRecord(c->ev[2], s));
     HIPCHK(kp_launch_template_init(d, s));
     HIPCHK(kp_launch_existing(d, s));
-    HIPCHK(hipEventRecord(c->ev[3], s));
     HIPCHK(c->d_self.ensure(1));
     d.self = c->d_self.p;
     HIPCHK(hipMemcpyAsync(c->d_self.p, &d, sizeof(KpDev), hipMemcpyHostToDevice, s));
+    HIPCHK(hipEventRecord(c->ev[3], s));
     HIPCHK(kp_launch_ffd(d, s));
     HIPCHK(hipEventRecord(c->ev[4], s));
     HIPCHK(kp_launch_finalize(d, d.NCcap, s));
@@ -2490,6 +2491,10 @@ extern "C" kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out) {
     for (int i = 0; i < 11; i++) c->cycles[19 + i] = st[ST_N_NOINV + i];
     for (int i = 0; i < 3; i++) c->cycles[30 + i] = st[ST_TOPO_QUICK + i];
     for (int i = 0; i < 4; i++) c->cycles[33 + i] = st[ST_REJ_REQ + i];
+    if (getenv("KPSIM_PROFILE") && st[ST_SLOW_WHY] + st[ST_SLOW_WHY + 1] + st[ST_SLOW_WHY + 2] + st[ST_SLOW_WHY + 3])
+        fprintf(stderr, "[kpsim] slow-path pods: no candidate %lld, class not absorbed %lld, witness short %lld, no witness table %lld; "
+                "no-op merge quick accepts %lld\n", (long long)st[ST_SLOW_WHY], (long long)st[ST_SLOW_WHY + 1],
+                (long long)st[ST_SLOW_WHY + 2], (long long)st[ST_SLOW_WHY + 3], (long long)st[ST_SLOW_WHY + 4]);
     if (getenv("KPSIM_PROFILE") && st[ST_TQ_WHY] + st[ST_TQ_WHY + 1] + st[ST_TQ_WHY + 2] + st[ST_TQ_WHY + 3] + st[ST_TQ_WHY + 4])
         fprintf(stderr, "[kpsim] topology pods past the prefilter: no survivor %lld, not QREC %lld, no quick row %lld, class not "
                         "absorbed %lld, quick row %lld (witness fits %lld, merge no-op %lld); NQ %d of %d NodeClaims\n",

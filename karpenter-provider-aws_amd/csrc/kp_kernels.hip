@@ -1010,11 +1010,28 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 cqscan += t_d - t_c;
                 if (f < N) {
                     const int fl = f - wb;
-                    bool ok = wa && A > 0;  // no witness table (A == 0): every pod is evaluated
+                    bool wfit = A > 0;  // no witness table (A == 0): every pod is evaluated
 #pragma unroll
                     for (int ai = 0; ai < KP_LDS_AXES; ai++)
-                        if (ai < A) ok &= pq[ai] <= wh[ai];
-                    const uint64_t okm = ballot(ok);
+                        if (ai < A) wfit &= pq[ai] <= wh[ai];
+                    uint64_t okm = ballot(wa && wfit);
+                    if (!((okm >> fl) & 1ull) && ((ballot(wfit) >> fl) & 1ull) && d.noop_quick) {
+                        // the NodeClaim at f has not absorbed the class but its witness fits: the Add is the quick accept
+                        // when the class's requirement merge changes nothing (and the class tolerates its template)
+                        const int nc = rl32((int)wo, fl), tm = (int)((uint32_t)rl32((int)wm, fl) >> 16);
+                        if (((tl >> tm) & 1ull) && merge_noop(d, S.ws[0], nc, c, lane)) {
+                            if (lane == fl) {
+                                wm = (wm & 0xFFFF0000u) | (uint32_t)(uint16_t)c;
+                                wa = true;
+                            }
+                            if (lane == 0) {
+                                slast[nc] = (uint16_t)c;  // its requirements are a subset of the class's
+                                if (d.profile) S.st[ST_SLOW_WHY + 4]++;
+                            }
+                            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                            okm |= 1ull << fl;
+                        }
+                    }
                     if ((okm >> fl) & 1ull) {
                         // quick accept: NodeClaim.Add(pod) succeeds with state (requirements, options) unchanged.
                         // Batch: the next pods of the same shape go one each to the following NodeClaims of the run of
@@ -1151,6 +1168,10 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                     }
                 }
                 // slow path: the whole block evaluates this pod
+                if (d.profile) {  // KPSIM_PROFILE: why the quick accept does not apply
+                    const bool fa = f < N && rl32(wa ? 1 : 0, (f - wb) & 63) != 0;
+                    if (lane == 0) S.st[ST_SLOW_WHY + (f >= N ? 0 : A == 0 ? 3 : !fa ? 1 : 2)]++;
+                }
                 win_flush();
                 wb = -1;
                 if (lane < R) S.pod_req[lane] = S.qw_req[off][lane];
