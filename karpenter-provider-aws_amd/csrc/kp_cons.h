@@ -16,6 +16,7 @@ enum { CS_POPS = 0, CS_EX_NODES, CS_NC_EVALS, CS_TMPL_EVALS, CS_PROBES, CS_BITMA
 
 #define KP_CONS_XTC 1024  // pod classes whose XT column of the cached node chunk is kept in LDS
 #define KP_CONS_STORE 8   // node chunks the fast probe variant keeps in its LDS headroom store
+#define KP_CONS_PP 16     // KPSIM_PROFILE: per-probe counters (kp_consolidate's diagnostics)
 
 struct KpCons {
     int32_t n_probes;           // probes of this call (out[0 .. n_probes))
@@ -86,6 +87,10 @@ struct KpCons {
     // request exceeds one on some axis skips the chunk without loading it (use_cmax: the LDS plan has room)
     const int64_t* cmax0;       // [EW][KP_LDS_AXES]
     int32_t use_cmax;
+    // multi-node probes' pods (multi_union_kernel): [ulen] {pod | pending << 31, candidate or -1}, in queue order; null:
+    // every probe marks and scans its own queue-position bitmap
+    const int2* ulist;
+    const int32_t* ulen;
     int32_t profile;            // s_memtime stage cycles (KPSIM_PROFILE)
     int64_t* prof_probe;        // KPSIM_PROFILE: [n_probes][4] cycles of build, existing-node placement, total; pods
     int32_t no_fast;            // diagnostics: every probe on the FULL variant (KPSIM_CONS_NOFAST)

@@ -271,7 +271,16 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
     for (int it = 0;; it++) {
         int probe = 0;
         if (!FULL) {  // static stride: a shared work counter serialises in L2 at thousands of probes
-            probe = wid + it * (int)gridDim.x;
+            const int nm = k.mode == KP_CONSOLIDATE_BOTH ? k.n_multi : 0;
+            const int G = (int)gridDim.x;
+            if (nm > 0 && G >= 2 * nm) {
+                // the pass waits for its longest probes, the multi-node prefixes: their workers take nothing else, the
+                // single-node probes stride over the other workers
+                if (wid < nm) probe = it == 0 ? wid : k.n_probes;
+                else probe = nm + (wid - nm) + it * (G - nm);
+            } else {
+                probe = wid + it * G;
+            }
         } else {
             if (lane == 0) {
                 if (k.no_fast == 1) {
@@ -294,6 +303,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
         int64_t st_pops = 0, st_nodes = 0, st_nc = 0, st_tmpl = 0, st_words = 0, st_placed = 0, st_loads = 0, st_hits = 0;
         int64_t st_skips = 0, st_relax = 0;
         long long pf_load = 0, pf_prep = 0, pf_nodes = 0, pf_visits = 0;  // KPSIM_PROFILE: fast-path stages
+        long long pf_many = 0, pf_iters = 0, pf_miss_cyc = 0, pf_miss = 0;
         long long cy_build = 0, cy_scan = 0, cy_nc = 0, cy_dec = 0;
         const bool prof = k.profile != 0;
         const long long cy0 = prof ? __builtin_amdgcn_s_memtime() : 0;
@@ -347,7 +357,23 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
         }
         // ---- the probe's pods in queue order ----
         int n = 0;
-        if (k.n_pending == 0 && n_np <= 64) {
+        if (!single && k.ulist) {
+            // multi-node prefix: the call's union list in queue order, filtered to candidates [0, c1) and pending pods
+            const int ul = ld32(k.ulen);
+            int2 nx = lane < ul ? k.ulist[lane] : make_int2(0, INT32_MAX);
+            for (int b = 0; b < ul; b += 64) {
+                const int2 e = nx;
+                nx = b + 64 + lane < ul ? k.ulist[b + 64 + lane] : make_int2(0, INT32_MAX);
+                const bool keep = e.y < c1;
+                const uint64_t m = ballot(keep);
+                if (keep) {
+                    const int pos = n + __popcll(m & ((1ull << lane) - 1ull));
+                    ring[pos] = e.x;
+                    rlast[pos] = -1;
+                }
+                n += __popcll(m);
+            }
+        } else if (k.n_pending == 0 && n_np <= 64) {
             // at most one pod per lane: bitonic sort of (queue position, pod) across the wave
             const int myp = lane < n_np ? k.cand_pods[po0 + lane] : -1;
             uint64_t key = myp >= 0 ? ((uint64_t)(uint32_t)k.rank[myp] << 32) | (uint32_t)myp : ~0ull;
@@ -441,6 +467,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             }
         };
         int n_nc = 0, nc_tmpl = -1, prev_shape = -1, xstart = 0, ok_np = 0, nc_nonpend = 0;
+        int nc_lc = -1;  // the class whose requirements the in-flight NodeClaim last merged (its Add is then Fits only)
         int relax_at = -1;  // queue position of the last Queue.Push(pod, relaxed): every lastLen pushed before is gone
         bool aborted = false;
         int cbase = -1, ccls = -1;  // cached node chunk (wave-uniform)
@@ -698,6 +725,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                         if (!em) continue;
                         uint64_t took = 0;
                         if (__popcll(em) > 4) {
+                            pf_many++;
                             // many: the prefix up to the first running-total overflow is taken in one round of prefix sums
                             bool over = false;
                             int64_t pv[KP_LDS_AXES];
@@ -720,6 +748,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                         // few: greedily in queue order with scalar running totals
                         for (; em; em &= em - 1) {
                             const int t = __ffsll((unsigned long long)em) - 1;
+                            pf_iters++;
                             int64_t qt[KP_LDS_AXES];
                             bool ok = true;
                             AXL(ai) {
@@ -748,6 +777,8 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     if (prof) pf_nodes += __builtin_amdgcn_s_memtime() - cn0;
                 }
                 // the pods no store node takes: the chunks after the store, serially in queue order
+                const long long cm0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+                if (prof) pf_miss += __popcll(U);
                 for (uint64_t m = U; m && !aborted; m &= m - 1) {
                     const int i = __ffsll((unsigned long long)m) - 1;
                     const int c = rl32(wc, i);
@@ -785,6 +816,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                         else bad = true;
                     }
                 }
+                if (prof) pf_miss_cyc += __builtin_amdgcn_s_memtime() - cm0;
                 if (FULL && live) pnode[wb + lane] = ((U >> lane) & 1ull) ? -1 : 0;
             }
             if (FULL && k.relax) {
@@ -912,8 +944,20 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                 a.host = E;  // the in-flight NodeClaim's hostname row
                 a.held = nc_held;
                 st_nc++;
-                if (tcons ? eval_wave<true, RESV, false, true, true>(d, Ev, S.CC, a, S.ws, lane)
-                          : eval_wave<false, RESV, false>(d, Ev, S.CC, a, S.ws, lane)) {
+                // the NodeClaim has absorbed the class (no topology, no reservations): the merge is idempotent and the
+                // label / offering filters already hold for its options, so the Add is Fits (+ minValues) only
+                const bool absorbed = c == nc_lc && !(TOPO && (cflags & CF_TOPO)) && !(RESV && d.resv_on);
+                if (absorbed) {
+                    if (eval_fits_only<true>(d, Ev, a, S.ws, lane)) {
+                        if (lane < TW) nc_opts = S.ws.opts[lane];
+                        if (lane < R) S.nc_req[lane] += preq[lane];
+                        __syncthreads();
+                        if (d.best_effort) commit_min_relax_lds(nch, S.ws, lane);
+                        placed = true;
+                    }
+                } else if (tcons ? eval_wave<true, RESV, false, true, true>(d, Ev, S.CC, a, S.ws, lane)
+                                 : eval_wave<false, RESV, false>(d, Ev, S.CC, a, S.ws, lane)) {
+                    nc_lc = c;
                     if (lane < S.CC.nck) {
                         const int kk = S.CC.key[lane];
                         nch[kk] = S.ws.hdr[lane];
@@ -981,6 +1025,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     }
                     nc_tmpl = j;
                     n_nc = 1;
+                    nc_lc = c;
                     placed = true;
                     __syncthreads();
                     if (d.best_effort) commit_min_relax_lds(nch, S.ws, lane);
@@ -1278,7 +1323,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
             S.st[CS_RELAXED] += st_relax;
             if (prof) {
                 if (k.prof_probe) {
-                    int64_t* pp = k.prof_probe + (size_t)oi * 8;
+                    int64_t* pp = k.prof_probe + (size_t)oi * KP_CONS_PP;
                     pp[0] = cy_build;
                     pp[1] = cy_scan;
                     pp[2] = __builtin_amdgcn_s_memtime() - cy0;
@@ -1287,6 +1332,12 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
                     pp[5] = pf_prep;
                     pp[6] = pf_nodes;
                     pp[7] = pf_visits;
+                    pp[8] = pf_many;
+                    pp[9] = pf_iters;
+                    pp[10] = pf_miss_cyc;
+                    pp[11] = pf_miss;
+                    pp[12] = cy_nc;
+                    pp[13] = cy_dec;
                 }
                 S.st[CS_CYC_BUILD] += cy_build;
                 S.st[CS_CYC_SCAN] += cy_scan;
@@ -1421,6 +1472,75 @@ hipError_t kp_launch_consolidate(const KpDev& d, const KpCons& k, int n_workers,
         if (d.ro) hipLaunchKernelGGL((consolidate_kernel<true, true>), dim3(n_workers), dim3(64), lds, s, d, k);
         else hipLaunchKernelGGL(consolidate_kernel<true>, dim3(n_workers), dim3(64), lds, s, d, k);
     }
+    return hipGetLastError();
+}
+
+// The multi-node probes' pods in queue order, built once per call: the pods of candidates [0, nu) (every multi-node
+// prefix of the call draws from them) and the pending pods, one entry per queue position holding either, as
+// {pod | pending << 31, candidate index or -1 for a pending pod}.  A probe over candidates [0, c1) takes the entries
+// with index < c1 in order (consolidate_kernel), instead of marking and scanning a bitmap over every queue position.
+// One block: mark the union's queue positions (and each position's candidate), then compact the marked positions.
+__global__ __launch_bounds__(1024) void multi_union_kernel(const int32_t* __restrict__ cand_off,
+                                                           const int32_t* __restrict__ cand_pods,
+                                                           const int32_t* __restrict__ rank,
+                                                           const int32_t* __restrict__ queue0,
+                                                           const uint64_t* __restrict__ pend_bits, int n_pending, int PW,
+                                                           int nu, uint64_t* __restrict__ ubits,
+                                                           int32_t* __restrict__ rcand, int2* __restrict__ ulist,
+                                                           int32_t* __restrict__ ulen) {
+    __shared__ int32_t wsum[1024];
+    __shared__ int32_t carry;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    for (int w = tid; w < PW; w += nt) ubits[w] = 0;
+    if (tid == 0) carry = 0;
+    __syncthreads();
+    // candidate of CSR entry i: the last c with cand_off[c] <= i (binary search over the union's candidates)
+    const int e0 = cand_off[0], e1 = cand_off[nu];
+    for (int i = e0 + tid; i < e1; i += nt) {
+        int lo = 0, hi = nu - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (cand_off[mid] <= i) lo = mid;
+            else hi = mid - 1;
+        }
+        const int r = rank[cand_pods[i]];
+        atomicOr((unsigned long long*)&ubits[r >> 6], 1ull << (r & 63));
+        rcand[r] = lo;
+    }
+    __syncthreads();
+    for (int wb = 0; wb < PW; wb += nt) {
+        const int w = wb + tid;
+        const uint64_t mine = w < PW ? ubits[w] : 0ull;
+        const uint64_t pend = (w < PW && n_pending) ? pend_bits[w] : 0ull;
+        uint64_t x = mine | pend;
+        const int cnt = __popcll(x);
+        wsum[tid] = cnt;
+        __syncthreads();
+        for (int o = 1; o < nt; o <<= 1) {  // inclusive scan of the words' counts
+            const int v = tid >= o ? wsum[tid - o] : 0;
+            __syncthreads();
+            wsum[tid] += v;
+            __syncthreads();
+        }
+        int pos = carry + wsum[tid] - cnt;
+        while (x) {
+            const int b = __ffsll((unsigned long long)x) - 1;
+            x &= x - 1;
+            const int r = w * 64 + b;
+            const bool pd = (pend >> b) & 1ull;
+            ulist[pos++] = make_int2(queue0[r] | (int32_t)((uint32_t)pd << 31), pd ? -1 : rcand[r]);
+        }
+        __syncthreads();
+        if (tid == nt - 1) carry += wsum[tid];
+        __syncthreads();
+    }
+    if (tid == 0) ulen[0] = carry;
+}
+
+hipError_t kp_launch_multi_union(const KpCons& k, int nu, uint64_t* ubits, int32_t* rcand, int2* ulist, int32_t* ulen,
+                                 const int32_t* queue0, hipStream_t s) {
+    hipLaunchKernelGGL(multi_union_kernel, dim3(1), dim3(1024), 0, s, k.cand_off, k.cand_pods, k.rank, queue0,
+                       k.pend_bits, k.n_pending, k.PW, nu, ubits, rcand, ulist, ulen);
     return hipGetLastError();
 }
 

@@ -42,6 +42,8 @@ bool kp_cons_plan_lds(const KpDev& d, KpCons& k, int max_bytes);
 hipError_t kp_launch_select_kernel(const KpLaunch& g, hipStream_t s);
 hipError_t kp_launch_consolidate(const KpDev& d, const KpCons& k, int n_workers, hipStream_t s);
 hipError_t kp_launch_cons_chunk_max(const KpDev& d, int64_t* cmax0, hipStream_t s);
+hipError_t kp_launch_multi_union(const KpCons& k, int nu, uint64_t* ubits, int32_t* rcand, int2* ulist, int32_t* ulen,
+                                 const int32_t* queue0, hipStream_t s);
 hipError_t kp_launch_cons_prep(const int32_t* queue0, int P, int32_t* rank, const int32_t* pending, int n_pending,
                                uint64_t* pend_bits, hipStream_t s);
 hipError_t kp_queue_sort(const int64_t* fields, int n, int32_t* perm_a, int32_t* perm_b, uint64_t* keys_a,
@@ -460,6 +462,9 @@ struct kp_ctx {
     int last_plan_nc = 0;                    // in-flight NodeClaim capacity of the last prepare
     bool nc_overflow = false;                // the last fetch found the solve out of in-flight NodeClaim capacity
     DBuf<uint64_t> d_pend_bits, d_pbits;
+    DBuf<uint64_t> d_ubits;                  // multi-node probes' union list (multi_union_kernel): queue-position bits,
+    DBuf<int32_t> d_rcand, d_ulen;           // candidate by queue position, list length
+    DBuf<int2> d_ulist;                      // entries
     DBuf<uint64_t> d_init;
     DBuf<kp_probe_result> d_probe_out;
     DBuf<int32_t> d_rec_i;                   // kp_consolidate_command's read-back of the chosen REPLACE probe
@@ -2283,6 +2288,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.topo_cands = getenv("KPSIM_TOPO_CANDS") ? std::max(1, std::min(KP_NWAVES, atoi(getenv("KPSIM_TOPO_CANDS")))) : KP_NWAVES;
     d.team_eval = getenv("KPSIM_NO_TEAM") ? 0 : 1;  // diagnostics: KPSIM_NO_TEAM=1 evaluates topology candidates one per wave
     d.noop_quick = getenv("KPSIM_NO_NOOP") ? 0 : 1;  // diagnostics: KPSIM_NO_NOOP=1 disables the no-op merge quick accept
+    d.team_first = getenv("KPSIM_NO_TEAM_FIRST") ? 0 : 1;  // diagnostics: KPSIM_NO_TEAM_FIRST=1 evaluates it beside the others
     // KPSIM_TRACE_POD=p traces pod p; KPSIM_TRACE_CLASS=c traces every slow-path pod of class c (trace_pod = -2 - c)
     d.trace_pod = getenv("KPSIM_TRACE_POD") ? atoi(getenv("KPSIM_TRACE_POD"))
                   : getenv("KPSIM_TRACE_CLASS") ? -2 - atoi(getenv("KPSIM_TRACE_CLASS")) : -1;
@@ -2493,8 +2499,11 @@ extern "C" kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out) {
     for (int i = 0; i < 4; i++) c->cycles[33 + i] = st[ST_REJ_REQ + i];
     if (getenv("KPSIM_PROFILE") && st[ST_SLOW_WHY] + st[ST_SLOW_WHY + 1] + st[ST_SLOW_WHY + 2] + st[ST_SLOW_WHY + 3])
         fprintf(stderr, "[kpsim] slow-path pods: no candidate %lld, class not absorbed %lld, witness short %lld, no witness table %lld; "
-                "no-op merge quick accepts %lld\n", (long long)st[ST_SLOW_WHY], (long long)st[ST_SLOW_WHY + 1],
-                (long long)st[ST_SLOW_WHY + 2], (long long)st[ST_SLOW_WHY + 3], (long long)st[ST_SLOW_WHY + 4]);
+                "no-op merge quick accepts %lld; placed by the first candidate %lld, a later one %lld, the templates %lld; "
+                "block-evaluated first candidates %lld\n",
+                (long long)st[ST_SLOW_WHY], (long long)st[ST_SLOW_WHY + 1], (long long)st[ST_SLOW_WHY + 2],
+                (long long)st[ST_SLOW_WHY + 3], (long long)st[ST_SLOW_WHY + 4], (long long)st[ST_SLOW_WHY + 5],
+                (long long)st[ST_SLOW_WHY + 6], (long long)st[ST_SLOW_WHY + 7], (long long)st[ST_SLOW_WHY + 8]);
     if (getenv("KPSIM_PROFILE") && st[ST_TQ_WHY] + st[ST_TQ_WHY + 1] + st[ST_TQ_WHY + 2] + st[ST_TQ_WHY + 3] + st[ST_TQ_WHY + 4])
         fprintf(stderr, "[kpsim] topology pods past the prefilter: no survivor %lld, not QREC %lld, no quick row %lld, class not "
                         "absorbed %lld, quick row %lld (witness fits %lld, merge no-op %lld); NQ %d of %d NodeClaims\n",
@@ -2936,10 +2945,22 @@ static kp_status cons_run(kp_ctx* ctx, int m0, int m1, int s0, int s1, kp_probe_
     k.profile = getenv("KPSIM_PROFILE") ? 1 : 0;
     k.no_fast = getenv("KPSIM_CONS_NOFAST") ? atoi(getenv("KPSIM_CONS_NOFAST")) : 0;  // 1: FULL only, 2: fast only
     if (A > KP_LDS_AXES) k.no_fast = 1;  // more requested axes than the probe registers hold: the FULL variant's serial path
+    k.ulist = nullptr;
+    k.ulen = nullptr;
+    if (nmp > 0 && !getenv("KPSIM_CONS_NOUNION")) {  // diagnostics: KPSIM_CONS_NOUNION=1 builds every probe from bitmaps
+        const int nu = std::min(NC, m1 + 1);  // candidates of the call's longest prefix
+        HIPCHK(c->d_ubits.ensure(std::max(k.PW, 1)));
+        HIPCHK(c->d_rcand.ensure(std::max(P, 1)));
+        HIPCHK(c->d_ulen.ensure(1));
+        HIPCHK(c->d_ulist.ensure((size_t)std::max(1, coff[nu] - coff[0] + c->cons_n_pending)));
+        HIPCHK(kp_launch_multi_union(k, nu, c->d_ubits.p, c->d_rcand.p, c->d_ulist.p, c->d_ulen.p, c->cons_q0, s));
+        k.ulist = c->d_ulist.p;
+        k.ulen = c->d_ulen.p;
+    }
     k.prof_probe = nullptr;
     if (k.profile) {
-        HIPCHK(c->d_prof_probe.ensure((size_t)nprobe * 8));
-        HIPCHK(hipMemsetAsync(c->d_prof_probe.p, 0, (size_t)nprobe * 8 * sizeof(int64_t), s));
+        HIPCHK(c->d_prof_probe.ensure((size_t)nprobe * KP_CONS_PP));
+        HIPCHK(hipMemsetAsync(c->d_prof_probe.p, 0, (size_t)nprobe * KP_CONS_PP * sizeof(int64_t), s));
         k.prof_probe = c->d_prof_probe.p;
     }
     k.rec_i = nullptr;
@@ -2973,19 +2994,22 @@ static kp_status cons_run(kp_ctx* ctx, int m0, int m1, int s0, int s1, kp_probe_
     c->cons_ms[2] = ns_since(t0) * 1e-6;
     for (int i = 0; i < CS_COUNT; i++) c->cons_stats[i] = cst[i];
     if (k.prof_probe) {  // diagnostics: the probes that bound the pass
-        std::vector<int64_t> pp((size_t)nprobe * 8);
+        std::vector<int64_t> pp((size_t)nprobe * KP_CONS_PP);
         HIPCHK(hipMemcpy(pp.data(), k.prof_probe, pp.size() * sizeof(int64_t), hipMemcpyDeviceToHost));
         for (int part = 0; part < 2; part++) {
             const int b = part == 0 ? 0 : nmp, e = part == 0 ? nmp : nprobe;
             int arg = -1;
             for (int i = b; i < e; i++)
-                if (arg < 0 || pp[(size_t)i * 8 + 2] > pp[(size_t)arg * 8 + 2]) arg = i;
+                if (arg < 0 || pp[(size_t)i * KP_CONS_PP + 2] > pp[(size_t)arg * KP_CONS_PP + 2]) arg = i;
             if (arg >= 0) {
-                const int64_t* q = &pp[(size_t)arg * 8];
+                const int64_t* q = &pp[(size_t)arg * KP_CONS_PP];
                 fprintf(stderr, "[kpsim] %s probes %d: longest #%d: %lld cycles (build %lld, placement %lld: window loads %lld, "
                         "chunk prep %lld, node intake %lld over %lld node visits), %lld pods\n",
                         part == 0 ? "multi-node" : "single-node", e - b, arg - b, (long long)q[2], (long long)q[0],
                         (long long)q[1], (long long)q[4], (long long)q[5], (long long)q[6], (long long)q[7], (long long)q[3]);
+                fprintf(stderr, "[kpsim]   intake: %lld prefix-sum rounds, %lld scalar steps; %lld pods past the store in %lld "
+                        "cycles; NodeClaim %lld cycles, decide %lld cycles\n", (long long)q[8], (long long)q[9],
+                        (long long)q[11], (long long)q[10], (long long)q[12], (long long)q[13]);
             }
         }
     }

@@ -1398,10 +1398,58 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
             __syncthreads();
             round++;
         }
-        for (; !team;) {
+        // a pod without topology terms whose first candidate needs the full Add (it has not absorbed the class): that
+        // candidate first, evaluated by the whole block (it takes most such pods); the others then in parallel as below
+        int first = 0;  // round-0 candidates already evaluated
+        bool team_won = false;
+        if (!team && d.team_first && S.n_cand[0] > 0) {
+            const int nc = sord[S.cand_pos[0][0]];
+            const int tm = d.nc_tmpl[nc];
+            const bool fast0 = !(S.CC.flags & CF_TOPO) && !(RESV && d.resv_on && ld_i32(&d.nc_rlive[nc])) &&
+                               (slast[nc] == (uint16_t)S.cur_cls || ((S.CC.flags & CF_NOKEYS) && ((S.CC.tol >> tm) & 1ull)));
+            if (!fast0) {
+                EvalIn a;
+                a.Ahdr = d.nc_hdr + (size_t)nc * K;
+                a.Aw = d.nc_words + (size_t)nc * d.DW;
+                a.opts = lane < TW ? d.nc_opts[(size_t)nc * TW + lane] : 0;
+                a.base_req = d.nc_req + (size_t)nc * R;
+                a.pod_req = S.pod_req;
+                a.tmpl = tm;
+                a.compat = true;
+                a.force_off = false;
+                a.prof = (d.profile && wave == 0) ? &S.st[ST_EV_REQ] : nullptr;
+                a.host = d.E + nc;
+                a.held = (RESV && d.resv_on) ? ld_u64(&d.nc_held[nc]) : 0ull;
+                const bool ok = (TOPO_ON && (S.CC.flags & CF_TOPO_CONS))
+                                    ? eval_wave<true, RESV, true, PREF, false, true>(d, E, S.CC, a, S.ws[wave], lane, &S.team[0],
+                                                                                     wave, KP_NWAVES)
+                                    : eval_wave<false, RESV, true, PREF, false, true>(d, E, S.CC, a, S.ws[wave], lane,
+                                                                                      &S.team[0], wave, KP_NWAVES);
+                if (wave == 0 && lane == 0) {
+                    S.fastp[0][0] = 0;
+                    S.acc[0][0] = ok;
+                    if (!ok && S.ws[0].memo_ok) {
+                        skey[S.cand_pos[0][0]] |= 0x80000000u;
+                        S.any_rej = 1;
+                    }
+                    if (!ok && !S.ws[0].memo_ok) S.rej_volatile = 1;
+                    S.st[ST_NC_EVALS]++;
+                    if (d.profile) S.st[ST_SLOW_WHY + 8]++;
+                }
+                first = 1;
+                if (ok) {
+                    win = 0;
+                    team_won = true;
+                }
+                __syncthreads();  // the team's scratch (S.team[0]) and acc[0][0] before the parallel round
+            }
+        }
+        for (; !team && !team_won;) {
             const int b = round & 1;
-            if (wave < S.n_cand[b]) {
-                const int nc = sord[S.cand_pos[b][wave]];
+            const int f0 = round == 0 ? first : 0;  // candidate index of wave 0
+            const int ci = wave + f0;
+            if (ci < S.n_cand[b]) {
+                const int nc = sord[S.cand_pos[b][ci]];
                 EvalIn a;
                 a.Ahdr = d.nc_hdr + (size_t)nc * K;
                 a.Aw = d.nc_words + (size_t)nc * d.DW;
@@ -1429,17 +1477,17 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                         e[1] = nc;
                         e[2] = ok;
                         e[3] = S.ws[wave].memo_ok | (fast << 1) | ((RESV ? ld_i32(&d.nc_rlive[nc]) : 0) << 2);
-                        e[4] = S.cand_pos[b][wave];
+                        e[4] = S.cand_pos[b][ci];
                         e[5] = (int)(a.held & 0xFFFFFFFFu);
                     }
                 }
                 if (lane == 0) {
-                    S.fastp[b][wave] = fast;
-                    S.acc[b][wave] = ok;
+                    S.fastp[b][ci] = fast;
+                    S.acc[b][ci] = ok;
                     if (!ok && S.ws[wave].memo_ok) {
                         // rejected this shape for good (positions are stable here); a rejection that depended on
                         // topology counts is not memoised, one that depended on reservation capacity until rel_flag
-                        skey[S.cand_pos[b][wave]] |= 0x80000000u;
+                        skey[S.cand_pos[b][ci]] |= 0x80000000u;
                         S.any_rej = 1;
                     }
                     if (!ok && !S.ws[wave].memo_ok) S.rej_volatile = 1;
@@ -1448,12 +1496,12 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
             }
             __syncthreads();
             const int nc_ = S.n_cand[b];
-            for (int w = 0; w < nc_; w++)
+            for (int w = f0; w < nc_; w++)
                 if (S.acc[b][w]) {
                     win = w;
                     break;
                 }
-            if (tid == 0) S.st[ST_NC_EVALS] += nc_;
+            if (tid == 0) S.st[ST_NC_EVALS] += nc_ > f0 ? nc_ - f0 : 0;
             if (win >= 0 || S.scan_done[b]) break;
             if (wave == 0)
                 collect_candidates(d, S, skey, sord, stmpl, S.topo_pod ? d.tol[S.cur_cls] : ~0ull, S.N, S.scan_next[b], b ^ 1, lane);
@@ -1464,8 +1512,11 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
             const long long t1 = __builtin_amdgcn_s_memtime();
             S.st[ST_CYC_SCAN] += t1 - c_slow;
         }
+        if (d.profile && tid == 0 && !S.topo_pod)  // KPSIM_PROFILE: where the slow path's pods land
+            S.st[ST_SLOW_WHY + (win < 0 ? 7 : (round == 0 && win == 0) ? 5 : 6)]++;
         if (win >= 0) {
-            const int cw = team ? 0 : win;  // the wave whose scratch holds the accepted Add (team: every wave's does)
+            // the wave whose scratch holds the accepted Add (team: every wave's does)
+            const int cw = (team || team_won) ? 0 : win - (round == 0 ? first : 0);
             if (wave == cw) {
                 const int pos = S.cand_pos[round & 1][win];
                 const int nc = sord[pos];

@@ -189,6 +189,7 @@ struct KpDev {
     int32_t topo_cands;              // NodeClaims evaluated per block round for a topology pod (<= KP_NWAVES)
     int32_t team_eval;               // topology pods: one candidate at a time, evaluated by the whole block (eval_wave TEAM)
     int32_t noop_quick;              // fast loop: quick accept on a NodeClaim whose merge with the class changes nothing
+    int32_t team_first;              // slow path: a first candidate that needs the full Add is evaluated by the whole block
     int32_t trace_pod;               // diagnostics (KPSIM_TRACE_POD): the slow path logs this pod's evaluations
     int32_t trace_max;               //   KPSIM_TRACE_CLASS: only pods with index <= KPSIM_TRACE_MAXPOD
     int32_t* trace;                  //   [1 + 6 * KP_TRACE_N]: count, then {round, nodeclaim (-1-j: template j), ok, flags, held lo/hi}
@@ -276,5 +277,5 @@ enum {
     ST_REJ_REQ = 48, ST_REJ_TOPO, ST_REJ_TYPES, ST_REJ_MIN,
     // KPSIM_PROFILE: topology pods past the prefilter — no surviving NodeClaim, class records through another class's
     // node filter (not QREC), NodeClaim without a quick row, class not absorbed, quick row present; witness fits
-    ST_TQ_WHY = 52, ST_SLOW_WHY = 59, ST_COUNT = 64
+    ST_TQ_WHY = 52, ST_SLOW_WHY = 59, ST_COUNT = 68
 };
