@@ -437,6 +437,7 @@ struct kp_ctx {
     DBuf<int32_t> d_kcat, d_kmulti, d_woff, d_nw, d_nval, d_vbase, d_cls_koff, d_cls_keys, d_cls_wsoff, d_min_keys;
     DBuf<uint8_t> d_val_isint, d_limit_set;
     DBuf<int64_t> d_val_int, d_daemon, d_remaining, d_pod_req, d_sort_fields, d_nc_req, d_stats;
+    DBuf<uint64_t> d_tmpl_lmask;             // [NT][TW] FFD kernel: types within each template's remaining limits
     DBuf<ReqHdr> d_cls_hdr, d_nc_hdr, d_empty_hdr;
     DBuf<uint64_t> d_cls_words, d_V, d_tmpl_rows, d_tmpl_opts, d_nc_words, d_nc_opts, d_empty_words, d_keys_a, d_keys_b;
     DBuf<int32_t> d_tmpl_ok, d_pod_cls, d_pod_shape, d_perm_a, d_perm_b, d_nc_tmpl, d_qbuf, d_last_len, d_pod_result,
@@ -2233,6 +2234,8 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.daemon = c->d_daemon.p;
     d.limit_set = c->d_limit_set.p;
     d.remaining = c->d_remaining.p;
+    HIPCHK(c->d_tmpl_lmask.ensure((size_t)std::max(1, d.NT) * std::max(1, d.TW)));
+    d.tmpl_lmask = c->d_tmpl_lmask.p;
     d.min_keys = c->d_min_keys.p;
     d.E = E;
     d.EW = EW;
@@ -2500,10 +2503,11 @@ extern "C" kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out) {
     if (getenv("KPSIM_PROFILE") && st[ST_SLOW_WHY] + st[ST_SLOW_WHY + 1] + st[ST_SLOW_WHY + 2] + st[ST_SLOW_WHY + 3])
         fprintf(stderr, "[kpsim] slow-path pods: no candidate %lld, class not absorbed %lld, witness short %lld, no witness table %lld; "
                 "no-op merge quick accepts %lld; placed by the first candidate %lld, a later one %lld, the templates %lld; "
-                "block-evaluated first candidates %lld\n",
+                "block-evaluated first candidates %lld; cycles: commit + templates %lld, class cache fills %lld\n",
                 (long long)st[ST_SLOW_WHY], (long long)st[ST_SLOW_WHY + 1], (long long)st[ST_SLOW_WHY + 2],
                 (long long)st[ST_SLOW_WHY + 3], (long long)st[ST_SLOW_WHY + 4], (long long)st[ST_SLOW_WHY + 5],
-                (long long)st[ST_SLOW_WHY + 6], (long long)st[ST_SLOW_WHY + 7], (long long)st[ST_SLOW_WHY + 8]);
+                (long long)st[ST_SLOW_WHY + 6], (long long)st[ST_SLOW_WHY + 7], (long long)st[ST_SLOW_WHY + 8],
+                (long long)st[ST_SLOW_WHY + 9], (long long)st[ST_SLOW_WHY + 10]);
     if (getenv("KPSIM_PROFILE") && st[ST_TQ_WHY] + st[ST_TQ_WHY + 1] + st[ST_TQ_WHY + 2] + st[ST_TQ_WHY + 3] + st[ST_TQ_WHY + 4])
         fprintf(stderr, "[kpsim] topology pods past the prefilter: no survivor %lld, not QREC %lld, no quick row %lld, class not "
                         "absorbed %lld, quick row %lld (witness fits %lld, merge no-op %lld); NQ %d of %d NodeClaims\n",

@@ -453,25 +453,30 @@ __device__ inline void collect_candidates(const KpDev& d, FfdShared& S, const ui
 }
 
 // types whose Capacity exceeds a NodePool's remaining limits (filterByRemainingResources)
-__device__ inline uint64_t limit_filter(const KpDev& d, int j, uint64_t o, int lane) {
-    bool any_limit = false;
-    for (int r = 0; r < d.R; r++) any_limit |= d.limit_set[(size_t)j * d.R + r] != 0;
-    if (!any_limit) return o;
-    uint64_t out = 0;
-    for (int w = 0; w < d.TW; w++) {
-        const uint64_t cw = rl64(o, w);
-        if (!cw) continue;
+// Types of template j whose capacity fits its NodePool's remaining limits (the NewNodeClaim limit filter): tmpl_lmask
+// holds them by word (lane w: word w), set at kernel start and recomputed for a template when a NodeClaim of it takes
+// capacity off its limits (limit_mask_update), so a template evaluation reads one word per lane.
+__device__ __forceinline__ uint64_t limit_filter(const KpDev& d, int j, uint64_t o, int lane) {
+    return lane < d.TW ? o & d.tmpl_lmask[(size_t)j * d.TW + lane] : o;
+}
+
+// tmpl_lmask[j][w] from the current remaining limits (one wave; every limited axis of j: capacity <= remaining).
+__device__ inline void limit_mask_update(const KpDev& d, int j, int lane) {
+    uint32_t lm = 0;
+    for (int r = 0; r < d.R; r++)
+        if (d.limit_set[(size_t)j * d.R + r]) lm |= 1u << r;
+    uint64_t mine = ~0ull;
+    for (int w = 0; w < d.TW && lm; w++) {
         const int t = w * 64 + lane;
-        bool keep = (cw >> lane) & 1ull;
-        if (keep) {
-            for (int r = 0; r < d.R; r++)
-                if (d.limit_set[(size_t)j * d.R + r] && d.cap[(size_t)r * d.T + t] > d.remaining[(size_t)j * d.R + r])
-                    keep = false;
+        bool keep = t < d.T;
+        for (uint32_t m = lm; m && keep; m &= m - 1) {
+            const int r = __ffs(m) - 1;
+            keep = d.cap[(size_t)r * d.T + t] <= ld_req(&d.remaining[(size_t)j * d.R + r]);
         }
         const uint64_t nb = ballot(keep);
-        if (lane == w) out = nb;
+        if (lane == w) mine = nb;
     }
-    return out;
+    if (lane < d.TW) d.tmpl_lmask[(size_t)j * d.TW + lane] = mine;
 }
 
 __device__ __forceinline__ long long prof_clock(const KpDev& d) { return d.profile ? __builtin_amdgcn_s_memtime() : 0; }
@@ -602,6 +607,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
         d.pod_result[p] = -1;
         d.pod_order[p] = -1;
     }
+    for (int j = wave; j < d.NT; j += KP_NWAVES) limit_mask_update(d, j, lane);  // the NodePools' limits of this solve
     if (PREF && d.relax_next)  // a previous execute may have relaxed pods: every pod starts from its input class
         for (int p = tid; p < P; p += nthr) {
             d.pod_cls[p] = d.pod_cls0[p];
@@ -1336,7 +1342,11 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 continue;
             }
         }
-        if (S.cls_fill) fill_class_cache(d, S.cur_cls, S.CC, tid, nthr);
+        {
+            const long long cf0 = (d.profile && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
+            if (S.cls_fill) fill_class_cache(d, S.cur_cls, S.CC, tid, nthr);
+            if (d.profile && tid == 0) S.st[ST_SLOW_WHY + 10] += __builtin_amdgcn_s_memtime() - cf0;
+        }
 
         // ================= in-flight NodeClaims in slice order: first whose Add succeeds =================
         int round = 0, win = -1;
@@ -1508,9 +1518,11 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
             __syncthreads();
             round++;
         }
+        long long c_ev = 0;
         if (tid == 0 && d.profile) {
             const long long t1 = __builtin_amdgcn_s_memtime();
             S.st[ST_CYC_SCAN] += t1 - c_slow;
+            c_ev = t1;
         }
         if (d.profile && tid == 0 && !S.topo_pod)  // KPSIM_PROFILE: where the slow path's pods land
             S.st[ST_SLOW_WHY + (win < 0 ? 7 : (round == 0 && win == 0) ? 5 : 6)]++;
@@ -1648,6 +1660,8 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                             mx = wave_max64(mx);
                             if (lane == 0) d.remaining[(size_t)jj * R + r] -= mx;
                         }
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the new remaining limits have landed
+                        limit_mask_update(d, jj, lane);
                         if (lane == 0) {
                             slast[n] = (uint16_t)S.cur_cls;
                             stmpl[n] = (uint8_t)jj;
@@ -1692,6 +1706,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
             S.topo_pod = 0;
         }
         __syncthreads();
+        if (tid == 0 && d.profile) S.st[ST_SLOW_WHY + 9] += __builtin_amdgcn_s_memtime() - c_ev;  // commit / templates
     }
 
     // ---- outputs ----

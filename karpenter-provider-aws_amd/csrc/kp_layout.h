@@ -142,6 +142,7 @@ struct KpDev {
     const int64_t* daemon;           // [NT][R]
     const uint8_t* limit_set;        // [NT][R]
     int64_t* remaining;              // [NT][R] (mutated by the FFD kernel)
+    uint64_t* tmpl_lmask;            // [NT][TW] types within each template's remaining limits (FFD kernel scratch)
     const int32_t* min_keys;         // [NT][KP_MAX_CLASS_KEYS] keys carrying minValues (-1 terminated)
 
     // ---------------- pods ----------------
@@ -277,5 +278,5 @@ enum {
     ST_REJ_REQ = 48, ST_REJ_TOPO, ST_REJ_TYPES, ST_REJ_MIN,
     // KPSIM_PROFILE: topology pods past the prefilter — no surviving NodeClaim, class records through another class's
     // node filter (not QREC), NodeClaim without a quick row, class not absorbed, quick row present; witness fits
-    ST_TQ_WHY = 52, ST_SLOW_WHY = 59, ST_COUNT = 68
+    ST_TQ_WHY = 52, ST_SLOW_WHY = 59, ST_COUNT = 70
 };
