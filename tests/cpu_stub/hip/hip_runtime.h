@@ -25,6 +25,10 @@ struct int4 {
     int x, y, z, w;
 };
 inline int4 make_int4(int x, int y, int z, int w) { return int4{x, y, z, w}; }
+struct int2 {
+    int x, y;
+};
+inline int2 make_int2(int x, int y) { return int2{x, y}; }
 
 hipError_t hipGetDeviceCount(int* n);
 hipError_t hipSetDevice(int d);

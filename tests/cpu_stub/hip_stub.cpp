@@ -140,6 +140,9 @@ hipError_t kp_launch_cons_prep(const int32_t*, int, int32_t*, const int32_t*, in
     return hipSuccess;
 }
 hipError_t kp_launch_cons_chunk_max(const KpDev&, int64_t*, hipStream_t) { return hipSuccess; }
+hipError_t kp_launch_multi_union(const KpCons&, int, uint64_t*, int32_t*, int2*, int32_t*, const int32_t*, hipStream_t) {
+    return hipSuccess;
+}
 hipError_t kp_queue_sort(const int64_t* fields, int n, int32_t* perm_a, int32_t*, uint64_t*, uint64_t*, void*,
                          size_t* temp_bytes, hipStream_t, int32_t** result) {
     if (!fields) {
