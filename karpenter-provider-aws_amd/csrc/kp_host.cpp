@@ -2292,6 +2292,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.team_eval = getenv("KPSIM_NO_TEAM") ? 0 : 1;  // diagnostics: KPSIM_NO_TEAM=1 evaluates topology candidates one per wave
     d.noop_quick = getenv("KPSIM_NO_NOOP") ? 0 : 1;  // diagnostics: KPSIM_NO_NOOP=1 disables the no-op merge quick accept
     d.team_first = getenv("KPSIM_NO_TEAM_FIRST") ? 0 : 1;  // diagnostics: KPSIM_NO_TEAM_FIRST=1 evaluates it beside the others
+    d.block_sort = getenv("KPSIM_NO_BLOCK_SORT") ? 0 : 1;  // diagnostics: KPSIM_NO_BLOCK_SORT=1 leaves it to wave 0
     // KPSIM_TRACE_POD=p traces pod p; KPSIM_TRACE_CLASS=c traces every slow-path pod of class c (trace_pod = -2 - c)
     d.trace_pod = getenv("KPSIM_TRACE_POD") ? atoi(getenv("KPSIM_TRACE_POD"))
                   : getenv("KPSIM_TRACE_CLASS") ? -2 - atoi(getenv("KPSIM_TRACE_CLASS")) : -1;

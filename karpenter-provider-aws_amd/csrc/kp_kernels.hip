@@ -174,6 +174,8 @@ struct FfdShared {
     int tacc[KP_NWAVES];
     int n_cand[2], scan_done[2], scan_next[2];
     int sstack[64 * 5];
+    int bred[2][KP_NWAVES];        // block_sort_move: per-wave first match, double-buffered by round
+    int eager, eager_pos, eager_e; // block_sort_move applied [eager_pos, eager_e) ahead of the add() that sorts
     // control state: owned by wave 0 inside its fast loop, by the block between the slow-path barriers
     int N, qhead, qcount, done, cur_pod, cur_cls, cur_shape, prev_shape;
     int dirty_kind, dirty_pos, seq, err, cls_fill, scan_start, any_rej;
@@ -554,6 +556,57 @@ __device__ __attribute__((noinline)) int existing_topo_scan(const KpDev* __restr
 // HBM: the slice arrays (9 B per in-flight NodeClaim) live in HBM (d.g_key ...) because the solve is planned for more
 // NodeClaims than LDS holds beside the fixed tables (kp_ffd_plan_lds sets d.slice_hbm); other instantiations keep them
 // in LDS and address them with ds instructions.
+// The slow path's commit leaves one slice change for sort.Slice at the next add(): position pos gained a pod.  When
+// pdqsort's handling of it is the stable move (sort_slice_after_change: no inversion, or n <= 12, or n >= 50 and pos
+// is not a pivot sample) the whole block applies it here, 512 positions per step, instead of wave 0 alone at its
+// next pop; otherwise the change stays for wave 0.  Every thread calls it (uniform control, barriers inside).
+__device__ inline void block_sort_move(FfdShared& S, SortSlice sl, int tid, int nthr) {
+    const int n = S.N, pos = S.dirty_pos;
+    if (S.dirty_kind != 1 || pos + 1 >= n) return;
+    const uint32_t kr = sl.key[pos], kv = kr & KEYMASK;
+    if ((sl.key[pos + 1] & KEYMASK) < kv) {
+        if (!(n <= 12 || (n >= 50 && !is_pivot_sample(n, pos)))) return;  // wave 0: pivot hint or pdqsort
+        const int lane = tid & 63, wave = tid >> 6;
+        // run end: the first position after pos whose key is >= the new key
+        int e = n;
+        for (int base = pos + 1, r = 0; base < n; base += nthr, r ^= 1) {
+            const int p = base + tid;
+            const uint64_t m = __ballot(p < n && (sl.key[p] & KEYMASK) >= kv);
+            if (lane == 0) S.bred[r][wave] = m ? base + wave * 64 + __ffsll((unsigned long long)m) - 1 : n;
+            __syncthreads();
+            for (int w = 0; w < KP_NWAVES; w++) e = S.bred[r][w] < e ? S.bred[r][w] : e;
+            if (e < n) break;
+        }
+        // [pos, e): element pos moves to e - 1, the rest shift left by one, 512 positions per step in order
+        const uint16_t fo = sl.ord[pos];
+        for (int base = pos; base < e - 1; base += nthr) {
+            const int i = base + tid;
+            uint16_t o = 0;
+            uint32_t k = 0;
+            if (i < e - 1) {
+                o = sl.ord[i + 1];
+                k = sl.key[i + 1];
+            }
+            __syncthreads();
+            if (i < e - 1) {
+                sl.ord[i] = o;
+                sl.key[i] = k;
+            }
+            __syncthreads();
+        }
+        if (tid == 0) {
+            sl.ord[e - 1] = fo;
+            sl.key[e - 1] = kr;
+            // Go sorts at the next add() that reaches the NodeClaims: if none does, the move is undone at the end
+            S.eager = 1;
+            S.eager_pos = pos;
+            S.eager_e = e;
+        }
+    }
+    __syncthreads();  // every thread has read dirty_kind
+    if (tid == 0) S.dirty_kind = 0;
+}
+
 template <bool RESV, bool TOPO, bool PREF, bool HBM = false>
 __device__ __forceinline__ void ffd_solve(KpDev d) {
     constexpr bool TOPO_ON = KP_TOPO_ON && TOPO;  // the solve has topology groups
@@ -624,6 +677,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
         S.qcount = P;
         S.done = 0;
         S.prev_shape = -1;
+        S.eager = 0;
         S.dirty_kind = 0;
         S.dirty_pos = 0;
         S.scan_start = 0;
@@ -693,6 +747,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
             int qhead = S.qhead, qcount = S.qcount;
             int seq = S.seq, prev_shape = S.prev_shape, dkind = S.dirty_kind, dpos = S.dirty_pos;
             int sstart = S.scan_start;  // every slice position < sstart has rejected the current shape
+            int eager = S.eager;        // a block_sort_move not yet reached by an add() that sorts
             int any_rej = S.any_rej;
             const int ep = S.epoch;
             if (PREF && d.relax_next && S.relaxed) {
@@ -906,6 +961,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 cqpop += t_b - t_a;
                 // sort.Slice(s.newNodeClaims, by len(Pods)) at the start of add(): at most one element changed since
                 // the last sort (dkind 1: position dpos gained a pod; dkind 2: a NodeClaim was appended)
+                eager = 0;  // this add() sorts: the eager move is now Go's too
                 if (dkind) {
                     int how = 0;
                     bool done_here = false;
@@ -1201,6 +1257,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 S.dirty_kind = dkind;
                 S.dirty_pos = dpos;
                 S.scan_start = sstart;
+                S.eager = eager;
                 S.any_rej = any_rej;
                 // reset here, behind the barrier that opens the slow path: the winner wave reads it at its commit,
                 // which no barrier separates from the end of the iteration
@@ -1334,6 +1391,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
             }
             __syncthreads();
             if (S.topo_quick) {
+                if (d.block_sort) block_sort_move(S, sl, tid, nthr);  // the quick accept's slice change
                 if (tid == 0) {
                     S.tp_n = 0;
                     S.topo_pod = 0;
@@ -1701,6 +1759,10 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 }
             }
         }
+        if (d.block_sort) {
+            __syncthreads();  // the commit's slice change (key, dirty_kind / dirty_pos) is visible
+            block_sort_move(S, sl, tid, nthr);
+        }
         if (tid == 0) {
             S.tp_n = 0;
             S.topo_pod = 0;
@@ -1708,6 +1770,32 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
         __syncthreads();
         if (tid == 0 && d.profile) S.st[ST_SLOW_WHY + 9] += __builtin_amdgcn_s_memtime() - c_ev;  // commit / templates
     }
+
+    if (S.eager && wave == 0) {  // no add() sorted after the last eager move: undo it (rotate [pos, e) right by one)
+        const int a = S.eager_pos, e = S.eager_e;
+        const uint32_t lk = skey[e - 1];
+        const uint16_t lo = sord[e - 1];
+        for (int top = e - 1; top > a; top -= 64) {  // descending chunks: each is read before it is overwritten
+            const int i = top - lane;
+            uint32_t k = 0;
+            uint16_t o = 0;
+            if (i > a) {
+                k = skey[i - 1];
+                o = sord[i - 1];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (i > a) {
+                skey[i] = k;
+                sord[i] = o;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
+        if (lane == 0) {
+            skey[a] = lk;
+            sord[a] = lo;
+        }
+    }
+    __syncthreads();
 
     // ---- outputs ----
     const int N = S.N;

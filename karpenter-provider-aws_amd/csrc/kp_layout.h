@@ -191,6 +191,7 @@ struct KpDev {
     int32_t team_eval;               // topology pods: one candidate at a time, evaluated by the whole block (eval_wave TEAM)
     int32_t noop_quick;              // fast loop: quick accept on a NodeClaim whose merge with the class changes nothing
     int32_t team_first;              // slow path: a first candidate that needs the full Add is evaluated by the whole block
+    int32_t block_sort;              // slow path: the commit's slice move by the whole block (block_sort_move)
     int32_t trace_pod;               // diagnostics (KPSIM_TRACE_POD): the slow path logs this pod's evaluations
     int32_t trace_max;               //   KPSIM_TRACE_CLASS: only pods with index <= KPSIM_TRACE_MAXPOD
     int32_t* trace;                  //   [1 + 6 * KP_TRACE_N]: count, then {round, nodeclaim (-1-j: template j), ok, flags, held lo/hi}
