@@ -1391,7 +1391,6 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
             }
             __syncthreads();
             if (S.topo_quick) {
-                if (d.block_sort) block_sort_move(S, sl, tid, nthr);  // the quick accept's slice change
                 if (tid == 0) {
                     S.tp_n = 0;
                     S.topo_pod = 0;
