@@ -38,7 +38,8 @@ def main():
     shutil.copy(stats, os.path.join(prof, "%s_kernel_stats.csv" % tag))
     recs = []
     # per kernel: profiles/pmc_<short>.json (bench.py reads hbm_bytes_per_launch as roofline.traffic)
-    for kernel, short in (("ffd_kernel", "ffd"), ("consolidate_kernel", "consolidate"), ("launch_kernel", "launch")):
+    for kernel, short in (("ffd_kernel", "ffd"), ("ffd_topo_kernel", "ffd_topo"), ("consolidate_kernel", "consolidate"),
+                          ("launch_kernel", "launch")):
         fetch_kb, nf = counter_per_launch(os.path.join(out, "fetch"), "FETCH_SIZE", kernel)
         write_kb, nw = counter_per_launch(os.path.join(out, "write"), "WRITE_SIZE", kernel)
         # rocprofv3 FETCH_SIZE / WRITE_SIZE are in KiB
@@ -46,7 +47,8 @@ def main():
         rec = {
             "kernel": kernel,
             "round": tag,
-            "command": "python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 (config2 50k pods; config4; config5 launch)",
+            "command": "python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 --no-reserved --no-consolidation-replace "
+                       "(config2 and config3 50k-pod Solves; config4; config5 launch)",
             "fetch_size_bytes_raw": fetch_b,
             "write_size_bytes": write_b,
             "hbm_bytes_per_launch": 2.0 * fetch_b + write_b,
@@ -57,6 +59,37 @@ def main():
             with open(os.path.join(prof, name), "w") as f:
                 json.dump(rec, f, indent=1)
         recs.append(rec)
+    # the Solve kernels' SQ issue / wait counters (per launch) and their KPSIM_PROFILE stage cycles
+    for kernel, short in (("ffd_kernel", "ffd"), ("ffd_topo_kernel", "ffd_topo")):
+        sq = {}
+        for pas in ("sq1", "sq2"):
+            d = os.path.join(out, pas)
+            if not os.path.isdir(d):
+                continue
+            names = set()
+            with open(find(d, "*counter_collection.csv")) as f:
+                for row in csv.DictReader(f):
+                    if kernel in row.get("Kernel_Name", ""):
+                        names.add(row["Counter_Name"])
+            for nm in sorted(names):
+                v, _ = counter_per_launch(d, nm, kernel)
+                sq[nm] = v
+        stages = {}
+        sj = os.path.join(out, "stages.json")
+        if os.path.exists(sj):
+            with open(sj) as f:
+                b = json.load(f)
+            leg = b if short == "ffd" else (b.get("topology") or {})
+            stages = {"kernel_ms": (leg.get("kernel_ms") or {}).get("ffd"), "ffd_counters": leg.get("ffd_counters"),
+                      "solve_stats": leg.get("solve_stats")}
+        if sq or stages:
+            rec = {"kernel": kernel, "round": tag, "sq_counters_per_launch": sq,
+                   "note": "SQ_* summed over the kernel's workgroup (one workgroup, 8 waves); cycles in shader clocks; "
+                           "stage cycles from KPSIM_PROFILE=1 s_memtime stamps (wave 0's fast loop, the block's slow "
+                           "path, templates) in a separate run",
+                   "kpsim_profile": stages}
+            with open(os.path.join(prof, "%s_pmc_%s_sq.json" % (tag, short)), "w") as f:
+                json.dump(rec, f, indent=1)
     with open(stats) as f:
         print(f.read())
     for rec in recs:
