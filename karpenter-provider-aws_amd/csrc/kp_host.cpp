@@ -2355,6 +2355,10 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         d.g_tmpl = c->d_g_tmpl.p;
     }
     if (!kp_ffd_plan_lds(d, KP_LDS_BYTES)) return fail(ctx, KP_E_UNSUPPORTED, "FFD kernel LDS plan exceeds 160 KB");
+    if (getenv("KPSIM_PROFILE"))
+        fprintf(stderr, "[kpsim] FFD LDS plan: fixed block %zu B, quick rows %d (axes %d), NodeClaim slots %d, allocatable %s, "
+                "%d B of %d\n", kp_ffd_shared_bytes(), d.lds_nq, d.lds_A, d.lds_ncmax, d.alloc_global ? "HBM" : "LDS",
+                d.lds_bytes, KP_LDS_BYTES);
     c->P = P;
     c->C = C;
     c->NT = NT;

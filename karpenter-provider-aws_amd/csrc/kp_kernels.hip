@@ -161,7 +161,6 @@ __global__ __launch_bounds__(64) void template_init_kernel(KpDev d) {
 // (kp_ffd_plan_lds): slice keys/order and last absorbed class per NodeClaim, the staged allocatable / offering /
 // multi-valued label tables, and the quick-accept headroom table hr[lds_A][lds_nq].
 struct FfdShared {
-    int64_t qw_req[64][KP_MAX_R];  // requests of the queue window's pods
     int fastp[2][KP_NWAVES];
     WaveScratch ws[KP_NWAVES];
     TeamBuf team[2];               // topology pods: the block evaluates one candidate at a time (eval_wave TEAM)
@@ -607,6 +606,12 @@ __device__ inline void block_sort_move(FfdShared& S, SortSlice sl, int tid, int 
     if (tid == 0) S.dirty_kind = 0;
 }
 
+#ifndef KP_TEAM_FIRST_RESV
+#define KP_TEAM_FIRST_RESV 0  // 0: no block-evaluated first candidate in the RESV instantiations (its registers cost config 5 15 %)
+#endif
+#ifndef KP_NOOP_RESV
+#define KP_NOOP_RESV 1        // A/B builds: 0 compiles the no-op merge quick accept out of the RESV instantiations
+#endif
 template <bool RESV, bool TOPO, bool PREF, bool HBM = false>
 __device__ __forceinline__ void ffd_solve(KpDev d) {
     constexpr bool TOPO_ON = KP_TOPO_ON && TOPO;  // the solve has topology groups
@@ -620,6 +625,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
     uint64_t* const sAvail = reinterpret_cast<uint64_t*>(smem + d.off_avail);
     uint16_t* const sMulti = reinterpret_cast<uint16_t*>(smem + d.off_multi);
     int32_t* const shr = reinterpret_cast<int32_t*>(smem + d.off_hr);       // [A][NQ] witness headroom
+    int64_t* const qw_req = reinterpret_cast<int64_t*>(smem + d.off_qw);    // [64][R] requests of the queue window's pods
     // reserved offerings and the ReservationManager's capacities (RESV instantiation: the catalog has reserved offerings)
     ResvTab* const sRo = RESV ? reinterpret_cast<ResvTab*>(smem + d.off_ro) : nullptr;
     int32_t* const sRcap = RESV ? reinterpret_cast<int32_t*>(smem + d.off_ro + sizeof(ResvTab)) : nullptr;
@@ -865,7 +871,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                         vshape = d.pod_shape[vp];
                         vlast = (PREF && d.last_ep && d.last_ep[vp] != ep) ? -1 : d.last_len[vp];
                         vtol = (d.tol[vc] & ~(1ull << 63)) | ((d.cls_flags[vc] & 4u) ? (1ull << 63) : 0ull);
-                        for (int r = 0; r < R; r++) S.qw_req[lane][r] = d.pod_req[(size_t)vp * R + r];
+                        for (int r = 0; r < R; r++) qw_req[lane * R + r] = d.pod_req[(size_t)vp * R + r];
 #pragma unroll
                         for (int ai = 0; ai < KP_LDS_AXES; ai++) {
                             const int64_t pr = ai < A ? d.pod_req[(size_t)vp * R + d.active_axes[ai]] : 0;
@@ -904,7 +910,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                     tl = rl64(vtol, off);
 #pragma unroll
                     for (int ai = 0; ai < KP_LDS_AXES; ai++) pq[ai] = rl32(vq[ai], off);
-                    if (lane < R) S.shape_req[lane] = S.qw_req[off][lane];
+                    if (lane < R) S.shape_req[lane] = qw_req[off * R + lane];
                     wa = wb >= 0 && wb + lane < N && absorbed(wm);
                     sstart = 0;
                     prev_shape = shape;
@@ -1044,7 +1050,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                     // recording, or the evaluation of candidates); counts change with every placement
                     win_flush();
                     wb = -1;
-                    if (lane < R) S.pod_req[lane] = S.qw_req[off][lane];
+                    if (lane < R) S.pod_req[lane] = qw_req[off * R + lane];
                     if (lane == 0) {
                         S.cur_pod = p;
                         S.cls_fill = S.CC.cls != c;
@@ -1077,7 +1083,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                     for (int ai = 0; ai < KP_LDS_AXES; ai++)
                         if (ai < A) wfit &= pq[ai] <= wh[ai];
                     uint64_t okm = ballot(wa && wfit);
-                    if (!((okm >> fl) & 1ull) && ((ballot(wfit) >> fl) & 1ull) && d.noop_quick) {
+                    if ((KP_NOOP_RESV | !RESV) && !((okm >> fl) & 1ull) && ((ballot(wfit) >> fl) & 1ull) && d.noop_quick) {
                         // the NodeClaim at f has not absorbed the class but its witness fits: the Add is the quick accept
                         // when the class's requirement merge changes nothing (and the class tolerates its template)
                         const int nc = rl32((int)wo, fl), tm = (int)((uint32_t)rl32((int)wm, fl) >> 16);
@@ -1236,7 +1242,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 }
                 win_flush();
                 wb = -1;
-                if (lane < R) S.pod_req[lane] = S.qw_req[off][lane];
+                if (lane < R) S.pod_req[lane] = qw_req[off * R + lane];
                 if (lane == 0) {
                     S.cur_pod = p;
                     S.cls_fill = S.CC.cls != c;  // decided before the barrier: fill_class_cache rewrites CC.cls
@@ -1469,6 +1475,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
         // candidate first, evaluated by the whole block (it takes most such pods); the others then in parallel as below
         int first = 0;  // round-0 candidates already evaluated
         bool team_won = false;
+        if (KP_TEAM_FIRST_RESV | !RESV)
         if (!team && d.team_first && S.n_cand[0] > 0) {
             const int nc = sord[S.cand_pos[0][0]];
             const int tm = d.nc_tmpl[nc];
@@ -2034,6 +2041,8 @@ bool kp_ffd_plan_lds(KpDev& d, int max_bytes) {
 static bool kp_ffd_plan_lds_tables(KpDev& d, int max_bytes) {
     auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
     size_t off = al(sizeof(FfdShared));
+    d.off_qw = (int)off;  // the queue window's pod requests, [64][R]
+    off = al(off + 64 * 8 * (size_t)(d.R > 0 ? d.R : 1));
     int ncmax = d.NCcap < KP_MAX_NC ? d.NCcap : KP_MAX_NC;
     d.slice_hbm = 0;
     if (d.alloc_global) {

@@ -249,7 +249,7 @@ struct KpDev {
     int32_t lds_nq;                  // NodeClaims with a quick-accept headroom row (ids < lds_nq)
     int32_t alloc_global;            // large slice plans: allocatable read from alloc_act in HBM, not staged in LDS
     const int64_t* alloc_act;        // [lds_nstage][lds_tpad] allocatable of the staged axes (alloc_global)
-    int32_t off_key, off_ord, off_last, off_tmpl, off_alloc, off_avail, off_multi, off_ro, off_tsnap, off_hr;
+    int32_t off_key, off_ord, off_last, off_tmpl, off_alloc, off_avail, off_multi, off_ro, off_tsnap, off_hr, off_qw;
     int32_t lds_bytes;
     int32_t qshift[KP_LDS_AXES];     // headroom scale per quick axis: value >> qshift fits 30 bits
 
