@@ -199,6 +199,9 @@ __device__ inline uint64_t commit_held(int32_t* rcap, uint64_t old, uint64_t nw,
 #define AXL(ai) _Pragma("unroll") for (int ai = 0; ai < (NA > 0 ? NA : KP_LDS_AXES); ai++) if (NA > 0 || ai < A)
 template <bool FULL, bool RESV = false, bool TOPO = false, int NA = 0>
 __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
+    // FULL variant after the fast one: nothing handed over, nothing to do (exit before the prologue's register spills
+    // to scratch, which cost every worker of an idle launch its own scratch writes)
+    if (FULL && k.no_fast != 1 && ld32(&k.next_probe[2]) == 0) return;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     ConsShared& S = *reinterpret_cast<ConsShared*>(smem);
     ReqHdr* nch = reinterpret_cast<ReqHdr*>(smem + k.off_hdr);
