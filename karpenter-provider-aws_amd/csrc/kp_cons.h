@@ -17,6 +17,7 @@ enum { CS_POPS = 0, CS_EX_NODES, CS_NC_EVALS, CS_TMPL_EVALS, CS_PROBES, CS_BITMA
 #define KP_CONS_XTC 1024  // pod classes whose XT column of the cached node chunk is kept in LDS
 #define KP_CONS_STORE 8   // node chunks the fast probe variant keeps in its LDS headroom store
 #define KP_CONS_PP 16     // KPSIM_PROFILE: per-probe counters (kp_consolidate's diagnostics)
+#define KP_CONS_FULL_WORKERS 1024  // FULL-variant workers: one per SIMD of 256 CUs (1 wave per SIMD at its VGPR count)
 
 struct KpCons {
     int32_t n_probes;           // probes of this call (out[0 .. n_probes))

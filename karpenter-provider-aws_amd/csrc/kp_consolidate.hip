@@ -1454,8 +1454,9 @@ hipError_t kp_launch_consolidate(const KpDev& d, const KpCons& k, int n_workers,
     if (k.G > 0) {
         if (k.no_fast != 1) hipLaunchKernelGGL((consolidate_kernel<false, false, true>), dim3(n_workers), dim3(64), lds, s, d, k);
         if (k.no_fast != 2) {
-            if (d.ro) hipLaunchKernelGGL((consolidate_kernel<true, true, true>), dim3(n_workers), dim3(64), lds, s, d, k);
-            else hipLaunchKernelGGL((consolidate_kernel<true, false, true>), dim3(n_workers), dim3(64), lds, s, d, k);
+            const dim3 gf(n_workers < KP_CONS_FULL_WORKERS ? n_workers : KP_CONS_FULL_WORKERS);  // as below
+            if (d.ro) hipLaunchKernelGGL((consolidate_kernel<true, true, true>), gf, dim3(64), lds, s, d, k);
+            else hipLaunchKernelGGL((consolidate_kernel<true, false, true>), gf, dim3(64), lds, s, d, k);
         }
         return hipGetLastError();
     }
@@ -1472,8 +1473,11 @@ hipError_t kp_launch_consolidate(const KpDev& d, const KpCons& k, int n_workers,
         }
     }
     if (k.no_fast != 2) {
-        if (d.ro) hipLaunchKernelGGL((consolidate_kernel<true, true>), dim3(n_workers), dim3(64), lds, s, d, k);
-        else hipLaunchKernelGGL(consolidate_kernel<true>, dim3(n_workers), dim3(64), lds, s, d, k);
+        // the FULL variant runs one wave per SIMD (its registers): more workers than SIMDs only queue, and each worker,
+        // even an idle one, first copies the kernel arguments to its scratch
+        const dim3 gf(n_workers < KP_CONS_FULL_WORKERS ? n_workers : KP_CONS_FULL_WORKERS);
+        if (d.ro) hipLaunchKernelGGL((consolidate_kernel<true, true>), gf, dim3(64), lds, s, d, k);
+        else hipLaunchKernelGGL(consolidate_kernel<true>, gf, dim3(64), lds, s, d, k);
     }
     return hipGetLastError();
 }
