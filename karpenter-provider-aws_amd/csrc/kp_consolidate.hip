@@ -198,10 +198,7 @@ __device__ inline uint64_t commit_held(int32_t* rcap, uint64_t old, uint64_t nw,
 // and prefix sums unroll without runtime guards (0: read from d.n_active).
 #define AXL(ai) _Pragma("unroll") for (int ai = 0; ai < (NA > 0 ? NA : KP_LDS_AXES); ai++) if (NA > 0 || ai < A)
 template <bool FULL, bool RESV = false, bool TOPO = false, int NA = 0>
-__global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
-    // FULL variant after the fast one: nothing handed over, nothing to do (exit before the prologue's register spills
-    // to scratch, which cost every worker of an idle launch its own scratch writes)
-    if (FULL && k.no_fast != 1 && ld32(&k.next_probe[2]) == 0) return;
+__device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     ConsShared& S = *reinterpret_cast<ConsShared*>(smem);
     ReqHdr* nch = reinterpret_cast<ReqHdr*>(smem + k.off_hdr);
@@ -1355,6 +1352,19 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
     if (lane < CS_COUNT && S.st[lane]) atomicAdd((unsigned long long*)&k.stats[lane], (unsigned long long)S.st[lane]);
 }
 
+// The fast variant takes its tables by value (kernel arguments).  The FULL variant takes them by pointer to device
+// copies: its body indexes them dynamically, so the compiler copies them to scratch, and with pointers that copy comes
+// after the check that lets an idle launch (the fast variant handed nothing over) exit at once.
+template <bool FULL, bool RESV = false, bool TOPO = false, int NA = 0>
+__global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
+    consolidate_body<FULL, RESV, TOPO, NA>(d, k);
+}
+template <bool RESV, bool TOPO>
+__global__ __launch_bounds__(64) void consolidate_full_kernel(const KpDev* __restrict__ dp, const KpCons* __restrict__ kp) {
+    if (kp->no_fast != 1 && ld32(&kp->next_probe[2]) == 0) return;
+    consolidate_body<true, RESV, TOPO, 0>(*dp, *kp);
+}
+
 // cmax0[w][ai]: the largest headroom on active axis ai over the nodes of chunk w (one wave per chunk; lanes past E and
 // axes past n_active hold INT64_MIN)
 __global__ __launch_bounds__(64) void chunk_max_kernel(const int64_t* __restrict__ ex_head, int E, int A,
@@ -1432,15 +1442,15 @@ bool kp_cons_plan_lds(const KpDev& d, KpCons& k, int max_bytes) {
 
 // Per-device kernel attributes, set by kp_ctx_create with the ctx's device current (see kp_ffd_set_attributes).
 hipError_t kp_cons_set_attributes() {
-    const void* fns[] = {(const void*)consolidate_kernel<false>, (const void*)consolidate_kernel<true>,
+    const void* fns[] = {(const void*)consolidate_kernel<false>, (const void*)consolidate_full_kernel<false, false>,
                          (const void*)consolidate_kernel<false, false, false, 1>,
                          (const void*)consolidate_kernel<false, false, false, 2>,
                          (const void*)consolidate_kernel<false, false, false, 3>,
                          (const void*)consolidate_kernel<false, false, false, 4>,
                          (const void*)consolidate_kernel<false, false, false, 5>,
                          (const void*)consolidate_kernel<false, false, false, 6>,
-                         (const void*)consolidate_kernel<true, true>, (const void*)consolidate_kernel<false, false, true>,
-                         (const void*)consolidate_kernel<true, false, true>, (const void*)consolidate_kernel<true, true, true>};
+                         (const void*)consolidate_full_kernel<true, false>, (const void*)consolidate_kernel<false, false, true>,
+                         (const void*)consolidate_full_kernel<false, true>, (const void*)consolidate_full_kernel<true, true>};
     for (const void* f : fns) {
         const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, KP_LDS_BYTES);
         if (e != hipSuccess) return e;
@@ -1448,15 +1458,16 @@ hipError_t kp_cons_set_attributes() {
     return hipSuccess;
 }
 
-hipError_t kp_launch_consolidate(const KpDev& d, const KpCons& k, int n_workers, hipStream_t s) {
+hipError_t kp_launch_consolidate(const KpDev& d, const KpCons& k, int n_workers, hipStream_t s, KpDev* d_dev,
+                                 KpCons* d_k) {
     if (n_workers <= 0 || k.n_probes <= 0) return hipSuccess;
     const size_t lds = (size_t)k.lds_bytes;
     if (k.G > 0) {
         if (k.no_fast != 1) hipLaunchKernelGGL((consolidate_kernel<false, false, true>), dim3(n_workers), dim3(64), lds, s, d, k);
         if (k.no_fast != 2) {
             const dim3 gf(n_workers < KP_CONS_FULL_WORKERS ? n_workers : KP_CONS_FULL_WORKERS);  // as below
-            if (d.ro) hipLaunchKernelGGL((consolidate_kernel<true, true, true>), gf, dim3(64), lds, s, d, k);
-            else hipLaunchKernelGGL((consolidate_kernel<true, false, true>), gf, dim3(64), lds, s, d, k);
+            if (d.ro) hipLaunchKernelGGL((consolidate_full_kernel<true, true>), gf, dim3(64), lds, s, d_dev, d_k);
+            else hipLaunchKernelGGL((consolidate_full_kernel<false, true>), gf, dim3(64), lds, s, d_dev, d_k);
         }
         return hipGetLastError();
     }
@@ -1476,8 +1487,8 @@ hipError_t kp_launch_consolidate(const KpDev& d, const KpCons& k, int n_workers,
         // the FULL variant runs one wave per SIMD (its registers): more workers than SIMDs only queue, and each worker,
         // even an idle one, first copies the kernel arguments to its scratch
         const dim3 gf(n_workers < KP_CONS_FULL_WORKERS ? n_workers : KP_CONS_FULL_WORKERS);
-        if (d.ro) hipLaunchKernelGGL((consolidate_kernel<true, true>), gf, dim3(64), lds, s, d, k);
-        else hipLaunchKernelGGL(consolidate_kernel<true>, gf, dim3(64), lds, s, d, k);
+        if (d.ro) hipLaunchKernelGGL((consolidate_full_kernel<true, false>), gf, dim3(64), lds, s, d_dev, d_k);
+        else hipLaunchKernelGGL((consolidate_full_kernel<false, false>), gf, dim3(64), lds, s, d_dev, d_k);
     }
     return hipGetLastError();
 }

@@ -40,7 +40,8 @@ hipError_t kp_cons_set_attributes();
 hipError_t kp_launch_finalize(const KpDev& d, int n_nodeclaims, hipStream_t s);
 bool kp_cons_plan_lds(const KpDev& d, KpCons& k, int max_bytes);
 hipError_t kp_launch_select_kernel(const KpLaunch& g, hipStream_t s);
-hipError_t kp_launch_consolidate(const KpDev& d, const KpCons& k, int n_workers, hipStream_t s);
+hipError_t kp_launch_consolidate(const KpDev& d, const KpCons& k, int n_workers, hipStream_t s, KpDev* d_dev,
+                                 KpCons* d_k);
 hipError_t kp_launch_cons_chunk_max(const KpDev& d, int64_t* cmax0, hipStream_t s);
 hipError_t kp_launch_multi_union(const KpCons& k, int nu, uint64_t* ubits, int32_t* rcand, int2* ulist, int32_t* ulen,
                                  const int32_t* queue0, hipStream_t s);
@@ -550,6 +551,8 @@ struct kp_ctx {
     DBuf<uint16_t> d_g_ord, d_g_last;
     DBuf<uint8_t> d_g_tmpl;
     DBuf<KpDev> d_self;  // device copy of dev for out-of-line kernel helpers (KpDev::self)
+    DBuf<KpDev> d_cons_dev;  // device copies of a consolidation launch's tables for the FULL variant (by pointer)
+    DBuf<KpCons> d_cons_k;
     std::vector<uint64_t> h_tknown_dg;       // [G] buildDomainGroups' domains (before any pod is counted)
     DBuf<int32_t> d_dec_soff, d_dec_moff, d_dec_g, d_dec_v, d_pt_cnt, d_pt_hd;
     DBuf<uint64_t> d_pt_known, d_pt_dgk;
@@ -2985,7 +2988,11 @@ static kp_status cons_run(kp_ctx* ctx, int m0, int m1, int s0, int s1, kp_probe_
         k.rec_words = c->d_rec_words.p;
         k.no_fast = 1;
     }
-    HIPCHK(kp_launch_consolidate(d, k, workers, s));
+    HIPCHK(c->d_cons_dev.ensure(1));
+    HIPCHK(c->d_cons_k.ensure(1));
+    HIPCHK(hipMemcpyAsync(c->d_cons_dev.p, &d, sizeof(KpDev), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->d_cons_k.p, &k, sizeof(KpCons), hipMemcpyHostToDevice, s));
+    HIPCHK(kp_launch_consolidate(d, k, workers, s, c->d_cons_dev.p, c->d_cons_k.p));
     HIPCHK(hipEventRecord(c->ev[2], s));
     if (nmp)
         HIPCHK(hipMemcpyAsync(out_multi, c->d_probe_out.p, (size_t)nmp * sizeof(kp_probe_result), hipMemcpyDeviceToHost, s));

@@ -123,7 +123,7 @@ bool kp_cons_plan_lds(const KpDev&, KpCons& k, int) {
     return true;
 }
 hipError_t kp_launch_select_kernel(const KpLaunch&, hipStream_t) { return hipSuccess; }
-hipError_t kp_launch_consolidate(const KpDev&, const KpCons& k, int, hipStream_t) {
+hipError_t kp_launch_consolidate(const KpDev&, const KpCons& k, int, hipStream_t, KpDev*, KpCons*) {
     for (int i = 0; i < k.n_probes; i++) {
         const int g = k.probe0 + i;
         kp_probe_result o{};
