@@ -946,7 +946,14 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
                 st_nc++;
                 // the NodeClaim has absorbed the class (no topology, no reservations): the merge is idempotent and the
                 // label / offering filters already hold for its options, so the Add is Fits (+ minValues) only
-                const bool absorbed = c == nc_lc && !(TOPO && (cflags & CF_TOPO)) && !(RESV && d.resv_on);
+                bool absorbed = c == nc_lc && !(TOPO && (cflags & CF_TOPO)) && !(RESV && d.resv_on);
+                // another class whose requirement merge changes nothing (and that tolerates the NodeClaim's template)
+                // is absorbed the same way
+                if (!absorbed && !(TOPO && (cflags & CF_TOPO)) && !(RESV && d.resv_on) && ((d.tol[c] >> nc_tmpl) & 1ull) &&
+                    merge_noop_at(d, S.ws, nch, ncw, c, lane)) {
+                    absorbed = true;
+                    nc_lc = c;  // its requirements are a subset of the class's
+                }
                 if (absorbed) {
                     if (eval_fits_only<true>(d, Ev, a, S.ws, lane)) {
                         if (lane < TW) nc_opts = S.ws.opts[lane];

@@ -1001,6 +1001,37 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
     return true;
 }
 
+// The requirement merge of NodeClaim.Add(pod of class c) on the NodeClaim digest (Ahdr [K], Aw [DW]) is a no-op: for
+// every key the class constrains (keys carried only for topology narrowing aside), the NodeClaim has the key and
+// Requirement.Intersection leaves it as it is (header and values), and the pair passes Compatible.  Then the Add keeps
+// the NodeClaim's requirements, so its options stay compatible and its offerings the same (one wave; ws.words is
+// scratch).
+__device__ inline bool merge_noop_at(const KpDev& d, WaveScratch& ws, const ReqHdr* Ahdr, const uint64_t* Aw, int c,
+                                     int lane) {
+    const int k0 = d.cls_koff[c], nck = d.cls_koff[c + 1] - k0;
+    bool ok = true;
+    if (lane < nck && !(d.cls_kneutral && d.cls_kneutral[k0 + lane])) {
+        const int k = d.cls_keys[k0 + lane], n = d.nw[k];
+        const ReqHdr A = Ahdr[k];
+        const uint64_t* aw = Aw + d.woff[k];
+        if (!(A.flags & RF_DEF)) {
+            ok = false;  // the merge adds the key
+        } else {
+            const ReqHdr B = d.cls_hdr[(size_t)c * d.K + k];
+            const uint64_t* bw = d.cls_words + (size_t)c * d.DW + d.woff[k];
+            uint64_t* ow = ws.words + d.cls_wsoff[k0 + lane];
+            ReqHdr O;
+            const int cnt = req_intersect(d, k, A, aw, B, bw, O, ow);
+            ok = O.flags == A.flags && O.gt == A.gt && O.lt == A.lt && O.minv == A.minv;
+            for (int i = 0; i < n && ok; i++) ok = ow[i] == aw[i];
+            if (!(O.flags & RF_CMP) && cnt == 0 &&
+                !(op_notin_or_dne(req_op(B.flags, popc_words(bw, n))) && op_notin_or_dne(req_op(A.flags, popc_words(aw, n)))))
+                ok = false;
+        }
+    }
+    return ballot(!ok) == 0;
+}
+
 // Write the merged class keys of a successful evaluation into NodeClaim slot n.
 __device__ __forceinline__ void commit_reqs(const KpDev& d, const ClassCache& CC, const WaveScratch& ws, int n, int lane) {
     if (lane < CC.nck) {

@@ -352,28 +352,7 @@ __device__ inline bool topo_pinned(const KpDev& d, const FfdShared& S, int nc) {
 // stay compatible and its offerings the same: the topology quick accept applies as for a NodeClaim that absorbed the
 // class (wave 0; ws.words is free scratch here).
 __device__ inline bool merge_noop(const KpDev& d, WaveScratch& ws, int nc, int c, int lane) {
-    const int k0 = d.cls_koff[c], nck = d.cls_koff[c + 1] - k0;
-    bool ok = true;
-    if (lane < nck && !(d.cls_kneutral && d.cls_kneutral[k0 + lane])) {
-        const int k = d.cls_keys[k0 + lane], n = d.nw[k];
-        const ReqHdr A = d.nc_hdr[(size_t)nc * d.K + k];
-        const uint64_t* aw = d.nc_words + (size_t)nc * d.DW + d.woff[k];
-        if (!(A.flags & RF_DEF)) {
-            ok = false;  // the merge adds the key
-        } else {
-            const ReqHdr B = d.cls_hdr[(size_t)c * d.K + k];
-            const uint64_t* bw = d.cls_words + (size_t)c * d.DW + d.woff[k];
-            uint64_t* ow = ws.words + d.cls_wsoff[k0 + lane];
-            ReqHdr O;
-            const int cnt = req_intersect(d, k, A, aw, B, bw, O, ow);
-            ok = O.flags == A.flags && O.gt == A.gt && O.lt == A.lt && O.minv == A.minv;
-            for (int i = 0; i < n && ok; i++) ok = ow[i] == aw[i];
-            if (!(O.flags & RF_CMP) && cnt == 0 &&
-                !(op_notin_or_dne(req_op(B.flags, popc_words(bw, n))) && op_notin_or_dne(req_op(A.flags, popc_words(aw, n)))))
-                ok = false;
-        }
-    }
-    return ballot(!ok) == 0;
+    return merge_noop_at(d, ws, d.nc_hdr + (size_t)nc * d.K, d.nc_words + (size_t)nc * d.DW, c, lane);
 }
 
 // Topology.Record of a quick accept onto NodeClaim nc (template tmpl): its requirements are unchanged by the Add, so
