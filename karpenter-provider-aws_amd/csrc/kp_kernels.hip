@@ -588,6 +588,9 @@ __device__ inline void block_sort_move(FfdShared& S, SortSlice sl, int tid, int 
 #ifndef KP_TEAM_FIRST_RESV
 #define KP_TEAM_FIRST_RESV 0  // 0: no block-evaluated first candidate in the RESV instantiations (its registers cost config 5 15 %)
 #endif
+#ifndef KP_TEAM_FIRST_TOPO
+#define KP_TEAM_FIRST_TOPO 1  // A/B builds: 0 compiles the block-evaluated first candidate out of the TOPO instantiations
+#endif
 #ifndef KP_NOOP_RESV
 #define KP_NOOP_RESV 1        // A/B builds: 0 compiles the no-op merge quick accept out of the RESV instantiations
 #endif
@@ -1454,7 +1457,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
         // candidate first, evaluated by the whole block (it takes most such pods); the others then in parallel as below
         int first = 0;  // round-0 candidates already evaluated
         bool team_won = false;
-        if (KP_TEAM_FIRST_RESV | !RESV)
+        if ((KP_TEAM_FIRST_RESV | !RESV) && (KP_TEAM_FIRST_TOPO | !TOPO))
         if (!team && d.team_first && S.n_cand[0] > 0) {
             const int nc = sord[S.cand_pos[0][0]];
             const int tm = d.nc_tmpl[nc];
