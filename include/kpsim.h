@@ -423,10 +423,12 @@ kp_status kp_consolidate_execute(kp_ctx* ctx, int32_t mode, int32_t probe_begin,
  * computeConsolidation is not a no-op; MultiNodeConsolidation.firstNConsolidationOption, multinodeconsolidation.go: the
  * binary search over the prefix length, a prefix kept when DELETE or a REPLACE with options left after
  * filterOutSameInstanceType) and their Command (consolidation.go computeConsolidation: delete set + replacement
- * NodeClaim).  One call evaluates every probe the loop could visit (one device pass, sharded over a multi-device ctx),
- * replays the loop over the results on the host, then re-runs the chosen probe on the primary device to read back its
- * replacement NodeClaim — the NodeClaim CloudProvider.Create (pkg/cloudprovider/cloudprovider.go:90-137) is later called
- * with:
+ * NodeClaim).  One call evaluates every probe the loop could visit (one device pass, sharded over a multi-device ctx)
+ * unless the last kp_consolidate_execute of the prepared pass already evaluated them all (a full pass of `mode`, or of
+ * KP_CONSOLIDATE_BOTH): then it replays that pass.  It replays the loop over the rows on the host, then re-runs the
+ * chosen probe on the primary device to read back its replacement NodeClaim (kept with the prepared pass: a repeated
+ * call, e.g. after KP_E_BUFFER, copies it) — the NodeClaim CloudProvider.Create (pkg/cloudprovider/cloudprovider.go:90-137)
+ * is later called with:
  *   type_ids      its InstanceTypeOptions after RemoveInstanceTypeOptionsByPriceAndMinValues (or the spot-to-spot cut
  *                 to max(15, minNeeded) cheapest) and, for multi-node, filterOutSameInstanceType; OrderByPrice order;
  *   requirements  its Requirements (FinalizeScheduling's reservation-id In [held IDs] included; capacity-type narrowed to
@@ -455,12 +457,19 @@ typedef struct kp_consolidation_command {
 
 /* KP_E_BUFFER (with n_type_ids / requirements_needed set) when a replacement does not fit the caller's buffers. */
 kp_status kp_consolidate_command(kp_ctx* ctx, int32_t mode, kp_consolidation_command* out);
+/* The command of one given probe of a prepared pass (mode KP_CONSOLIDATE_SINGLE or _MULTI, probe index in that mode's
+ * list): its row and, for a REPLACE, the replacement NodeClaim as kp_consolidate_command returns it.  For callers that
+ * replay the decision loops themselves over probe rows gathered from several processes (one GPU per process,
+ * kpsim.consolidation.compute_command with a torch.distributed group). */
+kp_status kp_consolidate_replacement(kp_ctx* ctx, int32_t mode, int32_t probe, kp_consolidation_command* out);
 
 /* Diagnostics of the last kp_consolidate: ms[3] = {device prep (queue sort, masks), probe kernel, whole call};
- * counters[17] = {pods popped, existing-node slots examined, NodeClaim evaluations, template evaluations, probes,
+ * counters[18] = {pods popped, existing-node slots examined, NodeClaim evaluations, template evaluations, probes,
  * queue-bitmap words scanned, existing-node placements, new NodeClaims, node chunks loaded, cached-chunk hits, then
  * with KPSIM_PROFILE set: s_memtime cycles of queue build, existing-node scans, NodeClaim/template evaluation,
- * decision, whole probe (summed over probes); then chunks the headroom summary skipped, preference relaxations}. */
+ * decision, whole probe (summed over probes); then chunks the headroom summary skipped, preference relaxations,
+ * probes run with per-probe node requirement copies (pods whose NotIn / DoesNotExist requirements change nodes)};
+ * counters[18..19] = {probe passes launched, replacement read-backs run} since the last kp_consolidate_prepare. */
 kp_status kp_consolidate_stats(kp_ctx* ctx, double* ms, int64_t* counters, int32_t n_counters);
 
 /*

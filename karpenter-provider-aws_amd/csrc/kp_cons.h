@@ -12,7 +12,7 @@
 
 enum { CS_POPS = 0, CS_EX_NODES, CS_NC_EVALS, CS_TMPL_EVALS, CS_PROBES, CS_BITMAP_WORDS, CS_PLACED_EXISTING,
        CS_NEW_NC, CS_CHUNK_LOADS, CS_CACHE_HITS, CS_CYC_BUILD, CS_CYC_SCAN, CS_CYC_NODECLAIM, CS_CYC_DECIDE,
-       CS_CYC_TOTAL, CS_CHUNK_SKIPS, CS_RELAXED, CS_COUNT = 17 };
+       CS_CYC_TOTAL, CS_CHUNK_SKIPS, CS_RELAXED, CS_MUT, CS_COUNT = 18 };
 
 #define KP_CONS_XTC 1024  // pod classes whose XT column of the cached node chunk is kept in LDS
 #define KP_CONS_STORE 8   // node chunks the fast probe variant keeps in its LDS headroom store
@@ -95,8 +95,20 @@ struct KpCons {
     int32_t profile;            // s_memtime stage cycles (KPSIM_PROFILE)
     int64_t* prof_probe;        // KPSIM_PROFILE: [n_probes][4] cycles of build, existing-node placement, total; pods
     int32_t no_fast;            // diagnostics: every probe on the FULL variant (KPSIM_CONS_NOFAST)
+    // MUT (ExistingNode.Add's requirement merge changes nodes, kp_solve_prepare's mutators): a probe that reschedules a
+    // mutator's pod (mut_s[candidate] / mut_m[prefix]) runs on the FULL variant's MUT instantiation, serially over its
+    // queue; a node whose requirements its merges change gets a copy of its digest (slot ov_slot[j], valid while the
+    // probe's LDS bit mutn[j] is set), and class × node compatibility of such a node is evaluated against the copy
+    int32_t mut;                // some probe of the pass is a MUT probe
+    const int32_t* mut_s;       // [n_cand]
+    const int32_t* mut_m;       // [multi-node probes]
+    int32_t ov_cap;             // digest copies per worker
+    int32_t* ov_slot;           // [FULL workers][E]
+    ReqHdr* ov_hdr;             // [FULL workers][ov_cap][K]
+    uint64_t* ov_words;         // [FULL workers][ov_cap][DW]
     // dynamic LDS plan (kp_cons_plan_lds)
     int32_t n_store;            // chunks in the fast variant's LDS headroom store (kp_cons_plan_lds)
     int32_t off_hdr, off_words, off_rem, off_excl, off_mod, off_init, off_xtc, off_touch, off_hmod, off_cmax, off_hs, off_hpos;
+    int32_t off_mutn;
     int32_t lds_bytes;
 };

@@ -196,8 +196,10 @@ __device__ inline uint64_t commit_held(int32_t* rcap, uint64_t old, uint64_t nw,
 // placement of a counted class is recorded.
 // NA (fast variant only): the number of active axes, fixed at compile time so that the window intake's per-axis tests
 // and prefix sums unroll without runtime guards (0: read from d.n_active).
+// MUT (FULL only): the pass has probes that reschedule a mutator's pod (KpCons::mut): such a probe runs serially over its
+// queue and applies ExistingNode.Add's requirement merge to its own copies of the nodes it changes (see KpCons).
 #define AXL(ai) _Pragma("unroll") for (int ai = 0; ai < (NA > 0 ? NA : KP_LDS_AXES); ai++) if (NA > 0 || ai < A)
-template <bool FULL, bool RESV = false, bool TOPO = false, int NA = 0>
+template <bool FULL, bool RESV = false, bool TOPO = false, int NA = 0, bool MUT = false>
 __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     ConsShared& S = *reinterpret_cast<ConsShared*>(smem);
@@ -209,6 +211,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
     uint64_t* initb = reinterpret_cast<uint64_t*>(smem + k.off_init);
     uint64_t* xtc = reinterpret_cast<uint64_t*>(smem + k.off_xtc);  // XT column of the cached chunk, by class
     int64_t* cmax = reinterpret_cast<int64_t*>(smem + k.off_cmax);  // [EW][KP_LDS_AXES] chunk headroom upper bounds
+    uint64_t* mutn = reinterpret_cast<uint64_t*>(smem + k.off_mutn);  // MUT: nodes whose requirements the probe changed
     const int lane = threadIdx.x;
     ProbeTopo P{};
     if (TOPO) {
@@ -235,6 +238,9 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
     int32_t* rshape = k.relax ? k.ring_shape + (size_t)wid * cap : nullptr;
     int64_t* delta = k.delta + (size_t)wid * A * (E > 0 ? E : 1);
     uint64_t* pbits = k.pbits + (size_t)wid * k.PW;
+    int32_t* const ov_slot = MUT ? k.ov_slot + (size_t)wid * (E > 0 ? E : 1) : nullptr;
+    ReqHdr* const ov_hdr = MUT ? k.ov_hdr + (size_t)wid * k.ov_cap * K : nullptr;
+    uint64_t* const ov_words = MUT ? k.ov_words + (size_t)wid * k.ov_cap * d.DW : nullptr;
 
     if (lane < 5) {
         const int rk = lane == 0 ? d.key_zone : lane == 1 ? d.key_ct : lane == 2 ? d.key_zoneid : lane == 3 ? d.key_resvid : d.key_resvtype;
@@ -312,7 +318,11 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
         for (int w = lane; w < EW; w += 64) {
             excl[w] = 0;
             modb[w] = 0;
+            if (MUT) mutn[w] = 0;
         }
+        // a MUT probe reschedules a mutator's pod: the fast variants hand it over, the MUT variant runs it serially
+        const bool mutp = k.mut && __builtin_amdgcn_readfirstlane(single ? k.mut_s[gp] : k.mut_m[gp]) != 0;
+        int n_ov = 0;  // MUT: node digest copies taken by this probe
         for (int i = lane; i < NT * R; i += 64) rem[i] = d.remaining[i];
         if (k.use_cmax)
             for (int i = lane; i < EW * KP_LDS_AXES; i += 64) cmax[i] = k.cmax0[i];
@@ -469,7 +479,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
         int n_nc = 0, nc_tmpl = -1, prev_shape = -1, xstart = 0, ok_np = 0, nc_nonpend = 0;
         int nc_lc = -1;  // the class whose requirements the in-flight NodeClaim last merged (its Add is then Fits only)
         int relax_at = -1;  // queue position of the last Queue.Push(pod, relaxed): every lastLen pushed before is gone
-        bool aborted = false;
+        bool aborted = !FULL && mutp;  // a MUT probe: the FULL variant's MUT instantiation redoes it
         int cbase = -1, ccls = -1;  // cached node chunk (wave-uniform)
         uint64_t cx = 0;
         // the cached chunk's words of the modified-node bitmap (written back to LDS when the chunk is evicted) and of
@@ -496,6 +506,77 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
         // checked per candidate node from HBM (ex_head minus this probe's delta slab, which holds them as soon as a
         // node takes a pod), and the probe runs the serial queue only (no window pass; the fast variant is not used)
         const bool wide = A > KP_LDS_AXES;
+        // serial: no window pass, every pod of the queue scans the existing nodes itself (wide probes; MUT probes, whose
+        // node compatibility changes as pods land)
+        const bool serial = wide || (MUT && mutp);
+        // MUT: the requirements digest of node j as this probe sees it (its copy once a merge changed it)
+        auto node_digest = [&](int j, const ReqHdr*& h, const uint64_t*& w) {
+            h = d.ex_hdr + (size_t)j * K;
+            w = d.ex_words + (size_t)j * d.DW;
+            if (MUT && mutp && ((uni64(mutn[j >> 6]) >> (j & 63)) & 1ull)) {
+                const int s = __builtin_amdgcn_readfirstlane(ld32(&ov_slot[j]));
+                h = ov_hdr + (size_t)s * K;
+                w = ov_words + (size_t)s * d.DW;
+            }
+        };
+        // MUT: class c's compatible nodes of chunk w (xw from XT) with the nodes this probe changed re-evaluated against
+        // their copies: taints tolerated ∧ static fit ∧ Requirements.Compatible(node copy, class)
+        auto mut_patch = [&](int c, int w, uint64_t xw) -> uint64_t {
+            if (!(MUT && mutp)) return xw;
+            const uint64_t mw = uni64(mutn[w] & ~excl[w]);
+            if (!mw) return xw;
+            bool ok = false;
+            if ((mw >> lane) & 1ull) {
+                const int j = w * 64 + lane;
+                const int s = ld32(&ov_slot[j]);
+                ok = d.ex_static[j] && ((d.ex_tol[(size_t)c * EW + w] >> lane) & 1ull) &&
+                     node_compatible(d, ov_hdr + (size_t)s * K, ov_words + (size_t)s * d.DW, c);
+            }
+            return uni64((xw & ~mw) | ballot(ok));
+        };
+        // MUT: ExistingNode.Add's requirement merge of a pod of class c placed on node j (nodeRequirements.Add(pod
+        // requirements), then .Add(topology requirements): for a topology class ws holds the merged class keys).  The
+        // first merge that changes the node copies its digest; a node's labels are single values that a compatible
+        // merge keeps, so only a class key the node lacks can change it.
+        auto mut_commit = [&](int c, int j, bool from_ws) {
+            int s;
+            if (!((uni64(mutn[j >> 6]) >> (j & 63)) & 1ull)) {
+                bool ch = false;
+                for (int i = d.cls_xkoff[c] + lane; i < d.cls_xkoff[c + 1]; i += 64)
+                    ch |= !(d.ex_hdr[(size_t)j * K + d.cls_xkeys[i]].flags & RF_DEF);
+                if (!ballot(ch)) return;
+                s = n_ov++;
+                for (int i = lane; i < K; i += 64) ov_hdr[(size_t)s * K + i] = d.ex_hdr[(size_t)j * K + i];
+                for (int i = lane; i < d.DW; i += 64) ov_words[(size_t)s * d.DW + i] = d.ex_words[(size_t)j * d.DW + i];
+                if (lane == 0) {
+                    __hip_atomic_store(&ov_slot[j], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    mutn[j >> 6] |= 1ull << (j & 63);
+                }
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");  // the copy is visible to every lane (past L1)
+            } else {
+                s = __builtin_amdgcn_readfirstlane(ld32(&ov_slot[j]));
+            }
+            ReqHdr* nh = ov_hdr + (size_t)s * K;
+            uint64_t* nwd = ov_words + (size_t)s * d.DW;
+            if (from_ws) {
+                if (lane < S.CC.nck) {
+                    const int kk = S.CC.key[lane];
+                    nh[kk] = S.ws.hdr[lane];
+                    for (int i = 0; i < S.CC.nw[lane]; i++) nwd[S.CC.woff[lane] + i] = S.ws.words[S.CC.wsoff[lane] + i];
+                }
+            } else {
+                for (int i = d.cls_xkoff[c] + lane; i < d.cls_xkoff[c + 1]; i += 64) {
+                    const int kk = d.cls_xkeys[i];
+                    ReqHdr a = nh[kk];
+                    req_merge_inplace(d, kk, a, nwd + d.woff[kk], d.cls_hdr[(size_t)c * K + kk],
+                                      d.cls_words + (size_t)c * d.DW + d.woff[kk]);
+                    nh[kk] = a;
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+        };
         auto scan_nodes = [&](int c, const int64_t (&q)[KP_LDS_AXES], int xs, bool tcons, const int64_t* pr) -> int {
             int jf = -1;
             uint64_t fmask = 0;
@@ -509,7 +590,8 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
                         const int wl = (fgrp << 6) + lane;
                         bool pc = false;
                         if (wl < EW) {
-                            pc = (d.XT[(size_t)c * EW + wl] & ~excl[wl]) != 0;
+                            const uint64_t mx = (MUT && mutp) ? mutn[wl] : 0ull;  // changed nodes: maybe compatible
+                            pc = ((d.XT[(size_t)c * EW + wl] | mx) & ~excl[wl]) != 0;
 #pragma unroll
                             for (int ai = 0; ai < KP_LDS_AXES; ai++)
                                 if (ai < A) pc = pc && q[ai] <= cmax[wl * KP_LDS_AXES + ai];
@@ -534,14 +616,14 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
                         cx = uni64((d.C <= KP_CONS_XTC) ? xtc[c] : (d.XT[(size_t)c * EW + w] & ~excl[w]));
                         ccls = c;
                     }
-                    xw = cx;
+                    xw = mut_patch(c, w, cx);
 #pragma unroll
                     for (int ai = 0; ai < KP_LDS_AXES; ai++) {
                         h[ai] = ch[ai];
                         dl[ai] = cd[ai];
                     }
                 } else {
-                    xw = uni64(d.XT[(size_t)c * EW + w] & ~excl[w]);
+                    xw = mut_patch(c, w, uni64(d.XT[(size_t)c * EW + w] & ~excl[w]));
                     if (!(xw & ge)) {
                         st_nodes += 64;
                         continue;
@@ -579,7 +661,10 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
                 if (TOPO && tcons) {  // ExistingNode.Add's topology step on each fitting node, in order
                     while (m) {
                         const int jj = __builtin_amdgcn_readfirstlane(base + __ffsll((unsigned long long)m) - 1);
-                        if (existing_topo_try<true, true>(d, S.CC, S.ws, jj, lane, &P)) break;
+                        const ReqHdr* nh;
+                        const uint64_t* nwd;
+                        node_digest(jj, nh, nwd);
+                        if (existing_topo_try<true, true>(d, S.CC, S.ws, jj, lane, &P, nh, nwd)) break;
                         m &= m - 1;
                     }
                     m = uni64(m);
@@ -631,7 +716,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
             }
             return jf;
         };
-        if (!TOPO && !wide) {
+        if (!TOPO && !serial) {
             // ---- existing nodes: the probe's pods in windows of 64, one pod per lane ----
             // Fast variant: every pod here lands on an existing node or the probe goes to the FULL variant, so the queue
             // is one pass in order and the probe is plain first fit: each pod takes the first node in scheduling order
@@ -835,7 +920,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
             if (FULL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (prof) cy_scan = __builtin_amdgcn_s_memtime() - cf0;
         }
-        if constexpr (FULL || TOPO) while (count > 0) {
+        if constexpr (FULL || TOPO) while (count > 0 && !aborted) {
             // loop-carried wave-uniform state: re-asserted scalar each pod, so the chunk tests below branch on SGPRs
             head = __builtin_amdgcn_readfirstlane(head);
             count = __builtin_amdgcn_readfirstlane(count);
@@ -858,7 +943,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
             count--;
             // FULL, no topology: the window pass above placed this pod on an existing node (first pop), or every node
             // refuses it
-            if (FULL && !TOPO && !wide && pos0 < n && rl32(vpn, off) >= 0) continue;
+            if (FULL && !TOPO && !serial && pos0 < n && rl32(vpn, off) >= 0) continue;
             st_pops++;
             const bool pend = ent < 0;
             const int p = ent & 0x3fffffff;
@@ -887,7 +972,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
             const bool tcons = TOPO && (cflags & CF_TOPO_CONS);
             const int xs = tcons ? 0 : xstart;
             const long long cs0 = prof ? __builtin_amdgcn_s_memtime() : 0;
-            const int jf = (FULL && !TOPO && !fresh && !wide) ? -1 : scan_nodes(c, q, xs, tcons, d.pod_req + (size_t)p * R);
+            const int jf = (FULL && !TOPO && !fresh && !serial) ? -1 : scan_nodes(c, q, xs, tcons, d.pod_req + (size_t)p * R);
             if (prof) cy_scan += __builtin_amdgcn_s_memtime() - cs0;
             if (jf >= 0) {
                 if (wide && lane == 0) {  // the axes past the registers: this probe's delta slab, valid from the first pod
@@ -910,10 +995,13 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
                 cmod |= 1ull << (jf & 63);  // jf lies in the cached chunk
                 if (!tcons) xstart = jf;
                 if (TOPO && (cflags & CF_TOPO)) {  // Topology.Record with the node's merged requirements and taints
-                    if (!tcons) existing_topo_try<false, true>(d, S.CC, S.ws, jf, lane, &P);
-                    topo_record<true>(d, S.CC, S.ws, d.ex_hdr + (size_t)jf * K, d.ex_words + (size_t)jf * d.DW, jf, -1,
-                                      false, lane, jf, &P);
+                    const ReqHdr* nh;
+                    const uint64_t* nwd;
+                    node_digest(jf, nh, nwd);
+                    if (!tcons) existing_topo_try<false, true>(d, S.CC, S.ws, jf, lane, &P, nh, nwd);
+                    topo_record<true>(d, S.CC, S.ws, nh, nwd, jf, -1, false, lane, jf, &P);
                 }
+                if (MUT && mutp) mut_commit(c, jf, TOPO && (cflags & CF_TOPO));
                 st_placed++;
                 if (!pend) {
                     if ((cinit >> (jf & 63)) & 1ull) ok_np++;
@@ -1328,6 +1416,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
             S.st[CS_CACHE_HITS] += st_hits;
             S.st[CS_CHUNK_SKIPS] += st_skips;
             S.st[CS_RELAXED] += st_relax;
+            if (MUT && mutp) S.st[CS_MUT] += 1;
             if (prof) {
                 if (k.prof_probe) {
                     int64_t* pp = k.prof_probe + (size_t)oi * KP_CONS_PP;
@@ -1366,10 +1455,10 @@ template <bool FULL, bool RESV = false, bool TOPO = false, int NA = 0>
 __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
     consolidate_body<FULL, RESV, TOPO, NA>(d, k);
 }
-template <bool RESV, bool TOPO>
+template <bool RESV, bool TOPO, bool MUT = false>
 __global__ __launch_bounds__(64) void consolidate_full_kernel(const KpDev* __restrict__ dp, const KpCons* __restrict__ kp) {
     if (kp->no_fast != 1 && ld32(&kp->next_probe[2]) == 0) return;
-    consolidate_body<true, RESV, TOPO, 0>(*dp, *kp);
+    consolidate_body<true, RESV, TOPO, 0, MUT>(*dp, *kp);
 }
 
 // cmax0[w][ai]: the largest headroom on active axis ai over the nodes of chunk w (one wave per chunk; lanes past E and
@@ -1420,6 +1509,8 @@ bool kp_cons_plan_lds(const KpDev& d, KpCons& k, int max_bytes) {
     off = al(off + 8 * (size_t)(d.EW > 0 ? d.EW : 1));
     k.off_init = (int)off;
     off = al(off + 8 * (size_t)(d.EW > 0 ? d.EW : 1));
+    k.off_mutn = (int)off;  // MUT: nodes whose requirements the probe changed
+    off = al(off + (k.mut ? 8 * (size_t)(d.EW > 0 ? d.EW : 1) : 0));
     k.off_xtc = (int)off;
     off = al(off + 8 * (size_t)(d.C < KP_CONS_XTC ? (d.C > 0 ? d.C : 1) : KP_CONS_XTC));
     k.off_touch = (int)off;  // TOPO: the probe's copied count rows and node host-count columns
@@ -1457,7 +1548,9 @@ hipError_t kp_cons_set_attributes() {
                          (const void*)consolidate_kernel<false, false, false, 5>,
                          (const void*)consolidate_kernel<false, false, false, 6>,
                          (const void*)consolidate_full_kernel<true, false>, (const void*)consolidate_kernel<false, false, true>,
-                         (const void*)consolidate_full_kernel<false, true>, (const void*)consolidate_full_kernel<true, true>};
+                         (const void*)consolidate_full_kernel<false, true>, (const void*)consolidate_full_kernel<true, true>,
+                         (const void*)consolidate_full_kernel<false, false, true>, (const void*)consolidate_full_kernel<true, false, true>,
+                         (const void*)consolidate_full_kernel<false, true, true>, (const void*)consolidate_full_kernel<true, true, true>};
     for (const void* f : fns) {
         const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, KP_LDS_BYTES);
         if (e != hipSuccess) return e;
@@ -1473,8 +1566,14 @@ hipError_t kp_launch_consolidate(const KpDev& d, const KpCons& k, int n_workers,
         if (k.no_fast != 1) hipLaunchKernelGGL((consolidate_kernel<false, false, true>), dim3(n_workers), dim3(64), lds, s, d, k);
         if (k.no_fast != 2) {
             const dim3 gf(n_workers < KP_CONS_FULL_WORKERS ? n_workers : KP_CONS_FULL_WORKERS);  // as below
-            if (d.ro) hipLaunchKernelGGL((consolidate_full_kernel<true, true>), gf, dim3(64), lds, s, d_dev, d_k);
-            else hipLaunchKernelGGL((consolidate_full_kernel<false, true>), gf, dim3(64), lds, s, d_dev, d_k);
+            if (k.mut) {  // MUT instantiation: per-probe node requirement copies
+                if (d.ro) hipLaunchKernelGGL((consolidate_full_kernel<true, true, true>), gf, dim3(64), lds, s, d_dev, d_k);
+                else hipLaunchKernelGGL((consolidate_full_kernel<false, true, true>), gf, dim3(64), lds, s, d_dev, d_k);
+            } else if (d.ro) {
+                hipLaunchKernelGGL((consolidate_full_kernel<true, true>), gf, dim3(64), lds, s, d_dev, d_k);
+            } else {
+                hipLaunchKernelGGL((consolidate_full_kernel<false, true>), gf, dim3(64), lds, s, d_dev, d_k);
+            }
         }
         return hipGetLastError();
     }
@@ -1494,8 +1593,14 @@ hipError_t kp_launch_consolidate(const KpDev& d, const KpCons& k, int n_workers,
         // the FULL variant runs one wave per SIMD (its registers): more workers than SIMDs only queue, and each worker,
         // even an idle one, first copies the kernel arguments to its scratch
         const dim3 gf(n_workers < KP_CONS_FULL_WORKERS ? n_workers : KP_CONS_FULL_WORKERS);
-        if (d.ro) hipLaunchKernelGGL((consolidate_full_kernel<true, false>), gf, dim3(64), lds, s, d_dev, d_k);
-        else hipLaunchKernelGGL((consolidate_full_kernel<false, false>), gf, dim3(64), lds, s, d_dev, d_k);
+        if (k.mut) {
+            if (d.ro) hipLaunchKernelGGL((consolidate_full_kernel<true, false, true>), gf, dim3(64), lds, s, d_dev, d_k);
+            else hipLaunchKernelGGL((consolidate_full_kernel<false, false, true>), gf, dim3(64), lds, s, d_dev, d_k);
+        } else if (d.ro) {
+            hipLaunchKernelGGL((consolidate_full_kernel<true, false>), gf, dim3(64), lds, s, d_dev, d_k);
+        } else {
+            hipLaunchKernelGGL((consolidate_full_kernel<false, false>), gf, dim3(64), lds, s, d_dev, d_k);
+        }
     }
     return hipGetLastError();
 }

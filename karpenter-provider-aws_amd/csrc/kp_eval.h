@@ -40,6 +40,10 @@ struct WaveScratch {
     int32_t n_minrel;
     int32_t minrel_k[KP_MAX_CLASS_KEYS];
     int32_t minrel_v[KP_MAX_CLASS_KEYS];
+    // TEAM evaluations whose join barrier this wave has passed (every wave of the block takes the same early rejects, so
+    // the count is block-uniform): the caller picks the TeamBuf by its parity, so two evaluations that reach the join
+    // back to back never share a buffer, whatever rejects came between them
+    int32_t team_joins;
 };
 
 // An unmet minValues key: Strict fails the Add; BestEffort records the relaxation (wave-uniform).
@@ -350,7 +354,8 @@ struct WitnessAcc {
 };
 
 // One evaluation shared by every wave of the block (TEAM): each wave sweeps the option words w ≡ rank (mod n); the
-// partial results meet here (double-buffered by evaluation parity, so one barrier per evaluation suffices).
+// partial results meet here (double-buffered by the parity of WaveScratch::team_joins, the joins actually reached, so
+// one barrier per evaluation suffices).
 struct TeamBuf {
     uint64_t nw[KP_TW_MAX];    // remaining options, by word (written by the word's wave)
     uint64_t any[KP_NWAVES];   // per wave: OR of its words
@@ -625,12 +630,14 @@ __device__ __forceinline__ void topo_record(const KpDev& d, const ClassCache& CC
 // ExistingNode.Add ([core] scheduling/existingnode.go) for a pod of a topology class on existing node j, one wave,
 // after the caller found j tolerated, Compatible (XT) and with headroom: the requirement merge of the class's keys into
 // the node's requirements (no undefined-label allowance), then Topology.AddRequirements with the node's own domains
-// (hostname = the node's name: host row j).  On success ws holds the merged class keys.
+// (hostname = the node's name: host row j).  On success ws holds the merged class keys.  nh_in / nw_in: the node's
+// requirements digest when it is not d.ex_hdr's row j (a consolidation probe's copy of a node it changed).
 template <bool CONS, bool CT = false>
 __device__ inline bool existing_topo_try(const KpDev& d, const ClassCache& CC, WaveScratch& ws, int j, int lane,
-                                         const ProbeTopo* pt = nullptr) {
-    const ReqHdr* nh = d.ex_hdr + (size_t)j * d.K;
-    const uint64_t* nwp = d.ex_words + (size_t)j * d.DW;
+                                         const ProbeTopo* pt = nullptr, const ReqHdr* nh_in = nullptr,
+                                         const uint64_t* nw_in = nullptr) {
+    const ReqHdr* nh = nh_in ? nh_in : d.ex_hdr + (size_t)j * d.K;
+    const uint64_t* nwp = nw_in ? nw_in : d.ex_words + (size_t)j * d.DW;
     if (lane < CC.nck) {
         const int k = CC.key[lane], n = CC.nw[lane];
         const ReqHdr A = nh[k];
@@ -906,6 +913,7 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
             tb->bt[trank] = wit.bt;
         }
         __syncthreads();
+        if (lane == 0) ws.team_joins++;
         newword = lane < TW ? tb->nw[lane] : 0ull;
         anyw = 0;
         for (int r = 0; r < tn; r++) {

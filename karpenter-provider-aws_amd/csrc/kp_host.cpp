@@ -451,8 +451,8 @@ struct kp_ctx {
     int64_t cycles[37] = {};  // FFD phases (s_memtime): pop, sort, scan+eval, templates, commit, full pdqsort
     bool any_min_values = false;             // some template requirement carries minValues
     bool min_multi = false;                  // ... on a multi-valued catalog key (zone, capacity type, ...)
-    bool cons_mayfix = false;                // a pod's NotIn/DoesNotExist merge can change a later Compatible
-    std::string cons_mayfix_key;
+    std::vector<uint8_t> cons_mutcls;        // per (expanded) class: its NotIn/DoesNotExist merge can change a node's
+                                             // requirements in a way a later decision sees (MUT probes)
     // consolidation probes
     DBuf<int32_t> d_retry, d_rank, d_cand_i, d_cand_off, d_cand_pods, d_pending, d_ring, d_ring_last, d_next, d_pnode;
     DBuf<double> d_cand_price;
@@ -473,6 +473,26 @@ struct kp_ctx {
     DBuf<int64_t> d_prof_probe;              // KPSIM_PROFILE: per-probe cycles
     DBuf<ReqHdr> d_rec_hdr;
     DBuf<uint64_t> d_rec_words;
+    // MUT probes: per-probe flags (single-node by candidate, multi-node by prefix) and the per-worker node requirement
+    // copies of the MUT variant
+    DBuf<int32_t> d_mut_s, d_mut_m, d_ov_slot;
+    DBuf<ReqHdr> d_ov_hdr;
+    DBuf<uint64_t> d_ov_words;
+    int cons_n_mut = 0;                      // probes of the prepared pass that run on the MUT variant
+    // kp_consolidate_command reuses the last full pass and the last read-back of the prepared pass (a command right
+    // after kp_consolidate_execute, or a retry after KP_E_BUFFER, launches nothing); cons_gen moves whenever device
+    // tables or the prepared pass change, which makes both stale
+    uint64_t cons_gen = 0;
+    uint64_t pass_gen = ~0ull;
+    int pass_mode = -1;
+    std::vector<kp_probe_result> pass_rows;  // probes of the last full pass of pass_mode
+    uint64_t rec_gen = ~0ull;
+    int rec_mode = -1, rec_probe = -1;
+    kp_probe_result rec_row{};
+    int32_t rec_ri[4 + 64 + 1] = {};
+    std::vector<ReqHdr> rec_h;
+    std::vector<uint64_t> rec_w;
+    int64_t n_pass_launches = 0, n_readbacks = 0;  // since the last kp_consolidate_prepare (kp_consolidate_stats)
     KpCons cons{};                         // prepared consolidation pass (device pointers set per execute)
     bool cons_prepared = false;
     // device prep of the prepared cluster (queue sort, ranks, pending bits, class / template / existing-node masks)
@@ -698,6 +718,7 @@ static kp_status catalog_upload_one(kp_ctx* ctx, const kp_catalog_view* v, uint6
     ctx->have_catalog = false;
     ctx->prepared = ctx->executed = false;
     ctx->cons_prepared = ctx->cons_prep_valid = false;
+    ctx->cons_gen++;  // cached pass rows and read-backs of kp_consolidate_command are stale
     HIPCHK(hipSetDevice(ctx->device));
     const int T = v->n_types, R = v->n_resources, KL = v->n_label_keys;
     if (T <= 0 || R <= 0 || R > KP_MAX_R) return fail(ctx, KP_E_INVALID, "bad n_types / n_resources");
@@ -1012,6 +1033,7 @@ extern "C" kp_status kp_catalog_upload(kp_ctx* ctx, const kp_catalog_view* v, ui
 static kp_status patch_avail_one(kp_ctx* ctx, const uint8_t* available, int32_t n, uint64_t epoch) {
     if (!ctx || !available) return KP_E_INVALID;
     ctx->cons_prep_valid = false;
+    ctx->cons_gen++;  // cached pass rows and read-backs of kp_consolidate_command are stale
     if (!ctx->have_catalog) return fail(ctx, KP_E_STATE, "no catalog");
     if (n != (int)ctx->off_type.size()) return fail(ctx, KP_E_INVALID, "offering count mismatch");
     HIPCHK(hipSetDevice(ctx->device));
@@ -1039,6 +1061,7 @@ extern "C" kp_status kp_catalog_patch_avail(kp_ctx* ctx, const uint8_t* availabl
 static kp_status patch_price_one(kp_ctx* ctx, const int32_t* idx, const double* price, int32_t n, uint64_t epoch) {
     if (!ctx || (n > 0 && (!idx || !price))) return KP_E_INVALID;
     ctx->cons_prep_valid = false;
+    ctx->cons_gen++;  // cached pass rows and read-backs of kp_consolidate_command are stale
     if (!ctx->have_catalog) return fail(ctx, KP_E_STATE, "no catalog");
     HIPCHK(hipSetDevice(ctx->device));
     for (int i = 0; i < n; i++) {
@@ -1467,6 +1490,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     g_prep_t = std::chrono::steady_clock::now();
     if (!ctx || !in) return KP_E_INVALID;
     ctx->cons_prep_valid = false;
+    ctx->cons_gen++;  // cached pass rows and read-backs of kp_consolidate_command are stale
     if (!ctx->have_catalog) return fail(ctx, KP_E_STATE, "kp_solve before kp_catalog_upload");
     if (!ctx->solve_unsupported.empty()) return fail(ctx, KP_E_UNSUPPORTED, "Solve: " + ctx->solve_unsupported);
     if (ctx->has_reserved && !ctx->ro_ok)
@@ -1541,16 +1565,21 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     const int K = (int)c->sol.keys.size();
     if (K > KP_MAX_KEYS) return fail(ctx, KP_E_UNSUPPORTED, "too many label keys");
     // ExistingNode.Add's requirement merge only changes a node when a NotIn / DoesNotExist pod requirement meets a key
-    // the node lacks, and that change only alters a later Compatible for a class constraining the key positively
-    // (In / Exists / Gt / Lt).  Consolidation probes treat node requirements as immutable, which needs this to be false.
+    // the node lacks (a node's labels are single values, which a compatible merge leaves as they are), and that change
+    // only alters a later decision for a class constraining the key positively (In / Exists / Gt / Lt: Compatible with
+    // the undefined key fails, with NotIn [v] it may pass) or when the key is a topology key (nodeDomains, Record).
+    // Such keys are the mutable keys; a class (relaxation stage) with a NotIn / DoesNotExist requirement on one is a
+    // mutator, and a consolidation probe that reschedules a mutator's pod keeps per-node requirement copies
+    // (consolidate_kernel's MUT variant).  Without mutators every probe treats node requirements as immutable.
     {
-        std::vector<uint8_t> neg(K, 0), pos(K, 0), undef(K, 0);
+        std::vector<uint8_t> neg(K, 0), pos(K, 0), undef(K, 0), topo(K, 0);
         for (int i = 0; i < C; i++)
             for (auto& kv : creq[i]) {
                 const HReq& q = kv.second;
                 const bool ng = (q.complement && !q.vals.empty()) || (!q.complement && q.vals.empty());
                 (ng ? neg : pos)[kv.first] = 1;
             }
+        for (const HGroup& g : th.g) topo[g.key] = 1;
         std::vector<uint8_t> has(K, 0);
         for (int j = 0; j < E; j++) {
             for (auto& kv : exlab[j]) has[kv.first] = 1;
@@ -1559,11 +1588,13 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
             }
             for (auto& kv : exlab[j]) has[kv.first] = 0;
         }
-        c->cons_mayfix = false;
-        for (int k = 0; k < K; k++)
-            if (neg[k] && pos[k] && undef[k]) {
-                c->cons_mayfix = true;
-                c->cons_mayfix_key = c->sol.keys[k].name;
+        c->cons_mutcls.assign(C, 0);
+        for (int i = 0; i < C; i++)
+            for (auto& kv : creq[i]) {
+                const HReq& q = kv.second;
+                const int k = kv.first;
+                const bool ng = (q.complement && !q.vals.empty()) || (!q.complement && q.vals.empty());
+                if (ng && undef[k] && (pos[k] || topo[k])) c->cons_mutcls[i] = 1;
             }
     }
     // ---- key layout ----
@@ -2382,6 +2413,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
 extern "C" kp_status kp_solve_execute(kp_ctx* ctx) {
     if (!ctx) return KP_E_INVALID;
     ctx->cons_prep_valid = false;
+    ctx->cons_gen++;  // cached pass rows and read-backs of kp_consolidate_command are stale
     if (!ctx->prepared || !ctx->have_catalog) return fail(ctx, KP_E_STATE, "kp_solve_execute before kp_solve_prepare");
     HIPCHK(hipSetDevice(ctx->device));
     kp_ctx* c = ctx;
@@ -2642,6 +2674,7 @@ static kp_status cons_prepare_one(kp_ctx* ctx, const kp_consolidate_input* in) t
     if (!ctx || !in) return KP_E_INVALID;
     ctx->cons_prepared = false;
     ctx->cons_prep_valid = false;
+    ctx->cons_gen++;  // cached pass rows and read-backs of kp_consolidate_command are stale
     if (ctx->has_reserved && !ctx->ro_ok)
         return fail(ctx, KP_E_UNSUPPORTED, "consolidation over a catalog with more than 64 reserved offerings");
     if (!ctx->solve_unsupported.empty()) return fail(ctx, KP_E_UNSUPPORTED, "consolidation: " + ctx->solve_unsupported);
@@ -2683,10 +2716,6 @@ static kp_status cons_prepare_one(kp_ctx* ctx, const kp_consolidate_input* in) t
     // on multi-valued labels run inside the probes as in the Solve (consolidate_kernel: relaxed queue entries, the Add's
     // relaxed minValues, per-probe positive hostname domains, prefix-OR distinct counts)
     const KpDev& d = c->dev;
-    if (c->cons_mayfix)
-        return fail(ctx, KP_E_UNSUPPORTED, "consolidation with NotIn/DoesNotExist pod requirements on keys some node lacks "
-                                           "and other pods select positively is not supported by this build (" +
-                                               c->cons_mayfix_key + ")");
     if (d.M <= 0 || d.M > 64) return fail(ctx, KP_E_UNSUPPORTED, "consolidation needs max_instance_types in 1..64");
     const int T = c->T, TW = c->TW, R = c->R, A = d.n_active;
     hipStream_t s = c->stream;
@@ -2811,12 +2840,43 @@ static kp_status cons_prepare_one(kp_ctx* ctx, const kp_consolidate_input* in) t
         HIPCHK(c->d_tg_ha.upload(ha, s));
         HIPCHK(c->d_hpos0.upload(hp, s));
     }
+    // mutators (kp_solve_prepare): a probe that reschedules a pod whose class, or a relaxation stage of it, may change a
+    // node's requirements runs on the MUT variant (per-probe node requirement copies); the others are unaffected
+    {
+        const int C0 = cl.n_classes;
+        std::vector<uint8_t> chain(std::max(C0, 1), 0);
+        for (int i = 0; i < C0; i++)
+            for (int s = i; s >= 0 && !chain[i]; s = c->pref.relax_next.empty() ? -1 : c->pref.relax_next[s])
+                if (s < (int)c->cons_mutcls.size() && c->cons_mutcls[s]) chain[i] = 1;
+        auto pod_mut = [&](int p) { return chain[cl.pods.class_id[p]] != 0; };
+        bool pend_mut = false;
+        for (int i = 0; i < in->n_pending; i++) pend_mut = pend_mut || pod_mut(in->pending[i]);
+        const int mx = c->cons_max_candidates;
+        const int nm = NC < 2 ? 0 : (NC <= mx ? NC - 1 : mx);
+        std::vector<int32_t> ms(std::max(NC, 1), 0), mm(std::max(nm, 1), 0);
+        int any = 0, pre = pend_mut ? 1 : 0;
+        for (int ci = 0; ci < NC; ci++) {
+            int f = pend_mut ? 1 : 0;
+            for (int q = 0; q < in->candidates[ci].n_pods && !f; q++) f = pod_mut(in->candidates[ci].pods[q]) ? 1 : 0;
+            ms[ci] = f;
+            any |= f;
+            pre |= f;  // multi-node probe i covers candidates [0, i + 2)
+            if (ci >= 1 && ci - 1 < nm) mm[ci - 1] = pre;
+        }
+        k.mut = any;
+        c->cons_n_mut = 0;
+        for (int ci = 0; ci < NC; ci++) c->cons_n_mut += ms[ci];
+        for (int i = 0; i < nm; i++) c->cons_n_mut += mm[i];
+        HIPCHK(c->d_mut_s.upload(ms, s));
+        HIPCHK(c->d_mut_m.upload(mm, s));
+    }
     HIPCHK(c->d_next.ensure(3));
     HIPCHK(c->d_rank.ensure(std::max(P, 1)));
     HIPCHK(c->d_pend_bits.ensure(k.PW));
     HIPCHK(c->d_cons_stats.ensure(CS_COUNT));
     HIPCHK(hipStreamSynchronize(s));
     c->cons_prepared = true;
+    c->n_pass_launches = c->n_readbacks = 0;
     return KP_OK;
 } catch (const std::exception& e) {
     return fail(ctx, KP_E_INVALID, e.what());
@@ -2949,6 +3009,20 @@ static kp_status cons_run(kp_ctx* ctx, int m0, int m1, int s0, int s1, kp_probe_
     k.ring_last = c->d_ring_last.p;
     k.pnode = c->d_pnode.p;
     k.delta = c->d_delta.p;
+    k.mut_s = c->d_mut_s.p;
+    k.mut_m = c->d_mut_m.p;
+    if (k.mut) {
+        // the MUT variant's node requirement copies: a probe copies a node's digest when a merge first changes it, at
+        // most once per node and per pod it places (FULL workers only; the fast variants hand MUT probes over)
+        const int fw = std::min(workers, KP_CONS_FULL_WORKERS);
+        k.ov_cap = std::max(1, std::min(std::max(E, 1), k.ring_cap));
+        HIPCHK(c->d_ov_slot.ensure((size_t)fw * std::max(E, 1)));
+        HIPCHK(c->d_ov_hdr.ensure((size_t)fw * k.ov_cap * std::max(d.K, 1)));
+        HIPCHK(c->d_ov_words.ensure((size_t)fw * k.ov_cap * std::max(d.DW, 1)));
+        k.ov_slot = c->d_ov_slot.p;
+        k.ov_hdr = c->d_ov_hdr.p;
+        k.ov_words = c->d_ov_words.p;
+    }
     k.pbits = c->d_pbits.p;
     k.next_probe = c->d_next.p;
     k.retry = c->d_retry.p;
@@ -3039,8 +3113,8 @@ static kp_status cons_run(kp_ctx* ctx, int m0, int m1, int s0, int s1, kp_probe_
 // long multi-node prefixes spread over the devices instead of all landing on the first), each device runs its two
 // shards in one launch from its own host thread, writing into its slices of `results`; counters are summed, device
 // times are the max over devices.  Probes are independent, so the gathered vector equals a single-device evaluation.
-extern "C" kp_status kp_consolidate_execute(kp_ctx* ctx, int32_t mode, int32_t probe_begin, int32_t probe_end,
-                                            kp_probe_result* results, int32_t cap_results) try {
+static kp_status cons_execute(kp_ctx* ctx, int32_t mode, int32_t probe_begin, int32_t probe_end,
+                              kp_probe_result* results, int32_t cap_results) try {
     if (!ctx) return KP_E_INVALID;
     if (!ctx->cons_prepared || !ctx->have_catalog)
         return fail(ctx, KP_E_STATE, "kp_consolidate_execute before kp_consolidate_prepare");
@@ -3113,6 +3187,26 @@ extern "C" kp_status kp_consolidate_execute(kp_ctx* ctx, int32_t mode, int32_t p
     return fail(ctx, KP_E_INVALID, e.what());
 }
 
+extern "C" kp_status kp_consolidate_execute(kp_ctx* ctx, int32_t mode, int32_t probe_begin, int32_t probe_end,
+                                            kp_probe_result* results, int32_t cap_results) try {
+    if (!ctx) return KP_E_INVALID;
+    const uint64_t gen = ctx->cons_gen;
+    const kp_status st = cons_execute(ctx, mode, probe_begin, probe_end, results, cap_results);
+    if (st != KP_OK) return st;
+    ctx->n_pass_launches++;
+    const int np = cons_probes(ctx, mode);
+    const int b0 = probe_begin > 0 ? probe_begin : 0;
+    const int b1 = probe_end > 0 && probe_end < np ? probe_end : np;
+    if (b0 == 0 && b1 == np && gen == ctx->cons_gen) {  // a full pass: kp_consolidate_command can replay it
+        ctx->pass_rows.assign(results, results + np);
+        ctx->pass_mode = mode;
+        ctx->pass_gen = gen;
+    }
+    return KP_OK;
+} catch (const std::exception& e) {
+    return fail(ctx, KP_E_INVALID, e.what());
+}
+
 extern "C" kp_status kp_consolidate(kp_ctx* ctx, const kp_consolidate_input* in, kp_probe_result* results,
                                     int32_t cap_results) {
     if (!ctx || !in) return KP_E_INVALID;
@@ -3146,12 +3240,7 @@ static int replay_multi(const kp_probe_result* r, int n_cand, int max_cand) {
     return best;
 }
 
-extern "C" kp_status kp_consolidate_command(kp_ctx* ctx, int32_t mode, kp_consolidation_command* out) try {
-    if (!ctx || !out) return KP_E_INVALID;
-    if (mode != KP_CONSOLIDATE_SINGLE && mode != KP_CONSOLIDATE_MULTI && mode != KP_CONSOLIDATE_BOTH)
-        return fail(ctx, KP_E_INVALID, "unknown consolidation mode");
-    if (!ctx->cons_prepared || !ctx->have_catalog)
-        return fail(ctx, KP_E_STATE, "kp_consolidate_command before kp_consolidate_prepare");
+static void command_clear(kp_consolidation_command* out) {
     out->decision = KP_DECISION_NONE;
     out->mode = -1;
     out->probe = -1;
@@ -3163,31 +3252,41 @@ extern "C" kp_status kp_consolidate_command(kp_ctx* ctx, int32_t mode, kp_consol
     out->requirements_needed = 0;
     out->result = kp_probe_result{};
     if (out->requirements && out->cap_requirements > 0) out->requirements[0] = 0;
-    const int NC = ctx->cons.n_cand, mx = ctx->cons_max_candidates;
-    const int nm = cons_probes(ctx, KP_CONSOLIDATE_MULTI), np = cons_probes(ctx, mode);
-    std::vector<kp_probe_result> res(std::max(np, 1));
-    if (np > 0) {
-        const kp_status st = kp_consolidate_execute(ctx, mode, 0, np, res.data(), np);
+}
+
+// The replacement NodeClaim of probe `probe` of mode `chosen` (SINGLE / MULTI): the probe re-run on the primary device
+// with the read-back on (FULL variant; the pass's timings and counters stay those of the pass), kept per prepared pass
+// so that a repeated call (a KP_E_BUFFER retry) copies it.  Fills out's replacement fields and result row.
+static kp_status cons_readback(kp_ctx* ctx, int chosen, int probe, kp_consolidation_command* out) {
+    if (!(ctx->rec_gen == ctx->cons_gen && ctx->rec_mode == chosen && ctx->rec_probe == probe)) {
+        double ms_keep[3];
+        int64_t st_keep[CS_COUNT];
+        memcpy(ms_keep, ctx->cons_ms, sizeof ms_keep);
+        memcpy(st_keep, ctx->cons_stats, sizeof st_keep);
+        const uint64_t gen = ctx->cons_gen;
+        kp_probe_result again{};
+        const bool multi = chosen == KP_CONSOLIDATE_MULTI;
+        const kp_status st = multi ? cons_run(ctx, probe, probe + 1, 0, 0, &again, nullptr, true)
+                                   : cons_run(ctx, 0, 0, probe, probe + 1, nullptr, &again, true);
+        memcpy(ctx->cons_ms, ms_keep, sizeof ms_keep);
+        memcpy(ctx->cons_stats, st_keep, sizeof st_keep);
         if (st != KP_OK) return st;
+        ctx->n_readbacks++;
+        const int K = ctx->K, DW = ctx->DW;
+        ctx->rec_h.assign(std::max(K, 1), ReqHdr{});
+        ctx->rec_w.assign(std::max(DW, 1), 0);
+        HIPCHK(hipMemcpy(ctx->rec_ri, ctx->d_rec_i.p, sizeof ctx->rec_ri, hipMemcpyDeviceToHost));
+        if (again.decision == KP_DECISION_REPLACE) {
+            HIPCHK(hipMemcpy(ctx->rec_h.data(), ctx->d_rec_hdr.p, (size_t)K * sizeof(ReqHdr), hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(ctx->rec_w.data(), ctx->d_rec_words.p, (size_t)DW * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        }
+        ctx->rec_row = again;
+        ctx->rec_gen = gen;
+        ctx->rec_mode = chosen;
+        ctx->rec_probe = probe;
     }
-    // the disruption controller's method order: multi-node (binary search), then single-node (first non-no-op)
-    int chosen = -1, probe = -1;
-    const kp_probe_result* rows = res.data();
-    if (mode != KP_CONSOLIDATE_SINGLE) {
-        probe = replay_multi(res.data(), NC, mx);
-        if (probe >= 0) chosen = KP_CONSOLIDATE_MULTI;
-    }
-    if (chosen < 0 && mode != KP_CONSOLIDATE_MULTI) {
-        rows = res.data() + (mode == KP_CONSOLIDATE_BOTH ? nm : 0);
-        for (int i = 0; i < NC; i++)
-            if (rows[i].decision != KP_DECISION_NONE) {
-                probe = i;
-                chosen = KP_CONSOLIDATE_SINGLE;
-                break;
-            }
-    }
-    if (chosen < 0) return KP_OK;
-    const kp_probe_result row = rows[probe];
+    const kp_probe_result& row = ctx->rec_row;
+    const int32_t* ri = ctx->rec_ri;
     out->mode = chosen;
     out->probe = probe;
     out->first_candidate = chosen == KP_CONSOLIDATE_SINGLE ? probe : 0;
@@ -3195,29 +3294,10 @@ extern "C" kp_status kp_consolidate_command(kp_ctx* ctx, int32_t mode, kp_consol
     out->result = row;
     out->decision = row.decision;
     if (row.decision != KP_DECISION_REPLACE) return KP_OK;
-    // the replacement NodeClaim: re-run the chosen probe on the primary device with the read-back on (the pass's
-    // timings and counters stay those of the pass)
-    double ms_keep[3];
-    int64_t st_keep[CS_COUNT];
-    memcpy(ms_keep, ctx->cons_ms, sizeof ms_keep);
-    memcpy(st_keep, ctx->cons_stats, sizeof st_keep);
-    kp_probe_result again{};
-    const bool multi = chosen == KP_CONSOLIDATE_MULTI;
-    const kp_status st = multi ? cons_run(ctx, probe, probe + 1, 0, 0, &again, nullptr, true)
-                               : cons_run(ctx, 0, 0, probe, probe + 1, nullptr, &again, true);
-    memcpy(ctx->cons_ms, ms_keep, sizeof ms_keep);
-    memcpy(ctx->cons_stats, st_keep, sizeof st_keep);
-    if (st != KP_OK) return st;
-    const int K = ctx->K, DW = ctx->DW;
-    int32_t ri[4 + 64 + 1];
-    std::vector<ReqHdr> h(std::max(K, 1));
-    std::vector<uint64_t> w(std::max(DW, 1));
-    HIPCHK(hipMemcpy(ri, ctx->d_rec_i.p, sizeof ri, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(h.data(), ctx->d_rec_hdr.p, (size_t)K * sizeof(ReqHdr), hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(w.data(), ctx->d_rec_words.p, (size_t)DW * sizeof(uint64_t), hipMemcpyDeviceToHost));
-    if (ri[0] != KP_DECISION_REPLACE || again.decision != row.decision || again.n_replacement_types != row.n_replacement_types ||
-        ri[3] != row.n_replacement_types || ri[1] < 0 || ri[1] >= (int)ctx->tmpl_np.size())
-        return fail(ctx, KP_E_DEVICE, "kp_consolidate_command: the read-back run disagrees with the pass");
+    if (ri[0] != KP_DECISION_REPLACE || ri[3] != row.n_replacement_types || ri[1] < 0 || ri[1] >= (int)ctx->tmpl_np.size())
+        return fail(ctx, KP_E_DEVICE, "consolidation read-back: inconsistent replacement record");
+    std::vector<ReqHdr> h = ctx->rec_h;
+    std::vector<uint64_t> w = ctx->rec_w;
     out->nodepool = ctx->tmpl_np[ri[1]];
     out->n_reserved = ri[4 + 64];
     // the replacement was priced as spot: Requirements.Add(capacity-type In [spot]) (consolidation.go)
@@ -3247,7 +3327,70 @@ extern "C" kp_status kp_consolidate_command(kp_ctx* ctx, int32_t mode, kp_consol
         memcpy(out->requirements, txt.c_str(), txt.size() + 1);
     else
         small = true;
-    return small ? fail(ctx, KP_E_BUFFER, "kp_consolidate_command: replacement buffers too small") : KP_OK;
+    return small ? fail(ctx, KP_E_BUFFER, "consolidation command: replacement buffers too small") : KP_OK;
+}
+
+extern "C" kp_status kp_consolidate_command(kp_ctx* ctx, int32_t mode, kp_consolidation_command* out) try {
+    if (!ctx || !out) return KP_E_INVALID;
+    if (mode != KP_CONSOLIDATE_SINGLE && mode != KP_CONSOLIDATE_MULTI && mode != KP_CONSOLIDATE_BOTH)
+        return fail(ctx, KP_E_INVALID, "unknown consolidation mode");
+    if (!ctx->cons_prepared || !ctx->have_catalog)
+        return fail(ctx, KP_E_STATE, "kp_consolidate_command before kp_consolidate_prepare");
+    command_clear(out);
+    const int NC = ctx->cons.n_cand, mx = ctx->cons_max_candidates;
+    const int nm = cons_probes(ctx, KP_CONSOLIDATE_MULTI), np = cons_probes(ctx, mode);
+    // the probe rows: the last full pass of this prepared pass when it covers `mode` (a BOTH pass covers either),
+    // else one pass now
+    const bool have = ctx->pass_gen == ctx->cons_gen && (ctx->pass_mode == mode || ctx->pass_mode == KP_CONSOLIDATE_BOTH);
+    if (!have && np > 0) {
+        std::vector<kp_probe_result> res(np);
+        const kp_status st = kp_consolidate_execute(ctx, mode, 0, np, res.data(), np);
+        if (st != KP_OK) return st;
+    }
+    const bool both_rows = ctx->pass_mode == KP_CONSOLIDATE_BOTH;
+    const kp_probe_result* mrows = ctx->pass_rows.data();                                  // multi-node rows
+    const kp_probe_result* srows = ctx->pass_rows.data() + (both_rows ? nm : 0);           // single-node rows
+    // the disruption controller's method order: multi-node (binary search), then single-node (first non-no-op)
+    int chosen = -1, probe = -1;
+    if (mode != KP_CONSOLIDATE_SINGLE && np > 0) {
+        probe = replay_multi(mrows, NC, mx);
+        if (probe >= 0) chosen = KP_CONSOLIDATE_MULTI;
+    }
+    if (chosen < 0 && mode != KP_CONSOLIDATE_MULTI && np > 0) {
+        for (int i = 0; i < NC; i++)
+            if (srows[i].decision != KP_DECISION_NONE) {
+                probe = i;
+                chosen = KP_CONSOLIDATE_SINGLE;
+                break;
+            }
+    }
+    if (chosen < 0) return KP_OK;
+    const kp_probe_result row = chosen == KP_CONSOLIDATE_MULTI ? mrows[probe] : srows[probe];
+    out->mode = chosen;
+    out->probe = probe;
+    out->first_candidate = chosen == KP_CONSOLIDATE_SINGLE ? probe : 0;
+    out->n_candidates = chosen == KP_CONSOLIDATE_SINGLE ? 1 : probe + 2;
+    out->result = row;
+    out->decision = row.decision;
+    if (row.decision != KP_DECISION_REPLACE) return KP_OK;
+    const kp_status st = cons_readback(ctx, chosen, probe, out);
+    if (st != KP_OK && st != KP_E_BUFFER) return st;
+    if (out->result.decision != row.decision || out->result.n_replacement_types != row.n_replacement_types)
+        return fail(ctx, KP_E_DEVICE, "kp_consolidate_command: the read-back run disagrees with the pass");
+    return st;
+} catch (const std::exception& e) {
+    return fail(ctx, KP_E_INVALID, e.what());
+}
+
+extern "C" kp_status kp_consolidate_replacement(kp_ctx* ctx, int32_t mode, int32_t probe, kp_consolidation_command* out) try {
+    if (!ctx || !out) return KP_E_INVALID;
+    if (mode != KP_CONSOLIDATE_SINGLE && mode != KP_CONSOLIDATE_MULTI)
+        return fail(ctx, KP_E_INVALID, "kp_consolidate_replacement: mode must be SINGLE or MULTI");
+    if (!ctx->cons_prepared || !ctx->have_catalog)
+        return fail(ctx, KP_E_STATE, "kp_consolidate_replacement before kp_consolidate_prepare");
+    if (probe < 0 || probe >= cons_probes(ctx, mode)) return fail(ctx, KP_E_INVALID, "probe out of range");
+    command_clear(out);
+    return cons_readback(ctx, mode, probe, out);
 } catch (const std::exception& e) {
     return fail(ctx, KP_E_INVALID, e.what());
 }
@@ -3257,7 +3400,8 @@ extern "C" kp_status kp_consolidate_stats(kp_ctx* ctx, double* ms, int64_t* coun
     if (ms)
         for (int i = 0; i < 3; i++) ms[i] = ctx->cons_ms[i];
     if (counters)
-        for (int i = 0; i < n_counters && i < CS_COUNT; i++) counters[i] = ctx->cons_stats[i];
+        for (int i = 0; i < n_counters && i < CS_COUNT + 2; i++)
+            counters[i] = i < CS_COUNT ? ctx->cons_stats[i] : i == CS_COUNT ? ctx->n_pass_launches : ctx->n_readbacks;
     return KP_OK;
 }
 

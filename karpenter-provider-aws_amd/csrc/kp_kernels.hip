@@ -649,6 +649,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
         d.pod_order[p] = -1;
     }
     for (int j = wave; j < d.NT; j += KP_NWAVES) limit_mask_update(d, j, lane);  // the NodePools' limits of this solve
+    if (lane == 0) S.ws[wave].team_joins = 0;
     if (PREF && d.relax_next)  // a previous execute may have relaxed pods: every pod starts from its input class
         for (int p = tid; p < P; p += nthr) {
             d.pod_cls[p] = d.pod_cls0[p];
@@ -1427,11 +1428,14 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 a.prof = (d.profile && wave == 0) ? &S.st[ST_EV_REQ] : nullptr;
                 a.host = d.E + nc;
                 a.held = (RESV && d.resv_on) ? ld_u64(&d.nc_held[nc]) : 0ull;
+                // the buffer by the joins reached so far, not by candidate index: a candidate rejected before the join
+                // (no barrier) must not flip the parity
+                TeamBuf* const tb = &S.team[__builtin_amdgcn_readfirstlane(S.ws[wave].team_joins) & 1];
                 const bool ok = (S.CC.flags & CF_TOPO_CONS)
-                                    ? eval_wave<true, RESV, true, PREF, false, true>(d, E, S.CC, a, S.ws[wave], lane, &S.team[ti & 1],
+                                    ? eval_wave<true, RESV, true, PREF, false, true>(d, E, S.CC, a, S.ws[wave], lane, tb,
                                                                                      wave, KP_NWAVES)
                                     : eval_wave<false, RESV, true, PREF, false, true>(d, E, S.CC, a, S.ws[wave], lane,
-                                                                                      &S.team[ti & 1], wave, KP_NWAVES);
+                                                                                      tb, wave, KP_NWAVES);
                 if (wave == 0 && lane == 0) {
                     S.fastp[b][i] = 0;
                     S.acc[b][i] = ok;
@@ -1476,11 +1480,12 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 a.prof = (d.profile && wave == 0) ? &S.st[ST_EV_REQ] : nullptr;
                 a.host = d.E + nc;
                 a.held = (RESV && d.resv_on) ? ld_u64(&d.nc_held[nc]) : 0ull;
+                TeamBuf* const tb = &S.team[__builtin_amdgcn_readfirstlane(S.ws[wave].team_joins) & 1];
                 const bool ok = (TOPO_ON && (S.CC.flags & CF_TOPO_CONS))
-                                    ? eval_wave<true, RESV, true, PREF, false, true>(d, E, S.CC, a, S.ws[wave], lane, &S.team[0],
+                                    ? eval_wave<true, RESV, true, PREF, false, true>(d, E, S.CC, a, S.ws[wave], lane, tb,
                                                                                      wave, KP_NWAVES)
                                     : eval_wave<false, RESV, true, PREF, false, true>(d, E, S.CC, a, S.ws[wave], lane,
-                                                                                      &S.team[0], wave, KP_NWAVES);
+                                                                                      tb, wave, KP_NWAVES);
                 if (wave == 0 && lane == 0) {
                     S.fastp[0][0] = 0;
                     S.acc[0][0] = ok;
@@ -1497,7 +1502,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                     win = 0;
                     team_won = true;
                 }
-                __syncthreads();  // the team's scratch (S.team[0]) and acc[0][0] before the parallel round
+                __syncthreads();  // the team's scratch and acc[0][0] before the parallel round
             }
         }
         for (; !team && !team_won;) {

@@ -92,13 +92,24 @@ def replay_multi(results: np.ndarray, n_candidates: int, max_candidates: int = 1
     return best
 
 
-def _command(cp, results, probe, mode) -> Command:
+def _command(cp, results, probe, mode, replacement_fn=None) -> Command:
+    """The Command of the chosen probe; replacement_fn(cp, mode, probe) -> Command (kp_consolidate_replacement on this
+    process's device, or the oracle's) supplies a REPLACE's replacement NodeClaim: NodePool, price-ordered options,
+    requirements, held reservations."""
     if probe < 0:
         return NO_OP
     r = results[probe]
     cands = [probe] if mode == abi.KP_CONSOLIDATE_SINGLE else list(range(probe + 2))
-    return Command(int(r["decision"]), cands, int(r["n_replacement_types"]), float(r["candidate_price"]),
-                   float(r["replacement_price"]))
+    cmd = Command(int(r["decision"]), cands, int(r["n_replacement_types"]), float(r["candidate_price"]),
+                  float(r["replacement_price"]), mode, probe)
+    if cmd.decision == abi.KP_DECISION_REPLACE and replacement_fn is not None:
+        rep = replacement_fn(cp, mode, probe)
+        if (rep.decision, rep.n_replacement_types, rep.replacement_price) != \
+                (cmd.decision, cmd.n_replacement_types, cmd.replacement_price):
+            raise RuntimeError("replacement read-back disagrees with the gathered probe row")
+        cmd.nodepool, cmd.type_ids, cmd.requirements, cmd.n_reserved = rep.nodepool, rep.type_ids, rep.requirements, \
+            rep.n_reserved
+    return cmd
 
 
 def shard_range(n_probes, rank, world):
@@ -109,11 +120,13 @@ def shard_range(n_probes, rank, world):
 
 
 def compute_command(cp: model.ConsolidationProblem, mode, probe_fn, max_candidates=100, group=None,
-                    distributed=True) -> Command:
+                    distributed=True, replacement_fn=None) -> Command:
     """ComputeCommand for one mode.  probe_fn(cp, mode, begin, end) evaluates probes [begin, end) (kp_consolidate on
     this rank's GPU).  With a torch.distributed group the probes are sharded across its ranks and one collective
     carries each rank's result: the first valid single-node probe of the shard, or the shard's multi-node rows.
-    distributed=False: probe_fn covers the whole range in this process (a multi-device kp_ctx shards internally)."""
+    distributed=False: probe_fn covers the whole range in this process (a multi-device kp_ctx shards internally).
+    replacement_fn(cp, mode, probe): a REPLACE's replacement NodeClaim, read back on every rank from its own prepared
+    pass (one probe, no further collective), so every rank returns the whole Command."""
     n = model.consolidation_probe_count(len(cp.candidates), mode, max_candidates)
     if n == 0:
         return NO_OP
@@ -121,7 +134,7 @@ def compute_command(cp: model.ConsolidationProblem, mode, probe_fn, max_candidat
         res = probe_fn(cp, mode, 0, 0)
         probe = first_valid_single(res) if mode == abi.KP_CONSOLIDATE_SINGLE else \
             replay_multi(res, len(cp.candidates), max_candidates)
-        return _command(cp, res, probe, mode)
+        return _command(cp, res, probe, mode, replacement_fn)
     import torch
     import torch.distributed as dist
     rank, world = dist.get_rank(group), dist.get_world_size(group)
@@ -148,7 +161,7 @@ def compute_command(cp: model.ConsolidationProblem, mode, probe_fn, max_candidat
             return NO_OP
         full = np.zeros(n, abi.PROBE_DTYPE)
         full[best] = best_row[0]
-        return _command(cp, full, best, mode)
+        return _command(cp, full, best, mode, replacement_fn)
     per = (n + world - 1) // world
     pad = np.zeros(per, abi.PROBE_DTYPE)
     pad[:len(res)] = res
@@ -157,7 +170,7 @@ def compute_command(cp: model.ConsolidationProblem, mode, probe_fn, max_candidat
     dist.all_gather(parts, loc, group=group)
     full = np.concatenate([p_.cpu().numpy().view(abi.PROBE_DTYPE) for p_ in parts])[:n]
     probe = replay_multi(full, len(cp.candidates), max_candidates)
-    return _command(cp, full, probe, mode)
+    return _command(cp, full, probe, mode, replacement_fn)
 
 
 def _dist_on():
@@ -181,7 +194,21 @@ class Consolidator:
 
     def probes(self, cp: model.ConsolidationProblem, mode, begin=0, end=0, cluster_view=None) -> np.ndarray:
         v = model.ConsolidateInputView(cp, mode, begin, end, self.spot_to_spot, self.max_candidates, cluster_view)
+        self._prepared = (cp, v)  # kp_consolidate leaves the pass prepared on the ctx
         return self.ctx.consolidate(v)
 
+    def replacement(self, cp: model.ConsolidationProblem, mode, probe) -> Command:
+        """kp_consolidate_replacement of one probe; prepares the pass first when this process evaluated no probe of it
+        (an empty shard)."""
+        prep = getattr(self, "_prepared", None)
+        if prep is None or prep[0] is not cp:
+            v = model.ConsolidateInputView(cp, mode, 0, 0, self.spot_to_spot, self.max_candidates)
+            self.ctx.consolidate_prepare(v)
+            self._prepared = (cp, v)
+        return self.ctx.consolidate_replacement(mode, probe)
+
     def compute_command(self, cp: model.ConsolidationProblem, mode, group=None) -> Command:
-        return compute_command(cp, mode, lambda c, m, b0, b1: self.probes(c, m, b0, b1), self.max_candidates, group)
+        """The Command of one method, with the replacement NodeClaim of a REPLACE (kp_consolidate_replacement over this
+        process's prepared pass)."""
+        return compute_command(cp, mode, lambda c, m, b0, b1: self.probes(c, m, b0, b1), self.max_candidates, group,
+                               replacement_fn=self.replacement)

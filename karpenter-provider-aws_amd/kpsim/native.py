@@ -13,7 +13,7 @@ EXPORTS = [
     "kp_result_nodeclaim_requirements", "kp_last_kernel_times", "kp_consolidate_probe_count", "kp_consolidate",
     "kp_consolidate_stats", "kp_consolidate_prepare", "kp_consolidate_execute", "kp_launch_select", "kp_launch_stats",
     "kp_nodeclaim_labels", "kp_catalog_build", "kp_catalog_get_view", "kp_catalog_overhead", "kp_catalog_resource_name",
-    "kp_catalog_free", "kp_consolidate_command",
+    "kp_catalog_free", "kp_consolidate_command", "kp_consolidate_replacement",
 ]
 
 _lib = None
@@ -56,6 +56,7 @@ def load():
                                          C.c_int32]
     L.kp_consolidate_stats.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.c_int32]
     L.kp_consolidate_command.argtypes = [C.c_void_p, C.c_int32, C.POINTER(abi.kp_consolidation_command)]
+    L.kp_consolidate_replacement.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(abi.kp_consolidation_command)]
     L.kp_launch_select.argtypes = [C.c_void_p, C.c_int32, C.POINTER(abi.kp_launch_request), C.c_int32,
                                    C.POINTER(abi.kp_launch_result), C.POINTER(C.c_int32), C.c_int32,
                                    C.POINTER(C.c_int32), C.c_int32]
@@ -208,11 +209,20 @@ class Context:
         self.check(st, "kp_consolidate_command")
         return cmd
 
+    def consolidate_replacement(self, mode, probe):
+        """kp_consolidate_replacement: the command of one probe of the prepared pass (its row and, for a REPLACE, the
+        replacement NodeClaim) -> kpsim.consolidation.Command."""
+        from kpsim import consolidation
+        st, cmd = consolidation.command_call(
+            lambda cc: self.L.kp_consolidate_replacement(self.h, mode, probe, C.byref(cc)))
+        self.check(st, "kp_consolidate_replacement")
+        return cmd
+
     def consolidate_stats(self):
-        """(ms[prep, probe kernel, call], counters[17]) of the last kp_consolidate (kpsim.h kp_consolidate_stats)."""
+        """(ms[prep, probe kernel, call], counters[20]) of the last kp_consolidate (kpsim.h kp_consolidate_stats)."""
         ms = (C.c_double * 3)()
-        ct = (C.c_int64 * 17)()
-        self.check(self.L.kp_consolidate_stats(self.h, ms, ct, 17), "kp_consolidate_stats")
+        ct = (C.c_int64 * 20)()
+        self.check(self.L.kp_consolidate_stats(self.h, ms, ct, 20), "kp_consolidate_stats")
         return list(ms), list(ct)
 
     def close(self):

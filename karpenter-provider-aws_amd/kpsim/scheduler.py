@@ -8,7 +8,7 @@ instance-type catalog is what CloudProvider.GetInstanceTypes returns (pkg/cloudp
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
-from . import model, native
+from . import abi, model, native
 
 
 @dataclass
@@ -42,7 +42,16 @@ class Scheduler:
         cap_nc = max(16, min(prob.pods.n + 1, 8192))
         m = prob.max_instance_types if prob.max_instance_types > 0 else len(self.catalog)
         out = model.OutputBuffers(prob.pods.n, cap_nc, cap_nc * m)
-        self.ctx.solve(iv, out)
+        try:
+            self.ctx.solve(iv, out)
+        except native.KpError as e:
+            if e.status != abi.KP_E_BUFFER:
+                raise
+            # more NodeClaims than the first buffers hold (node-dense solves): kp_solve_fetch reported the sizes and can
+            # be called again on the executed solve with buffers of exactly that size
+            v = out.view
+            out = model.OutputBuffers(prob.pods.n, max(1, v.n_nodeclaims), max(1, v.n_type_ids))
+            self.ctx.fetch(out)
         return out.results()
 
     def Solve(self, prob: model.Problem) -> SolveResults:

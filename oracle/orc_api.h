@@ -36,6 +36,9 @@ kp_status orc_consolidate_command(const kp_catalog_view* cat, const kp_consolida
 kp_status orc_consolidate_command_opts(const kp_catalog_view* cat, const kp_consolidate_input* in,
                                        const kp_device_opts* opts, int32_t mode, kp_consolidation_command* out,
                                        int32_t n_threads);
+kp_status orc_consolidate_replacement_opts(const kp_catalog_view* cat, const kp_consolidate_input* in,
+                                           const kp_device_opts* opts, int32_t mode, int32_t probe,
+                                           kp_consolidation_command* out);
 
 /* Launch-time selection (filter.go chain + Truncate + getCapacityType + getOverrides' offering side), same
  * contract as kp_launch_select. */

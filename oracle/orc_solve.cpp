@@ -1531,6 +1531,9 @@ extern "C" kp_status orc_consolidate(const kp_catalog_view* cat, const kp_consol
     return orc_consolidate_opts(cat, in, nullptr, results, cap_results, n_threads);
 }
 
+static kp_status fill_command(ConsEnv& env, kp_consolidate_input& im, int chosen, int probe, const kp_probe_result& row,
+                              kp_consolidation_command* out);
+
 extern "C" kp_status orc_consolidate_command_opts(const kp_catalog_view* cat, const kp_consolidate_input* in,
                                                   const kp_device_opts* opts, int32_t mode, kp_consolidation_command* out,
                                                   int32_t n_threads) {
@@ -1582,22 +1585,29 @@ extern "C" kp_status orc_consolidate_command_opts(const kp_catalog_view* cat, co
             }
     }
     if (chosen < 0) return KP_OK;
+    return fill_command(*env, im, chosen, probe, rows[probe], out);
+}
+
+// The command of probe `probe` of mode `chosen` with its row: delete set, and for a REPLACE the replacement NodeClaim
+// (the probe re-run with the read-back).
+static kp_status fill_command(ConsEnv& env, kp_consolidate_input& im, int chosen, int probe, const kp_probe_result& row,
+                              kp_consolidation_command* out) {
     out->mode = chosen;
     out->probe = probe;
     out->first_candidate = chosen == KP_CONSOLIDATE_SINGLE ? probe : 0;
     out->n_candidates = chosen == KP_CONSOLIDATE_SINGLE ? 1 : probe + 2;
-    out->result = rows[probe];
-    out->decision = rows[probe].decision;
+    out->result = row;
+    out->decision = row.decision;
     if (out->decision != KP_DECISION_REPLACE) return KP_OK;
     im.mode = chosen;
-    env->X.in = &im;
+    env.X.in = &im;
     Replacement rep;
     kp_probe_result again{};
-    run_probe(env->X, probe, again, &rep);
+    run_probe(env.X, probe, again, &rep);
     out->nodepool = rep.nodepool;
     out->n_reserved = rep.n_held;
     out->n_type_ids = (int)rep.opts.size();
-    const std::string txt = reqs_text(env->D, rep.reqs);
+    const std::string txt = reqs_text(env.D, rep.reqs);
     out->requirements_needed = (int64_t)txt.size() + 1;
     bool small = false;
     for (int i = 0; i < out->n_type_ids; i++) {
@@ -1609,6 +1619,29 @@ extern "C" kp_status orc_consolidate_command_opts(const kp_catalog_view* cat, co
     else
         small = true;
     return small ? KP_E_BUFFER : KP_OK;
+}
+
+// kp_consolidate_replacement's restatement: the command of one given probe (its row, and the replacement of a REPLACE).
+extern "C" kp_status orc_consolidate_replacement_opts(const kp_catalog_view* cat, const kp_consolidate_input* in,
+                                                      const kp_device_opts* opts, int32_t mode, int32_t probe,
+                                                      kp_consolidation_command* out) {
+    if (!cat || !in || !out) return KP_E_INVALID;
+    if (mode != KP_CONSOLIDATE_SINGLE && mode != KP_CONSOLIDATE_MULTI) return KP_E_INVALID;
+    auto env = std::make_unique<ConsEnv>();
+    kp_status st = cons_setup(cat, in, opts, *env);
+    if (st != KP_OK) return st;
+    kp_consolidate_input im = *in;
+    im.mode = mode;
+    if (probe < 0 || probe >= consolidate_probe_count(&im)) return KP_E_INVALID;
+    out->decision = KP_DECISION_NONE;
+    out->mode = out->probe = out->nodepool = -1;
+    out->first_candidate = out->n_candidates = out->n_type_ids = out->n_reserved = 0;
+    out->requirements_needed = 0;
+    out->result = kp_probe_result{};
+    env->X.in = &im;
+    kp_probe_result row{};
+    run_probe(env->X, probe, row);
+    return fill_command(*env, im, mode, probe, row, out);
 }
 
 extern "C" kp_status orc_consolidate_command(const kp_catalog_view* cat, const kp_consolidate_input* in, int32_t mode,

@@ -54,6 +54,11 @@ def lib():
                                                       C.POINTER(abi.kp_device_opts), C.c_int32,
                                                       C.POINTER(abi.kp_consolidation_command), C.c_int32]
         _lib.orc_consolidate_command_opts.restype = C.c_int32
+        _lib.orc_consolidate_replacement_opts.argtypes = [C.POINTER(abi.kp_catalog_view),
+                                                          C.POINTER(abi.kp_consolidate_input),
+                                                          C.POINTER(abi.kp_device_opts), C.c_int32, C.c_int32,
+                                                          C.POINTER(abi.kp_consolidation_command)]
+        _lib.orc_consolidate_replacement_opts.restype = C.c_int32
         _lib.orc_launch_select.argtypes = [C.POINTER(abi.kp_catalog_view), C.c_int32, C.POINTER(abi.kp_launch_request),
                                            C.c_int32, C.POINTER(abi.kp_launch_result), C.POINTER(C.c_int32), C.c_int32,
                                            C.POINTER(C.c_int32), C.c_int32]
@@ -186,6 +191,21 @@ def consolidate_command(cp, mode, spot_to_spot=False, max_candidates=100, n_thre
                                                   n_threads))
     if st != 0:
         raise RuntimeError("orc_consolidate_command failed: %d" % st)
+    return cmd
+
+
+def consolidate_replacement(cp, mode, probe, spot_to_spot=False, max_candidates=100, preference_policy=0):
+    """CPU oracle command of one given probe (orc_consolidate_replacement_opts) -> kpsim.consolidation.Command."""
+    from kpsim import abi, consolidation, model
+    L = lib()
+    opts = abi.kp_device_opts(preference_policy=preference_policy)
+    cv = model.CatalogView(cp.cluster.catalog)
+    iv = model.ConsolidateInputView(cp, mode, 0, 0, spot_to_spot, max_candidates)
+    st, cmd = consolidation.command_call(
+        lambda cc: L.orc_consolidate_replacement_opts(C.byref(cv.view), C.byref(iv.view), C.byref(opts), mode, probe,
+                                                      C.byref(cc)))
+    if st != 0:
+        raise RuntimeError("orc_consolidate_replacement failed: %d" % st)
     return cmd
 
 

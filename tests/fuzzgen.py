@@ -198,39 +198,67 @@ def fuzz_topology_problem(catalog, seed, n_pods=200, n_classes=10):
     return add_topology(np.random.Generator(np.random.PCG64(seed + 99)), prob)
 
 
-def _negative(r):
-    return r.op in ("NotIn", "DoesNotExist") and not (r.op == "NotIn" and not r.values)
+GPU_COUNT = AWS + "instance-gpu-count"
+NODEPOOL = "karpenter.sh/nodepool"
 
 
-def drop_mutating_requirements(prob):
-    """Remove NotIn/DoesNotExist pod requirements that could change a node's requirements in a way a later pod sees
-    (a key some node lacks that another class selects positively): consolidation probes keep nodes immutable and the
-    library rejects such inputs (KP_E_UNSUPPORTED)."""
-    def empty_in(pc, key):  # In requirements on one key with no common value: the merged requirement is In [] = DNE
-        ins = [set(r.values) for r in pc.requirements if r.key == key and r.op == "In"]
-        return len(ins) > 1 and not set.intersection(*ins)
-
-    keys = set()
+def add_mutators(rng, cp, gpu_catalog=None):
+    """The reference's shapes whose ExistingNode.Add merges change a node's requirements (a NotIn / DoesNotExist pod
+    requirement on a label the node lacks) in a way later pods see:
+      * GPU avoidance: non-GPU instance types carry instance-gpu-count / -name as DoesNotExist
+        (pkg/providers/instancetype/types.go:204-210) and only single-valued requirements become node labels
+        (pkg/cloudprovider/cloudprovider.go:387-398), so non-GPU nodes lack the labels; "keep off GPU nodes" pods say
+        instance-gpu-count DoesNotExist (or NotIn [..]) next to GPU pods selecting instance-gpu-count Gt 0;
+      * mixed node groups: pods with karpenter.sh/nodepool DoesNotExist in a cluster whose managed-node-group nodes lack
+        the label (website/content/en/preview/getting-started/migrating-from-cas/_index.md:117-123), next to pods
+        selecting a NodePool positively.
+    Some nodes become GPU nodes (labels of a GPU type from gpu_catalog), some Karpenter nodes (karpenter.sh/nodepool);
+    some classes get the negative and some the positive requirements."""
+    prob = cp.cluster
+    gpus = [it for it in (gpu_catalog or prob.catalog) if it.labels.get(GPU_COUNT) not in (None, [], "")]
+    for n in prob.existing:
+        if gpus and rng.random() < 0.25:
+            it = gpus[int(rng.integers(0, len(gpus)))]
+            for k in (GPU_COUNT, AWS + "instance-gpu-name", AWS + "instance-gpu-manufacturer"):
+                v = it.labels.get(k)
+                if isinstance(v, (list, tuple)):
+                    v = v[0] if v else None
+                if v is not None:
+                    n.labels[k] = str(v)
+        if rng.random() < 0.6:
+            n.labels[NODEPOOL] = prob.nodepools[int(rng.integers(0, len(prob.nodepools)))].name
+    pools = [np_.name for np_ in prob.nodepools]
     for pc in prob.classes:
-        keys |= {r.key for r in pc.requirements}
-    pos = {r.key for pc in prob.classes for r in pc.requirements if not _negative(r)}
-    undef = {k for k in keys if k != HOSTNAME and any(k not in n.labels for n in prob.existing)}
-    bad = pos & undef
-    for pc in prob.classes:
-        pc.requirements = [r for r in pc.requirements
-                           if not ((_negative(r) or empty_in(pc, r.key)) and r.key in bad)]
-    return prob
+        u = rng.random()
+        reqs = list(pc.requirements)
+        if u < 0.25:
+            reqs.append(Requirement(GPU_COUNT, "DoesNotExist"))
+        elif u < 0.35:
+            reqs.append(Requirement(GPU_COUNT, "NotIn", [str(rng.choice(["1", "4", "8"]))]))
+        elif u < 0.5:
+            reqs.append(Requirement(GPU_COUNT, "Gt", ["0"]))
+        elif u < 0.55:
+            reqs.append(Requirement(GPU_COUNT, "Exists"))
+        v = rng.random()
+        if v < 0.3:
+            reqs.append(Requirement(NODEPOOL, "DoesNotExist"))
+        elif v < 0.4:
+            reqs.append(Requirement(NODEPOOL, "NotIn", [str(rng.choice(pools))]))
+        elif v < 0.55:
+            reqs.append(Requirement(NODEPOOL, "In", sorted(set(rng.choice(pools, size=2).tolist()))))
+        elif v < 0.6:
+            reqs.append(Requirement(NODEPOOL, "Exists"))
+        pc.requirements = reqs
+    return cp
 
 
 def fuzz_consolidation(catalog, seed, n_nodes=40, n_pods=200, n_candidates=None, with_min=False, pending_frac=0.15,
-                       all_spot=False, supported=False, n_pools=3):
+                       all_spot=False, n_pools=3):
     """A consolidation pass over random state: fuzz_problem's classes / pools / existing nodes, NewScheduler node order
     (initialized first, then name), candidates with their bound pods, pending pods, candidate prices around their
     offering price (so REPLACE, price-filtered NONE and DELETE all occur)."""
     from kpsim import abi, synth
     prob = fuzz_problem(catalog, seed, n_pods=n_pods, n_classes=12, with_min=with_min, n_existing=n_nodes, n_pools=n_pools)
-    if supported:
-        drop_mutating_requirements(prob)
     rng = np.random.Generator(np.random.PCG64(seed + 7))
     E = len(prob.existing)
     init = (rng.random(E) < 0.9).astype(np.uint8)
@@ -276,7 +304,7 @@ def fuzz_topology_consolidation(catalog, seed, n_nodes=30, n_pods=160, n_bound=4
     """fuzz_consolidation over pods with topology terms (add_topology: zonal / hostname / capacity-type spread,
     anti-affinity, zonal affinity; hostname pod affinity turned into anti-affinity unless host_affinity) plus
     non-reschedulable pods bound to random nodes (cluster.bound)."""
-    cp = fuzz_consolidation(catalog, seed, n_nodes=n_nodes, n_pods=n_pods, all_spot=all_spot, supported=True)
+    cp = fuzz_consolidation(catalog, seed, n_nodes=n_nodes, n_pods=n_pods, all_spot=all_spot)
     rng = np.random.Generator(np.random.PCG64(seed + 123))
     prob = add_topology(rng, cp.cluster, p_term=0.4)
     for pc in prob.classes:
@@ -327,7 +355,7 @@ def fuzz_preference_consolidation(catalog, seed, n_nodes=30, n_pods=160, n_bound
     nodes (their selectors count), sometimes a PreferNoSchedule taint on a pool; best_effort: MIN_VALUES_POLICY=BestEffort
     with minValues on instance-family that a NodeClaim may not meet; zone_min: minValues on the zone label."""
     from kpsim import abi
-    cp = fuzz_consolidation(catalog, seed, n_nodes=n_nodes, n_pods=n_pods, all_spot=all_spot, supported=True,
+    cp = fuzz_consolidation(catalog, seed, n_nodes=n_nodes, n_pods=n_pods, all_spot=all_spot,
                             with_min=best_effort)
     rng = np.random.Generator(np.random.PCG64(seed + 321))
     prob = add_preferences(rng, cp.cluster)

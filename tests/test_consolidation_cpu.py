@@ -204,27 +204,41 @@ def _rank_main(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         out = []
-        for seed in (3, 4):
+        for seed in SHARD_SEEDS:
             cp = _fuzz_cp(seed)
             fn = lambda c, m, b0, b1: pyoracle.consolidate(c, m, b0, b1)  # noqa: E731
             for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
-                cmd = consolidation.compute_command(cp, mode, fn, group=dist.group.WORLD)
-                out.append((cmd.decision, tuple(cmd.candidates), cmd.n_replacement_types))
+                cmd = consolidation.compute_command(cp, mode, fn, group=dist.group.WORLD,
+                                                    replacement_fn=pyoracle.consolidate_replacement)
+                out.append(_cmd_fields(cmd))
         q.put((rank, out))
     finally:
         dist.destroy_process_group()
 
 
+SHARD_SEEDS = (3, 4, 8, 11)
+
+
+def _cmd_fields(cmd):
+    return (cmd.decision, tuple(cmd.candidates), cmd.n_replacement_types, cmd.candidate_price, cmd.replacement_price,
+            cmd.mode, cmd.probe, cmd.nodepool, tuple(cmd.type_ids), cmd.requirements, cmd.n_reserved)
+
+
 def test_sharded_command_equals_single_rank_gloo():
+    """compute_command over a world-size-2 gloo group (probes sharded, one all_gather, the replacement read back on every
+    rank) returns the whole Command — delete set, prices, the replacement's NodePool, price-ordered type ids,
+    requirements and held reservations — equal to the single-process command (orc_consolidate_command)."""
     import multiprocessing as mp
     import socket
     want = []
-    for seed in (3, 4):
+    n_replace = 0
+    for seed in SHARD_SEEDS:
         cp = _fuzz_cp(seed)
-        fn = lambda c, m, b0, b1: pyoracle.consolidate(c, m, b0, b1)  # noqa: E731
         for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
-            cmd = consolidation.compute_command(cp, mode, fn)
-            want.append((cmd.decision, tuple(cmd.candidates), cmd.n_replacement_types))
+            cmd = pyoracle.consolidate_command(cp, mode)
+            want.append(_cmd_fields(cmd))
+            n_replace += cmd.decision == abi.KP_DECISION_REPLACE and len(cmd.type_ids) > 0
+    assert n_replace >= 1
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]

@@ -44,10 +44,53 @@ def test_fuzz_consolidation(ctx, golden, seed):
     rng = np.random.Generator(np.random.PCG64(500 + seed))
     sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 300)), replace=False))]
     cp = fuzzgen.fuzz_consolidation(sub, 500 + seed, n_nodes=int(rng.integers(4, 80)),
-                                    n_pods=int(rng.integers(20, 300)), all_spot=seed % 4 == 0, supported=True)
+                                    n_pods=int(rng.integers(20, 300)), all_spot=seed % 4 == 0)
     for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
         s2s = seed % 2 == 0
         assert_probes_equal(device_probes(ctx, cp, mode, s2s), pyoracle.consolidate(cp, mode, spot_to_spot=s2s))
+
+
+@pytest.mark.parametrize("seed", range(20))
+def test_fuzz_consolidation_mutating(ctx, golden, seed):
+    """ExistingNode.Add's requirement merge changes nodes (the MUT probes): the GPU-avoidance pattern (instance-gpu-count
+    DoesNotExist / NotIn pods next to Gt 0 / Exists pods; non-GPU nodes lack the label) and the mixed node-group pattern
+    (karpenter.sh/nodepool DoesNotExist pods; managed-node-group nodes lack the label) over fuzzed clusters, plus the
+    fuzz generator's own NotIn / DoesNotExist custom-label and hostname requirements.  Probes of both modes and the
+    command against the oracle, and the pass really ran MUT probes."""
+    rng = np.random.Generator(np.random.PCG64(6100 + seed))
+    gpus = [it for it in golden if it.labels.get(fuzzgen.GPU_COUNT) not in (None, [], "")]
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 250)), replace=False))]
+    sub += [g for g in gpus[::max(1, len(gpus) // 12)] if g not in sub]
+    cp = fuzzgen.fuzz_consolidation(sub, 6100 + seed, n_nodes=int(rng.integers(6, 70)),
+                                    n_pods=int(rng.integers(30, 260)), all_spot=seed % 4 == 0,
+                                    with_min=seed % 5 == 3)
+    fuzzgen.add_mutators(rng, cp, gpus)
+    s2s = seed % 2 == 0
+    n_mut = 0
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        assert_probes_equal(device_probes(ctx, cp, mode, s2s), pyoracle.consolidate(cp, mode, spot_to_spot=s2s))
+        n_mut += ctx.consolidate_stats()[1][17]  # probes the MUT variant ran
+    assert n_mut > 0
+    assert_commands_equal(device_command(ctx, cp, abi.KP_CONSOLIDATE_BOTH, s2s),
+                          pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH, spot_to_spot=s2s))
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_fuzz_consolidation_mutating_topology(ctx, golden, seed):
+    """The mutating shapes over topology-constrained clusters (per-probe domain counts, ExistingNode.Add's topology step
+    on the probes' node copies) and over preferences that relax into them."""
+    rng = np.random.Generator(np.random.PCG64(6300 + seed))
+    gpus = [it for it in golden if it.labels.get(fuzzgen.GPU_COUNT) not in (None, [], "")]
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 250)), replace=False))]
+    sub += [g for g in gpus[::max(1, len(gpus) // 12)] if g not in sub]
+    cp = fuzzgen.fuzz_topology_consolidation(sub, 6300 + seed, n_nodes=int(rng.integers(6, 50)),
+                                             n_pods=int(rng.integers(30, 200)), all_spot=seed % 4 == 0)
+    fuzzgen.add_mutators(rng, cp, gpus)
+    s2s = seed % 2 == 1
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        assert_probes_equal(device_probes(ctx, cp, mode, s2s), pyoracle.consolidate(cp, mode, spot_to_spot=s2s))
+    assert_commands_equal(device_command(ctx, cp, abi.KP_CONSOLIDATE_BOTH, s2s),
+                          pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH, spot_to_spot=s2s))
 
 
 @pytest.mark.parametrize("seed", range(16))
@@ -58,7 +101,7 @@ def test_fuzz_consolidation_min_values(ctx, golden, seed):
     rng = np.random.Generator(np.random.PCG64(900 + seed))
     sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 300)), replace=False))]
     cp = fuzzgen.fuzz_consolidation(sub, 900 + seed, n_nodes=int(rng.integers(4, 80)),
-                                    n_pods=int(rng.integers(20, 300)), all_spot=seed % 3 == 0, supported=True,
+                                    n_pods=int(rng.integers(20, 300)), all_spot=seed % 3 == 0,
                                     with_min=True)
     for np_ in cp.cluster.nodepools:  # minValues on every pool, sometimes beyond what a truncated list can hold
         if not any(r.min_values for r in np_.requirements):
@@ -70,7 +113,7 @@ def test_fuzz_consolidation_min_values(ctx, golden, seed):
 
 
 def test_shard_ranges_concatenate(ctx, golden):
-    cp = fuzzgen.fuzz_consolidation(golden[:200], 77, n_nodes=60, n_pods=250, n_candidates=40, supported=True)
+    cp = fuzzgen.fuzz_consolidation(golden[:200], 77, n_nodes=60, n_pods=250, n_candidates=40)
     for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
         full = device_probes(ctx, cp, mode)
         n = len(full)
@@ -176,7 +219,7 @@ def _reserved_consolidation(golden, seed, full_cluster=False):
     sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(80, 240)), replace=False))]
     cat = synth.config5_catalog(sub, n_default=min(44, len(sub) // 2), n_block=min(20, len(sub) // 6), seed=1300 + seed)
     cp = fuzzgen.fuzz_consolidation(cat, 1300 + seed, n_nodes=int(rng.integers(4, 60)),
-                                    n_pods=int(rng.integers(20, 250)), all_spot=seed % 4 == 0, supported=True,
+                                    n_pods=int(rng.integers(20, 250)), all_spot=seed % 4 == 0,
                                     pending_frac=0.0 if full_cluster else 0.15)
     for np_ in cp.cluster.nodepools:
         for r in np_.requirements:
@@ -244,8 +287,7 @@ def test_both_modes_one_pass(ctx, golden, seed):
     mode's pass (and shards of the combined list concatenate to it)."""
     rng = np.random.Generator(np.random.PCG64(700 + seed))
     sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 300)), replace=False))]
-    cp = fuzzgen.fuzz_consolidation(sub, 700 + seed, n_nodes=int(rng.integers(4, 80)), n_pods=int(rng.integers(20, 300)),
-                                    supported=True)
+    cp = fuzzgen.fuzz_consolidation(sub, 700 + seed, n_nodes=int(rng.integers(4, 80)), n_pods=int(rng.integers(20, 300)))
     ctx.upload_catalog(model.CatalogView(cp.cluster.catalog))
     ctx.consolidate_prepare(model.ConsolidateInputView(cp, abi.KP_CONSOLIDATE_SINGLE))
     nc = len(cp.candidates)
@@ -286,7 +328,7 @@ def _command_cases(golden):
         rng = np.random.Generator(np.random.PCG64(2500 + seed))
         sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 300)), replace=False))]
         cp = fuzzgen.fuzz_consolidation(sub, 2500 + seed, n_nodes=int(rng.integers(4, 60)),
-                                        n_pods=int(rng.integers(20, 250)), all_spot=seed % 4 == 0, supported=True,
+                                        n_pods=int(rng.integers(20, 250)), all_spot=seed % 4 == 0,
                                         with_min=seed % 3 == 0)
         out.append((cp, seed % 2 == 0))
     for seed in range(8):
@@ -305,6 +347,58 @@ def test_command_parity(ctx, golden):
             assert_commands_equal(dev, pyoracle.consolidate_command(cp, mode, spot_to_spot=s2s))
             n_replace += dev.decision == abi.KP_DECISION_REPLACE and len(dev.type_ids) > 1
     assert n_replace >= 4
+
+
+def test_command_costs_one_pass(ctx, golden):
+    """kp_consolidate_command after kp_consolidate_execute of the same prepared pass replays that pass (no probe launch)
+    and reads the replacement back once; a KP_E_BUFFER retry and a repeated call copy it; a BOTH pass serves a SINGLE or
+    MULTI command; a new prepare starts over (kp_consolidate_stats counters 18-19: passes launched, read-backs run)."""
+    n_seen = 0
+    for cp, s2s in _command_cases(golden):
+        ctx.upload_catalog(model.CatalogView(cp.cluster.catalog))
+        ctx.consolidate_prepare(model.ConsolidateInputView(cp, abi.KP_CONSOLIDATE_SINGLE, spot_to_spot=s2s))
+        nc = len(cp.candidates)
+        n = model.consolidation_probe_count(nc, abi.KP_CONSOLIDATE_SINGLE) + \
+            model.consolidation_probe_count(nc, abi.KP_CONSOLIDATE_MULTI)
+        ctx.consolidate_execute(abi.KP_CONSOLIDATE_BOTH, n)
+        want = pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH, spot_to_spot=s2s)
+        rb = 1 if want.decision == abi.KP_DECISION_REPLACE else 0
+        tiny = consolidation.command_call(
+            lambda cc: ctx.L.kp_consolidate_command(ctx.h, abi.KP_CONSOLIDATE_BOTH, __import__("ctypes").byref(cc)),
+            cap_types=1, cap_req=4)[1]  # first try KP_E_BUFFER for a REPLACE, then the grown buffers
+        cmd = ctx.consolidate_command(abi.KP_CONSOLIDATE_BOTH)
+        assert_commands_equal(tiny, want)
+        assert_commands_equal(cmd, want)
+        ct = ctx.consolidate_stats()[1]
+        assert (ct[18], ct[19]) == (1, rb), (ct[18], ct[19])
+        single = pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_SINGLE, spot_to_spot=s2s)
+        assert_commands_equal(ctx.consolidate_command(abi.KP_CONSOLIDATE_SINGLE), single)
+        assert ctx.consolidate_stats()[1][18] == 1  # served by the BOTH pass
+        # a fresh prepare: the command runs its own pass
+        ctx.consolidate_prepare(model.ConsolidateInputView(cp, abi.KP_CONSOLIDATE_SINGLE, spot_to_spot=s2s))
+        assert_commands_equal(ctx.consolidate_command(abi.KP_CONSOLIDATE_BOTH), want)
+        ct = ctx.consolidate_stats()[1]
+        assert (ct[18], ct[19]) == (1, rb)
+        n_seen += rb
+    assert n_seen >= 2
+
+
+def test_consolidator_command_has_replacement(golden):
+    """kpsim.consolidation.Consolidator.compute_command (the per-process path; with a torch.distributed group each rank
+    evaluates a shard) returns the whole Command, the replacement NodeClaim included (kp_consolidate_replacement), equal
+    to the oracle's command of that method."""
+    from kpsim import native
+    n_rep = 0
+    for cp, s2s in _command_cases(golden):
+        con = consolidation.Consolidator(cp.cluster.catalog, ctx=native.Context(0), spot_to_spot=s2s)
+        try:
+            for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+                got = con.compute_command(cp, mode)
+                assert_commands_equal(got, pyoracle.consolidate_command(cp, mode, spot_to_spot=s2s))
+                n_rep += got.decision == abi.KP_DECISION_REPLACE
+        finally:
+            con.ctx.close()
+    assert n_rep >= 2
 
 
 @pytest.mark.parametrize("name", ["reserved_into", "reserved_between"])
@@ -517,7 +611,7 @@ def test_consolidation_many_nodepools(ctx, golden, seed):
     """40-60 NodePools: candidates' capacity back into their own pool's limits, replacements from any pool."""
     rng = np.random.Generator(np.random.PCG64(5300 + seed))
     sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=200, replace=False))]
-    cp = fuzzgen.fuzz_consolidation(sub, 5300 + seed, n_nodes=40, n_pods=200, supported=True,
+    cp = fuzzgen.fuzz_consolidation(sub, 5300 + seed, n_nodes=40, n_pods=200,
                                     n_pools=int(rng.integers(40, 61)))
     for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
         assert_probes_equal(device_probes(ctx, cp, mode), pyoracle.consolidate(cp, mode))
@@ -531,7 +625,7 @@ def test_consolidation_wide_axes(ctx, golden, seed):
     rng = np.random.Generator(np.random.PCG64(5500 + seed))
     sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(100, 300)), replace=False))]
     cp = fuzzgen.fuzz_consolidation(sub, 5500 + seed, n_nodes=int(rng.integers(10, 80)),
-                                    n_pods=int(rng.integers(50, 300)), supported=True, all_spot=seed % 4 == 0)
+                                    n_pods=int(rng.integers(50, 300)), all_spot=seed % 4 == 0)
     fuzzgen.add_extra_resources(rng, cp.cluster)
     active = (cp.cluster.pods.requests != 0).any(0).sum()
     assert active > 6, active
@@ -545,6 +639,6 @@ def test_consolidation_wide_catalog(ctx, golden):
     """Probes over a 1,300-type catalog (32 option words; OrderByPrice / Truncate over the wider option set)."""
     cat = synth.widen_catalog(golden, 1300)
     for seed in range(2):
-        cp = fuzzgen.fuzz_consolidation(cat, 5700 + seed, n_nodes=40, n_pods=200, supported=True, all_spot=seed == 1)
+        cp = fuzzgen.fuzz_consolidation(cat, 5700 + seed, n_nodes=40, n_pods=200, all_spot=seed == 1)
         for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
             assert_probes_equal(device_probes(ctx, cp, mode), pyoracle.consolidate(cp, mode))

@@ -208,6 +208,26 @@ def test_node_dense_20k_one_execute(golden):
         c.close()
 
 
+def test_scheduler_solve_grows_output_buffers(golden):
+    """kpsim.scheduler.Scheduler.Solve (the reference-shaped entry point) over the 10k node-dense Deployment: its first
+    output buffers hold 8,192 NodeClaims; kp_solve reports KP_E_BUFFER with the sizes and the scheduler re-fetches the
+    executed solve into buffers of that size (one execute).  The raw result equals the oracle's committed digest."""
+    from kpsim import native, scheduler
+    with open(os.path.join(os.path.dirname(__file__), "golden", "scale_digests.json")) as f:
+        want = json.load(f)["node_dense_10k"]
+    prob = TC.node_dense(golden, want["n_pods"])
+    c = native.Context(0)
+    try:
+        s = scheduler.Scheduler(prob.catalog, ctx=c)
+        res = s.Solve(prob)
+        assert len(res.new_nodeclaims) == 10_000 and not res.pod_errors
+        assert all(len(nc.pods) == 1 for nc in res.new_nodeclaims)
+        reqs = [model.parse_requirements_blob(c.nodeclaim_requirements(i)) for i in range(res.raw.n_nodeclaims)]
+        assert parity.result_digest((res.raw, reqs)) == {k: v for k, v in want.items() if k != "n_pods"}
+    finally:
+        c.close()
+
+
 def test_node_dense_does_not_stick_to_ctx(golden):
     """A node-dense solve does not leave its large plan on the ctx: a config-2 solve after it on the same
     ctx takes the same quick-accept path (counters) and result as on a fresh ctx."""
