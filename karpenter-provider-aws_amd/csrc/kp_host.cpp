@@ -553,6 +553,8 @@ struct kp_ctx {
     DBuf<int4> d_tg_info;
     DBuf<int32_t> d_tg_hrow, d_tg_owner, d_tg_pol, d_tg_cnt0, d_tg_cnt, d_tg_hcnt0, d_tg_hcnt, d_tg_pos0, d_tg_pos,
         d_cls_tcoff, d_cls_tc, d_cls_troff, d_cls_tr;
+    DBuf<KpTopoCons> d_cls_tce;
+    DBuf<KpTopoRec> d_cls_tre;
     DBuf<uint64_t> d_tg_known0, d_tg_known;
     DBuf<uint8_t> d_cls_kneutral, d_vrank;
     // consolidation over topology (kp_consolidate_prepare sets cons_extra before kp_solve_prepare): the candidates'
@@ -2035,6 +2037,8 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         std::vector<int32_t> thr_row(G1, -1), towner(G1, 0), tpol(G1, 0), tcnt0((size_t)G1 * 64, 0), tpos0(G1, 0);
         std::vector<uint64_t> tknown0(G1, 0);
         std::vector<int32_t> tcoff(C + 1, 0), tcl, troff(C + 1, 0), trl;
+        std::vector<KpTopoCons> tce;
+        std::vector<KpTopoRec> tre;
         std::vector<uint8_t> vrank((size_t)K * 64, 0xFF);
         // hostname rows: existing nodes, then NodeClaim ids 0 .. NCcap, the last a spare that stays 0 (a template
         // evaluation for a NodeClaim at capacity reads it; the capacity check then reports the overflow)
@@ -2112,6 +2116,50 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
                 for (int e : th.rec[i]) trl.push_back(e);
                 tcoff[i + 1] = (int)tcl.size();
                 troff[i + 1] = (int)trl.size();
+            }
+            // the entries' static operands (KpTopoCons / KpTopoRec): req_has over the encoded class digest, as the device
+            // evaluates it
+            auto digest_has = [&](int row, int k, int v) {
+                const ReqHdr& h = chdr[(size_t)row * K + k];
+                const bool bit = (cwords[(size_t)row * DW + woff[k] + v / 64] >> (v % 64)) & 1ull;
+                bool within = true;
+                if (h.flags & (RF_GT | RF_LT)) {
+                    const int b = vbase[k] + v;
+                    within = isint[b] && !((h.flags & RF_GT) && h.gt >= ival[b]) && !((h.flags & RF_LT) && h.lt <= ival[b]);
+                }
+                return (h.flags & RF_CMP) ? (!bit && within) : (bit && within);
+            };
+            for (int i = 0; i < C; i++) {
+                for (int e : th.cons[i]) {
+                    const int gi = e & 0x3FFFFFFF, self = (e >> 30) & 1;
+                    const HGroup& g = th.g[gi];
+                    KpTopoCons t{};
+                    t.g = gi;
+                    t.flags = g.type | (self << 2) | (g.host ? 8 : 0);
+                    t.skew = g.skew;
+                    t.mindom = g.mindom;
+                    if (g.host) {
+                        t.key = -1 - g.hrow;
+                    } else {
+                        t.key = g.key;
+                        for (int v = 0; v < 64 && v < nval[g.key]; v++) {
+                            t.vmask |= 1ull << v;
+                            if (digest_has(i, g.key, v)) t.podhas |= 1ull << v;
+                        }
+                    }
+                    tce.push_back(t);
+                }
+                for (int gi : th.rec[i]) {
+                    const HGroup& g = th.g[gi];
+                    KpTopoRec r{};
+                    r.g = gi;
+                    r.flags = g.type | (g.inverse ? 4 : 0) | (g.host ? 8 : 0);
+                    r.key = g.host ? -1 - g.hrow : g.key;
+                    if (!g.inverse && g.type == KP_TOPO_SPREAD && (g.pol & 2))
+                        for (int j = 0; j < NT; j++)
+                            if (!((tol[g.owner] >> j) & 1ull)) r.skip |= 1ull << j;
+                    tre.push_back(r);
+                }
             }
             // countDomains over the pods bound to existing nodes (forward groups that select the pod's class; a spread
             // group's node filter against the node's labels and taints) and updateInverseAffinities (the inverse
@@ -2192,6 +2240,10 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         }
         if (tcl.empty()) tcl.push_back(0);
         if (trl.empty()) trl.push_back(0);
+        if (tce.empty()) tce.push_back(KpTopoCons{});
+        if (tre.empty()) tre.push_back(KpTopoRec{});
+        HIPCHK(c->d_cls_tce.upload(tce, s));
+        HIPCHK(c->d_cls_tre.upload(tre, s));
         HIPCHK(c->d_tg_info.upload(tinfo, s));
         HIPCHK(c->d_tg_hrow.upload(thr_row, s));
         HIPCHK(c->d_tg_owner.upload(towner, s));
@@ -2350,6 +2402,8 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.cls_tc = c->d_cls_tc.p;
     d.cls_troff = c->d_cls_troff.p;
     d.cls_tr = c->d_cls_tr.p;
+    d.cls_tce = c->d_cls_tce.p;
+    d.cls_tre = c->d_cls_tre.p;
     d.cls_kneutral = c->d_cls_kneutral.p;
     d.vrank = c->d_vrank.p;
     // quick-accept headroom scale per active axis: every allocatable value >> qshift fits in 30 bits
@@ -2553,6 +2607,12 @@ extern "C" kp_status kp_solve_fetch(kp_ctx* ctx, kp_solve_output* out) {
                         "absorbed %lld, quick row %lld (witness fits %lld, merge no-op %lld); NQ %d of %d NodeClaims\n",
                 (long long)st[ST_TQ_WHY], (long long)st[ST_TQ_WHY + 1], (long long)st[ST_TQ_WHY + 2], (long long)st[ST_TQ_WHY + 3],
                 (long long)st[ST_TQ_WHY + 4], (long long)st[ST_TQ_WHY + 5], (long long)st[ST_TQ_WHY + 6], c->dev.lds_nq, N);
+    if (getenv("KPSIM_PROFILE") && st[ST_SEG])
+        fprintf(stderr, "[kpsim] solve loop segments (cycles): fast loop + slow-path entry %lld, topology section %lld "
+                        "(topology quick accepts: %lld iterations, %lld cycles from the slow-path entry), class cache %lld, "
+                        "evaluations %lld, commit / templates / slice move %lld\n",
+                (long long)st[ST_SEG], (long long)st[ST_SEG + 1], (long long)st[ST_TQ_ITERS], (long long)st[ST_TQ_CYC],
+                (long long)st[ST_SEG + 2], (long long)st[ST_SEG + 3], (long long)st[ST_SEG + 4]);
     so.ns_host_prep = c->ns_prep;
     so.ns_device_solve = c->ns_exec;
     if (N > out->cap_nodeclaims || n_ids > out->cap_type_ids) return fail(ctx, KP_E_BUFFER, "output buffers too small");

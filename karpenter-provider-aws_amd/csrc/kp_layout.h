@@ -90,6 +90,22 @@ struct ResvTab {
     uint64_t avail;                  // bit i: Offering.Available
 };
 
+// Static operands of one (class, constraining topology group) entry, so the FFD kernel's per-pod prefilter setup reads
+// one row instead of walking cls_tc → tg_info → the class digest: flags = type | self << 2 | hostname << 3; key = the
+// group's key, or -1 - its row of tg_hcnt for a hostname group; podhas = the class's domains of the key (value ids < 64
+// its requirement admits), vmask = the key's dictionary (value ids < nval).
+struct KpTopoCons {
+    int32_t g, key, flags, skew, mindom, pad;
+    uint64_t podhas, vmask;
+};
+// ... of one (class, recording topology group) entry: flags = type | inverse << 2 | hostname << 3; key as above;
+// skip = the templates on which TopologyNodeFilter's taint policy leaves the placement uncounted (a spread group with
+// nodeTaintsPolicy Honor whose owner does not tolerate the template).
+struct KpTopoRec {
+    int32_t g, key, flags, pad;
+    uint64_t skip;
+};
+
 // Device pointers and sizes for one solve (catalog tables + solve tables + state + outputs).
 struct KpDev {
     // ---------------- catalog (uploaded once per epoch) ----------------
@@ -233,6 +249,8 @@ struct KpDev {
     const int32_t* cls_tr;
     const uint8_t* cls_kneutral;     // parallel to cls_keys: 1 = key added only so topology can narrow it
     const uint8_t* vrank;            // [K][64] rank of value id v among the key's values by name (tie-break)
+    const struct KpTopoCons* cls_tce; // parallel to cls_tc: the entry's static operands (FFD kernel prefilter setup)
+    const struct KpTopoRec* cls_tre;  // parallel to cls_tr: the entry's static operands (topology quick accept's Record)
 
     // ---------------- FFD kernel LDS plan (kp_ffd_plan_lds) ----------------
     // Dynamic LDS after the fixed FfdShared block: slice arrays sized by lds_ncmax, the staged type tables
@@ -279,5 +297,10 @@ enum {
     ST_REJ_REQ = 48, ST_REJ_TOPO, ST_REJ_TYPES, ST_REJ_MIN,
     // KPSIM_PROFILE: topology pods past the prefilter — no surviving NodeClaim, class records through another class's
     // node filter (not QREC), NodeClaim without a quick row, class not absorbed, quick row present; witness fits
-    ST_TQ_WHY = 52, ST_SLOW_WHY = 59, ST_COUNT = 70
+    ST_TQ_WHY = 52, ST_SLOW_WHY = 59,
+    // KPSIM_PROFILE: one outer iteration of the solve loop cut into segments (thread 0's clock): the fast loop and the
+    // barrier that opens the slow path; the topology section (existing nodes, prefilter, scan, topology quick accept);
+    // the class cache fill; the candidate evaluations; commit / templates / slice move / closing barrier; then the
+    // iterations that end in a topology quick accept (count, cycles from the slow path's start to their end)
+    ST_SEG = 70, ST_TQ_ITERS = 75, ST_TQ_CYC = 76, ST_COUNT = 80
 };
