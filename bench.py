@@ -283,6 +283,16 @@ def launch_leg(a, golden, local, rank, world, dist, barrier):
     return out
 
 
+def ffd_kernel_name(prob):
+    """The Solve kernel instantiation a problem launches (kp_launch_ffd): topology groups → ffd_topo_kernel, reserved
+    offerings → ffd_resv_kernel, both → ffd_resv_topo_kernel (preference relaxation adds _pref)."""
+    topo = any(pc.topology for pc in prob.classes)
+    resv = any(o.capacity_type == "reserved" for it in prob.catalog for o in it.offerings)
+    pref = any(pc.preferred_terms or len(pc.required_terms) > 1 or
+               any(t.when_unsatisfiable == "ScheduleAnyway" or t.weight for t in pc.topology) for pc in prob.classes)
+    return "ffd_" + ("pref_" if pref else "") + ("resv_" if resv else "") + ("topo_" if topo else "") + "kernel"
+
+
 def solve_leg(a, cat, prob, metric, workload, cpu_sample, local, rank, world, dist, barrier):
     """A further Solve workload, same step as the headline leg: one kp_solve_execute with HBM-resident inputs; replicas
     across ranks (weak scaling, no collective); CPU baseline on a seeded subsample, with device parity on it."""
@@ -330,7 +340,7 @@ def solve_leg(a, cat, prob, metric, workload, cpu_sample, local, rank, world, di
         "end_to_end_ms": e2e_ms,
         "nodeclaims": res.n_nodeclaims,
         "unschedulable": int((res.pod_result == -1).sum()),
-        "roofline": {"bound": "hbm", "kernel": "ffd_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "roofline": {"bound": "hbm", "kernel": ffd_kernel_name(prob), "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes": int(B), "kernel_ms": float(kt[3])},
         "solve_stats": {k: v for k, v in res.stats.items() if not k.startswith("ns_")},
         "ffd_counters": dict(zip(FFD_COUNTERS, ctx.ffd_cycles())),

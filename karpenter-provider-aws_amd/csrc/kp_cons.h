@@ -109,6 +109,6 @@ struct KpCons {
     // dynamic LDS plan (kp_cons_plan_lds)
     int32_t n_store;            // chunks in the fast variant's LDS headroom store (kp_cons_plan_lds)
     int32_t off_hdr, off_words, off_rem, off_excl, off_mod, off_init, off_xtc, off_touch, off_hmod, off_cmax, off_hs, off_hpos;
-    int32_t off_mutn;
+    int32_t off_mutn, off_rcap;
     int32_t lds_bytes;
 };

@@ -32,7 +32,7 @@ struct ConsShared {
     Roles roles;
     int64_t nc_req[KP_MAX_R];
     int64_t st[CS_COUNT];
-    int32_t rcap[64];  // RESV: the probe's ReservationManager capacities (NewReservationManager per SimulateScheduling)
+    uint64_t mro[KP_RO_W];  // RESV: the reserved-offering rows compatible with the probe's NodeClaim (its finalisation)
 };
 
 __device__ __forceinline__ int32_t ld32(const int32_t* p) {
@@ -46,6 +46,10 @@ __device__ __forceinline__ uint64_t ld64u(const uint64_t* p) {
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32)) << 32) |
            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+}
+__device__ __forceinline__ int wave_sum_i32(int x) {
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+    return x;
 }
 __device__ __forceinline__ double wave_min_f64(double x) {
     for (int o = 32; o >= 1; o >>= 1) {
@@ -76,13 +80,13 @@ __device__ inline uint64_t limit_filter_rem(const KpDev& d, int j, uint64_t o, c
     return out;
 }
 
-// Offerings.Available().WorstLaunchPrice(reqs) over the admissible slots m and reserved offerings rm (ResvTab rows) of
-// type t: reserved, then spot, then on-demand; the most expensive offering of the first capacity type present.
-__device__ inline double worst_launch_price(const KpDev& d, const KpCons& k, int t, uint64_t m, uint64_t rm = 0) {
+// Offerings.Available().WorstLaunchPrice(reqs) over the admissible slots m and reserved offerings rm (bits of ResvTab
+// word rw) of type t: reserved, then spot, then on-demand; the most expensive offering of the first capacity type present.
+__device__ inline double worst_launch_price(const KpDev& d, const KpCons& k, int t, uint64_t m, uint64_t rm = 0, int rw = 0) {
     if (rm) {
         double mx = 0.0;
         for (uint64_t x = rm; x; x &= x - 1) {
-            const double p = d.ro_price[__ffsll((unsigned long long)x) - 1];
+            const double p = d.ro_price[rw * 64 + __ffsll((unsigned long long)x) - 1];
             mx = p > mx ? p : mx;
         }
         return mx;
@@ -172,14 +176,14 @@ __device__ inline void commit_min_relax_lds(ReqHdr* nch, const WaveScratch& ws, 
 
 }  // namespace
 
-// NodeClaim.Add's commit of offeringsToReserve (fallback mode): newly held IDs take one unit of capacity, IDs no longer
-// held are released (ReservationManager.Reserve / Release).  Returns the new held set.
-__device__ inline uint64_t commit_held(int32_t* rcap, uint64_t old, uint64_t nw, int lane) {
-    if (lane < 64) {
-        const uint64_t b = 1ull << lane;
-        if ((nw & b) && !(old & b)) rcap[lane]--;
-        if ((old & b) && !(nw & b)) rcap[lane]++;
-    }
+// NodeClaim.Add's commit of offeringsToReserve (fallback mode): newly held reservations take one unit of capacity,
+// those no longer held are released (ReservationManager.Reserve / Release).  Lane r: word r of the held set (old), the
+// Add's set in ws.minbits; returns the new word.
+__device__ inline uint64_t commit_held(int32_t* rcap, uint64_t old, const WaveScratch& ws, int ridw, int lane) {
+    if (lane >= ridw) return 0ull;
+    const uint64_t nw = ws.minbits[lane];
+    for (uint64_t x = nw & ~old; x; x &= x - 1) rcap[lane * 64 + __ffsll((unsigned long long)x) - 1]--;
+    for (uint64_t x = old & ~nw; x; x &= x - 1) rcap[lane * 64 + __ffsll((unsigned long long)x) - 1]++;
     return nw;
 }
 
@@ -269,7 +273,8 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
     }
     Ev.ro = RESV ? d.ro : nullptr;
     Ev.type_ro = RESV ? d.type_ro : nullptr;
-    Ev.rcap = RESV ? S.rcap : nullptr;
+    int32_t* const rcap = RESV ? reinterpret_cast<int32_t*>(smem + k.off_rcap) : nullptr;  // [nrid]
+    Ev.rcap = rcap;
     Ev.resv_on = RESV ? d.resv_on : 0;  // disruption simulations: ReservedOfferingModeFallback (STRICT = false below)
     Ev.pt = TOPO ? &P : nullptr;
     Ev.snap = nullptr;
@@ -326,7 +331,8 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
         for (int i = lane; i < NT * R; i += 64) rem[i] = d.remaining[i];
         if (k.use_cmax)
             for (int i = lane; i < EW * KP_LDS_AXES; i += 64) cmax[i] = k.cmax0[i];
-        if (RESV) S.rcap[lane] = d.rcap0[lane];
+        if (RESV)
+            for (int i = lane; i < d.ro_nrid; i += 64) rcap[i] = d.rcap0[i];
         __syncthreads();
         for (int c = c0 + lane; c < c1; c += 64) {
             const int node = k.cand_i[c * 4 + 0];
@@ -490,7 +496,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
         for (int ai = 0; ai < KP_LDS_AXES; ai++) ch[ai] = cd[ai] = 0;
         bool bad = false, stop = false;
         uint64_t nc_opts = 0;
-        uint64_t nc_held = 0;  // RESV: reservation IDs the in-flight NodeClaim holds
+        uint64_t nc_held = 0;  // RESV: lane r: word r of the reservations the in-flight NodeClaim holds
         // Largest headroom of the cached chunk's nodes that are not candidates (lanes past E hold 0): the chunk's entry
         // of the headroom summary when the chunk leaves the registers.
         auto chunk_max = [&](int base, const int64_t (&h)[KP_LDS_AXES], int ai) -> int64_t {
@@ -1060,7 +1066,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
                     }
                     if (lane < TW) nc_opts = S.ws.opts[lane];
                     if (lane < R) S.nc_req[lane] += preq[lane];
-                    if (RESV && d.resv_on) nc_held = commit_held(S.rcap, nc_held, S.ws.held, lane);
+                    if (RESV && d.resv_on) nc_held = commit_held(rcap, nc_held, S.ws, d.ro_ridw, lane);
                     __syncthreads();
                     if (d.best_effort) commit_min_relax_lds(nch, S.ws, lane);
                     if (TOPO && (cflags & CF_TOPO)) topo_record<true>(d, S.CC, S.ws, nch, ncw, E, nc_tmpl, true, lane, -1, &P);
@@ -1103,7 +1109,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
                     }
                     nc_opts = lane < TW ? S.ws.opts[lane] : 0;
                     if (lane < R) S.nc_req[lane] = d.daemon[(size_t)j * R + lane] + preq[lane];
-                    if (RESV && d.resv_on) nc_held = commit_held(S.rcap, 0ull, S.ws.held, lane);
+                    if (RESV && d.resv_on) nc_held = commit_held(rcap, 0ull, S.ws, d.ro_ridw, lane);
                     // subtractMax(remaining, nodeClaim.InstanceTypeOptions)
                     for (int r = 0; r < R; r++) {
                         if (!d.limit_set[(size_t)j * R + r]) continue;
@@ -1191,13 +1197,18 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
             valid = 1;
         } else if (FULL && all) {
             // FinalizeScheduling: a NodeClaim holding reservations gets reservation-id In [held IDs]
-            if (RESV && nc_held && d.key_resvid >= 0) {
+            if (RESV && ballot(nc_held != 0) && d.key_resvid >= 0) {
                 if (lane == 0) {
                     ReqHdr h{};
                     h.flags = RF_DEF;
                     nch[d.key_resvid] = h;
                 }
-                for (int i = lane; i < d.nw[d.key_resvid]; i += 64) ncw[d.woff[d.key_resvid] + i] = i == 0 ? nc_held : 0ull;
+                for (int i = lane; i < d.nw[d.key_resvid]; i += 64) ncw[d.woff[d.key_resvid] + i] = 0ull;
+                __syncthreads();
+                for (uint64_t x = lane < d.ro_ridw ? nc_held : 0ull; x; x &= x - 1) {  // the held IDs' value bits
+                    const int v = d.ro->rid_vid[lane * 64 + __ffsll((unsigned long long)x) - 1];
+                    atomicOr((unsigned long long*)&ncw[d.woff[d.key_resvid] + (v >> 6)], 1ull << (v & 63));
+                }
                 __syncthreads();
             }
             // Offerings.Available().Compatible(NodeClaim requirements) over zone × capacity-type slots
@@ -1220,18 +1231,19 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
                          dneok(d.key_resvtype);
             }
             const uint64_t mzc = ballot(okslot);
-            // ... and over the reserved offerings (capacity-type In [reserved], zone, zone-id, reservation id / type)
-            uint64_t mro = 0;
-            if (RESV) {
+            // ... and over the reserved offerings (capacity-type In [reserved], zone, zone-id, reservation id / type), 64
+            // rows per step into S.mro
+            for (int q = 0; RESV && q < d.ro_w; q++) {
+                const int ri = q * 64 + lane;
                 bool ok = false;
-                if (lane < d.ro->n && ((d.ro->avail >> lane) & 1ull)) {
+                if (ri < d.ro_n && d.ro->type[ri] >= 0 && ((d.ro->avail[q] >> lane) & 1ull)) {
                     auto adm = [&](int kk, int v) -> bool {
                         if (kk < 0) return true;
                         const ReqHdr h = nch[kk];
                         if (!(h.flags & RF_DEF)) return true;
                         return req_has(d, kk, v, h, ncw + d.woff[kk]);
                     };
-                    const int zid = d.ro->zid[lane], rt = d.ro->rtype[lane];
+                    const int zid = d.ro->zid[ri], rt = d.ro->rtype[ri];
                     bool rtok;
                     if (rt >= 0) {
                         rtok = adm(d.key_resvtype, rt);
@@ -1241,11 +1253,13 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
                         rtok = kk < 0 || !(h.flags & RF_DEF) ||
                                op_notin_or_dne(req_op(h.flags, popc_words(ncw + d.woff[kk], d.nw[kk])));
                     }
-                    ok = adm(d.key_ct, d.ro->ctv) && adm(d.key_zone, d.ro->zone[lane]) && (zid < 0 || adm(d.key_zoneid, zid)) &&
-                         adm(d.key_resvid, d.ro->rid[lane]) && rtok;
+                    ok = adm(d.key_ct, d.ro->ctv) && adm(d.key_zone, d.ro->zone[ri]) && (zid < 0 || adm(d.key_zoneid, zid)) &&
+                         adm(d.key_resvid, d.ro->ridv[ri]) && rtok;
                 }
-                mro = ballot(ok);
+                const uint64_t m = ballot(ok);
+                if (lane == 0) S.mro[q] = m;
             }
+            if (RESV) __syncthreads();
             // OrderByPrice(reqs) + Truncate(M): select the M cheapest options by (price, name)
             double pr[KP_TW_MAX];
             uint32_t rk[KP_TW_MAX];
@@ -1268,11 +1282,13 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
                             const double sp = d.slot_price[(size_t)t * KP_MAX_SLOTS + s];
                             price = sp < price ? sp : price;
                         }
-                        if (RESV)
-                            for (uint64_t x = d.type_ro[t] & mro; x; x &= x - 1) {
-                                const double rp = d.ro_price[__ffsll((unsigned long long)x) - 1];
+                        if (RESV) {
+                            const uint32_t tr = d.type_ro[t];
+                            for (uint64_t x = tr ? S.mro[tr >> 16] & ro_span_bits(tr) : 0ull; x; x &= x - 1) {
+                                const double rp = d.ro_price[(tr >> 16) * 64 + __ffsll((unsigned long long)x) - 1];
                                 price = rp < price ? rp : price;
                             }
+                        }
                         pr[w] = price;
                         rk[w] = d.name_rank[t];
                         present |= 1u << w;
@@ -1326,7 +1342,10 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
             };
             const bool has_spot = ct_has(k.v_spot), has_od = ct_has(k.v_od);
             const uint64_t mt = my_t >= 0 ? d.avail_zc[my_t] & mzc : 0;
-            const uint64_t mr = (RESV && my_t >= 0) ? d.type_ro[my_t] & mro : 0ull;  // the option's reserved offerings
+            // the option's reserved offerings (bits of ResvTab word mrw)
+            const uint32_t mtr = (RESV && my_t >= 0) ? d.type_ro[my_t] : 0u;
+            const uint64_t mr = mtr ? S.mro[mtr >> 16] & ro_span_bits(mtr) : 0ull;
+            const int mrw = (int)(mtr >> 16);
             bool keep = false, none = false, spot_only = false;
             if (!trunc_ok) {
                 // the dropped NodeClaim's pods get errors: if one of them is not pending, not all non-pending pods
@@ -1353,7 +1372,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
                     }
                 }
             } else {  // RemoveInstanceTypeOptionsByPriceAndMinValues
-                keep = my_t >= 0 && worst_launch_price(d, k, my_t, mt, mr) < cprice;
+                keep = my_t >= 0 && worst_launch_price(d, k, my_t, mt, mr, mrw) < cprice;
                 const uint64_t km = ballot(keep);
                 if (!km || (has_min && !min_values_ok(d, nch, nc_tmpl, my_t, km, lane, nullptr))) none = true;
                 spot_only = has_spot && has_od;  // spot/on-demand flexible replacement narrowed to spot
@@ -1364,7 +1383,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
             } else if (!none) {
                 decision = KP_DECISION_REPLACE;
                 const uint64_t ms = spot_only ? (mt & k.spot_slots) : mt;
-                const double wl = keep ? worst_launch_price(d, k, my_t, ms, spot_only ? 0ull : mr) : DBL_MAX;
+                const double wl = keep ? worst_launch_price(d, k, my_t, ms, spot_only ? 0ull : mr, mrw) : DBL_MAX;
                 if (!single) {  // filterOutSameInstanceType
                     double mp = DBL_MAX;
                     if (keep)
@@ -1378,12 +1397,13 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
                 nrep = __popcll(km);
                 rprice = nrep ? wave_min_f64(keep ? wl : DBL_MAX) : 0.0;
                 if (FULL && k.rec_i) {  // kp_consolidate_command: the replacement NodeClaim of this probe
+                    const int nheld = RESV ? wave_sum_i32(lane < d.ro_ridw ? __popcll(nc_held) : 0) : 0;
                     if (keep) k.rec_i[4 + __popcll(km & ((1ull << lane) - 1))] = my_t;
                     if (lane == 0) {
                         k.rec_i[1] = nc_tmpl;
                         k.rec_i[2] = spot_only ? 1 : 0;
                         k.rec_i[3] = nrep;
-                        k.rec_i[4 + 64] = __popcll(nc_held);
+                        k.rec_i[4 + 64] = nheld;
                     }
                     for (int kk = lane; kk < K; kk += 64) k.rec_hdr[kk] = nch[kk];
                     for (int i = lane; i < d.DW; i += 64) k.rec_words[i] = ncw[i];
@@ -1509,6 +1529,8 @@ bool kp_cons_plan_lds(const KpDev& d, KpCons& k, int max_bytes) {
     off = al(off + 8 * (size_t)(d.EW > 0 ? d.EW : 1));
     k.off_init = (int)off;
     off = al(off + 8 * (size_t)(d.EW > 0 ? d.EW : 1));
+    k.off_rcap = (int)off;  // RESV: the probe's ReservationManager capacities (NewReservationManager per SimulateScheduling)
+    off = al(off + (d.ro ? 4 * (size_t)(d.ro_nrid > 0 ? d.ro_nrid : 1) : 0));
     k.off_mutn = (int)off;  // MUT: nodes whose requirements the probe changed
     off = al(off + (k.mut ? 8 * (size_t)(d.EW > 0 ? d.EW : 1) : 0));
     k.off_xtc = (int)off;

@@ -47,6 +47,16 @@ __device__ __forceinline__ int req_op(uint32_t flags, int nvals) {
 }
 __device__ __forceinline__ bool op_notin_or_dne(int op) { return op == OP_NOTIN || op == OP_DNE; }
 
+// A type's reserved-offering rows as bits of their ResvTab word (KpDev::type_ro packing: word << 16 | first << 8 | n).
+__device__ __forceinline__ uint64_t ro_span_bits(uint32_t tr) {
+    const uint32_t n = tr & 255u, b = (tr >> 8) & 255u;
+    return n == 0 ? 0ull : ((n >= 64 ? ~0ull : ((1ull << n) - 1ull)) << b);
+}
+// 64-bit __shfl (per-lane source lane)
+__device__ __forceinline__ uint64_t shfl64(uint64_t x, int src) {
+    return ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(x >> 32), src) << 32) | (uint32_t)__shfl((int)(uint32_t)x, src);
+}
+
 // withinIntPtrs(value, gt, lt)
 __device__ __forceinline__ bool within(const KpDev& d, int k, int v, const ReqHdr& h) {
     if (!(h.flags & (RF_GT | RF_LT))) return true;

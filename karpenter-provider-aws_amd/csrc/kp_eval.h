@@ -28,13 +28,13 @@ struct WaveScratch {
     ReqHdr hdr[KP_MAX_CLASS_KEYS];
     uint64_t words[KP_MAX_SCR_WORDS];
     uint64_t opts[KP_TW_MAX];
-    uint64_t minbits[KP_MAX_MIN_WORDS];
+    uint64_t minbits[KP_MAX_MIN_WORDS];  // minValues distinct values; after the reservation step of a successful Add:
+                                         // the reservations the NodeClaim holds (ResvTab::ridw words)
     int32_t hr[KP_LDS_AXES];   // quick-accept headroom of the chosen witness type (scaled, lower bound)
     int32_t memo_ok;           // a failed evaluation may be memoised for the shape (it did not depend on topology
                                // counts: see topo_narrow; one that depended on reservation capacity is memoised
                                // until a capacity comes back from 0, see the reservation step)
     int32_t rlive;             // success: the new options keep a compatible available reserved offering
-    uint64_t held;             // success: reservation IDs the NodeClaim holds after the Add
     // success under MIN_VALUES_POLICY=BestEffort: keys whose minValues the Add relaxes to the distinct values the
     // remaining options offer (SatisfiesMinValues' unsatisfiable keys); the commit writes them into the NodeClaim
     int32_t n_minrel;
@@ -137,8 +137,8 @@ struct EvalEnv {
     const Roles* roles;
     uint64_t min_tmpl_mask;    // templates whose requirements carry minValues
     const ResvTab* ro;         // reserved offerings (null: none)
-    const uint64_t* type_ro;   // [T] the type's reserved offerings (bits over ro index)
-    const int32_t* rcap;       // ReservationManager capacity by reservation-id value id (FFD kernel LDS)
+    const uint32_t* type_ro;   // [T] the type's reserved-offering rows (packed, ro_span_bits)
+    const int32_t* rcap;       // ReservationManager capacity by reservation (ResvTab::rid; LDS)
     int resv_on;               // run the reservation step of NodeClaim.Add
     const ProbeTopo* pt;       // consolidation probe topology counts (eval_wave<..., CT = true>)
     const TopoSnap* snap;      // FFD kernel: the current pod's topology snapshot (null: read the global counters)
@@ -252,19 +252,26 @@ __device__ __forceinline__ bool role_dneok(const KpDev& d, const EvalEnv& E, con
     return op_notin_or_dne(req_op(h.flags, popc_words(w, n)));
 }
 
-// Offerings.Available() ∧ reqs.IsCompatible(offering.Requirements) for the reserved offerings (lane i = offering i):
-// capacity-type In [reserved], zone, zone-id, reservation-id In [id], reservation-type In [type] (offering.go:178-186).
+// Offerings.Available() ∧ reqs.IsCompatible(offering.Requirements) for the reserved offerings: capacity-type In
+// [reserved], zone, zone-id, reservation-id In [id], reservation-type In [type] (offering.go:178-186).  64 rows per
+// ballot; lane q returns word q of the row bitset.
 __device__ __forceinline__ uint64_t resv_adm(const KpDev& d, const EvalEnv& E, const ClassCache& CC, const WaveScratch& ws,
                                              const ReqHdr* Ahdr, const uint64_t* Aw, int lane) {
     const ResvTab& X = *E.ro;
-    bool ok = false;
-    if (lane < X.n && ((X.avail >> lane) & 1ull)) {
-        const int zid = X.zid[lane], rt = X.rtype[lane];
-        ok = role_adm(d, E, CC, ws, Ahdr, Aw, 1, X.ctv) && role_adm(d, E, CC, ws, Ahdr, Aw, 0, X.zone[lane]) &&
-             (zid < 0 || role_adm(d, E, CC, ws, Ahdr, Aw, 2, zid)) && role_adm(d, E, CC, ws, Ahdr, Aw, 3, X.rid[lane]) &&
-             (rt < 0 ? role_dneok(d, E, CC, ws, Ahdr, Aw, 4) : role_adm(d, E, CC, ws, Ahdr, Aw, 4, rt));
+    uint64_t mine = 0;
+    for (int q = 0; q < X.w; q++) {
+        const int i = q * 64 + lane;
+        bool ok = false;
+        if (i < X.n && ((X.avail[q] >> lane) & 1ull)) {
+            const int zid = X.zid[i], rt = X.rtype[i];
+            ok = X.type[i] >= 0 && role_adm(d, E, CC, ws, Ahdr, Aw, 1, X.ctv) && role_adm(d, E, CC, ws, Ahdr, Aw, 0, X.zone[i]) &&
+                 (zid < 0 || role_adm(d, E, CC, ws, Ahdr, Aw, 2, zid)) && role_adm(d, E, CC, ws, Ahdr, Aw, 3, X.ridv[i]) &&
+                 (rt < 0 ? role_dneok(d, E, CC, ws, Ahdr, Aw, 4) : role_adm(d, E, CC, ws, Ahdr, Aw, 4, rt));
+        }
+        const uint64_t m = ballot(ok);
+        if (lane == q) mine = m;
     }
-    return ballot(ok);
+    return mine;
 }
 
 // Quick-accept witness for the NodeClaim state an evaluation produces (options `newword`, totals `tot`).
@@ -374,7 +381,7 @@ struct EvalIn {
     bool force_off;           // always apply the offering test (template filter)
     long long* prof;          // LDS stage-cycle counters (diagnostics) or null
     int host;                 // topology hostname domain of the candidate (E + NodeClaim id)
-    uint64_t held;            // reservation IDs the candidate holds (0 for a new NodeClaim)
+    uint64_t held;            // lane r < ResvTab::ridw: word r of the reservations the candidate holds (0: new NodeClaim)
 };
 
 __device__ __forceinline__ int ld_i32(const int32_t* p) {
@@ -845,9 +852,11 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         }
         mzc = ballot(ok);
     }
-    // reserved offerings: a type also has an offering when one of its reserved offerings is compatible
+    // reserved offerings: a type also has an offering when one of its reserved offerings is compatible (lane q: word q
+    // of the compatible rows)
     const uint64_t mro =
-        (RESV && E.ro && E.ro->n > 0 && (need_off || E.resv_on)) ? resv_adm(d, E, CC, ws, a.Ahdr, a.Aw, lane) : 0ull;
+        (RESV && E.ro && (need_off || E.resv_on)) ? resv_adm(d, E, CC, ws, a.Ahdr, a.Aw, lane) : 0ull;
+    const bool mro_any = RESV && ballot(mro != 0) != 0;
     EV_STAMP(2);
 
     const int n_extra = d.n_active > KP_LDS_AXES ? d.n_active - KP_LDS_AXES : 0;
@@ -891,7 +900,10 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         }
         if (need_off) {
             bool off = (E.avail[t] & mzc) != 0;
-            if (RESV && mro) off |= (E.type_ro[t < T ? t : 0] & mro) != 0;
+            if (RESV && mro_any) {  // the type's rows within their word
+                const uint32_t tr = E.type_ro[t < T ? t : 0];
+                off |= (shfl64(mro, (int)(tr >> 16)) & ro_span_bits(tr)) != 0;
+            }
             keep &= off;
         }
         if (keep && wit.on) wit.add(av, tot, t);
@@ -987,19 +999,26 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
     bool rlive = false;
     if (RESV && E.resv_on) {
         const ResvTab& X = *E.ro;
-        const int tt = lane < X.n ? X.type[lane] : 0;
-        const uint64_t wd = __shfl(newword, tt >> 6);
-        const bool comp = lane < X.n && ((mro >> lane) & 1ull) && ((wd >> (tt & 63)) & 1ull);
-        const int rid = lane < X.n ? X.rid[lane] : 0;
-        const bool res = comp && (((a.held >> rid) & 1ull) || E.rcap[rid] > 0);
-        const uint64_t cm = ballot(comp), rm = ballot(res);
-        if (STRICT && ((cm && !rm) || (a.held && !rm))) return false;
-        rlive = cm != 0;
-        const uint64_t nh = wave_or64(res ? (1ull << rid) : 0ull);
-        if (lane == 0) {
-            ws.held = nh;
-            ws.rlive = rlive ? 1 : 0;
+        // the reservations the Add holds accumulate in ws.minbits (its minValues use is over)
+        for (int i = lane; i < X.ridw; i += 64) ws.minbits[i] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        bool cm = false, rm = false;
+        for (int q = 0; q < X.w; q++) {  // 64 rows per step: row q * 64 + lane
+            const int i = q * 64 + lane;
+            const int tt = i < X.n ? X.type[i] : -1;
+            const uint64_t wd = shfl64(newword, tt >= 0 ? tt >> 6 : 0);
+            const bool comp = tt >= 0 && ((rl64(mro, q) >> lane) & 1ull) && ((wd >> (tt & 63)) & 1ull);
+            const int rid = tt >= 0 ? X.rid[i] : 0;
+            const uint64_t hw = shfl64(a.held, rid >> 6);
+            const bool res = comp && (((hw >> (rid & 63)) & 1ull) || E.rcap[rid] > 0);
+            cm |= ballot(comp) != 0;
+            rm |= ballot(res) != 0;
+            if (res) atomicOr((unsigned long long*)&ws.minbits[rid >> 6], 1ull << (rid & 63));
         }
+        if (STRICT && ((cm && !rm) || (ballot(a.held != 0) && !rm))) return false;
+        rlive = cm;
+        if (lane == 0) ws.rlive = rlive ? 1 : 0;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
     if (lane < TW) ws.opts[lane] = newword;
     // a NodeClaim that keeps reserved offerings is never quick-accepted (hr = -1): every Add recomputes its reservations

@@ -389,16 +389,25 @@ __device__ inline void limit_mask_update(const KpDev& d, int j, int lane) {
 __device__ __forceinline__ long long prof_clock(const KpDev& d) { return d.profile ? __builtin_amdgcn_s_memtime() : 0; }
 
 
-// The winner's reservations (one lane): ReservationManager.Reserve for the IDs newly held, Release for the IDs the
-// Add no longer holds (NodeClaim.Add's reservedOfferings update), then the NodeClaim's held set and liveness.
+// The winner's reservations (one wave; lane r: word r of the held set): ReservationManager.Reserve for the
+// reservations newly held, Release for those the Add no longer holds (NodeClaim.Add's reservedOfferings update), then
+// the NodeClaim's held set and liveness.  fresh: a NodeClaim being created (it held nothing).
 __device__ __forceinline__ void commit_reservations(const KpDev& d, int32_t* rcap, const WaveScratch& ws, int nc,
-                                                    uint64_t old, int* rel_flag) {
-    const uint64_t nh = ws.held;
-    for (uint64_t x = nh & ~old; x; x &= x - 1) rcap[__ffsll((unsigned long long)x) - 1]--;
-    for (uint64_t x = old & ~nh; x; x &= x - 1)
-        if (rcap[__ffsll((unsigned long long)x) - 1]++ == 0) *rel_flag = 1;
-    __hip_atomic_store(&d.nc_held[nc], nh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&d.nc_rlive[nc], ws.rlive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                                    bool fresh, int* rel_flag, int lane) {
+    const int RW = d.ro_ridw;
+    if (lane < RW) {
+        uint64_t* hp = d.nc_held + (size_t)nc * RW + lane;
+        const uint64_t old = fresh ? 0ull : ld_u64(hp), nh = ws.minbits[lane];
+        for (uint64_t x = nh & ~old; x; x &= x - 1) rcap[lane * 64 + __ffsll((unsigned long long)x) - 1]--;
+        for (uint64_t x = old & ~nh; x; x &= x - 1)
+            if (rcap[lane * 64 + __ffsll((unsigned long long)x) - 1]++ == 0) *rel_flag = 1;
+        __hip_atomic_store(hp, nh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) __hip_atomic_store(&d.nc_rlive[nc], ws.rlive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// lane r: word r of the reservations NodeClaim nc holds
+__device__ __forceinline__ uint64_t held_word(const KpDev& d, int nc, int lane) {
+    return lane < d.ro_ridw ? ld_u64(&d.nc_held[(size_t)nc * d.ro_ridw + lane]) : 0ull;
 }
 
 // Scheduler.Solve.  Wave 0 runs the queue, the sort.Slice emulation and the first-fit scan for as many pods as it
@@ -540,7 +549,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
     int64_t* const qw_req = reinterpret_cast<int64_t*>(smem + d.off_qw);    // [64][R] requests of the queue window's pods
     // reserved offerings and the ReservationManager's capacities (RESV instantiation: the catalog has reserved offerings)
     ResvTab* const sRo = RESV ? reinterpret_cast<ResvTab*>(smem + d.off_ro) : nullptr;
-    int32_t* const sRcap = RESV ? reinterpret_cast<int32_t*>(smem + d.off_ro + sizeof(ResvTab)) : nullptr;
+    int32_t* const sRcap = RESV ? reinterpret_cast<int32_t*>(smem + d.off_ro + sizeof(ResvTab)) : nullptr;  // [nrid]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nthr = blockDim.x;
     const int T = d.T, TW = d.TW, K = d.K, R = d.R, P = d.P;
     const int TP = d.lds_tpad, NQ = d.lds_nq, A = d.lds_A, NCMAX = d.lds_ncmax;
@@ -567,10 +576,37 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
         S.roles.nw[tid] = rk >= 0 ? d.nw[rk] : 0;
     }
     if (RESV) {
-        const int32_t* src = reinterpret_cast<const int32_t*>(d.ro);
-        int32_t* dst = reinterpret_cast<int32_t*>(sRo);
-        for (int i = tid; i < (int)(sizeof(ResvTab) / 4); i += nthr) dst[i] = src[i];
-        for (int i = tid; i < 64; i += nthr) sRcap[i] = d.rcap0[i];  // NewReservationManager
+        // the ReservationManager (NewReservationManager: every reservation's capacity) and the ResvTab header in LDS;
+        // small tables (d.ro_stage) also get their rows staged after the capacities, the header pointing at them
+        for (int i = tid; i < d.ro_nrid; i += nthr) sRcap[i] = d.rcap0[i];
+        const ResvTab& G = *d.ro;
+        const int n = d.ro_n;
+        int32_t* st = sRcap + ((d.ro_nrid + 1) & ~1);
+        if (d.ro_stage) {
+            for (int i = tid; i < n; i += nthr) {
+                st[i] = G.type[i];
+                st[n + i] = G.zone[i];
+                st[2 * n + i] = G.zid[i];
+                st[3 * n + i] = G.rid[i];
+                st[4 * n + i] = G.ridv[i];
+                st[5 * n + i] = G.rtype[i];
+            }
+            uint64_t* av = reinterpret_cast<uint64_t*>(st + 6 * ((n + 1) & ~1));
+            for (int i = tid; i < d.ro_w; i += nthr) av[i] = G.avail[i];
+        }
+        if (tid == 0) {
+            ResvTab h = G;
+            if (d.ro_stage) {
+                h.type = st;
+                h.zone = st + n;
+                h.zid = st + 2 * n;
+                h.rid = st + 3 * n;
+                h.ridv = st + 4 * n;
+                h.rtype = st + 5 * n;
+                h.avail = reinterpret_cast<const uint64_t*>(st + 6 * ((n + 1) & ~1));
+            }
+            *sRo = h;
+        }
     }
     for (int p = tid; p < P; p += nthr) {
         d.qbuf[p] = d.queue0[p];
@@ -1382,7 +1418,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 a.force_off = false;
                 a.prof = (d.profile && wave == 0) ? &S.st[ST_EV_REQ] : nullptr;
                 a.host = d.E + nc;
-                a.held = (RESV && d.resv_on) ? ld_u64(&d.nc_held[nc]) : 0ull;
+                a.held = (RESV && d.resv_on) ? held_word(d, nc, lane) : 0ull;
                 // the buffer by the joins reached so far, not by candidate index: a candidate rejected before the join
                 // (no barrier) must not flip the parity
                 TeamBuf* const tb = &S.team[__builtin_amdgcn_readfirstlane(S.ws[wave].team_joins) & 1];
@@ -1434,7 +1470,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 a.force_off = false;
                 a.prof = (d.profile && wave == 0) ? &S.st[ST_EV_REQ] : nullptr;
                 a.host = d.E + nc;
-                a.held = (RESV && d.resv_on) ? ld_u64(&d.nc_held[nc]) : 0ull;
+                a.held = (RESV && d.resv_on) ? held_word(d, nc, lane) : 0ull;
                 TeamBuf* const tb = &S.team[__builtin_amdgcn_readfirstlane(S.ws[wave].team_joins) & 1];
                 const bool ok = (TOPO_ON && (S.CC.flags & CF_TOPO_CONS))
                                     ? eval_wave<true, RESV, true, PREF, false, true>(d, E, S.CC, a, S.ws[wave], lane, tb,
@@ -1477,7 +1513,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 a.force_off = false;
                 a.prof = d.profile ? &S.st[ST_EV_REQ] : nullptr;
                 a.host = d.E + nc;
-                a.held = (RESV && d.resv_on) ? ld_u64(&d.nc_held[nc]) : 0ull;
+                a.held = (RESV && d.resv_on) ? held_word(d, nc, lane) : 0ull;
                 // a NodeClaim that keeps reserved offerings re-runs the whole Add (its reservations are recomputed)
                 const bool fast = !(S.CC.flags & CF_TOPO) && !(RESV && d.resv_on && ld_i32(&d.nc_rlive[nc])) &&
                                   (slast[nc] == (uint16_t)S.cur_cls || ((S.CC.flags & CF_NOKEYS) && ((S.CC.tol >> a.tmpl) & 1ull)));
@@ -1494,7 +1530,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                         e[2] = ok;
                         e[3] = S.ws[wave].memo_ok | (fast << 1) | ((RESV ? ld_i32(&d.nc_rlive[nc]) : 0) << 2);
                         e[4] = S.cand_pos[b][ci];
-                        e[5] = (int)(a.held & 0xFFFFFFFFu);
+                        e[5] = (int)(rl64(a.held, 0) & 0xFFFFFFFFu);
                     }
                 }
                 if (lane == 0) {
@@ -1541,7 +1577,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 const int nc = sord[pos];
                 if (!S.fastp[round & 1][win]) {
                     commit_reqs(d, S.CC, S.ws[cw], nc, lane);
-                    if (RESV && d.resv_on && lane == 0) commit_reservations(d, sRcap, S.ws[cw], nc, ld_u64(&d.nc_held[nc]), &S.rel_flag);
+                    if (RESV && d.resv_on) commit_reservations(d, sRcap, S.ws[cw], nc, false, &S.rel_flag, lane);
                 }
                 if (PREF && d.best_effort) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // commit_reqs' header rows have landed
@@ -1644,7 +1680,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the header rows above have landed
                             commit_min_relax(d, S.ws[wave], n, lane);
                         }
-                        if (RESV && d.resv_on && lane == 0) commit_reservations(d, sRcap, S.ws[wave], n, 0ull, &S.rel_flag);
+                        if (RESV && d.resv_on) commit_reservations(d, sRcap, S.ws[wave], n, true, &S.rel_flag, lane);
                         if (TOPO_ON && (S.CC.flags & CF_TOPO))
                             topo_record(d, S.CC, S.ws[wave], d.cls_hdr + (size_t)(d.C + jj) * K,
                                         d.cls_words + (size_t)(d.C + jj) * d.DW, d.E + n, jj, true, lane);

@@ -508,14 +508,22 @@ struct kp_ctx {
     std::string solve_unsupported;           // catalog the Solve tables cannot hold (launch selection still works)
     // reserved offerings in Solve (ReservationManager): <= 64 per catalog
     bool ro_ok = true;
-    ResvTab h_ro{};
+    bool wide_resvid = false;                // the reservation-id label has > 64 values (no type value masks for it)
+    // reserved offerings (ResvTab rows, kp_layout.h; padding rows have type -1 and offering -1)
+    std::vector<int32_t> ro_type, ro_zone, ro_zid, ro_rid, ro_ridv, ro_rtype;
+    std::vector<int32_t> ro_rid_vid;         // [nrid] reservation-id value id of each reservation
+    std::vector<uint64_t> ro_avail;          // [w]
+    std::vector<int32_t> ro_off;             // offering row of reserved-offering row i
+    std::vector<uint32_t> type_ro;           // [T] packed span of the type's rows
+    std::vector<int32_t> rcap0;              // [nrid]
+    std::vector<double> ro_price;            // [rows]
+    ResvTab h_ro{};                          // header with the device pointers below
     std::vector<ResvTab> h_ro_up;            // upload staging of h_ro (outlives the async copy)
-    std::vector<int32_t> ro_off;             // offering row of reserved offering i
-    std::vector<uint64_t> type_ro;           // [T]
-    std::vector<int32_t> rcap0;              // [64]
-    std::vector<double> ro_price;            // [KP_MAX_RO]
     DBuf<ResvTab> d_ro;
-    DBuf<uint64_t> d_type_ro, d_nc_held;
+    DBuf<int32_t> d_ro_type, d_ro_zone, d_ro_zid, d_ro_rid, d_ro_ridv, d_ro_rtype, d_ro_rid_vid;
+    DBuf<uint64_t> d_ro_avail;
+    DBuf<uint32_t> d_type_ro;
+    DBuf<uint64_t> d_nc_held;
     DBuf<int32_t> d_rcap0, d_nc_rlive;
     DBuf<double> d_ro_price;
     DBuf<int32_t> d_trace;                   // KPSIM_TRACE_POD diagnostics
@@ -713,6 +721,40 @@ static void rebuild_avail(kp_ctx* c, const std::vector<uint8_t>& avail) {
 
 static kp_status upload_launch_tables(kp_ctx* c, const kp_catalog_view* v, const std::vector<uint8_t>& avail);
 
+// The ResvTab rows, the header with their device pointers, and the per-type spans / capacities / prices.
+static hipError_t upload_resv(kp_ctx* c, hipStream_t s) {
+    ResvTab& X = c->h_ro;
+    X = ResvTab{};
+    X.n = (int)c->ro_type.size();
+    X.w = (X.n + 63) / 64;
+    X.nrid = (int)c->ro_rid_vid.size();
+    X.ridw = (X.nrid + 63) / 64;
+    X.ctv = c->key_ct >= 0 ? c->cat.keys[c->key_ct].find("reserved") : -1;
+    hipError_t e;
+    auto up = [&](DBuf<int32_t>& b, const std::vector<int32_t>& v) -> const int32_t* {
+        if ((e = b.upload(v, s)) != hipSuccess) return nullptr;
+        return b.p;
+    };
+    X.type = up(c->d_ro_type, c->ro_type);
+    X.zone = up(c->d_ro_zone, c->ro_zone);
+    X.zid = up(c->d_ro_zid, c->ro_zid);
+    X.rid = up(c->d_ro_rid, c->ro_rid);
+    X.ridv = up(c->d_ro_ridv, c->ro_ridv);
+    X.rtype = up(c->d_ro_rtype, c->ro_rtype);
+    X.rid_vid = up(c->d_ro_rid_vid, c->ro_rid_vid);
+    if ((e = c->d_ro_avail.upload(c->ro_avail, s)) != hipSuccess) return e;
+    X.avail = c->d_ro_avail.p;
+    c->h_ro_up.assign(1, X);
+    if ((e = c->d_ro.upload(c->h_ro_up, s)) != hipSuccess) return e;
+    if ((e = c->d_type_ro.upload(c->type_ro, s)) != hipSuccess) return e;
+    std::vector<int32_t> rc = c->rcap0;
+    if (rc.empty()) rc.push_back(0);
+    if ((e = c->d_rcap0.upload(rc, s)) != hipSuccess) return e;
+    std::vector<double> pr = c->ro_price;
+    if (pr.empty()) pr.push_back(0.0);
+    return c->d_ro_price.upload(pr, s);
+}
+
 static kp_status catalog_upload_one(kp_ctx* ctx, const kp_catalog_view* v, uint64_t epoch) try {
     if (!ctx || !v) return KP_E_INVALID;
     // every prepared solve / consolidation pass captured device pointers and sizes of the previous catalog, and the
@@ -870,59 +912,96 @@ static kp_status catalog_upload_one(kp_ctx* ctx, const kp_catalog_view* v, uint6
     }
     c->avail_zc.assign(T, 0);
     rebuild_avail(c, avail);
-    // reserved offerings: ResvTab (ordered by type), the ReservationManager's initial capacity per reservation ID
+    // reserved offerings: ResvTab rows ordered by type, each type's rows inside one 64-row word (padding rows between),
+    // reservations numbered densely in row order; the ReservationManager's initial capacity per reservation
     // (NewReservationManager: the least ReservationCapacity among the offerings carrying the ID)
-    c->ro_ok = (int)ro_rows.size() <= KP_MAX_RO;
-    c->h_ro = ResvTab{};
+    c->ro_ok = true;
+    c->ro_type.clear();
+    c->ro_zone.clear();
+    c->ro_zid.clear();
+    c->ro_rid.clear();
+    c->ro_ridv.clear();
+    c->ro_rtype.clear();
+    c->ro_rid_vid.clear();
     c->ro_off.clear();
-    c->type_ro.assign(T, 0);
-    c->rcap0.assign(64, 0);
-    c->ro_price.assign(KP_MAX_RO, 0.0);
-    if (c->ro_ok && !ro_rows.empty()) {
+    c->ro_price.clear();
+    c->rcap0.clear();
+    c->type_ro.assign(T, 0u);
+    if (!ro_rows.empty()) {
         std::stable_sort(ro_rows.begin(), ro_rows.end(), [&](int a, int b) { return c->off_type[a] < c->off_type[b]; });
-        std::vector<uint8_t> seen(64, 0);
-        ResvTab& X = c->h_ro;
-        X.n = (int)ro_rows.size();
-        X.ctv = c->cat.keys[c->key_ct].id("reserved");
-        for (int i = 0; i < X.n; i++) {
-            const int o = ro_rows[i];
-            auto lab = [&](int k, int& state) -> const char* {
-                state = k < 0 ? KP_LABEL_ABSENT : v->offering_label_state[(size_t)o * KO + k];
-                return k < 0 ? nullptr : v->offering_label_values[(size_t)o * KO + k];
-            };
-            int sz, sc, szi, sri, srt;
-            const char* z = lab(kz, sz);
-            const char* ct = lab(kc, sc);
-            const char* zi = lab(kzi, szi);
-            const char* ri = lab(kri, sri);
-            const char* rt = lab(krt, srt);
-            if (strcmp(ct, "reserved") != 0 || sri != KP_LABEL_IN)
-                return fail(ctx, KP_E_UNSUPPORTED, "reserved offering without capacity-type reserved / reservation-id");
-            X.type[i] = c->off_type[o];
-            X.zone[i] = c->cat.keys[c->key_zone].id(z);
-            X.zid[i] = szi == KP_LABEL_IN ? c->cat.keys[c->key_zoneid].id(zi) : -1;
-            X.rid[i] = c->cat.keys[c->key_resvid].id(ri);
-            X.rtype[i] = srt == KP_LABEL_IN ? c->cat.keys[c->key_resvtype].id(rt) : -1;
-            if (X.rid[i] >= 64) {  // more than 64 reservation IDs: Solve refuses the catalog (solve_unsupported)
+        std::map<int, int> rid_of;  // reservation-id value id -> reservation
+        for (size_t a = 0; a < ro_rows.size() && c->ro_ok;) {
+            size_t b = a;
+            while (b < ro_rows.size() && c->off_type[ro_rows[b]] == c->off_type[ro_rows[a]]) b++;
+            const int cnt = (int)(b - a), t = c->off_type[ro_rows[a]];
+            if (cnt > 64) {  // one instance type with more than 64 reservations: its rows do not fit one word
                 c->ro_ok = false;
                 break;
             }
-            if (avail[o]) X.avail |= 1ull << i;
-            const int rc = v->offering_reservation_capacity ? v->offering_reservation_capacity[o] : 0;
-            c->rcap0[X.rid[i]] = seen[X.rid[i]] ? std::min(c->rcap0[X.rid[i]], rc) : rc;
-            seen[X.rid[i]] = 1;
-            c->type_ro[X.type[i]] |= 1ull << i;
-            c->ro_price[i] = v->offering_price[o];
-            c->ro_off.push_back(o);
+            while ((c->ro_type.size() % 64) + cnt > 64) {  // padding up to the next word
+                c->ro_type.push_back(-1);
+                c->ro_zone.push_back(0);
+                c->ro_zid.push_back(-1);
+                c->ro_rid.push_back(0);
+                c->ro_ridv.push_back(0);
+                c->ro_rtype.push_back(-1);
+                c->ro_off.push_back(-1);
+                c->ro_price.push_back(0.0);
+            }
+            const int first = (int)c->ro_type.size();
+            c->type_ro[t] = (uint32_t)(first / 64) << 16 | (uint32_t)(first % 64) << 8 | (uint32_t)cnt;
+            for (size_t i = a; i < b; i++) {
+                const int o = ro_rows[i];
+                auto lab = [&](int k, int& state) -> const char* {
+                    state = k < 0 ? KP_LABEL_ABSENT : v->offering_label_state[(size_t)o * KO + k];
+                    return k < 0 ? nullptr : v->offering_label_values[(size_t)o * KO + k];
+                };
+                int sz, sc, szi, sri, srt;
+                const char* z = lab(kz, sz);
+                const char* ct = lab(kc, sc);
+                const char* zi = lab(kzi, szi);
+                const char* ri = lab(kri, sri);
+                const char* rt = lab(krt, srt);
+                if (strcmp(ct, "reserved") != 0 || sri != KP_LABEL_IN)
+                    return fail(ctx, KP_E_UNSUPPORTED, "reserved offering without capacity-type reserved / reservation-id");
+                const int ridv = c->cat.keys[c->key_resvid].id(ri);
+                auto it = rid_of.find(ridv);
+                const int rc = v->offering_reservation_capacity ? v->offering_reservation_capacity[o] : 0;
+                int r;
+                if (it == rid_of.end()) {
+                    r = (int)c->ro_rid_vid.size();
+                    rid_of[ridv] = r;
+                    c->ro_rid_vid.push_back(ridv);
+                    c->rcap0.push_back(rc);
+                } else {
+                    r = it->second;
+                    c->rcap0[r] = std::min(c->rcap0[r], rc);
+                }
+                c->ro_type.push_back(t);
+                c->ro_zone.push_back(c->cat.keys[c->key_zone].id(z));
+                c->ro_zid.push_back(szi == KP_LABEL_IN ? c->cat.keys[c->key_zoneid].id(zi) : -1);
+                c->ro_rid.push_back(r);
+                c->ro_ridv.push_back(ridv);
+                c->ro_rtype.push_back(srt == KP_LABEL_IN ? c->cat.keys[c->key_resvtype].id(rt) : -1);
+                c->ro_off.push_back(o);
+                c->ro_price.push_back(v->offering_price[o]);
+            }
+            a = b;
         }
+        if ((int)c->ro_type.size() > KP_MAX_RO || (int)c->ro_rid_vid.size() > KP_MAX_RO) c->ro_ok = false;
         if (!c->ro_ok) {
-            c->h_ro = ResvTab{};
-            c->ro_off.clear();
-            c->type_ro.assign(T, 0);
-            c->rcap0.assign(64, 0);
+            for (auto* x : {&c->ro_type, &c->ro_zone, &c->ro_zid, &c->ro_rid, &c->ro_ridv, &c->ro_rtype, &c->ro_rid_vid,
+                            &c->ro_off, &c->rcap0})
+                x->clear();
+            c->ro_price.clear();
+            c->type_ro.assign(T, 0u);
         }
     }
+    c->ro_avail.assign(std::max<size_t>(1, (c->ro_type.size() + 63) / 64), 0ull);
+    for (size_t i = 0; i < c->ro_off.size(); i++)
+        if (c->ro_off[i] >= 0 && avail[c->ro_off[i]]) c->ro_avail[i / 64] |= 1ull << (i % 64);
     // multi-valued keys: value masks (<= 64 values)
+    c->wide_resvid = false;
     c->cat_kflags.assign(Kc, 0);
     c->cat_multi.assign(Kc, -1);
     c->n_multi = 0;
@@ -932,7 +1011,14 @@ static kp_status catalog_upload_one(kp_ctx* ctx, const kp_catalog_view* v, uint6
         if (!present && !multi[k]) continue;  // offering-only key absent from every type
         if (multi[k]) {
             if (c->cat.keys[k].vals.size() > 64) {
-                // the Solve tables hold a multi-valued label as a 64-bit value mask; the launch path has no such limit
+                // the Solve tables hold a multi-valued label as a 64-bit value mask; the launch path has no such limit.
+                // The reservation-id label (one value per capacity reservation) is exempt: reserved offerings are
+                // evaluated through ResvTab, and only a pod or NodePool requirement on the key would need its type
+                // masks (kp_solve_prepare refuses that: wide_resvid)
+                if (k == c->key_resvid && c->ro_ok) {
+                    c->wide_resvid = true;
+                    continue;
+                }
                 c->solve_unsupported = "multi-valued label " + c->cat.keys[k].name + " with > 64 values";
                 continue;
             }
@@ -1004,11 +1090,7 @@ static kp_status catalog_upload_one(kp_ctx* ctx, const kp_catalog_view* v, uint6
     HIPCHK(c->d_slot_zoneid.upload(c->slot_zoneid, s));
     HIPCHK(c->d_name_rank.upload(rank, s));
     HIPCHK(c->d_nonneg.upload(nonneg, s));
-    c->h_ro_up.assign(1, c->h_ro);
-    HIPCHK(c->d_ro.upload(c->h_ro_up, s));
-    HIPCHK(c->d_type_ro.upload(c->type_ro, s));
-    HIPCHK(c->d_rcap0.upload(c->rcap0, s));
-    HIPCHK(c->d_ro_price.upload(c->ro_price, s));
+    HIPCHK(upload_resv(c, s));
     {
         kp_status lst = upload_launch_tables(c, v, avail);
         if (lst != KP_OK) return lst;
@@ -1041,11 +1123,10 @@ static kp_status patch_avail_one(kp_ctx* ctx, const uint8_t* available, int32_t 
     HIPCHK(hipSetDevice(ctx->device));
     rebuild_avail(ctx, std::vector<uint8_t>(available, available + n));
     HIPCHK(ctx->d_avail_zc.upload(ctx->avail_zc, ctx->stream));
-    ctx->h_ro.avail = 0;
+    std::fill(ctx->ro_avail.begin(), ctx->ro_avail.end(), 0ull);
     for (size_t i = 0; i < ctx->ro_off.size(); i++)
-        if (available[ctx->ro_off[i]]) ctx->h_ro.avail |= 1ull << i;
-    ctx->h_ro_up.assign(1, ctx->h_ro);
-    HIPCHK(ctx->d_ro.upload(ctx->h_ro_up, ctx->stream));
+        if (ctx->ro_off[i] >= 0 && available[ctx->ro_off[i]]) ctx->ro_avail[i / 64] |= 1ull << (i % 64);
+    HIPCHK(ctx->d_ro_avail.upload(ctx->ro_avail, ctx->stream));
     for (int o = 0; o < n; o++) ctx->l_avail[o] = available[o] ? 1 : 0;
     HIPCHK(ctx->d_l_avail.upload(ctx->l_avail, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -1071,10 +1152,10 @@ static kp_status patch_price_one(kp_ctx* ctx, const int32_t* idx, const double* 
         if (ctx->off_slot[idx[i]] >= 0)
             ctx->slot_price[(size_t)ctx->off_type[idx[i]] * KP_MAX_SLOTS + ctx->off_slot[idx[i]]] = price[i];
         for (size_t r = 0; r < ctx->ro_off.size(); r++)
-            if (ctx->ro_off[r] == idx[i]) ctx->ro_price[r] = price[i];
+            if (ctx->ro_off[r] == idx[i]) ctx->ro_price[r] = price[i];  // (padding rows hold -1)
         ctx->l_price[idx[i]] = price[i];
     }
-    HIPCHK(ctx->d_ro_price.upload(ctx->ro_price, ctx->stream));
+    if (!ctx->ro_price.empty()) HIPCHK(ctx->d_ro_price.upload(ctx->ro_price, ctx->stream));
     HIPCHK(ctx->d_slot_price.upload(ctx->slot_price, ctx->stream));
     HIPCHK(ctx->d_l_price.upload(ctx->l_price, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -1543,6 +1624,14 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     for (int i = 0; i < C; i++)
         for (auto& kv : creq[i])
             if (kv.second.has_min) return fail(ctx, KP_E_INVALID, "pod requirements cannot carry minValues");
+    if (c->wide_resvid) {  // see catalog_upload_one: no per-type value masks for a reservation-id label this wide
+        for (int i = 0; i < C; i++)
+            if (creq[i].count(c->key_resvid))
+                return fail(ctx, KP_E_UNSUPPORTED, "a pod requirement on capacity-reservation-id over more than 64 reservations");
+        for (int j = 0; j < NT; j++)
+            if (treq[j].count(c->key_resvid))
+                return fail(ctx, KP_E_UNSUPPORTED, "a NodePool requirement on capacity-reservation-id over more than 64 reservations");
+    }
     TopoHost th;
     {
         const kp_status ts = topo_build(c, in, creq, th, err);
@@ -2000,7 +2089,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     HIPCHK(c->d_nc_opts.ensure((size_t)NCcap * TW));
     HIPCHK(c->d_nc_req.ensure((size_t)NCcap * R));
     HIPCHK(c->d_nc_tmpl.ensure(NCcap));
-    HIPCHK(c->d_nc_held.ensure(NCcap));
+    HIPCHK(c->d_nc_held.ensure((size_t)NCcap * std::max(1, c->h_ro.ridw)));
     HIPCHK(c->d_nc_rlive.ensure(NCcap));
     HIPCHK(c->d_qbuf.ensure(std::max(P, 1)));
     HIPCHK(c->d_last_len.ensure(std::max(P, 1)));
@@ -2419,6 +2508,10 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.ro = c->h_ro.n > 0 ? c->d_ro.p : nullptr;
     d.type_ro = c->d_type_ro.p;
     d.ro_price = c->d_ro_price.p;
+    d.ro_n = c->h_ro.n;
+    d.ro_w = c->h_ro.w;
+    d.ro_nrid = c->h_ro.nrid;
+    d.ro_ridw = c->h_ro.ridw;
     d.resv_on = (c->reserved_capacity && c->h_ro.n > 0) ? 1 : 0;
     d.rcap0 = c->d_rcap0.p;
     d.nc_held = c->d_nc_held.p;

@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(KpDev d) {
     __shared__ uint64_t s_key[KP_MAX_TYPES];
     __shared__ uint32_t s_rank[KP_MAX_TYPES];
     __shared__ uint16_t s_t[KP_MAX_TYPES];
-    __shared__ uint64_t s_mzc, s_mro;
+    __shared__ uint64_t s_mzc, s_mro[KP_RO_W];
     __shared__ int s_n;
     __shared__ uint64_t s_bits[KP_MAX_MIN_WORDS];
     __shared__ int s_ok;
@@ -161,16 +161,21 @@ __global__ __launch_bounds__(256) void finalize_kernel(KpDev d) {
         s_ok = 1;
         // FinalizeScheduling: a NodeClaim holding reservations gets ReservationIDLabel In [held IDs] (Requirements.Add:
         // the held IDs are admitted by the NodeClaim's requirement, so the intersection is In [held], minValues kept)
-        const uint64_t held = d.resv_on ? d.nc_held[nc] : 0ull;
-        if (held && d.key_resvid >= 0) {
+        bool any = false;
+        for (int r = 0; d.resv_on && r < d.ro_ridw; r++) any |= d.nc_held[(size_t)nc * d.ro_ridw + r] != 0;
+        if (any && d.key_resvid >= 0) {
             ReqHdr* hp = d.nc_hdr + (size_t)nc * d.K + d.key_resvid;
             uint64_t* wp = d.nc_words + (size_t)nc * d.DW + d.woff[d.key_resvid];
             ReqHdr o{};
             o.flags = RF_DEF | (hp->flags & RF_MIN);
             o.minv = hp->minv;
             *hp = o;
-            wp[0] = held;
-            for (int i = 1; i < d.nw[d.key_resvid]; i++) wp[i] = 0;
+            for (int i = 0; i < d.nw[d.key_resvid]; i++) wp[i] = 0;
+            for (int r = 0; r < d.ro_ridw; r++)
+                for (uint64_t x = d.nc_held[(size_t)nc * d.ro_ridw + r]; x; x &= x - 1) {
+                    const int v = d.ro->rid_vid[r * 64 + __ffsll((unsigned long long)x) - 1];
+                    wp[v >> 6] |= 1ull << (v & 63);
+                }
         }
     }
     __syncthreads();
@@ -196,33 +201,36 @@ __global__ __launch_bounds__(256) void finalize_kernel(KpDev d) {
         }
         const uint64_t m = ballot(ok);
         if (lane == 0) s_mzc = m;
-        // the reserved offerings
-        bool rok = false;
-        if (d.ro && lane < d.ro->n && ((d.ro->avail >> lane) & 1ull)) {
-            auto adm = [&](int k, int v) -> bool {
-                if (k < 0) return true;
-                const ReqHdr h = H[k];
-                if (!(h.flags & RF_DEF)) return true;
-                return req_has(d, k, v, h, W + d.woff[k]);
-            };
-            const int zid = d.ro->zid[lane], rt = d.ro->rtype[lane];
-            bool rtok;
-            if (rt >= 0) {
-                rtok = adm(d.key_resvtype, rt);
-            } else {
-                const ReqHdr h = d.key_resvtype >= 0 ? H[d.key_resvtype] : ReqHdr{};
-                rtok = !(h.flags & RF_DEF) ||
-                       op_notin_or_dne(req_op(h.flags, popc_words(W + d.woff[d.key_resvtype], d.nw[d.key_resvtype])));
+        // the reserved offerings, 64 rows per step (word q of s_mro)
+        for (int q = 0; d.ro && q < d.ro_w; q++) {
+            const int i = q * 64 + lane;
+            bool rok = false;
+            if (i < d.ro_n && d.ro->type[i] >= 0 && ((d.ro->avail[q] >> lane) & 1ull)) {
+                auto adm = [&](int k, int v) -> bool {
+                    if (k < 0) return true;
+                    const ReqHdr h = H[k];
+                    if (!(h.flags & RF_DEF)) return true;
+                    return req_has(d, k, v, h, W + d.woff[k]);
+                };
+                const int zid = d.ro->zid[i], rt = d.ro->rtype[i];
+                bool rtok;
+                if (rt >= 0) {
+                    rtok = adm(d.key_resvtype, rt);
+                } else {
+                    const ReqHdr h = d.key_resvtype >= 0 ? H[d.key_resvtype] : ReqHdr{};
+                    rtok = !(h.flags & RF_DEF) ||
+                           op_notin_or_dne(req_op(h.flags, popc_words(W + d.woff[d.key_resvtype], d.nw[d.key_resvtype])));
+                }
+                rok = adm(d.key_ct, d.ro->ctv) && adm(d.key_zone, d.ro->zone[i]) && (zid < 0 || adm(d.key_zoneid, zid)) &&
+                      adm(d.key_resvid, d.ro->ridv[i]) && rtok;
             }
-            rok = adm(d.key_ct, d.ro->ctv) && adm(d.key_zone, d.ro->zone[lane]) && (zid < 0 || adm(d.key_zoneid, zid)) &&
-                  adm(d.key_resvid, d.ro->rid[lane]) && rtok;
+            const uint64_t rm = ballot(rok);
+            if (lane == 0) s_mro[q] = rm;
         }
-        const uint64_t rm = ballot(rok);
-        if (lane == 0) s_mro = rm;
     }
     if (tid < d.R) s_tot[tid] = d.nc_req[(size_t)nc * d.R + tid];
     __syncthreads();
-    const uint64_t mzc = s_mzc, mro = s_mro;
+    const uint64_t mzc = s_mzc;
     for (int t = tid; t < TW * 64; t += blockDim.x) {
         if (t >= T) continue;
         if (!((d.nc_opts[(size_t)nc * TW + (t >> 6)] >> (t & 63)) & 1ull)) continue;
@@ -242,9 +250,12 @@ __global__ __launch_bounds__(256) void finalize_kernel(KpDev d) {
             const double p = d.slot_price[(size_t)t * KP_MAX_SLOTS + s];
             price = p < price ? p : price;
         }
-        for (uint64_t rmk = mro ? d.type_ro[t] & mro : 0ull; rmk; rmk &= rmk - 1) {
-            const double p = d.ro_price[__ffsll((unsigned long long)rmk) - 1];
-            price = p < price ? p : price;
+        if (d.ro) {  // the type's compatible available reserved offerings (its rows within their word)
+            const uint32_t tr = d.type_ro[t];
+            for (uint64_t rmk = tr ? s_mro[tr >> 16] & ro_span_bits(tr) : 0ull; rmk; rmk &= rmk - 1) {
+                const double p = d.ro_price[(tr >> 16) * 64 + __ffsll((unsigned long long)rmk) - 1];
+                price = p < price ? p : price;
+            }
         }
         const int i = atomicAdd(&s_n, 1);
         s_key[i] = (uint64_t)__double_as_longlong(price);
@@ -342,6 +353,11 @@ bool kp_ffd_plan_lds(KpDev& d, int max_bytes) {
 
 static bool kp_ffd_plan_lds_tables(KpDev& d, int max_bytes) {
     auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    // reserved offerings: the ResvTab header and the ReservationManager's capacities, then (small tables, up to
+    // KP_RO_STAGE rows) the rows themselves (ffd_solve's staging)
+    d.ro_stage = d.ro && d.ro_n <= KP_RO_STAGE ? 1 : 0;
+    const size_t ro_bytes = !d.ro ? 0 : sizeof(ResvTab) + 4 * (size_t)((d.ro_nrid + 1) & ~1) +
+                                        (d.ro_stage ? 24 * (size_t)((d.ro_n + 1) & ~1) + 8 * (size_t)d.ro_w : 0);
     size_t off = al(sizeof(FfdShared));
     d.off_qw = (int)off;  // the queue window's pod requests, [64][R]
     off = al(off + 64 * 8 * (size_t)(d.R > 0 ? d.R : 1));
@@ -350,7 +366,7 @@ static bool kp_ffd_plan_lds_tables(KpDev& d, int max_bytes) {
     if (d.alloc_global) {
         const int tp0 = (d.T + 63) / 64 * 64;
         size_t fixed = off + 8 * (size_t)tp0 + (d.multi16 ? 2 * (size_t)d.n_multi * tp0 : 0) +
-                       (d.ro ? sizeof(ResvTab) + 4 * 64 : 0) + (d.G > 0 ? sizeof(TopoSnap) : 0) + 256;
+                       ro_bytes + (d.G > 0 ? sizeof(TopoSnap) : 0) + 256;
         const long room = ((long)max_bytes - (long)fixed) / 9;
         // more NodeClaims than LDS holds beside the fixed tables: the slice arrays go to HBM (the HBM instantiations)
         if (room < ncmax) d.slice_hbm = d.g_key != nullptr;
@@ -376,7 +392,7 @@ static bool kp_ffd_plan_lds_tables(KpDev& d, int max_bytes) {
     d.off_multi = (int)off;
     if (d.multi16) off = al(off + 2 * (size_t)d.n_multi * tp);
     d.off_ro = (int)off;
-    if (d.ro) off = al(off + sizeof(ResvTab) + 4 * 64);
+    if (d.ro) off = al(off + ro_bytes);
     d.off_tsnap = (int)off;
     if (d.G > 0) off = al(off + sizeof(TopoSnap));
     d.off_hr = (int)off;

@@ -75,20 +75,27 @@ struct ReqHdr {
     int64_t lt;
 };
 
-// Reserved offerings of the catalog (offering.go:164-194), at most 64, as one evaluation reads them (LDS copy in the
-// FFD kernel).  Requirement values are value ids of the offering-role keys; `rid` (the reservation-id value id, < 64
-// because the key is multi-valued) is also the ReservationManager slot.
-#define KP_MAX_RO 64
+// Reserved offerings of the catalog (offering.go:164-194: one per capacity reservation of the EC2NodeClass), SoA in
+// HBM (the FFD kernel stages small tables in LDS).  Rows are ordered by instance type and placed so that a type's
+// rows lie inside one 64-row word (padding rows: type -1, unavailable); type_ro[t] packs that word and the rows' span.
+// rid is the row's reservation (a dense index < nrid: its ReservationManager slot and its bit in a NodeClaim's held
+// set of ridw words); ridv / zone / zid / rtype are value ids of the offering-role keys (zid, rtype -1: none).
+#define KP_MAX_RO 1024               // reserved-offering rows (incl. padding) per catalog
+#define KP_RO_W (KP_MAX_RO / 64)     // words of a row bitset or a held-reservation set
+#define KP_RO_STAGE 128              // FFD kernel: tables of up to this many rows are staged in LDS
 struct ResvTab {
-    int32_t n;                       // reserved offerings
-    int32_t ctv;                     // capacity-type value id of "reserved"
-    int32_t type[KP_MAX_RO];         // instance type row
-    int32_t zone[KP_MAX_RO];         // zone value id
-    int32_t zid[KP_MAX_RO];          // zone-id value id or -1 (no zone-id requirement)
-    int32_t rid[KP_MAX_RO];          // reservation-id value id
-    int32_t rtype[KP_MAX_RO];        // reservation-type value id or -1 (DoesNotExist)
-    uint64_t avail;                  // bit i: Offering.Available
+    int32_t n, ctv, nrid, w;         // rows, capacity-type value id of "reserved", reservation IDs, row words
+    int32_t ridw, pad;               // words of a held set: ceil(nrid / 64)
+    const int32_t* type;             // [n] instance type row (-1: padding)
+    const int32_t* zone;
+    const int32_t* zid;
+    const int32_t* rid;
+    const int32_t* ridv;
+    const int32_t* rtype;
+    const uint64_t* avail;           // [w] bit i of word i / 64: row i is Available
+    const int32_t* rid_vid;          // [nrid] reservation-id value id of reservation r
 };
+// type_ro[t] = word << 16 | first bit << 8 | rows: the type's reserved-offering rows within their word (0: none)
 
 // Static operands of one (class, constraining topology group) entry, so the FFD kernel's per-pod prefilter setup reads
 // one row instead of walking cls_tc → tg_info → the class digest: flags = type | self << 2 | hostname << 3; key = the
@@ -272,12 +279,14 @@ struct KpDev {
     int32_t qshift[KP_LDS_AXES];     // headroom scale per quick axis: value >> qshift fits 30 bits
 
     // ---------------- reserved capacity ([core] scheduling/reservationmanager.go, nodeclaim.go) ----------------
-    const ResvTab* ro;               // reserved offerings (global copy)
-    const uint64_t* type_ro;         // [T] bits over ro index: the type's reserved offerings
-    const double* ro_price;          // [KP_MAX_RO]
+    const ResvTab* ro;               // reserved offerings (device copy of the header; null: none)
+    const uint32_t* type_ro;         // [T] the type's rows (ro_span_bits), see ResvTab
+    const double* ro_price;          // [ro_n] price of row i
+    int32_t ro_n, ro_w, ro_nrid, ro_ridw;  // the header's sizes, for kernels that size loops without reading it
+    int32_t ro_stage;                // FFD kernel: the rows fit its LDS plan and are staged there
     int32_t resv_on;                 // ReservedCapacity gate ∧ reserved offerings exist: NodeClaim.Add reserves
-    const int32_t* rcap0;            // [64] ReservationManager capacity per reservation-id value id (least over offerings)
-    uint64_t* nc_held;               // [NCcap] reservation IDs a NodeClaim holds (NodeClaim.reservedOfferings' IDs)
+    const int32_t* rcap0;            // [ro_nrid] ReservationManager capacity per reservation (least over its offerings)
+    uint64_t* nc_held;               // [NCcap][ro_ridw] reservations a NodeClaim holds (NodeClaim.reservedOfferings' IDs)
     int32_t* nc_rlive;               // [NCcap] the NodeClaim's options keep a compatible available reserved offering
 
     // a device copy of this struct (uploaded before each FFD launch): out-of-line device functions take it instead of

@@ -376,6 +376,43 @@ def config5_catalog(catalog, n_default=40, n_block=20, seed=SEED, expiring_frac=
     return cat
 
 
+def wide_reservation_catalog(catalog, n_reservations=200, max_per_type=4, seed=SEED, expiring_frac=0.10,
+                             rcap=(1, 21)):
+    """A catalog with more capacity reservations than one 64-bit word holds (offering.go:164-194 makes one reserved
+    offering per reservation, without bound): n_reservations ODCR-default / capacity-block reservations over types
+    drawn from the catalog, 1 to max_per_type reservations per type (in its on-demand zones), ReservationCapacity drawn
+    from rcap, price = odPrice / 1e7, some expiring.  Returns a new catalog list (types copied)."""
+    import copy
+    rng = np.random.Generator(np.random.PCG64(seed + 55))
+    cat = copy.deepcopy(catalog)
+    cands = [t for t, it in enumerate(cat) if any(o.capacity_type == "on-demand" for o in it.offerings)]
+    assert len(cands) * max_per_type >= n_reservations, "catalog too small for %d reservations" % n_reservations
+    made = 0
+    while made < n_reservations:
+        t = int(rng.choice(cands))
+        it = cat[t]
+        od = [o for o in it.offerings if o.capacity_type == "on-demand"]
+        for _ in range(int(rng.integers(1, max_per_type + 1))):
+            if made >= n_reservations or sum(o.capacity_type == "reserved" for o in it.offerings) >= max_per_type:
+                break
+            z = od[int(rng.integers(len(od)))]
+            expiring = rng.random() < expiring_frac
+            it.offerings.append(model.Offering(
+                capacity_type="reserved", zone=z.zone, price=z.price / 10_000_000.0, available=not expiring,
+                zone_id=z.zone_id, reservation_id="cr-w%05d" % made,
+                reservation_type="default" if rng.random() < 0.7 else "capacity-block",
+                reservation_capacity=int(rng.integers(*rcap))))
+            made += 1
+        res = [o for o in it.offerings if o.capacity_type == "reserved"]
+        if res:
+            cts = list(it.labels.get(CAPACITY_TYPE) or [])
+            if "reserved" not in cts:
+                it.labels[CAPACITY_TYPE] = cts + ["reserved"]
+            it.labels[model.RESERVATION_ID] = sorted({o.reservation_id for o in res})
+            it.labels[model.RESERVATION_TYPE] = sorted({o.reservation_type for o in res})
+    return cat
+
+
 def config5(n_pods=200_000, n_classes=250, catalog=None, golden=None, seed=SEED) -> Problem:
     """BASELINE configs[4] as a Solve: config-2 pods over the reserved-offering catalog (config5_catalog), with the
     ODCR NodePool patterns of designs/odcr.md:140-180 — an ODCR-only NodePool first (capacity-type In [reserved],

@@ -5,6 +5,7 @@ import numpy as np
 import pytest
 
 import launch_cases as LC
+import parity
 import pyoracle
 from kpsim import abi, model, native, synth
 
@@ -106,15 +107,13 @@ def test_patches_reach_launch(ctx, golden):
     LC.assert_same(dev, orc)
 
 
-def test_solve_rejects_over_64_reserved_offerings(ctx, golden):
-    """Solve keeps the reserved offerings in one 64-bit table (ResvTab); a larger catalog is refused loudly (the launch
-    path has no such limit)."""
+def test_solve_over_64_reserved_offerings(ctx, golden):
+    """Solve keeps the reserved offerings in multi-word rows (ResvTab.w words): a 70-reservation catalog solves
+    bit-identically to the oracle (tests/test_gpu_wide_reserved.py covers up to 700)."""
     cat = synth.config5_catalog(golden, n_default=50, n_block=20)
-    ctx.upload_catalog(model.CatalogView(cat))
+    cv = model.CatalogView(cat)
     prob = synth.config2(n_pods=200, catalog=cat)
-    with pytest.raises(native.KpError) as e:
-        ctx.prepare(model.SolveInputView(prob))
-    assert e.value.status == abi.KP_E_UNSUPPORTED
+    parity.assert_same(parity.run_device(ctx, prob, cv), parity.run_oracle(prob, cv))
 
 
 def test_empty_batch(ctx, golden):
