@@ -79,6 +79,10 @@ struct KpCons {
     // hostname pod affinity (a self-selecting pod bootstraps a domain only when no hostname domain holds a selected
     // pod): per probe, the positive-domain count of each such group after its candidates' pods come off —
     // hpos0[(single ? candidate : n_cand + prefix) * n_ha + ga]; tg_ha[g] = ga or -1
+    // late topology identities (KpDev.tg_late) each probe's NewTopology creates: single-node probe ci / multi-node
+    // probe i (null: none)
+    const uint64_t* born_s;
+    const uint64_t* born_m;
     int32_t n_ha;
     const int32_t* hpos0;
     const int32_t* tg_ha;

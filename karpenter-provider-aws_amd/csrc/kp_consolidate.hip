@@ -33,6 +33,7 @@ struct ConsShared {
     int64_t nc_req[KP_MAX_R];
     int64_t st[CS_COUNT];
     uint64_t mro[KP_RO_W];  // RESV: the reserved-offering rows compatible with the probe's NodeClaim (its finalisation)
+    uint64_t born;          // TOPO: the probe's late topology identities created so far (ProbeTopo::born)
 };
 
 __device__ __forceinline__ int32_t ld32(const int32_t* p) {
@@ -227,6 +228,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
         P.dgk = k.pt_dgk;
         P.hpos = reinterpret_cast<int32_t*>(smem + k.off_hpos);
         P.ha = k.tg_ha;
+        P.born = &S.born;
         P.E = d.E;
         P.HG = k.HG;
     }
@@ -347,6 +349,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
             const int r0 = single ? k.dec_soff[gp] : k.dec_moff[gp], r1 = single ? k.dec_soff[gp + 1] : k.dec_moff[gp + 1];
             for (int r = r0; r < r1; r++) pt_init_row(d, P, k.dec_g[r], k.dec_v + (size_t)r * 64, lane);
             for (int ga = lane; ga < k.n_ha; ga += 64) P.hpos[ga] = k.hpos0[(size_t)(single ? gp : k.n_cand + gp) * k.n_ha + ga];
+            if (lane == 0) S.born = k.born_s ? (single ? k.born_s[gp] : k.born_m[gp]) : ~0ull;
         }
         // the probe's candidates are [c0, c1) and their pods one contiguous run of cand_pods (CSR in candidate order)
         const int po0 = k.cand_off[c0], po1 = k.cand_off[c1];
@@ -1159,6 +1162,8 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
             if (nx >= 0) {
                 relax_at = tail;
                 st_relax++;
+                // Topology.Update: the relaxed spec's new groups are created (one wave: its LDS ops stay in order)
+                if (TOPO && d.tg_late && lane == 0) S.born |= d.cls_birth[nx];
             }
             if (lane == 0) {
                 ring[tail % cap] = nent;

@@ -86,6 +86,7 @@ struct ClassCache {
     int ntc, ntr;               // topology groups constraining / recording the class
     int tc[KP_MAX_TOPO];        // group | self << 30
     int tc_ki[KP_MAX_TOPO];     // class-key index of a value-keyed group's key (-1 for hostname groups)
+    uint64_t tc_podhas[KP_MAX_TOPO];  // podDomains of the group's key: the class's strict requirements (KpTopoCons)
     int tr[KP_MAX_TOPO_REC];
     int tr_ki[KP_MAX_TOPO_REC]; // class-key index of the group's key, -1 when the class does not constrain it
 };
@@ -112,6 +113,7 @@ struct ProbeTopo {
     const uint64_t* dgk;   // [G] domains of buildDomainGroups (registered before any pod is counted)
     int32_t* hpos;         // LDS [n_ha]: hostname domains holding a selected pod, per hostname-affinity group
     const int32_t* ha;     // [G] hostname-affinity group index into hpos, or -1
+    uint64_t* born;        // LDS: the probe's born late identities (KpDev.tg_late)
     int E, HG;
 };
 
@@ -201,6 +203,7 @@ __device__ inline void fill_class_cache(const KpDev& d, int c, ClassCache& CC, i
         if (cons) {
             CC.tc[tid] = e;
             CC.tc_ki[tid] = ki;
+            CC.tc_podhas[tid] = d.cls_tce[d.cls_tcoff[c] + tid].podhas;
         } else {
             CC.tr[tid - CC.ntc] = e;
             CC.tr_ki[tid - CC.ntc] = ki;
@@ -481,7 +484,7 @@ __device__ __forceinline__ bool topo_narrow(const KpDev& d, const ClassCache& CC
             const uint64_t known = ld_u64(CT ? &pt->known[g] : &d.tg_known[g]);
             kn = valid && ((known >> lane) & 1ull);
             cnt = kn ? ld_i32(CT ? &pt->cnt[(size_t)g * 64 + lane] : &d.tg_cnt[(size_t)g * 64 + lane]) : 0;
-            pod_has = valid && req_has(d, k, lane, CC.hdr[ki], CC.words + CC.wsoff[ki]);
+            pod_has = valid && ((CC.tc_podhas[e] >> lane) & 1ull);
             rk = valid ? d.vrank[(size_t)k * 64 + lane] : 0xFFu;
         }
         const ReqHdr nh = ws.hdr[ki];
@@ -559,17 +562,19 @@ __device__ __forceinline__ bool topo_narrow(const KpDev& d, const ClassCache& CC
 
 // Topology.Record for a committed placement (one wave).  The merged requirements are ws for the class's keys and the
 // candidate's base digest (Ahdr / Aw) for the others; `host` is its hostname domain and `tmpl` its template (taints).
-// Counts(pod): forward groups selecting the class, through the spread node filter (owner's requirements with the
-// AllowUndefinedWellKnownLabels option when allow_wk, owner's tolerations); spread / affinity record a single-valued
-// domain, anti-affinity and inverse groups record every value (requirement.Values(), the excluded set of a complement).
+// Counts(pod): forward groups selecting the class, through the spread node filter (TopologyNodeFilter.Matches: the
+// requirements are Compatible with one of the filter rows tg_frow — the owner's nodeSelector with each remaining
+// required node-affinity term — with the AllowUndefinedWellKnownLabels option when allow_wk; the owner's
+// tolerations); spread / affinity record a single-valued domain, anti-affinity and inverse groups record every value
+// (requirement.Values(), the excluded set of a complement).
 __device__ inline bool topo_filter_compatible(const KpDev& d, const ClassCache& CC, const WaveScratch& ws,
-                                              const ReqHdr* Ahdr, const uint64_t* Aw, int owner, bool allow_wk, int lane,
+                                              const ReqHdr* Ahdr, const uint64_t* Aw, int row, bool allow_wk, int lane,
                                               bool exnode = false) {
     bool ok = true;
-    for (int i = d.cls_xkoff[owner] + lane; i < d.cls_xkoff[owner + 1]; i += 64) {
+    for (int i = d.cls_xkoff[row] + lane; i < d.cls_xkoff[row + 1]; i += 64) {
         const int k = d.cls_xkeys[i];
-        const ReqHdr B = d.cls_hdr[(size_t)owner * d.K + k];
-        const uint64_t* bw = d.cls_words + (size_t)owner * d.DW + d.woff[k];
+        const ReqHdr B = d.cls_hdr[(size_t)row * d.K + k];
+        const uint64_t* bw = d.cls_words + (size_t)row * d.DW + d.woff[k];
         const bool bno = op_notin_or_dne(req_op(B.flags, popc_words(bw, d.nw[k])));
         if (k == d.key_host && !exnode) {  // NodeClaim hostname In [placeholder]: only a complement without bounds admits it
             if (!((B.flags & RF_CMP) && !(B.flags & (RF_GT | RF_LT)))) ok = false;
@@ -591,12 +596,18 @@ __device__ inline bool topo_filter_compatible(const KpDev& d, const ClassCache& 
 }
 
 // exnode >= 0: the placement is on existing node exnode (its taints: ex_tol; its hostname is a real node name).
+// born: the late identities created so far (the FFD kernel's; a probe's is *pt->born).
 template <bool CT = false>
 __device__ __forceinline__ void topo_record(const KpDev& d, const ClassCache& CC, const WaveScratch& ws, const ReqHdr* Ahdr,
                                          const uint64_t* Aw, int host, int tmpl, bool allow_wk, int lane, int exnode = -1,
-                                         const ProbeTopo* pt = nullptr) {
+                                         const ProbeTopo* pt = nullptr, uint64_t born = ~0ull) {
+    if (CT && d.tg_late) born = *pt->born;
     for (int e = 0; e < CC.ntr; e++) {
         const int g = CC.tr[e], ki = CC.tr_ki[e];
+        if (d.tg_late) {  // a group Topology.Update has not created yet records nothing
+            const int lt = d.tg_late[g];
+            if (lt >= 0 && !((born >> lt) & 1ull)) continue;
+        }
         const int4 info = d.tg_info[g];
         const int type = info.x & TG_TYPE;
         const bool inv = info.x & TG_INVERSE;
@@ -605,9 +616,13 @@ __device__ __forceinline__ void topo_record(const KpDev& d, const ClassCache& CC
             const bool tolerated = exnode >= 0 ? ((d.ex_tol[(size_t)owner * d.EW + (exnode >> 6)] >> (exnode & 63)) & 1ull) != 0
                                                : ((d.tol[owner] >> tmpl) & 1ull) != 0;
             if ((pol & 2) && !tolerated) continue;
-            if ((pol & 1) && owner != CC.cls &&
-                !topo_filter_compatible(d, CC, ws, Ahdr, Aw, owner, allow_wk, lane, exnode >= 0))
-                continue;
+            if ((pol & 1) && owner != CC.cls) {
+                const int2 fr = d.tg_frow[g];
+                bool m = false;
+                for (int f = fr.x; f < fr.x + fr.y && !m; f++)
+                    m = topo_filter_compatible(d, CC, ws, Ahdr, Aw, f, allow_wk, lane, exnode >= 0);
+                if (!m) continue;
+            }
         }
         if (info.x & TG_HOST) {
             if (CT) {

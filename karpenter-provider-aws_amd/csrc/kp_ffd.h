@@ -75,6 +75,7 @@ struct FfdShared {
                                    // reservation-dependent rejections memoised so far may no longer hold
     int epoch;                     // lastLen generation: Queue.Push(pod, relaxed = true) clears lastLen
     int relaxed;                   // a pod relaxed since wave 0 last loaded its queue window (its lastLens are stale)
+    uint64_t born;                 // late topology identities created so far (KpDev.tg_late)
     int xstart;                    // every existing node < xstart has rejected the current shape
     uint64_t cur_tol;              // tolerations word of the current shape's class (bit 63: no requirement keys)
     int32_t cur_pq[KP_LDS_AXES];   // scaled quick-accept requests of the current shape
@@ -272,7 +273,7 @@ __device__ inline bool merge_noop(const KpDev& d, WaveScratch& ws, int nc, int c
 // every recorded domain comes from its digest (hostname groups: its host E + nc).  CF_TOPO_QREC guarantees that no
 // recording group needs the node-affinity filter of another class.  Lane i takes recording entry i (KpTopoRec) and its
 // key of the NodeClaim's digest, so the entries' loads form one round; the counts are then added entry by entry.
-__device__ inline void topo_record_quick(const KpDev& d, int c, int nc, int tmpl, int lane) {
+__device__ inline void topo_record_quick(const KpDev& d, int c, int nc, int tmpl, uint64_t born, int lane) {
     const int r0 = d.cls_troff[c], nr = d.cls_troff[c + 1] - r0;
     for (int base = 0; base < nr; base += 64) {
         const int i = base + lane;
@@ -282,7 +283,7 @@ __device__ inline void topo_record_quick(const KpDev& d, int c, int nc, int tmpl
         bool live = false;
         if (i < nr) {
             R = d.cls_tre[r0 + i];
-            live = !((R.skip >> tmpl) & 1ull);
+            live = !((R.skip >> tmpl) & 1ull) && (R.late < 0 || ((born >> R.late) & 1ull));
             if (live && !(R.flags & 8)) {
                 fl = d.nc_hdr[(size_t)nc * d.K + R.key].flags;
                 w = d.nc_words[(size_t)nc * d.DW + d.woff[R.key]];
@@ -449,7 +450,7 @@ static __device__ __attribute__((noinline)) int existing_topo_scan(const KpDev* 
     if (placed >= 0) {
         existing_topo_commit(d, S.CC, S.ws[0], placed, lane);
         topo_record(d, S.CC, S.ws[0], d.ex_hdr + (size_t)placed * K, d.ex_words + (size_t)placed * d.DW,
-                    placed, 0, false, lane, placed);
+                    placed, 0, false, lane, placed, nullptr, S.born);
         if (lane < d.n_active) {
             const int64_t x = S.pod_req[d.active_axes[lane]];
             if (x) atomicAdd((unsigned long long*)&d.ex_head[(size_t)lane * d.E + placed], (unsigned long long)(-x));
@@ -641,6 +642,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
         S.rel_flag = 0;
         S.epoch = 0;
         S.relaxed = 0;
+        S.born = d.born0;
         S.xstart = 0;
         S.seq = 0;
         S.err = 0;
@@ -1337,7 +1339,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                         if (lane < A) shr[lane * NQ + nc] -= S.cur_pq[lane];
                         if (lane < R && S.pod_req[lane])
                             atomicAdd((unsigned long long*)&d.nc_req[(size_t)nc * R + lane], (unsigned long long)S.pod_req[lane]);
-                        topo_record_quick(d, c, nc, tm, lane);
+                        topo_record_quick(d, c, nc, tm, S.born, lane);
                         if (lane == 0) {
                             skey[f]++;
                             d.pod_result[pod] = nc;
@@ -1585,7 +1587,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 }
                 if (TOPO_ON && (S.CC.flags & CF_TOPO))
                     topo_record(d, S.CC, S.ws[cw], d.nc_hdr + (size_t)nc * K, d.nc_words + (size_t)nc * d.DW,
-                                d.E + nc, d.nc_tmpl[nc], true, lane);
+                                d.E + nc, d.nc_tmpl[nc], true, lane, -1, nullptr, S.born);
                 if (lane < TW) d.nc_opts[(size_t)nc * TW + lane] = S.ws[cw].opts[lane];
                 if (lane < R && S.pod_req[lane])
                     atomicAdd((unsigned long long*)&d.nc_req[(size_t)nc * R + lane], (unsigned long long)S.pod_req[lane]);
@@ -1683,7 +1685,8 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                         if (RESV && d.resv_on) commit_reservations(d, sRcap, S.ws[wave], n, true, &S.rel_flag, lane);
                         if (TOPO_ON && (S.CC.flags & CF_TOPO))
                             topo_record(d, S.CC, S.ws[wave], d.cls_hdr + (size_t)(d.C + jj) * K,
-                                        d.cls_words + (size_t)(d.C + jj) * d.DW, d.E + n, jj, true, lane);
+                                        d.cls_words + (size_t)(d.C + jj) * d.DW, d.E + n, jj, true, lane, -1, nullptr,
+                                        S.born);
                         if (lane < TW) d.nc_opts[(size_t)n * TW + lane] = S.ws[wave].opts[lane];
                         for (int r = lane; r < R; r += 64)
                             __hip_atomic_store(&d.nc_req[(size_t)n * R + r], d.daemon[(size_t)jj * R + r] + S.pod_req[r],
@@ -1737,6 +1740,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                         d.pod_shape[pod] = d.shape_next[S.prev_shape];
                         S.epoch++;
                         S.relaxed = 1;
+                        if (d.tg_late) S.born |= d.cls_birth[nx];  // Topology.Update creates the spec's new groups
                     } else {
                         d.last_len[pod] = S.qcount;
                         if (PREF && d.last_ep) d.last_ep[pod] = S.epoch;

@@ -269,6 +269,14 @@ struct PrefExpansion {
     std::vector<std::vector<kp_requirement>> reqs;
     std::vector<std::vector<kp_toleration>> tols;
     std::vector<std::vector<kp_topology_term>> terms;
+    // per expanded class: the spread node filter (MakeTopologyNodeFilter: the nodeSelector with each remaining required
+    // node-affinity term, ORed; no preference) and, when a preferred node-affinity term is in force, the strict
+    // requirements (NewStrictPodRequirements: nodeSelector + the first remaining required term) that give podDomains
+    std::vector<std::vector<std::vector<kp_requirement>>> filt;
+    std::vector<std::vector<kp_requirement>> strict;
+    std::vector<uint8_t> has_strict;
+    std::vector<int32_t> origin;  // per expanded class: its input class
+    int n_input = 0;
 };
 
 // Persistent worker threads of a ctx for the host-side batch work of kp_launch_select (request encoding, result
@@ -562,6 +570,11 @@ struct kp_ctx {
     DBuf<int32_t> d_tg_hrow, d_tg_owner, d_tg_pol, d_tg_cnt0, d_tg_cnt, d_tg_hcnt0, d_tg_hcnt, d_tg_pos0, d_tg_pos,
         d_cls_tcoff, d_cls_tc, d_cls_troff, d_cls_tr;
     DBuf<KpTopoCons> d_cls_tce;
+    DBuf<int2> d_tg_frow;
+    DBuf<int32_t> d_tg_late;
+    DBuf<uint64_t> d_cls_birth, d_born_s, d_born_m;
+    int tg_nlate = 0;
+    std::vector<uint64_t> h_cls_birth;
     DBuf<KpTopoRec> d_cls_tre;
     DBuf<uint64_t> d_tg_known0, d_tg_known;
     DBuf<uint8_t> d_cls_kneutral, d_vrank;
@@ -1271,7 +1284,9 @@ namespace {
 struct HGroup {
     int type = 0, key = -1, owner = -1, skew = 0, mindom = 0, pol = 0, hrow = -1;
     bool host = false, inverse = false;
-    std::vector<uint8_t> sel;  // per class: namespace ∈ namespaces ∧ the label selector matches
+    std::vector<uint8_t> sel;   // per class: namespace ∈ namespaces ∧ the label selector matches
+    std::vector<uint8_t> memb;  // per class: the class owns the group (owner = the first)
+    int ident = -1;             // TopologyGroup.Hash() identity (topo_build)
 };
 struct TopoHost {
     std::vector<HGroup> g;
@@ -1279,7 +1294,29 @@ struct TopoHost {
     std::vector<std::vector<int>> neutral;    // per class: keys added to its digest only for narrowing
     int key_host = -1;
     int n_host = 0;
+    // groups created by Topology.Update on a relaxed pod (see topo_build): identity → bit among the late identities
+    // (-1: created by NewTopology whenever a pod owns it), the late identities each class owns
+    std::vector<int> ident_late;
+    std::vector<uint64_t> cls_birth;
+    int n_late = 0;
 };
+
+// hashstructure (FormatV2, SlicesAsSets) folds a slice by XOR of its elements' hashes: elements that occur an even
+// number of times cancel.  The identity string of such a slice keeps the elements of odd multiplicity, sorted.
+std::string parity_join(std::vector<std::string> v) {
+    std::sort(v.begin(), v.end());
+    std::string out;
+    for (size_t i = 0; i < v.size();) {
+        size_t j = i;
+        while (j < v.size() && v[j] == v[i]) j++;
+        if ((j - i) & 1) {
+            out += v[i];
+            out += '\x1f';
+        }
+        i = j;
+    }
+    return out;
+}
 
 // labels.Selector over pod labels (metav1.LabelSelector: matchLabels as In, matchExpressions In/NotIn/Exists/DNE)
 bool selector_matches(const kp_topology_term& t, const kp_pod_class& pc) {
@@ -1314,10 +1351,6 @@ static kp_status expand_preferences(const kp_solve_input* in, int pref_policy, P
             const char* e = in->nodepools[i].taints[j].effect;
             tol_pns |= e && !strcmp(e, "PreferNoSchedule");
         }
-    std::set<std::string> topo_keys;
-    for (int c = 0; c < C0; c++)
-        for (int i = 0; i < in->classes[c].n_topology; i++)
-            if (in->classes[c].topology[i].topology_key) topo_keys.insert(normalize(in->classes[c].topology[i].topology_key));
     struct St {
         int cls, origin, req_first;
         std::vector<int> pnode, paff, panti, spreads;
@@ -1340,38 +1373,16 @@ static kp_status expand_preferences(const kp_solve_input* in, int pref_policy, P
         for (int i = 0; i < pc.n_preferred_terms; i++) x.pnode.push_back(i);
         std::stable_sort(x.pnode.begin(), x.pnode.end(),
                          [&](int a, int b) { return pc.preferred_terms[a].weight > pc.preferred_terms[b].weight; });
-        bool honor = false;
         for (int i = 0; i < pc.n_topology; i++) {
             const kp_topology_term& t = pc.topology[i];
             if (t.type == KP_TOPO_SPREAD) {
                 x.spreads.push_back(i);
-                honor |= t.node_affinity_policy == KP_POLICY_HONOR;
             } else if (t.weight > 0) {
                 (t.type == KP_TOPO_AFFINITY ? x.paff : x.panti).push_back(i);
             }
         }
         for (auto* v : {&x.paff, &x.panti})
             std::stable_sort(v->begin(), v->end(), [&](int a, int b) { return pc.topology[a].weight > pc.topology[b].weight; });
-        // the topology node filter takes the nodeSelector with EVERY required term (ORed) and no preference; pod domains
-        // come from the strict requirements: combinations that would need those apart are refused, not approximated
-        if (honor && pc.n_required_terms > 1) {
-            err = "a spread with nodeAffinityPolicy Honor on a pod with several required node-affinity terms";
-            return KP_E_UNSUPPORTED;
-        }
-        if (pref_policy == KP_PREFERENCE_RESPECT && pc.n_preferred_terms > 0) {
-            if (honor) {
-                err = "a spread with nodeAffinityPolicy Honor on a pod with preferred node affinity";
-                return KP_E_UNSUPPORTED;
-            }
-            for (int i = 0; i < pc.n_preferred_terms; i++)
-                for (int j = 0; j < pc.preferred_terms[i].n_requirements; j++) {
-                    const char* k = pc.preferred_terms[i].requirements[j].key;
-                    if (k && topo_keys.count(normalize(k))) {
-                        err = "a preferred node-affinity term on a topology key";
-                        return KP_E_UNSUPPORTED;
-                    }
-                }
-        }
         st.push_back(std::move(x));
     }
     X.relax_next.assign(C0, -1);
@@ -1425,6 +1436,12 @@ static kp_status expand_preferences(const kp_solve_input* in, int pref_policy, P
     X.reqs.assign(CX, {});
     X.tols.assign(CX, {});
     X.terms.assign(CX, {});
+    X.filt.assign(CX, {});
+    X.origin.assign(CX, 0);
+    X.n_input = C0;
+    for (const St& x : st) X.origin[x.cls] = x.origin;
+    X.strict.assign(CX, {});
+    X.has_strict.assign(CX, 0);
     static const kp_toleration pns_tol = {"", KP_TOL_EXISTS, "", "PreferNoSchedule"};
     for (const St& x : st) {
         const kp_pod_class& pc = in->classes[x.origin];
@@ -1436,7 +1453,19 @@ static kp_status expand_preferences(const kp_solve_input* in, int pref_policy, P
             const kp_node_selector_term& t = pc.required_terms[x.req_first];
             rq.insert(rq.end(), t.requirements, t.requirements + t.n_requirements);
         }
+        auto& fl = X.filt[x.cls];
+        if (pc.n_required_terms == 0) {
+            fl.emplace_back(pc.requirements, pc.requirements + pc.n_requirements);
+        } else {
+            for (int i = x.req_first; i < pc.n_required_terms; i++) {
+                const kp_node_selector_term& t = pc.required_terms[i];
+                fl.emplace_back(pc.requirements, pc.requirements + pc.n_requirements);
+                fl.back().insert(fl.back().end(), t.requirements, t.requirements + t.n_requirements);
+            }
+        }
         if (pref_policy == KP_PREFERENCE_RESPECT && !x.pnode.empty()) {
+            X.strict[x.cls] = rq;
+            X.has_strict[x.cls] = 1;
             const kp_node_selector_term& t = pc.preferred_terms[x.pnode[0]];
             rq.insert(rq.end(), t.requirements, t.requirements + t.n_requirements);
         }
@@ -1473,15 +1502,37 @@ static kp_status expand_preferences(const kp_solve_input* in, int pref_policy, P
     return KP_OK;
 }
 
-// One forward group per (class, term) and one inverse group per required anti-affinity term (per-class groups decide
-// exactly like Go's hash-shared ones: groups that share a hash count the same pods).  Interns the topology keys.
+// Topology groups ([core] scheduling/topology.go Update / updateInverseAntiAffinity, topologygroup.go Hash): Go keeps
+// one group per TopologyGroup.Hash() — topology key, type, namespaces, label selector, maxSkew and the node filter
+// (MakeTopologyNodeFilter: the requirement key sets of the nodeSelector with each required term, the policies, the
+// tolerations); hashstructure skips unexported fields, so requirement values and minDomains are not part of it.  Here
+// the (class, term) groups whose identities AND semantics agree are one group owned by all those classes; groups of one
+// identity whose filter values / minDomains differ stay apart (Go would keep the first pod's, DESIGN.md §4 lists this).
+// A group is created by NewTopology when a pod that owns it is in the batch, or by Topology.Update when a pod relaxes
+// into a spec that owns it (countDomains then counts only the bound pods): an identity that only a relaxed stage can
+// own — its other owners do not include that stage's input class — is "late", born on the device when the first pod
+// relaxes into an owner (at most 64 such identities).  Interns the topology keys.
 static kp_status topo_build(kp_ctx* c, const kp_solve_input* in, const std::vector<std::map<int, HReq>>& creq,
-                            TopoHost& th, std::string& err) {
+                            const std::vector<std::vector<std::map<int, HReq>>>& cfilt, TopoHost& th, std::string& err) {
     const int C = in->n_classes;
+    const PrefExpansion& X = c->pref;
     th = TopoHost();
     th.cons.assign(C, {});
     th.rec.assign(C, {});
     th.neutral.assign(C, {});
+    std::map<std::string, int> gidx;    // identity + semantics → group
+    std::map<std::string, int> idents;  // identity → index
+    auto hreq_str = [](const HReq& q) {
+        std::string r = std::to_string(q.key) + (q.complement ? "!" : "=");
+        for (int v : q.vals) r += std::to_string(v) + ",";
+        if (q.has_gt) r += ">" + std::to_string(q.gt);
+        if (q.has_lt) r += "<" + std::to_string(q.lt);
+        return r;
+    };
+    auto tol_str = [](const kp_toleration& t) {
+        return std::string(t.key ? t.key : "") + "\x1d" + std::to_string(t.op) + "\x1d" + (t.value ? t.value : "") + "\x1d" +
+               (t.effect ? t.effect : "");
+    };
     for (int i = 0; i < C; i++) {
         const kp_pod_class& pc = in->classes[i];
         for (int q = 0; q < pc.n_topology; q++) {
@@ -1503,32 +1554,127 @@ static kp_status topo_build(kp_ctx* c, const kp_solve_input* in, const std::vect
                     err = "label selector operators are In / NotIn / Exists / DoesNotExist";
                     return KP_E_INVALID;
                 }
-            const int key = c->sol.key(normalize(x.topology_key));
+            const std::string nkey = normalize(x.topology_key);
+            const int key = c->sol.key(nkey);
+            const bool spread = x.type == KP_TOPO_SPREAD;
+            // identity fields shared by the forward and inverse group
+            std::set<std::string> nss;
+            if (spread || x.n_namespaces <= 0) nss.insert(ns_of(pc));
+            else
+                for (int n = 0; n < x.n_namespaces; n++) nss.insert(x.namespaces[n] ? x.namespaces[n] : "");
+            std::string base = std::to_string(x.type) + "\x1e" + nkey + "\x1e";
+            for (auto& n : nss) base += n + "\x1f";
+            base += "\x1e";
+            if (x.n_selector < 0) {
+                base += "nil";
+            } else {
+                std::vector<std::string> el;
+                for (int j = 0; j < x.n_selector; j++) {
+                    const kp_requirement& r = x.selector[j];
+                    std::vector<std::string> vs;
+                    for (int v = 0; v < r.n_values; v++) vs.push_back(r.values[v] ? r.values[v] : "");
+                    el.push_back(std::string(r.key) + "\x1d" + std::to_string(r.op) + "\x1d" + parity_join(vs));
+                }
+                base += "sel" + parity_join(el);
+            }
+            base += "\x1e" + std::to_string(spread ? x.max_skew : INT32_MAX) + "\x1e";
+            std::vector<uint8_t> sel(C, 0);
+            for (int o = 0; o < C; o++) {
+                const kp_pod_class& oc = in->classes[o];
+                bool ns_ok = false;
+                if (spread || x.n_namespaces <= 0) ns_ok = !strcmp(ns_of(oc), ns_of(pc));
+                else
+                    for (int n = 0; n < x.n_namespaces; n++) ns_ok = ns_ok || (x.namespaces[n] && !strcmp(x.namespaces[n], ns_of(oc)));
+                sel[o] = ns_ok && selector_matches(x, oc);
+            }
+            const int pol = spread ? (x.node_affinity_policy == KP_POLICY_HONOR ? 1 : 0) | (x.node_taints_policy == KP_POLICY_HONOR ? 2 : 0) : 0;
             for (int inv = 0; inv < 2; inv++) {
                 if (inv && (x.type != KP_TOPO_ANTI_AFFINITY || preferred)) break;  // inverse: required anti-affinity only
+                std::string id = (inv ? "I\x1e" : "F\x1e") + base;
+                std::string sig = std::to_string(spread && x.min_domains > 0 ? x.min_domains : 0) + "\x1e";
+                for (uint8_t b : sel) sig += (char)('0' + b);
+                if (spread) {  // the node filter (a forward group: spreads have no inverse group)
+                    std::vector<std::string> ks;
+                    for (auto& f : X.filt[i]) {
+                        std::set<std::string> keys;
+                        for (auto& r : f)
+                            if (r.key) keys.insert(normalize(r.key));
+                        std::string k;
+                        for (auto& kk : keys) k += kk + "\x1c";
+                        ks.push_back(k);
+                    }
+                    std::vector<std::string> tl;
+                    for (int t = 0; t < pc.n_tolerations; t++) tl.push_back(tol_str(pc.tolerations[t]));
+                    id += parity_join(ks) + "\x1e" + std::to_string(pol) + "\x1e" + parity_join(tl);
+                    if (pol & 1) {  // filter values: one requirement set per filter row, ORed
+                        std::set<std::string> rows;
+                        for (auto& m : cfilt[i]) {
+                            std::string r;
+                            for (auto& kv : m) r += hreq_str(kv.second) + ";";
+                            rows.insert(r);
+                        }
+                        sig += "\x1e";
+                        for (auto& r : rows) sig += r + "|";
+                    }
+                    if (pol & 2) {
+                        std::set<std::string> ts(tl.begin(), tl.end());
+                        sig += "\x1e";
+                        for (auto& t : ts) sig += t + "|";
+                    }
+                }
+                auto iit = idents.find(id);
+                const int ident = iit != idents.end() ? iit->second : (int)idents.size();
+                if (iit == idents.end()) idents[id] = ident;
+                const std::string gk = id + "\x1b" + sig;
+                auto git = gidx.find(gk);
+                if (git != gidx.end()) {
+                    th.g[git->second].memb[i] = 1;
+                    continue;
+                }
                 HGroup g;
                 g.type = x.type;
                 g.key = key;
                 g.inverse = inv == 1;
                 g.owner = i;
-                g.skew = x.type == KP_TOPO_SPREAD ? x.max_skew : INT32_MAX;
-                g.mindom = x.type == KP_TOPO_SPREAD && x.min_domains > 0 ? x.min_domains : 0;
-                if (x.type == KP_TOPO_SPREAD)
-                    g.pol = (x.node_affinity_policy == KP_POLICY_HONOR ? 1 : 0) | (x.node_taints_policy == KP_POLICY_HONOR ? 2 : 0);
-                g.sel.assign(C, 0);
-                for (int o = 0; o < C; o++) {
-                    const kp_pod_class& oc = in->classes[o];
-                    bool ns_ok = false;
-                    if (x.type == KP_TOPO_SPREAD || x.n_namespaces <= 0) ns_ok = !strcmp(ns_of(oc), ns_of(pc));
-                    else
-                        for (int n = 0; n < x.n_namespaces; n++) ns_ok = ns_ok || (x.namespaces[n] && !strcmp(x.namespaces[n], ns_of(oc)));
-                    g.sel[o] = ns_ok && selector_matches(x, oc);
-                }
+                g.skew = spread ? x.max_skew : INT32_MAX;
+                g.mindom = spread && x.min_domains > 0 ? x.min_domains : 0;
+                g.pol = pol;
+                g.sel = sel;
+                g.memb.assign(C, 0);
+                g.memb[i] = 1;
+                g.ident = ident;
+                gidx[gk] = (int)th.g.size();
                 th.g.push_back(std::move(g));
             }
         }
     }
     if (th.g.empty()) return KP_OK;
+    // late identities: a relaxed stage owns it and its input class does not
+    const int NI = (int)idents.size();
+    const int C0 = X.n_input;
+    std::vector<std::vector<uint8_t>> own0(NI);  // identity → input classes owning it at stage 0
+    for (auto& own : own0) own.assign(std::max(C0, 1), 0);
+    for (const HGroup& g : th.g)
+        for (int o = 0; o < C && o < C0; o++)
+            if (g.memb[o]) own0[g.ident][o] = 1;
+    th.ident_late.assign(NI, -1);
+    for (const HGroup& g : th.g) {
+        if (th.ident_late[g.ident] >= 0) continue;
+        for (int o = C0; o < C; o++)
+            if (g.memb[o] && !own0[g.ident][X.origin[o]]) {
+                if (th.n_late >= 64) {
+                    err = "more than 64 topology groups that only relaxed pods own";
+                    return KP_E_UNSUPPORTED;
+                }
+                th.ident_late[g.ident] = th.n_late++;
+                break;
+            }
+    }
+    th.cls_birth.assign(C, 0);
+    for (const HGroup& g : th.g)
+        if (th.ident_late[g.ident] >= 0)
+            for (int o = 0; o < C; o++)
+                if (g.memb[o]) th.cls_birth[o] |= 1ull << th.ident_late[g.ident];
     th.key_host = c->sol.key("kubernetes.io/hostname");
     for (int gi = 0; gi < (int)th.g.size(); gi++) {
         HGroup& g = th.g[gi];
@@ -1537,9 +1683,9 @@ static kp_status topo_build(kp_ctx* c, const kp_solve_input* in, const std::vect
         for (int o = 0; o < C; o++) {
             if (g.inverse) {
                 if (g.sel[o]) th.cons[o].push_back(gi | (g.sel[o] << 30));
-                if (g.owner == o) th.rec[o].push_back(gi);
+                if (g.memb[o]) th.rec[o].push_back(gi);
             } else {
-                if (g.owner == o) th.cons[o].push_back(gi | (g.sel[o] << 30));
+                if (g.memb[o]) th.cons[o].push_back(gi | (g.sel[o] << 30));
                 if (g.sel[o]) th.rec[o].push_back(gi);
             }
         }
@@ -1577,7 +1723,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     if (!ctx->have_catalog) return fail(ctx, KP_E_STATE, "kp_solve before kp_catalog_upload");
     if (!ctx->solve_unsupported.empty()) return fail(ctx, KP_E_UNSUPPORTED, "Solve: " + ctx->solve_unsupported);
     if (ctx->has_reserved && !ctx->ro_ok)
-        return fail(ctx, KP_E_UNSUPPORTED, "Solve over a catalog with more than 64 reserved offerings");
+        return fail(ctx, KP_E_UNSUPPORTED, "Solve over a catalog with more than KP_MAX_RO (1024) reserved offerings");
     const auto t0 = clk::now();
     HIPCHK(hipSetDevice(ctx->device));
     kp_ctx* c = ctx;
@@ -1606,6 +1752,24 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     std::string err;
     for (int i = 0; i < C; i++)
         if (!build_hreqs(c, in->classes[i].requirements, in->classes[i].n_requirements, creq[i], err)) return fail(ctx, KP_E_INVALID, err);
+    // spread node filters of classes with a nodeAffinityPolicy Honor spread, and strict requirements (podDomains) of
+    // classes whose requirements carry a preferred node-affinity term (expand_preferences)
+    std::vector<std::vector<std::map<int, HReq>>> cfilt(C);
+    std::vector<std::map<int, HReq>> cstrict(C);
+    for (int i = 0; i < C; i++) {
+        bool honor = false;
+        for (int q = 0; q < in->classes[i].n_topology; q++)
+            honor |= in->classes[i].topology[q].type == KP_TOPO_SPREAD &&
+                     in->classes[i].topology[q].node_affinity_policy == KP_POLICY_HONOR;
+        if (honor)
+            for (auto& f : c->pref.filt[i]) {
+                cfilt[i].emplace_back();
+                if (!build_hreqs(c, f.data(), (int)f.size(), cfilt[i].back(), err)) return fail(ctx, KP_E_INVALID, err);
+            }
+        if (c->pref.has_strict[i] &&
+            !build_hreqs(c, c->pref.strict[i].data(), (int)c->pref.strict[i].size(), cstrict[i], err))
+            return fail(ctx, KP_E_INVALID, err);
+    }
     // templates: NodePools ordered by weight desc, name asc ([core] NodePoolList.OrderByWeight)
     std::vector<int> npo(in->n_nodepools);
     for (int i = 0; i < in->n_nodepools; i++) npo[i] = i;
@@ -1634,7 +1798,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     }
     TopoHost th;
     {
-        const kp_status ts = topo_build(c, in, creq, th, err);
+        const kp_status ts = topo_build(c, in, creq, cfilt, th, err);
         if (ts != KP_OK) return fail(ctx, ts, err);
     }
     // existing nodes (ExistingNode, [core] scheduling/existingnode.go NewExistingNode): requirements =
@@ -1807,6 +1971,33 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
                 c->any_min_values = true;
                 if (kv.first < c->Kcat && (c->cat_kflags[kv.first] & KF_CAT_MULTI)) c->min_multi = true;
             }
+    }
+    // spread node-filter rows after the templates: each Honor spread group's filter is its owner's rows
+    std::vector<int2> frow(C, make_int2(0, 0));
+    xkoff.resize(CT + 1, xkoff[C]);  // template rows: no keys
+    {
+        int F = 0;
+        for (int i = 0; i < C; i++) F += (int)cfilt[i].size();
+        chdr.resize((size_t)(CT + F) * K);
+        cwords.resize((size_t)(CT + F) * DW, 0);
+        int row = CT;
+        for (int i = 0; i < C; i++) {
+            frow[i] = make_int2(row, (int)cfilt[i].size());
+            for (auto& rq : cfilt[i]) {
+                for (auto& kv : rq) {
+                    const HReq& q = kv.second;
+                    ReqHdr h{};
+                    h.flags = RF_DEF | (q.complement ? RF_CMP : 0u) | (q.has_gt ? RF_GT : 0u) | (q.has_lt ? RF_LT : 0u);
+                    h.gt = q.gt;
+                    h.lt = q.lt;
+                    chdr[(size_t)row * K + q.key] = h;
+                    for (int vv : q.vals) cwords[(size_t)row * DW + woff[q.key] + vv / 64] |= 1ull << (vv % 64);
+                    xkeys.push_back(q.key);
+                }
+                xkoff.push_back((int)xkeys.size());
+                row++;
+            }
+        }
     }
     // ---- templates: taints, daemon overhead, limits, instance-type rows ----
     std::vector<uint64_t> tol(std::max(C, 1), 0);
@@ -2072,10 +2263,13 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         std::vector<int64_t> ccount(std::max(C, 1), 0);
         for (int p = 0; p < P; p++) ccount[in->pods.class_id[p]]++;
         for (const HGroup& g : th.g)
-            if (!g.inverse && g.host && g.owner >= 0 && g.owner < C && g.sel[g.owner]) {
+            if (!g.inverse && g.host) {
+                int64_t m = 0;  // pods of the self-selecting classes that own the group
+                for (int o = 0; o < C; o++)
+                    if (g.memb[o] && g.sel[o]) m += ccount[o];
                 int64_t n = 0;
-                if (g.type == KP_TOPO_ANTI_AFFINITY) n = ccount[g.owner];
-                else if (g.type == KP_TOPO_SPREAD && g.skew > 0) n = (ccount[g.owner] + g.skew - 1) / g.skew;
+                if (g.type == KP_TOPO_ANTI_AFFINITY) n = m;
+                else if (g.type == KP_TOPO_SPREAD && g.skew > 0) n = (m + g.skew - 1) / g.skew;
                 dense = std::max(dense, n - E);
             }
     }
@@ -2124,6 +2318,8 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         const int G1 = std::max(G, 1);
         std::vector<int4> tinfo(G1);
         std::vector<int32_t> thr_row(G1, -1), towner(G1, 0), tpol(G1, 0), tcnt0((size_t)G1 * 64, 0), tpos0(G1, 0);
+        std::vector<int2> tfrow(G1, make_int2(0, 0));
+        std::vector<int32_t> tlate(G1, -1);
         std::vector<uint64_t> tknown0(G1, 0);
         std::vector<int32_t> tcoff(C + 1, 0), tcl, troff(C + 1, 0), trl;
         std::vector<KpTopoCons> tce;
@@ -2187,6 +2383,8 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
                 thr_row[gi] = g.hrow;
                 towner[gi] = g.owner;
                 tpol[gi] = g.pol;
+                if (!g.inverse && g.type == KP_TOPO_SPREAD && (g.pol & 1)) tfrow[gi] = frow[g.owner];
+                tlate[gi] = th.ident_late[g.ident];
                 if (g.host) continue;
                 for (auto& kv : domains_of(g.key)) {
                     bool ok = !(g.type == KP_TOPO_SPREAD && (g.pol & 2));
@@ -2231,9 +2429,13 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
                         t.key = -1 - g.hrow;
                     } else {
                         t.key = g.key;
+                        // podDomains: the strict requirements' (no preferred term) requirement for the key, else Exists
+                        const bool strict = c->pref.has_strict[i] != 0;
+                        const auto sit = strict ? cstrict[i].find(g.key) : cstrict[i].end();
                         for (int v = 0; v < 64 && v < nval[g.key]; v++) {
                             t.vmask |= 1ull << v;
-                            if (digest_has(i, g.key, v)) t.podhas |= 1ull << v;
+                            const bool has = strict ? (sit == cstrict[i].end() || hreq_has(sit->second, v)) : digest_has(i, g.key, v);
+                            if (has) t.podhas |= 1ull << v;
                         }
                     }
                     tce.push_back(t);
@@ -2244,6 +2446,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
                     r.g = gi;
                     r.flags = g.type | (g.inverse ? 4 : 0) | (g.host ? 8 : 0);
                     r.key = g.host ? -1 - g.hrow : g.key;
+                    r.late = th.ident_late[g.ident];
                     if (!g.inverse && g.type == KP_TOPO_SPREAD && (g.pol & 2))
                         for (int j = 0; j < NT; j++)
                             if (!((tol[g.owner] >> j) & 1ull)) r.skip |= 1ull << j;
@@ -2259,18 +2462,24 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
                     if (e.first == k) return e.second;
                 return -1;
             };
-            auto node_compatible_with = [&](int j, int owner) {  // Compatible(node labels, owner reqs), no wk allowance
-                for (auto& kv : creq[owner]) {
-                    const HReq& q = kv.second;
-                    const int v = node_val(j, kv.first);
-                    const bool qno = (q.complement && !q.vals.empty()) || (!q.complement && q.vals.empty());
-                    if (v < 0) {
-                        if (!qno) return false;
-                        continue;
+            // TopologyNodeFilter.MatchesRequirements: Compatible(node labels, a filter row of the owner), no wk allowance
+            auto node_compatible_with = [&](int j, int owner) {
+                for (auto& rq : cfilt[owner]) {
+                    bool ok = true;
+                    for (auto& kv : rq) {
+                        const HReq& q = kv.second;
+                        const int v = node_val(j, kv.first);
+                        const bool qno = (q.complement && !q.vals.empty()) || (!q.complement && q.vals.empty());
+                        if (v < 0) {
+                            if (!qno) ok = false;
+                        } else if (!hreq_has(q, v)) {
+                            ok = false;
+                        }
+                        if (!ok) break;
                     }
-                    if (!hreq_has(q, v)) return false;
+                    if (ok) return true;
                 }
-                return true;
+                return false;
             };
             auto node_tolerated_by = [&](int j, int owner) {
                 const kp_existing_node& en = in->existing[j];
@@ -2284,7 +2493,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
             auto count_pod = [&](int j, int b, int cand) -> bool {
                 for (int gi = 0; gi < G; gi++) {
                     const HGroup& g = th.g[gi];
-                    if (g.inverse ? g.owner != b : !g.sel[b]) continue;
+                    if (g.inverse ? !g.memb[b] : !g.sel[b]) continue;
                     if (!g.inverse && g.type == KP_TOPO_SPREAD) {
                         if ((g.pol & 1) && !node_compatible_with(j, g.owner)) continue;
                         if ((g.pol & 2) && !node_tolerated_by(j, g.owner)) continue;
@@ -2337,6 +2546,17 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         HIPCHK(c->d_tg_hrow.upload(thr_row, s));
         HIPCHK(c->d_tg_owner.upload(towner, s));
         HIPCHK(c->d_tg_pol.upload(tpol, s));
+        HIPCHK(c->d_tg_frow.upload(tfrow, s));
+        // late identities (topo_build): born at the start when a pod of the Solve (its input class) owns them
+        c->tg_nlate = G > 0 ? th.n_late : 0;
+        c->h_cls_birth.assign(std::max(C, 1), 0);
+        d.born0 = 0;
+        if (c->tg_nlate > 0) {
+            HIPCHK(c->d_tg_late.upload(tlate, s));
+            c->h_cls_birth.assign(th.cls_birth.begin(), th.cls_birth.end());
+            HIPCHK(c->d_cls_birth.upload(c->h_cls_birth, s));
+            for (int i = 0; i < P; i++) d.born0 |= th.cls_birth[in->pods.class_id[i]];
+        }
         HIPCHK(c->d_tg_cnt0.upload(tcnt0, s));
         HIPCHK(c->d_tg_cnt.ensure(tcnt0.size()));
         HIPCHK(c->d_tg_known0.upload(tknown0, s));
@@ -2483,6 +2703,9 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.tg_hrow = c->d_tg_hrow.p;
     d.tg_owner = c->d_tg_owner.p;
     d.tg_pol = c->d_tg_pol.p;
+    d.tg_frow = c->d_tg_frow.p;
+    d.tg_late = c->tg_nlate > 0 ? c->d_tg_late.p : nullptr;
+    d.cls_birth = c->tg_nlate > 0 ? c->d_cls_birth.p : nullptr;
     d.tg_cnt = c->d_tg_cnt.p;
     d.tg_known = c->d_tg_known.p;
     d.tg_hcnt = c->d_tg_hcnt.p;
@@ -2829,7 +3052,7 @@ static kp_status cons_prepare_one(kp_ctx* ctx, const kp_consolidate_input* in) t
     ctx->cons_prep_valid = false;
     ctx->cons_gen++;  // cached pass rows and read-backs of kp_consolidate_command are stale
     if (ctx->has_reserved && !ctx->ro_ok)
-        return fail(ctx, KP_E_UNSUPPORTED, "consolidation over a catalog with more than 64 reserved offerings");
+        return fail(ctx, KP_E_UNSUPPORTED, "consolidation over a catalog with more than KP_MAX_RO (1024) reserved offerings");
     if (!ctx->solve_unsupported.empty()) return fail(ctx, KP_E_UNSUPPORTED, "consolidation: " + ctx->solve_unsupported);
     if (in->mode != KP_CONSOLIDATE_SINGLE && in->mode != KP_CONSOLIDATE_MULTI)
         return fail(ctx, KP_E_INVALID, "unknown consolidation mode");
@@ -3022,6 +3245,24 @@ static kp_status cons_prepare_one(kp_ctx* ctx, const kp_consolidate_input* in) t
         for (int i = 0; i < nm; i++) c->cons_n_mut += mm[i];
         HIPCHK(c->d_mut_s.upload(ms, s));
         HIPCHK(c->d_mut_m.upload(mm, s));
+        // late topology identities a probe's NewTopology creates: owned by its pending pods or its candidates' pods
+        k.born_s = k.born_m = nullptr;
+        if (c->tg_nlate > 0) {
+            uint64_t bp = 0;
+            for (int i = 0; i < in->n_pending; i++) bp |= c->h_cls_birth[cl.pods.class_id[in->pending[i]]];
+            std::vector<uint64_t> bs(std::max(NC, 1), bp), bm(std::max(nm, 1), bp);
+            uint64_t acc = bp;
+            for (int ci = 0; ci < NC; ci++) {
+                for (int q = 0; q < in->candidates[ci].n_pods; q++)
+                    bs[ci] |= c->h_cls_birth[cl.pods.class_id[in->candidates[ci].pods[q]]];
+                acc |= bs[ci];
+                if (ci >= 1 && ci - 1 < nm) bm[ci - 1] = acc;  // multi-node probe i covers candidates [0, i + 2)
+            }
+            HIPCHK(c->d_born_s.upload(bs, s));
+            HIPCHK(c->d_born_m.upload(bm, s));
+            k.born_s = c->d_born_s.p;
+            k.born_m = c->d_born_m.p;
+        }
     }
     HIPCHK(c->d_next.ensure(3));
     HIPCHK(c->d_rank.ensure(std::max(P, 1)));

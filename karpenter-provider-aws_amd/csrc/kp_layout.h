@@ -109,7 +109,7 @@ struct KpTopoCons {
 // skip = the templates on which TopologyNodeFilter's taint policy leaves the placement uncounted (a spread group with
 // nodeTaintsPolicy Honor whose owner does not tolerate the template).
 struct KpTopoRec {
-    int32_t g, key, flags, pad;
+    int32_t g, key, flags, late;  // late: the group's late-identity bit or -1 (KpDev.tg_late)
     uint64_t skip;
 };
 
@@ -231,7 +231,8 @@ struct KpDev {
     uint8_t* ex_static;              // [E] Fits holds on every inactive axis and no available quantity is negative
     uint64_t* XT;                    // [C][EW] taints tolerated ∧ static fit ∧ Requirements.Compatible(node, class)
     const uint64_t* ex_tol;          // [C][EW] the class tolerates the node's taints
-    const int32_t* cls_xkoff;        // [C+1] CSR of every key a pod class constrains (incl. hostname)
+    const int32_t* cls_xkoff;        // [C+NT+F+1] CSR of every key a digest row constrains (incl. hostname): pod
+                                     // classes, templates (empty), then the F spread node-filter rows (tg_frow)
     const int32_t* cls_xkeys;
     int32_t ex_mayfix;               // some class has a NotIn/DoesNotExist key: Add may change node requirements
 
@@ -246,6 +247,13 @@ struct KpDev {
     const int32_t* tg_hrow;          // [G] row of tg_hcnt (hostname groups), else -1
     const int32_t* tg_owner;         // [G] class owning the term (spread node filter)
     const int32_t* tg_pol;           // [G] spread node filter: bit0 nodeAffinityPolicy Honor, bit1 nodeTaintsPolicy Honor
+    const int2* tg_frow;             // [G] bit0 of tg_pol: the filter's digest rows [x, x + y) of cls_hdr / cls_xkoff
+    // groups that Topology.Update creates when a pod relaxes into a spec owning them (kp_host.cpp topo_build): bit of
+    // the group's late identity or -1 (null: none); cls_birth[c] = late identities class c owns (a pod relaxing into c
+    // creates them); born0 = those a pod of the Solve owns from the start.  Records skip a late group until it is born.
+    const int32_t* tg_late;
+    const uint64_t* cls_birth;
+    uint64_t born0;
     int32_t* tg_cnt;                 // [G][64] counts by value id (value-keyed groups)
     uint64_t* tg_known;              // [G] value ids present in the group's domains map
     int32_t* tg_hcnt;                // [hostname groups][HN]

@@ -25,7 +25,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <map>
 #include <memory>
+#include <set>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -121,6 +123,11 @@ struct TopoTerm {
 
 struct PodClass {
     Reqs reqs;
+    // MakeTopologyNodeFilter's requirements: the nodeSelector with each remaining required node-affinity term (ORed),
+    // no preference; and NewStrictPodRequirements (podDomains in AddRequirements) when a preferred term is in reqs
+    std::vector<Reqs> filter;
+    Reqs strict;
+    bool has_strict = false;
     std::vector<Toleration> tols;
     std::string ns = "default";
     std::map<std::string, std::string> labels;
@@ -134,6 +141,7 @@ struct PodClass {
 // Register their hostnames in every hostname group), so only recorded hosts are stored.
 struct TopoGroup {
     int type = 0, key = -1;
+    int late = -1;             // late identity bit (build_topology): created by Topology.Update when a pod relaxes
     bool host = false;
     bool inverse = false;      // inverseTopologyGroups (updateInverseAntiAffinity): constrains the pods it selects
     int owner = -1;            // class that owns the term
@@ -218,6 +226,13 @@ struct Solver {
     std::vector<TopoGroup> groups;    // Topology.topologyGroups ∪ inverseTopologyGroups
     std::vector<TopoGroup> groups_dg; // ... as buildDomainGroups left them, before countDomains
     std::vector<std::vector<int>> t_cons, t_rec;  // per class: groups that constrain / count its pods
+    // TopologyGroup.Hash() identities that only a relaxed spec owns (see build_topology): per class, the late identities
+    // it owns (a pod relaxing into the class creates them); born = those created so far in this simulation
+    std::vector<uint64_t> cls_birth;
+    int n_late = 0;
+    uint64_t born = ~0ull;
+    std::vector<int> cls_origin;  // per class: its input class
+    int n_input = 0;
     kp_solve_stats stats{};
     // ReservationManager ([core] scheduling/reservationmanager.go): capacity per reservation ID, the least
     // ReservationCapacity among the offerings that carry the ID; NodeClaims hold IDs (NodeClaim.reservedOfferings).
@@ -414,7 +429,8 @@ struct Solver {
         Reqs topo = r;
         for (int gi : t_cons[c]) {
             const TopoGroup& g = groups[gi];
-            const Req podDom = pc.reqs.get(g.key);  // Exists when the pod does not constrain the key
+            // podDomains: the strict requirements' (no preferred term) requirement for the key; Exists without one
+            const Req podDom = (pc.has_strict ? pc.strict : pc.reqs).get(g.key);
             const Req nodeDom = r.get(g.key);
             const Req dom = topo_get(g, c, podDom, nodeDom);
             if (dom.Len() == 0) return false;  // topologyError
@@ -424,6 +440,12 @@ struct Solver {
         r.add_all(D, topo);
         return true;
     }
+    // TopologyNodeFilter.MatchesRequirements: Compatible with one of the filter's requirement sets
+    bool filter_matches(const PodClass& fc, const Reqs& r, bool allow_wk) const {
+        for (const Reqs& f : fc.filter)
+            if (reqs_compatible(D, r, f, allow_wk)) return true;
+        return false;
+    }
     // Topology.Record(pod, taints, requirements): every group whose Counts(pod) holds records the domain(s) the pod
     // lands in; inverse groups owned by the pod record every value of the requirement.
     void topo_record(int li, const Reqs& r, const std::vector<Taint>& taints, bool allow_wk) {
@@ -431,11 +453,12 @@ struct Solver {
         if (t_rec.empty()) return;
         for (int gi : t_rec[c]) {
             TopoGroup& g = groups[gi];
+            if (g.late >= 0 && !((born >> g.late) & 1ull)) continue;  // not created yet
             const Req dom = r.get(g.key);
             if (!g.inverse) {
                 if (g.type == KP_TOPO_SPREAD) {  // TopologyNodeFilter.Matches
                     const PodClass& fc = (*cp)[g.owner];
-                    if (g.aff_pol == KP_POLICY_HONOR && !reqs_compatible(D, r, fc.reqs, allow_wk)) continue;
+                    if (g.aff_pol == KP_POLICY_HONOR && !filter_matches(fc, r, allow_wk)) continue;
                     if (g.taint_pol == KP_POLICY_HONOR && !tolerates_all(taints, fc.tols)) continue;
                 }
                 if (g.type != KP_TOPO_ANTI_AFFINITY) {  // the domain is recorded only once it is a single value
@@ -611,6 +634,12 @@ struct Solver {
     }
 
     void solve() {
+        // NewTopology creates the groups the batch's pods own; Topology.Update those of a relaxed pod's new spec
+        born = ~0ull;
+        if (n_late > 0 && !getenv("ORC_NO_LATE")) {  // ORC_NO_LATE (diagnostics): every group counts from the start
+            born = 0;
+            for (int li = 0; li < (int)plist.size(); li++) born |= cls_birth[pod_at(li).cls];
+        }
         // NewQueue: sort.Slice(pods, byCPUAndMemoryDescending) — a total order (Kubernetes UIDs are unique).  Inputs
         // without UIDs (kp_pods_view.uids NULL) keep their input order on ties, as the device's stable radix passes do.
         const int n = (int)plist.size();
@@ -647,6 +676,7 @@ struct Solver {
             q.push_back(li);
             if (nx >= 0) {
                 pcls[li] = nx;
+                if (n_late > 0) born |= cls_birth[nx];
                 lastLen.clear();
             } else {
                 lastLen[li] = (int)q.size();
@@ -806,10 +836,6 @@ static kp_status parse_into(Solver& s, const kp_catalog_view* cat, const kp_solv
         for (int j = 0; j < in->nodepools[i].n_taints; j++)
             if (in->nodepools[i].taints[j].effect && !strcmp(in->nodepools[i].taints[j].effect, "PreferNoSchedule"))
                 tol_pns = true;
-    std::vector<std::string> topo_keys;  // every topology key of the input (strict pod requirements, see below)
-    for (int c = 0; c < in->n_classes; c++)
-        for (int i = 0; i < in->classes[c].n_topology; i++)
-            if (in->classes[c].topology[i].topology_key) topo_keys.push_back(normalize_label(in->classes[c].topology[i].topology_key));
     auto parse_term = [&](const kp_topology_term& x, const std::string& ns, TopoTerm& t) -> kp_status {
         if (x.type < KP_TOPO_SPREAD || x.type > KP_TOPO_ANTI_AFFINITY || !x.topology_key) return KP_E_INVALID;
         t.type = x.type;
@@ -863,21 +889,6 @@ static kp_status parse_into(Solver& s, const kp_catalog_view* cat, const kp_solv
         }
         for (auto* v : {&sp.paff, &sp.panti})
             std::stable_sort(v->begin(), v->end(), [&](int a, int b) { return pc.topology[a].weight > pc.topology[b].weight; });
-        // restrictions shared with the device build: the topology node filter takes the nodeSelector and EVERY required
-        // term (ORed) but no preference, and pod domains come from the strict requirements (no preferred term)
-        bool honor_spread = false;
-        for (int i = 0; i < pc.n_topology; i++)
-            honor_spread |= pc.topology[i].type == KP_TOPO_SPREAD && pc.topology[i].node_affinity_policy == KP_POLICY_HONOR;
-        if (honor_spread && pc.n_required_terms > 1) return KP_E_UNSUPPORTED;
-        if (pref_policy == KP_PREFERENCE_RESPECT && pc.n_preferred_terms > 0) {
-            if (honor_spread) return KP_E_UNSUPPORTED;
-            for (int i = 0; i < pc.n_preferred_terms; i++)
-                for (int j = 0; j < pc.preferred_terms[i].n_requirements; j++) {
-                    const char* k = pc.preferred_terms[i].requirements[j].key;
-                    if (k && std::find(topo_keys.begin(), topo_keys.end(), normalize_label(k)) != topo_keys.end())
-                        return KP_E_UNSUPPORTED;
-                }
-        }
         work.push_back({c, sp});
     }
     auto has_pns_tol = [](const kp_pod_class& pc) {  // Toleration.MatchToleration of {Exists, PreferNoSchedule}
@@ -902,9 +913,22 @@ static kp_status parse_into(Solver& s, const kp_catalog_view* cat, const kp_solv
         if (pc.n_required_terms > 0 &&
             !build_reqs(D, pc.required_terms[sp.req_first].requirements, pc.required_terms[sp.req_first].n_requirements, out.reqs))
             return KP_E_INVALID;
-        if (pref_policy == KP_PREFERENCE_RESPECT && !sp.pnode.empty() &&
-            !build_reqs(D, pc.preferred_terms[sp.pnode[0]].requirements, pc.preferred_terms[sp.pnode[0]].n_requirements, out.reqs))
-            return KP_E_INVALID;
+        if (pc.n_required_terms == 0) {
+            out.filter.emplace_back();
+            if (!build_reqs(D, pc.requirements, pc.n_requirements, out.filter.back())) return KP_E_INVALID;
+        }
+        for (int i = sp.req_first; i < pc.n_required_terms; i++) {
+            out.filter.emplace_back();
+            if (!build_reqs(D, pc.requirements, pc.n_requirements, out.filter.back()) ||
+                !build_reqs(D, pc.required_terms[i].requirements, pc.required_terms[i].n_requirements, out.filter.back()))
+                return KP_E_INVALID;
+        }
+        if (pref_policy == KP_PREFERENCE_RESPECT && !sp.pnode.empty()) {
+            out.strict = out.reqs;
+            out.has_strict = true;
+            if (!build_reqs(D, pc.preferred_terms[sp.pnode[0]].requirements, pc.preferred_terms[sp.pnode[0]].n_requirements, out.reqs))
+                return KP_E_INVALID;
+        }
         for (int i = 0; i < pc.n_tolerations; i++) {
             Toleration t;
             t.key = pc.tolerations[i].key ? pc.tolerations[i].key : "";
@@ -974,6 +998,8 @@ static kp_status parse_into(Solver& s, const kp_catalog_view* cat, const kp_solv
         }
     }
     if (!any_relax) s.relax_next.clear();
+    s.cls_origin = origin;
+    s.n_input = C0;
     // pods
     const kp_pods_view& pv = in->pods;
     s.own_pods.resize(pv.n_pods);
@@ -1115,6 +1141,84 @@ static kp_status build_topology(Solver& s, const kp_solve_input* in, const std::
             }
         }
     }
+    // Topology.Update creates a group (countDomains counts the bound pods) unless one of equal TopologyGroup.Hash()
+    // exists: key, type, namespaces, selector, maxSkew and the node filter — the requirement KEY sets of the
+    // nodeSelector with each remaining required term (hashstructure skips unexported fields: no values), the
+    // policies and the tolerations; slices hash as the XOR of their elements (SlicesAsSets), so pairs cancel.  An
+    // identity that a relaxed spec owns while its input class's stage 0 does not can only be created by a relaxation:
+    // it is "late" and records nothing until then.
+    {
+        auto parity = [](std::vector<std::string> v) {
+            std::sort(v.begin(), v.end());
+            std::string o;
+            for (size_t i = 0; i < v.size();) {
+                size_t j = i;
+                while (j < v.size() && v[j] == v[i]) j++;
+                if ((j - i) & 1) o += v[i] + "\x1f";
+                i = j;
+            }
+            return o;
+        };
+        std::map<std::string, int> ids;
+        std::vector<int> gid(s.groups.size());
+        size_t gi = 0;
+        for (int c = 0; c < C; c++) {
+            const PodClass& pc = s.own_classes[c];
+            for (const TopoTerm& t : pc.terms) {
+                std::set<std::string> nss(t.namespaces.begin(), t.namespaces.end());
+                std::string base = std::to_string(t.type) + "\x1e" + std::to_string(t.key) + "\x1e";
+                for (auto& n : nss) base += n + "\x1f";
+                base += "\x1e";
+                if (t.sel.nil) {
+                    base += "nil";
+                } else {
+                    std::vector<std::string> el;
+                    for (auto& q : t.sel.terms) el.push_back(q.key + "\x1d" + std::to_string(q.op) + "\x1d" + parity(q.values));
+                    base += "sel" + parity(el);
+                }
+                base += "\x1e" + std::to_string(t.max_skew) + "\x1e";
+                for (int inv = 0; inv < 2; inv++) {
+                    if (inv && (t.type != KP_TOPO_ANTI_AFFINITY || t.preferred)) break;
+                    std::string id = (inv ? "I\x1e" : "F\x1e") + base;
+                    if (t.type == KP_TOPO_SPREAD) {
+                        std::vector<std::string> ks, tl;
+                        for (const Reqs& f : pc.filter) {
+                            std::string k;
+                            for (auto& kv : f.m) k += std::to_string(kv.first) + "\x1c";
+                            ks.push_back(k);
+                        }
+                        for (auto& x : pc.tols) tl.push_back(x.key + "\x1d" + std::to_string(x.op) + "\x1d" + x.value + "\x1d" + x.effect);
+                        id += parity(ks) + "\x1e" + std::to_string(t.aff_pol) + std::to_string(t.taint_pol) + "\x1e" + parity(tl);
+                    }
+                    auto it = ids.find(id);
+                    int ix;
+                    if (it != ids.end()) {
+                        ix = it->second;
+                    } else {
+                        ix = (int)ids.size();
+                        ids.emplace(id, ix);
+                    }
+                    gid[gi++] = ix;
+                }
+            }
+        }
+        const int NI = (int)ids.size();
+        std::vector<std::set<int>> own0(NI);
+        for (size_t g = 0; g < s.groups.size(); g++)
+            if (s.groups[g].owner < s.n_input) own0[gid[g]].insert(s.groups[g].owner);
+        std::vector<int> late(NI, -1);
+        for (size_t g = 0; g < s.groups.size(); g++) {
+            const int o = s.groups[g].owner;
+            if (o < s.n_input || late[gid[g]] >= 0 || own0[gid[g]].count(s.cls_origin[o])) continue;
+            if (s.n_late >= 64) return KP_E_UNSUPPORTED;  // shared with the device build
+            late[gid[g]] = s.n_late++;
+        }
+        s.cls_birth.assign(C, 0);
+        for (size_t g = 0; g < s.groups.size(); g++) {
+            s.groups[g].late = late[gid[g]];
+            if (late[gid[g]] >= 0) s.cls_birth[s.groups[g].owner] |= 1ull << late[gid[g]];
+        }
+    }
     s.t_cons.assign(C, {});
     s.t_rec.assign(C, {});
     for (int gi = 0; gi < (int)s.groups.size(); gi++) {
@@ -1148,7 +1252,7 @@ static void count_bound_pod(Solver& s, int j, int b) {
         if (g.inverse ? g.owner != b : !g.sel[b]) continue;
         if (!g.inverse && g.type == KP_TOPO_SPREAD) {
             const PodClass& fc = (*s.cp)[g.owner];
-            if (g.aff_pol == KP_POLICY_HONOR && !reqs_compatible(s.D, n.reqs, fc.reqs, false)) continue;
+            if (g.aff_pol == KP_POLICY_HONOR && !s.filter_matches(fc, n.reqs, false)) continue;
             if (g.taint_pol == KP_POLICY_HONOR && !tolerates_all(n.taints, fc.tols)) continue;
         }
         int dom;
@@ -1341,6 +1445,8 @@ static void run_probe(const ConsCtx& X, int probe, kp_probe_result& pr, Replacem
         s.groups = b.groups_dg;
         s.t_cons = b.t_cons;
         s.t_rec = b.t_rec;
+        s.cls_birth = b.cls_birth;
+        s.n_late = b.n_late;
         for (int i = 0; i < in->cluster.n_bound; i++) count_bound_pod(s, in->cluster.bound_node[i], in->cluster.bound_class[i]);
         for (int c = 0; c < in->n_candidates; c++) {
             if (c >= c0 && c < c1) continue;

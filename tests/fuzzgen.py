@@ -349,6 +349,65 @@ def add_preferences(rng, prob, p_node=0.45, p_topo=0.6):
     return prob
 
 
+def add_topology_preferences(rng, prob, p_pref=0.5):
+    """Preferred node-affinity terms next to topology terms (after add_topology): terms on the topology keys themselves
+    (zone, capacity-type: the NodeClaim takes the preference, podDomains the strict requirements) and on
+    instance-category / arch (outside a nodeAffinityPolicy Honor spread's node filter), weights 1-100."""
+    zones = sorted({o.zone for it in prob.catalog for o in it.offerings})
+    cats = ["c", "m", "r", "t", "g", "i"]
+    for pc in prob.classes:
+        if rng.random() >= p_pref:
+            continue
+        terms = []
+        for _ in range(int(rng.integers(1, 4))):
+            u = rng.random()
+            if u < 0.4:
+                r = Requirement(ZONE, "In", sorted(set(rng.choice(zones, size=int(rng.integers(1, 3))).tolist())))
+            elif u < 0.55:
+                r = Requirement(CAPACITY_TYPE, "In", [str(rng.choice(["spot", "on-demand"]))])
+            elif u < 0.85:
+                r = Requirement(AWS + "instance-category", "In",
+                                sorted(set(rng.choice(cats, size=int(rng.integers(1, 3))).tolist())))
+            else:
+                r = Requirement(ARCH, "In", [str(rng.choice(["amd64", "arm64"]))])
+            terms.append((int(rng.integers(1, 100)), [r]))
+        pc.preferred_terms = terms
+    return prob
+
+
+def add_relaxing_topology(rng, prob, p_req=0.5):
+    """Pods whose relaxation changes their spread groups' TopologyGroup.Hash() (topology.go Update creates the new
+    spec's groups then): ORed required node-affinity terms (instance-category / arch / zone, 2-3 terms, the first often
+    unsatisfiable for the pod's spread) next to zonal / hostname spreads under both nodeAffinityPolicies, and sometimes
+    a PreferNoSchedule taint on a NodePool (the added toleration is part of the node filter's hash)."""
+    zones = sorted({o.zone for it in prob.catalog for o in it.offerings})
+    cats = ["c", "m", "r", "t", "g", "i"]
+    for pc in prob.classes:
+        if rng.random() >= p_req:
+            continue
+        terms = []
+        for _ in range(int(rng.integers(2, 4))):
+            u = rng.random()
+            if u < 0.4:
+                t = [Requirement(ZONE, "In", [str(rng.choice(zones))])]
+            elif u < 0.7:
+                t = [Requirement(AWS + "instance-category", "In", [str(rng.choice(cats))])]
+            else:
+                t = [Requirement(AWS + "instance-category", "In", [str(rng.choice(cats))]),
+                     Requirement(ARCH, "In", [str(rng.choice(["amd64", "arm64"]))])]
+            terms.append(t)
+        pc.required_terms = terms
+        if not any(t.kind == "spread" for t in pc.topology):
+            sel = [Requirement("app", "In", [pc.labels.get("app", "x")])]
+            pc.topology = list(pc.topology) + [model.TopologyTerm(
+                "spread", ZONE if rng.random() < 0.7 else HOSTNAME, sel, max_skew=int(rng.integers(1, 3)),
+                node_affinity_policy=str(rng.choice(["Honor", "Ignore"])))]
+    if rng.random() < 0.5:
+        np_ = prob.nodepools[int(rng.integers(0, len(prob.nodepools)))]
+        np_.taints = list(np_.taints) + [Taint("example.com/soft", "", "PreferNoSchedule")]
+    return prob
+
+
 def fuzz_preference_consolidation(catalog, seed, n_nodes=30, n_pods=160, n_bound=30, all_spot=False, best_effort=False,
                                   zone_min=False):
     """fuzz_consolidation over pods with preferences to relax (add_preferences), pods of those classes bound to random

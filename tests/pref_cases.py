@@ -11,6 +11,8 @@ The relaxation order and the Queue.Push(pod, relaxed) semantics are [core] sched
 recalled (not vendored); those cases are hand-computed from that restatement ("parity unpinned" beyond the oracle).
 """
 from dataclasses import dataclass, field
+
+import numpy as np
 from typing import Callable, List
 
 from kpsim import abi, catalog, model, synth
@@ -196,6 +198,98 @@ def prefer_no_schedule_already_tolerated(fx):
     c = prefer_no_schedule_tolerated_after_relax(fx)
     c.problem.classes = [PodClass([], tolerations=[Toleration("", "Exists", "", "PreferNoSchedule")])]
     return PrefCase("prefer_no_schedule_already_tolerated", c.ref, c.problem, c.check)
+
+
+@case
+def preferred_zone_term_strict_pod_domains(fx):
+    """A preferred zone term on a zone spread's key: the NodeClaim's requirements take the preference (zone In [1a]) but
+    podDomains come from the strict requirements (NewStrictPodRequirements: every zone), so the skew counts the empty
+    zones.  Pod 1 lands in 1a; pods 2-3 see 1a at skew 2, fail, drop the preference and open 1b and 1c; pod 4 (skew 1
+    again) joins 1a.  Pod domains taken from the preference would put all four pods in 1a."""
+    cat = catalog.fake_catalog(fx=fx)
+    pc = PodClass([], labels={"app": "web"},
+                  topology=[TopologyTerm("spread", ZONE, selector=[Requirement("app", "In", ["web"])])],
+                  preferred_terms=[(10, [Requirement(ZONE, "In", [Z1A])])])
+    prob = _prob(cat, [synth.default_nodepool()], [pc], [(0, {"cpu": "100m"})] * 4)
+
+    def check(prob, res, q):
+        _scheduled(res)
+        assert res.n_nodeclaims == 3
+        assert sorted(q[i][ZONE][4] for i in range(3)) == [(Z1A,), (Z1B,), (Z1C,)]
+        assert sorted(int(n) for n in res.nodeclaim_n_pods[:3]) == [1, 1, 2]
+    return PrefCase("preferred_zone_term_strict_pod_domains", "[core] nodeclaim.go CanAdd (podData.StrictRequirements)",
+                    prob, check)
+
+
+@case
+def honor_spread_filter_ignores_preference(fx):
+    """nodeAffinityPolicy Honor with a preferred node-affinity term: MakeTopologyNodeFilter takes the nodeSelector and
+    the required terms only, so two bound pods on t3.large nodes in zone 1a count although the pod prefers m5.large; the
+    pod's NodeClaim (m5.large by preference) avoids 1a.  A filter carrying the preference would count nothing there and
+    pick 1a (smallest domain name)."""
+    cat = catalog.fake_catalog(fx=fx)
+    t3 = next(it for it in cat if it.name == "t3.large")
+    sel = [Requirement("app", "In", ["web"])]
+    pc = PodClass([], labels={"app": "web"}, topology=[TopologyTerm("spread", ZONE, selector=sel)],
+                  preferred_terms=[(10, [Requirement(INSTANCE_TYPE, "In", ["m5.large"])])])
+    nodes = [model.ExistingNode("t3-%d" % j, synth.node_labels(t3, Z1A, "on-demand"), np.zeros(model.R, np.int64))
+             for j in range(2)]
+    prob = _prob(cat, [synth.default_nodepool()], [pc], [(0, {"cpu": "100m"})], existing=nodes, bound=[(0, 0), (1, 0)])
+
+    def check(prob, res, q):
+        _scheduled(res)
+        assert res.n_nodeclaims == 1
+        assert q[0][ZONE][4] == (Z1B,)
+        assert q[0][INSTANCE_TYPE][4] == ("m5.large",)
+    return PrefCase("honor_spread_filter_ignores_preference", "[core] topologynodefilter.go MakeTopologyNodeFilter",
+                    prob, check)
+
+
+@case
+def relaxed_spec_spread_group_created_late(fx):
+    """Topology.Update creates the spread group of a relaxed spec (its node filter keeps the remaining required terms,
+    so it hashes apart from the first spec's group) when the first pod relaxes, counting only bound pods from then on.
+    Required terms [t3.large] | [m5.large, amd64], zone spread (maxSkew 1, nodeAffinityPolicy Ignore): pods 1-2 take
+    t3.large in 1a / 1b; pods 3-4 cannot reach 1c with t3.large, relax, and the new group (empty) spreads them over
+    m5.large in 1a then 1b.  A group counting since the start would send pod 3 to 1c and pod 4 after it (3 NodeClaims)."""
+    cat = catalog.fake_catalog(fx=fx)
+    sel = [Requirement("app", "In", ["web"])]
+    pc = PodClass([], labels={"app": "web"},
+                  topology=[TopologyTerm("spread", ZONE, selector=sel, node_affinity_policy="Ignore")],
+                  required_terms=[[Requirement(INSTANCE_TYPE, "In", ["t3.large"])],
+                                  [Requirement(INSTANCE_TYPE, "In", ["m5.large"]), Requirement(model.ARCH, "In", ["amd64"])]])
+    prob = _prob(cat, [synth.default_nodepool()], [pc], [(0, {"cpu": "100m"})] * 4)
+
+    def check(prob, res, q):
+        _scheduled(res)
+        assert res.n_nodeclaims == 4
+        got = sorted((q[i][INSTANCE_TYPE][4], q[i][ZONE][4]) for i in range(4))
+        assert got == [(("m5.large",), (Z1A,)), (("m5.large",), (Z1B,)), (("t3.large",), (Z1A,)), (("t3.large",), (Z1B,))], got
+    return PrefCase("relaxed_spec_spread_group_created_late", "[core] topology.go Update (countDomains for a new hash)",
+                    prob, check)
+
+
+@case
+def honor_spread_several_required_terms(fx):
+    """nodeAffinityPolicy Honor with ORed required terms: the node filter matches a node compatible with ANY remaining
+    term.  Two bound pods on t3.large nodes in 1a count for the spread of a pod whose first term (t3.large) fails;
+    after Relax its spec's group is new (late) and also counts them (countDomains at creation), so the m5.large
+    NodeClaim goes to 1b."""
+    cat = catalog.fake_catalog(fx=fx)
+    t3 = next(it for it in cat if it.name == "t3.large")
+    sel = [Requirement("app", "In", ["web"])]
+    pc = PodClass([], labels={"app": "web"}, topology=[TopologyTerm("spread", ZONE, selector=sel)],
+                  required_terms=[[Requirement(INSTANCE_TYPE, "In", ["no-such-type"])],
+                                  [Requirement(INSTANCE_TYPE, "In", ["m5.large", "t3.large"])]])
+    nodes = [model.ExistingNode("t3-%d" % j, synth.node_labels(t3, Z1A, "on-demand"), np.zeros(model.R, np.int64))
+             for j in range(2)]
+    prob = _prob(cat, [synth.default_nodepool()], [pc], [(0, {"cpu": "100m"})], existing=nodes, bound=[(0, 0), (1, 0)])
+
+    def check(prob, res, q):
+        _scheduled(res)
+        assert res.n_nodeclaims == 1
+        assert q[0][ZONE][4] == (Z1B,)
+    return PrefCase("honor_spread_several_required_terms", "[core] topologynodefilter.go MatchesRequirements", prob, check)
 
 
 def _best_effort_problem(golden, policy):

@@ -508,6 +508,36 @@ def test_fuzz_consolidation_preferences(pctx, golden, seed, policy):
                           pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH, spot_to_spot=s2s, preference_policy=pol))
 
 
+@pytest.mark.parametrize("seed", range(10))
+def test_fuzz_consolidation_topology_preferences(pctx, golden, seed):
+    """Probes over pods with topology terms and preferred node-affinity terms (fuzzgen.add_topology_preferences):
+    preferences on topology keys and nodeAffinityPolicy Honor spreads, under Respect."""
+    ctx = pctx[abi.KP_PREFERENCE_RESPECT]
+    rng = np.random.Generator(np.random.PCG64(4300 + seed))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 300)), replace=False))]
+    cp = fuzzgen.fuzz_topology_consolidation(sub, 4300 + seed, n_nodes=int(rng.integers(4, 50)),
+                                             n_pods=int(rng.integers(20, 200)), all_spot=seed % 4 == 0)
+    fuzzgen.add_topology_preferences(rng, cp.cluster)
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        assert_probes_equal(device_probes(ctx, cp, mode),
+                            pyoracle.consolidate(cp, mode, preference_policy=abi.KP_PREFERENCE_RESPECT))
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_fuzz_consolidation_relaxing_topology(pctx, golden, seed):
+    """Probes whose pods relax into specs with new spread groups (fuzzgen.add_relaxing_topology): each probe's
+    NewTopology creates the groups its own pods own; a relaxed pod's Topology.Update creates the rest."""
+    ctx = pctx[abi.KP_PREFERENCE_RESPECT]
+    rng = np.random.Generator(np.random.PCG64(4500 + seed))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 300)), replace=False))]
+    cp = fuzzgen.fuzz_topology_consolidation(sub, 4500 + seed, n_nodes=int(rng.integers(4, 50)),
+                                             n_pods=int(rng.integers(20, 200)), all_spot=seed % 4 == 0)
+    fuzzgen.add_relaxing_topology(rng, cp.cluster)
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        assert_probes_equal(device_probes(ctx, cp, mode),
+                            pyoracle.consolidate(cp, mode, preference_policy=abi.KP_PREFERENCE_RESPECT))
+
+
 def test_preference_relaxations_in_probes(pctx, golden):
     """The fuzz above relaxes preferences inside the probes (kp_consolidate_stats counter 16): under Respect every
     preference kind; under Ignore only the ORed required node-affinity terms (removeRequiredNodeAffinityTerm)."""

@@ -90,6 +90,50 @@ def test_preference_fuzz(golden, seed):
         parity.assert_same(dev, _oracle(prob, policy))
 
 
+@pytest.mark.parametrize("seed", range(12))
+def test_topology_preference_fuzz(golden, seed):
+    """Preferred node-affinity terms on pods with topology terms over a cluster (fuzzgen.add_topology_preferences after
+    fuzz_topology_existing_problem): preferences on the zone / capacity-type topology keys (podDomains from the strict
+    requirements) and nodeAffinityPolicy Honor spreads whose node filter leaves the preference out."""
+    import fuzzgen
+    rng = np.random.Generator(np.random.PCG64(7300 + seed))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(80, 300)), replace=False))]
+    prob = fuzzgen.fuzz_topology_existing_problem(sub, 7300 + seed, n_pods=int(rng.integers(100, 400)))
+    fuzzgen.add_topology_preferences(rng, prob)
+    assert any(pc.preferred_terms for pc in prob.classes)
+    for policy in (abi.KP_PREFERENCE_RESPECT, abi.KP_PREFERENCE_IGNORE):
+        ctx = _ctx(policy)
+        try:
+            dev = parity.run_device(ctx, prob)
+        finally:
+            ctx.close()
+        parity.assert_same(dev, _oracle(prob, policy))
+
+
+def relaxing_topology_problem(golden, seed):
+    import fuzzgen
+    rng = np.random.Generator(np.random.PCG64(7600 + seed))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(80, 300)), replace=False))]
+    prob = fuzzgen.fuzz_topology_existing_problem(sub, 7600 + seed, n_pods=int(rng.integers(100, 400)))
+    return fuzzgen.add_relaxing_topology(rng, prob)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_relaxing_topology_fuzz(golden, seed):
+    """Relaxations that change a spread group's TopologyGroup.Hash() (ORed required terms under both
+    nodeAffinityPolicies, the PreferNoSchedule toleration): the relaxed spec's groups are created when the first pod
+    relaxes into it and count only the bound pods until then (fuzzgen.add_relaxing_topology; seeds 6, 7 and 11 decide
+    differently if those groups count from the start, ORC_NO_LATE)."""
+    prob = relaxing_topology_problem(golden, seed)
+    for policy in (abi.KP_PREFERENCE_RESPECT, abi.KP_PREFERENCE_IGNORE):
+        ctx = _ctx(policy)
+        try:
+            dev = parity.run_device(ctx, prob)
+        finally:
+            ctx.close()
+        parity.assert_same(dev, _oracle(prob, policy))
+
+
 def test_repeated_execute_restores_classes(golden):
     """kp_solve_execute twice on one prepare: relaxed pods start again from their input classes."""
     prob = fuzz_problem(golden, 1)

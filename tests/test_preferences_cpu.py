@@ -18,12 +18,3 @@ def test_pref_case_oracle(fx, mk):
     c = mk(fx)
     res, reqs = run_oracle(c)
     c.check(c.problem, res, reqs)
-
-
-def test_preferred_node_term_on_topology_key_unsupported(fx):
-    """Pod domains come from the strict requirements (no preference): a preferred term on a topology key of the input is
-    refused rather than mis-scheduled (KP_E_UNSUPPORTED, shared with the device build)."""
-    c = PC.schedule_anyway_spread_respected(fx)
-    c.problem.classes[0].preferred_terms = [(5, [model.Requirement(model.HOSTNAME, "Exists")])]
-    with pytest.raises(RuntimeError, match="7"):
-        run_oracle(c)
