@@ -86,9 +86,8 @@ struct ClassCache {
     int ntc, ntr;               // topology groups constraining / recording the class
     int tc[KP_MAX_TOPO];        // group | self << 30
     int tc_ki[KP_MAX_TOPO];     // class-key index of a value-keyed group's key (-1 for hostname groups)
-    uint64_t tc_podhas[KP_MAX_TOPO];  // podDomains of the group's key: the class's strict requirements (KpTopoCons)
-    int tr[KP_MAX_TOPO_REC];
-    int tr_ki[KP_MAX_TOPO_REC]; // class-key index of the group's key, -1 when the class does not constrain it
+    int tr[KP_CC_REC];          // the first KP_CC_REC recording groups (the others: rec_entry)
+    int tr_ki[KP_CC_REC];       // class-key index of the group's key, -1 when the class does not constrain it
 };
 
 // Offering-role keys (zone, capacity-type, zone-id, reservation-id, reservation-type) of the solve.
@@ -121,10 +120,10 @@ struct ProbeTopo {
 // topo_prefilter_setup in CC.tc order): counts only change when a pod commits, so every candidate evaluation of the pod
 // reads them here instead of from the global counters.
 struct TopoSnap {
-    int32_t cnt[KP_MAX_TOPO][64];   // domain counts (0 where the domain is not registered)
-    uint8_t rk[KP_MAX_TOPO][64];    // value-name rank of each domain (tie-break)
-    uint64_t known[KP_MAX_TOPO];    // registered domains
-    uint64_t podhas[KP_MAX_TOPO];   // domains the pod's own requirement for the key admits
+    int32_t cnt[KP_SNAP_ROWS][64];   // domain counts (0 where the domain is not registered)
+    uint8_t rk[KP_SNAP_ROWS][64];    // value-name rank of each domain (tie-break)
+    uint64_t known[KP_SNAP_ROWS];    // registered domains
+    uint64_t podhas[KP_SNAP_ROWS];   // domains the pod's own requirement for the key admits
 };
 
 // Tables shared by every evaluation of a kernel (LDS in ffd_kernel).
@@ -203,8 +202,7 @@ __device__ inline void fill_class_cache(const KpDev& d, int c, ClassCache& CC, i
         if (cons) {
             CC.tc[tid] = e;
             CC.tc_ki[tid] = ki;
-            CC.tc_podhas[tid] = d.cls_tce[d.cls_tcoff[c] + tid].podhas;
-        } else {
+        } else if (tid - CC.ntc < KP_CC_REC) {
             CC.tr[tid - CC.ntc] = e;
             CC.tr_ki[tid - CC.ntc] = ki;
         }
@@ -451,8 +449,8 @@ template <bool CT = false>
 __device__ __forceinline__ bool topo_narrow(const KpDev& d, const ClassCache& CC, WaveScratch& ws, int host, bool allow_wk,
                                          int lane, const ProbeTopo* pt = nullptr, const TopoSnap* snap = nullptr) {
     int nk = 0;
-    int kidx[KP_MAX_TOPO];
-    uint64_t kmask[KP_MAX_TOPO];
+    int kidx[KP_MAX_TOPO_KEYS];
+    uint64_t kmask[KP_MAX_TOPO_KEYS];
     for (int e = 0; e < CC.ntc; e++) {
         const int g = CC.tc[e] & 0x3FFFFFFF, self = (CC.tc[e] >> 30) & 1, ki = CC.tc_ki[e];
         const int4 info = d.tg_info[g];
@@ -474,7 +472,7 @@ __device__ __forceinline__ bool topo_narrow(const KpDev& d, const ClassCache& CC
         bool kn, pod_has;
         int cnt;
         uint32_t rk;
-        if (!CT && snap) {
+        if (!CT && snap && CC.ntc <= KP_SNAP_ROWS) {
             kn = valid && ((snap->known[e] >> lane) & 1ull);
             cnt = kn ? snap->cnt[e][lane] : 0;
             pod_has = valid && ((snap->podhas[e] >> lane) & 1ull);
@@ -484,7 +482,8 @@ __device__ __forceinline__ bool topo_narrow(const KpDev& d, const ClassCache& CC
             const uint64_t known = ld_u64(CT ? &pt->known[g] : &d.tg_known[g]);
             kn = valid && ((known >> lane) & 1ull);
             cnt = kn ? ld_i32(CT ? &pt->cnt[(size_t)g * 64 + lane] : &d.tg_cnt[(size_t)g * 64 + lane]) : 0;
-            pod_has = valid && ((CC.tc_podhas[e] >> lane) & 1ull);
+            // podDomains: the class's strict requirements (KpTopoCons)
+            pod_has = valid && ((d.cls_tce[d.cls_tcoff[CC.cls] + e].podhas >> lane) & 1ull);
             rk = valid ? d.vrank[(size_t)k * 64 + lane] : 0xFFu;
         }
         const ReqHdr nh = ws.hdr[ki];
@@ -567,32 +566,38 @@ __device__ __forceinline__ bool topo_narrow(const KpDev& d, const ClassCache& CC
 // required node-affinity term — with the AllowUndefinedWellKnownLabels option when allow_wk; the owner's
 // tolerations); spread / affinity record a single-valued domain, anti-affinity and inverse groups record every value
 // (requirement.Values(), the excluded set of a complement).
+// The filter rows [r0, r0 + n) in one pass: lane i takes entry i of their concatenated key lists, and a row matches
+// when none of its entries fails (n <= 64; kp_solve_prepare caps it).
 __device__ inline bool topo_filter_compatible(const KpDev& d, const ClassCache& CC, const WaveScratch& ws,
-                                              const ReqHdr* Ahdr, const uint64_t* Aw, int row, bool allow_wk, int lane,
-                                              bool exnode = false) {
-    bool ok = true;
-    for (int i = d.cls_xkoff[row] + lane; i < d.cls_xkoff[row + 1]; i += 64) {
-        const int k = d.cls_xkeys[i];
-        const ReqHdr B = d.cls_hdr[(size_t)row * d.K + k];
-        const uint64_t* bw = d.cls_words + (size_t)row * d.DW + d.woff[k];
-        const bool bno = op_notin_or_dne(req_op(B.flags, popc_words(bw, d.nw[k])));
-        if (k == d.key_host && !exnode) {  // NodeClaim hostname In [placeholder]: only a complement without bounds admits it
-            if (!((B.flags & RF_CMP) && !(B.flags & (RF_GT | RF_LT)))) ok = false;
-            continue;
+                                              const ReqHdr* Ahdr, const uint64_t* Aw, int r0, int n, bool allow_wk,
+                                              int lane, bool exnode = false) {
+    const int i0 = d.cls_xkoff[r0], i1 = d.cls_xkoff[r0 + n];
+    uint64_t bad = 0;  // rows with an incompatible key
+    for (int i = i0 + lane; i - lane < i1; i += 64) {
+        bool ok = true;
+        int row = 0;
+        if (i < i1) {
+            while (d.cls_xkoff[r0 + row + 1] <= i) row++;
+            const int rw = r0 + row;
+            const int k = d.cls_xkeys[i];
+            const ReqHdr B = d.cls_hdr[(size_t)rw * d.K + k];
+            const uint64_t* bw = d.cls_words + (size_t)rw * d.DW + d.woff[k];
+            const bool bno = op_notin_or_dne(req_op(B.flags, popc_words(bw, d.nw[k])));
+            if (k == d.key_host && !exnode) {  // NodeClaim hostname In [placeholder]: only a complement without bounds admits it
+                ok = (B.flags & RF_CMP) && !(B.flags & (RF_GT | RF_LT));
+            } else {
+                int ci = -1;
+                for (int q = 0; q < CC.nck; q++)
+                    if (CC.key[q] == k) ci = q;
+                const ReqHdr A = ci >= 0 ? ws.hdr[ci] : Ahdr[k];
+                const uint64_t* aw = ci >= 0 ? ws.words + CC.wsoff[ci] : Aw + d.woff[k];
+                if (!(A.flags & RF_DEF)) ok = bno || (allow_wk && (d.kflags[k] & KF_WELL_KNOWN));
+                else ok = !req_intersect_empty(d, k, A, aw, B, bw) || (bno && op_notin_or_dne(req_op(A.flags, popc_words(aw, d.nw[k]))));
+            }
         }
-        int ci = -1;
-        for (int q = 0; q < CC.nck; q++)
-            if (CC.key[q] == k) ci = q;
-        const ReqHdr A = ci >= 0 ? ws.hdr[ci] : Ahdr[k];
-        const uint64_t* aw = ci >= 0 ? ws.words + CC.wsoff[ci] : Aw + d.woff[k];
-        if (!(A.flags & RF_DEF)) {
-            if (!bno && !(allow_wk && (d.kflags[k] & KF_WELL_KNOWN))) ok = false;
-            continue;
-        }
-        if (req_intersect_empty(d, k, A, aw, B, bw) && !(bno && op_notin_or_dne(req_op(A.flags, popc_words(aw, d.nw[k])))))
-            ok = false;
+        bad |= wave_or64(ok ? 0ull : 1ull << row);
     }
-    return ballot(!ok) == 0;
+    return bad != (n >= 64 ? ~0ull : (1ull << n) - 1);
 }
 
 // exnode >= 0: the placement is on existing node exnode (its taints: ex_tol; its hostname is a real node name).
@@ -603,7 +608,19 @@ __device__ __forceinline__ void topo_record(const KpDev& d, const ClassCache& CC
                                          const ProbeTopo* pt = nullptr, uint64_t born = ~0ull) {
     if (CT && d.tg_late) born = *pt->born;
     for (int e = 0; e < CC.ntr; e++) {
-        const int g = CC.tr[e], ki = CC.tr_ki[e];
+        int g, ki;
+        if (e < KP_CC_REC) {
+            g = CC.tr[e];
+            ki = CC.tr_ki[e];
+        }
+        else {  // beyond the cached entries: the class's list, and the group's key among the class keys
+            g = d.cls_tr[d.cls_troff[CC.cls] + e];
+            ki = -1;
+            const int4 inf = d.tg_info[g];
+            if (!(inf.x & TG_HOST))
+                for (int i = 0; i < CC.nck; i++)
+                    if (CC.key[i] == inf.y) ki = i;
+        }
         if (d.tg_late) {  // a group Topology.Update has not created yet records nothing
             const int lt = d.tg_late[g];
             if (lt >= 0 && !((born >> lt) & 1ull)) continue;
@@ -618,10 +635,7 @@ __device__ __forceinline__ void topo_record(const KpDev& d, const ClassCache& CC
             if ((pol & 2) && !tolerated) continue;
             if ((pol & 1) && owner != CC.cls) {
                 const int2 fr = d.tg_frow[g];
-                bool m = false;
-                for (int f = fr.x; f < fr.x + fr.y && !m; f++)
-                    m = topo_filter_compatible(d, CC, ws, Ahdr, Aw, f, allow_wk, lane, exnode >= 0);
-                if (!m) continue;
+                if (!topo_filter_compatible(d, CC, ws, Ahdr, Aw, fr.x, fr.y, allow_wk, lane, exnode >= 0)) continue;
             }
         }
         if (info.x & TG_HOST) {

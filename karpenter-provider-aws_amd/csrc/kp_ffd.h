@@ -85,21 +85,24 @@ struct FfdShared {
     // domain a constraining group allows cannot accept the pod, and is skipped without an evaluation
     int tp_n, topo_pod, topo_quick;
     int ex_placed;                 // the current topology pod went to this existing node (-1: none accepted it)
-    int tp_k[KP_MAX_TOPO];         // value-keyed group: key; hostname group: -1 - row of tg_hcnt
-    int tp_lo[KP_MAX_TOPO], tp_hi[KP_MAX_TOPO];  // hostname group: the host's count must lie in [lo, hi]
-    int tp_cmp[KP_MAX_TOPO];       // value-keyed: a complement (NotIn) NodeClaim requirement is not prefiltered
-    uint64_t tp_elig[KP_MAX_TOPO]; // value-keyed: allowed domains ∩ the pod's domains
+    int tp_all;                    // the prefilter holds every constraining group (at most KP_SNAP_ROWS)
+    int tp_k[KP_SNAP_ROWS];        // value-keyed group: key; hostname group: -1 - row of tg_hcnt
+    int tp_lo[KP_SNAP_ROWS], tp_hi[KP_SNAP_ROWS];  // hostname group: the host's count must lie in [lo, hi]
+    int tp_cmp[KP_SNAP_ROWS];      // value-keyed: a complement (NotIn) NodeClaim requirement is not prefiltered
+    uint64_t tp_elig[KP_SNAP_ROWS]; // value-keyed: allowed domains ∩ the pod's domains
     TopoSnap* tsnap;               // topology solves: the pod's value-keyed group counts for topo_narrow (dynamic LDS,
                                    // EvalEnv.snap); null otherwise, so other solves keep that LDS for quick-accept rows
 };
 
 // Once per pod of a class with constraining topology groups: the per-group conditions topo_narrow applies, reduced to
 // what depends on the candidate (its host's count, or its own domains of the key).  Exact up to the NotIn/DoesNotExist
-// Compatible exception, which the prefilter leaves to the evaluation.  Group e is set up by wave e (at most
-// KP_MAX_TOPO = KP_NWAVES groups constrain a class): the groups' dependent loads overlap instead of queueing on wave 0.
-static_assert(KP_MAX_TOPO <= KP_NWAVES, "one wave per constraining topology group");
+// Compatible exception, which the prefilter leaves to the evaluation.  Group e is set up by wave e: the groups'
+// dependent loads overlap instead of queueing on wave 0.  A class constrained by more than KP_SNAP_ROWS groups is
+// prefiltered by its first KP_SNAP_ROWS (a superset of the candidates that pass all: evaluations stay exact, read the
+// global counters, and the quick accept is off).
 __device__ inline void topo_prefilter_setup(const KpDev& d, FfdShared& S, int c, int wave, int lane) {
-    const int t0 = d.cls_tcoff[c], nt = d.cls_tcoff[c + 1] - t0;
+    const int t0 = d.cls_tcoff[c], nall = d.cls_tcoff[c + 1] - t0;
+    const int nt = nall < KP_SNAP_ROWS ? nall : KP_SNAP_ROWS;
     for (int e = wave; e < nt; e += KP_NWAVES) {
         // the entry's static operands (KpTopoCons), then the group's counts: one round of independent loads
         const KpTopoCons T = d.cls_tce[t0 + e];
@@ -152,7 +155,10 @@ __device__ inline void topo_prefilter_setup(const KpDev& d, FfdShared& S, int c,
             S.tp_elig[e] = elig;
         }
     }
-    if (wave == 0 && lane == 0) S.tp_n = nt;
+    if (wave == 0 && lane == 0) {
+        S.tp_n = nt;
+        S.tp_all = nall <= KP_SNAP_ROWS;
+    }
 }
 
 __device__ __forceinline__ bool topo_prefilter_pass(const KpDev& d, const FfdShared& S, int nc) {
@@ -1297,7 +1303,10 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
             const int scan_from = S.scan_start;
             const uint64_t ctol = d.tol[c];
 #if KP_TOPO_BLOCK_SCAN
-            if (tid == 0) S.tp_n = 0;
+            if (tid == 0) {
+                S.tp_n = 0;
+                S.tp_all = 1;
+            }
             if (cfl & CF_TOPO_CONS) topo_prefilter_setup(d, S, c, wave, lane);
             __syncthreads();  // every group's entry and TopoSnap row
             const long long t1 = prof_clock(d);
@@ -1306,7 +1315,10 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
             int f = N;
             long long t1 = 0;
             if (wave == 0) {
-                if (lane == 0) S.tp_n = 0;
+                if (lane == 0) {
+                    S.tp_n = 0;
+                    S.tp_all = 1;
+                }
                 if (cfl & CF_TOPO_CONS)
                     for (int w = 0; w < KP_NWAVES; w++) topo_prefilter_setup(d, S, c, w, lane);
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1323,7 +1335,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                                   : !(slast[nc] == (uint16_t)c || ((cfl & CF_NOKEYS) && ((d.tol[c] >> stmpl[nc]) & 1ull))) ? 3 : 4;
                     S.st[ST_TQ_WHY + why]++;
                 }
-                if (f < N && (cfl & CF_TOPO_QREC) && A > 0) {
+                if (f < N && (cfl & CF_TOPO_QREC) && A > 0 && S.tp_all) {
                     const int nc = sord[f], tm = stmpl[nc];
                     const bool absd = slast[nc] == (uint16_t)c || ((cfl & CF_NOKEYS) && ((d.tol[c] >> tm) & 1ull));
                     bool ok = nc < NQ;

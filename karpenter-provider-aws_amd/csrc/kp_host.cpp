@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "../../include/kpsim.h"
+#include "kp_gosort_host.h"
 #include "kp_cons.h"
 #include "kp_launch.h"
 #include "kp_layout.h"
@@ -1361,18 +1362,17 @@ static kp_status expand_preferences(const kp_solve_input* in, int pref_policy, P
     for (int c = 0; c < C0; c++) {
         const kp_pod_class& pc = in->classes[c];
         St x{c, c, 0, {}, {}, {}, {}, false};
-        if (pc.n_preferred_terms > 12) {
-            err = "more than 12 preferred node-affinity terms (newPodRequirements' sort.Slice order)";
-            return KP_E_UNSUPPORTED;
-        }
         if ((pc.n_required_terms > 0 && !pc.required_terms) || (pc.n_preferred_terms > 0 && !pc.preferred_terms) ||
             (pc.n_topology > 0 && !pc.topology)) {
             err = "pod class arrays";
             return KP_E_INVALID;
         }
+        // newPodRequirements: sort.Slice(preferred, weight desc) in place (unstable beyond 12 terms: Go's pdqsort);
+        // later sorts of the sorted slice, and Relax's SliceStable, keep that order
         for (int i = 0; i < pc.n_preferred_terms; i++) x.pnode.push_back(i);
-        std::stable_sort(x.pnode.begin(), x.pnode.end(),
-                         [&](int a, int b) { return pc.preferred_terms[a].weight > pc.preferred_terms[b].weight; });
+        go_sort_slice((int)x.pnode.size(),
+                      [&](int a, int b) { return pc.preferred_terms[x.pnode[a]].weight > pc.preferred_terms[x.pnode[b]].weight; },
+                      [&](int a, int b) { std::swap(x.pnode[a], x.pnode[b]); });
         for (int i = 0; i < pc.n_topology; i++) {
             const kp_topology_term& t = pc.topology[i];
             if (t.type == KP_TOPO_SPREAD) {
@@ -1695,6 +1695,13 @@ static kp_status topo_build(kp_ctx* c, const kp_solve_input* in, const std::vect
             err = "a pod class is constrained or counted by too many topology groups";
             return KP_E_UNSUPPORTED;
         }
+        std::set<int> vkeys;  // topo_narrow intersects the groups' domains per value-keyed key
+        for (int e : th.cons[o])
+            if (!th.g[e & 0x3FFFFFFF].host) vkeys.insert(th.g[e & 0x3FFFFFFF].key);
+        if (vkeys.size() > KP_MAX_TOPO_KEYS) {
+            err = "a pod class constrained on more than 8 value-keyed topology keys";
+            return KP_E_UNSUPPORTED;
+        }
         for (int e : th.cons[o]) {
             const HGroup& g = th.g[e & 0x3FFFFFFF];
             if (!g.host && !creq[o].count(g.key) &&
@@ -1761,6 +1768,8 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         for (int q = 0; q < in->classes[i].n_topology; q++)
             honor |= in->classes[i].topology[q].type == KP_TOPO_SPREAD &&
                      in->classes[i].topology[q].node_affinity_policy == KP_POLICY_HONOR;
+        if (honor && c->pref.filt[i].size() > 64)
+            return fail(ctx, KP_E_UNSUPPORTED, "a nodeAffinityPolicy Honor spread with more than 64 node-filter terms");
         if (honor)
             for (auto& f : c->pref.filt[i]) {
                 cfilt[i].emplace_back();
@@ -1950,7 +1959,8 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
             bool qrec = true;
             for (int gi : th.rec[row]) {
                 const HGroup& g = th.g[gi];
-                if (!g.inverse && g.type == KP_TOPO_SPREAD && (g.pol & 1) && g.owner != row) qrec = false;
+                // a member's pods satisfy the group's node filter (its semantics equal the member's own filter)
+                if (!g.inverse && g.type == KP_TOPO_SPREAD && (g.pol & 1) && !g.memb[row]) qrec = false;
             }
             if (qrec) cflags[row] |= CF_TOPO_QREC;
         }

@@ -876,12 +876,20 @@ static kp_status parse_into(Solver& s, const kp_catalog_view* cat, const kp_solv
     std::vector<std::pair<int, Spec>> work;  // (class id, spec) whose Relax step is still to be derived
     for (int c = 0; c < C0; c++) {
         const kp_pod_class& pc = in->classes[c];
-        if (pc.n_preferred_terms > 12) return KP_E_UNSUPPORTED;  // newPodRequirements' sort.Slice is stable only up to 12
         Spec sp;
+        // newPodRequirements: sort.Slice(preferred, weight desc) in place — Go's pdqsort (insertion sort up to 12
+        // terms); the sorted slice stays as it is under later sorts and Relax's SliceStable
         for (int i = 0; i < pc.n_preferred_terms; i++) sp.pnode.push_back(i);
-        std::stable_sort(sp.pnode.begin(), sp.pnode.end(), [&](int a, int b) {
-            return pc.preferred_terms[a].weight > pc.preferred_terms[b].weight;
-        });
+        {
+            struct D {
+                std::vector<int>& v;
+                const kp_pod_class& pc;
+                int size() const { return (int)v.size(); }
+                bool less(int a, int b) const { return pc.preferred_terms[v[a]].weight > pc.preferred_terms[v[b]].weight; }
+                void swap(int a, int b) { std::swap(v[a], v[b]); }
+            } d{sp.pnode, pc};
+            orc::go_sort_slice(d);
+        }
         for (int i = 0; i < pc.n_topology; i++) {
             const kp_topology_term& x = pc.topology[i];
             if (x.type == KP_TOPO_SPREAD) sp.spreads.push_back(i);

@@ -408,6 +408,31 @@ def add_relaxing_topology(rng, prob, p_req=0.5):
     return prob
 
 
+def add_many_groups(rng, prob, n_terms=24):
+    """Many distinct topology groups over one popular label (tier=web): spreads of several keys and maxSkews,
+    required anti-affinity (whose inverse groups constrain every pod they select) and affinity, spread over the
+    classes, so that the web classes are constrained by more than 8 groups and counted by more than 16."""
+    zones_keys = [ZONE, HOSTNAME, CAPACITY_TYPE]
+    for pc in prob.classes:
+        pc.labels = dict(pc.labels)
+        if rng.random() < 0.6:
+            pc.labels["tier"] = "web"
+    web = [Requirement("tier", "In", ["web"])]
+    for i in range(n_terms):
+        pc = prob.classes[int(rng.integers(0, len(prob.classes)))]
+        key = str(rng.choice(zones_keys, p=[0.45, 0.4, 0.15]))
+        u = rng.random()
+        if u < 0.5:
+            t = model.TopologyTerm("spread", key, web, max_skew=int(rng.integers(1, 40)),
+                                   node_affinity_policy=str(rng.choice(["Honor", "Ignore"])))
+        elif u < 0.8:
+            t = model.TopologyTerm("anti", key, web + [Requirement("app", "NotIn", ["x%d" % i])])
+        else:
+            t = model.TopologyTerm("affinity", key, web + [Requirement("app", "NotIn", ["y%d" % i])])
+        pc.topology = list(pc.topology) + [t]
+    return prob
+
+
 def fuzz_preference_consolidation(catalog, seed, n_nodes=30, n_pods=160, n_bound=30, all_spot=False, best_effort=False,
                                   zone_min=False):
     """fuzz_consolidation over pods with preferences to relax (add_preferences), pods of those classes bound to random

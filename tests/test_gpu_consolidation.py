@@ -538,6 +538,18 @@ def test_fuzz_consolidation_relaxing_topology(pctx, golden, seed):
                             pyoracle.consolidate(cp, mode, preference_policy=abi.KP_PREFERENCE_RESPECT))
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_fuzz_consolidation_many_groups(ctx, golden, seed):
+    """Probes over classes constrained by more than 8 topology groups and counted by more than 16 (add_many_groups)."""
+    rng = np.random.Generator(np.random.PCG64(4700 + seed))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 300)), replace=False))]
+    cp = fuzzgen.fuzz_topology_consolidation(sub, 4700 + seed, n_nodes=int(rng.integers(4, 50)),
+                                             n_pods=int(rng.integers(20, 200)), all_spot=seed % 4 == 0)
+    fuzzgen.add_many_groups(rng, cp.cluster, n_terms=int(rng.integers(14, 30)))
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        assert_probes_equal(device_probes(ctx, cp, mode), pyoracle.consolidate(cp, mode))
+
+
 def test_preference_relaxations_in_probes(pctx, golden):
     """The fuzz above relaxes preferences inside the probes (kp_consolidate_stats counter 16): under Respect every
     preference kind; under Ignore only the ORed required node-affinity terms (removeRequiredNodeAffinityTerm)."""

@@ -110,6 +110,34 @@ def test_topology_preference_fuzz(golden, seed):
         parity.assert_same(dev, _oracle(prob, policy))
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_many_preferred_terms_fuzz(golden, seed):
+    """More than 12 preferred node-affinity terms with tied weights: newPodRequirements' sort.Slice is Go's pdqsort
+    (unstable), so which tied term is tried first follows its exact swap sequence (kp_gosort_host.h on the host,
+    oracle/gosort.h in the oracle); Relax then walks that order."""
+    rng = np.random.Generator(np.random.PCG64(7800 + seed))
+    prob = synth.subsample(synth.config2(catalog=golden, seed=synth.SEED + seed), int(rng.integers(200, 600)))
+    cats = ["c", "m", "r", "t", "g", "i", "x", "z"]
+    zones = sorted({o.zone for it in golden for o in it.offerings})
+    for pc in prob.classes:
+        if rng.random() < 0.5:
+            continue
+        terms = []
+        for _ in range(int(rng.integers(13, 40))):
+            if rng.random() < 0.5:
+                r = Requirement(AWS + "instance-category", "In", [str(rng.choice(cats))])
+            else:
+                r = Requirement(model.ZONE, "In", [str(rng.choice(zones))])
+            terms.append((int(rng.choice([1, 5, 5, 10, 10, 10, 50])), [r]))
+        pc.preferred_terms = terms
+    ctx = _ctx(abi.KP_PREFERENCE_RESPECT)
+    try:
+        dev = parity.run_device(ctx, prob)
+    finally:
+        ctx.close()
+    parity.assert_same(dev, _oracle(prob, abi.KP_PREFERENCE_RESPECT))
+
+
 def relaxing_topology_problem(golden, seed):
     import fuzzgen
     rng = np.random.Generator(np.random.PCG64(7600 + seed))

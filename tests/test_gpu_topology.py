@@ -262,3 +262,15 @@ def test_overflow_rerun_once(golden):
         parity.assert_same(dev, parity.run_oracle(prob))
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_fuzz_many_groups(ctx, golden, seed):
+    """More than 8 topology groups constraining a class and more than 16 counting it (fuzzgen.add_many_groups): up to
+    KP_MAX_TOPO = 16 / KP_MAX_TOPO_REC = 64 per class, over a cluster with bound pods."""
+    rng = np.random.Generator(np.random.PCG64(seed + 8100))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=200, replace=False))]
+    prob = fuzzgen.fuzz_topology_existing_problem(sub, seed + 8100, n_pods=int(rng.integers(100, 400)),
+                                                  n_existing=int(rng.integers(4, 40)))
+    fuzzgen.add_many_groups(rng, prob, n_terms=int(rng.integers(10, 18)))  # 8-13 constraining, up to 27 counting
+    same(ctx, prob)
