@@ -119,11 +119,16 @@ struct ProbeTopo {
 // Per-pod snapshot of the value-keyed topology groups that constrain the current pod's class (FFD kernel, LDS; filled by
 // topo_prefilter_setup in CC.tc order): counts only change when a pod commits, so every candidate evaluation of the pod
 // reads them here instead of from the global counters.
+// One row per group; the LDS plan holds KpDev.snap_rows of them (the most constraining groups of any class, <=
+// KP_SNAP_ROWS), so a solve pays only for the rows its classes use.
+struct SnapRow {
+    int32_t cnt[64];   // domain counts (0 where the domain is not registered)
+    uint8_t rk[64];    // value-name rank of each domain (tie-break)
+    uint64_t known;    // registered domains
+    uint64_t podhas;   // domains the pod's own requirement for the key admits
+};
 struct TopoSnap {
-    int32_t cnt[KP_SNAP_ROWS][64];   // domain counts (0 where the domain is not registered)
-    uint8_t rk[KP_SNAP_ROWS][64];    // value-name rank of each domain (tie-break)
-    uint64_t known[KP_SNAP_ROWS];    // registered domains
-    uint64_t podhas[KP_SNAP_ROWS];   // domains the pod's own requirement for the key admits
+    SnapRow r[KP_SNAP_ROWS];
 };
 
 // Tables shared by every evaluation of a kernel (LDS in ffd_kernel).
@@ -473,10 +478,10 @@ __device__ __forceinline__ bool topo_narrow(const KpDev& d, const ClassCache& CC
         int cnt;
         uint32_t rk;
         if (!CT && snap && CC.ntc <= KP_SNAP_ROWS) {
-            kn = valid && ((snap->known[e] >> lane) & 1ull);
-            cnt = kn ? snap->cnt[e][lane] : 0;
-            pod_has = valid && ((snap->podhas[e] >> lane) & 1ull);
-            rk = valid ? snap->rk[e][lane] : 0xFFu;
+            kn = valid && ((snap->r[e].known >> lane) & 1ull);
+            cnt = kn ? snap->r[e].cnt[lane] : 0;
+            pod_has = valid && ((snap->r[e].podhas >> lane) & 1ull);
+            rk = valid ? snap->r[e].rk[lane] : 0xFFu;
         } else {
             if (CT) pt_row(d, *pt, g, lane);
             const uint64_t known = ld_u64(CT ? &pt->known[g] : &d.tg_known[g]);

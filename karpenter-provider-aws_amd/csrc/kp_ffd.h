@@ -110,27 +110,31 @@ __device__ inline void topo_prefilter_setup(const KpDev& d, FfdShared& S, int c,
         int k = T.key, lo = 0, hi = INT32_MAX, cmp = 0;
         uint64_t elig = 0;
         if (T.flags & 8) {  // hostname group: the candidate's host count must lie in [lo, hi]
-            if (type == 0) hi = T.skew - self;
-            else if (type == 2) hi = 0;
-            else lo = (self && ld_i32(&d.tg_pos[g]) == 0) ? 0 : 1;
+            if (type == 0) {
+                hi = T.skew - self;
+            } else if (type == 2) {
+                hi = 0;
+            } else {
+                lo = (self && ld_i32(&d.tg_pos[g]) == 0) ? 0 : 1;
+            }
         } else {
             const bool valid = (T.vmask >> lane) & 1ull;
+            SnapRow& Z = S.tsnap->r[e];
             const uint64_t known = ld_u64(&d.tg_known[g]);
             const int cnt_raw = ld_i32(&d.tg_cnt[(size_t)g * 64 + lane]);
             const uint8_t rk = d.vrank[(size_t)k * 64 + lane];
+            const int cnt = (valid && ((known >> lane) & 1ull)) ? cnt_raw : 0;
+            // topo_narrow's view of the group for every candidate of this pod (TopoSnap)
+            Z.cnt[lane] = cnt;
+            Z.rk[lane] = valid ? rk : 0xFFu;
+            if (lane == 0) {
+                Z.known = known;
+                Z.podhas = T.podhas;
+            }
             // the pod's domains: its requirement for the key (every class a value-keyed group constrains carries the key,
             // a topology-only key as Exists)
             const bool pod_has = (T.podhas >> lane) & 1ull;
             const bool kn = valid && ((known >> lane) & 1ull);
-            const int cnt = kn ? cnt_raw : 0;
-            // topo_narrow's view of the group for every candidate of this pod (TopoSnap)
-            TopoSnap& Z = *S.tsnap;
-            Z.cnt[e][lane] = cnt;
-            Z.rk[e][lane] = valid ? rk : 0xFFu;
-            if (lane == 0) {
-                Z.known[e] = known;
-                Z.podhas[e] = T.podhas;
-            }
             if (type == 0) {
                 const uint64_t sup = ballot(kn && pod_has);
                 int mn = wave_min_i32((kn && pod_has) ? cnt : INT32_MAX);

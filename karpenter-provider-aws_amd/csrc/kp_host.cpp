@@ -2558,6 +2558,10 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         HIPCHK(c->d_tg_pol.upload(tpol, s));
         HIPCHK(c->d_tg_frow.upload(tfrow, s));
         // late identities (topo_build): born at the start when a pod of the Solve (its input class) owns them
+        // TopoSnap rows the FFD kernel's LDS plan holds: the most constraining groups of any class (at most KP_SNAP_ROWS)
+        d.snap_rows = 1;
+        for (int i = 0; i < C && G > 0; i++)
+            d.snap_rows = std::max(d.snap_rows, std::min((int)th.cons[i].size(), (int)KP_SNAP_ROWS));
         c->tg_nlate = G > 0 ? th.n_late : 0;
         c->h_cls_birth.assign(std::max(C, 1), 0);
         d.born0 = 0;

@@ -366,7 +366,7 @@ static bool kp_ffd_plan_lds_tables(KpDev& d, int max_bytes) {
     if (d.alloc_global) {
         const int tp0 = (d.T + 63) / 64 * 64;
         size_t fixed = off + 8 * (size_t)tp0 + (d.multi16 ? 2 * (size_t)d.n_multi * tp0 : 0) +
-                       ro_bytes + (d.G > 0 ? sizeof(TopoSnap) : 0) + 256;
+                       ro_bytes + (d.G > 0 ? sizeof(SnapRow) * (size_t)d.snap_rows : 0) + 256;
         const long room = ((long)max_bytes - (long)fixed) / 9;
         // more NodeClaims than LDS holds beside the fixed tables: the slice arrays go to HBM (the HBM instantiations)
         if (room < ncmax) d.slice_hbm = d.g_key != nullptr;
@@ -394,7 +394,7 @@ static bool kp_ffd_plan_lds_tables(KpDev& d, int max_bytes) {
     d.off_ro = (int)off;
     if (d.ro) off = al(off + ro_bytes);
     d.off_tsnap = (int)off;
-    if (d.G > 0) off = al(off + sizeof(TopoSnap));
+    if (d.G > 0) off = al(off + sizeof(SnapRow) * (size_t)d.snap_rows);
     d.off_hr = (int)off;
     if ((int)off > max_bytes) {
         // large catalogs: the staged allocatable, then the multi-valued label masks, are read from HBM instead

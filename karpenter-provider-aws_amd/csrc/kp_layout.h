@@ -258,6 +258,7 @@ struct KpDev {
     // groups that Topology.Update creates when a pod relaxes into a spec owning them (kp_host.cpp topo_build): bit of
     // the group's late identity or -1 (null: none); cls_birth[c] = late identities class c owns (a pod relaxing into c
     // creates them); born0 = those a pod of the Solve owns from the start.  Records skip a late group until it is born.
+    int32_t snap_rows;               // TopoSnap rows in the FFD kernel's LDS plan (SnapRow)
     const int32_t* tg_late;
     const uint64_t* cls_birth;
     uint64_t born0;
