@@ -283,6 +283,29 @@ def launch_leg(a, golden, local, rank, world, dist, barrier):
     return out
 
 
+ROOFLINE_NOTE = ("the Solve is one serial chain run by ONE workgroup (8 waves on 1 of 256 CUs; every placement changes "
+                 "the state the next pod is checked against), so algorithmic bytes / kernel time is not an HBM-bandwidth "
+                 "figure: the kernel is latency-bound (waves waiting on dependent LDS / L2 round trips) — "
+                 "stage_cycles_per_pod breaks its time down")
+
+
+def stage_cycles_per_pod(ctx, iv, out, n_pods):
+    """One more kp_solve with KPSIM_PROFILE=1 (s_memtime stamps, after the timed region): the FFD kernel's shader-clock
+    cycles per pod by stage (wave 0's fast loop and slice sort, the block's slow-path evaluations and templates, the
+    topology prefilter setup / first-survivor scan), and the pods each path placed."""
+    os.environ["KPSIM_PROFILE"] = "1"
+    try:
+        ctx.solve(iv, out)
+        cyc = dict(zip(FFD_COUNTERS, ctx.ffd_cycles()))
+    finally:
+        del os.environ["KPSIM_PROFILE"]
+    ctx.prepare(iv)
+    out = {k: cyc[k] / n_pods for k in ("cyc_fast_loop", "cyc_sort", "cyc_slow_eval", "cyc_templates", "cyc_topo_setup",
+                                        "cyc_topo_scan") if cyc.get(k)}
+    out.update({k: int(cyc[k]) for k in ("quick_accepts", "topo_quick", "slow_pods", "ev_calls") if k in cyc})
+    return out
+
+
 def ffd_kernel_name(prob):
     """The Solve kernel instantiation a problem launches (kp_launch_ffd): topology groups → ffd_topo_kernel, reserved
     offerings → ffd_resv_kernel, both → ffd_resv_topo_kernel (preference relaxation adds _pref)."""
@@ -346,6 +369,8 @@ def solve_leg(a, cat, prob, metric, workload, cpu_sample, local, rank, world, di
         "ffd_counters": dict(zip(FFD_COUNTERS, ctx.ffd_cycles())),
         "cpu_baseline": None,
     }
+    line["roofline"]["note"] = ROOFLINE_NOTE
+    line["stage_cycles_per_pod"] = stage_cycles_per_pod(ctx, iv, out, P)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         import parity
         import pyoracle
@@ -483,6 +508,7 @@ def main():
         elapsed = float(tt.item())
 
     kt = np.array(ffd_ms).mean(axis=0)
+    stages = stage_cycles_per_pod(ctx, iv, out, prob.pods.n) if rank == 0 else None
     P = prob.pods.n
     value = P * a.steps * world / elapsed
     T = len(cat)
@@ -546,7 +572,9 @@ def main():
                        "parallelism": "replicas" if world > 1 else "single"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "ffd_kernel", "kernel_ms": float(kt[3]), "algorithmic_bytes": int(B)},
+                         "kernel": "ffd_kernel", "kernel_ms": float(kt[3]), "algorithmic_bytes": int(B),
+                         "note": ROOFLINE_NOTE},
+            "stage_cycles_per_pod": stages,
             "cpu_baseline": cpu,
             "parity_vs_cpu_baseline": parity_ok,  # device result bit-identical to the oracle's on the same input
             "kernel_ms": {"queue_sort": float(kt[0]), "class_mask": float(kt[1]), "template_init": float(kt[2]),
