@@ -5,6 +5,4 @@
 // One named entry point per feature instantiation, so kernel traces (rocprofv3 --stats) report the common case
 // (ffd_kernel: no topology groups, no reserved offerings) separately from the topology / reservation variants.
 __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_kernel(KpDev d) { ffd_solve<false, false, false>(d); }
-__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_topo_kernel(KpDev d) { ffd_solve<false, true, false>(d); }
 __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_hbm_kernel(KpDev d) { ffd_solve<false, false, false, true>(d); }
-__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_topo_hbm_kernel(KpDev d) { ffd_solve<false, true, false, true>(d); }

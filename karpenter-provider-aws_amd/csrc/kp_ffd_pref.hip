@@ -3,6 +3,4 @@
 #include "kp_ffd.h"
 
 __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_pref_kernel(KpDev d) { ffd_solve<false, false, true>(d); }
-__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_pref_topo_kernel(KpDev d) { ffd_solve<false, true, true>(d); }
 __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_pref_hbm_kernel(KpDev d) { ffd_solve<false, false, true, true>(d); }
-__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_pref_topo_hbm_kernel(KpDev d) { ffd_solve<false, true, true, true>(d); }

@@ -3,6 +3,4 @@
 #include "kp_ffd.h"
 
 __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_pref_resv_kernel(KpDev d) { ffd_solve<true, false, true>(d); }
-__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_pref_resv_topo_kernel(KpDev d) { ffd_solve<true, true, true>(d); }
 __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_pref_resv_hbm_kernel(KpDev d) { ffd_solve<true, false, true, true>(d); }
-__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_pref_resv_topo_hbm_kernel(KpDev d) { ffd_solve<true, true, true, true>(d); }

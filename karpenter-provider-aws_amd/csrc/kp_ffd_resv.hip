@@ -3,6 +3,4 @@
 #include "kp_ffd.h"
 
 __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_resv_kernel(KpDev d) { ffd_solve<true, false, false>(d); }
-__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_resv_topo_kernel(KpDev d) { ffd_solve<true, true, false>(d); }
 __global__ __launch_bounds__(KP_NWAVES * 64) void ffd_resv_hbm_kernel(KpDev d) { ffd_solve<true, false, false, true>(d); }
-__global__ __launch_bounds__(KP_NWAVES * 64) void ffd_resv_topo_hbm_kernel(KpDev d) { ffd_solve<true, true, false, true>(d); }

@@ -31,6 +31,7 @@
 #include "kp_layout.h"
 
 size_t kp_ffd_shared_bytes();
+size_t kp_ffd_shared_bytes_topo();
 bool kp_ffd_plan_lds(KpDev& d, int max_bytes);
 hipError_t kp_launch_class_mask(const KpDev& d, hipStream_t s);
 hipError_t kp_launch_template_init(const KpDev& d, hipStream_t s);
@@ -2697,7 +2698,10 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.err = c->d_err.p;
     d.profile = getenv("KPSIM_PROFILE") ? 1 : 0;
     // topology pods: candidates per block round (KPSIM_TOPO_CANDS, diagnostics)
-    d.topo_cands = getenv("KPSIM_TOPO_CANDS") ? std::max(1, std::min(KP_NWAVES, atoi(getenv("KPSIM_TOPO_CANDS")))) : KP_NWAVES;
+    {  // topology solves run the KP_NWAVES_TOPO-wave instantiations
+        const int nw = G > 0 ? KP_NWAVES_TOPO : KP_NWAVES;
+        d.topo_cands = getenv("KPSIM_TOPO_CANDS") ? std::max(1, std::min(nw, atoi(getenv("KPSIM_TOPO_CANDS")))) : nw;
+    }
     d.team_eval = getenv("KPSIM_NO_TEAM") ? 0 : 1;  // diagnostics: KPSIM_NO_TEAM=1 evaluates topology candidates one per wave
     d.noop_quick = getenv("KPSIM_NO_NOOP") ? 0 : 1;  // diagnostics: KPSIM_NO_NOOP=1 disables the no-op merge quick accept
     d.team_first = getenv("KPSIM_NO_TEAM_FIRST") ? 0 : 1;  // diagnostics: KPSIM_NO_TEAM_FIRST=1 evaluates it beside the others
@@ -2775,7 +2779,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     if (!kp_ffd_plan_lds(d, KP_LDS_BYTES)) return fail(ctx, KP_E_UNSUPPORTED, "FFD kernel LDS plan exceeds 160 KB");
     if (getenv("KPSIM_PROFILE"))
         fprintf(stderr, "[kpsim] FFD LDS plan: fixed block %zu B, quick rows %d (axes %d), NodeClaim slots %d, allocatable %s, "
-                "%d B of %d\n", kp_ffd_shared_bytes(), d.lds_nq, d.lds_A, d.lds_ncmax, d.alloc_global ? "HBM" : "LDS",
+                "%d B of %d\n", d.G > 0 ? kp_ffd_shared_bytes_topo() : kp_ffd_shared_bytes(), d.lds_nq, d.lds_A, d.lds_ncmax, d.alloc_global ? "HBM" : "LDS",
                 d.lds_bytes, KP_LDS_BYTES);
     c->P = P;
     c->C = C;

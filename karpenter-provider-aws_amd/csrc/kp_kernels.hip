@@ -337,6 +337,7 @@ __global__ void iota_kernel(int32_t* out, int n) {
 #include <hipcub/hipcub.hpp>
 
 size_t kp_ffd_shared_bytes() { return sizeof(FfdShared); }
+size_t kp_ffd_shared_bytes_topo();  // kp_ffd_base_topo.hip: FfdShared at KP_NWAVES_TOPO waves
 
 // Lay out the FFD kernel's dynamic LDS for this solve (fills d.off_*, d.lds_*).  Returns false if even the
 // quick-accept-free layout exceeds max_bytes.
@@ -358,7 +359,8 @@ static bool kp_ffd_plan_lds_tables(KpDev& d, int max_bytes) {
     d.ro_stage = d.ro && d.ro_n <= KP_RO_STAGE ? 1 : 0;
     const size_t ro_bytes = !d.ro ? 0 : sizeof(ResvTab) + 4 * (size_t)((d.ro_nrid + 1) & ~1) +
                                         (d.ro_stage ? 24 * (size_t)((d.ro_n + 1) & ~1) + 8 * (size_t)d.ro_w : 0);
-    size_t off = al(sizeof(FfdShared));
+    // the topology instantiations run KP_NWAVES_TOPO waves: their fixed block is smaller
+    size_t off = al(d.G > 0 ? kp_ffd_shared_bytes_topo() : sizeof(FfdShared));
     d.off_qw = (int)off;  // the queue window's pod requests, [64][R]
     off = al(off + 64 * 8 * (size_t)(d.R > 0 ? d.R : 1));
     int ncmax = d.NCcap < KP_MAX_NC ? d.NCcap : KP_MAX_NC;
@@ -457,7 +459,7 @@ hipError_t kp_launch_ffd(const KpDev& d, hipStream_t s) {
     const size_t bytes = (size_t)d.lds_bytes;
     // instantiation by solve features: reserved offerings (RESV), topology groups (TOPO), preference relaxation or
     // BestEffort minValues (PREF)
-    const dim3 g(1), b(KP_NWAVES * 64);
+    const dim3 g(1), b((d.G > 0 ? KP_NWAVES_TOPO : KP_NWAVES) * 64);
     const bool pref = d.relax_next || d.best_effort;
     if (d.slice_hbm) {
         void (*k)(KpDev) = pref ? (d.ro ? (d.G > 0 ? ffd_pref_resv_topo_hbm_kernel : ffd_pref_resv_hbm_kernel)

@@ -28,8 +28,9 @@
 #define KP_MAX_NP 63                 // NodePools (templates) per solve: template bitmasks are u64, bit 63 a flag
 #define KP_MAX_R 16                  // resource axes
 #ifndef KP_NWAVES
-#define KP_NWAVES 8                  // waves in the single-workgroup FFD kernel
+#define KP_NWAVES 8                  // waves in the single-workgroup FFD kernel (kp_ffd_*_topo.hip: KP_NWAVES_TOPO)
 #endif
+#define KP_NWAVES_TOPO 4             // waves of the topology instantiations
 #define KP_LDS_AXES 6                // allocatable axes staged in LDS
 #define KP_MAX_SCR_WORDS 64          // value-bitset words of one class's keys (per-wave LDS scratch)
 #define KP_MAX_MIN_WORDS 64          // value bitset for a minValues distinct count (4096 values)

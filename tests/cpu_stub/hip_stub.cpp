@@ -95,6 +95,7 @@ hipError_t hipEventElapsedTime(float* ms, hipEvent_t a, hipEvent_t b) {
 
 // ---- kernel launchers (the real ones live in kp_kernels.hip / kp_consolidate.hip / kp_launch.hip) ----
 size_t kp_ffd_shared_bytes() { return 0; }
+size_t kp_ffd_shared_bytes_topo() { return 0; }
 bool kp_ffd_plan_lds(KpDev& d, int) {
     d.lds_ncmax = d.NCcap < KP_MAX_NC ? d.NCcap : KP_MAX_NC;
     d.lds_tpad = (d.T + 63) / 64 * 64;
