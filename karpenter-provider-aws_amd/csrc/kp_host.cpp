@@ -1650,6 +1650,14 @@ static kp_status topo_build(kp_ctx* c, const kp_solve_input* in, const std::vect
         }
     }
     if (th.g.empty()) return KP_OK;
+    if (getenv("KPSIM_DIAG_IDENT")) {  // diagnostics: identities held by groups of different semantics
+        std::vector<int> per(idents.size(), 0);
+        for (const HGroup& g : th.g) per[g.ident]++;
+        int amb = 0;
+        for (int n : per) amb += n > 1;
+        fprintf(stderr, "[kpsim] topology identities %zu, groups %zu, identities with several semantics %d\n",
+                idents.size(), th.g.size(), amb);
+    }
     // late identities: a relaxed stage owns it and its input class does not
     const int NI = (int)idents.size();
     const int C0 = X.n_input;
