@@ -30,7 +30,9 @@
 #ifndef KP_NWAVES
 #define KP_NWAVES 8                  // waves in the single-workgroup FFD kernel (kp_ffd_*_topo.hip: KP_NWAVES_TOPO)
 #endif
+#ifndef KP_NWAVES_TOPO
 #define KP_NWAVES_TOPO 4             // waves of the topology instantiations
+#endif
 #define KP_LDS_AXES 6                // allocatable axes staged in LDS
 #define KP_MAX_SCR_WORDS 64          // value-bitset words of one class's keys (per-wave LDS scratch)
 #define KP_MAX_MIN_WORDS 64          // value bitset for a minValues distinct count (4096 values)

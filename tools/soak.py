@@ -108,19 +108,20 @@ def fam_cons_wide_resv(seed):
         assert_probes_equal(device_probes(ctx, cp, mode), pyoracle.consolidate(cp, mode))
 
 
-for name, fn in [("wide reservations (Solve)", fam_wide_resv), ("topology x preferences (Solve, 2 policies)", fam_topo_pref),
-                 ("relaxing topology (Solve, 2 policies)", fam_relaxing), ("many groups (Solve)", fam_many_groups),
-                 ("mutators x topology (consolidation)", fam_cons_mut_topo),
-                 ("wide reservations (consolidation)", fam_cons_wide_resv)]:
-    t = time.time()
-    bad = []
-    for seed in range(N):
-        try:
-            fn(seed)
-        except Exception:
-            bad.append(seed)
-            if len(bad) == 1:
-                traceback.print_exc(limit=3, file=sys.stderr)
-    print("%-45s seeds %d, mismatches %d %s, refused %d (%.0f s)" % (name, N, len(bad), bad[:8], len(REFUSED),
-                                                                    time.time() - t), flush=True)
-    REFUSED.clear()
+if __name__ == "__main__":
+    for name, fn in [("wide reservations (Solve)", fam_wide_resv), ("topology x preferences (Solve, 2 policies)", fam_topo_pref),
+                     ("relaxing topology (Solve, 2 policies)", fam_relaxing), ("many groups (Solve)", fam_many_groups),
+                     ("mutators x topology (consolidation)", fam_cons_mut_topo),
+                     ("wide reservations (consolidation)", fam_cons_wide_resv)]:
+        t = time.time()
+        bad = []
+        for seed in range(N):
+            try:
+                fn(seed)
+            except Exception:
+                bad.append(seed)
+                if len(bad) == 1:
+                    traceback.print_exc(limit=3, file=sys.stderr)
+        print("%-45s seeds %d, mismatches %d %s, refused %d (%.0f s)" % (name, N, len(bad), bad[:8], len(REFUSED),
+                                                                        time.time() - t), flush=True)
+        REFUSED.clear()
