@@ -229,6 +229,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
         P.hpos = reinterpret_cast<int32_t*>(smem + k.off_hpos);
         P.ha = k.tg_ha;
         P.born = &S.born;
+        P.excl = excl;
         P.E = d.E;
         P.HG = k.HG;
     }

@@ -113,6 +113,7 @@ struct ProbeTopo {
     int32_t* hpos;         // LDS [n_ha]: hostname domains holding a selected pod, per hostname-affinity group
     const int32_t* ha;     // [G] hostname-affinity group index into hpos, or -1
     uint64_t* born;        // LDS: the probe's born late identities (KpDev.tg_late)
+    const uint64_t* excl;  // LDS [EW]: the probe's candidates (their nodes leave the cluster)
     int E, HG;
 };
 
@@ -429,6 +430,29 @@ __device__ __forceinline__ int pt_hcnt(const KpDev& d, const ProbeTopo& P, int h
     if ((P.hmod[host >> 6] >> (host & 63)) & 1ull) c += ld_i32(col + host);
     return c;
 }
+// nextDomainAffinity's bootstrap test for a self-selecting hostname affinity (entry T of the class, group g): no host
+// the pod's domains admit holds a selected pod (options.Len() == 0).  podDomains is every host unless the pod requires
+// the hostname (T.hdom): In — none of the listed existing nodes is positive; NotIn — every positive host is listed.
+// A listed node among a consolidation probe's candidates counts what its own reschedulable pods leave.  Whole wave.
+template <bool CT>
+__device__ inline bool host_aff_unseeded(const KpDev& d, const KpTopoCons& T, int g, const ProbeTopo* pt, int lane) {
+    const int pos = CT ? pt->hpos[pt->ha[g]] : ld_i32(&d.tg_pos[g]);
+    const int mode = T.hdom & 3;
+    if (mode == 0) return pos == 0;
+    const int n = T.hdom >> 2, hrow = -1 - T.key;
+    int np = 0;
+    for (int b = 0; b < n; b += 64) {
+        bool p = false;
+        if (b + lane < n) {
+            const int2 h = d.tce_hosts[T.podhas + b + lane];
+            if (CT && ((pt->excl[h.x >> 6] >> (h.x & 63)) & 1ull)) p = h.y != 0;
+            else p = (CT ? pt_hcnt(d, *pt, hrow, h.x) : ld_i32(&d.tg_hcnt[(size_t)hrow * d.HN + h.x])) > 0;
+        }
+        np += __popcll(ballot(p));
+    }
+    return mode == 1 ? np == 0 : pos == np;
+}
+
 // one more pod counted in hostname row hrow at `host` (whole wave)
 __device__ inline void pt_hadd(const ProbeTopo& P, int hrow, int host, int lane) {
     if (host < P.E && !((P.hmod[host >> 6] >> (host & 63)) & 1ull)) {
@@ -465,7 +489,7 @@ __device__ __forceinline__ bool topo_narrow(const KpDev& d, const ClassCache& CC
             bool ok;
             if (type == 0) ok = cnt + self <= info.z;             // spread: hostname domainMinCount is 0
             else if (type == 2) ok = cnt == 0;                    // anti-affinity: an empty domain
-            else ok = cnt > 0 || (self && (CT ? pt->hpos[pt->ha[g]] : ld_i32(&d.tg_pos[g])) == 0);  // affinity (self-selecting bootstrap)
+            else ok = cnt > 0 || (self && host_aff_unseeded<CT>(d, d.cls_tce[d.cls_tcoff[CC.cls] + e], g, pt, lane));  // affinity (self-selecting bootstrap)
             if (!ok) {
                 ws.memo_ok = 0;
                 return false;

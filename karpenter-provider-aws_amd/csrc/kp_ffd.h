@@ -85,6 +85,10 @@ struct FfdShared {
     // domain a constraining group allows cannot accept the pod, and is skipped without an evaluation
     int tp_n, topo_pod, topo_quick;
     int ex_placed;                 // the current topology pod went to this existing node (-1: none accepted it)
+    // add() tries the existing nodes before sort.Slice: a topology pod meets a pending slice sort (dirty_kind, eager) with
+    // the existing nodes still untried — the block tries them first (topo_defer) and, when none takes the pod, hands it
+    // back to wave 0 (topo_resume) for the sort; topo_exdone: the block skips the existing nodes on that pass
+    int topo_defer, topo_resume, topo_exdone;
     int tp_all;                    // the prefilter holds every constraining group (at most KP_SNAP_ROWS)
     int tp_k[KP_SNAP_ROWS];        // value-keyed group: key; hostname group: -1 - row of tg_hcnt
     int tp_lo[KP_SNAP_ROWS], tp_hi[KP_SNAP_ROWS];  // hostname group: the host's count must lie in [lo, hi]
@@ -115,7 +119,7 @@ __device__ inline void topo_prefilter_setup(const KpDev& d, FfdShared& S, int c,
             } else if (type == 2) {
                 hi = 0;
             } else {
-                lo = (self && ld_i32(&d.tg_pos[g]) == 0) ? 0 : 1;
+                lo = (self && host_aff_unseeded<false>(d, T, g, nullptr, lane)) ? 0 : 1;
             }
         } else {
             const bool valid = (T.vmask >> lane) & 1ull;
@@ -639,6 +643,9 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
         S.tsnap = d.G > 0 ? reinterpret_cast<TopoSnap*>(smem + d.off_tsnap) : nullptr;
         S.topo_pod = 0;
         S.topo_quick = 0;
+        S.topo_defer = 0;
+        S.topo_resume = 0;
+        S.topo_exdone = 0;
         S.qhead = 0;
         S.qcount = P;
         S.done = 0;
@@ -812,7 +819,17 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 wa = q < N && absorbed(wm);
                 wcnt = 0;
             };
+            int resume = TOPO_ON ? S.topo_resume : 0;  // the current pod comes back from the block for the sort
             for (;;) {
+              int p, off, shape;
+              long long t_a;
+              if (TOPO_ON && resume) {
+                resume = 0;
+                p = S.cur_pod;
+                off = -1;
+                shape = prev_shape;
+                t_a = prof_clock(d);
+              } else {
                 if (qcount == 0 || err) {
                     done = 1;
                     break;
@@ -845,13 +862,14 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                     qw_used = 0;
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 }
-                const long long t_a = prof_clock(d);
-                const int off = qw_used;
+                t_a = prof_clock(d);
+                off = qw_used;
                 if (rl32(vlast, off) == qcount) {
                     done = 1;
                     break;
                 }
-                const int p = rl32(vp, off), shape = rl32(vshape, off);
+                p = rl32(vp, off);
+                shape = rl32(vshape, off);
                 qw_used++;
                 qhead = qhead + 1 == P ? 0 : qhead + 1;
                 qcount--;
@@ -924,6 +942,22 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                     ex_flush();
                     xstart = d.E;
                 }
+                if (TOPO_ON && ctopo && (dkind || eager) && d.E > 0) {
+                    // the slice sort (or the block's eager move becoming Go's) waits for the block's existing-node
+                    // pass (topo_defer above)
+                    win_flush();
+                    wb = -1;
+                    if (lane < R) S.pod_req[lane] = qw_req[off * R + lane];
+                    if (lane == 0) {
+                        S.cur_pod = p;
+                        S.cls_fill = S.CC.cls != c;
+                        S.topo_pod = 1;
+                        S.topo_defer = 1;
+                        S.topo_exdone = 0;
+                    }
+                    break;
+                }
+              }
                 scanned += N;
                 const long long t_b = prof_clock(d);
                 cqpop += t_b - t_a;
@@ -1012,11 +1046,12 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                     // recording, or the evaluation of candidates); counts change with every placement
                     win_flush();
                     wb = -1;
-                    if (lane < R) S.pod_req[lane] = qw_req[off * R + lane];
+                    if (off >= 0 && lane < R) S.pod_req[lane] = qw_req[off * R + lane];
                     if (lane == 0) {
                         S.cur_pod = p;
                         S.cls_fill = S.CC.cls != c;
                         S.topo_pod = 1;
+                        S.topo_exdone = off < 0;  // a resumed pod: no existing node took it
                     }
                     break;
                 }
@@ -1227,6 +1262,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 S.scan_start = sstart;
                 S.eager = eager;
                 S.any_rej = any_rej;
+                S.topo_resume = 0;
                 // reset here, behind the barrier that opens the slow path: the winner wave reads it at its commit,
                 // which no barrier separates from the end of the iteration
                 S.rej_volatile = 0;
@@ -1272,7 +1308,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
         const long long c_slow = prof_clock(d);
         if (d.profile && tid == 0) S.st[ST_SEG + 0] += c_slow - c_top;
         const int pod = S.cur_pod;
-        if (TOPO_ON && S.topo_pod && d.E > 0) {
+        if (TOPO_ON && S.topo_pod && d.E > 0 && !S.topo_exdone) {
             // ================= a pod with topology terms: existing nodes first (wave 0) =================
             // ExistingNode.Add in scheduling order: tolerations + Compatible (XT) and headroom, then the requirement
             // merge and Topology.AddRequirements on the node's own domains; the first node that accepts takes the pod
@@ -1287,10 +1323,12 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 }
             }
             __syncthreads();
-            if (S.ex_placed >= 0) {
+            if (S.ex_placed >= 0 || S.topo_defer) {
                 if (tid == 0) {
                     S.tp_n = 0;
                     S.topo_pod = 0;
+                    S.topo_resume = S.ex_placed < 0;  // no existing node took it: wave 0 sorts, then the NodeClaims
+                    S.topo_defer = 0;
                 }
                 __syncthreads();
                 continue;

@@ -572,6 +572,7 @@ struct kp_ctx {
     DBuf<int32_t> d_tg_hrow, d_tg_owner, d_tg_pol, d_tg_cnt0, d_tg_cnt, d_tg_hcnt0, d_tg_hcnt, d_tg_pos0, d_tg_pos,
         d_cls_tcoff, d_cls_tc, d_cls_troff, d_cls_tr;
     DBuf<KpTopoCons> d_cls_tce;
+    DBuf<int2> d_tce_hosts;
     DBuf<int2> d_tg_frow;
     DBuf<int32_t> d_tg_late;
     DBuf<uint64_t> d_cls_birth, d_born_s, d_born_m;
@@ -1835,6 +1836,9 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         }
         if (hostname_key >= 0) exlab[j].push_back({hostname_key, c->sol.keys[hostname_key].id(en.name ? en.name : "")});
     }
+    std::map<int, int> host_node;  // hostname value id → existing node
+    if (hostname_key >= 0)
+        for (int j = E - 1; j >= 0; j--) host_node[exlab[j].back().second] = j;
     const int K = (int)c->sol.keys.size();
     if (K > KP_MAX_KEYS) return fail(ctx, KP_E_UNSUPPORTED, "too many label keys");
     // ExistingNode.Add's requirement merge only changes a node when a NotIn / DoesNotExist pod requirement meets a key
@@ -2342,6 +2346,8 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         std::vector<uint64_t> tknown0(G1, 0);
         std::vector<int32_t> tcoff(C + 1, 0), tcl, troff(C + 1, 0), trl;
         std::vector<KpTopoCons> tce;
+        std::vector<int2> tce_hosts;  // KpTopoCons.hdom lists
+        std::vector<int> tce_hosts_g; // ... the entry's group
         std::vector<KpTopoRec> tre;
         std::vector<uint8_t> vrank((size_t)K * 64, 0xFF);
         // hostname rows: existing nodes, then NodeClaim ids 0 .. NCcap, the last a spare that stays 0 (a template
@@ -2446,6 +2452,25 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
                     t.mindom = g.mindom;
                     if (g.host) {
                         t.key = -1 - g.hrow;
+                        // nextDomainAffinity counts the positive domains podDomains admits: a pod requiring the hostname
+                        // (In / NotIn a list; Exists admits every host) lists the existing nodes its values name
+                        const auto& rq = c->pref.has_strict[i] ? cstrict[i] : creq[i];
+                        const auto hit = rq.find(g.key);
+                        if (g.type == KP_TOPO_AFFINITY && self && !g.inverse && hit != rq.end()) {
+                            const HReq& q = hit->second;
+                            if (!(q.complement && q.vals.empty() && !q.has_gt && !q.has_lt)) {
+                                const int off = (int)tce_hosts.size();
+                                if (!q.has_gt && !q.has_lt)  // bounds admit no host name (Has parses an integer)
+                                    for (int v : q.vals) {
+                                        const auto f = host_node.find(v);
+                                        if (f == host_node.end()) continue;
+                                        tce_hosts.push_back(make_int2(f->second, 0));
+                                        tce_hosts_g.push_back(gi);
+                                    }
+                                t.hdom = (((int)tce_hosts.size() - off) << 2) | (q.complement ? 2 : 1);
+                                t.podhas = (uint64_t)off;
+                            }
+                        }
                     } else {
                         t.key = g.key;
                         // podDomains: the strict requirements' (no preferred term) requirement for the key, else Exists
@@ -2553,11 +2578,26 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
             for (int ci = 0; ci < c->cons_extra_ncand; ci++)
                 for (auto& kv : c->cons_hdec[ci])
                     if (hc0[(size_t)th.g[kv.first].hrow * HN + cand_node[ci]] == kv.second) c->cons_hlost[ci].push_back(kv.first);
+            // hostname lists (KpTopoCons.hdom): a candidate's node keeps a selected pod its probe does not reschedule
+            std::map<int, int> node_cand;
+            for (int ci = 0; ci < c->cons_extra_ncand; ci++) node_cand[cand_node[ci]] = ci;
+            for (size_t q = 0; q < tce_hosts.size(); q++) {
+                const int j = tce_hosts[q].x, gi = tce_hosts_g[q];
+                int left = hc0[(size_t)th.g[gi].hrow * HN + j];
+                const auto nc = node_cand.find(j);
+                if (nc != node_cand.end()) {
+                    const auto dec = c->cons_hdec[nc->second].find(gi);
+                    if (dec != c->cons_hdec[nc->second].end()) left -= dec->second;
+                }
+                tce_hosts[q].y = left > 0;
+            }
             c->h_tpos0.assign(tpos0.begin(), tpos0.end());
         }
         if (tcl.empty()) tcl.push_back(0);
         if (trl.empty()) trl.push_back(0);
         if (tce.empty()) tce.push_back(KpTopoCons{});
+        if (tce_hosts.empty()) tce_hosts.push_back(make_int2(0, 0));
+        HIPCHK(c->d_tce_hosts.upload(tce_hosts, s));
         if (tre.empty()) tre.push_back(KpTopoRec{});
         HIPCHK(c->d_cls_tce.upload(tce, s));
         HIPCHK(c->d_cls_tre.upload(tre, s));
@@ -2741,6 +2781,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.cls_troff = c->d_cls_troff.p;
     d.cls_tr = c->d_cls_tr.p;
     d.cls_tce = c->d_cls_tce.p;
+    d.tce_hosts = c->d_tce_hosts.p;
     d.cls_tre = c->d_cls_tre.p;
     d.cls_kneutral = c->d_cls_kneutral.p;
     d.vrank = c->d_vrank.p;

@@ -111,8 +111,11 @@ struct ResvTab {
 // one row instead of walking cls_tc → tg_info → the class digest: flags = type | self << 2 | hostname << 3; key = the
 // group's key, or -1 - its row of tg_hcnt for a hostname group; podhas = the class's domains of the key (value ids < 64
 // its requirement admits), vmask = the key's dictionary (value ids < nval).
+// A self-selecting hostname pod affinity whose pod requirements restrict the hostname (podDomains In / NotIn a list):
+// hdom = (n << 2) | 1 (In) or 2 (NotIn), podhas = the offset of the list's n existing nodes in KpDev.tce_hosts; hdom = 0
+// when podDomains holds every host.
 struct KpTopoCons {
-    int32_t g, key, flags, skew, mindom, pad;
+    int32_t g, key, flags, skew, mindom, hdom;
     uint64_t podhas, vmask;
 };
 // ... of one (class, recording topology group) entry: flags = type | inverse << 2 | hostname << 3; key as above;
@@ -276,6 +279,8 @@ struct KpDev {
     const uint8_t* cls_kneutral;     // parallel to cls_keys: 1 = key added only so topology can narrow it
     const uint8_t* vrank;            // [K][64] rank of value id v among the key's values by name (tie-break)
     const struct KpTopoCons* cls_tce; // parallel to cls_tc: the entry's static operands (FFD kernel prefilter setup)
+    const int2* tce_hosts;           // KpTopoCons.hdom lists: (existing node, 1 = it still holds a selected pod once its
+                                     // own consolidation candidate's pods leave)
     const struct KpTopoRec* cls_tre;  // parallel to cls_tr: the entry's static operands (topology quick accept's Record)
 
     // ---------------- FFD kernel LDS plan (kp_ffd_plan_lds) ----------------

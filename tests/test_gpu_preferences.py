@@ -90,7 +90,7 @@ def test_preference_fuzz(golden, seed):
         parity.assert_same(dev, _oracle(prob, policy))
 
 
-@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("seed", list(range(12)) + [2058, 2233])  # + tools/soak.py topo_pref 58 / 233
 def test_topology_preference_fuzz(golden, seed):
     """Preferred node-affinity terms on pods with topology terms over a cluster (fuzzgen.add_topology_preferences after
     fuzz_topology_existing_problem): preferences on the zone / capacity-type topology keys (podDomains from the strict

@@ -153,6 +153,68 @@ def test_existing_nodes_hostname_anti_affinity(ctx, golden):
     assert r.n_nodeclaims == 5
 
 
+def _hostname_affinity_problem(golden, op, hosts, bound_on):
+    """a self-selecting hostname pod affinity whose pod requires the hostname (op hosts); a selected pod is bound on
+    node `bound_on` of three existing nodes"""
+    lab = {"app": "ha", "tier": "web"}
+    pc = model.PodClass(labels=lab, requirements=[model.Requirement(model.HOSTNAME, op, hosts)],
+                        topology=[model.TopologyTerm("affinity", model.HOSTNAME, TC.sel({"tier": "web"}))])
+    pods = synth.pods_from_specs([(0, {"cpu": "1", "memory": "1Gi"})] * 2)
+    it = next(t for t in golden if t.name == "m5.2xlarge")
+    nodes = [model.ExistingNode("node-%d" % j, synth.node_labels(it, "test-zone-1a", "on-demand", "default"),
+                                np.array(it.allocatable, np.int64)) for j in range(3)]
+    return model.Problem(golden, [synth.default_nodepool()], [pc], pods, nodes, bound=[(bound_on, 0)])
+
+
+@pytest.mark.parametrize("op,hosts,bound_on,want", [
+    ("In", ["node-1"], 0, [-3, -3]),             # the positive host is outside podDomains: bootstrap on node-1
+    ("In", ["node-0", "node-1"], 0, [-2, -2]),   # a positive host inside podDomains: only it
+    ("NotIn", ["node-0"], 0, [-3, -3]),          # every positive host excluded: bootstrap on the first node left
+    ("NotIn", ["node-2"], 0, [-2, -2]),
+    ("In", ["node-2", "node-7"], 1, [-4, -4]),   # a name no node carries
+])
+def test_hostname_affinity_pod_domains(ctx, golden, op, hosts, bound_on, want):
+    """nextDomainAffinity counts only the positive domains the pod's own requirements admit (soak: many_groups 199):
+    a pod requiring hostname In [node-1] with a selected pod bound elsewhere bootstraps on node-1."""
+    r, _ = same(ctx, _hostname_affinity_problem(golden, op, hosts, bound_on))
+    assert list(r.pod_result) == want
+
+
+def _sort_skipped_problem(golden):
+    """four self-spread pods fill NodeClaims 0 and 1 (two each; the slice is [1, 0] after the fourth), a plain pod joins
+    NodeClaim 1 (a sort pending: 3 pods ahead of 2), and the last pod — a topology pod only the tainted existing node accepts — never reaches sort.Slice"""
+    sp = model.PodClass(labels={"app": "s"}, topology=[model.TopologyTerm("spread", model.HOSTNAME, TC.sel({"app": "s"}),
+                                                                         max_skew=2)])
+    plain = model.PodClass(labels={"app": "y"})
+    tp = model.PodClass(labels={"app": "t"}, requirements=[model.Requirement("team", "In", ["a"])],
+                        tolerations=[model.Toleration("dedicated", "Exists")],
+                        topology=[model.TopologyTerm("anti", model.HOSTNAME, TC.sel({"app": "nobody"}))])
+    pods = synth.pods_from_specs([(0, {"cpu": "2", "memory": "1Gi"})] * 4 + [(1, {"cpu": "1500m", "memory": "1Gi"}),
+                                                                          (2, {"cpu": "1", "memory": "1Gi"})])
+    it = next(t for t in golden if t.name == "m5.2xlarge")
+    labels = dict(synth.node_labels(it, "test-zone-1a", "on-demand", "default"), team="a")
+    node = model.ExistingNode("node-0", labels, np.array(it.allocatable, np.int64),
+                              taints=[model.Taint("dedicated", "x", "NoSchedule")])
+    return model.Problem(golden, [synth.default_nodepool()], [sp, plain, tp], pods, [node])
+
+
+def _eager_move_problem(golden):
+    """_sort_skipped_problem with the plain pod a topology pod too: the block commits it and moves its NodeClaim ahead
+    of the sort (the eager move), which the last pod's add() — taken by the existing node — must not adopt"""
+    prob = _sort_skipped_problem(golden)
+    prob.classes[1].topology = [model.TopologyTerm("anti", model.HOSTNAME, TC.sel({"app": "nobody"}))]
+    return prob
+
+
+@pytest.mark.parametrize("mk", [_sort_skipped_problem, _eager_move_problem])
+def test_existing_node_takes_topology_pod_before_sort(ctx, golden, mk):
+    """add() tries the existing nodes before sort.Slice(newNodeClaims): a topology pod an existing node takes leaves the
+    slice unsorted (soak: topo_pref 58 — the device sorted for it, then placed it on the node)."""
+    r, _ = same(ctx, mk(golden))
+    assert list(r.pod_result) == [0, 0, 1, 1, 1, -2]
+    assert list(r.nodeclaim_slice_pos) == [1, 0]
+
+
 @pytest.mark.parametrize("seed", range(24))
 def test_fuzz_topology_existing(ctx, golden, seed):
     """Topology terms over a cluster: existing nodes (placement order, headroom, taints, team labels, hostname /
@@ -264,7 +326,7 @@ def test_overflow_rerun_once(golden):
         c.close()
 
 
-@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("seed", list(range(8)) + [1872, 1899])  # + tools/soak.py many_groups 172 / 199
 def test_fuzz_many_groups(ctx, golden, seed):
     """More than 8 topology groups constraining a class and more than 16 counting it (fuzzgen.add_many_groups): up to
     KP_MAX_TOPO = 16 / KP_MAX_TOPO_REC = 64 per class, over a cluster with bound pods."""
