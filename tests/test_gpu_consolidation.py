@@ -474,6 +474,35 @@ def test_fuzz_consolidation_hostname_affinity(ctx, golden, seed):
                           pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH, spot_to_spot=s2s))
 
 
+def hostname_pod_domains_consolidation(golden, seed):
+    """fuzz_topology_consolidation with hostname pod affinity, and hostname requirements (In / NotIn a few node names,
+    candidates among them) on the classes with a hostname affinity term: the bootstrap counts only the positive hosts
+    the pod admits, a candidate's node counting what its reschedulable pods leave (KpTopoCons.hdom)"""
+    rng = np.random.Generator(np.random.PCG64(3900 + seed))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 300)), replace=False))]
+    cp = fuzzgen.fuzz_topology_consolidation(sub, 3900 + seed, n_nodes=int(rng.integers(4, 40)),
+                                             n_pods=int(rng.integers(20, 200)), host_affinity=True,
+                                             n_bound=int(rng.integers(0, 40)))
+    names = [e.name for e in cp.cluster.existing]
+    for pc in cp.cluster.classes:
+        if not any(t.kind == "affinity" and t.key == model.HOSTNAME for t in pc.topology) or rng.random() < 0.3:
+            continue
+        pick = sorted(set(str(names[int(i)]) for i in rng.integers(0, len(names), size=int(rng.integers(1, 5)))))
+        pc.requirements = [r for r in pc.requirements if r.key != model.HOSTNAME]
+        pc.requirements.append(model.Requirement(model.HOSTNAME, "In" if rng.random() < 0.5 else "NotIn", pick))
+    return cp
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_fuzz_consolidation_hostname_pod_domains(ctx, golden, seed):
+    """Probes and the command over hostname_pod_domains_consolidation against the oracle."""
+    cp = hostname_pod_domains_consolidation(golden, seed)
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        assert_probes_equal(device_probes(ctx, cp, mode), pyoracle.consolidate(cp, mode))
+    assert_commands_equal(device_command(ctx, cp, abi.KP_CONSOLIDATE_BOTH),
+                          pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH))
+
+
 # ------------------------------------------------------------------------------------------------
 # consolidation over pods with preferences (PREFERENCE_POLICY Respect / Ignore) and MIN_VALUES_POLICY=BestEffort
 # ------------------------------------------------------------------------------------------------

@@ -16,7 +16,8 @@ import fuzzgen  # noqa: E402
 import parity  # noqa: E402
 import pyoracle  # noqa: E402
 from kpsim import abi, catalog, model, native, synth  # noqa: E402
-from test_gpu_consolidation import assert_probes_equal, device_probes  # noqa: E402
+from test_gpu_consolidation import (assert_commands_equal, assert_probes_equal, device_command, device_probes,  # noqa: E402
+                                    hostname_pod_domains_consolidation)
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 40
 REFUSED = []
@@ -108,11 +109,20 @@ def fam_cons_wide_resv(seed):
         assert_probes_equal(device_probes(ctx, cp, mode), pyoracle.consolidate(cp, mode))
 
 
+def fam_cons_host_domains(seed):
+    cp = hostname_pod_domains_consolidation(g, 1000 + seed)
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        assert_probes_equal(device_probes(ctx, cp, mode), pyoracle.consolidate(cp, mode))
+    assert_commands_equal(device_command(ctx, cp, abi.KP_CONSOLIDATE_BOTH),
+                          pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH))
+
+
 if __name__ == "__main__":
     for name, fn in [("wide reservations (Solve)", fam_wide_resv), ("topology x preferences (Solve, 2 policies)", fam_topo_pref),
                      ("relaxing topology (Solve, 2 policies)", fam_relaxing), ("many groups (Solve)", fam_many_groups),
                      ("mutators x topology (consolidation)", fam_cons_mut_topo),
-                     ("wide reservations (consolidation)", fam_cons_wide_resv)]:
+                     ("wide reservations (consolidation)", fam_cons_wide_resv),
+                     ("hostname podDomains (consolidation)", fam_cons_host_domains)]:
         t = time.time()
         bad = []
         for seed in range(N):
