@@ -189,14 +189,18 @@ __device__ __forceinline__ bool topo_prefilter_pass(const KpDev& d, const FfdSha
 
 // wave 0: the first slice position in [start, N) that has not rejected the shape, whose template's taints the class
 // tolerates (tol: bit j = template j) and that passes the topology prefilter (N if none).  Four 64-position chunks per
-// round so the prefilter's global loads of 256 NodeClaims overlap.
+// round (KP_TSCAN_U) so the prefilter's global loads of 64 * KP_TSCAN_U NodeClaims overlap.
+#ifndef KP_TSCAN_U
+#define KP_TSCAN_U 2
+#endif
 __device__ inline int topo_scan(const KpDev& d, const FfdShared& S, const uint32_t* skey, const uint16_t* sord,
                                 const uint8_t* stmpl, uint64_t tol, int N, int start, int lane) {
-    for (int base = start; base < N; base += 256) {
-        bool ok[4];
-        int nc[4];
+    constexpr int U = KP_TSCAN_U;
+    for (int base = start; base < N; base += 64 * U) {
+        bool ok[U];
+        int nc[U];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < U; u++) {
             const int p = base + u * 64 + lane;
             ok[u] = p < N && !(skey[p] >> 31);
             nc[u] = ok[u] ? (int)sord[p] : 0;
@@ -207,23 +211,23 @@ __device__ inline int topo_scan(const KpDev& d, const FfdShared& S, const uint32
             if (k < 0) {
                 const int32_t* row = d.tg_hcnt + (size_t)(-1 - k) * d.HN + d.E;
                 const int lo = S.tp_lo[e], hi = S.tp_hi[e];
-                int cnt[4];
+                int cnt[U];
 #pragma unroll
-                for (int u = 0; u < 4; u++) cnt[u] = ok[u] ? ld_i32(row + nc[u]) : 0;
+                for (int u = 0; u < U; u++) cnt[u] = ok[u] ? ld_i32(row + nc[u]) : 0;
 #pragma unroll
-                for (int u = 0; u < 4; u++) ok[u] = ok[u] && cnt[u] >= lo && cnt[u] <= hi;
+                for (int u = 0; u < U; u++) ok[u] = ok[u] && cnt[u] >= lo && cnt[u] <= hi;
             } else {
                 const uint64_t el = S.tp_elig[e];
                 const bool cmp = S.tp_cmp[e];
-                uint32_t fl[4];
-                uint64_t w[4];
+                uint32_t fl[U];
+                uint64_t w[U];
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
+                for (int u = 0; u < U; u++) {
                     fl[u] = ok[u] ? d.nc_hdr[(size_t)nc[u] * d.K + k].flags : 0u;
                     w[u] = ok[u] ? d.nc_words[(size_t)nc[u] * d.DW + d.woff[k]] : 0ull;
                 }
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
+                for (int u = 0; u < U; u++) {
                     const bool pass = !(fl[u] & RF_DEF) ? el != 0 : (fl[u] & RF_CMP) ? (cmp || (~w[u] & el) != 0)
                                                                                        : (w[u] & el) != 0;
                     ok[u] = ok[u] && pass;
@@ -231,7 +235,7 @@ __device__ inline int topo_scan(const KpDev& d, const FfdShared& S, const uint32
             }
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < U; u++) {
             const uint64_t m = ballot(ok[u]);
             if (m) return base + u * 64 + __ffsll((unsigned long long)m) - 1;
         }
@@ -240,13 +244,14 @@ __device__ inline int topo_scan(const KpDev& d, const FfdShared& S, const uint32
 }
 
 // The whole block: the first slice position in [start, N) that passes topo_scan's tests (N if none).  Wave w scans the
-// 256 positions [base + 256 w, base + 256 w + 256) of each round (2,048 positions per round, one barrier), and the
+// SPAN = 64 * KP_TSCAN_U positions [base + SPAN w, base + SPAN (w + 1)) of each round (one barrier per round), and the
 // round's lowest survivor wins; rounds stop at the first that has one.  red: [2][KP_NWAVES] LDS, by round parity.
 __device__ inline int topo_scan_block(const KpDev& d, const FfdShared& S, const uint32_t* skey, const uint16_t* sord,
                                       const uint8_t* stmpl, uint64_t tol, int N, int start, int (*red)[KP_NWAVES],
                                       int wave, int lane) {
-    for (int base = start, r = 0; base < N; base += 256 * KP_NWAVES, r ^= 1) {
-        const int wb = base + 256 * wave, we = wb + 256 < N ? wb + 256 : N;
+    constexpr int SPAN = 64 * KP_TSCAN_U;
+    for (int base = start, r = 0; base < N; base += SPAN * KP_NWAVES, r ^= 1) {
+        const int wb = base + SPAN * wave, we = wb + SPAN < N ? wb + SPAN : N;
         int f = wb < N ? topo_scan(d, S, skey, sord, stmpl, tol, we, wb, lane) : N;
         if (f >= we) f = N;  // topo_scan reports "none" as its end bound
         if (lane == 0) red[r][wave] = f;
