@@ -585,6 +585,10 @@ struct kp_ctx {
     // reschedulable pods (node, pod, candidate) join the base counts; cons_dec[candidate][group] = its value-keyed counts
     std::vector<std::array<int, 3>> cons_extra;
     int cons_extra_ncand = 0;
+    // ... and the pending pods, in SimulateScheduling's order: with cons_topo set, topo_build picks each topology
+    // identity's first owner per probe (pending pods, then the candidates' pods) instead of over the cluster's pods
+    std::vector<int> cons_pend;
+    bool cons_topo = false;
     std::vector<std::map<int, std::vector<int32_t>>> cons_dec;
     // hostname pod affinity: per candidate, the hostname-affinity groups whose domain on its node holds a selected pod
     // only through the candidate's reschedulable pods (a probe of the candidate has one positive domain less); h_tpos0 =
@@ -1508,9 +1512,8 @@ static kp_status expand_preferences(const kp_solve_input* in, int pref_policy, P
 // one group per TopologyGroup.Hash() — topology key, type, namespaces, label selector, maxSkew and the node filter
 // (MakeTopologyNodeFilter: the requirement key sets of the nodeSelector with each required term, the policies, the
 // tolerations); hashstructure skips unexported fields, so requirement values and minDomains are not part of it.  Here
-// the (class, term) groups whose identities AND semantics agree are one group owned by all those classes; groups of one
-// identity whose filter values / minDomains differ stay apart (Go would keep the first pod's, DESIGN.md §4 lists this).
-// A group is created by NewTopology when a pod that owns it is in the batch, or by Topology.Update when a pod relaxes
+// every (class, term) of one identity is one group owned by all those classes, with the first owner's node filter,
+// minDomains and selector (see the owner choice below).  A group is created by NewTopology when a pod that owns it is in the batch, or by Topology.Update when a pod relaxes
 // into a spec that owns it (countDomains then counts only the bound pods): an identity that only a relaxed stage can
 // own — its other owners do not include that stage's input class — is "late", born on the device when the first pod
 // relaxes into an owner (at most 64 such identities).  Interns the topology keys.
@@ -1522,8 +1525,14 @@ static kp_status topo_build(kp_ctx* c, const kp_solve_input* in, const std::vect
     th.cons.assign(C, {});
     th.rec.assign(C, {});
     th.neutral.assign(C, {});
-    std::map<std::string, int> gidx;    // identity + semantics → group
-    std::map<std::string, int> idents;  // identity → index
+    struct TEnt {  // one (class, term[, inverse]) owner of an identity
+        int cls = 0;
+        std::string sig;  // the semantics Hash() does not see: selection, minDomains, Honor filter values / tolerations
+        HGroup g;
+    };
+    std::vector<TEnt> ents;
+    std::vector<std::vector<int>> by_ident;  // identity → its entries, class order
+    std::map<std::string, int> idents;       // identity → index
     auto hreq_str = [](const HReq& q) {
         std::string r = std::to_string(q.key) + (q.complement ? "!" : "=");
         for (int v : q.vals) r += std::to_string(v) + ",";
@@ -1626,42 +1635,128 @@ static kp_status topo_build(kp_ctx* c, const kp_solve_input* in, const std::vect
                 }
                 auto iit = idents.find(id);
                 const int ident = iit != idents.end() ? iit->second : (int)idents.size();
-                if (iit == idents.end()) idents[id] = ident;
-                const std::string gk = id + "\x1b" + sig;
-                auto git = gidx.find(gk);
-                if (git != gidx.end()) {
-                    th.g[git->second].memb[i] = 1;
-                    continue;
+                if (iit == idents.end()) {
+                    idents[id] = ident;
+                    by_ident.emplace_back();
                 }
-                HGroup g;
-                g.type = x.type;
-                g.key = key;
-                g.inverse = inv == 1;
-                g.owner = i;
-                g.skew = spread ? x.max_skew : INT32_MAX;
-                g.mindom = spread && x.min_domains > 0 ? x.min_domains : 0;
-                g.pol = pol;
-                g.sel = sel;
-                g.memb.assign(C, 0);
-                g.memb[i] = 1;
-                g.ident = ident;
-                gidx[gk] = (int)th.g.size();
-                th.g.push_back(std::move(g));
+                TEnt e;
+                e.cls = i;
+                e.sig = std::move(sig);
+                e.g.type = x.type;
+                e.g.key = key;
+                e.g.inverse = inv == 1;
+                e.g.owner = i;
+                e.g.skew = spread ? x.max_skew : INT32_MAX;
+                e.g.mindom = spread && x.min_domains > 0 ? x.min_domains : 0;
+                e.g.pol = pol;
+                e.g.sel = sel;
+                e.g.ident = ident;
+                by_ident[ident].push_back((int)ents.size());
+                ents.push_back(std::move(e));
             }
         }
     }
-    if (th.g.empty()) return KP_OK;
-    if (getenv("KPSIM_DIAG_IDENT")) {  // diagnostics: identities held by groups of different semantics
-        std::vector<int> per(idents.size(), 0);
-        for (const HGroup& g : th.g) per[g.ident]++;
-        int amb = 0;
-        for (int n : per) amb += n > 1;
-        fprintf(stderr, "[kpsim] topology identities %zu, groups %zu, identities with several semantics %d\n",
-                idents.size(), th.g.size(), amb);
-    }
-    // late identities: a relaxed stage owns it and its input class does not
+    if (ents.empty()) return KP_OK;
     const int NI = (int)idents.size();
     const int C0 = X.n_input;
+    // One group per identity, as Topology.Update keeps topologyGroups[hash]: the group is the first owner's
+    // TopologyGroup (its node filter, minDomains and selector), every later owner only AddOwner()s.  NewTopology
+    // iterates its pods in input order, so the first owner is the class of the first input pod whose spec owns the
+    // identity; consolidation probes each run their own NewTopology over the pending pods, then their candidates' pods.
+    // When the owners' semantics agree any owner is that group.  Otherwise a first owner that a probe, or a relaxation at
+    // run time, would choose differently is refused.
+    {
+        const int P = in->pods.n_pods;
+        std::vector<int64_t> firstpos(std::max(C, 1), INT64_MAX);  // Solve: first input pod per stage-0 class
+        if (!c->cons_topo) {
+            for (int p = P - 1; p >= 0; p--) firstpos[in->pods.class_id[p]] = p;
+        } else {
+            for (int q = (int)c->cons_pend.size() - 1; q >= 0; q--) firstpos[in->pods.class_id[c->cons_pend[q]]] = q;
+        }
+        int amb = 0;
+        for (int I = 0; I < NI; I++) {
+            const std::vector<int>& es = by_ident[I];
+            bool one = true;
+            for (int e : es) one = one && ents[e].sig == ents[es[0]].sig;
+            int own = es[0];
+            auto first_by = [&](const std::vector<int64_t>& pos) {  // the stage-0 owner entry of the smallest position
+                int b = -1;
+                for (int e : es)
+                    if (ents[e].cls < C0 && pos[ents[e].cls] != INT64_MAX && (b < 0 || pos[ents[e].cls] < pos[ents[b].cls])) b = e;
+                return b;
+            };
+            if (!one) {
+                amb++;
+                std::vector<int> relaxed;  // owners that only a relaxation reaches (a stage past 0)
+                for (int e : es)
+                    if (ents[e].cls >= C0) relaxed.push_back(e);
+                auto relaxed_agree = [&](const std::string& s) {
+                    for (int e : relaxed)
+                        if (ents[e].sig != s) return false;
+                    return true;
+                };
+                const int b = first_by(firstpos);
+                if (b >= 0) {
+                    own = b;  // every Solve / probe creates it from this pod at NewTopology
+                } else if (!c->cons_topo) {
+                    // no input pod owns it: only a relaxation creates it, from whichever pod relaxes first
+                    if (!relaxed.empty()) {
+                        if (!relaxed_agree(ents[relaxed[0]].sig)) {
+                            err = "topology groups of one TopologyGroup.Hash() identity with different node filters or "
+                                  "minDomains that only relaxed pods create";
+                            return KP_E_UNSUPPORTED;
+                        }
+                        own = relaxed[0];
+                    }
+                } else {
+                    // consolidation: each probe's first owner is the first of its candidates' pods owning it
+                    std::vector<int64_t> cpos(std::max(C, 1), INT64_MAX);
+                    int prev = -1, got = -1;
+                    bool missing = false, same = true;
+                    auto close_cand = [&]() {
+                        if (prev < 0) return;
+                        const int f = first_by(cpos);
+                        if (f < 0) missing = true;
+                        else if (got < 0) got = f;
+                        else same = same && ents[f].sig == ents[got].sig;
+                        std::fill(cpos.begin(), cpos.end(), INT64_MAX);
+                    };
+                    int posq = 0;
+                    for (auto& ex : c->cons_extra) {
+                        if (ex[2] != prev) {
+                            close_cand();
+                            prev = ex[2];
+                            posq = 0;
+                        }
+                        const int cl = in->pods.class_id[ex[1]];
+                        if (cpos[cl] == INT64_MAX) cpos[cl] = posq;
+                        posq++;
+                    }
+                    close_cand();
+                    for (int ci = 0, seen = 0; ci < c->cons_extra_ncand && !missing; ci++) {  // candidates without pods
+                        bool has = false;
+                        for (; seen < (int)c->cons_extra.size() && c->cons_extra[seen][2] == ci; seen++) has = true;
+                        missing = missing || !has;
+                    }
+                    if (!same || (got >= 0 && missing && !relaxed_agree(ents[got].sig)) ||
+                        (got < 0 && !relaxed.empty() && !relaxed_agree(ents[relaxed[0]].sig))) {
+                        err = "topology groups of one TopologyGroup.Hash() identity with different node filters or "
+                              "minDomains whose first owner differs between consolidation probes";
+                        return KP_E_UNSUPPORTED;
+                    }
+                    own = got >= 0 ? got : (!relaxed.empty() ? relaxed[0] : es[0]);
+                }
+            }
+            HGroup g = ents[own].g;
+            g.memb.assign(C, 0);
+            for (int e : es) g.memb[ents[e].cls] = 1;
+            th.g.push_back(std::move(g));
+        }
+        if (getenv("KPSIM_DIAG_IDENT"))  // diagnostics: identities whose owners' semantics differ
+            fprintf(stderr, "[kpsim] topology identities %d, owner entries %zu, identities with several semantics %d\n", NI,
+                    ents.size(), amb);
+    }
+    // late identities: a relaxed stage owns it and its input class does not
     std::vector<std::vector<uint8_t>> own0(NI);  // identity → input classes owning it at stage 0
     for (auto& own : own0) own.assign(std::max(C0, 1), 0);
     for (const HGroup& g : th.g)
@@ -3150,7 +3245,11 @@ static kp_status cons_prepare_one(kp_ctx* ctx, const kp_consolidate_input* in) t
     for (int ci = 0; ci < NC; ci++)
         for (int q = 0; q < in->candidates[ci].n_pods; q++)
             ctx->cons_extra.push_back({in->candidates[ci].node, in->candidates[ci].pods[q], ci});
+    ctx->cons_pend.assign(in->pending, in->pending + in->n_pending);
+    ctx->cons_topo = true;
     kp_status st = kp_solve_prepare(ctx, &cl);
+    ctx->cons_topo = false;
+    ctx->cons_pend.clear();
     ctx->cons_extra.clear();
     ctx->cons_extra_ncand = 0;
     if (st != KP_OK) return st;

@@ -134,8 +134,9 @@ struct PodClass {
     std::vector<TopoTerm> terms;
 };
 
-// [core] scheduling/topologygroup.go TopologyGroup.  One group per (pod class, term): Go shares a group between pods
-// whose terms hash equal, but groups that share a hash count the same pods, so per-class groups decide identically.
+// [core] scheduling/topologygroup.go TopologyGroup.  One group per (pod class, term); Go keeps one TopologyGroup per
+// Hash() (Topology.Update: topologyGroups[hash], first insert wins), so every group of one identity takes the first
+// owner's selector, minDomains, node filter and tolerations (Solver::adopt) and they all count the same pods.
 // `cnt` is the domains map (domain value id → count; emptyDomains = the domains with count 0, since counts only grow
 // within a Solve).  Hostname groups know every registered host implicitly (NewNodeClaim and NewExistingNode
 // Register their hostnames in every hostname group), so only recorded hosts are stored.
@@ -145,6 +146,8 @@ struct TopoGroup {
     bool host = false;
     bool inverse = false;      // inverseTopologyGroups (updateInverseAntiAffinity): constrains the pods it selects
     int owner = -1;            // class that owns the term
+    int ident = -1;            // TopologyGroup.Hash() identity (build_topology)
+    int sem = -1;              // class whose TopologyGroup the identity keeps (its first owner): node filter, tolerations
     int max_skew = 0, min_domains = -1;
     int aff_pol = KP_POLICY_IGNORE, taint_pol = KP_POLICY_IGNORE;  // TopologyNodeFilter (spread only)
     std::vector<uint8_t> sel;  // per class: selects(pod) = namespace ∈ namespaces ∧ selector matches labels
@@ -231,6 +234,9 @@ struct Solver {
     std::vector<uint64_t> cls_birth;
     int n_late = 0;
     uint64_t born = ~0ull;
+    std::vector<std::vector<int>> ident_groups;  // identity → its (class, term) groups
+    std::vector<int> late_ident;                 // late bit → identity
+    std::vector<std::pair<int, int>> bound_pods; // (node, class) of the pods countDomains counts in this simulation
     std::vector<int> cls_origin;  // per class: its input class
     int n_input = 0;
     kp_solve_stats stats{};
@@ -457,7 +463,7 @@ struct Solver {
             const Req dom = r.get(g.key);
             if (!g.inverse) {
                 if (g.type == KP_TOPO_SPREAD) {  // TopologyNodeFilter.Matches
-                    const PodClass& fc = (*cp)[g.owner];
+                    const PodClass& fc = (*cp)[g.sem];
                     if (g.aff_pol == KP_POLICY_HONOR && !filter_matches(fc, r, allow_wk)) continue;
                     if (g.taint_pol == KP_POLICY_HONOR && !tolerates_all(taints, fc.tols)) continue;
                 }
@@ -633,6 +639,101 @@ struct Solver {
         return false;
     }
 
+    // Topology.Update keeps topologyGroups[hash]: the first owner's TopologyGroup, later owners only AddOwner().  Every
+    // (class, term) group of the identity takes the first owner's selector, minDomains, node filter and tolerations and
+    // its domains as buildDomainGroups left them for that owner (countDomains follows).
+    void adopt(int ident, int cls) {
+        int src = -1;
+        for (int gi : ident_groups[ident])
+            if (groups_dg[gi].owner == cls) {
+                src = gi;
+                break;
+            }
+        if (src < 0) return;
+        const TopoGroup& f = groups_dg[src];
+        for (int gi : ident_groups[ident]) {
+            TopoGroup& g = groups[gi];
+            g.sem = cls;
+            g.min_domains = f.min_domains;
+            g.sel = f.sel;
+            g.cnt = f.cnt;
+        }
+    }
+    // per class: the groups that constrain its pods (owned forward groups, inverse groups that select it) and those that
+    // count them (forward groups that select it, owned inverse groups)
+    void index_groups() {
+        const int C = (int)cp->size();
+        t_cons.assign(C, {});
+        t_rec.assign(C, {});
+        for (int gi = 0; gi < (int)groups.size(); gi++) {
+            const TopoGroup& g = groups[gi];
+            for (int c = 0; c < C; c++) {
+                if (g.inverse) {
+                    if (g.sel[c]) t_cons[c].push_back(gi);  // getMatchingTopologies: inverse groups that select the pod
+                    if (g.owner == c) t_rec[c].push_back(gi);
+                } else {
+                    if (g.owner == c) t_cons[c].push_back(gi);
+                    if (g.sel[c]) t_rec[c].push_back(gi);
+                }
+            }
+        }
+    }
+    // countDomains / updateInverseAffinities for one pod of class b bound to existing node j (every group, or only
+    // those of identity `only`)
+    void count_bound(int j, int b, int only) {
+        const ExistingNode& n = (*ex_base)[j];
+        for (TopoGroup& g : groups) {
+            if (only >= 0 && g.ident != only) continue;
+            if (g.inverse ? g.owner != b : !g.sel[b]) continue;
+            if (!g.inverse && g.type == KP_TOPO_SPREAD) {
+                const PodClass& fc = (*cp)[g.sem];
+                if (g.aff_pol == KP_POLICY_HONOR && !filter_matches(fc, n.reqs, false)) continue;
+                if (g.taint_pol == KP_POLICY_HONOR && !tolerates_all(n.taints, fc.tols)) continue;
+            }
+            int dom;
+            if (g.host) {
+                dom = n.host;
+            } else {
+                auto it = n.reqs.m.find(g.key);
+                if (it == n.reqs.m.end() || it->second.complement || it->second.values.size() != 1) continue;  // unlabeled
+                dom = it->second.values[0];
+            }
+            g.cnt[dom]++;
+        }
+    }
+    // NewTopology over this simulation's pods (plist, input order): each identity is created from the first pod whose
+    // spec owns it, then countDomains over bound_pods.  An identity no pod owns yet keeps its per-class groups until a
+    // relaxation creates it (birth).
+    void new_topology() {
+        groups = groups_dg;
+        if (groups.empty()) return;
+        std::vector<int> firstpos(cp->size(), INT32_MAX);
+        for (int li = (int)plist.size() - 1; li >= 0; li--) firstpos[pod_at(li).cls] = li;
+        for (int I = 0; I < (int)ident_groups.size(); I++) {
+            int best = -1;
+            for (int gi : ident_groups[I]) {
+                const int o = groups_dg[gi].owner;
+                if (o < n_input && firstpos[o] != INT32_MAX && (best < 0 || firstpos[o] < firstpos[best])) best = o;
+            }
+            if (best >= 0) adopt(I, best);
+        }
+        index_groups();
+        for (auto& bp : bound_pods) count_bound(bp.first, bp.second, -1);
+    }
+    // Topology.Update of a pod relaxed into class cls creates the late identities it owns that no pod created yet: from
+    // this pod's spec, countDomains over the bound pods only (the pods of this Solve are excluded)
+    void birth(int cls) {
+        const uint64_t fresh = cls_birth[cls] & ~born;
+        if (!fresh) return;
+        born |= fresh;
+        for (uint64_t x = fresh; x; x &= x - 1) {
+            const int I = late_ident[__builtin_ctzll(x)];
+            adopt(I, cls);
+            for (auto& bp : bound_pods) count_bound(bp.first, bp.second, I);
+        }
+        index_groups();
+    }
+
     void solve() {
         // NewTopology creates the groups the batch's pods own; Topology.Update those of a relaxed pod's new spec
         born = ~0ull;
@@ -676,7 +777,7 @@ struct Solver {
             q.push_back(li);
             if (nx >= 0) {
                 pcls[li] = nx;
-                if (n_late > 0) born |= cls_birth[nx];
+                if (n_late > 0) birth(nx);
                 lastLen.clear();
             } else {
                 lastLen[li] = (int)q.size();
@@ -758,7 +859,6 @@ struct orc_result {
 // Input views → NewScheduler state (catalog rows, classes, pods, NodeClaimTemplates in weight order, existing nodes),
 // then NewTopology (domain groups, topology groups, counts of the bound pods).
 static kp_status build_topology(Solver& s, const kp_solve_input* in, const std::vector<PoolDomains>& pools);
-static void count_bound_pod(Solver& s, int j, int b);
 
 static kp_status parse_into(Solver& s, const kp_catalog_view* cat, const kp_solve_input* in, int pref_policy) {
     Dict& D = s.D;
@@ -1131,6 +1231,7 @@ static kp_status build_topology(Solver& s, const kp_solve_input* in, const std::
                 g.host = t.key == s.hostname_key;
                 g.inverse = inv == 1;
                 g.owner = c;
+                g.sem = c;
                 g.max_skew = t.max_skew;
                 g.min_domains = t.min_domains;
                 g.aff_pol = t.aff_pol;
@@ -1222,57 +1323,29 @@ static kp_status build_topology(Solver& s, const kp_solve_input* in, const std::
             late[gid[g]] = s.n_late++;
         }
         s.cls_birth.assign(C, 0);
+        s.late_ident.assign(s.n_late, -1);
+        s.ident_groups.assign(NI, {});
         for (size_t g = 0; g < s.groups.size(); g++) {
             s.groups[g].late = late[gid[g]];
-            if (late[gid[g]] >= 0) s.cls_birth[s.groups[g].owner] |= 1ull << late[gid[g]];
-        }
-    }
-    s.t_cons.assign(C, {});
-    s.t_rec.assign(C, {});
-    for (int gi = 0; gi < (int)s.groups.size(); gi++) {
-        const TopoGroup& g = s.groups[gi];
-        for (int c = 0; c < C; c++) {
-            if (g.inverse) {
-                if (g.sel[c]) s.t_cons[c].push_back(gi);  // getMatchingTopologies: inverse groups that select the pod
-                if (g.owner == c) s.t_rec[c].push_back(gi);
-            } else {
-                if (g.owner == c) s.t_cons[c].push_back(gi);
-                if (g.sel[c]) s.t_rec[c].push_back(gi);
+            s.groups[g].ident = gid[g];
+            s.ident_groups[gid[g]].push_back((int)g);
+            if (late[gid[g]] >= 0) {
+                s.cls_birth[s.groups[g].owner] |= 1ull << late[gid[g]];
+                s.late_ident[late[gid[g]]] = gid[g];
             }
         }
     }
-    s.groups_dg = s.groups;  // the domain groups before any pod is counted (consolidation probes recount)
+    s.groups_dg = s.groups;  // the domain groups before any pod is counted (Solver::new_topology counts)
+    s.index_groups();
     // bound pods: countDomains (forward groups; node filter against the node's labels and taints) and the inverse
-    // anti-affinity of bound pods (recorded at their node's domain)
+    // anti-affinity of bound pods (recorded at their node's domain), in Solver::new_topology once the pods are known
     const int E = (int)s.own_existing.size();
     for (int i = 0; i < in->n_bound; i++) {
         const int j = in->bound_node[i], b = in->bound_class[i];
         if (j < 0 || j >= E || b < 0 || b >= C) return KP_E_INVALID;
-        count_bound_pod(s, j, b);
+        s.bound_pods.push_back({j, b});
     }
     return KP_OK;
-}
-
-// countDomains / updateInverseAffinities for one pod of class b bound to existing node j.
-static void count_bound_pod(Solver& s, int j, int b) {
-    const ExistingNode& n = (*s.ex_base)[j];
-    for (TopoGroup& g : s.groups) {
-        if (g.inverse ? g.owner != b : !g.sel[b]) continue;
-        if (!g.inverse && g.type == KP_TOPO_SPREAD) {
-            const PodClass& fc = (*s.cp)[g.owner];
-            if (g.aff_pol == KP_POLICY_HONOR && !s.filter_matches(fc, n.reqs, false)) continue;
-            if (g.taint_pol == KP_POLICY_HONOR && !tolerates_all(n.taints, fc.tols)) continue;
-        }
-        int dom;
-        if (g.host) {
-            dom = n.host;
-        } else {
-            auto it = n.reqs.m.find(g.key);
-            if (it == n.reqs.m.end() || it->second.complement || it->second.values.size() != 1) continue;  // unlabeled
-            dom = it->second.values[0];
-        }
-        g.cnt[dom]++;
-    }
 }
 
 extern "C" kp_status orc_solve_opts(const kp_catalog_view* cat, const kp_solve_input* in, const kp_device_opts* opts,
@@ -1293,6 +1366,7 @@ extern "C" kp_status orc_solve_opts(const kp_catalog_view* cat, const kp_solve_i
     const kp_pods_view& pv = in->pods;
     s.plist.resize(pv.n_pods);
     for (int p = 0; p < pv.n_pods; p++) s.plist[p] = p;
+    s.new_topology();
 
     const auto t1 = clk::now();
     s.solve();
@@ -1446,27 +1520,29 @@ static void run_probe(const ConsCtx& X, int probe, kp_probe_result& pr, Replacem
     }
     for (int j = 0; j < (int)b.own_existing.size(); j++)
         if (!excluded[j]) s.ex_idx.push_back(j);
-    // NewTopology of the simulation: the domain groups, then countDomains over the pods bound in the cluster except
-    // the ones this simulation schedules (excludedPods = its candidates' reschedulable pods): the pods of
-    // cluster.bound and every other candidate's reschedulable pods on that candidate's node
-    if (!b.groups.empty()) {
-        s.groups = b.groups_dg;
-        s.t_cons = b.t_cons;
-        s.t_rec = b.t_rec;
-        s.cls_birth = b.cls_birth;
-        s.n_late = b.n_late;
-        for (int i = 0; i < in->cluster.n_bound; i++) count_bound_pod(s, in->cluster.bound_node[i], in->cluster.bound_class[i]);
-        for (int c = 0; c < in->n_candidates; c++) {
-            if (c >= c0 && c < c1) continue;
-            const kp_candidate& cd = in->candidates[c];
-            for (int i = 0; i < cd.n_pods; i++) count_bound_pod(s, cd.node, b.own_pods[cd.pods[i]].cls);
-        }
-    }
     // pods = pending + candidates' reschedulable pods
     for (int i = 0; i < in->n_pending; i++) s.plist.push_back(in->pending[i]);
     const int n_pending = (int)s.plist.size();
     for (int c = c0; c < c1; c++)
         for (int i = 0; i < in->candidates[c].n_pods; i++) s.plist.push_back(in->candidates[c].pods[i]);
+    // NewTopology of the simulation: the domain groups, then countDomains over the pods bound in the cluster except
+    // the ones this simulation schedules (excludedPods = its candidates' reschedulable pods): the pods of
+    // cluster.bound and every other candidate's reschedulable pods on that candidate's node
+    if (!b.groups.empty()) {
+        s.groups_dg = b.groups_dg;
+        s.ident_groups = b.ident_groups;
+        s.late_ident = b.late_ident;
+        s.cls_birth = b.cls_birth;
+        s.n_late = b.n_late;
+        s.n_input = b.n_input;
+        for (int i = 0; i < in->cluster.n_bound; i++) s.bound_pods.push_back({in->cluster.bound_node[i], in->cluster.bound_class[i]});
+        for (int c = 0; c < in->n_candidates; c++) {
+            if (c >= c0 && c < c1) continue;
+            const kp_candidate& cd = in->candidates[c];
+            for (int i = 0; i < cd.n_pods; i++) s.bound_pods.push_back({cd.node, b.own_pods[cd.pods[i]].cls});
+        }
+        s.new_topology();  // each identity from the first of this simulation's pods that owns it
+    }
     pr.n_pods = (int)s.plist.size();
     pr.candidate_price = cprice;
 

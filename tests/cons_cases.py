@@ -114,3 +114,30 @@ def check_expect(cmd, cp, expect):
 
 
 SCENARIOS = {"reserved_into": reserved_into, "reserved_between": reserved_between}
+
+
+def shared_identity_cluster(golden, pending_a):
+    """Two m5.2xlarge nodes (1a, 1b), each a candidate holding one pod of test_topology_cpu.shared_filter_problem's
+    Deployments (one spread identity, Honor filters zone In [1a, 1b] vs [1b, 1c]); a third node (1c) with room.  Each
+    single-node probe's NewTopology sees only its own candidate's pod (and the pending pods), so without a pending pod
+    the two probes create the group from different owners: kp_consolidate refuses that.  pending_a adds a pending pod
+    of A's Deployment, which every probe sees first."""
+    import test_topology_cpu as TC
+    prob = TC.shared_filter_problem(golden, True)
+    it = golden[row(golden, "m5.2xlarge")]
+    specs = [(0, {"cpu": "1", "memory": "1Gi"}), (1, {"cpu": "1", "memory": "1Gi"})]
+    if pending_a:
+        specs.append((0, {"cpu": "1", "memory": "1Gi"}))
+    pods = synth.pods_from_specs(specs)
+    nodes, cands = [], []
+    for j, zone in enumerate(["test-zone-1a", "test-zone-1b", "test-zone-1c"]):
+        labels = synth.node_labels(it, zone, "on-demand", "default")
+        avail = np.array(it.allocatable, np.int64) - (pods.requests[j] if j < 2 else 0)
+        nodes.append(model.ExistingNode("node-%d" % j, labels, avail, np.zeros(model.R, np.int64)))
+        if j < 2:
+            cands.append(model.Candidate(node=j, pods=np.array([j], np.int32), price=synth.candidate_price(it, labels),
+                                         capacity_type=abi.KP_CT_ON_DEMAND, instance_type=row(golden, "m5.2xlarge"),
+                                         nodepool=0, capacity=np.array(it.capacity, np.int64)))
+    cluster = model.Problem(golden, prob.nodepools, prob.classes, pods, nodes)
+    pending = np.array([2] if pending_a else [], np.int32)
+    return model.ConsolidationProblem(cluster, cands, pending, np.ones(3, np.uint8))

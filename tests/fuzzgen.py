@@ -433,6 +433,92 @@ def add_many_groups(rng, prob, n_terms=24):
     return prob
 
 
+def _revalue(rng, r, zones):
+    """the same requirement key and operator with other values (the node filter's hash sees only the key)"""
+    if r.key == ZONE and r.op in ("In", "NotIn"):
+        return Requirement(ZONE, r.op, sorted(set(rng.choice(zones, size=int(rng.integers(1, 3))).tolist())))
+    if r.key == CAPACITY_TYPE and r.op in ("In", "NotIn"):
+        return Requirement(CAPACITY_TYPE, r.op, [str(rng.choice(["spot", "on-demand"]))])
+    if r.op in ("Gt", "Lt") and r.values and r.values[0].lstrip("-").isdigit():
+        return Requirement(r.key, r.op, [str(max(0, int(r.values[0]) + int(rng.integers(-3, 4))))])
+    return Requirement(r.key, r.op, list(r.values), r.min_values)
+
+
+def add_shared_identities(rng, prob, n_families=None, p_move=0.5):
+    """Deployments whose topology terms share one TopologyGroup.Hash() identity while what Hash() does not see differs
+    ([core] topology.go Update keeps topologyGroups[hash], the first owner's group): a family's base class (one with a
+    spread; one is made if none has) gets 1-2 sibling classes — same labels, namespace, tolerations, terms and
+    requirement keys — whose requirement values (zone / capacity-type subsets, Gt / Lt bounds: the Honor node filter's
+    values) and spread minDomains differ.  A share of the base's pods move to the siblings, so whichever of them comes
+    first in input order decides the group's node filter and minDomains (website scheduling.md:347-372, faq.md:180-182)."""
+    import copy
+    zones = sorted({o.zone for it in prob.catalog for o in it.offerings})
+    bases = [c for c, pc in enumerate(prob.classes) if any(t.kind == "spread" for t in pc.topology)]
+    if not bases:
+        pc = prob.classes[0]
+        pc.topology = list(pc.topology) + [model.TopologyTerm(
+            "spread", ZONE, [Requirement("app", "In", [pc.labels.get("app", "x")])], max_skew=1)]
+        bases = [0]
+    rng.shuffle(bases)
+    cls = prob.pods.class_id.copy()
+    prob.shared_families = []
+    for b in bases[:int(n_families or rng.integers(1, 4))]:
+        fam = [b]
+        base = prob.classes[b]
+        if not any(r.key == ZONE for r in base.requirements) and rng.random() < 0.8:
+            base.requirements = list(base.requirements) + [
+                Requirement(ZONE, "In", sorted(set(rng.choice(zones, size=2).tolist())))]
+        for t in base.topology:
+            if t.kind == "spread" and rng.random() < 0.5:
+                t.node_affinity_policy = "Honor"
+        for _ in range(int(rng.integers(1, 3))):
+            sib = copy.deepcopy(base)
+            sib.requirements = [_revalue(rng, r, zones) for r in base.requirements]
+            for t in sib.topology:
+                if t.kind == "spread" and rng.random() < 0.5:
+                    t.min_domains = int(rng.integers(1, 6)) if rng.random() < 0.7 else None
+            prob.classes.append(sib)
+            fam.append(len(prob.classes) - 1)
+            idx = np.nonzero(cls == b)[0]
+            cls[idx[rng.random(len(idx)) < p_move]] = len(prob.classes) - 1
+        prob.bound = [(j, (len(prob.classes) - 1 if c == b and rng.random() < p_move else c)) for j, c in prob.bound]
+        prob.shared_families.append(fam)
+    prob.pods.class_id = cls.astype(prob.pods.class_id.dtype)
+    return prob
+
+
+def fuzz_shared_identity_problem(catalog, seed, n_pods=200, n_existing=0):
+    """fuzz_topology_problem (or its cluster variant with existing nodes and bound pods) plus add_shared_identities."""
+    if n_existing:
+        prob = fuzz_topology_existing_problem(catalog, seed, n_pods=n_pods, n_existing=n_existing)
+    else:
+        prob = fuzz_topology_problem(catalog, seed, n_pods=n_pods)
+    return add_shared_identities(np.random.Generator(np.random.PCG64(seed + 4242)), prob)
+
+
+def fuzz_shared_identity_consolidation(catalog, seed, n_nodes=30, n_pods=160):
+    """fuzz_topology_consolidation plus add_shared_identities.  Every probe's NewTopology runs over the pending pods
+    first, so a family with a pending pod has one first owner in every probe: one pod of each family that has none
+    moves from its candidate to the front of the pending pods (a family whose first owner differed between probes is
+    refused by the device, test_gpu_consolidation.py covers that separately)."""
+    cp = fuzz_topology_consolidation(catalog, seed, n_nodes=n_nodes, n_pods=n_pods)
+    rng = np.random.Generator(np.random.PCG64(seed + 4343))
+    prob = add_shared_identities(rng, cp.cluster)
+    cls = prob.pods.class_id
+    pending = [int(p) for p in cp.pending]
+    for fam in prob.shared_families:
+        if any(int(cls[p]) in fam for p in pending):
+            continue
+        for cd in cp.candidates:
+            hit = [int(p) for p in cd.pods if int(cls[p]) in fam]
+            if hit:
+                cd.pods = np.array([p for p in cd.pods if int(p) != hit[0]], np.int32)
+                pending.insert(0, hit[0])
+                break
+    cp.pending = np.array(pending, np.int32)
+    return cp
+
+
 def fuzz_preference_consolidation(catalog, seed, n_nodes=30, n_pods=160, n_bound=30, all_spot=False, best_effort=False,
                                   zone_min=False):
     """fuzz_consolidation over pods with preferences to relax (add_preferences), pods of those classes bound to random

@@ -713,3 +713,43 @@ def test_consolidation_wide_catalog(ctx, golden):
         cp = fuzzgen.fuzz_consolidation(cat, 5700 + seed, n_nodes=40, n_pods=200, all_spot=seed == 1)
         for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
             assert_probes_equal(device_probes(ctx, cp, mode), pyoracle.consolidate(cp, mode))
+
+
+# ---- topology groups shared by TopologyGroup.Hash() identity in the probes (row N1): each probe's NewTopology creates
+# the group from the first of its pods (pending, then its candidates' pods) that owns it ----
+
+def test_shared_identity_probes(ctx, golden):
+    """A pending pod of A's Deployment comes first in every probe: the group is A's (filter zone In [1a, 1b]) in all of
+    them; probes and command against the oracle."""
+    import cons_cases
+    cp = cons_cases.shared_identity_cluster(golden, pending_a=True)
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        assert_probes_equal(device_probes(ctx, cp, mode), pyoracle.consolidate(cp, mode))
+    assert_commands_equal(device_command(ctx, cp, abi.KP_CONSOLIDATE_BOTH),
+                          pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH))
+
+
+def test_shared_identity_probes_refused(ctx, golden):
+    """No pending pod: probe 0 creates the group from A's pod, probe 1 from B's — two node filters for one identity in
+    one pass, which the device's one group per identity cannot hold: refused (KP_E_UNSUPPORTED), never approximated."""
+    import cons_cases
+    from kpsim import native
+    cp = cons_cases.shared_identity_cluster(golden, pending_a=False)
+    with pytest.raises(native.KpError) as e:
+        device_probes(ctx, cp, abi.KP_CONSOLIDATE_SINGLE)
+    assert e.value.status == abi.KP_E_UNSUPPORTED and "differs between consolidation probes" in str(e.value)
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_fuzz_consolidation_shared_identity(ctx, golden, seed):
+    """fuzzgen.fuzz_shared_identity_consolidation: sibling Deployments with equal spread identities and different Honor
+    filter values / minDomains over topology-constrained clusters, a pod of each family pending; both modes and the
+    command against the oracle."""
+    rng = np.random.Generator(np.random.PCG64(4500 + seed))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 300)), replace=False))]
+    cp = fuzzgen.fuzz_shared_identity_consolidation(sub, 4500 + seed, n_nodes=int(rng.integers(4, 50)),
+                                                    n_pods=int(rng.integers(20, 200)))
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        assert_probes_equal(device_probes(ctx, cp, mode), pyoracle.consolidate(cp, mode))
+    assert_commands_equal(device_command(ctx, cp, abi.KP_CONSOLIDATE_BOTH),
+                          pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH))

@@ -336,3 +336,42 @@ def test_fuzz_many_groups(ctx, golden, seed):
                                                   n_existing=int(rng.integers(4, 40)))
     fuzzgen.add_many_groups(rng, prob, n_terms=int(rng.integers(10, 18)))  # 8-13 constraining, up to 27 counting
     same(ctx, prob)
+
+
+# ---- one group per TopologyGroup.Hash() identity, with the first owner's node filter / minDomains (row N1) ----
+
+@pytest.mark.parametrize("a_first", [True, False])
+def test_shared_identity_first_owner_filter(ctx, golden, a_first):
+    """Equal identities, Honor node filters zone In [1a, 1b] vs [1b, 1c]: the first pod in input order decides the
+    group's filter (hand-derived placements in test_topology_cpu.SHARED_FILTER_WANT)."""
+    r, q = same(ctx, TC.shared_filter_problem(golden, a_first))
+    want, zones = TC.SHARED_FILTER_WANT[a_first]
+    assert list(r.pod_result) == want
+    assert [TC.zone_of(x) for x in q] == [(z,) for z in zones]
+
+
+@pytest.mark.parametrize("a_first", [True, False])
+def test_shared_identity_first_owner_min_domains(ctx, golden, a_first):
+    """Equal identities, minDomains 4 vs none: the first pod in input order decides the group's minDomains."""
+    r, _ = same(ctx, TC.shared_min_domains_problem(golden, a_first))
+    assert list(r.pod_result) == TC.SHARED_MIN_DOMAINS_WANT[a_first]
+
+
+def test_shared_identity_relaxed_only_refused(ctx, golden):
+    """An identity with two filters that only relaxed pods create: the group's filter is decided by whichever pod
+    relaxes first at run time, which the device does not emulate — kp_solve refuses (never approximated)."""
+    from kpsim import native
+    with pytest.raises(native.KpError) as e:
+        parity.run_device(ctx, TC.relaxed_only_shared_problem(golden))
+    assert e.value.status == abi.KP_E_UNSUPPORTED and "only relaxed pods create" in str(e.value)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_fuzz_shared_identity(ctx, golden, seed):
+    """fuzzgen.add_shared_identities over the topology fuzz families (odd seeds: with existing nodes and bound pods):
+    sibling classes whose terms hash equal while their Honor filter values and minDomains differ, pods of a family
+    interleaved in input order."""
+    rng = np.random.Generator(np.random.PCG64(seed + 500))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=160, replace=False))]
+    same(ctx, fuzzgen.fuzz_shared_identity_problem(sub, seed, n_pods=int(rng.integers(80, 300)),
+                                                   n_existing=(seed % 2) * 20))

@@ -205,3 +205,86 @@ def node_dense(cat, n_pods):
     lab = {"app": "node-dense"}
     pc, pods = deployment(n_pods, lab, [model.TopologyTerm("anti", model.HOSTNAME, sel(lab))])
     return model.Problem(cat, [e2e_nodepool(None)], [pc], pods)
+
+
+# ---- one group per TopologyGroup.Hash() identity: the first owner's node filter and minDomains ([core] topology.go
+# Update keeps topologyGroups[hash]; hashstructure skips Requirement values and minDomains, topologygroup.go Hash) ----
+
+def _web_spread(min_domains=None):
+    lab = {"app": "web"}
+    return lab, TopologyTerm("spread", ZONE, sel(lab), max_skew=1, min_domains=min_domains, node_affinity_policy="Honor")
+
+
+def shared_filter_problem(golden, a_first):
+    """Two Deployments share an app label and a zonal spread (website scheduling.md:347-372), one pinned to zones 1a/1b,
+    the other to 1b/1c, under nodeAffinityPolicy Honor: one identity, two node filters.  A's pods (2 cpu) are
+    scheduled before B's (1 cpu) either way; a_first puts A's pods first in the input (NewTopology's order)."""
+    lab, term = _web_spread()
+    a = PodClass([Requirement(ZONE, "In", ["test-zone-1a", "test-zone-1b"])], labels=lab, topology=[term])
+    b = PodClass([Requirement(ZONE, "In", ["test-zone-1b", "test-zone-1c"])], labels=lab, topology=[term])
+    pa, pb = [(0, {"cpu": "2", "memory": "1Gi"})] * 3, [(1, {"cpu": "1", "memory": "1Gi"})] * 3
+    pods = synth.pods_from_specs(pa + pb if a_first else pb + pa)
+    return model.Problem(golden, [synth.default_nodepool()], [a, b], pods)
+
+
+def shared_min_domains_problem(golden, a_first):
+    """Two Deployments with one zonal spread identity, A's with minDomains 4 (more than the 3 zones: the global
+    minimum counts as 0, faq.md:180-182), B's without; A's pods (2 cpu) schedule first."""
+    lab, _ = _web_spread()
+    a = PodClass(labels=lab, topology=[_web_spread(4)[1]])
+    b = PodClass(labels=lab, topology=[_web_spread()[1]])
+    pa, pb = [(0, {"cpu": "2", "memory": "1Gi"})] * 2, [(1, {"cpu": "1", "memory": "1Gi"})] * 3
+    pods = synth.pods_from_specs(pa + pb if a_first else pb + pa)
+    return model.Problem(golden, [synth.default_nodepool()], [a, b], pods)
+
+
+# hand-derived placements (pod_result in input order, NodeClaim zones in creation order):
+# filter A {1a,1b}: A → 1a, 1b (1a is 1 ahead), 1a; B pods land in 1c and are never counted (A's filter excludes 1c),
+#   so 1b stays one ahead of 1c and all three B pods share the 1c NodeClaim.
+# filter B {1b,1c}: A's pods in 1a are never counted, so all three share the 1a NodeClaim; B → 1b, 1c, then 1b again.
+SHARED_FILTER_WANT = {
+    True: ([0, 1, 0, 2, 2, 2], ["test-zone-1a", "test-zone-1b", "test-zone-1c"]),
+    False: ([1, 2, 1, 0, 0, 0], ["test-zone-1a", "test-zone-1b", "test-zone-1c"]),
+}
+# minDomains 4 (A first): every zone may hold one selected pod (min is 0 with 3 < 4 domains) → A 1a, A 1b, B 1c, then
+#   two B pods unschedulable.  No minDomains (B first): A 1a, A 1b, B 1c, then B joins the first NodeClaims in slice order.
+SHARED_MIN_DOMAINS_WANT = {
+    True: [0, 1, 2, -1, -1],
+    False: [2, 0, 1, 0, 1],
+}
+
+
+@pytest.mark.parametrize("a_first", [True, False])
+def test_shared_identity_first_owner_filter(golden, a_first):
+    r, q = solve(shared_filter_problem(golden, a_first))
+    want, zones = SHARED_FILTER_WANT[a_first]
+    assert list(r.pod_result) == want
+    assert [zone_of(x) for x in q] == [(z,) for z in zones]
+
+
+@pytest.mark.parametrize("a_first", [True, False])
+def test_shared_identity_first_owner_min_domains(golden, a_first):
+    r, _ = solve(shared_min_domains_problem(golden, a_first))
+    assert list(r.pod_result) == SHARED_MIN_DOMAINS_WANT[a_first]
+
+
+def relaxed_only_shared_problem(golden):
+    """Two Deployments with ORed required node-affinity terms whose first term no type satisfies: after Relax drops it,
+    each spread's node filter is its second term, zone In [1a] vs zone In [1b] — one identity that only relaxed pods
+    create, with two filters.  Topology.Update creates it from whichever pod relaxes first; the device refuses it
+    (KP_E_UNSUPPORTED), the oracle follows the first relaxation (A's pods, 2 cpu, pop first)."""
+    lab, term = _web_spread()
+    nothing = [Requirement(AWS + "instance-category", "In", ["zz"])]
+    a = PodClass(labels=lab, topology=[term], required_terms=[nothing, [Requirement(ZONE, "In", ["test-zone-1a"])]])
+    b = PodClass(labels=lab, topology=[term], required_terms=[nothing, [Requirement(ZONE, "In", ["test-zone-1b"])]])
+    pods = synth.pods_from_specs([(0, {"cpu": "2", "memory": "1Gi"})] * 2 + [(1, {"cpu": "1", "memory": "1Gi"})] * 2)
+    return model.Problem(golden, [synth.default_nodepool()], [a, b], pods)
+
+
+def test_relaxed_only_shared_identity_oracle(golden):
+    """The oracle creates the relaxed identity from the first pod that relaxes into it (A: filter zone In [1a]); B's pods
+    in 1b are never counted, so both share one 1b NodeClaim; A's two pods go to 1a together (A's filter counts them,
+    but the only admitted domain is 1a and its own count is the minimum)."""
+    r, q = solve(relaxed_only_shared_problem(golden))
+    assert list(r.pod_result) == [0, 0, 1, 1]
+    assert [zone_of(x) for x in q] == [("test-zone-1a",), ("test-zone-1b",)]
