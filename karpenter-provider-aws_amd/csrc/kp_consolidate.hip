@@ -350,7 +350,10 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
             const int r0 = single ? k.dec_soff[gp] : k.dec_moff[gp], r1 = single ? k.dec_soff[gp + 1] : k.dec_moff[gp + 1];
             for (int r = r0; r < r1; r++) pt_init_row(d, P, k.dec_g[r], k.dec_v + (size_t)r * 64, lane);
             for (int ga = lane; ga < k.n_ha; ga += 64) P.hpos[ga] = k.hpos0[(size_t)(single ? gp : k.n_cand + gp) * k.n_ha + ga];
-            if (lane == 0) S.born = k.born_s ? (single ? k.born_s[gp] : k.born_m[gp]) : ~0ull;
+            if (lane == 0) {
+                S.born = k.born_s ? (single ? k.born_s[gp] : k.born_m[gp]) : ~0ull;
+                if (d.late_sib) S.CC.cls = -1;  // the class caches route variant groups by this probe's births
+            }
         }
         // the probe's candidates are [c0, c1) and their pods one contiguous run of cand_pods (CSR in candidate order)
         const int po0 = k.cand_off[c0], po1 = k.cand_off[c1];
@@ -977,7 +980,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
             uint32_t cflags = 0;
             if (TOPO) {
                 cflags = __builtin_amdgcn_readfirstlane(d.cls_flags[c]);
-                if ((cflags & CF_TOPO) && S.CC.cls != c) fill_class_cache(d, c, S.CC, lane, 64);
+                if ((cflags & CF_TOPO) && S.CC.cls != c) fill_class_cache(d, c, S.CC, lane, 64, TOPO ? S.born : 0ull);
             }
             const bool tcons = TOPO && (cflags & CF_TOPO_CONS);
             const int xs = tcons ? 0 : xstart;
@@ -1028,7 +1031,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
             const long long cn0 = prof ? __builtin_amdgcn_s_memtime() : 0;
             const int64_t* preq = d.pod_req + (size_t)p * R;
             if (n_nc == 1) {  // NodeClaim.Add on the in-flight NodeClaim
-                if (S.CC.cls != c) fill_class_cache(d, c, S.CC, lane, 64);
+                if (S.CC.cls != c) fill_class_cache(d, c, S.CC, lane, 64, TOPO ? S.born : 0ull);
                 EvalIn a;
                 a.Ahdr = nch;
                 a.Aw = ncw;
@@ -1082,7 +1085,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
                     uint64_t o = (lane < TW && d.tmpl_ok[j]) ? d.tmpl_opts[(size_t)j * TW + lane] : 0;
                     o = limit_filter_rem(d, j, o, rem, lane);
                     if (!ballot(o != 0)) continue;
-                    if (S.CC.cls != c) fill_class_cache(d, c, S.CC, lane, 64);
+                    if (S.CC.cls != c) fill_class_cache(d, c, S.CC, lane, 64, TOPO ? S.born : 0ull);
                     EvalIn a;
                     a.Ahdr = d.cls_hdr + (size_t)(d.C + j) * K;
                     a.Aw = d.cls_words + (size_t)(d.C + j) * d.DW;
@@ -1164,7 +1167,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
                 relax_at = tail;
                 st_relax++;
                 // Topology.Update: the relaxed spec's new groups are created (one wave: its LDS ops stay in order)
-                if (TOPO && d.tg_late && lane == 0) S.born |= d.cls_birth[nx];
+                if (TOPO && d.tg_late && lane == 0) S.born = topo_birth(d, S.born, d.cls_birth[nx]);
             }
             if (lane == 0) {
                 ring[tail % cap] = nent;

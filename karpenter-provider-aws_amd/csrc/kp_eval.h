@@ -152,7 +152,27 @@ struct EvalEnv {
 };
 
 // Cooperative fill by all threads of the block; contains two __syncthreads().
-__device__ inline void fill_class_cache(const KpDev& d, int c, ClassCache& CC, int tid, int nthr) {
+// Topology.Update of a pod relaxed into a class that owns the late bits `add`: each group is created unless a variant
+// sibling of its identity already was (the identity's group then exists, with that sibling's semantics).
+__device__ __forceinline__ uint64_t topo_birth(const KpDev& d, uint64_t born, uint64_t add) {
+    if (!d.late_sib) return born | add;
+    for (uint64_t x = add & ~born; x; x &= x - 1) {
+        const int b = __ffsll((unsigned long long)x) - 1;
+        if (!(born & d.late_sib[b])) born |= 1ull << b;
+    }
+    return born;
+}
+// A class's constraint on group g: for a variant group, the identity's born variant (g itself until one is born).
+__device__ __forceinline__ int topo_variant(const KpDev& d, int g, uint64_t born) {
+    if (!d.late_sib) return g;
+    const int lt = d.tg_late[g];
+    if (lt < 0) return g;
+    const uint64_t m = born & d.late_sib[lt];
+    return m ? d.late_grp[__ffsll((unsigned long long)m) - 1] : g;
+}
+
+// born: the late topology groups created so far (routes a constraint on a variant group to the born variant)
+__device__ inline void fill_class_cache(const KpDev& d, int c, ClassCache& CC, int tid, int nthr, uint64_t born = 0) {
     const int k0 = d.cls_koff[c], nck = d.cls_koff[c + 1] - k0;
     for (int i = tid; i < nck; i += nthr) {
         const int k = d.cls_keys[k0 + i];
@@ -206,7 +226,7 @@ __device__ inline void fill_class_cache(const KpDev& d, int c, ClassCache& CC, i
             for (int i = 0; i < nck; i++)
                 if (CC.key[i] == info.y) ki = i;
         if (cons) {
-            CC.tc[tid] = e;
+            CC.tc[tid] = (e & ~0x3FFFFFFF) | topo_variant(d, e & 0x3FFFFFFF, born);
             CC.tc_ki[tid] = ki;
         } else if (tid - CC.ntc < KP_CC_REC) {
             CC.tr[tid - CC.ntc] = e;

@@ -109,7 +109,11 @@ __device__ inline void topo_prefilter_setup(const KpDev& d, FfdShared& S, int c,
     const int nt = nall < KP_SNAP_ROWS ? nall : KP_SNAP_ROWS;
     for (int e = wave; e < nt; e += KP_NWAVES) {
         // the entry's static operands (KpTopoCons), then the group's counts: one round of independent loads
-        const KpTopoCons T = d.cls_tce[t0 + e];
+        KpTopoCons T = d.cls_tce[t0 + e];
+        if (d.late_sib) {  // a variant group: the identity's born variant (its minDomains)
+            T.g = topo_variant(d, T.g, S.born);
+            T.mindom = d.tg_info[T.g].w;
+        }
         const int g = T.g, type = T.flags & TG_TYPE, self = (T.flags >> 2) & 1;
         int k = T.key, lo = 0, hi = INT32_MAX, cmp = 0;
         uint64_t elig = 0;
@@ -1318,7 +1322,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
             // ExistingNode.Add in scheduling order: tolerations + Compatible (XT) and headroom, then the requirement
             // merge and Topology.AddRequirements on the node's own domains; the first node that accepts takes the pod
             // and Topology.Record counts it there.  Counts change with every placement, so nothing is memoised.
-            if (S.cls_fill) fill_class_cache(d, S.cur_cls, S.CC, tid, nthr);
+            if (S.cls_fill) fill_class_cache(d, S.cur_cls, S.CC, tid, nthr, S.born);
             __syncthreads();
             if (wave == 0) {
                 const int placed = existing_topo_scan(d.self, S, pod, lane);
@@ -1437,7 +1441,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
         long long c_ev0 = 0;
         {
             const long long cf0 = (d.profile && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
-            if (S.cls_fill) fill_class_cache(d, S.cur_cls, S.CC, tid, nthr);
+            if (S.cls_fill) fill_class_cache(d, S.cur_cls, S.CC, tid, nthr, S.born);
             if (d.profile && tid == 0) {
                 c_ev0 = __builtin_amdgcn_s_memtime();
                 S.st[ST_SLOW_WHY + 10] += c_ev0 - cf0;
@@ -1799,7 +1803,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                         d.pod_shape[pod] = d.shape_next[S.prev_shape];
                         S.epoch++;
                         S.relaxed = 1;
-                        if (d.tg_late) S.born |= d.cls_birth[nx];  // Topology.Update creates the spec's new groups
+                        if (d.tg_late) S.born = topo_birth(d, S.born, d.cls_birth[nx]);  // Topology.Update: the spec's new groups
                     } else {
                         d.last_len[pod] = S.qcount;
                         if (PREF && d.last_ep) d.last_ep[pod] = S.epoch;

@@ -518,6 +518,7 @@ struct kp_ctx {
     std::string solve_unsupported;           // catalog the Solve tables cannot hold (launch selection still works)
     // reserved offerings in Solve (ReservationManager): <= 64 per catalog
     bool ro_ok = true;
+    std::string ro_why;  // why the reserved offerings do not fit ResvTab (Solve / consolidation refuse with it)
     bool wide_resvid = false;                // the reservation-id label has > 64 values (no type value masks for it)
     // reserved offerings (ResvTab rows, kp_layout.h; padding rows have type -1 and offering -1)
     std::vector<int32_t> ro_type, ro_zone, ro_zid, ro_rid, ro_ridv, ro_rtype;
@@ -575,8 +576,11 @@ struct kp_ctx {
     DBuf<int2> d_tce_hosts;
     DBuf<int2> d_tg_frow;
     DBuf<int32_t> d_tg_late;
-    DBuf<uint64_t> d_cls_birth, d_born_s, d_born_m;
+    DBuf<uint64_t> d_cls_birth, d_born_s, d_born_m, d_late_sib;
+    DBuf<int32_t> d_late_grp;
     int tg_nlate = 0;
+    bool tg_var = false;  // variant groups (topo_build): late_sib / late_grp are live
+    std::vector<uint64_t> h_late_sib;
     std::vector<uint64_t> h_cls_birth;
     DBuf<KpTopoRec> d_cls_tre;
     DBuf<uint64_t> d_tg_known0, d_tg_known;
@@ -750,9 +754,12 @@ static hipError_t upload_resv(kp_ctx* c, hipStream_t s) {
     X.nrid = (int)c->ro_rid_vid.size();
     X.ridw = (X.nrid + 63) / 64;
     X.ctv = c->key_ct >= 0 ? c->cat.keys[c->key_ct].find("reserved") : -1;
-    hipError_t e;
+    hipError_t e = hipSuccess, first = hipSuccess;  // the first failed upload is returned before the header goes up
     auto up = [&](DBuf<int32_t>& b, const std::vector<int32_t>& v) -> const int32_t* {
-        if ((e = b.upload(v, s)) != hipSuccess) return nullptr;
+        if ((e = b.upload(v, s)) != hipSuccess) {
+            if (first == hipSuccess) first = e;
+            return nullptr;
+        }
         return b.p;
     };
     X.type = up(c->d_ro_type, c->ro_type);
@@ -762,6 +769,7 @@ static hipError_t upload_resv(kp_ctx* c, hipStream_t s) {
     X.ridv = up(c->d_ro_ridv, c->ro_ridv);
     X.rtype = up(c->d_ro_rtype, c->ro_rtype);
     X.rid_vid = up(c->d_ro_rid_vid, c->ro_rid_vid);
+    if (first != hipSuccess) return first;
     if ((e = c->d_ro_avail.upload(c->ro_avail, s)) != hipSuccess) return e;
     X.avail = c->d_ro_avail.p;
     c->h_ro_up.assign(1, X);
@@ -936,6 +944,7 @@ static kp_status catalog_upload_one(kp_ctx* ctx, const kp_catalog_view* v, uint6
     // reservations numbered densely in row order; the ReservationManager's initial capacity per reservation
     // (NewReservationManager: the least ReservationCapacity among the offerings carrying the ID)
     c->ro_ok = true;
+    c->ro_why.clear();
     c->ro_type.clear();
     c->ro_zone.clear();
     c->ro_zid.clear();
@@ -956,6 +965,8 @@ static kp_status catalog_upload_one(kp_ctx* ctx, const kp_catalog_view* v, uint6
             const int cnt = (int)(b - a), t = c->off_type[ro_rows[a]];
             if (cnt > 64) {  // one instance type with more than 64 reservations: its rows do not fit one word
                 c->ro_ok = false;
+                c->ro_why = std::string("instance type ") + (v->type_names && v->type_names[t] ? v->type_names[t] : "?") +
+                            " has more than 64 reserved offerings (one 64-row ResvTab word per type)";
                 break;
             }
             while ((c->ro_type.size() % 64) + cnt > 64) {  // padding up to the next word
@@ -1008,7 +1019,10 @@ static kp_status catalog_upload_one(kp_ctx* ctx, const kp_catalog_view* v, uint6
             }
             a = b;
         }
-        if ((int)c->ro_type.size() > KP_MAX_RO || (int)c->ro_rid_vid.size() > KP_MAX_RO) c->ro_ok = false;
+        if (c->ro_ok && ((int)c->ro_type.size() > KP_MAX_RO || (int)c->ro_rid_vid.size() > KP_MAX_RO)) {
+            c->ro_ok = false;
+            c->ro_why = "more than KP_MAX_RO (1024) reserved offerings";
+        }
         if (!c->ro_ok) {
             for (auto* x : {&c->ro_type, &c->ro_zone, &c->ro_zid, &c->ro_rid, &c->ro_ridv, &c->ro_rtype, &c->ro_rid_vid,
                             &c->ro_off, &c->rcap0})
@@ -1039,7 +1053,9 @@ static kp_status catalog_upload_one(kp_ctx* ctx, const kp_catalog_view* v, uint6
                     c->wide_resvid = true;
                     continue;
                 }
-                c->solve_unsupported = "multi-valued label " + c->cat.keys[k].name + " with > 64 values";
+                c->solve_unsupported = k == c->key_resvid && !c->ro_why.empty()
+                                           ? c->ro_why
+                                           : "multi-valued label " + c->cat.keys[k].name + " with > 64 values";
                 continue;
             }
             c->cat_kflags[k] = KF_CAT_MULTI;
@@ -1292,7 +1308,8 @@ struct HGroup {
     int type = 0, key = -1, owner = -1, skew = 0, mindom = 0, pol = 0, hrow = -1;
     bool host = false, inverse = false;
     std::vector<uint8_t> sel;   // per class: namespace ∈ namespaces ∧ the label selector matches
-    std::vector<uint8_t> memb;  // per class: the class owns the group (owner = the first)
+    std::vector<uint8_t> memb;  // per class: the class owns the group (owner = the first owner, topo_build)
+    std::vector<uint8_t> same;  // per class: an owner whose term's semantics equal the first owner's (filter, minDomains)
     int ident = -1;             // TopologyGroup.Hash() identity (topo_build)
 };
 struct TopoHost {
@@ -1301,10 +1318,14 @@ struct TopoHost {
     std::vector<std::vector<int>> neutral;    // per class: keys added to its digest only for narrowing
     int key_host = -1;
     int n_host = 0;
-    // groups created by Topology.Update on a relaxed pod (see topo_build): identity → bit among the late identities
-    // (-1: created by NewTopology whenever a pod owns it), the late identities each class owns
-    std::vector<int> ident_late;
+    // groups created by Topology.Update on a relaxed pod (see topo_build): group → its late bit (-1: created by
+    // NewTopology whenever a pod owns it), the late bits each class owns; per late bit, the bits of its identity's
+    // variant groups (itself alone for a plain late group) and its group
+    std::vector<int> g_late;
     std::vector<uint64_t> cls_birth;
+    std::vector<uint64_t> late_sib;
+    std::vector<int32_t> late_grp;
+    bool any_var = false;
     int n_late = 0;
 };
 
@@ -1508,6 +1529,17 @@ static kp_status expand_preferences(const kp_solve_input* in, int pref_policy, P
     return KP_OK;
 }
 
+// topo_birth (kp_eval.h) on the host: the late bits `add` are born unless a variant sibling already is (sib empty: no
+// variant groups)
+static uint64_t late_birth(const std::vector<uint64_t>& sib, uint64_t born, uint64_t add) {
+    if (sib.empty()) return born | add;
+    for (uint64_t x = add & ~born; x; x &= x - 1) {
+        const int b = __builtin_ctzll(x);
+        if (!(born & sib[b])) born |= 1ull << b;
+    }
+    return born;
+}
+
 // Topology groups ([core] scheduling/topology.go Update / updateInverseAntiAffinity, topologygroup.go Hash): Go keeps
 // one group per TopologyGroup.Hash() — topology key, type, namespaces, label selector, maxSkew and the node filter
 // (MakeTopologyNodeFilter: the requirement key sets of the nodeSelector with each required term, the policies, the
@@ -1663,8 +1695,13 @@ static kp_status topo_build(kp_ctx* c, const kp_solve_input* in, const std::vect
     // TopologyGroup (its node filter, minDomains and selector), every later owner only AddOwner()s.  NewTopology
     // iterates its pods in input order, so the first owner is the class of the first input pod whose spec owns the
     // identity; consolidation probes each run their own NewTopology over the pending pods, then their candidates' pods.
-    // When the owners' semantics agree any owner is that group.  Otherwise a first owner that a probe, or a relaxation at
-    // run time, would choose differently is refused.
+    // When the owners' semantics agree any owner is that group.  An identity that only relaxed pods create (no pod of the
+    // Solve, or of any probe, owns it at NewTopology) takes the semantics of whichever pod relaxes into it first: it
+    // becomes one "variant" group per distinct semantics, each with a late bit of its own; the first relaxation births
+    // its variant only (topo_birth: KpDev.late_sib), and the class caches of every owner route the identity's
+    // constraint to the born variant (fill_class_cache).  A first owner that differs between consolidation probes, or a
+    // probe-dependent mix of NewTopology and relaxation owners, is refused.
+    std::vector<uint8_t> gvar;  // per device group: a variant group
     {
         const int P = in->pods.n_pods;
         std::vector<int64_t> firstpos(std::max(C, 1), INT64_MAX);  // Solve: first input pod per stage-0 class
@@ -1673,17 +1710,28 @@ static kp_status topo_build(kp_ctx* c, const kp_solve_input* in, const std::vect
         } else {
             for (int q = (int)c->cons_pend.size() - 1; q >= 0; q--) firstpos[in->pods.class_id[c->cons_pend[q]]] = q;
         }
-        int amb = 0;
+        int amb = 0, nvar = 0;
         for (int I = 0; I < NI; I++) {
             const std::vector<int>& es = by_ident[I];
             bool one = true;
             for (int e : es) one = one && ents[e].sig == ents[es[0]].sig;
             int own = es[0];
+            bool variant = false;
             auto first_by = [&](const std::vector<int64_t>& pos) {  // the stage-0 owner entry of the smallest position
                 int b = -1;
                 for (int e : es)
                     if (ents[e].cls < C0 && pos[ents[e].cls] != INT64_MAX && (b < 0 || pos[ents[e].cls] < pos[ents[b].cls])) b = e;
                 return b;
+            };
+            // variants need equal selection (Counts) and one semantics per class; inverse and affinity groups have no
+            // node filter or minDomains, so their semantics differ only in selection
+            auto variants_ok = [&]() {
+                for (int e : es) {
+                    if (ents[e].g.inverse || ents[e].g.type != KP_TOPO_SPREAD || ents[e].g.sel != ents[es[0]].g.sel) return false;
+                    for (int f : es)
+                        if (ents[f].cls == ents[e].cls && ents[f].sig != ents[e].sig) return false;
+                }
+                return true;
             };
             if (!one) {
                 amb++;
@@ -1696,23 +1744,12 @@ static kp_status topo_build(kp_ctx* c, const kp_solve_input* in, const std::vect
                     return true;
                 };
                 const int b = first_by(firstpos);
-                if (b >= 0) {
-                    own = b;  // every Solve / probe creates it from this pod at NewTopology
-                } else if (!c->cons_topo) {
-                    // no input pod owns it: only a relaxation creates it, from whichever pod relaxes first
-                    if (!relaxed.empty()) {
-                        if (!relaxed_agree(ents[relaxed[0]].sig)) {
-                            err = "topology groups of one TopologyGroup.Hash() identity with different node filters or "
-                                  "minDomains that only relaxed pods create";
-                            return KP_E_UNSUPPORTED;
-                        }
-                        own = relaxed[0];
-                    }
-                } else {
+                int got = -1;
+                bool missing = false, same = true;
+                if (b < 0 && c->cons_topo) {
                     // consolidation: each probe's first owner is the first of its candidates' pods owning it
                     std::vector<int64_t> cpos(std::max(C, 1), INT64_MAX);
-                    int prev = -1, got = -1;
-                    bool missing = false, same = true;
+                    int prev = -1;
                     auto close_cand = [&]() {
                         if (prev < 0) return;
                         const int f = first_by(cpos);
@@ -1738,48 +1775,106 @@ static kp_status topo_build(kp_ctx* c, const kp_solve_input* in, const std::vect
                         for (; seen < (int)c->cons_extra.size() && c->cons_extra[seen][2] == ci; seen++) has = true;
                         missing = missing || !has;
                     }
-                    if (!same || (got >= 0 && missing && !relaxed_agree(ents[got].sig)) ||
-                        (got < 0 && !relaxed.empty() && !relaxed_agree(ents[relaxed[0]].sig))) {
-                        err = "topology groups of one TopologyGroup.Hash() identity with different node filters or "
-                              "minDomains whose first owner differs between consolidation probes";
+                }
+                if (b >= 0) {
+                    own = b;  // every Solve / probe creates it from this pod at NewTopology
+                } else if (got >= 0 && same && !(missing && !relaxed_agree(ents[got].sig))) {
+                    own = got;  // every probe that creates it has a first owner of these semantics
+                } else if (got >= 0) {
+                    // the first owner differs between probes (or some probe's relaxation creates it): one variant per
+                    // semantics, each probe starting with its own first owner's variant born (kp_consolidate_prepare)
+                    if (!variants_ok()) {
+                        err = "topology groups of one TopologyGroup.Hash() identity with different selections whose "
+                              "first owner differs between consolidation probes";
                         return KP_E_UNSUPPORTED;
                     }
-                    own = got >= 0 ? got : (!relaxed.empty() ? relaxed[0] : es[0]);
+                    variant = true;
+                } else if (!relaxed.empty() && !relaxed_agree(ents[relaxed[0]].sig)) {
+                    // no pod owns it at NewTopology: the first relaxation into it decides
+                    if (!variants_ok()) {
+                        err = "topology groups of one TopologyGroup.Hash() identity with different selections that only "
+                              "relaxed pods create";
+                        return KP_E_UNSUPPORTED;
+                    }
+                    variant = true;
+                } else if (!relaxed.empty()) {
+                    own = relaxed[0];
                 }
             }
-            HGroup g = ents[own].g;
-            g.memb.assign(C, 0);
-            for (int e : es) g.memb[ents[e].cls] = 1;
-            th.g.push_back(std::move(g));
+            if (!variant) {
+                HGroup g = ents[own].g;
+                g.memb.assign(C, 0);
+                g.same.assign(C, 0);
+                for (int e : es) {
+                    g.memb[ents[e].cls] = 1;
+                    g.same[ents[e].cls] |= ents[e].sig == ents[own].sig;
+                }
+                th.g.push_back(std::move(g));
+                gvar.push_back(0);
+                continue;
+            }
+            std::vector<int> done(es.size(), 0);
+            for (size_t i = 0; i < es.size(); i++) {  // one group per distinct semantics, its owners the classes holding it
+                if (done[i]) continue;
+                HGroup g = ents[es[i]].g;
+                g.memb.assign(C, 0);
+                for (size_t j = i; j < es.size(); j++)
+                    if (ents[es[j]].sig == ents[es[i]].sig) {
+                        g.memb[ents[es[j]].cls] = 1;
+                        done[j] = 1;
+                    }
+                g.same = g.memb;
+                th.g.push_back(std::move(g));
+                gvar.push_back(1);
+                nvar++;
+            }
         }
         if (getenv("KPSIM_DIAG_IDENT"))  // diagnostics: identities whose owners' semantics differ
-            fprintf(stderr, "[kpsim] topology identities %d, owner entries %zu, identities with several semantics %d\n", NI,
-                    ents.size(), amb);
+            fprintf(stderr, "[kpsim] topology identities %d, owner entries %zu, identities with several semantics %d, "
+                    "variant groups %d\n", NI, ents.size(), amb, nvar);
     }
-    // late identities: a relaxed stage owns it and its input class does not
+    // late identities: a relaxed stage owns it and its input class does not; every variant group is late
     std::vector<std::vector<uint8_t>> own0(NI);  // identity → input classes owning it at stage 0
     for (auto& own : own0) own.assign(std::max(C0, 1), 0);
     for (const HGroup& g : th.g)
         for (int o = 0; o < C && o < C0; o++)
             if (g.memb[o]) own0[g.ident][o] = 1;
-    th.ident_late.assign(NI, -1);
-    for (const HGroup& g : th.g) {
-        if (th.ident_late[g.ident] >= 0) continue;
+    th.g_late.assign(th.g.size(), -1);
+    th.late_sib.clear();
+    th.late_grp.clear();
+    auto new_bit = [&](int gi) -> bool {
+        if (th.n_late >= 64) {
+            err = "more than 64 topology groups that only relaxed pods own";
+            return false;
+        }
+        th.g_late[gi] = th.n_late++;
+        th.late_sib.push_back(1ull << th.g_late[gi]);
+        th.late_grp.push_back(gi);
+        return true;
+    };
+    for (int gi = 0; gi < (int)th.g.size(); gi++) {
+        const HGroup& g = th.g[gi];
+        if (gvar[gi]) {
+            if (!new_bit(gi)) return KP_E_UNSUPPORTED;
+            continue;
+        }
         for (int o = C0; o < C; o++)
             if (g.memb[o] && !own0[g.ident][X.origin[o]]) {
-                if (th.n_late >= 64) {
-                    err = "more than 64 topology groups that only relaxed pods own";
-                    return KP_E_UNSUPPORTED;
-                }
-                th.ident_late[g.ident] = th.n_late++;
+                if (!new_bit(gi)) return KP_E_UNSUPPORTED;
                 break;
             }
     }
+    for (int gi = 0; gi < (int)th.g.size(); gi++)  // variant siblings: the late bits of one identity's variant groups
+        if (gvar[gi])
+            for (int gj = 0; gj < (int)th.g.size(); gj++)
+                if (gvar[gj] && th.g[gj].ident == th.g[gi].ident) th.late_sib[th.g_late[gi]] |= 1ull << th.g_late[gj];
+    th.any_var = false;
+    for (uint8_t v : gvar) th.any_var = th.any_var || v;
     th.cls_birth.assign(C, 0);
-    for (const HGroup& g : th.g)
-        if (th.ident_late[g.ident] >= 0)
+    for (int gi = 0; gi < (int)th.g.size(); gi++)
+        if (th.g_late[gi] >= 0)
             for (int o = 0; o < C; o++)
-                if (g.memb[o]) th.cls_birth[o] |= 1ull << th.ident_late[g.ident];
+                if (th.g[gi].memb[o]) th.cls_birth[o] |= 1ull << th.g_late[gi];
     th.key_host = c->sol.key("kubernetes.io/hostname");
     for (int gi = 0; gi < (int)th.g.size(); gi++) {
         HGroup& g = th.g[gi];
@@ -1835,7 +1930,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     if (!ctx->have_catalog) return fail(ctx, KP_E_STATE, "kp_solve before kp_catalog_upload");
     if (!ctx->solve_unsupported.empty()) return fail(ctx, KP_E_UNSUPPORTED, "Solve: " + ctx->solve_unsupported);
     if (ctx->has_reserved && !ctx->ro_ok)
-        return fail(ctx, KP_E_UNSUPPORTED, "Solve over a catalog with more than KP_MAX_RO (1024) reserved offerings");
+        return fail(ctx, KP_E_UNSUPPORTED, "Solve over this catalog: " + ctx->ro_why);
     const auto t0 = clk::now();
     HIPCHK(hipSetDevice(ctx->device));
     kp_ctx* c = ctx;
@@ -2067,8 +2162,9 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
             bool qrec = true;
             for (int gi : th.rec[row]) {
                 const HGroup& g = th.g[gi];
-                // a member's pods satisfy the group's node filter (its semantics equal the member's own filter)
-                if (!g.inverse && g.type == KP_TOPO_SPREAD && (g.pol & 1) && !g.memb[row]) qrec = false;
+                // an owner's pods satisfy their own node filter: the group's when the owner's semantics are the first
+                // owner's (an owner of the identity with another filter records through the group's, topo_record)
+                if (!g.inverse && g.type == KP_TOPO_SPREAD && (g.pol & 1) && !g.same[row]) qrec = false;
             }
             if (qrec) cflags[row] |= CF_TOPO_QREC;
         }
@@ -2504,7 +2600,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
                 towner[gi] = g.owner;
                 tpol[gi] = g.pol;
                 if (!g.inverse && g.type == KP_TOPO_SPREAD && (g.pol & 1)) tfrow[gi] = frow[g.owner];
-                tlate[gi] = th.ident_late[g.ident];
+                tlate[gi] = th.g_late[gi];
                 if (g.host) continue;
                 for (auto& kv : domains_of(g.key)) {
                     bool ok = !(g.type == KP_TOPO_SPREAD && (g.pol & 2));
@@ -2585,7 +2681,7 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
                     r.g = gi;
                     r.flags = g.type | (g.inverse ? 4 : 0) | (g.host ? 8 : 0);
                     r.key = g.host ? -1 - g.hrow : g.key;
-                    r.late = th.ident_late[g.ident];
+                    r.late = th.g_late[gi];
                     if (!g.inverse && g.type == KP_TOPO_SPREAD && (g.pol & 2))
                         for (int j = 0; j < NT; j++)
                             if (!((tol[g.owner] >> j) & 1ull)) r.skip |= 1ull << j;
@@ -2713,7 +2809,14 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
             HIPCHK(c->d_tg_late.upload(tlate, s));
             c->h_cls_birth.assign(th.cls_birth.begin(), th.cls_birth.end());
             HIPCHK(c->d_cls_birth.upload(c->h_cls_birth, s));
-            for (int i = 0; i < P; i++) d.born0 |= th.cls_birth[in->pods.class_id[i]];
+            // NewTopology over the pods in input order: a variant is born only while no sibling is (topo_birth)
+            for (int i = 0; i < P; i++) d.born0 = late_birth(th.late_sib, d.born0, th.cls_birth[in->pods.class_id[i]]);
+        }
+        c->tg_var = c->tg_nlate > 0 && th.any_var;
+        c->h_late_sib = th.late_sib;
+        if (c->tg_var) {
+            HIPCHK(c->d_late_sib.upload(th.late_sib, s));
+            HIPCHK(c->d_late_grp.upload(th.late_grp, s));
         }
         HIPCHK(c->d_tg_cnt0.upload(tcnt0, s));
         HIPCHK(c->d_tg_cnt.ensure(tcnt0.size()));
@@ -2867,6 +2970,8 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     d.tg_frow = c->d_tg_frow.p;
     d.tg_late = c->tg_nlate > 0 ? c->d_tg_late.p : nullptr;
     d.cls_birth = c->tg_nlate > 0 ? c->d_cls_birth.p : nullptr;
+    d.late_sib = c->tg_var ? c->d_late_sib.p : nullptr;
+    d.late_grp = c->tg_var ? c->d_late_grp.p : nullptr;
     d.tg_cnt = c->d_tg_cnt.p;
     d.tg_known = c->d_tg_known.p;
     d.tg_hcnt = c->d_tg_hcnt.p;
@@ -3214,7 +3319,7 @@ static kp_status cons_prepare_one(kp_ctx* ctx, const kp_consolidate_input* in) t
     ctx->cons_prep_valid = false;
     ctx->cons_gen++;  // cached pass rows and read-backs of kp_consolidate_command are stale
     if (ctx->has_reserved && !ctx->ro_ok)
-        return fail(ctx, KP_E_UNSUPPORTED, "consolidation over a catalog with more than KP_MAX_RO (1024) reserved offerings");
+        return fail(ctx, KP_E_UNSUPPORTED, "consolidation over this catalog: " + ctx->ro_why);
     if (!ctx->solve_unsupported.empty()) return fail(ctx, KP_E_UNSUPPORTED, "consolidation: " + ctx->solve_unsupported);
     if (in->mode != KP_CONSOLIDATE_SINGLE && in->mode != KP_CONSOLIDATE_MULTI)
         return fail(ctx, KP_E_INVALID, "unknown consolidation mode");
@@ -3414,14 +3519,19 @@ static kp_status cons_prepare_one(kp_ctx* ctx, const kp_consolidate_input* in) t
         // late topology identities a probe's NewTopology creates: owned by its pending pods or its candidates' pods
         k.born_s = k.born_m = nullptr;
         if (c->tg_nlate > 0) {
+            // in the probe's pod order (pending, then its candidates' pods): a variant is born only while no sibling
+            // is, so each probe starts with its own first owner's variant
+            const std::vector<uint64_t>& sib = c->tg_var ? c->h_late_sib : std::vector<uint64_t>();
             uint64_t bp = 0;
-            for (int i = 0; i < in->n_pending; i++) bp |= c->h_cls_birth[cl.pods.class_id[in->pending[i]]];
+            for (int i = 0; i < in->n_pending; i++) bp = late_birth(sib, bp, c->h_cls_birth[cl.pods.class_id[in->pending[i]]]);
             std::vector<uint64_t> bs(std::max(NC, 1), bp), bm(std::max(nm, 1), bp);
             uint64_t acc = bp;
             for (int ci = 0; ci < NC; ci++) {
-                for (int q = 0; q < in->candidates[ci].n_pods; q++)
-                    bs[ci] |= c->h_cls_birth[cl.pods.class_id[in->candidates[ci].pods[q]]];
-                acc |= bs[ci];
+                for (int q = 0; q < in->candidates[ci].n_pods; q++) {
+                    const uint64_t cb = c->h_cls_birth[cl.pods.class_id[in->candidates[ci].pods[q]]];
+                    bs[ci] = late_birth(sib, bs[ci], cb);
+                    acc = late_birth(sib, acc, cb);
+                }
                 if (ci >= 1 && ci - 1 < nm) bm[ci - 1] = acc;  // multi-node probe i covers candidates [0, i + 2)
             }
             HIPCHK(c->d_born_s.upload(bs, s));

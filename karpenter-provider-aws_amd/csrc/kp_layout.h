@@ -268,6 +268,12 @@ struct KpDev {
     const int32_t* tg_late;
     const uint64_t* cls_birth;
     uint64_t born0;
+    // variant groups (an identity only relaxed pods create, its owners' node filters / minDomains differing): per late
+    // bit, the bits of its identity's variants (itself alone for a plain late group) and its group; null without
+    // variants.  A relaxation births a variant only while none of its siblings is born (topo_birth), and a class's
+    // constraint entry on a variant routes to the born sibling (fill_class_cache, topo_prefilter_setup).
+    const uint64_t* late_sib;
+    const int32_t* late_grp;
     int32_t* tg_cnt;                 // [G][64] counts by value id (value-keyed groups)
     uint64_t* tg_known;              // [G] value ids present in the group's domains map
     int32_t* tg_hcnt;                // [hostname groups][HN]

@@ -194,17 +194,18 @@ class Consolidator:
 
     def probes(self, cp: model.ConsolidationProblem, mode, begin=0, end=0, cluster_view=None) -> np.ndarray:
         v = model.ConsolidateInputView(cp, mode, begin, end, self.spot_to_spot, self.max_candidates, cluster_view)
-        self._prepared = (cp, v)  # kp_consolidate leaves the pass prepared on the ctx
-        return self.ctx.consolidate(v)
+        res = self.ctx.consolidate(v)
+        self._prepared = (cp, mode, self.ctx.pass_gen, v)  # kp_consolidate leaves the pass prepared on the ctx
+        return res
 
     def replacement(self, cp: model.ConsolidationProblem, mode, probe) -> Command:
-        """kp_consolidate_replacement of one probe; prepares the pass first when this process evaluated no probe of it
-        (an empty shard)."""
+        """kp_consolidate_replacement of one probe; prepares the pass first unless the ctx still holds this process's
+        pass of (cp, mode): nothing else (a Solve, another pass, a catalog change) ran on the ctx since (pass_gen)."""
         prep = getattr(self, "_prepared", None)
-        if prep is None or prep[0] is not cp:
+        if prep is None or prep[0] is not cp or prep[1] != mode or prep[2] != self.ctx.pass_gen:
             v = model.ConsolidateInputView(cp, mode, 0, 0, self.spot_to_spot, self.max_candidates)
             self.ctx.consolidate_prepare(v)
-            self._prepared = (cp, v)
+            self._prepared = (cp, mode, self.ctx.pass_gen, v)
         return self.ctx.consolidate_replacement(mode, probe)
 
     def compute_command(self, cp: model.ConsolidationProblem, mode, group=None) -> Command:

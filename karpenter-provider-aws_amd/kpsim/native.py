@@ -88,22 +88,28 @@ class Context:
             raise KpError(st, "kp_ctx_create(device=%d) — a gfx950 device is required" % device)
         self.h = h
         self._catalog = None
+        # bumped by every call that replaces the ctx's catalog or prepared pass (kp_catalog_*, kp_solve*,
+        # kp_consolidate[_prepare]): lets a caller tell whether the pass it prepared is still the ctx's
+        self.pass_gen = 0
 
     def check(self, st, what):
         if st != 0:
             raise KpError(st, "%s: %s" % (what, self.L.kp_last_error(self.h).decode()))
 
     def upload_catalog(self, catalog_view, epoch=1):
+        self.pass_gen += 1
         self.check(self.L.kp_catalog_upload(self.h, C.byref(catalog_view.view), epoch), "kp_catalog_upload")
         self._catalog = catalog_view
 
     def patch_avail(self, available, epoch):
+        self.pass_gen += 1
         import numpy as np
         a = np.ascontiguousarray(available, np.uint8)
         self.check(self.L.kp_catalog_patch_avail(self.h, a.ctypes.data_as(C.POINTER(C.c_uint8)), len(a), epoch),
                    "kp_catalog_patch_avail")
 
     def patch_price(self, idx, price, epoch):
+        self.pass_gen += 1
         import numpy as np
         i = np.ascontiguousarray(idx, np.int32)
         p = np.ascontiguousarray(price, np.float64)
@@ -142,6 +148,7 @@ class Context:
         return list(ms)
 
     def prepare(self, input_view):
+        self.pass_gen += 1
         self.check(self.L.kp_solve_prepare(self.h, C.byref(input_view.view)), "kp_solve_prepare")
 
     def execute(self):
@@ -151,6 +158,7 @@ class Context:
         self.check(self.L.kp_solve_fetch(self.h, C.byref(out_buffers.view)), "kp_solve_fetch")
 
     def solve(self, input_view, out_buffers):
+        self.pass_gen += 1
         self.check(self.L.kp_solve(self.h, C.byref(input_view.view), C.byref(out_buffers.view)), "kp_solve")
 
     def nodeclaim_requirements(self, nc):
@@ -179,6 +187,7 @@ class Context:
 
     def consolidate(self, cons_view):
         """kp_consolidate over the view's probe range -> numpy array of abi.PROBE_DTYPE (one row per probe)."""
+        self.pass_gen += 1
         import numpy as np
         v = cons_view.view
         n = self.L.kp_consolidate_probe_count(C.byref(v))
@@ -190,6 +199,7 @@ class Context:
         return out[:max(0, b1 - b0)]
 
     def consolidate_prepare(self, cons_view):
+        self.pass_gen += 1
         self.check(self.L.kp_consolidate_prepare(self.h, C.byref(cons_view.view)), "kp_consolidate_prepare")
 
     def consolidate_execute(self, mode, n_probes, begin=0, end=0):

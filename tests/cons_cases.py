@@ -116,14 +116,22 @@ def check_expect(cmd, cp, expect):
 SCENARIOS = {"reserved_into": reserved_into, "reserved_between": reserved_between}
 
 
-def shared_identity_cluster(golden, pending_a):
+def shared_identity_cluster(golden, pending_a, selection=False):
     """Two m5.2xlarge nodes (1a, 1b), each a candidate holding one pod of test_topology_cpu.shared_filter_problem's
     Deployments (one spread identity, Honor filters zone In [1a, 1b] vs [1b, 1c]); a third node (1c) with room.  Each
     single-node probe's NewTopology sees only its own candidate's pod (and the pending pods), so without a pending pod
     the two probes create the group from different owners: kp_consolidate refuses that.  pending_a adds a pending pod
-    of A's Deployment, which every probe sees first."""
+    of A's Deployment, which every probe sees first.  Without one, each probe starts with its own first owner's variant
+    group born (kp_consolidate_prepare).  selection: A's selector is app In [web] twice — hashstructure folds the pair
+    away (SlicesAsSets XOR), so it hashes like B's empty selector, which also selects a third class (app=db): one
+    identity, two selections, which variant groups do not cover — refused."""
     import test_topology_cpu as TC
     prob = TC.shared_filter_problem(golden, True)
+    if selection:
+        web = model.Requirement("app", "In", ["web"])
+        prob.classes[0].topology = [model.TopologyTerm("spread", model.ZONE, [web, web], max_skew=1)]
+        prob.classes[1].topology = [model.TopologyTerm("spread", model.ZONE, [], max_skew=1)]
+        prob.classes.append(model.PodClass(labels={"app": "db"}))
     it = golden[row(golden, "m5.2xlarge")]
     specs = [(0, {"cpu": "1", "memory": "1Gi"}), (1, {"cpu": "1", "memory": "1Gi"})]
     if pending_a:

@@ -496,16 +496,20 @@ def fuzz_shared_identity_problem(catalog, seed, n_pods=200, n_existing=0):
     return add_shared_identities(np.random.Generator(np.random.PCG64(seed + 4242)), prob)
 
 
-def fuzz_shared_identity_consolidation(catalog, seed, n_nodes=30, n_pods=160):
+def fuzz_shared_identity_consolidation(catalog, seed, n_nodes=30, n_pods=160, pending_owner=True):
     """fuzz_topology_consolidation plus add_shared_identities.  Every probe's NewTopology runs over the pending pods
-    first, so a family with a pending pod has one first owner in every probe: one pod of each family that has none
-    moves from its candidate to the front of the pending pods (a family whose first owner differed between probes is
-    refused by the device, test_gpu_consolidation.py covers that separately)."""
+    first, so a family with a pending pod has one first owner in every probe.  pending_owner: one pod of each family
+    that has none moves from its candidate to the front of the pending pods; otherwise the pending pods of the families
+    are dropped, so each probe's first owner is among its own candidates' pods."""
     cp = fuzz_topology_consolidation(catalog, seed, n_nodes=n_nodes, n_pods=n_pods)
     rng = np.random.Generator(np.random.PCG64(seed + 4343))
     prob = add_shared_identities(rng, cp.cluster)
     cls = prob.pods.class_id
     pending = [int(p) for p in cp.pending]
+    if not pending_owner:
+        fam_cls = {c for fam in prob.shared_families for c in fam}
+        cp.pending = np.array([p for p in pending if int(cls[p]) not in fam_cls], np.int32)
+        return cp
     for fam in prob.shared_families:
         if any(int(cls[p]) in fam for p in pending):
             continue

@@ -39,7 +39,8 @@ def main():
     for a_first in (True, False):
         run("filter_%s" % a_first, lambda: solve_prep(TC.shared_filter_problem(golden, a_first)))
         run("min_domains_%s" % a_first, lambda: solve_prep(TC.shared_min_domains_problem(golden, a_first)))
-    run("relaxed_only", lambda: solve_prep(TC.relaxed_only_shared_problem(golden)))
+    for a_big in (True, False):
+        run("relaxed_only_%s" % a_big, lambda: solve_prep(TC.relaxed_only_shared_problem(golden, a_big)))
     for seed in range(int(sys.argv[1]) if len(sys.argv) > 1 else 8):
         rng = np.random.Generator(np.random.PCG64(seed + 500))
         sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=160, replace=False))]
@@ -48,12 +49,23 @@ def main():
         run("fuzz_%d" % seed, lambda: solve_prep(prob))
     for pend in (True, False):
         run("cons_pending_%s" % pend, lambda: cons_prep(cons_cases.shared_identity_cluster(golden, pend)))
+    run("cons_selection", lambda: cons_prep(cons_cases.shared_identity_cluster(golden, False, selection=True)))
     for seed in range(4):
         rng = np.random.Generator(np.random.PCG64(4500 + seed))
         sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 300)), replace=False))]
         cp = fuzzgen.fuzz_shared_identity_consolidation(sub, 4500 + seed, n_nodes=int(rng.integers(4, 50)),
-                                                        n_pods=int(rng.integers(20, 200)))
+                                                        n_pods=int(rng.integers(20, 200)), pending_owner=seed % 2 == 0)
         run("cons_fuzz_%d" % seed, lambda: cons_prep(cp))
+    # reserved offerings: one type with 70 reservations (its rows exceed one 64-row ResvTab word) and more than
+    # KP_MAX_RO in all are refused with their own reasons
+    import copy
+    from kpsim import synth
+    cat = copy.deepcopy(golden)
+    for i in range(70):
+        cons_cases.add_reservation(cat, "m5.large", "cr-p%03d" % i)
+    run("resv_per_type_70", lambda: solve_prep(synth.config2(n_pods=50, catalog=cat)))
+    wide = synth.wide_reservation_catalog(golden, 1100, max_per_type=4)
+    run("resv_over_max", lambda: solve_prep(synth.config2(n_pods=50, catalog=wide)))
     ctx.close()
     print(json.dumps(out))
 

@@ -718,37 +718,40 @@ def test_consolidation_wide_catalog(ctx, golden):
 # ---- topology groups shared by TopologyGroup.Hash() identity in the probes (row N1): each probe's NewTopology creates
 # the group from the first of its pods (pending, then its candidates' pods) that owns it ----
 
-def test_shared_identity_probes(ctx, golden):
-    """A pending pod of A's Deployment comes first in every probe: the group is A's (filter zone In [1a, 1b]) in all of
-    them; probes and command against the oracle."""
+@pytest.mark.parametrize("pending_a", [True, False])
+def test_shared_identity_probes(ctx, golden, pending_a):
+    """pending_a: a pending pod of A's Deployment comes first in every probe, so the group is A's (filter zone In
+    [1a, 1b]) in all of them.  Without it probe 0 creates the group from A's pod and probe 1 from B's: one variant group
+    per filter, each probe starting with its own first owner's variant born.  Probes and command against the oracle."""
     import cons_cases
-    cp = cons_cases.shared_identity_cluster(golden, pending_a=True)
+    cp = cons_cases.shared_identity_cluster(golden, pending_a)
     for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
         assert_probes_equal(device_probes(ctx, cp, mode), pyoracle.consolidate(cp, mode))
     assert_commands_equal(device_command(ctx, cp, abi.KP_CONSOLIDATE_BOTH),
                           pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH))
 
 
-def test_shared_identity_probes_refused(ctx, golden):
-    """No pending pod: probe 0 creates the group from A's pod, probe 1 from B's — two node filters for one identity in
-    one pass, which the device's one group per identity cannot hold: refused (KP_E_UNSUPPORTED), never approximated."""
+def test_shared_identity_selection_refused(ctx, golden):
+    """One identity whose owners select different pods (a selector pair hashstructure folds away) and whose first owner
+    differs between probes: variant groups need one selection, so the pass is refused (KP_E_UNSUPPORTED)."""
     import cons_cases
     from kpsim import native
-    cp = cons_cases.shared_identity_cluster(golden, pending_a=False)
+    cp = cons_cases.shared_identity_cluster(golden, pending_a=False, selection=True)
     with pytest.raises(native.KpError) as e:
         device_probes(ctx, cp, abi.KP_CONSOLIDATE_SINGLE)
-    assert e.value.status == abi.KP_E_UNSUPPORTED and "differs between consolidation probes" in str(e.value)
+    assert e.value.status == abi.KP_E_UNSUPPORTED and "different selections" in str(e.value)
 
 
-@pytest.mark.parametrize("seed", range(10))
+@pytest.mark.parametrize("seed", range(12))
 def test_fuzz_consolidation_shared_identity(ctx, golden, seed):
     """fuzzgen.fuzz_shared_identity_consolidation: sibling Deployments with equal spread identities and different Honor
-    filter values / minDomains over topology-constrained clusters, a pod of each family pending; both modes and the
-    command against the oracle."""
+    filter values / minDomains over topology-constrained clusters; even seeds put a pod of each family first among the
+    pending pods (one first owner for every probe), odd seeds leave the first owner to each probe (variant groups).
+    Both modes and the command against the oracle."""
     rng = np.random.Generator(np.random.PCG64(4500 + seed))
     sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 300)), replace=False))]
     cp = fuzzgen.fuzz_shared_identity_consolidation(sub, 4500 + seed, n_nodes=int(rng.integers(4, 50)),
-                                                    n_pods=int(rng.integers(20, 200)))
+                                                    n_pods=int(rng.integers(20, 200)), pending_owner=seed % 2 == 0)
     for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
         assert_probes_equal(device_probes(ctx, cp, mode), pyoracle.consolidate(cp, mode))
     assert_commands_equal(device_command(ctx, cp, abi.KP_CONSOLIDATE_BOTH),

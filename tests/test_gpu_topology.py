@@ -357,13 +357,13 @@ def test_shared_identity_first_owner_min_domains(ctx, golden, a_first):
     assert list(r.pod_result) == TC.SHARED_MIN_DOMAINS_WANT[a_first]
 
 
-def test_shared_identity_relaxed_only_refused(ctx, golden):
-    """An identity with two filters that only relaxed pods create: the group's filter is decided by whichever pod
-    relaxes first at run time, which the device does not emulate — kp_solve refuses (never approximated)."""
-    from kpsim import native
-    with pytest.raises(native.KpError) as e:
-        parity.run_device(ctx, TC.relaxed_only_shared_problem(golden))
-    assert e.value.status == abi.KP_E_UNSUPPORTED and "only relaxed pods create" in str(e.value)
+@pytest.mark.parametrize("a_big", [True, False])
+def test_shared_identity_relaxed_only(ctx, golden, a_big):
+    """An identity with two filters that only relaxed pods create: one variant group per filter, the first relaxation
+    births its own (KpDev.late_sib), and every owner's constraint routes to it (hand-derived placements in
+    test_topology_cpu.RELAXED_ONLY_WANT)."""
+    r, _ = same(ctx, TC.relaxed_only_shared_problem(golden, a_big))
+    assert list(r.pod_result) == TC.RELAXED_ONLY_WANT[a_big]
 
 
 @pytest.mark.parametrize("seed", range(16))

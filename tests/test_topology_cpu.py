@@ -268,23 +268,29 @@ def test_shared_identity_first_owner_min_domains(golden, a_first):
     assert list(r.pod_result) == SHARED_MIN_DOMAINS_WANT[a_first]
 
 
-def relaxed_only_shared_problem(golden):
+def relaxed_only_shared_problem(golden, a_big=True):
     """Two Deployments with ORed required node-affinity terms whose first term no type satisfies: after Relax drops it,
-    each spread's node filter is its second term, zone In [1a] vs zone In [1b] — one identity that only relaxed pods
-    create, with two filters.  Topology.Update creates it from whichever pod relaxes first; the device refuses it
-    (KP_E_UNSUPPORTED), the oracle follows the first relaxation (A's pods, 2 cpu, pop first)."""
+    each spread's node filter is its second term, zone In [1a, 1b] vs zone In [1b, 1c] — one identity that only relaxed
+    pods create, with two filters.  Topology.Update creates it from whichever pod relaxes first: the bigger pods (2 cpu)
+    pop and relax first, A's when a_big (the device keeps one variant group per filter and births the first one)."""
     lab, term = _web_spread()
     nothing = [Requirement(AWS + "instance-category", "In", ["zz"])]
-    a = PodClass(labels=lab, topology=[term], required_terms=[nothing, [Requirement(ZONE, "In", ["test-zone-1a"])]])
-    b = PodClass(labels=lab, topology=[term], required_terms=[nothing, [Requirement(ZONE, "In", ["test-zone-1b"])]])
-    pods = synth.pods_from_specs([(0, {"cpu": "2", "memory": "1Gi"})] * 2 + [(1, {"cpu": "1", "memory": "1Gi"})] * 2)
+    a = PodClass(labels=lab, topology=[term],
+                 required_terms=[nothing, [Requirement(ZONE, "In", ["test-zone-1a", "test-zone-1b"])]])
+    b = PodClass(labels=lab, topology=[term],
+                 required_terms=[nothing, [Requirement(ZONE, "In", ["test-zone-1b", "test-zone-1c"])]])
+    big, small = {"cpu": "2", "memory": "1Gi"}, {"cpu": "1", "memory": "1Gi"}
+    pods = synth.pods_from_specs([(0, big if a_big else small)] * 3 + [(1, small if a_big else big)] * 3)
     return model.Problem(golden, [synth.default_nodepool()], [a, b], pods)
 
 
-def test_relaxed_only_shared_identity_oracle(golden):
-    """The oracle creates the relaxed identity from the first pod that relaxes into it (A: filter zone In [1a]); B's pods
-    in 1b are never counted, so both share one 1b NodeClaim; A's two pods go to 1a together (A's filter counts them,
-    but the only admitted domain is 1a and its own count is the minimum)."""
-    r, q = solve(relaxed_only_shared_problem(golden))
-    assert list(r.pod_result) == [0, 0, 1, 1]
-    assert [zone_of(x) for x in q] == [("test-zone-1a",), ("test-zone-1b",)]
+# A relaxes first: A's filter {1a,1b} (as SHARED_FILTER_WANT[True]).  B relaxes first: B's filter {1b,1c}; B → 1b, 1c,
+# 1b; A's pods in 1a are never counted, so all three share a 1a NodeClaim.
+RELAXED_ONLY_WANT = {True: [0, 1, 0, 2, 2, 2], False: [2, 2, 2, 0, 1, 0]}
+
+
+@pytest.mark.parametrize("a_big", [True, False])
+def test_relaxed_only_shared_identity_oracle(golden, a_big):
+    """The oracle creates the relaxed identity from the first pod that relaxes into it (Solver::birth)."""
+    r, _ = solve(relaxed_only_shared_problem(golden, a_big))
+    assert list(r.pod_result) == RELAXED_ONLY_WANT[a_big]

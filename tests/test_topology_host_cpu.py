@@ -3,7 +3,7 @@ with the first owner's node filter and minDomains), decided by kp_solve_prepare 
 the CPU stub of the HIP runtime (tests/cpu_stub, build/libkpsim_stub.so) and run in a child process
 (tests/stub_topology_checks.py).  The device's results for the accepted inputs are the -m gpu tests
 (test_gpu_topology.py, test_gpu_consolidation.py); here: the first-owner KATs and the shared-identity fuzz families are
-accepted, and the two shapes whose first owner the device cannot fix at prepare are refused."""
+accepted, and an identity whose owners' selections differ while its first owner differs between probes is refused."""
 import json
 import os
 import shutil
@@ -37,13 +37,21 @@ def test_shared_identity_fuzz_accepted(checks):
     for k, v in checks.items():
         if k.startswith("fuzz_") or k.startswith("cons_fuzz_"):
             assert v == "ok", (k, v)
-    assert checks["cons_pending_True"] == "ok"
+    assert checks["cons_pending_True"] == "ok" and checks["cons_pending_False"] == "ok"
 
 
-def test_relaxed_only_identity_refused(checks):
-    assert checks["relaxed_only"].startswith("KP_E_UNSUPPORTED") and "only relaxed pods create" in checks["relaxed_only"]
+def test_relaxed_only_identity_accepted(checks):
+    """one variant group per filter, born by the first relaxation (topo_build's variant groups)"""
+    assert checks["relaxed_only_True"] == "ok" and checks["relaxed_only_False"] == "ok"
 
 
-def test_probe_dependent_owner_refused(checks):
-    v = checks["cons_pending_False"]
-    assert v.startswith("KP_E_UNSUPPORTED") and "differs between consolidation probes" in v
+def test_probe_dependent_selection_refused(checks):
+    """an identity whose owners select different pods and whose first owner differs between probes"""
+    v = checks["cons_selection"]
+    assert v.startswith("KP_E_UNSUPPORTED") and "different selections" in v
+
+
+def test_reserved_offering_refusal_reasons(checks):
+    """ResvTab limits name their cause: a type with more than 64 reservations, or more than 1,024 reserved offerings."""
+    assert checks["resv_per_type_70"].startswith("KP_E_UNSUPPORTED") and "m5.large has more than 64" in checks["resv_per_type_70"]
+    assert checks["resv_over_max"].startswith("KP_E_UNSUPPORTED") and "KP_MAX_RO" in checks["resv_over_max"]
