@@ -23,6 +23,10 @@
 #include "kp_wave.h"
 #include "kp_device.h"
 
+// wave-count namespace (kp_layout.h KP_WNS): the 4-wave topology units and the 8-wave units hold distinct
+// definitions of the wave-shaped types (FfdShared, TeamBuf ...) and of every helper that uses them
+namespace KP_WNS {
+
 // Per-wave LDS scratch: merged requirements of the class's keys, resulting options, minValues bitset.
 struct WaveScratch {
     ReqHdr hdr[KP_MAX_CLASS_KEYS];
@@ -1232,3 +1236,6 @@ __device__ __forceinline__ bool eval_fits_only(const KpDev& d, const EvalEnv& E,
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     return true;
 }
+
+}  // namespace KP_WNS
+using namespace KP_WNS;

@@ -12,6 +12,10 @@
 #include "kp_gosort.h"
 #include "kp_layout.h"
 
+// wave-count namespace (kp_layout.h KP_WNS): the 4-wave topology units and the 8-wave units hold distinct
+// definitions of the wave-shaped types (FfdShared, TeamBuf ...) and of every helper that uses them
+namespace KP_WNS {
+
 #ifdef KP_NO_TOPO
 #define KP_TOPO_ON 0  // A/B builds only (tools/ab_variants.sh): topology code compiled out
 #else
@@ -1865,3 +1869,5 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
     }
 }
 
+}  // namespace KP_WNS
+using namespace KP_WNS;

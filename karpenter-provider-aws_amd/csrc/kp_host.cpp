@@ -1671,6 +1671,9 @@ static kp_status topo_build(kp_ctx* c, const kp_solve_input* in, const std::vect
                     idents[id] = ident;
                     by_ident.emplace_back();
                 }
+                // a pod whose terms repeat an identity owns the group its first such term creates (the later ones
+                // only AddOwner): one entry per class
+                if (!by_ident[ident].empty() && ents[by_ident[ident].back()].cls == i) continue;
                 TEnt e;
                 e.cls = i;
                 e.sig = std::move(sig);
@@ -1723,14 +1726,11 @@ static kp_status topo_build(kp_ctx* c, const kp_solve_input* in, const std::vect
                     if (ents[e].cls < C0 && pos[ents[e].cls] != INT64_MAX && (b < 0 || pos[ents[e].cls] < pos[ents[b].cls])) b = e;
                 return b;
             };
-            // variants need equal selection (Counts) and one semantics per class; inverse and affinity groups have no
-            // node filter or minDomains, so their semantics differ only in selection
+            // variants need equal selection (Counts); inverse and affinity groups have no node filter or minDomains, so
+            // their semantics differ only in selection
             auto variants_ok = [&]() {
-                for (int e : es) {
+                for (int e : es)
                     if (ents[e].g.inverse || ents[e].g.type != KP_TOPO_SPREAD || ents[e].g.sel != ents[es[0]].g.sel) return false;
-                    for (int f : es)
-                        if (ents[f].cls == ents[e].cls && ents[f].sig != ents[e].sig) return false;
-                }
                 return true;
             };
             if (!one) {

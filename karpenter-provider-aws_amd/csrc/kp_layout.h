@@ -33,6 +33,10 @@
 #ifndef KP_NWAVES_TOPO
 #define KP_NWAVES_TOPO 4             // waves of the topology instantiations
 #endif
+// the FFD headers' namespace per wave count (kp_w8, kp_w4): one definition per name across the kp_ffd_*.hip units
+#define KP_WNS_CAT2(n) kp_w##n
+#define KP_WNS_CAT(n) KP_WNS_CAT2(n)
+#define KP_WNS KP_WNS_CAT(KP_NWAVES)
 #define KP_LDS_AXES 6                // allocatable axes staged in LDS
 #define KP_MAX_SCR_WORDS 64          // value-bitset words of one class's keys (per-wave LDS scratch)
 #define KP_MAX_MIN_WORDS 64          // value bitset for a minValues distinct count (4096 values)

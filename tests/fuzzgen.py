@@ -487,6 +487,22 @@ def add_shared_identities(rng, prob, n_families=None, p_move=0.5):
     return prob
 
 
+def add_relaxed_shared(rng, prob, p_family=0.7):
+    """Shared identities that only relaxation creates: each family of add_shared_identities gets ORed required
+    node-affinity terms [instance-category In [zz]] (no type) then zone In [a per-class subset]; every pod relaxes the
+    first term away, and the relaxed spreads' node filters (the zone term alone) hash equal while their values differ.
+    Topology.Update creates that group from the first pod to relax (the device: variant groups, KpDev.late_sib)."""
+    zones = sorted({o.zone for it in prob.catalog for o in it.offerings})
+    nothing = [Requirement(AWS + "instance-category", "In", ["zz"])]
+    for fam in getattr(prob, "shared_families", []):
+        if rng.random() >= p_family:
+            continue
+        for c in fam:
+            sub = sorted(set(rng.choice(zones, size=int(rng.integers(1, 3))).tolist()))
+            prob.classes[c].required_terms = [list(nothing), [Requirement(ZONE, "In", sub)]]
+    return prob
+
+
 def fuzz_shared_identity_problem(catalog, seed, n_pods=200, n_existing=0):
     """fuzz_topology_problem (or its cluster variant with existing nodes and bound pods) plus add_shared_identities."""
     if n_existing:

@@ -375,3 +375,14 @@ def test_fuzz_shared_identity(ctx, golden, seed):
     sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=160, replace=False))]
     same(ctx, fuzzgen.fuzz_shared_identity_problem(sub, seed, n_pods=int(rng.integers(80, 300)),
                                                    n_existing=(seed % 2) * 20))
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_fuzz_shared_identity_relaxed(ctx, golden, seed):
+    """fuzzgen.add_relaxed_shared on top: families whose shared spread identity only relaxation creates (variant
+    groups, the first relaxation births its own) next to families whose first input pod decides."""
+    rng = np.random.Generator(np.random.PCG64(seed + 700))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=160, replace=False))]
+    prob = fuzzgen.fuzz_shared_identity_problem(sub, seed + 700, n_pods=int(rng.integers(80, 300)),
+                                                n_existing=(seed % 2) * 20)
+    same(ctx, fuzzgen.add_relaxed_shared(rng, prob))

@@ -1,5 +1,6 @@
 """GPU box: parity soak over many more seeds than the -m gpu suite runs — device vs oracle on the round's new shapes
-(wide reservation catalogs, preference / topology interplay, relaxing topology, many groups, mutating consolidation).
+(wide reservation catalogs, preference / topology interplay, relaxing topology, many groups, mutating consolidation,
+shared topology identities).
 Prints one line per family: seeds run, mismatches (the first failing seeds).  Usage: python tools/soak.py [seeds]"""
 import os
 import sys
@@ -117,12 +118,43 @@ def fam_cons_host_domains(seed):
                           pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH))
 
 
+def fam_shared_solve(seed):
+    rng = np.random.Generator(np.random.PCG64(10100 + seed))
+    sub = [g[int(i)] for i in sorted(rng.choice(len(g), size=int(rng.integers(80, 300)), replace=False))]
+    prob = fuzzgen.fuzz_shared_identity_problem(sub, 10100 + seed, n_pods=int(rng.integers(80, 400)),
+                                                n_existing=(seed % 2) * int(rng.integers(4, 40)))
+    if seed % 3 == 0:
+        fuzzgen.add_relaxed_shared(rng, prob)
+    for pol in (abi.KP_PREFERENCE_RESPECT, abi.KP_PREFERENCE_IGNORE):
+        solve_case(prob, pol)
+
+
+def fam_shared_cons(seed):
+    rng = np.random.Generator(np.random.PCG64(10300 + seed))
+    sub = [g[int(i)] for i in sorted(rng.choice(len(g), size=int(rng.integers(60, 300)), replace=False))]
+    cp = fuzzgen.fuzz_shared_identity_consolidation(sub, 10300 + seed, n_nodes=int(rng.integers(4, 50)),
+                                                    n_pods=int(rng.integers(20, 200)), pending_owner=seed % 2 == 0)
+    if seed % 3 == 0:
+        fuzzgen.add_relaxed_shared(rng, cp.cluster)
+    c = pctx[abi.KP_PREFERENCE_RESPECT]
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        assert_probes_equal(device_probes(c, cp, mode),
+                            pyoracle.consolidate(cp, mode, preference_policy=abi.KP_PREFERENCE_RESPECT))
+
+
+FAMILIES = [("wide reservations (Solve)", fam_wide_resv), ("topology x preferences (Solve, 2 policies)", fam_topo_pref),
+            ("relaxing topology (Solve, 2 policies)", fam_relaxing), ("many groups (Solve)", fam_many_groups),
+            ("mutators x topology (consolidation)", fam_cons_mut_topo),
+            ("wide reservations (consolidation)", fam_cons_wide_resv),
+            ("hostname podDomains (consolidation)", fam_cons_host_domains),
+            ("shared topology identities (Solve, 2 policies)", fam_shared_solve),
+            ("shared topology identities (consolidation)", fam_shared_cons)]
+
 if __name__ == "__main__":
-    for name, fn in [("wide reservations (Solve)", fam_wide_resv), ("topology x preferences (Solve, 2 policies)", fam_topo_pref),
-                     ("relaxing topology (Solve, 2 policies)", fam_relaxing), ("many groups (Solve)", fam_many_groups),
-                     ("mutators x topology (consolidation)", fam_cons_mut_topo),
-                     ("wide reservations (consolidation)", fam_cons_wide_resv),
-                     ("hostname podDomains (consolidation)", fam_cons_host_domains)]:
+    only = os.environ.get("SOAK_FAMILIES")  # comma-separated substrings of family names
+    for name, fn in FAMILIES:
+        if only and not any(x in name for x in only.split(",")):
+            continue
         t = time.time()
         bad = []
         for seed in range(N):
