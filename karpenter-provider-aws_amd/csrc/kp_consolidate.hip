@@ -980,7 +980,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
             uint32_t cflags = 0;
             if (TOPO) {
                 cflags = __builtin_amdgcn_readfirstlane(d.cls_flags[c]);
-                if ((cflags & CF_TOPO) && S.CC.cls != c) fill_class_cache(d, c, S.CC, lane, 64, TOPO ? S.born : 0ull);
+                if ((cflags & CF_TOPO) && S.CC.cls != c) fill_class_cache<TOPO>(d, c, S.CC, lane, 64, TOPO ? S.born : 0ull);
             }
             const bool tcons = TOPO && (cflags & CF_TOPO_CONS);
             const int xs = tcons ? 0 : xstart;
@@ -1031,7 +1031,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
             const long long cn0 = prof ? __builtin_amdgcn_s_memtime() : 0;
             const int64_t* preq = d.pod_req + (size_t)p * R;
             if (n_nc == 1) {  // NodeClaim.Add on the in-flight NodeClaim
-                if (S.CC.cls != c) fill_class_cache(d, c, S.CC, lane, 64, TOPO ? S.born : 0ull);
+                if (S.CC.cls != c) fill_class_cache<TOPO>(d, c, S.CC, lane, 64, TOPO ? S.born : 0ull);
                 EvalIn a;
                 a.Ahdr = nch;
                 a.Aw = ncw;
@@ -1085,7 +1085,7 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
                     uint64_t o = (lane < TW && d.tmpl_ok[j]) ? d.tmpl_opts[(size_t)j * TW + lane] : 0;
                     o = limit_filter_rem(d, j, o, rem, lane);
                     if (!ballot(o != 0)) continue;
-                    if (S.CC.cls != c) fill_class_cache(d, c, S.CC, lane, 64, TOPO ? S.born : 0ull);
+                    if (S.CC.cls != c) fill_class_cache<TOPO>(d, c, S.CC, lane, 64, TOPO ? S.born : 0ull);
                     EvalIn a;
                     a.Ahdr = d.cls_hdr + (size_t)(d.C + j) * K;
                     a.Aw = d.cls_words + (size_t)(d.C + j) * d.DW;

@@ -175,7 +175,9 @@ __device__ __forceinline__ int topo_variant(const KpDev& d, int g, uint64_t born
     return m ? d.late_grp[__ffsll((unsigned long long)m) - 1] : g;
 }
 
-// born: the late topology groups created so far (routes a constraint on a variant group to the born variant)
+// born: the late topology groups created so far (routes a constraint on a variant group to the born variant).  TOPO:
+// the caller's instantiation has topology groups (without, their lists are not filled: G = 0)
+template <bool TOPO = false>
 __device__ inline void fill_class_cache(const KpDev& d, int c, ClassCache& CC, int tid, int nthr, uint64_t born = 0) {
     const int k0 = d.cls_koff[c], nck = d.cls_koff[c + 1] - k0;
     for (int i = tid; i < nck; i += nthr) {
@@ -209,8 +211,8 @@ __device__ inline void fill_class_cache(const KpDev& d, int c, ClassCache& CC, i
         if (d.cls_kneutral)
             for (int i = 0; i < nck; i++) kn |= d.cls_kneutral[k0 + i] ? (1u << i) : 0u;
         CC.kneutral = kn;
-        CC.ntc = (c < d.C && d.G > 0) ? d.cls_tcoff[c + 1] - d.cls_tcoff[c] : 0;
-        CC.ntr = (c < d.C && d.G > 0) ? d.cls_troff[c + 1] - d.cls_troff[c] : 0;
+        CC.ntc = (TOPO && c < d.C && d.G > 0) ? d.cls_tcoff[c + 1] - d.cls_tcoff[c] : 0;
+        CC.ntr = (TOPO && c < d.C && d.G > 0) ? d.cls_troff[c + 1] - d.cls_troff[c] : 0;
     }
     __syncthreads();
     if (tid < 5) {
@@ -221,7 +223,7 @@ __device__ inline void fill_class_cache(const KpDev& d, int c, ClassCache& CC, i
         CC.role[tid] = idx;
     }
     // topology group lists with the class-key index of each group's key
-    if (tid < CC.ntc + CC.ntr) {
+    if (TOPO && tid < CC.ntc + CC.ntr) {
         const bool cons = tid < CC.ntc;
         const int e = cons ? d.cls_tc[d.cls_tcoff[c] + tid] : d.cls_tr[d.cls_troff[c] + tid - CC.ntc];
         const int4 info = d.tg_info[e & 0x3FFFFFFF];

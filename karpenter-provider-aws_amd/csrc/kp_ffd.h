@@ -1326,7 +1326,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
             // ExistingNode.Add in scheduling order: tolerations + Compatible (XT) and headroom, then the requirement
             // merge and Topology.AddRequirements on the node's own domains; the first node that accepts takes the pod
             // and Topology.Record counts it there.  Counts change with every placement, so nothing is memoised.
-            if (S.cls_fill) fill_class_cache(d, S.cur_cls, S.CC, tid, nthr, S.born);
+            if (S.cls_fill) fill_class_cache<TOPO>(d, S.cur_cls, S.CC, tid, nthr, TOPO ? S.born : 0ull);
             __syncthreads();
             if (wave == 0) {
                 const int placed = existing_topo_scan(d.self, S, pod, lane);
@@ -1445,7 +1445,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
         long long c_ev0 = 0;
         {
             const long long cf0 = (d.profile && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
-            if (S.cls_fill) fill_class_cache(d, S.cur_cls, S.CC, tid, nthr, S.born);
+            if (S.cls_fill) fill_class_cache<TOPO>(d, S.cur_cls, S.CC, tid, nthr, TOPO ? S.born : 0ull);
             if (d.profile && tid == 0) {
                 c_ev0 = __builtin_amdgcn_s_memtime();
                 S.st[ST_SLOW_WHY + 10] += c_ev0 - cf0;

@@ -35,6 +35,26 @@ class Kat:
     extra: dict = field(default_factory=dict)
 
 
+class Cat(list):
+    """A catalog list that remembers how catalog.fake_catalog built it: native_parts = [(fixtures, kwargs)] per
+    concatenated part (None: not an envtest build), so tests/test_gpu_ingest.py builds the same catalog through the
+    library's ingestion path (kp_catalog_build)."""
+    native_parts = None
+
+    def __add__(self, other):
+        out = Cat(list.__add__(self, other))
+        a, b = self.native_parts, getattr(other, "native_parts", None)
+        out.native_parts = a + b if a is not None and b is not None else None
+        return out
+
+
+def envtest(fx, **kw):
+    """catalog.fake_catalog(fx=fx, **kw) as a Cat (kw: opts, ice, spot_prices)"""
+    c = Cat(catalog.fake_catalog(fx=fx, **kw))
+    c.native_parts = [(fx, dict(kw))]
+    return c
+
+
 CASES: List[Callable] = []
 
 
@@ -121,7 +141,7 @@ def make_instances(fx, names_=None, vcpus=None, spot_prices=None):
                       "memory_mib": 8192, "max_enis": 3, "ipv4_per_eni": 10, "default_card": 0, "cards": [3]})
     fxc = dict(fx)
     fxc["fake"] = {"instance_types": infos, "offerings": [[i["name"], Z1A] for i in infos]}
-    return catalog.fake_catalog(fx=fxc, spot_prices=spot_prices)
+    return envtest(fxc, spot_prices=spot_prices)
 
 
 def unique_families(fx, n):
@@ -197,8 +217,8 @@ def _all_scheduled(prob, res, reqs):
 @case
 def labels_individual(fx):
     """Every well-known label as its own nodeSelector; all pods schedule (default + windows NodePools)."""
-    lin = catalog.fake_catalog(fx=fx)
-    win = catalog.fake_catalog(fx=fx, opts=catalog.TypeOptions(ami_family="Windows2022"))
+    lin = envtest(fx)
+    win = envtest(fx, opts=catalog.TypeOptions(ami_family="Windows2022"))
     cat = lin + win
     nps = [synth.default_nodepool("default", instance_types=list(range(len(lin)))),
            synth.default_nodepool("windows", instance_types=list(range(len(lin), len(cat))))]
@@ -217,7 +237,7 @@ def labels_individual(fx):
 
 @case
 def labels_combined(fx):
-    cat = catalog.fake_catalog(fx=fx)
+    cat = envtest(fx)
     prob = problem(cat, [synth.default_nodepool()], [PodClass(sel_map(G4DN_LABELS))], [(0, {})])
 
     def check(prob, res, reqs):
@@ -229,7 +249,7 @@ def labels_combined(fx):
 
 @case
 def labels_accelerator(fx):
-    cat = catalog.fake_catalog(fx=fx)
+    cat = envtest(fx)
     prob = problem(cat, [synth.default_nodepool()], [PodClass(sel_map(INF2_LABELS))], [(0, {})])
 
     def check(prob, res, reqs):
@@ -261,7 +281,7 @@ def spot_cheaper_than_cheapest_od(fx):
 
 @case
 def metal_kept_with_min_values(fx):
-    cat = catalog.fake_catalog(fx=fx)
+    cat = envtest(fx)
     np_ = model.NodePool("default", requirements=[Requirement(CAPACITY_TYPE, "In", ["spot"], 1)])
     prob = problem(cat, [np_], [PodClass()], [(0, {"cpu": "1"})])
 
@@ -273,7 +293,7 @@ def metal_kept_with_min_values(fx):
 
 @case
 def deprioritize_metal_and_gpu(fx):
-    cat = catalog.fake_catalog(fx=fx)
+    cat = envtest(fx)
     prob = problem(cat, [synth.default_nodepool()], [PodClass()], [(0, {"cpu": "1"})])
 
     def launch_check(cat, lreqs, lres):
@@ -287,7 +307,7 @@ def deprioritize_metal_and_gpu(fx):
 
 @case
 def launch_on_metal(fx):
-    cat = catalog.fake_catalog(fx=fx)
+    cat = envtest(fx)
     np_ = synth.default_nodepool(requirements=[Requirement(INSTANCE_TYPE, "Exists")])
     prob = problem(cat, [np_], [PodClass(sel(**{AWS + "instance-size": "metal"}))], [(0, {"cpu": "1"})])
 
@@ -302,7 +322,7 @@ def launch_on_metal(fx):
 
 @case
 def flex_instance_type(fx):
-    cat = catalog.fake_catalog(fx=fx)
+    cat = envtest(fx)
     prob = problem(cat, [synth.default_nodepool()], [PodClass(sel(**{AWS + "instance-capacity-flex": "true"}))],
                    [(0, {})])
 
@@ -314,7 +334,7 @@ def flex_instance_type(fx):
 
 @case
 def flex_disallowed(fx):
-    cat = catalog.fake_catalog(fx=fx)
+    cat = envtest(fx)
     np_ = synth.default_nodepool(requirements=[Requirement(AWS + "instance-capacity-flex", "NotIn", ["true"])])
     prob = problem(cat, [np_], [PodClass(sel(**{AWS + "instance-capacity-flex": "true"}))], [(0, {})])
 
@@ -327,7 +347,7 @@ def flex_disallowed(fx):
 # instancetype/suite_test.go — Insufficient Capacity Error cache (:2039-2215)
 # ----------------------------------------------------------------------------------------------------------------------
 def _inf2_pair(fx, ice):
-    cat = catalog.fake_catalog(fx=fx, ice=ice)
+    cat = envtest(fx, ice=ice)
     cls = [PodClass(sel(**{ZONE: Z1A}))]
     return cat, problem(cat, [synth.default_nodepool()], cls, [(0, {"aws.amazon.com/neuron": "1"})] * 2)
 
@@ -363,7 +383,7 @@ def ice_inf2_first_attempt(fx):
 
 
 def _zone_fallback(fx, typ, resource, lines):
-    cat = catalog.fake_catalog(fx=fx, ice={("on-demand", typ, Z1A)})
+    cat = envtest(fx, ice={("on-demand", typ, Z1A)})
     prob = problem(cat, [synth.default_nodepool()], [PodClass(sel(**{INSTANCE_TYPE: typ}))], [(0, {resource: "1"})])
 
     def check(prob, res, reqs):
@@ -388,7 +408,7 @@ def ice_zone_fallback_dl1(fx):
 
 
 def _m5_pair(fx, ice):
-    cat = catalog.fake_catalog(fx=fx, ice=ice)
+    cat = envtest(fx, ice=ice)
     np_ = synth.default_nodepool(requirements=[Requirement(INSTANCE_TYPE, "In", ["m5.large", "m5.xlarge"])])
     return cat, problem(cat, [np_], [PodClass(sel(**{ZONE: Z1A}))], [(0, {"cpu": "1"})] * 2)
 
@@ -415,7 +435,7 @@ def ice_smaller_first_attempt(fx):
 
 
 def _expiry(fx, ice):
-    cat = catalog.fake_catalog(fx=fx, ice=ice)
+    cat = envtest(fx, ice=ice)
     return cat, problem(cat, [synth.default_nodepool()], [PodClass(sel(**{INSTANCE_TYPE: "inf2.24xlarge"}))],
                         [(0, {"aws.amazon.com/neuron": "2"})])
 
@@ -441,9 +461,9 @@ def ice_expiry_expired(fx):
 
 @case
 def ice_spot_falls_back_to_od(fx):
-    fake = catalog.fake_catalog(fx=fx)
+    fake = envtest(fx)
     ice = {("spot", it.name, Z1A) for it in fake}
-    cat = catalog.fake_catalog(fx=fx, ice=ice)
+    cat = envtest(fx, ice=ice)
     np_ = model.NodePool("default", requirements=[Requirement(CAPACITY_TYPE, "In", ["spot", "on-demand"]),
                                                   Requirement(ZONE, "In", [Z1A])])
     prob = problem(cat, [np_], [PodClass()], [(0, {})])
@@ -461,7 +481,7 @@ def ice_spot_falls_back_to_od(fx):
 # ----------------------------------------------------------------------------------------------------------------------
 @case
 def capacity_type_default_od(fx):
-    cat = catalog.fake_catalog(fx=fx)
+    cat = envtest(fx)
     prob = problem(cat, [synth.default_nodepool()], [PodClass()], [(0, {})])
 
     def launch_check(cat, lreqs, lres):
@@ -472,7 +492,7 @@ def capacity_type_default_od(fx):
 
 @case
 def capacity_type_spot_when_flexible(fx):
-    cat = catalog.fake_catalog(fx=fx)
+    cat = envtest(fx)
     prob = problem(cat, [model.NodePool("default", requirements=[Requirement(CAPACITY_TYPE, "In",
                                                                              ["spot", "on-demand"])])],
                    [PodClass()], [(0, {})])
@@ -484,7 +504,7 @@ def capacity_type_spot_when_flexible(fx):
 
 
 def _m5_spot_only_1a(fx, zone_req):
-    cat = catalog.fake_catalog(fx=fx, spot_prices={("m5.large", Z1A): 0.004})
+    cat = envtest(fx, spot_prices={("m5.large", Z1A): 0.004})
     reqs = [Requirement(CAPACITY_TYPE, "In", ["spot"]), Requirement(INSTANCE_TYPE, "In", ["m5.large"])]
     if zone_req:
         reqs.append(Requirement(ZONE, "In", [Z1B]))
@@ -680,6 +700,29 @@ def build(fx, mk):
 
 def ids():
     return [c.__name__ for c in CASES]
+
+
+# the cases over the envtest catalog (pkg/fake EC2 records: an input of the ingestion path, kp_catalog_build); the e2e
+# cases run over the golden-doc catalog, whose labels and allocatable come from the doc, not from EC2 records
+ENVTEST_CASES = [c for c in CASES if not c.__name__.startswith("e2e_")]
+
+
+def native_catalog(cat):
+    """The same catalog built by the library's ingestion path: (NativeCatalog views, their InstanceTypes concatenated),
+    or None for a catalog not built by envtest()."""
+    from kpsim import ingest
+    parts = getattr(cat, "native_parts", None)
+    if parts is None:
+        return None
+    nats, types = [], []
+    for pfx, kw in parts:
+        kw = dict(kw)
+        opts = kw.pop("opts", None)
+        nc = ingest.NodeClass(ami_family=opts.ami_family) if opts is not None else None
+        nat = ingest.fake_catalog(pfx, nodeclass=nc, **kw)
+        nats.append(nat)
+        types += nat.instance_types()
+    return nats, types
 
 
 def clone_problem(prob):

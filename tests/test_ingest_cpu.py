@@ -317,3 +317,16 @@ def test_oracle_solve_over_ingested_view(fx, fam):
     b = parity.run_oracle(prob, model.CatalogView(py))
     parity.assert_same(a, b)
     assert a[0].n_nodeclaims > 0
+
+
+def test_envtest_kat_catalogs_through_ingestion(fx):
+    """Every known-answer case over the envtest catalog (kat_cases.ENVTEST_CASES) rebuilds its catalog — ICE marks, spot
+    prices, MakeInstances types, the Windows NodeClass — through kp_catalog_build, equal to the host builder's
+    (labels, capacity, allocatable, offerings); test_gpu_ingest.py then runs each through Solve on the device."""
+    import kat_cases as KC
+    from test_gpu_ingest import _same_catalog
+    for mk in KC.ENVTEST_CASES:
+        k = mk(fx)
+        got = KC.native_catalog(k.problem.catalog)
+        assert got is not None, mk.__name__
+        assert _same_catalog(got[1], k.problem.catalog), mk.__name__
