@@ -520,6 +520,7 @@ struct kp_ctx {
     bool ro_ok = true;
     std::string ro_why;  // why the reserved offerings do not fit ResvTab (Solve / consolidation refuse with it)
     bool wide_resvid = false;                // the reservation-id label has > 64 values (no type value masks for it)
+    bool resvid_rows = false;                // ... and every type's label is its ResvTab rows' IDs (KF_RESV_ROWS)
     // reserved offerings (ResvTab rows, kp_layout.h; padding rows have type -1 and offering -1)
     std::vector<int32_t> ro_type, ro_zone, ro_zid, ro_rid, ro_ridv, ro_rtype;
     std::vector<int32_t> ro_rid_vid;         // [nrid] reservation-id value id of each reservation
@@ -1036,6 +1037,7 @@ static kp_status catalog_upload_one(kp_ctx* ctx, const kp_catalog_view* v, uint6
         if (c->ro_off[i] >= 0 && avail[c->ro_off[i]]) c->ro_avail[i / 64] |= 1ull << (i % 64);
     // multi-valued keys: value masks (<= 64 values)
     c->wide_resvid = false;
+    c->resvid_rows = false;
     c->cat_kflags.assign(Kc, 0);
     c->cat_multi.assign(Kc, -1);
     c->n_multi = 0;
@@ -1047,10 +1049,27 @@ static kp_status catalog_upload_one(kp_ctx* ctx, const kp_catalog_view* v, uint6
             if (c->cat.keys[k].vals.size() > 64) {
                 // the Solve tables hold a multi-valued label as a 64-bit value mask; the launch path has no such limit.
                 // The reservation-id label (one value per capacity reservation) is exempt: reserved offerings are
-                // evaluated through ResvTab, and only a pod or NodePool requirement on the key would need its type
-                // masks (kp_solve_prepare refuses that: wide_resvid)
+                // evaluated through ResvTab, and a type's label values are its ResvTab rows' reservation IDs, so a
+                // pod or NodePool requirement on the key is tested per type over those rows (KF_RESV_ROWS, eval_wave)
+                // instead of a 64-bit value mask — when every type's label is exactly its rows' IDs (else refused:
+                // wide_resvid without resvid_rows)
                 if (k == c->key_resvid && c->ro_ok) {
                     c->wide_resvid = true;
+                    bool rows_ok = true;
+                    for (int t = 0; t < T && rows_ok; t++) {
+                        const uint32_t tr = c->type_ro[t];
+                        const int r0 = (int)(tr >> 16) * 64 + (int)((tr >> 8) & 0xFF), n = (int)(tr & 0xFF);
+                        std::set<int> rows;
+                        for (int r = 0; r < n; r++) rows.insert(c->ro_ridv[r0 + r]);
+                        const int8_t ls = st[(size_t)t * Kc + k];
+                        if (ls == KP_LABEL_IN) {
+                            const std::vector<int>& lv = tv[(size_t)t * Kc + k];
+                            rows_ok = std::set<int>(lv.begin(), lv.end()) == rows;
+                        } else {
+                            rows_ok = rows.empty();
+                        }
+                    }
+                    c->resvid_rows = rows_ok;  // the Solve's key layout flags it (KF_RESV_ROWS); no mask, no cat flag
                     continue;
                 }
                 c->solve_unsupported = k == c->key_resvid && !c->ro_why.empty()
@@ -1998,12 +2017,19 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
         for (auto& kv : creq[i])
             if (kv.second.has_min) return fail(ctx, KP_E_INVALID, "pod requirements cannot carry minValues");
     if (c->wide_resvid) {  // see catalog_upload_one: no per-type value masks for a reservation-id label this wide
-        for (int i = 0; i < C; i++)
+        for (int i = 0; i < C && !c->resvid_rows; i++)
             if (creq[i].count(c->key_resvid))
-                return fail(ctx, KP_E_UNSUPPORTED, "a pod requirement on capacity-reservation-id over more than 64 reservations");
-        for (int j = 0; j < NT; j++)
-            if (treq[j].count(c->key_resvid))
-                return fail(ctx, KP_E_UNSUPPORTED, "a NodePool requirement on capacity-reservation-id over more than 64 reservations");
+                return fail(ctx, KP_E_UNSUPPORTED, "a pod requirement on capacity-reservation-id over more than 64 reservations "
+                                                   "whose labels are not the types' reserved offerings");
+        for (int j = 0; j < NT; j++) {
+            auto it = treq[j].find(c->key_resvid);
+            if (it == treq[j].end()) continue;
+            if (!c->resvid_rows)
+                return fail(ctx, KP_E_UNSUPPORTED, "a NodePool requirement on capacity-reservation-id over more than 64 "
+                                                   "reservations whose labels are not the types' reserved offerings");
+            if (it->second.has_min)  // minValues counts distinct values per type through 64-bit masks
+                return fail(ctx, KP_E_UNSUPPORTED, "minValues on capacity-reservation-id over more than 64 reservations");
+        }
     }
     TopoHost th;
     {
@@ -2077,6 +2103,9 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
             kflags[k] |= c->cat_kflags[k];
             kcat[k] = k;
             kmulti[k] = c->cat_multi[k];
+        } else if (k == c->key_resvid && c->resvid_rows) {  // values per type: its ResvTab rows (DoesNotExist: dne_mask)
+            kflags[k] |= KF_RESV_ROWS;
+            kcat[k] = k;
         }
         nval[k] = (int)kd.vals.size();
         nw[k] = std::max(1, (nval[k] + 63) / 64);

@@ -77,6 +77,7 @@
 #define KF_WELL_KNOWN 1u             // AllowUndefinedWellKnownLabels
 #define KF_CAT_SINGLE 2u             // catalog label key, every type has <= 1 value
 #define KF_CAT_MULTI 4u              // catalog label key with a multi-valued type (zone, capacity-type, ...)
+#define KF_RESV_ROWS 8u              // the reservation-id label beyond 64 values: a type's values are its ResvTab rows' IDs
 
 // type value ids for single-valued keys
 #define VAL_DNE 0xFFFFu              // label DoesNotExist on the type

@@ -539,6 +539,34 @@ def fuzz_shared_identity_consolidation(catalog, seed, n_nodes=30, n_pods=160, pe
     return cp
 
 
+def add_reservation_id_requirements(rng, prob, p_class=0.35, p_pool=0.5):
+    """Pods and NodePools that select capacity reservations by ID (website odcrs.md:53-57: karpenter.k8s.aws/
+    capacity-reservation-id as a scheduling constraint): In / NotIn 1-4 IDs of the catalog, Exists, DoesNotExist, on
+    some pod classes and NodePools (those NodePools also allow capacity-type reserved)."""
+    ids = sorted({o.reservation_id for it in prob.catalog for o in it.offerings if o.capacity_type == "reserved"})
+    if not ids:
+        return prob
+    RID = AWS + "capacity-reservation-id"
+
+    def req():
+        u = rng.random()
+        if u < 0.55:
+            return Requirement(RID, "In", sorted(set(rng.choice(ids, size=int(rng.integers(1, 5))).tolist())))
+        if u < 0.75:
+            return Requirement(RID, "NotIn", sorted(set(rng.choice(ids, size=int(rng.integers(1, 4))).tolist())))
+        return Requirement(RID, "Exists" if u < 0.9 else "DoesNotExist")
+    for pc in prob.classes:
+        if rng.random() < p_class:
+            pc.requirements = list(pc.requirements) + [req()]
+    for np_ in prob.nodepools:
+        if rng.random() < p_pool:
+            np_.requirements = list(np_.requirements) + [req()]
+            for r in np_.requirements:
+                if r.key == CAPACITY_TYPE and r.op == "In":
+                    r.values = sorted(set(r.values) | {"reserved"})
+    return prob
+
+
 def fuzz_preference_consolidation(catalog, seed, n_nodes=30, n_pods=160, n_bound=30, all_spot=False, best_effort=False,
                                   zone_min=False):
     """fuzz_consolidation over pods with preferences to relax (add_preferences), pods of those classes bound to random

@@ -66,6 +66,15 @@ def main():
     run("resv_per_type_70", lambda: solve_prep(synth.config2(n_pods=50, catalog=cat)))
     wide = synth.wide_reservation_catalog(golden, 1100, max_per_type=4)
     run("resv_over_max", lambda: solve_prep(synth.config2(n_pods=50, catalog=wide)))
+    # reservation-ID selections over more than 64 reservations: accepted (KF_RESV_ROWS); minValues on the key refused
+    cat200 = synth.wide_reservation_catalog(golden, 200)
+    prob = synth.config5(n_pods=300, catalog=cat200)
+    fuzzgen.add_reservation_id_requirements(np.random.Generator(np.random.PCG64(5)), prob, p_class=1.0, p_pool=1.0)
+    run("resv_id_selection", lambda: solve_prep(prob))
+    prob2 = synth.config5(n_pods=300, catalog=cat200)
+    prob2.nodepools[0].requirements = list(prob2.nodepools[0].requirements) + [
+        model.Requirement(model.RESERVATION_ID, "Exists", [], 2)]
+    run("resv_id_min_values", lambda: solve_prep(prob2))
     ctx.close()
     print(json.dumps(out))
 

@@ -112,17 +112,50 @@ def test_wide_consolidation_command(ctx, golden):
     assert n_replace >= 4 and n_held >= 3
 
 
-def test_wide_reservation_id_requirement_refused(ctx, cat200):
-    """A pod requirement on karpenter.k8s.aws/capacity-reservation-id is refused when the catalog's reservation IDs
-    exceed one 64-value word (the key is kept out of the requirement digests then)."""
-    prob = synth.config5(n_pods=200, catalog=cat200)
+def test_wide_reservation_id_requirement(ctx, cat200):
+    """A pod requirement on karpenter.k8s.aws/capacity-reservation-id over a catalog with more reservation IDs than one
+    64-value word: the key's per-type values are the type's ResvTab rows (KF_RESV_ROWS), bit-exact with the oracle."""
+    prob = synth.config5(n_pods=2000, catalog=cat200)
     rid = next(o.reservation_id for it in cat200 for o in it.offerings if o.capacity_type == "reserved")
     prob.classes[0].requirements = list(prob.classes[0].requirements) + [
         model.Requirement(model.RESERVATION_ID, "In", [rid])]
-    ctx.upload_catalog(model.CatalogView(cat200))
-    with pytest.raises(native.KpError) as e:
-        ctx.prepare(model.SolveInputView(prob))
-    assert e.value.status == abi.KP_E_UNSUPPORTED
+    cv = model.CatalogView(cat200)
+    dev = parity.run_device(ctx, prob, cv)
+    parity.assert_same(dev, parity.run_oracle(prob, cv))
+    placed = dev[0].pod_result[prob.pods.class_id == 0]
+    assert (placed >= 0).any()
+
+
+@pytest.mark.parametrize("n", [2000, 20000])
+def test_wide_reservation_id_selection_config5(ctx, cat200, n):
+    """config 5 over the 200-reservation catalog with pods and NodePools selecting reservations by ID (In / NotIn /
+    Exists / DoesNotExist; website odcrs.md:53-57), at 2k and 20k pods."""
+    prob = synth.config5(n_pods=n, catalog=cat200)
+    fuzzgen.add_reservation_id_requirements(np.random.Generator(np.random.PCG64(77 + n)), prob)
+    cv = model.CatalogView(cat200)
+    dev = parity.run_device(ctx, prob, cv)
+    parity.assert_same(dev, parity.run_oracle(prob, cv))
+    assert _held(dev[1]) > 0
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_wide_reservation_id_fuzz(ctx, golden, seed):
+    """wide_scarce_problem (65-700 reservations, capacity 0-3) with reservation-ID selections on pods and NodePools."""
+    prob = wide_scarce_problem(golden, 40 + seed)
+    fuzzgen.add_reservation_id_requirements(np.random.Generator(np.random.PCG64(4100 + seed)), prob)
+    cv = model.CatalogView(prob.catalog)
+    parity.assert_same(parity.run_device(ctx, prob, cv), parity.run_oracle(prob, cv))
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_wide_reservation_id_consolidation_fuzz(ctx, golden, seed):
+    """Consolidation probes and the command over 65-260 reservations with reservation-ID selections."""
+    cp = _wide_consolidation(golden, 60 + seed, full_cluster=seed % 2 == 0)
+    fuzzgen.add_reservation_id_requirements(np.random.Generator(np.random.PCG64(4200 + seed)), cp.cluster)
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        assert_probes_equal(device_probes(ctx, cp, mode), pyoracle.consolidate(cp, mode))
+    assert_commands_equal(device_command(ctx, cp, abi.KP_CONSOLIDATE_BOTH),
+                          pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH))
 
 
 def test_over_max_reserved_offerings_refused(ctx, golden):

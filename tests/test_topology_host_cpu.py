@@ -55,3 +55,10 @@ def test_reserved_offering_refusal_reasons(checks):
     """ResvTab limits name their cause: a type with more than 64 reservations, or more than 1,024 reserved offerings."""
     assert checks["resv_per_type_70"].startswith("KP_E_UNSUPPORTED") and "m5.large has more than 64" in checks["resv_per_type_70"]
     assert checks["resv_over_max"].startswith("KP_E_UNSUPPORTED") and "KP_MAX_RO" in checks["resv_over_max"]
+
+
+def test_reservation_id_selection_beyond_64(checks):
+    """pod and NodePool requirements on capacity-reservation-id over 200 reservations are accepted (per-type values
+    through ResvTab rows); minValues on that key is refused (distinct counts use 64-bit masks)"""
+    assert checks["resv_id_selection"] == "ok"
+    assert checks["resv_id_min_values"].startswith("KP_E_UNSUPPORTED") and "minValues" in checks["resv_id_min_values"]
