@@ -12,6 +12,7 @@ Rank 0 prints one JSON line.
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -150,7 +151,7 @@ def consolidation_leg(a, cat, local, rank, world, dist, barrier, headroom=None):
         "roofline": {"bound": "hbm", "kernel": "consolidate_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes": int(B),
                      "kernel_ms": float(km[1]),
-                     "traffic_per_launch": pmc_traffic("consolidate")},
+                     "traffic_per_launch": pmc_traffic("consolidate" if headroom is None else "consolidate_replace")},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -161,7 +162,7 @@ def consolidation_leg(a, cat, local, rank, world, dist, barrier, headroom=None):
         r2 = pyoracle.consolidate(cp, abi.KP_CONSOLIDATE_MULTI, n_threads=nthr)
         cpu_s += pyoracle.last_consolidate_seconds()
         out["cpu_baseline"] = {"value": cpu_s * 1e3, "unit": "ms", "candidates_per_s": (n_s + n_m) / cpu_s,
-                               "cores": nthr, "kind": "port",
+                               "cores": nthr, "cpu_model": cpu_model(), "kind": "port",
                                "sample": "oracle orc_consolidate (std::thread x %d) over the full pass: %.3f s of "
                                          "probes, timed inside the oracle (input parsing excluded)" % (nthr, cpu_s)}
         d1 = ctx.consolidate_execute(abi.KP_CONSOLIDATE_SINGLE, n_s)
@@ -269,7 +270,7 @@ def launch_leg(a, golden, local, rank, world, dist, barrier):
         t = time.perf_counter()
         stc, orc = pyoracle.launch_select(cv, sb, 60)
         cpu_s = max(1e-9, time.perf_counter() - t - parse_s)
-        out["cpu_baseline"] = {"value": n / cpu_s, "unit": "nodeclaims/s", "cores": 1, "kind": "port",
+        out["cpu_baseline"] = {"value": n / cpu_s, "unit": "nodeclaims/s", "cores": 1, "cpu_model": cpu_model(), "kind": "port",
                                "sample": "oracle orc_launch_select, 1 thread, first %d requests of the batch: %.2f s "
                                          "(catalog parsing, %.2f s, excluded)" % (n, cpu_s, parse_s)}
         dev = ctx.launch_select(sb, 60)
@@ -289,16 +290,32 @@ ROOFLINE_NOTE = ("the Solve is one serial chain run by ONE workgroup (8 waves on
                  "stage_cycles_per_pod breaks its time down")
 
 
+def cpu_model():
+    """The GPU box host's CPU model (lscpu "Model name", from /proc/cpuinfo), stated with every cpu_baseline."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.lower().startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
 def stage_cycles_per_pod(ctx, iv, out, n_pods):
     """One more kp_solve with KPSIM_PROFILE=1 (s_memtime stamps, after the timed region): the FFD kernel's shader-clock
     cycles per pod by stage (wave 0's fast loop and slice sort, the block's slow-path evaluations and templates, the
     topology prefilter setup / first-survivor scan), and the pods each path placed."""
+    prev = os.environ.get("KPSIM_PROFILE")
     os.environ["KPSIM_PROFILE"] = "1"
     try:
         ctx.solve(iv, out)
         cyc = dict(zip(FFD_COUNTERS, ctx.ffd_cycles()))
-    finally:
-        del os.environ["KPSIM_PROFILE"]
+    finally:  # a caller's own KPSIM_PROFILE (tools/profile_round.sh's stage run) stays for the later legs
+        if prev is None:
+            del os.environ["KPSIM_PROFILE"]
+        else:
+            os.environ["KPSIM_PROFILE"] = prev
     ctx.prepare(iv)
     out = {k: cyc[k] / n_pods for k in ("cyc_fast_loop", "cyc_sort", "cyc_slow_eval", "cyc_templates", "cyc_topo_setup",
                                         "cyc_topo_scan") if cyc.get(k)}
@@ -364,7 +381,9 @@ def solve_leg(a, cat, prob, metric, workload, cpu_sample, local, rank, world, di
         "nodeclaims": res.n_nodeclaims,
         "unschedulable": int((res.pod_result == -1).sum()),
         "roofline": {"bound": "hbm", "kernel": ffd_kernel_name(prob), "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes": int(B), "kernel_ms": float(kt[3])},
+                     "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes": int(B), "kernel_ms": float(kt[3]),
+                     "traffic": pmc_traffic({"ffd_topo_kernel": "ffd_topo", "ffd_resv_kernel": "ffd_resv"}.get(
+                         ffd_kernel_name(prob), "ffd"))},
         "solve_stats": {k: v for k, v in res.stats.items() if not k.startswith("ns_")},
         "ffd_counters": dict(zip(FFD_COUNTERS, ctx.ffd_cycles())),
         "cpu_baseline": None,
@@ -380,7 +399,8 @@ def solve_leg(a, cat, prob, metric, workload, cpu_sample, local, rank, world, di
         orc = pyoracle.solve(sample)
         cpu_s = oracle_solve_seconds(orc)
         what = "the full %d-pod workload" % sample.pods.n if full else "a seeded %d-pod subsample" % sample.pods.n
-        line["cpu_baseline"] = {"value": sample.pods.n / cpu_s, "unit": "pods/s", "cores": 1, "kind": "port",
+        line["cpu_baseline"] = {"value": sample.pods.n / cpu_s, "unit": "pods/s", "cores": 1, "cpu_model": cpu_model(),
+                                "kind": "port",
                                 "sample": "oracle (1 thread) on %s: %.2f s of Solve + Truncate "
                                           "(input parsing excluded)" % (what, cpu_s)}
         dev = parity.run_device(ctx, sample)
@@ -431,6 +451,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-consolidation", action="store_true")
     ap.add_argument("--no-consolidation-replace", action="store_true")
+    ap.add_argument("--no-config4", action="store_true", help="skip the config-4 consolidation pass (keep the replace leg)")
     ap.add_argument("--nodes", type=int, default=5000, help="config4 cluster size (consolidation leg)")
     ap.add_argument("--launch-batch", type=int, default=10_000, help="config5 launch batch (NodeClaims)")
     ap.add_argument("--no-launch", action="store_true")
@@ -518,7 +539,7 @@ def main():
     traffic = pmc_traffic("ffd")
 
     log("config2 solve leg done: %.1f ms/step" % (elapsed / a.steps * 1e3))
-    cons = None if a.no_consolidation else consolidation_leg(a, cat, local, rank, world, dist, barrier)
+    cons = None if (a.no_consolidation or a.no_config4) else consolidation_leg(a, cat, local, rank, world, dist, barrier)
     log("consolidation leg done")
     cons_r = None if (a.no_consolidation or a.no_consolidation_replace) else consolidation_leg(
         a, cat, local, rank, world, dist, barrier, headroom=0.02)
@@ -542,7 +563,7 @@ def main():
         cpu_s = oracle_solve_seconds(orc)
         what = ("the full %d-pod config2 workload" % sample.pods.n if full else
                 "a seeded %d-pod subsample of the config2 workload (same catalog, NodePools, classes)" % sample.pods.n)
-        cpu = {"value": sample.pods.n / cpu_s, "unit": "pods/s", "cores": 1, "kind": "port",
+        cpu = {"value": sample.pods.n / cpu_s, "unit": "pods/s", "cores": 1, "cpu_model": cpu_model(), "kind": "port",
                "sample": "oracle (C++ restatement of Solve, 1 thread) on %s: %.2f s of Solve + Truncate "
                          "(input parsing excluded)" % (what, cpu_s)}
         dev = parity.run_device(ctx, sample)

@@ -196,7 +196,7 @@ __device__ __forceinline__ bool topo_prefilter_pass(const KpDev& d, const FfdSha
 }
 
 // wave 0: the first slice position in [start, N) that has not rejected the shape, whose template's taints the class
-// tolerates (tol: bit j = template j) and that passes the topology prefilter (N if none).  Four 64-position chunks per
+// tolerates (tol: bit j = template j) and that passes the topology prefilter (N if none).  Two 64-position chunks per
 // round (KP_TSCAN_U) so the prefilter's global loads of 64 * KP_TSCAN_U NodeClaims overlap.
 #ifndef KP_TSCAN_U
 #define KP_TSCAN_U 2
