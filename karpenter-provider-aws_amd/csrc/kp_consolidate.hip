@@ -204,8 +204,12 @@ __device__ inline uint64_t commit_held(int32_t* rcap, uint64_t old, const WaveSc
 // MUT (FULL only): the pass has probes that reschedule a mutator's pod (KpCons::mut): such a probe runs serially over its
 // queue and applies ExistingNode.Add's requirement merge to its own copies of the nodes it changes (see KpCons).
 #define AXL(ai) _Pragma("unroll") for (int ai = 0; ai < (NA > 0 ? NA : KP_LDS_AXES); ai++) if (NA > 0 || ai < A)
-template <bool FULL, bool RESV = false, bool TOPO = false, int NA = 0, bool MUT = false>
-__device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
+// DevT / ConsT: KpDev / KpCons by value (the fast variant: its kernel arguments) or const references to the FULL
+// variant's device copies — a by-value copy of those, indexed dynamically (active_axes ...), went to scratch per lane
+// (1.3 KB per lane, 87 MB of scratch writes per replace-leg launch).
+template <bool FULL, bool RESV = false, bool TOPO = false, int NA = 0, bool MUT = false, class DevT = KpDev,
+          class ConsT = KpCons>
+__device__ __forceinline__ void consolidate_body(DevT d, ConsT k) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     ConsShared& S = *reinterpret_cast<ConsShared*>(smem);
     ReqHdr* nch = reinterpret_cast<ReqHdr*>(smem + k.off_hdr);
@@ -1478,8 +1482,8 @@ __device__ __forceinline__ void consolidate_body(KpDev d, KpCons k) {
 }
 
 // The fast variant takes its tables by value (kernel arguments).  The FULL variant takes them by pointer to device
-// copies: its body indexes them dynamically, so the compiler copies them to scratch, and with pointers that copy comes
-// after the check that lets an idle launch (the fast variant handed nothing over) exit at once.
+// copies and reads them through const references (no per-lane scratch copy); an idle launch (the fast variant handed
+// nothing over) exits at once.
 template <bool FULL, bool RESV = false, bool TOPO = false, int NA = 0>
 __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
     consolidate_body<FULL, RESV, TOPO, NA>(d, k);
@@ -1487,7 +1491,7 @@ __global__ __launch_bounds__(64) void consolidate_kernel(KpDev d, KpCons k) {
 template <bool RESV, bool TOPO, bool MUT = false>
 __global__ __launch_bounds__(64) void consolidate_full_kernel(const KpDev* __restrict__ dp, const KpCons* __restrict__ kp) {
     if (kp->no_fast != 1 && ld32(&kp->next_probe[2]) == 0) return;
-    consolidate_body<true, RESV, TOPO, 0, MUT>(*dp, *kp);
+    consolidate_body<true, RESV, TOPO, 0, MUT, const KpDev&, const KpCons&>(*dp, *kp);
 }
 
 // cmax0[w][ai]: the largest headroom on active axis ai over the nodes of chunk w (one wave per chunk; lanes past E and
