@@ -836,7 +836,7 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
         const uint32_t kf = CC.kflags[lane];
         if (!(O.flags & RF_DEF)) return;
         if (kf & (KF_CAT_SINGLE | KF_CAT_MULTI | KF_RESV_ROWS)) kill = !op_notin_or_dne(req_op(O.flags, cnt));
-        rrow = (kf & KF_RESV_ROWS) != 0;
+        rrow = RESV && (kf & KF_RESV_ROWS) != 0;  // only catalogs with reserved offerings (the RESV instantiations)
         if (kf & KF_CAT_MULTI) {
             kmul = CC.kmulti[lane];
             const int nv = CC.nval[lane] < 64 ? CC.nval[lane] : 64;
@@ -922,7 +922,28 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
                                         : (CC.kcat[i] >= 0 ? d.dne_mask[(size_t)CC.kcat[i] * TW + lane] : 0ull));
     }
     const uint64_t mm = ballot(kmul >= 0);
-    const uint64_t mrr = ballot(rrow);
+    const uint64_t mrr = RESV ? ballot(rrow) : 0ull;
+    if (RESV && mrr) {
+        // the reservation-id label beyond 64 values (rare; kept out of the type sweep below): a type's values are its
+        // ResvTab rows' IDs (none: the label is DoesNotExist, left to the dne elimination above)
+        const int i = __ffsll((unsigned long long)mrr) - 1;
+        const ReqHdr O = ws.hdr[i];
+        const uint64_t* ow = ws.words + CC.wsoff[i];
+        for (int w = 0; w < TW; w++) {
+            const uint64_t cw = rl64(myopt, w);
+            if (cw == 0) continue;
+            const int t = w * 64 + lane;
+            bool ok = true;
+            if ((cw >> lane) & 1ull) {
+                const uint32_t tr = d.type_ro[t < T ? t : 0];
+                const int r0 = (int)(tr >> 16) * 64 + (int)((tr >> 8) & 0xFFu), nr = (int)(tr & 0xFFu);
+                ok = nr == 0;
+                for (int r = 0; r < nr && !ok; r++) ok = req_has(d, CC.key[i], d.ro->ridv[r0 + r], O, ow);
+            }
+            const uint64_t m = ballot(ok);
+            if (lane == w) myopt &= m;
+        }
+    }
     EV_STAMP(1);
 
     // ---- offerings over zone × capacity-type slots ----
@@ -984,18 +1005,6 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
             const uint64_t tm = E.multi16 ? (uint64_t)E.multi16[m * E.astride + t]
                                           : d.multi_mask[(size_t)m * T + (t < T ? t : 0)];
             keep &= (tm == 0) | ((tm & am) != 0);
-        }
-        if (mrr && keep) {
-            // the reservation-id label beyond 64 values: the type's values are its ResvTab rows' IDs (none: the label
-            // is DoesNotExist, left to the dne elimination above)
-            const int i = __ffsll((unsigned long long)mrr) - 1;
-            const ReqHdr O = ws.hdr[i];
-            const uint64_t* ow = ws.words + CC.wsoff[i];
-            const uint32_t tr = d.type_ro[t < T ? t : 0];
-            const int r0 = (int)(tr >> 16) * 64 + (int)((tr >> 8) & 0xFFu), nr = (int)(tr & 0xFFu);
-            bool ok = nr == 0;
-            for (int r = 0; r < nr && !ok; r++) ok = req_has(d, CC.key[i], d.ro->ridv[r0 + r], O, ow);
-            keep &= ok;
         }
         if (need_off) {
             bool off = (E.avail[t] & mzc) != 0;
