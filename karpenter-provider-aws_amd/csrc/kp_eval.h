@@ -44,10 +44,6 @@ struct WaveScratch {
     int32_t n_minrel;
     int32_t minrel_k[KP_MAX_CLASS_KEYS];
     int32_t minrel_v[KP_MAX_CLASS_KEYS];
-    // TEAM evaluations whose join barrier this wave has passed (every wave of the block takes the same early rejects, so
-    // the count is block-uniform): the caller picks the TeamBuf by its parity, so two evaluations that reach the join
-    // back to back never share a buffer, whatever rejects came between them
-    int32_t team_joins;
 };
 
 // An unmet minValues key: Strict fails the Add; BestEffort records the relaxation (wave-uniform).
@@ -394,8 +390,8 @@ struct WitnessAcc {
 };
 
 // One evaluation shared by every wave of the block (TEAM): each wave sweeps the option words w ≡ rank (mod n); the
-// partial results meet here (double-buffered by the parity of WaveScratch::team_joins, the joins actually reached, so
-// one barrier per evaluation suffices).
+// partial results meet here (double-buffered by the parity of the joins actually reached — eval_wave's `joins`, which
+// every wave of the block counts alike since they take the same early rejects — so one barrier per evaluation suffices).
 struct TeamBuf {
     uint64_t nw[KP_TW_MAX];    // remaining options, by word (written by the word's wave)
     uint64_t any[KP_NWAVES];   // per wave: OR of its words
@@ -804,7 +800,8 @@ __device__ inline void existing_topo_commit(const KpDev& d, const ClassCache& CC
 // and one block barrier joins the partial sweeps; every wave ends with the same result in its ws.
 template <bool TOPO, bool RESV = false, bool STRICT = true, bool BE = true, bool CT = false, bool TEAM = false>
 __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, const ClassCache& CC, const EvalIn& a,
-                                          WaveScratch& ws, int lane, TeamBuf* tb = nullptr, int trank = 0, int tn = 1) {
+                                          WaveScratch& ws, int lane, TeamBuf* tb = nullptr, int trank = 0, int tn = 1,
+                                          int* joins = nullptr) {
     const int TW = d.TW, T = d.T;
     long long _t0 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
     if (a.prof && lane == 0) atomicAdd((unsigned long long*)&a.prof[ST_EV_CALLS - ST_EV_REQ], 1ull);
@@ -1033,7 +1030,7 @@ __device__ __forceinline__ bool eval_wave(const KpDev& d, const EvalEnv& E, cons
             tb->bt[trank] = wit.bt;
         }
         __syncthreads();
-        if (lane == 0) ws.team_joins++;
+        (*joins)++;  // the caller's count of the joins reached (wave-uniform, a register once inlined)
         newword = lane < TW ? tb->nw[lane] : 0ull;
         anyw = 0;
         for (int r = 0; r < tn; r++) {

@@ -643,7 +643,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
         d.pod_order[p] = -1;
     }
     for (int j = wave; j < d.NT; j += KP_NWAVES) limit_mask_update(d, j, lane);  // the NodePools' limits of this solve
-    if (lane == 0) S.ws[wave].team_joins = 0;
+    int tjoins = 0;  // TEAM evaluations whose join this wave passed (block-uniform): the TeamBuf parity
     if (PREF && d.relax_next)  // a previous execute may have relaxed pods: every pod starts from its input class
         for (int p = tid; p < P; p += nthr) {
             d.pod_cls[p] = d.pod_cls0[p];
@@ -1490,12 +1490,12 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 a.held = (RESV && d.resv_on) ? held_word(d, nc, lane) : 0ull;
                 // the buffer by the joins reached so far, not by candidate index: a candidate rejected before the join
                 // (no barrier) must not flip the parity
-                TeamBuf* const tb = &S.team[__builtin_amdgcn_readfirstlane(S.ws[wave].team_joins) & 1];
+                TeamBuf* const tb = &S.team[tjoins & 1];
                 const bool ok = (S.CC.flags & CF_TOPO_CONS)
                                     ? eval_wave<true, RESV, true, PREF, false, true>(d, E, S.CC, a, S.ws[wave], lane, tb,
-                                                                                     wave, KP_NWAVES)
+                                                                                     wave, KP_NWAVES, &tjoins)
                                     : eval_wave<false, RESV, true, PREF, false, true>(d, E, S.CC, a, S.ws[wave], lane,
-                                                                                      tb, wave, KP_NWAVES);
+                                                                                      tb, wave, KP_NWAVES, &tjoins);
                 if (wave == 0 && lane == 0) {
                     S.fastp[b][i] = 0;
                     S.acc[b][i] = ok;
@@ -1540,12 +1540,12 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 a.prof = (d.profile && wave == 0) ? &S.st[ST_EV_REQ] : nullptr;
                 a.host = d.E + nc;
                 a.held = (RESV && d.resv_on) ? held_word(d, nc, lane) : 0ull;
-                TeamBuf* const tb = &S.team[__builtin_amdgcn_readfirstlane(S.ws[wave].team_joins) & 1];
+                TeamBuf* const tb = &S.team[tjoins & 1];
                 const bool ok = (TOPO_ON && (S.CC.flags & CF_TOPO_CONS))
                                     ? eval_wave<true, RESV, true, PREF, false, true>(d, E, S.CC, a, S.ws[wave], lane, tb,
-                                                                                     wave, KP_NWAVES)
+                                                                                     wave, KP_NWAVES, &tjoins)
                                     : eval_wave<false, RESV, true, PREF, false, true>(d, E, S.CC, a, S.ws[wave], lane,
-                                                                                      tb, wave, KP_NWAVES);
+                                                                                      tb, wave, KP_NWAVES, &tjoins);
                 if (wave == 0 && lane == 0) {
                     S.fastp[0][0] = 0;
                     S.acc[0][0] = ok;

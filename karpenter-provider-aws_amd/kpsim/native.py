@@ -56,7 +56,8 @@ def load():
                                          C.c_int32]
     L.kp_consolidate_stats.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.c_int32]
     L.kp_consolidate_command.argtypes = [C.c_void_p, C.c_int32, C.POINTER(abi.kp_consolidation_command)]
-    L.kp_consolidate_replacement.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(abi.kp_consolidation_command)]
+    if hasattr(L, "kp_consolidate_replacement"):  # (absent from pre-round-5 libraries, A/B only)
+        L.kp_consolidate_replacement.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(abi.kp_consolidation_command)]
     L.kp_launch_select.argtypes = [C.c_void_p, C.c_int32, C.POINTER(abi.kp_launch_request), C.c_int32,
                                    C.POINTER(abi.kp_launch_result), C.POINTER(C.c_int32), C.c_int32,
                                    C.POINTER(C.c_int32), C.c_int32]
@@ -64,6 +65,8 @@ def load():
     L.kp_nodeclaim_labels.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_char_p, C.c_char_p, C.c_int32, C.c_char_p,
                                       C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     for f in EXPORTS:
+        if os.environ.get("KPSIM_LIB") and not hasattr(L, f):
+            continue  # A/B diagnostics: an older library without a later entry point (its callers are not used)
         if f not in ("kp_last_error", "kp_version", "kp_catalog_resource_name"):
             getattr(L, f).restype = C.c_int32
     _lib = L

@@ -17,7 +17,7 @@ for r in $(seq 1 $ROUNDS); do
     KPSIM_LIB=$PWD/$lib timeout -k 10 300 python bench.py $args > gpurun_out/ab_$n.json 2> gpurun_out/ab_$n.err || { tail -5 gpurun_out/ab_$n.err; exit 1; }
     python3 -c "
 import json; b=json.loads(open('gpurun_out/ab_$n.json').read().strip().splitlines()[-1])
-t=b.get('topology',{}).get('kernel_ms',{}).get('ffd'); v=b.get('reserved',{}).get('kernel_ms',{}).get('ffd')
+t=(b.get('topology') or {}).get('kernel_ms',{}).get('ffd'); v=(b.get('reserved') or {}).get('kernel_ms',{}).get('ffd')
 print('$r %-34s c2 ffd %.2f ms' % ('$n', b['kernel_ms']['ffd']), (' c3 ffd %.1f' % t) if t else '', (' c5 ffd %.1f' % v) if v else '', flush=True)"
   done
 done
