@@ -84,8 +84,8 @@ struct ClassCache {
     uint64_t dne[KP_MAX_CLASS_KEYS][KP_DNE_TW];
     uint32_t kneutral;          // class keys present only for topology narrowing (bit per class-key index)
     int ntc, ntr;               // topology groups constraining / recording the class
-    int tc[KP_MAX_TOPO];        // group | self << 30
-    int tc_ki[KP_MAX_TOPO];     // class-key index of a value-keyed group's key (-1 for hostname groups)
+    int tc[KP_CC_TC];           // the first KP_CC_TC constraining groups: group | self << 30 (the others: cls_tc)
+    int tc_ki[KP_CC_TC];        // class-key index of a value-keyed group's key (-1 for hostname groups)
     int tr[KP_CC_REC];          // the first KP_CC_REC recording groups (the others: rec_entry)
     int tr_ki[KP_CC_REC];       // class-key index of the group's key, -1 when the class does not constrain it
 };
@@ -228,8 +228,10 @@ __device__ inline void fill_class_cache(const KpDev& d, int c, ClassCache& CC, i
             for (int i = 0; i < nck; i++)
                 if (CC.key[i] == info.y) ki = i;
         if (cons) {
-            CC.tc[tid] = (e & ~0x3FFFFFFF) | topo_variant(d, e & 0x3FFFFFFF, born);
-            CC.tc_ki[tid] = ki;
+            if (tid < KP_CC_TC) {
+                CC.tc[tid] = (e & ~0x3FFFFFFF) | topo_variant(d, e & 0x3FFFFFFF, born);
+                CC.tc_ki[tid] = ki;
+            }
         } else if (tid - CC.ntc < KP_CC_REC) {
             CC.tr[tid - CC.ntc] = e;
             CC.tr_ki[tid - CC.ntc] = ki;
@@ -503,8 +505,17 @@ __device__ __forceinline__ bool topo_narrow(const KpDev& d, const ClassCache& CC
     int kidx[KP_MAX_TOPO_KEYS];
     uint64_t kmask[KP_MAX_TOPO_KEYS];
     for (int e = 0; e < CC.ntc; e++) {
-        const int g = CC.tc[e] & 0x3FFFFFFF, self = (CC.tc[e] >> 30) & 1, ki = CC.tc_ki[e];
+        // beyond the cached entries: the class's list (no variant groups there, kp_solve_prepare), the key's class index
+        const int te = e < KP_CC_TC ? CC.tc[e] : d.cls_tc[d.cls_tcoff[CC.cls] + e];
+        const int g = te & 0x3FFFFFFF, self = (te >> 30) & 1;
         const int4 info = d.tg_info[g];
+        int ki = -1;
+        if (e < KP_CC_TC) {
+            ki = CC.tc_ki[e];
+        } else if (!(info.x & TG_HOST)) {
+            for (int i = 0; i < CC.nck; i++)
+                if (CC.key[i] == info.y) ki = i;
+        }
         const int type = info.x & TG_TYPE;
         if (info.x & TG_HOST) {
             const int cnt = CT ? pt_hcnt(d, *pt, d.tg_hrow[g], host) : ld_i32(&d.tg_hcnt[(size_t)d.tg_hrow[g] * d.HN + host]);

@@ -1909,11 +1909,22 @@ static kp_status topo_build(kp_ctx* c, const kp_solve_input* in, const std::vect
             }
         }
     }
+    if (getenv("KPSIM_DIAG_IDENT")) {  // diagnostics: the most constraining / counting groups of one class
+        size_t mc = 0, mr = 0;
+        for (int o = 0; o < C; o++) mc = std::max(mc, th.cons[o].size()), mr = std::max(mr, th.rec[o].size());
+        fprintf(stderr, "[kpsim] topology groups per class: constraining <= %zu, counting <= %zu\n", mc, mr);
+    }
     for (int o = 0; o < C; o++) {
         if (th.cons[o].size() > KP_MAX_TOPO || th.rec[o].size() > KP_MAX_TOPO_REC) {
             err = "a pod class is constrained or counted by too many topology groups";
             return KP_E_UNSUPPORTED;
         }
+        // constraining entries past the class cache's KP_CC_TC are read from cls_tc as they are: no variant there
+        for (size_t q = KP_CC_TC; q < th.cons[o].size(); q++)
+            if (gvar[th.cons[o][q] & 0x3FFFFFFF]) {
+                err = "a pod class constrained by more than 16 topology groups, one of them a variant group";
+                return KP_E_UNSUPPORTED;
+            }
         std::set<int> vkeys;  // topo_narrow intersects the groups' domains per value-keyed key
         for (int e : th.cons[o])
             if (!th.g[e & 0x3FFFFFFF].host) vkeys.insert(th.g[e & 0x3FFFFFFF].key);

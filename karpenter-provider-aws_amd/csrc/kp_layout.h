@@ -42,13 +42,14 @@
 #define KP_MAX_MIN_WORDS 64          // value bitset for a minValues distinct count (4096 values)
 #define KP_LDS_BYTES (160 * 1024)    // LDS per workgroup on gfx950
 #ifndef KP_MAX_TOPO
-#define KP_MAX_TOPO 16               // topology groups constraining one pod class
+#define KP_MAX_TOPO 32               // topology groups constraining one pod class
 #endif
 #ifndef KP_MAX_TOPO_REC
 #define KP_MAX_TOPO_REC 64           // ... recording (counting) its pods
 #endif
 #define KP_SNAP_ROWS 8               // constraining groups the FFD kernel snapshots / prefilters per pod (LDS)
 #define KP_CC_REC 16                 // recording groups a ClassCache holds (the rest are read from cls_tr)
+#define KP_CC_TC 16                  // constraining groups a ClassCache holds (the rest are read from cls_tc)
 #define KP_MAX_TOPO_KEYS 8           // distinct value-keyed topology keys among a class's constraining groups
 #define KP_TRACE_N 16384             // diagnostics ring (KPSIM_TRACE_*)           // topology groups recording one pod class's placements
 

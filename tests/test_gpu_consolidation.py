@@ -756,3 +756,15 @@ def test_fuzz_consolidation_shared_identity(ctx, golden, seed):
         assert_probes_equal(device_probes(ctx, cp, mode), pyoracle.consolidate(cp, mode))
     assert_commands_equal(device_command(ctx, cp, abi.KP_CONSOLIDATE_BOTH),
                           pyoracle.consolidate_command(cp, abi.KP_CONSOLIDATE_BOTH))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_fuzz_consolidation_more_than_16_constraining_groups(ctx, golden, seed):
+    """Probes over classes constrained by more than 16 topology groups (add_many_groups with 36-47 terms)."""
+    rng = np.random.Generator(np.random.PCG64(4800 + seed))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=int(rng.integers(60, 300)), replace=False))]
+    cp = fuzzgen.fuzz_topology_consolidation(sub, 4800 + seed, n_nodes=int(rng.integers(4, 50)),
+                                             n_pods=int(rng.integers(20, 200)), all_spot=seed % 4 == 0)
+    fuzzgen.add_many_groups(rng, cp.cluster, n_terms=int(rng.integers(36, 48)))
+    for mode in (abi.KP_CONSOLIDATE_SINGLE, abi.KP_CONSOLIDATE_MULTI):
+        assert_probes_equal(device_probes(ctx, cp, mode), pyoracle.consolidate(cp, mode))

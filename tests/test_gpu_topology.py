@@ -329,7 +329,7 @@ def test_overflow_rerun_once(golden):
 @pytest.mark.parametrize("seed", list(range(8)) + [1872, 1899])  # + tools/soak.py many_groups 172 / 199
 def test_fuzz_many_groups(ctx, golden, seed):
     """More than 8 topology groups constraining a class and more than 16 counting it (fuzzgen.add_many_groups): up to
-    KP_MAX_TOPO = 16 / KP_MAX_TOPO_REC = 64 per class, over a cluster with bound pods."""
+    KP_MAX_TOPO = 32 / KP_MAX_TOPO_REC = 64 per class, over a cluster with bound pods."""
     rng = np.random.Generator(np.random.PCG64(seed + 8100))
     sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=200, replace=False))]
     prob = fuzzgen.fuzz_topology_existing_problem(sub, seed + 8100, n_pods=int(rng.integers(100, 400)),
@@ -386,3 +386,15 @@ def test_fuzz_shared_identity_relaxed(ctx, golden, seed):
     prob = fuzzgen.fuzz_shared_identity_problem(sub, seed + 700, n_pods=int(rng.integers(80, 300)),
                                                 n_existing=(seed % 2) * 20)
     same(ctx, fuzzgen.add_relaxed_shared(rng, prob))
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_fuzz_more_than_16_constraining_groups(ctx, golden, seed):
+    """add_many_groups with 36-47 terms: classes constrained by 17-24 topology groups (KP_MAX_TOPO = 32; beyond the
+    8-row prefilter snapshot, read from the global counters) and counted by up to 50, over clusters with bound pods."""
+    rng = np.random.Generator(np.random.PCG64(seed + 8300))
+    sub = [golden[int(i)] for i in sorted(rng.choice(len(golden), size=200, replace=False))]
+    prob = fuzzgen.fuzz_topology_existing_problem(sub, seed + 8300, n_pods=int(rng.integers(100, 300)),
+                                                  n_existing=int(rng.integers(4, 40)))
+    fuzzgen.add_many_groups(rng, prob, n_terms=int(rng.integers(36, 48)))
+    same(ctx, prob)
