@@ -470,6 +470,7 @@ struct kp_ctx {
     // kp_solve_prepare's per-pod host arrays, kept across calls
     std::vector<int32_t> h_uid_p;
     std::vector<uint64_t> h_uid_k;
+    std::vector<int32_t> h_shape_tab;
     int nc_cap_once = 0;                     // > 0: the next prepare plans for this many NodeClaims (after an overflow)
     int last_plan_nc = 0;                    // in-flight NodeClaim capacity of the last prepare
     bool nc_overflow = false;                // the last fetch found the solve out of in-flight NodeClaim capacity
@@ -2333,12 +2334,43 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     for (int j = 0; j < NT; j++)
         for (int r = 0; r < R; r++)
             if (daemon[(size_t)j * R + r] != 0) active[r] = 1;
-    struct ShapeKey {
+    // shapes: (class, requests) interned in an open-addressing table of shape ids; a shape's requests point at the
+    // pinned row of its first pod (relaxation stages share the row of the shape they relax)
+    struct ShapeRec {
         int cls;
-        std::vector<int64_t> req;
-        bool operator<(const ShapeKey& o) const { return cls != o.cls ? cls < o.cls : req < o.req; }
+        const int64_t* req;
     };
-    std::map<ShapeKey, int> shapes;
+    std::vector<ShapeRec> shapes;
+    std::vector<int32_t>& stab = c->h_shape_tab;
+    size_t SHT = 1024;
+    while (SHT < (size_t)P * 2) SHT <<= 1;
+    if (stab.size() < SHT) stab.resize(SHT);
+    std::fill(stab.begin(), stab.begin() + SHT, -1);
+    auto shape_hash = [&](int cl, const int64_t* rq) {
+        uint64_t h = (uint64_t)(uint32_t)cl * 0x9E3779B97F4A7C15ull;
+        for (int r = 0; r < R; r++) h = (h ^ (uint64_t)rq[r]) * 0xBF58476D1CE4E5B9ull + 0x94D049BB133111EBull;
+        return (size_t)(h ^ (h >> 31));
+    };
+    auto shape_id = [&](int cl, const int64_t* rq) -> int {
+        if (shapes.size() * 2 >= SHT) {  // keep the load ≤ 1/2 (relaxation stages can add shapes beyond P)
+            SHT <<= 1;
+            stab.assign(SHT, -1);
+            for (size_t i = 0; i < shapes.size(); i++) {
+                size_t h = shape_hash(shapes[i].cls, shapes[i].req) & (SHT - 1);
+                while (stab[h] >= 0) h = (h + 1) & (SHT - 1);
+                stab[h] = (int32_t)i;
+            }
+        }
+        for (size_t h = shape_hash(cl, rq) & (SHT - 1);; h = (h + 1) & (SHT - 1)) {
+            const int id = stab[h];
+            if (id < 0) {
+                stab[h] = (int32_t)shapes.size();
+                shapes.push_back({cl, rq});
+                return (int)shapes.size() - 1;
+            }
+            if (shapes[id].cls == cl && memcmp(shapes[id].req, rq, sizeof(int64_t) * R) == 0) return id;
+        }
+    };
     // NewQueue's UID tie-break enters as the UID's first 8 bytes; distinct UIDs sharing them are detected with an
     // open-addressing table over those prefixes (ctx scratch, cleared per call)
     size_t HT = 1024;
@@ -2354,56 +2386,79 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     const kp_pods_view& pv = in->pods;
     // kp_pods_view.uids is optional (NULL, or NULL entries): a missing UID is the empty string
     auto uid_of = [&](int p) -> const char* { return pv.uids && pv.uids[p] ? pv.uids[p] : ""; };
-    int prev_shape = -1;
-    for (int p = 0; p < P; p++) {
-        const int cl = pv.class_id[p];
-        if (cl < 0 || cl >= C) return fail(ctx, KP_E_INVALID, "pod class out of range");
-        pcls[p] = cl;
-        const int64_t* rq = pv.requests + (size_t)p * R;
-        int64_t* dst = &preq[(size_t)p * R];
-        for (int r = 0; r < R; r++) {
-            dst[r] = rq[r];
-            if (rq[r] != 0) active[r] = 1;
-            if (rq[r] < 0) return fail(ctx, KP_E_INVALID, "negative request");
-        }
-        // shapes are numbered in order of first appearance; a pod with the previous pod's class and requests (the pods
-        // of one Deployment, typically) reuses its shape without a lookup
-        if (p > 0 && cl == pcls[p - 1] && memcmp(dst, dst - R, sizeof(int64_t) * R) == 0) {
-            pshape[p] = prev_shape;
-        } else {
-            ShapeKey sk{cl, std::vector<int64_t>(rq, rq + R)};
-            auto it = shapes.find(sk);
-            if (it == shapes.end()) it = shapes.emplace(std::move(sk), (int)shapes.size()).first;
-            pshape[p] = prev_shape = it->second;
-        }
-        // NewQueue key: cpu desc, memory desc, creation asc, UID asc.  The UID enters as its first 8 bytes
-        // (big-endian, order-preserving); if two distinct UIDs share that prefix, exact string ranks are used.
-        const char* u = uid_of(p);
-        uint64_t uk = 0;
-        const char* q = u;
-        for (int i = 0; i < 8; i++) {
-            uk <<= 8;
-            if (*q) uk |= (uint8_t)*q++;
-        }
-        fields[(size_t)p * 4 + 0] = dst[cpu_axis];
-        fields[(size_t)p * 4 + 1] = dst[mem_axis];
-        fields[(size_t)p * 4 + 2] = pv.creation_ns ? pv.creation_ns[p] : 0;
-        fields[(size_t)p * 4 + 3] = (int64_t)(uk ^ 0x8000000000000000ull);
-        if (!uid_collision) {
-            size_t h = (size_t)((uk * 0x9E3779B97F4A7C15ull) >> 20) & (HT - 1);
-            for (;; h = (h + 1) & (HT - 1)) {
-                if (uid_p[h] < 0) {
-                    uid_k[h] = uk;
-                    uid_p[h] = p;
-                    break;
+    // two independent passes over the pods, run side by side on the ctx's worker pool for large batches: the rows
+    // (class, requests, shapes) and the NewQueue keys (the UID strings are separate host allocations, a pointer chase)
+    const char* perr = nullptr;
+    auto pod_rows = [&]() {
+        int prev_shape = -1;
+        for (int p = 0; p < P; p++) {
+            const int cl = pv.class_id[p];
+            if (cl < 0 || cl >= C) {
+                perr = "pod class out of range";
+                return;
+            }
+            pcls[p] = cl;
+            const int64_t* rq = pv.requests + (size_t)p * R;
+            int64_t* dst = &preq[(size_t)p * R];
+            for (int r = 0; r < R; r++) {
+                dst[r] = rq[r];
+                if (rq[r] != 0) active[r] = 1;
+                if (rq[r] < 0) {
+                    perr = "negative request";
+                    return;
                 }
-                if (uid_k[h] == uk) {
-                    if (strcmp(uid_of(uid_p[h]), u) != 0) uid_collision = true;
-                    break;
+            }
+            // shapes are numbered in order of first appearance; a pod with the previous pod's class and requests (the
+            // pods of one Deployment, typically) reuses its shape without a lookup
+            if (p > 0 && cl == pcls[p - 1] && memcmp(dst, dst - R, sizeof(int64_t) * R) == 0) {
+                pshape[p] = prev_shape;
+            } else {
+                pshape[p] = prev_shape = shape_id(cl, dst);
+            }
+        }
+    };
+    auto pod_keys = [&]() {
+        for (int p = 0; p < P; p++) {
+            // NewQueue key: cpu desc, memory desc, creation asc, UID asc.  The UID enters as its first 8 bytes
+            // (big-endian, order-preserving); if two distinct UIDs share that prefix, exact string ranks are used.
+            if (pv.uids && p + 16 < P && pv.uids[p + 16]) __builtin_prefetch(pv.uids[p + 16]);
+            const char* u = uid_of(p);
+            uint64_t uk = 0;
+            const char* q = u;
+            for (int i = 0; i < 8; i++) {
+                uk <<= 8;
+                if (*q) uk |= (uint8_t)*q++;
+            }
+            const int64_t* rq = pv.requests + (size_t)p * R;
+            fields[(size_t)p * 4 + 0] = rq[cpu_axis];
+            fields[(size_t)p * 4 + 1] = rq[mem_axis];
+            fields[(size_t)p * 4 + 2] = pv.creation_ns ? pv.creation_ns[p] : 0;
+            fields[(size_t)p * 4 + 3] = (int64_t)(uk ^ 0x8000000000000000ull);
+            if (!uid_collision) {
+                size_t h = (size_t)((uk * 0x9E3779B97F4A7C15ull) >> 20) & (HT - 1);
+                for (;; h = (h + 1) & (HT - 1)) {
+                    if (uid_p[h] < 0) {
+                        uid_k[h] = uk;
+                        uid_p[h] = p;
+                        break;
+                    }
+                    if (uid_k[h] == uk) {
+                        if (strcmp(uid_of(uid_p[h]), u) != 0) uid_collision = true;
+                        break;
+                    }
                 }
             }
         }
+    };
+    if (P >= 16384) {
+        c->pool.grow(2);
+        if (!c->pool.run(2, [&](int t) { t == 0 ? pod_rows() : pod_keys(); }))
+            return fail(ctx, KP_E_INVALID, "kp_solve_prepare: host error in a worker thread");
+    } else {
+        pod_rows();
+        pod_keys();
     }
+    if (perr) return fail(ctx, KP_E_INVALID, perr);
     if (uid_collision) {
         std::vector<int> idx(P);
         for (int p = 0; p < P; p++) idx[p] = p;
@@ -2418,21 +2473,9 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
     // relaxation stages of every shape: shape_next[s] = the shape of (relax_next[class of s], the same requests)
     std::vector<int32_t> shape_next;
     if (!c->pref.relax_next.empty()) {
-        std::vector<const ShapeKey*> by_id(shapes.size());
-        for (auto& kv : shapes) by_id[kv.second] = &kv.first;  // std::map nodes do not move
-        for (size_t sid = 0; sid < by_id.size(); sid++) {
-            const int nx = c->pref.relax_next[by_id[sid]->cls];
-            int id = -1;
-            if (nx >= 0) {
-                ShapeKey sk{nx, by_id[sid]->req};
-                auto it = shapes.find(sk);
-                if (it == shapes.end()) {
-                    it = shapes.emplace(std::move(sk), (int)shapes.size()).first;
-                    by_id.push_back(&it->first);
-                }
-                id = it->second;
-            }
-            shape_next.push_back(id);
+        for (size_t sid = 0; sid < shapes.size(); sid++) {
+            const int nx = c->pref.relax_next[shapes[sid].cls];
+            shape_next.push_back(nx >= 0 ? shape_id(nx, shapes[sid].req) : -1);
         }
     }
     KpDev& d = c->dev;
