@@ -648,18 +648,22 @@ __device__ __forceinline__ void consolidate_body(DevT d, ConsT k) {
                     st_loads++;
                     fresh = true;
                     mw = uni64(modb[w]);  // not the cached chunk's word: LDS is current
-                    if (mw & xw) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this probe's delta stores landed
-                    const bool md = (mw >> lane) & 1ull;
+                    // the static headroom first: its loads are in flight while the delta stores drain
 #pragma unroll
                     for (int ai = 0; ai < KP_LDS_AXES; ai++) {
                         h[ai] = 0;
                         dl[ai] = 0;
-                        if (ai < A && j < E) {
-                            h[ai] = d.ex_head[(size_t)ai * E + j];
-                            if (md) dl[ai] = ld_req(&delta[(size_t)ai * E + j]);
-                            h[ai] -= dl[ai];
-                        }
+                        if (ai < A && j < E) h[ai] = d.ex_head[(size_t)ai * E + j];
                     }
+                    if (mw) {
+                        if (mw & xw) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this probe's delta stores landed
+                        const bool md = (mw >> lane) & 1ull;
+#pragma unroll
+                        for (int ai = 0; ai < KP_LDS_AXES; ai++)
+                            if (ai < A && j < E && md) dl[ai] = ld_req(&delta[(size_t)ai * E + j]);
+                    }
+#pragma unroll
+                    for (int ai = 0; ai < KP_LDS_AXES; ai++) h[ai] -= dl[ai];
                 }
                 bool cand = (xw & ge) >> lane & 1ull;
 #pragma unroll
@@ -1467,6 +1471,8 @@ __device__ __forceinline__ void consolidate_body(DevT d, ConsT k) {
                     pp[11] = pf_miss;
                     pp[12] = cy_nc;
                     pp[13] = cy_dec;
+                    pp[14] = st_loads;
+                    pp[15] = st_skips;
                 }
                 S.st[CS_CYC_BUILD] += cy_build;
                 S.st[CS_CYC_SCAN] += cy_scan;

@@ -3851,8 +3851,9 @@ static kp_status cons_run(kp_ctx* ctx, int m0, int m1, int s0, int s1, kp_probe_
                         part == 0 ? "multi-node" : "single-node", e - b, arg - b, (long long)q[2], (long long)q[0],
                         (long long)q[1], (long long)q[4], (long long)q[5], (long long)q[6], (long long)q[7], (long long)q[3]);
                 fprintf(stderr, "[kpsim]   intake: %lld prefix-sum rounds, %lld scalar steps; %lld pods past the store in %lld "
-                        "cycles; NodeClaim %lld cycles, decide %lld cycles\n", (long long)q[8], (long long)q[9],
-                        (long long)q[11], (long long)q[10], (long long)q[12], (long long)q[13]);
+                        "cycles; NodeClaim %lld cycles, decide %lld cycles; chunk loads %lld, summary skips %lld\n", (long long)q[8],
+                        (long long)q[9], (long long)q[11], (long long)q[10], (long long)q[12], (long long)q[13],
+                        (long long)q[14], (long long)q[15]);
             }
         }
     }
