@@ -94,6 +94,10 @@ struct FfdShared {
     // back to wave 0 (topo_resume) for the sort; topo_exdone: the block skips the existing nodes on that pass
     int topo_defer, topo_resume, topo_exdone;
     int tp_all;                    // the prefilter holds every constraining group (at most KP_SNAP_ROWS)
+    // the static entries (KpTopoCons) of class tp_cls's first KP_SNAP_ROWS constraining groups and its group count: the
+    // setup of the next pod of that class reads them here (set behind the barrier after a setup, read after the next)
+    int tp_cls, tp_nall;
+    KpTopoCons tp_T[KP_SNAP_ROWS];
     int tp_k[KP_SNAP_ROWS];        // value-keyed group: key; hostname group: -1 - row of tg_hcnt
     int tp_lo[KP_SNAP_ROWS], tp_hi[KP_SNAP_ROWS];  // hostname group: the host's count must lie in [lo, hi]
     int tp_cmp[KP_SNAP_ROWS];      // value-keyed: a complement (NotIn) NodeClaim requirement is not prefiltered
@@ -109,11 +113,13 @@ struct FfdShared {
 // prefiltered by its first KP_SNAP_ROWS (a superset of the candidates that pass all: evaluations stay exact, read the
 // global counters, and the quick accept is off).
 __device__ inline void topo_prefilter_setup(const KpDev& d, FfdShared& S, int c, int wave, int lane) {
-    const int t0 = d.cls_tcoff[c], nall = d.cls_tcoff[c + 1] - t0;
+    const bool hit = S.tp_cls == c;  // the previous setup's class: its static entries are in LDS
+    const int t0 = hit ? 0 : d.cls_tcoff[c], nall = hit ? S.tp_nall : d.cls_tcoff[c + 1] - t0;
     const int nt = nall < KP_SNAP_ROWS ? nall : KP_SNAP_ROWS;
     for (int e = wave; e < nt; e += KP_NWAVES) {
         // the entry's static operands (KpTopoCons), then the group's counts: one round of independent loads
-        KpTopoCons T = d.cls_tce[t0 + e];
+        KpTopoCons T = hit ? S.tp_T[e] : d.cls_tce[t0 + e];
+        if (!hit && lane == 0) S.tp_T[e] = T;
         if (d.late_sib) {  // a variant group: the identity's born variant (its minDomains)
             T.g = topo_variant(d, T.g, S.born);
             T.mindom = d.tg_info[T.g].w;
@@ -174,6 +180,7 @@ __device__ inline void topo_prefilter_setup(const KpDev& d, FfdShared& S, int c,
     if (wave == 0 && lane == 0) {
         S.tp_n = nt;
         S.tp_all = nall <= KP_SNAP_ROWS;
+        S.tp_nall = nall;
     }
 }
 
@@ -653,6 +660,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
     if (tid == 0) {
         S.N = 0;
         S.tp_n = 0;
+        S.tp_cls = -1;
         S.tsnap = d.G > 0 ? reinterpret_cast<TopoSnap*>(smem + d.off_tsnap) : nullptr;
         S.topo_pod = 0;
         S.topo_quick = 0;
@@ -1364,6 +1372,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
             }
             if (cfl & CF_TOPO_CONS) topo_prefilter_setup(d, S, c, wave, lane);
             __syncthreads();  // every group's entry and TopoSnap row
+            if (tid == 0 && (cfl & CF_TOPO_CONS)) S.tp_cls = c;  // read by the next setup, behind the next slow-path barrier
             const long long t1 = prof_clock(d);
             const int f = topo_scan_block(d, S, skey, sord, stmpl, ctol, N, scan_from, S.bred, wave, lane);
 #else
