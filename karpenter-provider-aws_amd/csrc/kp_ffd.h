@@ -98,6 +98,9 @@ struct FfdShared {
     // setup of the next pod of that class reads them here (set behind the barrier after a setup, read after the next)
     int tp_cls, tp_nall;
     KpTopoCons tp_T[KP_SNAP_ROWS];
+    // the recording entries (KpTopoRec) of class tr_cls when it has at most KP_SNAP_ROWS (wave 0's quick-accept Record)
+    int tr_cls, tr_n;
+    KpTopoRec tr_R[KP_SNAP_ROWS];
     int tp_k[KP_SNAP_ROWS];        // value-keyed group: key; hostname group: -1 - row of tg_hcnt
     int tp_lo[KP_SNAP_ROWS], tp_hi[KP_SNAP_ROWS];  // hostname group: the host's count must lie in [lo, hi]
     int tp_cmp[KP_SNAP_ROWS];      // value-keyed: a complement (NotIn) NodeClaim requirement is not prefiltered
@@ -307,8 +310,10 @@ __device__ inline bool merge_noop(const KpDev& d, WaveScratch& ws, int nc, int c
 // every recorded domain comes from its digest (hostname groups: its host E + nc).  CF_TOPO_QREC guarantees that no
 // recording group needs the node-affinity filter of another class.  Lane i takes recording entry i (KpTopoRec) and its
 // key of the NodeClaim's digest, so the entries' loads form one round; the counts are then added entry by entry.
-__device__ inline void topo_record_quick(const KpDev& d, int c, int nc, int tmpl, uint64_t born, int lane) {
-    const int r0 = d.cls_troff[c], nr = d.cls_troff[c + 1] - r0;
+__device__ inline void topo_record_quick(const KpDev& d, FfdShared& S, int c, int nc, int tmpl, uint64_t born, int lane) {
+    const bool hit = S.tr_cls == c;  // the entries are in LDS (wave 0 alone reads and writes them)
+    const int r0 = hit ? 0 : d.cls_troff[c], nr = hit ? S.tr_n : d.cls_troff[c + 1] - r0;
+    const bool keep = !hit && nr <= KP_SNAP_ROWS;
     for (int base = 0; base < nr; base += 64) {
         const int i = base + lane;
         KpTopoRec R{};
@@ -316,7 +321,8 @@ __device__ inline void topo_record_quick(const KpDev& d, int c, int nc, int tmpl
         uint64_t w = 0;
         bool live = false;
         if (i < nr) {
-            R = d.cls_tre[r0 + i];
+            R = hit ? S.tr_R[i] : d.cls_tre[r0 + i];
+            if (keep) S.tr_R[i] = R;
             live = !((R.skip >> tmpl) & 1ull) && (R.late < 0 || ((born >> R.late) & 1ull));
             if (live && !(R.flags & 8)) {
                 fl = d.nc_hdr[(size_t)nc * d.K + R.key].flags;
@@ -341,6 +347,10 @@ __device__ inline void topo_record_quick(const KpDev& d, int c, int nc, int tmpl
             if ((wv >> lane) & 1ull) atomicAdd(&d.tg_cnt[(size_t)g * 64 + lane], 1);
             if (lane == 0 && wv) atomicOr((unsigned long long*)&d.tg_known[g], (unsigned long long)wv);
         }
+    }
+    if (keep && lane == 0) {
+        S.tr_n = nr;
+        S.tr_cls = c;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -661,6 +671,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
         S.N = 0;
         S.tp_n = 0;
         S.tp_cls = -1;
+        S.tr_cls = -1;
         S.tsnap = d.G > 0 ? reinterpret_cast<TopoSnap*>(smem + d.off_tsnap) : nullptr;
         S.topo_pod = 0;
         S.topo_quick = 0;
@@ -1415,7 +1426,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                         if (lane < A) shr[lane * NQ + nc] -= S.cur_pq[lane];
                         if (lane < R && S.pod_req[lane])
                             atomicAdd((unsigned long long*)&d.nc_req[(size_t)nc * R + lane], (unsigned long long)S.pod_req[lane]);
-                        topo_record_quick(d, c, nc, tm, S.born, lane);
+                        topo_record_quick(d, S, c, nc, tm, S.born, lane);
                         if (lane == 0) {
                             skey[f]++;
                             d.pod_result[pod] = nc;
