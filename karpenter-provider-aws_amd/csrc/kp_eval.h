@@ -1175,6 +1175,33 @@ __device__ inline bool merge_noop_at(const KpDev& d, WaveScratch& ws, const ReqH
     return ballot(!ok) == 0;
 }
 
+// merge_noop_at with the class's operands from the class cache (CC.cls is the class): keys, headers and words from LDS,
+// so the NodeClaim's headers and words are the only global loads.
+__device__ inline bool merge_noop_cc(const KpDev& d, const ClassCache& CC, WaveScratch& ws, const ReqHdr* Ahdr,
+                                     const uint64_t* Aw, int lane) {
+    bool ok = true;
+    if (lane < CC.nck && !((CC.kneutral >> lane) & 1u)) {
+        const int k = CC.key[lane], n = CC.nw[lane];
+        const ReqHdr A = Ahdr[k];
+        const uint64_t* aw = Aw + CC.woff[lane];
+        if (!(A.flags & RF_DEF)) {
+            ok = false;  // the merge adds the key
+        } else {
+            const ReqHdr B = CC.hdr[lane];
+            const uint64_t* bw = CC.words + CC.wsoff[lane];
+            uint64_t* ow = ws.words + CC.wsoff[lane];
+            ReqHdr O;
+            const int cnt = req_intersect(d, k, A, aw, B, bw, O, ow);
+            ok = O.flags == A.flags && O.gt == A.gt && O.lt == A.lt && O.minv == A.minv;
+            for (int i = 0; i < n && ok; i++) ok = ow[i] == aw[i];
+            if (!(O.flags & RF_CMP) && cnt == 0 &&
+                !(op_notin_or_dne(req_op(B.flags, popc_words(bw, n))) && op_notin_or_dne(req_op(A.flags, popc_words(aw, n)))))
+                ok = false;
+        }
+    }
+    return ballot(!ok) == 0;
+}
+
 // Write the merged class keys of a successful evaluation into NodeClaim slot n.
 __device__ __forceinline__ void commit_reqs(const KpDev& d, const ClassCache& CC, const WaveScratch& ws, int n, int lane) {
     if (lane < CC.nck) {

@@ -302,8 +302,10 @@ __device__ inline bool topo_pinned(const KpDev& d, const FfdShared& S, int nc, i
 // is (header and values), and the pair passes Compatible.  Then the Add keeps the NodeClaim's requirements, so its options
 // stay compatible and its offerings the same: the topology quick accept applies as for a NodeClaim that absorbed the
 // class (wave 0; ws.words is free scratch here).
-__device__ inline bool merge_noop(const KpDev& d, WaveScratch& ws, int nc, int c, int lane) {
-    return merge_noop_at(d, ws, d.nc_hdr + (size_t)nc * d.K, d.nc_words + (size_t)nc * d.DW, c, lane);
+__device__ inline bool merge_noop(const KpDev& d, FfdShared& S, int nc, int c, int lane) {
+    const ReqHdr* h = d.nc_hdr + (size_t)nc * d.K;
+    const uint64_t* w = d.nc_words + (size_t)nc * d.DW;
+    return S.CC.cls == c ? merge_noop_cc(d, S.CC, S.ws[0], h, w, lane) : merge_noop_at(d, S.ws[0], h, w, c, lane);
 }
 
 // Topology.Record of a quick accept onto NodeClaim nc (template tmpl): its requirements are unchanged by the Add, so
@@ -1116,7 +1118,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                         // the NodeClaim at f has not absorbed the class but its witness fits: the Add is the quick accept
                         // when the class's requirement merge changes nothing (and the class tolerates its template)
                         const int nc = rl32((int)wo, fl), tm = (int)((uint32_t)rl32((int)wm, fl) >> 16);
-                        if (((tl >> tm) & 1ull) && merge_noop(d, S.ws[0], nc, c, lane)) {
+                        if (((tl >> tm) & 1ull) && merge_noop(d, S, nc, c, lane)) {
                             if (lane == fl) {
                                 wm = (wm & 0xFFFF0000u) | (uint32_t)(uint16_t)c;
                                 wa = true;
@@ -1418,7 +1420,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                     if (d.profile && lane == 0 && nc < NQ && ok) S.st[ST_TQ_WHY + 5]++;  // witness fits
                     ok = ok && topo_pinned(d, S, nc, lane);
                     // a NodeClaim that has not absorbed the class: quick when the Add's merge changes nothing
-                    const bool noop = ok && !absd && merge_noop(d, S.ws[0], nc, c, lane);
+                    const bool noop = ok && !absd && merge_noop(d, S, nc, c, lane);
                     if (d.profile && lane == 0 && noop) S.st[ST_TQ_WHY + 6]++;
                     quick = ok && (absd || noop);
                     if (noop && lane == 0) slast[nc] = (uint16_t)c;  // its requirements are a subset of the class's
