@@ -2450,7 +2450,9 @@ extern "C" kp_status kp_solve_prepare(kp_ctx* ctx, const kp_solve_input* in) try
             }
         }
     };
-    if (P >= 16384) {
+    // KPSIM_PREP_SPLIT_MIN: the batch size from which the two passes run side by side (tests force small batches)
+    static const int split_min = getenv("KPSIM_PREP_SPLIT_MIN") ? atoi(getenv("KPSIM_PREP_SPLIT_MIN")) : 16384;
+    if (P >= split_min) {
         c->pool.grow(2);
         if (!c->pool.run(2, [&](int t) { t == 0 ? pod_rows() : pod_keys(); }))
             return fail(ctx, KP_E_INVALID, "kp_solve_prepare: host error in a worker thread");

@@ -30,3 +30,14 @@ def test_concurrent_contexts_tsan(binary):
     assert "ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
     assert r.returncode == 0, r.stderr[-4000:]
     assert r.stdout.startswith("ok: 8 threads")
+
+
+def test_concurrent_contexts_tsan_split_prepare(binary):
+    """The same run with kp_solve_prepare's two pod passes on the ctx's worker pool for every batch (they run side by
+    side only from 16,384 pods by default)."""
+    env = dict(os.environ, KP_STUB_DEVICES="2", KPSIM_PREP_SPLIT_MIN="1",
+               TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1")
+    r = subprocess.run([binary, "8", "3"], capture_output=True, text=True, timeout=600, env=env)
+    assert "ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert r.stdout.startswith("ok: 8 threads")
