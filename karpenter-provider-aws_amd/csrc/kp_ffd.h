@@ -577,6 +577,10 @@ __device__ inline void block_sort_move(FfdShared& S, SortSlice sl, int tid, int 
 #ifndef KP_TEAM_FIRST_TOPO
 #define KP_TEAM_FIRST_TOPO 1  // A/B builds: 0 compiles the block-evaluated first candidate out of the TOPO instantiations
 #endif
+#ifndef KP_TEAM_TMPL
+#define KP_TEAM_TMPL 1         // the templates evaluated one at a time by the whole block (the instantiations without
+                              // reserved offerings or topology groups: config 2 91.9 -> 90.5 ms; config 3 unchanged)
+#endif
 #ifndef KP_NOOP_RESV
 #define KP_NOOP_RESV 1        // A/B builds: 0 compiles the no-op merge quick accept out of the RESV instantiations
 #endif
@@ -1709,7 +1713,98 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
         } else {
             // ================= new NodeClaim from the templates (NodePool weight order) =================
             const long long c_t = prof_clock(d);
+            // NewNodeClaim(template jj) for the pod, by wave cw (whose scratch holds the template's accepted Add)
+            auto commit_tmpl = [&](int jj, int cw) {
+                const int n = S.N;
+                // NewNodeClaim(template): requirements = template requirements, then the Add's merge
+                for (int k = lane; k < K; k += 64) d.nc_hdr[(size_t)n * K + k] = d.cls_hdr[(size_t)(d.C + jj) * K + k];
+                for (int i = lane; i < d.DW; i += 64)
+                    d.nc_words[(size_t)n * d.DW + i] = d.cls_words[(size_t)(d.C + jj) * d.DW + i];
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                commit_reqs(d, S.CC, S.ws[cw], n, lane);
+                if (PREF && d.best_effort) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the header rows above have landed
+                    commit_min_relax(d, S.ws[cw], n, lane);
+                }
+                if (RESV && d.resv_on) commit_reservations(d, sRcap, S.ws[cw], n, true, &S.rel_flag, lane);
+                if (TOPO_ON && (S.CC.flags & CF_TOPO))
+                    topo_record(d, S.CC, S.ws[cw], d.cls_hdr + (size_t)(d.C + jj) * K,
+                                d.cls_words + (size_t)(d.C + jj) * d.DW, d.E + n, jj, true, lane, -1, nullptr,
+                                S.born);
+                if (lane < TW) d.nc_opts[(size_t)n * TW + lane] = S.ws[cw].opts[lane];
+                for (int r = lane; r < R; r += 64)
+                    __hip_atomic_store(&d.nc_req[(size_t)n * R + r], d.daemon[(size_t)jj * R + r] + S.pod_req[r],
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lane < A && n < NQ) shr[lane * NQ + n] = S.ws[cw].hr[lane];
+                // subtractMax(remaining, nodeClaim.InstanceTypeOptions)
+                for (int r = 0; r < R; r++) {
+                    if (!d.limit_set[(size_t)jj * R + r]) continue;
+                    int64_t mx = INT64_MIN;
+                    for (int w2 = 0; w2 < TW; w2++) {
+                        const uint64_t ow = S.ws[cw].opts[w2];
+                        if ((ow >> lane) & 1ull) {
+                            const int64_t cp = d.cap[(size_t)r * T + w2 * 64 + lane];
+                            mx = cp > mx ? cp : mx;
+                        }
+                    }
+                    mx = wave_max64(mx);
+                    if (lane == 0) d.remaining[(size_t)jj * R + r] -= mx;
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the new remaining limits have landed
+                limit_mask_update(d, jj, lane);
+                if (lane == 0) {
+                    slast[n] = (uint16_t)S.cur_cls;
+                    stmpl[n] = (uint8_t)jj;
+                    d.nc_tmpl[n] = jj;
+                    sord[n] = (uint16_t)n;
+                    skey[n] = 1;
+                    S.N = n + 1;
+                    S.dirty_kind = 2;
+                    S.dirty_pos = n;
+                    d.pod_result[pod] = n;
+                    d.pod_order[pod] = S.seq++;
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            };
             int twin = -1;
+            if (KP_TEAM_TMPL && !RESV && !TOPO && d.team_first) {
+                // the templates one at a time in weight order, each evaluated by the whole block (the type sweep split
+                // over the waves, as for a team candidate): the first that accepts wins, and every wave's scratch holds
+                // its Add
+                for (int j = 0; j < d.NT; j++) {
+                    uint64_t o = (lane < TW && d.tmpl_ok[j]) ? d.tmpl_opts[(size_t)j * TW + lane] : 0;
+                    o = limit_filter(d, j, o, lane);
+                    if (!ballot(o != 0)) continue;  // the same for every wave
+                    EvalIn a;
+                    a.Ahdr = d.cls_hdr + (size_t)(d.C + j) * K;
+                    a.Aw = d.cls_words + (size_t)(d.C + j) * d.DW;
+                    a.opts = o;
+                    a.base_req = d.daemon + (size_t)j * R;
+                    a.pod_req = S.pod_req;
+                    a.tmpl = j;
+                    a.compat = true;
+                    a.force_off = false;
+                    a.prof = nullptr;
+                    a.host = d.E + S.N;  // NewNodeClaim's fresh hostname (no pod counted there yet)
+                    a.held = 0;
+                    TeamBuf* const tbuf = &S.team[tjoins & 1];
+                    const bool ok = (TOPO_ON && (S.CC.flags & CF_TOPO_CONS))
+                                        ? eval_wave<true, RESV, true, PREF, false, true>(d, E, S.CC, a, S.ws[wave], lane, tbuf,
+                                                                                         wave, KP_NWAVES, &tjoins)
+                                        : eval_wave<false, RESV, true, PREF, false, true>(d, E, S.CC, a, S.ws[wave], lane,
+                                                                                          tbuf, wave, KP_NWAVES, &tjoins);
+                    if (tid == 0) S.st[ST_TMPL_EVALS]++;
+                    if (ok) {
+                        twin = j;
+                        break;
+                    }
+                }
+                if (twin >= 0 && (S.N >= NCMAX || S.N >= d.NCcap)) {
+                    if (tid == 0) S.err = 1;
+                    twin = -1;
+                }
+                if (twin >= 0 && wave == 0) commit_tmpl(twin, 0);
+            } else
             for (int tb = 0; tb < d.NT; tb += KP_NWAVES) {
                 const int j = tb + wave;
                 if (j < d.NT) {
