@@ -581,6 +581,9 @@ __device__ inline void block_sort_move(FfdShared& S, SortSlice sl, int tid, int 
 #define KP_TEAM_TMPL 1         // the templates evaluated one at a time by the whole block (the instantiations without
                               // reserved offerings or topology groups: config 2 91.9 -> 90.5 ms; config 3 unchanged)
 #endif
+#ifndef KP_TEAM_TMPL_RESV
+#define KP_TEAM_TMPL_RESV 0    // A/B builds: 1 also in the RESV instantiations
+#endif
 #ifndef KP_NOOP_RESV
 #define KP_NOOP_RESV 1        // A/B builds: 0 compiles the no-op merge quick accept out of the RESV instantiations
 #endif
@@ -1767,7 +1770,7 @@ __device__ __forceinline__ void ffd_solve(KpDev d) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             };
             int twin = -1;
-            if (KP_TEAM_TMPL && !RESV && !TOPO && d.team_first) {
+            if (KP_TEAM_TMPL && (!RESV || KP_TEAM_TMPL_RESV) && !TOPO && d.team_first) {
                 // the templates one at a time in weight order, each evaluated by the whole block (the type sweep split
                 // over the waves, as for a team candidate): the first that accepts wins, and every wave's scratch holds
                 // its Add
